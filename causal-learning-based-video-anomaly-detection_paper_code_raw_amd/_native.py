@@ -1,0 +1,84 @@
+"""ctypes binding of libvadhip.so (the C ABI in include/vad.h).
+
+There is no fallback: if the library is missing or no HIP device is present, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_LIB = None
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvadhip.so")
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_U64 = ctypes.c_uint64
+_U32 = ctypes.c_uint32
+_F = ctypes.c_float
+
+_SIGS = {
+    "vad_abi_version": (_I, []),
+    "vad_last_error": (ctypes.c_char_p, []),
+    "vad_rng_u24": (_I, [_U64, _U32, _U64, _I64, _I64, _I64, _P, _P]),
+    "vad_synth_frames": (_I, [_U64, _U64, _I64, _I64, _I64, _I, _P, _P]),
+    "vad_cad_num_slots": (_I, []),
+    "vad_cad_slot_name": (ctypes.c_char_p, [_I]),
+    "vad_cad_slot_numel": (_I64, [_I]),
+    "vad_cad_slot_offset": (_I64, [_I]),
+    "vad_cad_slot_group": (_I, [_I]),
+    "vad_cad_param_floats": (_I64, []),
+    "vad_cad_num_bufs": (_I, []),
+    "vad_cad_buf_name": (ctypes.c_char_p, [_I]),
+    "vad_cad_buf_numel": (_I64, [_I]),
+    "vad_cad_buf_offset": (_I64, [_I]),
+    "vad_cad_buf_floats": (_I64, []),
+    "vad_cad_num_bn": (_I, []),
+    "vad_cad_create": (_I, [_I, _I, _I, _I, ctypes.POINTER(_P)]),
+    "vad_cad_destroy": (None, [_P]),
+    "vad_cad_workspace_bytes": (_I64, [_P]),
+    "vad_cad_bind": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "vad_cad_forward": (_I, [_P, _P, _I, _U64, _U64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "vad_cad_backward": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "vad_cad_optimizer_step": (_I, [_P, _F, _F, _F, _F, _F, _F, _F, _P, _P]),
+}
+
+
+def lib():
+    """Load libvadhip.so (after torch, so both share one HIP runtime)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    import torch  # noqa: F401  (loads torch's libamdhip64.so.7 first)
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libvadhip.so is not built ({LIB_PATH}); run __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.vad_abi_version() != 1:
+        raise RuntimeError("libvadhip ABI mismatch")
+    _LIB = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise RuntimeError("libvadhip: " + lib().vad_last_error().decode())
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(device) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_hip(t) -> None:
+    import torch
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise RuntimeError("this build runs on MI355X (HIP) devices only; got a tensor on "
+                           f"{getattr(t, 'device', type(t))}")

@@ -1,0 +1,70 @@
+// Host-side launchers for the per-frame CNN (ResNetBackbone, causal_anomaly_detection.py:110-158) and the
+// shared dense-layer GEMMs.  All tensors are fp32, activations NHWC, frames folded into the batch axis.
+#pragma once
+#include "common.h"
+
+namespace vad {
+
+// ---------------------------------------------------------------- conv1 (1 -> 32, 7x7, s2, p3) + BN stats
+int conv1_fwd(const float* x, int NF, int H, int W, const float* w, const float* b, float* y, int OH, int OW,
+              float* partials, int* nparts, hipStream_t st);
+int conv1_num_parts(int NF, int OH);
+
+// ---------------------------------------------------------------- BatchNorm (training mode)
+// partials: [P][2*C] (sum | sumsq).  Writes mean/invstd/scale/shift [C] and updates running stats.
+int bn_finalize(const float* partials, int P, int C, double count, const float* gamma, const float* beta,
+                float* running_mean, float* running_var, float momentum, float eps, int training, float* stats,
+                hipStream_t st);
+// stats layout per layer: [0:C) mean, [C:2C) invstd, [2C:3C) scale, [3C:4C) shift, [4C:5C) k (bwd),
+//                         [5C:6C) mean(dZ), [6C:7C) mean(dZ*xhat)
+int bn_bwd_reduce(const float* dA, const float* y, const float* stats, int M, int C, float* partials, int* nparts,
+                  hipStream_t st);
+int bn_bwd_finalize(const float* partials, int P, int C, double count, const float* gamma, float* stats,
+                    float* dgamma, float* dbeta, hipStream_t st);
+int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
+                 int* nparts, hipStream_t st);
+int bn_rows_parts(int M, int C);
+
+// ---------------------------------------------------------------- pools
+int maxpool3s2_bnrelu(const float* y, const float* stats, int NF, int H, int W, int C, float* out, int OH, int OW,
+                      hipStream_t st);
+// AdaptiveAvgPool2d((4,6)) of relu(bn(y)) -> features [NF][C*24] (torch flatten order) and the mean over T.
+int avgpool_fwd(const float* y, const float* stats, int B, int T, int H, int W, int C, float* feats, float* pooled,
+                hipStream_t st);
+int avgpool_bwd(const float* dfeat, const float* dpooled, int B, int T, int H, int W, int C, float* dA,
+                hipStream_t st);
+
+// ---------------------------------------------------------------- 3x3 conv as implicit GEMM
+struct Conv3Layer {
+  int NF, Ci, Co, IH, IW, OH, OW, stride;
+};
+// weight relayout: W[co][ci][3][3] -> Wf[co][9][ci] and per-parity-class dgrad images Wd[ci][taps][co]
+int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd, hipStream_t st);
+int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats /*nullable: BN+ReLU on load*/,
+              const float* wf, const float* bias, float* y, float* partials, int* nparts, hipStream_t st);
+int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
+int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
+                int* nsplit, int64_t partial_cap, hipStream_t st);
+int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, const float* bias_partials,
+                       int nbias_parts, float* dW, float* db, hipStream_t st);
+
+// ---------------------------------------------------------------- dense layers  Y = act(X W^T + b)
+struct DenseAct {
+  int relu = 0;
+  // dropout after the activation (keep iff u24 >= thr), keyed by (h1, global row, col)
+  int drop = 0;
+  uint64_t h1 = 0;
+  uint32_t thr = 0;
+  float dscale = 1.f;
+  int64_t row0 = 0;
+};
+int dense_fwd(const float* X, int M, int K, const float* W, const float* b, int N, float* Y, const DenseAct& act,
+              float* scratch, int64_t scratch_floats, hipStream_t st);
+// dX = (dY W) * gate', where gate' = (gate > 0 ? gscale : 0) when gate != nullptr
+int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX, const float* gate, float gscale,
+                const int* skip, hipStream_t st);
+// dW = dY^T X, db = colsum(dY) (written, not accumulated)
+int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW, float* db, float* scratch,
+                int64_t scratch_floats, const int* skip, hipStream_t st);
+
+}  // namespace vad

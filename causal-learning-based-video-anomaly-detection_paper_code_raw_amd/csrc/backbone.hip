@@ -1,0 +1,898 @@
+// Per-frame CNN kernels for gfx950: conv1 (direct, VALU), 3x3 convs (implicit GEMM on f32 MFMA),
+// train-mode BatchNorm forward/backward, max/adaptive-avg pooling, and the dense-layer GEMMs.
+// Reference semantics: ResNetBackbone (causal_anomaly_detection.py:110-158), nn.BatchNorm2d train mode,
+// nn.MaxPool2d(3,2,1), nn.AdaptiveAvgPool2d((4,6)), nn.Linear / ReLU / Dropout stacks (cad:167-179, 525-538).
+#include "backbone.h"
+#include "gemm.h"
+
+namespace vad {
+
+// =====================================================================================================
+// conv1: 1 -> 32 channels, 7x7, stride 2, pad 3.  One block = one frame x a band of RB output rows; the
+// zero-padded input band is staged in LDS, weights are wave-uniform (scalar loads), each thread owns whole
+// pixels (32 accumulators) so the NHWC store is 128 contiguous bytes.  BN statistics of the raw output are
+// reduced per block into partials (deterministic, no atomics).
+// =====================================================================================================
+constexpr int C1_RB = 8;
+constexpr int C1_CO = 32;
+
+__global__ __launch_bounds__(256) void conv1_kernel(const float* __restrict__ x, int H, int W,
+                                                    const float* __restrict__ w, const float* __restrict__ bias,
+                                                    float* __restrict__ y, int OH, int OW, int bands,
+                                                    float* __restrict__ partials) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int img = blockIdx.x / bands, band = blockIdx.x % bands;
+  const int r0 = band * C1_RB;
+  const int PW = 2 * OW + 6;              // padded band width
+  const int PH = 2 * C1_RB + 5;
+  float* patch = sm;                      // [PH][PW]
+  const float* xi = x + (int64_t)img * H * W;
+  for (int i = threadIdx.x; i < PH * PW; i += 256) {
+    const int pr = i / PW, pc = i - pr * PW;
+    const int ih = 2 * r0 - 3 + pr, iw = pc - 3;
+    patch[i] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? xi[(int64_t)ih * W + iw] : 0.f;
+  }
+  __syncthreads();
+  float s1[C1_CO], s2[C1_CO];
+#pragma unroll
+  for (int c = 0; c < C1_CO; ++c) s1[c] = s2[c] = 0.f;
+  const int rows = min(C1_RB, OH - r0);
+  for (int p = threadIdx.x; p < rows * OW; p += 256) {
+    const int oy = p / OW, ox = p - oy * OW;
+    float acc[C1_CO];
+#pragma unroll
+    for (int c = 0; c < C1_CO; ++c) acc[c] = bias[c];
+    const float* pp = patch + (2 * oy) * PW + 2 * ox;
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) {
+#pragma unroll
+      for (int kw = 0; kw < 7; ++kw) {
+        const float v = pp[kh * PW + kw];
+#pragma unroll
+        for (int c = 0; c < C1_CO; ++c) acc[c] = fmaf(v, w[c * 49 + kh * 7 + kw], acc[c]);
+      }
+    }
+    float* dst = y + (((int64_t)img * OH + r0 + oy) * OW + ox) * C1_CO;
+#pragma unroll
+    for (int c = 0; c < C1_CO; c += 4) {
+      f32x4 v = {acc[c], acc[c + 1], acc[c + 2], acc[c + 3]};
+      *reinterpret_cast<f32x4*>(dst + c) = v;
+    }
+#pragma unroll
+    for (int c = 0; c < C1_CO; ++c) {
+      s1[c] += acc[c];
+      s2[c] = fmaf(acc[c], acc[c], s2[c]);
+    }
+  }
+  __syncthreads();
+  float* red = sm;  // [4 waves][2][32]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < C1_CO; ++c) {
+    const float a = wave_sum(s1[c]), b = wave_sum(s2[c]);
+    if (lane == 0) {
+      red[wave * 64 + c] = a;
+      red[wave * 64 + 32 + c] = b;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int t = threadIdx.x;
+    const float v = red[t] + red[64 + t] + red[128 + t] + red[192 + t];
+    // partial layout [P][2*C]: sums then sums of squares
+    partials[(int64_t)blockIdx.x * 2 * C1_CO + t] = v;
+  }
+}
+
+int conv1_num_parts(int NF, int OH) { return NF * (int)cdiv(OH, C1_RB); }
+
+int conv1_fwd(const float* x, int NF, int H, int W, const float* w, const float* b, float* y, int OH, int OW,
+              float* partials, int* nparts, hipStream_t st) {
+  VAD_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1, "conv1: bad output dims");
+  const int bands = (int)cdiv(OH, C1_RB);
+  const size_t lds = (size_t)(2 * C1_RB + 5) * (2 * OW + 6) * sizeof(float);
+  VAD_CHECK(lds <= 160 * 1024, "conv1: frame too wide for the LDS band");
+  hipLaunchKernelGGL(conv1_kernel, dim3(NF * bands), dim3(256), lds, st, x, H, W, w, b, y, OH, OW, bands, partials);
+  VAD_LAUNCH_CHECK();
+  *nparts = NF * bands;
+  return 0;
+}
+
+// =====================================================================================================
+// BatchNorm finalize: combine partial sums in double; batch stats, affine folding, running-stat update
+// (momentum 0.1, unbiased variance for running_var; nn.BatchNorm2d train semantics).
+// =====================================================================================================
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ partials, int P, int C,
+                                                          double count, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* running_mean,
+                                                          float* running_var, float momentum, float eps,
+                                                          int training, float* __restrict__ stats) {
+  const int c = blockIdx.x;
+  __shared__ double red[2][256];
+  double a = 0.0, b = 0.0;
+  if (training) {
+    for (int p = threadIdx.x; p < P; p += 256) {
+      a += (double)partials[(int64_t)p * 2 * C + c];
+      b += (double)partials[(int64_t)p * 2 * C + C + c];
+    }
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double mean, var;
+    if (training) {
+      mean = red[0][0] / count;
+      var = red[1][0] / count - mean * mean;
+      if (var < 0) var = 0;
+      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * var * count / (count - 1.0));
+    } else {
+      mean = running_mean[c];
+      var = running_var[c];
+    }
+    const double invstd = 1.0 / sqrt(var + (double)eps);
+    const double scale = (double)gamma[c] * invstd;
+    stats[c] = (float)mean;
+    stats[C + c] = (float)invstd;
+    stats[2 * C + c] = (float)scale;
+    stats[3 * C + c] = (float)((double)beta[c] - mean * scale);
+  }
+}
+
+int bn_finalize(const float* partials, int P, int C, double count, const float* gamma, const float* beta,
+                float* running_mean, float* running_var, float momentum, float eps, int training, float* stats,
+                hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, partials, P, C, count, gamma, beta,
+                     running_mean, running_var, momentum, eps, training, stats);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+// =====================================================================================================
+// BatchNorm backward (through the ReLU that follows it):  dZ = dA * [scale*y+shift > 0]
+//   reduce: per-channel sum(dZ), sum(dZ*xhat)          -> partials
+//   finalize: dgamma = sum(dZ*xhat), dbeta = sum(dZ), k = gamma*invstd, means
+//   apply: dY = k * (dZ - mean(dZ) - xhat*mean(dZ*xhat)), plus per-block sum(dY) for the conv bias grad
+// Thread layout over [M][C] rows: thread -> (row offset, channel quad); 1024 rows per block.
+// =====================================================================================================
+constexpr int BN_ROWS = 1024;
+
+int bn_rows_parts(int M, int C) {
+  (void)C;
+  return (int)cdiv(M, BN_ROWS);
+}
+
+__device__ inline void bn_block_reduce_store(float (&v)[2][4], int C, float* out) {
+  // threads sharing a channel quad: tid % (C/4) equal.  Reduce through LDS.
+  __shared__ float red[256 * 8];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[(s * 4 + e) * 256 + t] = v[s][e];
+  __syncthreads();
+  const int nq = C / 4, groups = 256 / nq;
+  for (int idx = t; idx < 2 * C; idx += 256) {
+    const int s = idx / C, c = idx % C, q = c / 4, e = c % 4;
+    float acc = 0.f;
+    for (int g = 0; g < groups; ++g) acc += red[(s * 4 + e) * 256 + g * nq + q];
+    out[s * C + c] = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ dA, const float* __restrict__ y,
+                                                            const float* __restrict__ stats, int M, int C,
+                                                            float* __restrict__ partials) {
+  const int nq = C / 4, groups = 256 / nq;
+  const int q = threadIdx.x % nq, g = threadIdx.x / nq;
+  const int c = q * 4;
+  const f32x4 mean = *reinterpret_cast<const f32x4*>(stats + c);
+  const f32x4 inv = *reinterpret_cast<const f32x4*>(stats + C + c);
+  const f32x4 sc = *reinterpret_cast<const f32x4*>(stats + 2 * C + c);
+  const f32x4 sh = *reinterpret_cast<const f32x4*>(stats + 3 * C + c);
+  float v[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  const int r0 = blockIdx.x * BN_ROWS;
+  const int r1 = min(M, r0 + BN_ROWS);
+  for (int r = r0 + g; r < r1; r += groups) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(dA + (int64_t)r * C + c);
+    const f32x4 yy = *reinterpret_cast<const f32x4*>(y + (int64_t)r * C + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float z = fmaf(yy[e], sc[e], sh[e]);
+      const float dz = z > 0.f ? a[e] : 0.f;
+      v[0][e] += dz;
+      v[1][e] = fmaf(dz, (yy[e] - mean[e]) * inv[e], v[1][e]);
+    }
+  }
+  bn_block_reduce_store(v, C, partials + (int64_t)blockIdx.x * 2 * C);
+}
+
+int bn_bwd_reduce(const float* dA, const float* y, const float* stats, int M, int C, float* partials, int* nparts,
+                  hipStream_t st) {
+  VAD_CHECK(C % 4 == 0 && C <= 1024 && 256 % (C / 4) == 0, "bn_bwd_reduce: unsupported C");
+  const int P = bn_rows_parts(M, C);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(P), dim3(256), 0, st, dA, y, stats, M, C, partials);
+  VAD_LAUNCH_CHECK();
+  *nparts = P;
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ partials, int P, int C,
+                                                              double count, const float* __restrict__ gamma,
+                                                              float* __restrict__ stats, float* dgamma,
+                                                              float* dbeta) {
+  const int c = blockIdx.x;
+  __shared__ double red[2][256];
+  double a = 0.0, b = 0.0;
+  for (int p = threadIdx.x; p < P; p += 256) {
+    a += (double)partials[(int64_t)p * 2 * C + c];
+    b += (double)partials[(int64_t)p * 2 * C + C + c];
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double sdz = red[0][0], sdzx = red[1][0];
+    if (dgamma) dgamma[c] = (float)sdzx;
+    if (dbeta) dbeta[c] = (float)sdz;
+    stats[4 * C + c] = gamma[c] * stats[C + c];
+    stats[5 * C + c] = (float)(sdz / count);
+    stats[6 * C + c] = (float)(sdzx / count);
+  }
+}
+
+int bn_bwd_finalize(const float* partials, int P, int C, double count, const float* gamma, float* stats,
+                    float* dgamma, float* dbeta, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partials, P, C, count, gamma, stats, dgamma,
+                     dbeta);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ dA, const float* __restrict__ y,
+                                                           const float* __restrict__ stats, int M, int C,
+                                                           float* __restrict__ dY, float* __restrict__ bparts) {
+  const int nq = C / 4, groups = 256 / nq;
+  const int q = threadIdx.x % nq, g = threadIdx.x / nq;
+  const int c = q * 4;
+  const f32x4 mean = *reinterpret_cast<const f32x4*>(stats + c);
+  const f32x4 inv = *reinterpret_cast<const f32x4*>(stats + C + c);
+  const f32x4 sc = *reinterpret_cast<const f32x4*>(stats + 2 * C + c);
+  const f32x4 sh = *reinterpret_cast<const f32x4*>(stats + 3 * C + c);
+  const f32x4 k = *reinterpret_cast<const f32x4*>(stats + 4 * C + c);
+  const f32x4 mdz = *reinterpret_cast<const f32x4*>(stats + 5 * C + c);
+  const f32x4 mdzx = *reinterpret_cast<const f32x4*>(stats + 6 * C + c);
+  float v[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  const int r0 = blockIdx.x * BN_ROWS;
+  const int r1 = min(M, r0 + BN_ROWS);
+  for (int r = r0 + g; r < r1; r += groups) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(dA + (int64_t)r * C + c);
+    const f32x4 yy = *reinterpret_cast<const f32x4*>(y + (int64_t)r * C + c);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float z = fmaf(yy[e], sc[e], sh[e]);
+      const float dz = z > 0.f ? a[e] : 0.f;
+      const float xh = (yy[e] - mean[e]) * inv[e];
+      o[e] = k[e] * (dz - mdz[e] - xh * mdzx[e]);
+      v[0][e] += o[e];
+    }
+    *reinterpret_cast<f32x4*>(dY + (int64_t)r * C + c) = o;
+  }
+  bn_block_reduce_store(v, C, bparts + (int64_t)blockIdx.x * 2 * C);
+}
+
+int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
+                 int* nparts, hipStream_t st) {
+  const int P = bn_rows_parts(M, C);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(P), dim3(256), 0, st, dA, y, stats, M, C, dY, bias_partials);
+  VAD_LAUNCH_CHECK();
+  *nparts = P;
+  return 0;
+}
+
+// =====================================================================================================
+// MaxPool 3x3 s2 p1 over relu(bn1(y)) (the frozen stem: forward only).
+// =====================================================================================================
+__global__ __launch_bounds__(256) void maxpool_kernel(const float* __restrict__ y, const float* __restrict__ stats,
+                                                      int NF, int H, int W, int C, float* __restrict__ out, int OH,
+                                                      int OW) {
+  const int nq = C / 4;
+  const int64_t total = (int64_t)NF * OH * OW * nq;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int q = (int)(i % nq);
+    int64_t p = i / nq;
+    const int ox = (int)(p % OW);
+    p /= OW;
+    const int oy = (int)(p % OH);
+    const int img = (int)(p / OH);
+    const int c = q * 4;
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(stats + 2 * C + c);
+    const f32x4 sh = *reinterpret_cast<const f32x4*>(stats + 3 * C + c);
+    f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int iy = 2 * oy + dy;
+      if (iy < 0 || iy >= H) continue;
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int ix = 2 * ox + dx;
+        if (ix < 0 || ix >= W) continue;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(y + (((int64_t)img * H + iy) * W + ix) * C + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f));
+      }
+    }
+    *reinterpret_cast<f32x4*>(out + (((int64_t)img * OH + oy) * OW + ox) * C + c) = m;
+  }
+}
+
+int maxpool3s2_bnrelu(const float* y, const float* stats, int NF, int H, int W, int C, float* out, int OH, int OW,
+                      hipStream_t st) {
+  VAD_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && C % 4 == 0, "maxpool: bad dims");
+  const int64_t total = (int64_t)NF * OH * OW * (C / 4);
+  const int grid = (int)std::min<int64_t>(cdiv(total, 256), 8192);
+  hipLaunchKernelGGL(maxpool_kernel, dim3(grid), dim3(256), 0, st, y, stats, NF, H, W, C, out, OH, OW);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+// =====================================================================================================
+// AdaptiveAvgPool2d((4,6)) on relu(bn(y)) + flatten (c*24 + i*6 + j) + mean over T, and its backward.
+// torch bins: start = floor(i*In/Out), end = ceil((i+1)*In/Out).
+// =====================================================================================================
+__device__ inline int ap_start(int i, int in, int out) { return (i * in) / out; }
+__device__ inline int ap_end(int i, int in, int out) { return ((i + 1) * in + out - 1) / out; }
+
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restrict__ y, const float* __restrict__ stats,
+                                                          int B, int T, int H, int W, int C,
+                                                          float* __restrict__ feats, float* __restrict__ pooled) {
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float sc = stats[2 * C + c], sh = stats[3 * C + c];
+  float psum[24];
+#pragma unroll
+  for (int k = 0; k < 24; ++k) psum[k] = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const int img = b * T + t;
+    const float* yi = y + (int64_t)img * H * W * C;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int h0 = ap_start(i, H, 4), h1 = ap_end(i, H, 4);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int w0 = ap_start(j, W, 6), w1 = ap_end(j, W, 6);
+        float s = 0.f;
+        for (int hh = h0; hh < h1; ++hh)
+          for (int ww = w0; ww < w1; ++ww) s += fmaxf(fmaf(yi[((int64_t)hh * W + ww) * C + c], sc, sh), 0.f);
+        const float v = s / (float)((h1 - h0) * (w1 - w0));
+        feats[(int64_t)img * C * 24 + c * 24 + i * 6 + j] = v;
+        psum[i * 6 + j] += v;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 24; ++k) pooled[(int64_t)b * C * 24 + c * 24 + k] = psum[k] / (float)T;
+}
+
+int avgpool_fwd(const float* y, const float* stats, int B, int T, int H, int W, int C, float* feats, float* pooled,
+                hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((unsigned)cdiv(C, 256), B), dim3(256), 0, st, y, stats, B, T, H, W, C,
+                     feats, pooled);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restrict__ dfeat,
+                                                          const float* __restrict__ dpooled, int B, int T, int H,
+                                                          int W, int C, float* __restrict__ dA) {
+  const int img = blockIdx.y;
+  const int b = img / T;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float g[24];
+  const float invT = 1.f / (float)T;
+#pragma unroll
+  for (int k = 0; k < 24; ++k) {
+    float v = dfeat ? dfeat[(int64_t)img * C * 24 + c * 24 + k] : 0.f;
+    if (dpooled) v += dpooled[(int64_t)b * C * 24 + c * 24 + k] * invT;
+    g[k] = v;
+  }
+  for (int hh = 0; hh < H; ++hh) {
+    for (int ww = 0; ww < W; ++ww) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int h0 = ap_start(i, H, 4), h1 = ap_end(i, H, 4);
+        if (hh < h0 || hh >= h1) continue;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          const int w0 = ap_start(j, W, 6), w1 = ap_end(j, W, 6);
+          if (ww < w0 || ww >= w1) continue;
+          s += g[i * 6 + j] / (float)((h1 - h0) * (w1 - w0));
+        }
+      }
+      dA[(((int64_t)img * H + hh) * W + ww) * C + c] = s;
+    }
+  }
+}
+
+int avgpool_bwd(const float* dfeat, const float* dpooled, int B, int T, int H, int W, int C, float* dA,
+                hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3((unsigned)cdiv(C, 256), B * T), dim3(256), 0, st, dfeat, dpooled, B, T,
+                     H, W, C, dA);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+// =====================================================================================================
+// GEMM epilogues
+// =====================================================================================================
+struct EpiConvFwd {  // y = acc + bias (NHWC rows), plus per-block BN partial sums
+  static constexpr int SCRATCH = 2 * 4 * 256;
+  struct Params { float* y; const float* bias; int C; float* partials; };
+  template <class Cfg>
+  static __device__ void apply(const Params& P, f32x16 (&acc)[Cfg::TM][Cfg::TN], int m0, int n0, int wm, int wn,
+                               int lane, int M, int N, float* lds) {
+    float s1[Cfg::TN], s2[Cfg::TN];
+#pragma unroll
+    for (int j = 0; j < Cfg::TN; ++j) {
+      s1[j] = s2[j] = 0.f;
+      const int col = n0 + acc_col<Cfg>(wn, j, lane);
+      const float bj = col < N ? P.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + acc_row<Cfg>(wm, i, r, lane);
+          if (row < M && col < N) {
+            const float v = acc[i][j][r] + bj;
+            P.y[(int64_t)row * P.C + col] = v;
+            s1[j] += v;
+            s2[j] = fmaf(v, v, s2[j]);
+          }
+        }
+      s1[j] += __shfl_xor(s1[j], 32, 64);
+      s2[j] += __shfl_xor(s2[j], 32, 64);
+    }
+    // lds is free: the main loop ended with a barrier
+    constexpr int BN = Cfg::BN;
+    if (lane < 32) {
+#pragma unroll
+      for (int j = 0; j < Cfg::TN; ++j) {
+        const int c = (wn * Cfg::TN + j) * 32 + lane;
+        lds[wm * BN + c] = s1[j];
+        lds[Cfg::WM * BN + wm * BN + c] = s2[j];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < BN; c += 256) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < Cfg::WM; ++w) {
+        a += lds[w * BN + c];
+        b += lds[Cfg::WM * BN + w * BN + c];
+      }
+      if (n0 + c < N) {
+        P.partials[(int64_t)blockIdx.x * 2 * P.C + n0 + c] = a;
+        P.partials[(int64_t)blockIdx.x * 2 * P.C + P.C + n0 + c] = b;
+      }
+    }
+  }
+};
+
+struct EpiConvDgrad {  // scatter rows of a (parity-class) grid back to the full NHWC input gradient
+  static constexpr int SCRATCH = 0;
+  struct Params { float* dst; int GA, GB, ra, pa, rb, pb, DH, DW, C; };
+  template <class Cfg>
+  static __device__ void apply(const Params& P, f32x16 (&acc)[Cfg::TM][Cfg::TN], int m0, int n0, int wm, int wn,
+                               int lane, int M, int N, float*) {
+#pragma unroll
+    for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + acc_row<Cfg>(wm, i, r, lane);
+        if (row >= M) continue;
+        const int img = row / (P.GA * P.GB);
+        const int rem = row - img * P.GA * P.GB;
+        const int a = rem / P.GB, b = rem - a * P.GB;
+        const int64_t base = (((int64_t)img * P.DH + a * P.ra + P.pa) * P.DW + b * P.rb + P.pb) * P.C;
+#pragma unroll
+        for (int j = 0; j < Cfg::TN; ++j) {
+          const int col = n0 + acc_col<Cfg>(wn, j, lane);
+          if (col < N) P.dst[base + col] = acc[i][j][r];
+        }
+      }
+  }
+};
+
+struct EpiPartial {  // split-K slab: part[z][row][col]
+  static constexpr int SCRATCH = 0;
+  struct Params { float* part; int64_t ld; };
+  template <class Cfg>
+  static __device__ void apply(const Params& P, f32x16 (&acc)[Cfg::TM][Cfg::TN], int m0, int n0, int wm, int wn,
+                               int lane, int M, int N, float*) {
+    float* base = P.part + (int64_t)blockIdx.z * M * P.ld;
+#pragma unroll
+    for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + acc_row<Cfg>(wm, i, r, lane);
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < Cfg::TN; ++j) {
+          const int col = n0 + acc_col<Cfg>(wn, j, lane);
+          if (col < N) base[(int64_t)row * P.ld + col] = acc[i][j][r];
+        }
+      }
+  }
+};
+
+struct DenseEpiArgs {
+  float* out; int64_t ldc; const float* bias; int relu; int drop; uint64_t h1; uint32_t thr; float dscale;
+  int64_t row0; const float* gate; float gscale;
+};
+
+__device__ inline float dense_finish(const DenseEpiArgs& P, int row, int col, float v) {
+  if (P.bias) v += P.bias[col];
+  if (P.relu) v = fmaxf(v, 0.f);
+  if (P.drop) v = (rng_u24(P.h1, (uint64_t)(P.row0 + row), (uint64_t)col) >= P.thr) ? v * P.dscale : 0.f;
+  if (P.gate) v = P.gate[(int64_t)row * P.ldc + col] > 0.f ? v * P.gscale : 0.f;
+  return v;
+}
+
+struct EpiDense {
+  static constexpr int SCRATCH = 0;
+  using Params = DenseEpiArgs;
+  template <class Cfg>
+  static __device__ void apply(const Params& P, f32x16 (&acc)[Cfg::TM][Cfg::TN], int m0, int n0, int wm, int wn,
+                               int lane, int M, int N, float*) {
+#pragma unroll
+    for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + acc_row<Cfg>(wm, i, r, lane);
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < Cfg::TN; ++j) {
+          const int col = n0 + acc_col<Cfg>(wn, j, lane);
+          if (col < N) P.out[(int64_t)row * P.ldc + col] = dense_finish(P, row, col, acc[i][j][r]);
+        }
+      }
+  }
+};
+
+__global__ __launch_bounds__(256) void dense_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                                  DenseEpiArgs P, const int* skip) {
+  if (skip && *skip == 0) return;
+  const int64_t total = (int64_t)M * N;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += part[z * total + i];
+    const int row = (int)(i / N), col = (int)(i % N);
+    P.out[(int64_t)row * P.ldc + col] = dense_finish(P, row, col, s);
+  }
+}
+
+// weight grad of a Linear: part[S][N][K+1] -> dW[N][K], db[N]
+__global__ __launch_bounds__(256) void dense_wgrad_reduce_kernel(const float* __restrict__ part, int S, int N, int K,
+                                                                 float* __restrict__ dW, float* __restrict__ db,
+                                                                 const int* skip) {
+  if (skip && *skip == 0) return;
+  const int64_t ld = K + 1;
+  const int64_t total = (int64_t)N * ld;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += part[z * total + i];
+    const int row = (int)(i / ld), col = (int)(i % ld);
+    if (col < K) dW[(int64_t)row * K + col] = s;
+    else db[row] = s;
+  }
+}
+
+// =====================================================================================================
+// launch helpers
+// =====================================================================================================
+template <class Cfg, template <int> class LA, template <int> class LB, class Epi>
+static int launch_gemm(const typename LA<Cfg::BM>::Params& pa, const typename LB<Cfg::BN>::Params& pb,
+                       const typename Epi::Params& pe, int M, int N, int K, int splits, const int* skip,
+                       hipStream_t st, int* used_splits = nullptr) {
+  if (M <= 0 || N <= 0) return 0;
+  splits = std::max(1, splits);
+  int kps = (int)(cdiv(cdiv(K, splits), BK) * BK);
+  if (kps <= 0) kps = BK;
+  splits = (int)cdiv(K, kps);
+  if (splits < 1) splits = 1;
+  dim3 grid((unsigned)cdiv(M, Cfg::BM), (unsigned)cdiv(N, Cfg::BN), (unsigned)splits);
+  hipLaunchKernelGGL((gemm_kernel<Cfg, LA<Cfg::BM>, LB<Cfg::BN>, Epi>), grid, dim3(256), 0, st, pa, pb, pe, M, N, K,
+                     kps, skip);
+  VAD_LAUNCH_CHECK();
+  if (used_splits) *used_splits = splits;
+  return 0;
+}
+
+using T128x32 = TileCfg<4, 1, 1, 1>;
+using T128x64 = TileCfg<2, 2, 2, 1>;
+using T64x64 = TileCfg<2, 2, 1, 1>;
+using T128x128 = TileCfg<2, 2, 2, 2>;
+using T32x128 = TileCfg<1, 4, 1, 1>;
+
+// =====================================================================================================
+// 3x3 convs
+// =====================================================================================================
+static void fwd_taps(TapTable& t) {
+  t.ntaps = 9;
+  for (int k = 0; k < 9; ++k) {
+    t.dh[k] = (int8_t)(k / 3 - 1);
+    t.dw[k] = (int8_t)(k % 3 - 1);
+  }
+}
+
+// dgrad parity classes.  stride 1: one class, all taps, src offset = 1 - k.  stride 2: class (ph,pw) uses
+// taps kh with (ph+1-kh) even, src offset (ph+1-kh)/2.
+struct DgradClass {
+  int ph, pw, nrt, nct;
+  int kh[2], dh[2], kw[2], dw[2];
+};
+static int dgrad_classes(int stride, DgradClass* cls) {
+  if (stride == 1) return 0;
+  int n = 0;
+  for (int ph = 0; ph < 2; ++ph)
+    for (int pw = 0; pw < 2; ++pw) {
+      DgradClass c{};
+      c.ph = ph; c.pw = pw; c.nrt = c.nct = 0;
+      for (int k = 0; k < 3; ++k) {
+        if (((ph + 1 - k) & 1) == 0) { c.kh[c.nrt] = k; c.dh[c.nrt] = (ph + 1 - k) / 2; ++c.nrt; }
+        if (((pw + 1 - k) & 1) == 0) { c.kw[c.nct] = k; c.dw[c.nct] = (pw + 1 - k) / 2; ++c.nct; }
+      }
+      cls[n++] = c;
+    }
+  return n;
+}
+
+// dgrad weight images: stride 1 -> Wd[ci][t=kh*3+kw][co]; stride 2 -> per class, concatenated,
+// Wd_c[ci][ri*nct+cj][co] for taps (kh[ri], kw[cj]).
+__global__ void conv3_prep_kernel(const float* __restrict__ w, int Ci, int Co, int stride, float* __restrict__ wf,
+                                  float* __restrict__ wd) {
+  const int64_t total = (int64_t)Co * Ci * 9;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int t = (int)(i % 9);
+    const int ci = (int)((i / 9) % Ci);
+    const int co = (int)(i / (9 * Ci));
+    const float v = w[i];
+    wf[((int64_t)co * 9 + t) * Ci + ci] = v;
+    const int kh = t / 3, kw = t % 3;
+    if (stride == 1) {
+      wd[((int64_t)ci * 9 + t) * Co + co] = v;
+    } else {
+      // class (ph,pw): kh valid iff (ph+1-kh) even -> ph = (kh+1)&1; its index among the class's row taps
+      const int ph = (kh + 1) & 1, pw = (kw + 1) & 1;
+      const int ri = (ph == 0) ? 0 : (kh == 0 ? 0 : 1);
+      const int cj = (pw == 0) ? 0 : (kw == 0 ? 0 : 1);
+      const int nrt = ph == 0 ? 1 : 2, nct = pw == 0 ? 1 : 2;
+      int64_t off = 0;  // classes in order (0,0),(0,1),(1,0),(1,1)
+      for (int c = 0; c < ph * 2 + pw; ++c) {
+        const int r = (c >> 1) == 0 ? 1 : 2, q = (c & 1) == 0 ? 1 : 2;
+        off += (int64_t)r * q * Ci * Co;
+      }
+      wd[off + ((int64_t)ci * (nrt * nct) + ri * nct + cj) * Co + co] = v;
+    }
+  }
+}
+
+int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd, hipStream_t st) {
+  const int64_t total = (int64_t)L.Co * L.Ci * 9;
+  hipLaunchKernelGGL(conv3_prep_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, w, L.Ci, L.Co, L.stride,
+                     wf, wd);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
+              float* y, float* partials, int* nparts, hipStream_t st) {
+  VAD_CHECK(L.Ci % 32 == 0, "conv3_fwd: Ci must be a multiple of 32");
+  ConvGeom g{L.NF, L.OH, L.OW, L.stride, L.stride, L.IH, L.IW, L.Ci};
+  TapTable taps;
+  fwd_taps(taps);
+  const int M = L.NF * L.OH * L.OW, N = L.Co, K = 9 * L.Ci;
+  EpiConvFwd::Params pe{y, bias, L.Co, partials};
+  if (L.Co == 32) {
+    using C = T128x32;
+    ConvGatherKC<C::BM>::Params pa{src, g, taps, src_stats ? src_stats + 2 * L.Ci : nullptr,
+                                   src_stats ? src_stats + 3 * L.Ci : nullptr};
+    DenseKC<C::BN>::Params pb{wf, K, N, K};
+    VAD_TRY((launch_gemm<C, ConvGatherKC, DenseKC, EpiConvFwd>(pa, pb, pe, M, N, K, 1, nullptr, st)));
+    *nparts = (int)cdiv(M, C::BM);
+  } else if (M >= 64 * 1024) {
+    using C = T128x64;
+    ConvGatherKC<C::BM>::Params pa{src, g, taps, src_stats ? src_stats + 2 * L.Ci : nullptr,
+                                   src_stats ? src_stats + 3 * L.Ci : nullptr};
+    DenseKC<C::BN>::Params pb{wf, K, N, K};
+    VAD_TRY((launch_gemm<C, ConvGatherKC, DenseKC, EpiConvFwd>(pa, pb, pe, M, N, K, 1, nullptr, st)));
+    *nparts = (int)cdiv(M, C::BM);
+  } else {
+    using C = T64x64;
+    ConvGatherKC<C::BM>::Params pa{src, g, taps, src_stats ? src_stats + 2 * L.Ci : nullptr,
+                                   src_stats ? src_stats + 3 * L.Ci : nullptr};
+    DenseKC<C::BN>::Params pb{wf, K, N, K};
+    VAD_TRY((launch_gemm<C, ConvGatherKC, DenseKC, EpiConvFwd>(pa, pb, pe, M, N, K, 1, nullptr, st)));
+    *nparts = (int)cdiv(M, C::BM);
+  }
+  return 0;
+}
+
+template <class C>
+static int dgrad_launch(const ConvGeom& g, const TapTable& taps, const float* dY, const float* wd, int N,
+                        const EpiConvDgrad::Params& pe, hipStream_t st) {
+  const int M = g.imgs * g.GA * g.GB, K = taps.ntaps * g.C;
+  typename ConvGatherKC<C::BM>::Params pa{dY, g, taps, nullptr, nullptr};
+  typename DenseKC<C::BN>::Params pb{wd, K, N, K};
+  return launch_gemm<C, ConvGatherKC, DenseKC, EpiConvDgrad>(pa, pb, pe, M, N, K, 1, nullptr, st);
+}
+
+int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st) {
+  VAD_CHECK(L.Co % 32 == 0, "conv3_dgrad: Co must be a multiple of 32");
+  const int N = L.Ci;
+  if (L.stride == 1) {
+    ConvGeom g{L.NF, L.IH, L.IW, 1, 1, L.OH, L.OW, L.Co};
+    TapTable taps;
+    taps.ntaps = 9;
+    for (int k = 0; k < 9; ++k) {
+      taps.dh[k] = (int8_t)(1 - k / 3);
+      taps.dw[k] = (int8_t)(1 - k % 3);
+    }
+    EpiConvDgrad::Params pe{dX, L.IH, L.IW, 1, 0, 1, 0, L.IH, L.IW, L.Ci};
+    const int M = L.NF * L.IH * L.IW;
+    if (N == 32) return dgrad_launch<T128x32>(g, taps, dY, wd, N, pe, st);
+    if (M >= 64 * 1024) return dgrad_launch<T128x64>(g, taps, dY, wd, N, pe, st);
+    return dgrad_launch<T64x64>(g, taps, dY, wd, N, pe, st);
+  }
+  DgradClass cls[4];
+  const int nc = dgrad_classes(2, cls);
+  int64_t off = 0;
+  for (int ci = 0; ci < nc; ++ci) {
+    const DgradClass& c = cls[ci];
+    const int GA = (L.IH - c.ph + 1) / 2, GB = (L.IW - c.pw + 1) / 2;
+    ConvGeom g{L.NF, GA, GB, 1, 1, L.OH, L.OW, L.Co};
+    TapTable taps;
+    taps.ntaps = c.nrt * c.nct;
+    for (int r = 0; r < c.nrt; ++r)
+      for (int q = 0; q < c.nct; ++q) {
+        taps.dh[r * c.nct + q] = (int8_t)c.dh[r];
+        taps.dw[r * c.nct + q] = (int8_t)c.dw[q];
+      }
+    EpiConvDgrad::Params pe{dX, GA, GB, 2, c.ph, 2, c.pw, L.IH, L.IW, L.Ci};
+    const float* w = wd + off;
+    const int M = L.NF * GA * GB;
+    if (N == 32) VAD_TRY(dgrad_launch<T128x32>(g, taps, dY, w, N, pe, st));
+    else if (M >= 64 * 1024) VAD_TRY(dgrad_launch<T128x64>(g, taps, dY, w, N, pe, st));
+    else VAD_TRY(dgrad_launch<T64x64>(g, taps, dY, w, N, pe, st));
+    off += (int64_t)taps.ntaps * L.Ci * L.Co;
+  }
+  return 0;
+}
+
+int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
+                int* nsplit, int64_t partial_cap, hipStream_t st) {
+  const int M = L.Co, N = 9 * L.Ci, K = L.NF * L.OH * L.OW;
+  ConvPatchKM<128>::Params dummy{};
+  (void)dummy;
+  auto run = [&](auto cfg) -> int {
+    using C = decltype(cfg);
+    const int tiles = (int)(cdiv(M, C::BM) * cdiv(N, C::BN));
+    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(1024, tiles), cdiv(K, 4 * BK)));
+    while ((int64_t)splits * M * N > partial_cap && splits > 1) splits /= 2;
+    typename DenseKM<C::BM>::Params pa{dY, L.Co, L.Co, K, -1};
+    typename ConvPatchKM<C::BN>::Params pb{src, L.NF, L.OH, L.OW, L.stride, 1, L.IH, L.IW, L.Ci, 3, N,
+                                           src_stats ? src_stats + 2 * L.Ci : nullptr,
+                                           src_stats ? src_stats + 3 * L.Ci : nullptr};
+    EpiPartial::Params pe{partial, N};
+    return launch_gemm<C, DenseKM, ConvPatchKM, EpiPartial>(pa, pb, pe, M, N, K, splits, nullptr, st, nsplit);
+  };
+  if (M == 32) return run(T32x128{});
+  return run(T64x64{});
+}
+
+__global__ __launch_bounds__(256) void conv3_wgrad_reduce_kernel(const float* __restrict__ part, int S, int Co, int Ci,
+                                                                 const float* __restrict__ bparts, int NB,
+                                                                 float* __restrict__ dW, float* __restrict__ db) {
+  const int64_t total = (int64_t)Co * Ci * 9;
+  const int64_t ldp = 9 * Ci;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    // i indexes dW[co][ci][t]
+    const int t = (int)(i % 9);
+    const int ci = (int)((i / 9) % Ci);
+    const int co = (int)(i / (9 * Ci));
+    const int64_t src = (int64_t)co * ldp + t * Ci + ci;
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += part[(int64_t)z * Co * ldp + src];
+    dW[i] = s;
+  }
+  if (blockIdx.x == 0) {
+    for (int co = threadIdx.x; co < Co; co += 256) {
+      float s = 0.f;
+      for (int p = 0; p < NB; ++p) s += bparts[(int64_t)p * 2 * Co + co];
+      db[co] = s;
+    }
+  }
+}
+
+int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, const float* bias_partials,
+                       int nbias_parts, float* dW, float* db, hipStream_t st) {
+  const int64_t total = (int64_t)L.Co * L.Ci * 9;
+  const int grid = (int)std::min<int64_t>(cdiv(total, 256), 2048);
+  hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3(grid), dim3(256), 0, st, partial, nsplit, L.Co, L.Ci,
+                     bias_partials, nbias_parts, dW, db);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+// =====================================================================================================
+// dense layers
+// =====================================================================================================
+int dense_fwd(const float* X, int M, int K, const float* W, const float* b, int N, float* Y, const DenseAct& act,
+              float* scratch, int64_t scratch_floats, hipStream_t st) {
+  using C = T64x64;
+  DenseEpiArgs pe{Y, N, b, act.relu, act.drop, act.h1, act.thr, act.dscale, act.row0, nullptr, 1.f};
+  DenseKC<C::BM>::Params pa{X, K, M, K};
+  DenseKC<C::BN>::Params pb{W, K, N, K};
+  const int tiles = (int)(cdiv(M, C::BM) * cdiv(N, C::BN));
+  int splits = (int)std::min<int64_t>(cdiv(256, tiles), cdiv(K, 4 * BK));
+  while (splits > 1 && (int64_t)splits * M * N > scratch_floats) splits /= 2;
+  if (splits <= 1) return launch_gemm<C, DenseKC, DenseKC, EpiDense>(pa, pb, pe, M, N, K, 1, nullptr, st);
+  EpiPartial::Params pp{scratch, N};
+  int used = 1;
+  VAD_TRY((launch_gemm<C, DenseKC, DenseKC, EpiPartial>(pa, pb, pp, M, N, K, splits, nullptr, st, &used)));
+  const int64_t total = (int64_t)M * N;
+  hipLaunchKernelGGL(dense_splitk_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 1024)), dim3(256),
+                     0, st, scratch, used, M, N, pe, nullptr);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX, const float* gate, float gscale,
+                const int* skip, hipStream_t st) {
+  // dX[m][k] = sum_n dY[m][n] W[n][k]: A = dY (KC over n), B(row k, red n) = W[n][k] (KM, ld K)
+  using C = T64x64;
+  DenseEpiArgs pe{dX, K, nullptr, 0, 0, 0, 0, 1.f, 0, gate, gscale};
+  DenseKC<C::BM>::Params pa{dY, N, M, N};
+  DenseKM<C::BN>::Params pb{W, K, K, N, -1};
+  return launch_gemm<C, DenseKC, DenseKM, EpiDense>(pa, pb, pe, M, K, N, 1, skip, st);
+}
+
+int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW, float* db, float* scratch,
+                int64_t scratch_floats, const int* skip, hipStream_t st) {
+  // GEMM rows = out feature n, cols = in feature k (+ ones column for the bias), reduction over m
+  using C = T64x64;
+  const int GN = K + 1;
+  DenseKM<C::BM>::Params pa{dY, N, N, M, -1};
+  DenseKM<C::BN>::Params pb{X, K, K, M, K};
+  const int tiles = (int)(cdiv(N, C::BM) * cdiv(GN, C::BN));
+  int splits = (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(256, tiles)), cdiv(M, 4 * BK));
+  while (splits > 1 && (int64_t)splits * N * GN > scratch_floats) splits /= 2;
+  VAD_CHECK((int64_t)N * GN <= scratch_floats, "dense_wgrad: scratch too small");
+  EpiPartial::Params pp{scratch, GN};
+  int used = 1;
+  VAD_TRY((launch_gemm<C, DenseKM, DenseKM, EpiPartial>(pa, pb, pp, N, GN, M, splits, skip, st, &used)));
+  const int64_t total = (int64_t)N * GN;
+  hipLaunchKernelGGL(dense_wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 2048)), dim3(256),
+                     0, st, scratch, used, N, K, dW, db, skip);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace vad

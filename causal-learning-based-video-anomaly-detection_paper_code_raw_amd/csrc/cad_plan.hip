@@ -1,0 +1,699 @@
+// Orchestration of the CausalAnomalyDetector train step (causal_anomaly_detection.py:540-586, 609-690) on one
+// HIP stream, plus the optimizer kernels and the extern "C" ABI declared in include/vad.h.
+// The plan owns no device memory: PyTorch allocates the workspace and the flat parameter/grad/state buffers.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/vad.h"
+#include "backbone.h"
+#include "head.h"
+
+namespace vad {
+
+// ------------------------------------------------------------------ parameter slot table (state_dict order)
+enum Group { G_FROZEN = 0, G_ALWAYS = 1, G_DET = 2, G_STRUCT = 3, G_NEVER = 4 };
+struct Slot {
+  std::string name;
+  int64_t numel;
+  int group;
+  int64_t offset;
+};
+struct BufSlot {
+  std::string name;
+  int64_t numel;
+  int64_t offset;
+};
+
+constexpr int64_t ALIGN = 256;
+static int64_t align_up(int64_t v) { return (v + ALIGN - 1) / ALIGN * ALIGN; }
+
+struct CadLayout {
+  std::vector<Slot> slots;
+  std::vector<BufSlot> bufs;
+  int64_t param_floats = 0, buf_floats = 0;
+  // indices
+  int conv1_w, conv1_b, bn1_w, bn1_b;
+  int conv_w[8], conv_b[8], bn_w[8], bn_b[8];
+  int det_w[5], det_b[5], dir_w[5], dir_b[5];
+  int head0;  // first head slot (tracker.reid_net.0.weight)
+  int rm[9], rv[9];
+  CadLayout() {
+    auto add = [&](const std::string& n, int64_t k, int g) {
+      slots.push_back({n, k, g, 0});
+      return (int)slots.size() - 1;
+    };
+    auto addb = [&](const std::string& n, int64_t k) {
+      bufs.push_back({n, k, 0});
+      return (int)bufs.size() - 1;
+    };
+    conv1_w = add("backbone.conv1.weight", 32 * 49, G_FROZEN);
+    conv1_b = add("backbone.conv1.bias", 32, G_FROZEN);
+    bn1_w = add("backbone.bn1.weight", 32, G_FROZEN);
+    bn1_b = add("backbone.bn1.bias", 32, G_FROZEN);
+    rm[0] = addb("backbone.bn1.running_mean", 32);
+    rv[0] = addb("backbone.bn1.running_var", 32);
+    const int cin[8] = {32, 32, 32, 64, 64, 128, 128, 256};
+    const int cout[8] = {32, 32, 64, 64, 128, 128, 256, 256};
+    for (int l = 0; l < 8; ++l) {
+      const std::string L = "backbone.layer" + std::to_string(l / 2 + 1) + ".";
+      const std::string c = L + (l % 2 == 0 ? "0" : "3"), b = L + (l % 2 == 0 ? "1" : "4");
+      conv_w[l] = add(c + ".weight", (int64_t)cout[l] * cin[l] * 9, G_ALWAYS);
+      conv_b[l] = add(c + ".bias", cout[l], G_ALWAYS);
+      bn_w[l] = add(b + ".weight", cout[l], G_ALWAYS);
+      bn_b[l] = add(b + ".bias", cout[l], G_ALWAYS);
+      rm[l + 1] = addb(b + ".running_mean", cout[l]);
+      rv[l + 1] = addb(b + ".running_var", cout[l]);
+    }
+    const int dims[6] = {6144, 512, 256, 128, 64, 20};
+    const int didx[5] = {0, 3, 6, 8, 10};
+    for (int i = 0; i < 5; ++i) {
+      det_w[i] = add("detector.detector_net." + std::to_string(didx[i]) + ".weight", (int64_t)dims[i + 1] * dims[i],
+                     G_DET);
+      det_b[i] = add("detector.detector_net." + std::to_string(didx[i]) + ".bias", dims[i + 1], G_DET);
+    }
+    struct H { const char* n; int64_t k; int g; };
+    const H head[H_NUM] = {
+        {"tracker.reid_net.0.weight", 32 * 4, G_ALWAYS}, {"tracker.reid_net.0.bias", 32, G_ALWAYS},
+        {"tracker.reid_net.2.weight", 64 * 32, G_ALWAYS}, {"tracker.reid_net.2.bias", 64, G_ALWAYS},
+        {"tracker.reid_net.4.weight", 64 * 64, G_ALWAYS}, {"tracker.reid_net.4.bias", 64, G_ALWAYS},
+        {"traj_encoder.gru.weight_ih_l0", 192 * 68, G_ALWAYS}, {"traj_encoder.gru.weight_hh_l0", 192 * 64, G_ALWAYS},
+        {"traj_encoder.gru.bias_ih_l0", 192, G_ALWAYS}, {"traj_encoder.gru.bias_hh_l0", 192, G_ALWAYS},
+        {"traj_encoder.encoder.weight", 32 * 64, G_ALWAYS}, {"traj_encoder.encoder.bias", 32, G_ALWAYS},
+        {"causal_extractor.encoder.0.weight", 32 * 32, G_ALWAYS}, {"causal_extractor.encoder.0.bias", 32, G_ALWAYS},
+        {"causal_extractor.encoder.2.weight", 32 * 32, G_ALWAYS}, {"causal_extractor.encoder.2.bias", 32, G_ALWAYS},
+        {"causal_extractor.mu_head.weight", 6 * 32, G_ALWAYS}, {"causal_extractor.mu_head.bias", 6, G_ALWAYS},
+        {"causal_extractor.logvar_head.weight", 6 * 32, G_ALWAYS}, {"causal_extractor.logvar_head.bias", 6, G_ALWAYS},
+        {"structure_learner.structure_params", 36, G_NEVER},
+        {"structure_learner.node_encoder.weight", 32 * 6, G_STRUCT}, {"structure_learner.node_encoder.bias", 32, G_STRUCT},
+        {"structure_learner.edge_predictor.0.weight", 32 * 64, G_STRUCT},
+        {"structure_learner.edge_predictor.0.bias", 32, G_STRUCT},
+        {"structure_learner.edge_predictor.2.weight", 32, G_STRUCT},
+        {"structure_learner.edge_predictor.2.bias", 1, G_STRUCT},
+        {"dynamics_predictor.dynamics_net.0.weight", 32 * 6, G_ALWAYS}, {"dynamics_predictor.dynamics_net.0.bias", 32, G_ALWAYS},
+        {"dynamics_predictor.dynamics_net.2.weight", 32 * 32, G_ALWAYS}, {"dynamics_predictor.dynamics_net.2.bias", 32, G_ALWAYS},
+        {"dynamics_predictor.dynamics_net.4.weight", 6 * 32, G_ALWAYS}, {"dynamics_predictor.dynamics_net.4.bias", 6, G_ALWAYS},
+        {"anomaly_scorer.causal_scorer.0.weight", 64 * 18, G_ALWAYS}, {"anomaly_scorer.causal_scorer.0.bias", 64, G_ALWAYS},
+        {"anomaly_scorer.causal_scorer.3.weight", 32 * 64, G_ALWAYS}, {"anomaly_scorer.causal_scorer.3.bias", 32, G_ALWAYS},
+        {"anomaly_scorer.causal_scorer.5.weight", 32, G_ALWAYS}, {"anomaly_scorer.causal_scorer.5.bias", 1, G_ALWAYS},
+        {"anomaly_scorer.motion_scorer.0.weight", 32 * 12, G_ALWAYS}, {"anomaly_scorer.motion_scorer.0.bias", 32, G_ALWAYS},
+        {"anomaly_scorer.motion_scorer.2.weight", 16 * 32, G_ALWAYS}, {"anomaly_scorer.motion_scorer.2.bias", 16, G_ALWAYS},
+        {"anomaly_scorer.motion_scorer.4.weight", 16, G_ALWAYS}, {"anomaly_scorer.motion_scorer.4.bias", 1, G_ALWAYS},
+        {"anomaly_scorer.temporal_scorer.0.weight", 32 * 6, G_ALWAYS}, {"anomaly_scorer.temporal_scorer.0.bias", 32, G_ALWAYS},
+        {"anomaly_scorer.temporal_scorer.2.weight", 16 * 32, G_ALWAYS}, {"anomaly_scorer.temporal_scorer.2.bias", 16, G_ALWAYS},
+        {"anomaly_scorer.temporal_scorer.4.weight", 16, G_ALWAYS}, {"anomaly_scorer.temporal_scorer.4.bias", 1, G_ALWAYS},
+    };
+    head0 = (int)slots.size();
+    for (int i = 0; i < H_NUM; ++i) add(head[i].n, head[i].k, head[i].g);
+    for (int i = 0; i < 5; ++i) {
+      dir_w[i] = add("direct_classifier." + std::to_string(didx[i]) + ".weight",
+                     (int64_t)(i == 4 ? 2 : dims[i + 1]) * dims[i], G_ALWAYS);
+      dir_b[i] = add("direct_classifier." + std::to_string(didx[i]) + ".bias", i == 4 ? 2 : dims[i + 1], G_ALWAYS);
+    }
+    int64_t o = 0;
+    for (auto& s : slots) {
+      s.offset = o;
+      o = align_up(o + s.numel);
+    }
+    param_floats = o;
+    o = 0;
+    for (auto& b : bufs) {
+      b.offset = o;
+      o = align_up(o + b.numel);
+    }
+    buf_floats = o;
+  }
+};
+
+static const CadLayout& layout() {
+  static CadLayout L;
+  return L;
+}
+
+constexpr int64_t FLAG_FLOATS = 256;  // grad buffer tail: [0] det flag, [1] struct flag (summed under DP)
+
+// ------------------------------------------------------------------ optimizer kernels
+__global__ __launch_bounds__(256) void sqsum_kernel(const float* __restrict__ g, int64_t n, float scale,
+                                                    float* __restrict__ partials) {
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float v = g[i] * scale;
+    s += (double)v * v;
+  }
+  __shared__ double red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partials[blockIdx.x] = (float)red[0];
+}
+
+struct SlotTab {
+  int64_t off[160];
+  int32_t group[160];
+  int nslots;
+};
+
+// per-slot step bump + bias corrections; clip coefficient (torch clip_grad_norm_: coef = max/(norm+1e-6) <= 1)
+__global__ void opt_prepare_kernel(const float* __restrict__ partials, int np, const float* __restrict__ flags,
+                                   SlotTab tab, int32_t* steps, float beta1, float beta2, float max_norm,
+                                   float* __restrict__ slot_info /* [nslots][4] */, float* clip_out,
+                                   float* total_norm_out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < np; i += 256) s += partials[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  const float norm = (float)sqrt(red[0]);
+  if (threadIdx.x == 0) {
+    float coef = max_norm / (norm + 1e-6f);
+    clip_out[0] = coef < 1.f ? coef : 1.f;
+    if (total_norm_out) total_norm_out[0] = norm;
+  }
+  for (int i = threadIdx.x; i < tab.nslots; i += 256) {
+    const int g = tab.group[i];
+    bool active = g == G_ALWAYS || (g == G_DET && flags[0] > 0.f) || (g == G_STRUCT && flags[1] > 0.f);
+    float st = 0.f, bc1 = 1.f, bc2s = 1.f;
+    if (active) {
+      const int step = steps[i] + 1;
+      steps[i] = step;
+      st = (float)step;
+      bc1 = (float)(1.0 - pow((double)beta1, (double)step));
+      bc2s = (float)sqrt(1.0 - pow((double)beta2, (double)step));
+    }
+    slot_info[i * 4 + 0] = active ? 1.f : 0.f;
+    slot_info[i * 4 + 1] = bc1;
+    slot_info[i * 4 + 2] = bc2s;
+    slot_info[i * 4 + 3] = st;
+  }
+}
+
+// torch.optim.AdamW single-tensor update, one 256-element chunk per block iteration (slots are 256-aligned)
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    const int16_t* __restrict__ chunk_slot, int64_t nchunks,
+                                                    const float* __restrict__ slot_info,
+                                                    const float* __restrict__ clip, float grad_scale, float lr,
+                                                    float beta1, float beta2, float eps, float wd) {
+  const float coef = clip[0] * grad_scale;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int s = chunk_slot[c];
+    if (s < 0) continue;
+    if (slot_info[s * 4] == 0.f) continue;
+    const float bc1 = slot_info[s * 4 + 1], bc2s = slot_info[s * 4 + 2];
+    const int64_t i = c * 256 + threadIdx.x;
+    const float gr = g[i] * coef;
+    float pv = p[i] * (1.f - lr * wd);
+    const float mv = m[i] + (gr - m[i]) * (1.f - beta1);
+    const float vv = v[i] * beta2 + gr * gr * (1.f - beta2);
+    const float denom = sqrtf(vv) / bc2s + eps;
+    pv = pv - (lr / bc1) * mv / denom;
+    p[i] = pv;
+    m[i] = mv;
+    v[i] = vv;
+  }
+}
+
+__global__ void nbt_bump_kernel(int64_t* nbt, int n) {
+  if (threadIdx.x < n) nbt[threadIdx.x] += 1;
+}
+
+__global__ void rng_u24_kernel(uint64_t h1, int64_t row0, int64_t nrows, int64_t ncols, uint32_t* out) {
+  const int64_t total = nrows * ncols;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256)
+    out[i] = rng_u24(h1, (uint64_t)(row0 + i / ncols), (uint64_t)(i % ncols));
+}
+
+// mode 0: (u8 - 0.5)/0.5 (cad Normalize); mode 1: u8/255 (ToTensor range, mc:120 / bbox:411)
+__global__ void synth_kernel(uint64_t h1, int64_t frame0, int64_t nframes, int64_t npix, int mode, float* out) {
+  const int64_t total = nframes * npix;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const uint32_t u8 = (uint32_t)(rng_hash(h1, (uint64_t)(frame0 + i / npix), (uint64_t)(i % npix)) >> 56);
+    out[i] = mode == 0 ? ((float)u8 - 0.5f) / 0.5f : (float)u8 / 255.f;
+  }
+}
+
+// ------------------------------------------------------------------ the plan
+struct Ws {
+  char* base = nullptr;
+  int64_t off = 0;
+  bool dry = true;
+  template <class T>
+  T* take(int64_t n) {
+    off = (off + 255) / 256 * 256;
+    T* p = dry ? nullptr : reinterpret_cast<T*>(base + off);
+    off += n * (int64_t)sizeof(T);
+    return p;
+  }
+};
+
+struct CadPlanImpl {
+  int B, T, H, W, NF;
+  int H1, W1, HP, WP, HF, WF;
+  Conv3Layer L[8];
+  int64_t ws_bytes = 0;
+  // bound buffers
+  float *params = nullptr, *grads = nullptr, *bufs = nullptr, *m = nullptr, *v = nullptr;
+  int64_t* nbt = nullptr;
+  int32_t* steps = nullptr;
+  // workspace carve
+  float *y1, *pool, *y[8], *stats[9], *parts, *wf[8], *wd[8], *feats, *pooled;
+  float *dh[5], *dlog, *gh[5], *glog;
+  float *head_ws;
+  int* head_iws;
+  float *probs, *finalv, *causal, *kl, *z, *adj, *boxes;
+  int *counts, *nmax, *clip_flags, *flags;
+  float *d_causal, *d_kl, *d_glog, *d_dlog, *slabs, *d_feat_det, *d_pooled, *dense_scratch;
+  float *dg[5], *ddh[5];
+  float *dA, *dY, *bparts, *wpart;
+  float *sq_parts, *slot_info, *clip;
+  int16_t* chunk_slot;
+  int64_t parts_floats, dense_scratch_floats, wpart_floats, slab_len, act_max;
+  int64_t clip0 = 0;
+  int training = 1;
+  bool have_labels = false;
+  uint64_t seed = 0, step = 0;
+  const int64_t* labels = nullptr;
+
+  void carve(Ws& w) {
+    const int64_t nf = NF;
+    y1 = w.take<float>(nf * H1 * W1 * 32);
+    pool = w.take<float>(nf * HP * WP * 32);
+    act_max = nf * HP * WP * 32;
+    for (int l = 0; l < 8; ++l) {
+      y[l] = w.take<float>(nf * L[l].OH * L[l].OW * L[l].Co);
+      wf[l] = w.take<float>((int64_t)L[l].Co * L[l].Ci * 9);
+      wd[l] = w.take<float>((int64_t)L[l].Co * L[l].Ci * 9);
+      act_max = std::max<int64_t>(act_max, nf * L[l].OH * L[l].OW * L[l].Co);
+    }
+    const int cs[9] = {32, 32, 32, 64, 64, 128, 128, 256, 256};
+    for (int l = 0; l < 9; ++l) stats[l] = w.take<float>(7 * cs[l]);
+    parts_floats = std::max<int64_t>((int64_t)conv1_num_parts(NF, H1) * 64, 1024);
+    for (int l = 0; l < 8; ++l) {
+      const int64_t M = nf * L[l].OH * L[l].OW;
+      parts_floats = std::max<int64_t>(parts_floats, cdiv(M, 64) * 2 * L[l].Co);
+    }
+    parts = w.take<float>(parts_floats);
+    feats = w.take<float>(nf * 6144);
+    pooled = w.take<float>((int64_t)B * 6144);
+    const int dd[5] = {512, 256, 128, 64, 20};
+    const int gd[5] = {512, 256, 128, 64, 2};
+    for (int i = 0; i < 4; ++i) dh[i] = w.take<float>(nf * dd[i]);
+    dlog = w.take<float>(nf * 20);
+    for (int i = 0; i < 4; ++i) gh[i] = w.take<float>((int64_t)B * gd[i]);
+    glog = w.take<float>((int64_t)B * 2);
+    head_ws = w.take<float>((int64_t)B * head_ws_floats(T));
+    head_iws = w.take<int>((int64_t)B * head_iws_ints(T));
+    probs = w.take<float>(B * 2);
+    finalv = w.take<float>(B);
+    causal = w.take<float>(B);
+    kl = w.take<float>(B);
+    z = w.take<float>(B * 30);
+    adj = w.take<float>(B * 36);
+    boxes = w.take<float>(nf * 20);
+    counts = w.take<int>(nf);
+    nmax = w.take<int>(B);
+    clip_flags = w.take<int>(B * 2);
+    flags = w.take<int>(4);
+    d_causal = w.take<float>(B);
+    d_kl = w.take<float>(B);
+    d_glog = w.take<float>(B * 2);
+    d_dlog = w.take<float>(nf * 20);
+    const CadLayout& LY = layout();
+    slab_len = LY.slots[LY.dir_w[0]].offset - LY.slots[LY.head0].offset;
+    slabs = w.take<float>((int64_t)B * slab_len);
+    d_feat_det = w.take<float>(nf * 6144);
+    d_pooled = w.take<float>((int64_t)B * 6144);
+    for (int i = 0; i < 4; ++i) {
+      ddh[i] = w.take<float>(nf * dd[i]);
+      dg[i] = w.take<float>((int64_t)B * gd[i]);
+    }
+    dense_scratch_floats = std::max<int64_t>(512ll * 6145, 16ll * nf * 512);
+    dense_scratch_floats = std::max<int64_t>(dense_scratch_floats, 16ll * B * 512);
+    dense_scratch = w.take<float>(dense_scratch_floats);
+    dA = w.take<float>(act_max);
+    dY = w.take<float>(act_max);
+    bparts = w.take<float>(cdiv(act_max / 32, 1024) * 2 * 256 + 1024);
+    wpart_floats = 16ll << 20;
+    wpart = w.take<float>(wpart_floats);
+    sq_parts = w.take<float>(1024);
+    slot_info = w.take<float>(4 * 160);
+    clip = w.take<float>(4);
+    chunk_slot = w.take<int16_t>(LY.param_floats / 256 + 1);
+  }
+
+  float* P(int slot) const { return params + layout().slots[slot].offset; }
+  float* G(int slot) const { return grads + layout().slots[slot].offset; }
+  float* RM(int i) const { return bufs + layout().bufs[layout().rm[i]].offset; }
+  float* RV(int i) const { return bufs + layout().bufs[layout().rv[i]].offset; }
+
+  HeadArgs head_args() const {
+    const CadLayout& LY = layout();
+    HeadArgs a{};
+    a.B = B;
+    a.T = T;
+    a.clip0 = clip0;
+    a.training = training;
+    a.h1_eps = rng_h1(seed, S_EPS, step);
+    a.h1_drop = rng_h1(seed, S_SCORER_DROP, step);
+    a.thr_drop = drop_threshold(0.2);
+    a.pbase = params;
+    for (int i = 0; i < H_NUM; ++i) a.off[i] = LY.slots[LY.head0 + i].offset;
+    a.head_begin = LY.slots[LY.head0].offset;
+    a.ws = head_ws;
+    a.ws_stride = head_ws_floats(T);
+    a.iws = head_iws;
+    a.iws_stride = head_iws_ints(T);
+    return a;
+  }
+  HeadOut head_out() const { return HeadOut{causal, kl, z, adj, boxes, counts, nmax, clip_flags}; }
+
+  DenseAct act(bool relu, int stream_id, double p, int64_t row0) const {
+    DenseAct a;
+    a.relu = relu ? 1 : 0;
+    if (training && stream_id > 0) {
+      a.drop = 1;
+      a.h1 = rng_h1(seed, (uint32_t)stream_id, step);
+      a.thr = drop_threshold(p);
+      a.dscale = 1.0f / (float)(1.0 - p);
+      a.row0 = row0;
+    }
+    return a;
+  }
+
+  int forward(const float* x, hipStream_t st) {
+    const CadLayout& LY = layout();
+    for (int l = 0; l < 8; ++l) VAD_TRY(conv3_prep_weights(P(LY.conv_w[l]), L[l], wf[l], wd[l], st));
+    int np = 0;
+    VAD_TRY(conv1_fwd(x, NF, H, W, P(LY.conv1_w), P(LY.conv1_b), y1, H1, W1, parts, &np, st));
+    VAD_TRY(bn_finalize(parts, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), RM(0), RV(0), 0.1f, 1e-5f,
+                        training, stats[0], st));
+    VAD_TRY(maxpool3s2_bnrelu(y1, stats[0], NF, H1, W1, 32, pool, HP, WP, st));
+    const float* src = pool;
+    const float* sst = nullptr;
+    for (int l = 0; l < 8; ++l) {
+      VAD_TRY(conv3_fwd(L[l], src, sst, wf[l], P(LY.conv_b[l]), y[l], parts, &np, st));
+      VAD_TRY(bn_finalize(parts, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]),
+                          RM(l + 1), RV(l + 1), 0.1f, 1e-5f, training, stats[l + 1], st));
+      src = y[l];
+      sst = stats[l + 1];
+    }
+    VAD_TRY(avgpool_fwd(y[7], stats[8], B, T, HF, WF, 256, feats, pooled, st));
+    // detector_net (cad:167-179)
+    const int64_t f0 = clip0 * T;
+    const int dd[6] = {6144, 512, 256, 128, 64, 20};
+    const float* in = feats;
+    for (int i = 0; i < 5; ++i) {
+      float* out = i < 4 ? dh[i] : dlog;
+      const int sid = i == 0 ? S_DET_DROP1 : (i == 1 ? S_DET_DROP2 : 0);
+      const double p = i == 0 ? 0.3 : 0.2;
+      VAD_TRY(dense_fwd(in, NF, dd[i], P(LY.det_w[i]), P(LY.det_b[i]), dd[i + 1], out, act(i < 4, sid, p, f0),
+                        dense_scratch, dense_scratch_floats, st));
+      in = out;
+    }
+    // direct_classifier on the mean over T (cad:525-538, 568-570)
+    const int gd[6] = {6144, 512, 256, 128, 64, 2};
+    in = pooled;
+    for (int i = 0; i < 5; ++i) {
+      float* out = i < 4 ? gh[i] : glog;
+      const int sid = i == 0 ? S_DIRECT_DROP1 : (i == 1 ? S_DIRECT_DROP2 : 0);
+      const double p = i == 0 ? 0.3 : 0.2;
+      VAD_TRY(dense_fwd(in, B, gd[i], P(LY.dir_w[i]), P(LY.dir_b[i]), gd[i + 1], out, act(i < 4, sid, p, clip0),
+                        dense_scratch, dense_scratch_floats, st));
+      in = out;
+    }
+    VAD_TRY(head_fwd(head_args(), dlog, head_out(), st));
+    TailArgs t = tail_args(nullptr, nullptr, nullptr, nullptr);
+    VAD_TRY(cad_tail_fwd(t, st));
+    if (training && nbt) {
+      hipLaunchKernelGGL(nbt_bump_kernel, dim3(1), dim3(64), 0, st, nbt, 9);
+      VAD_LAUNCH_CHECK();
+    }
+    return 0;
+  }
+
+  TailArgs tail_args(const float* dfin, const float* dprobs, const float* dcaus, const float* dkl) const {
+    TailArgs t{};
+    t.B = B;
+    t.direct_logits = glog;
+    t.causal = causal;
+    t.kl = kl;
+    t.clip_flags = clip_flags;
+    t.probs = probs;
+    t.final_scores = finalv;
+    t.flags = flags;
+    t.flags_f = grads ? grads + layout().param_floats : nullptr;
+    t.labels = labels;
+    t.losses = losses_ptr;
+    t.ext_d_final = dfin;
+    t.ext_d_probs = dprobs;
+    t.ext_d_causal = dcaus;
+    t.ext_d_kl = dkl;
+    t.d_causal = d_causal;
+    t.d_kl = d_kl;
+    t.d_direct_logits = d_glog;
+    return t;
+  }
+  float* losses_ptr = nullptr;
+
+  int backward(bool use_loss, const float* dfin, const float* dprobs, const float* dcaus, const float* dkl,
+               const float* dz, const float* dadj, hipStream_t st) {
+    const CadLayout& LY = layout();
+    VAD_CHECK(grads != nullptr, "backward: grads not bound");
+    VAD_CHECK(!use_loss || labels != nullptr, "backward(use_loss): forward ran without labels");
+    // grads of frozen / never-used slots stay zero
+    VAD_HIP(hipMemsetAsync(grads, 0, sizeof(float) * LY.param_floats, st));
+    TailArgs t = use_loss ? tail_args(nullptr, nullptr, nullptr, nullptr) : tail_args(dfin, dprobs, dcaus, dkl);
+    if (!use_loss) t.labels = nullptr;
+    VAD_TRY(cad_tail_bwd(t, st));
+    HeadUp up{d_causal, d_kl, dz, dadj};
+    VAD_TRY(head_bwd(head_args(), dlog, head_out(), up, slabs, slab_len, d_dlog, st));
+    VAD_TRY(head_slab_reduce(slabs, B, slab_len, grads + LY.slots[LY.head0].offset, st));
+    // direct classifier chain
+    const int gd[6] = {6144, 512, 256, 128, 64, 2};
+    const double gp[5] = {0.3, 0.2, 0.0, 0.0, 0.0};
+    const float* dcur = d_glog;
+    for (int i = 4; i >= 0; --i) {
+      const float* xin = i == 0 ? pooled : gh[i - 1];
+      VAD_TRY(dense_wgrad(dcur, B, gd[i + 1], xin, gd[i], G(LY.dir_w[i]), G(LY.dir_b[i]), dense_scratch,
+                          dense_scratch_floats, nullptr, st));
+      float* dnext = i == 0 ? d_pooled : dg[i - 1];
+      const float gs = (i >= 1 && training && gp[i - 1] > 0) ? (float)(1.0 / (1.0 - gp[i - 1])) : 1.f;
+      VAD_TRY(dense_dgrad(dcur, B, gd[i + 1], P(LY.dir_w[i]), gd[i], dnext, i == 0 ? nullptr : gh[i - 1], gs, nullptr,
+                          st));
+      dcur = dnext;
+    }
+    // detector chain (skipped on device when no box was in range: no grads reach it, cad:221-226)
+    VAD_HIP(hipMemsetAsync(d_feat_det, 0, sizeof(float) * (size_t)NF * 6144, st));
+    const int dd[6] = {6144, 512, 256, 128, 64, 20};
+    dcur = d_dlog;
+    for (int i = 4; i >= 0; --i) {
+      const float* xin = i == 0 ? feats : dh[i - 1];
+      VAD_TRY(dense_wgrad(dcur, NF, dd[i + 1], xin, dd[i], G(LY.det_w[i]), G(LY.det_b[i]), dense_scratch,
+                          dense_scratch_floats, flags, st));
+      float* dnext = i == 0 ? d_feat_det : ddh[i - 1];
+      const float gs = (i >= 1 && training && gp[i - 1] > 0) ? (float)(1.0 / (1.0 - gp[i - 1])) : 1.f;
+      VAD_TRY(dense_dgrad(dcur, NF, dd[i + 1], P(LY.det_w[i]), dd[i], dnext, i == 0 ? nullptr : dh[i - 1], gs, flags,
+                          st));
+      dcur = dnext;
+    }
+    // backbone
+    VAD_TRY(avgpool_bwd(d_feat_det, d_pooled, B, T, HF, WF, 256, dA, st));
+    for (int l = 7; l >= 0; --l) {
+      const int64_t M = (int64_t)NF * L[l].OH * L[l].OW;
+      const int C = L[l].Co;
+      int np = 0, nb = 0, ns = 0;
+      VAD_TRY(bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st));
+      VAD_TRY(bn_bwd_finalize(parts, np, C, (double)M, P(LY.bn_w[l]), stats[l + 1], G(LY.bn_w[l]), G(LY.bn_b[l]), st));
+      VAD_TRY(bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dY, bparts, &nb, st));
+      const float* src = l == 0 ? pool : y[l - 1];
+      const float* sst = l == 0 ? nullptr : stats[l];
+      VAD_TRY(conv3_wgrad(L[l], dY, src, sst, wpart, &ns, wpart_floats, st));
+      VAD_TRY(conv3_wgrad_reduce(L[l], wpart, ns, bparts, nb, G(LY.conv_w[l]), G(LY.conv_b[l]), st));
+      if (l > 0) VAD_TRY(conv3_dgrad(L[l], dY, wd[l], dA, st));
+    }
+    return 0;
+  }
+
+  int optimizer(float lr, float b1, float b2, float eps, float wd_, float max_norm, float gscale, float* tn,
+                hipStream_t st) {
+    const CadLayout& LY = layout();
+    VAD_CHECK(m && v && steps, "optimizer: state buffers not bound");
+    const int nb = 512;
+    hipLaunchKernelGGL(sqsum_kernel, dim3(nb), dim3(256), 0, st, grads, LY.param_floats, gscale, sq_parts);
+    VAD_LAUNCH_CHECK();
+    SlotTab tab{};
+    tab.nslots = (int)LY.slots.size();
+    VAD_CHECK(tab.nslots <= 160, "too many slots");
+    for (int i = 0; i < tab.nslots; ++i) {
+      tab.off[i] = LY.slots[i].offset;
+      tab.group[i] = LY.slots[i].group;
+    }
+    hipLaunchKernelGGL(opt_prepare_kernel, dim3(1), dim3(256), 0, st, sq_parts, nb, grads + LY.param_floats, tab,
+                       steps, b1, b2, max_norm, slot_info, clip, tn);
+    VAD_LAUNCH_CHECK();
+    const int64_t nchunks = LY.param_floats / 256;
+    hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)std::min<int64_t>(nchunks, 4096)), dim3(256), 0, st, params,
+                       grads, m, v, chunk_slot, nchunks, slot_info, clip, gscale, lr, b1, b2, eps, wd_);
+    VAD_LAUNCH_CHECK();
+    return 0;
+  }
+};
+
+}  // namespace vad
+
+struct vad_cad_plan {
+  vad::CadPlanImpl impl;
+  std::vector<int16_t> chunk_host;
+  bool chunk_uploaded = false;
+};
+
+using namespace vad;
+
+extern "C" {
+
+int vad_abi_version(void) { return VAD_ABI_VERSION; }
+const char* vad_last_error(void) { return vad::last_error(); }
+
+int vad_rng_u24(uint64_t seed, uint32_t stream_id, uint64_t step, int64_t row0, int64_t nrows, int64_t ncols,
+                uint32_t* out, void* stream) {
+  const int64_t total = nrows * ncols;
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(rng_u24_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 4096)), dim3(256), 0,
+                     (hipStream_t)stream, rng_h1(seed, stream_id, step), row0, nrows, ncols, out);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int vad_synth_frames(uint64_t seed, uint64_t step, int64_t frame0, int64_t nframes, int64_t npix, int mode,
+                     float* out, void* stream) {
+  const int64_t total = nframes * npix;
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(synth_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 8192)), dim3(256), 0,
+                     (hipStream_t)stream, rng_h1(seed, S_INPUT, step), frame0, nframes, npix, mode, out);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int vad_cad_num_slots(void) { return (int)layout().slots.size(); }
+const char* vad_cad_slot_name(int i) {
+  return (i >= 0 && i < vad_cad_num_slots()) ? layout().slots[i].name.c_str() : nullptr;
+}
+int64_t vad_cad_slot_numel(int i) { return (i >= 0 && i < vad_cad_num_slots()) ? layout().slots[i].numel : -1; }
+int64_t vad_cad_slot_offset(int i) { return (i >= 0 && i < vad_cad_num_slots()) ? layout().slots[i].offset : -1; }
+int vad_cad_slot_group(int i) { return (i >= 0 && i < vad_cad_num_slots()) ? layout().slots[i].group : -1; }
+int64_t vad_cad_param_floats(void) { return layout().param_floats; }
+int vad_cad_num_bufs(void) { return (int)layout().bufs.size(); }
+const char* vad_cad_buf_name(int i) {
+  return (i >= 0 && i < vad_cad_num_bufs()) ? layout().bufs[i].name.c_str() : nullptr;
+}
+int64_t vad_cad_buf_numel(int i) { return (i >= 0 && i < vad_cad_num_bufs()) ? layout().bufs[i].numel : -1; }
+int64_t vad_cad_buf_offset(int i) { return (i >= 0 && i < vad_cad_num_bufs()) ? layout().bufs[i].offset : -1; }
+int64_t vad_cad_buf_floats(void) { return layout().buf_floats; }
+int vad_cad_num_bn(void) { return 9; }
+
+int vad_cad_create(int B, int T, int H, int W, vad_cad_plan** out) {
+  VAD_CHECK(out != nullptr, "vad_cad_create: out is null");
+  VAD_CHECK(B >= 1 && T >= 1 && T <= 256 && H >= 16 && W >= 16, "vad_cad_create: unsupported shape");
+  auto* p = new vad_cad_plan();
+  CadPlanImpl& c = p->impl;
+  c.B = B; c.T = T; c.H = H; c.W = W; c.NF = B * T;
+  c.H1 = (H - 1) / 2 + 1; c.W1 = (W - 1) / 2 + 1;
+  c.HP = (c.H1 - 1) / 2 + 1; c.WP = (c.W1 - 1) / 2 + 1;
+  const int cin[8] = {32, 32, 32, 64, 64, 128, 128, 256};
+  const int cout[8] = {32, 32, 64, 64, 128, 128, 256, 256};
+  const int strd[8] = {1, 1, 2, 1, 2, 1, 2, 1};
+  int h = c.HP, w = c.WP;
+  for (int l = 0; l < 8; ++l) {
+    const int oh = (h - 1) / strd[l] + 1, ow = (w - 1) / strd[l] + 1;
+    c.L[l] = Conv3Layer{c.NF, cin[l], cout[l], h, w, oh, ow, strd[l]};
+    h = oh;
+    w = ow;
+  }
+  c.HF = h; c.WF = w;
+  Ws ws;
+  c.carve(ws);
+  c.ws_bytes = ws.off + 256;
+  const CadLayout& LY = layout();
+  p->chunk_host.assign(LY.param_floats / 256 + 1, (int16_t)-1);
+  for (int i = 0; i < (int)LY.slots.size(); ++i) {
+    const auto& s = LY.slots[i];
+    for (int64_t q = s.offset / 256; q < cdiv(s.offset + s.numel, 256); ++q) p->chunk_host[q] = (int16_t)i;
+  }
+  *out = p;
+  return 0;
+}
+
+void vad_cad_destroy(vad_cad_plan* plan) { delete plan; }
+
+int64_t vad_cad_workspace_bytes(const vad_cad_plan* plan) { return plan ? plan->impl.ws_bytes : -1; }
+
+int vad_cad_bind(vad_cad_plan* plan, void* workspace, float* params, float* grads, float* bufs, int64_t* nbt,
+                 float* exp_avg, float* exp_avg_sq, int32_t* steps) {
+  VAD_CHECK(plan && workspace && params && bufs, "vad_cad_bind: null argument");
+  VAD_CHECK((reinterpret_cast<uintptr_t>(workspace) & 255) == 0, "vad_cad_bind: workspace must be 256-B aligned");
+  CadPlanImpl& c = plan->impl;
+  Ws ws;
+  ws.base = reinterpret_cast<char*>(workspace);
+  ws.dry = false;
+  c.carve(ws);
+  c.params = params; c.grads = grads; c.bufs = bufs; c.nbt = nbt;
+  c.m = exp_avg; c.v = exp_avg_sq; c.steps = steps;
+  VAD_HIP(hipMemcpy(c.chunk_slot, plan->chunk_host.data(), plan->chunk_host.size() * sizeof(int16_t),
+                    hipMemcpyHostToDevice));
+  return 0;
+}
+
+int vad_cad_forward(vad_cad_plan* plan, const float* x, int training, uint64_t seed, uint64_t step, int64_t clip0,
+                    const int64_t* labels, float* final_scores, float* probs, float* causal, float* kl, float* z,
+                    float* adj, int32_t* nmax, float* boxes, int32_t* counts, float* losses, int32_t* flags,
+                    void* stream) {
+  VAD_CHECK(plan && x, "vad_cad_forward: null argument");
+  CadPlanImpl& c = plan->impl;
+  VAD_CHECK(c.params != nullptr, "vad_cad_forward: plan not bound");
+  hipStream_t st = (hipStream_t)stream;
+  c.training = training;
+  c.seed = seed;
+  c.step = step;
+  c.clip0 = clip0;
+  c.labels = labels;
+  c.losses_ptr = losses ? losses : c.sq_parts;  // scratch when not requested
+  VAD_TRY(c.forward(x, st));
+  auto cp = [&](void* dst, const void* src, size_t bytes) -> int {
+    if (dst) VAD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
+    return 0;
+  };
+  const int B = c.B, NF = c.NF;
+  VAD_TRY(cp(final_scores, c.finalv, B * 4));
+  VAD_TRY(cp(probs, c.probs, B * 8));
+  VAD_TRY(cp(causal, c.causal, B * 4));
+  VAD_TRY(cp(kl, c.kl, B * 4));
+  VAD_TRY(cp(z, c.z, B * 30 * 4));
+  VAD_TRY(cp(adj, c.adj, B * 36 * 4));
+  VAD_TRY(cp(nmax, c.nmax, B * 4));
+  VAD_TRY(cp(boxes, c.boxes, (size_t)NF * 80));
+  VAD_TRY(cp(counts, c.counts, (size_t)NF * 4));
+  VAD_TRY(cp(flags, c.flags, 8));
+  return 0;
+}
+
+int vad_cad_backward(vad_cad_plan* plan, int use_loss, const float* d_final, const float* d_probs,
+                     const float* d_causal, const float* d_kl, const float* d_z, const float* d_adj, void* stream) {
+  VAD_CHECK(plan != nullptr, "vad_cad_backward: null plan");
+  return plan->impl.backward(use_loss != 0, d_final, d_probs, d_causal, d_kl, d_z, d_adj, (hipStream_t)stream);
+}
+
+int vad_cad_optimizer_step(vad_cad_plan* plan, float lr, float beta1, float beta2, float eps, float weight_decay,
+                           float max_norm, float grad_scale, float* total_norm, void* stream) {
+  VAD_CHECK(plan != nullptr, "vad_cad_optimizer_step: null plan");
+  return plan->impl.optimizer(lr, beta1, beta2, eps, weight_decay, max_norm, grad_scale, total_norm,
+                              (hipStream_t)stream);
+}
+
+}  // extern "C"

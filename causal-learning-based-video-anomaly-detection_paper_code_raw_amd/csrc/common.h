@@ -1,0 +1,106 @@
+// Shared device/host helpers for libvadhip (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace vad {
+
+// ---------------------------------------------------------------- errors
+void set_error(const std::string& msg);
+const char* last_error();
+
+#define VAD_HIP(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess) {                                                               \
+      ::vad::set_error(std::string(#expr) + ": " + hipGetErrorString(_e) + " @" __FILE__ \
+                       ":" + std::to_string(__LINE__));                                   \
+      return 2;                                                                           \
+    }                                                                                     \
+  } while (0)
+
+#define VAD_CHECK(cond, msg)                 \
+  do {                                       \
+    if (!(cond)) {                           \
+      ::vad::set_error(std::string(msg));    \
+      return 1;                              \
+    }                                        \
+  } while (0)
+
+#define VAD_LAUNCH_CHECK() VAD_HIP(hipGetLastError())
+
+#define VAD_TRY(expr)        \
+  do {                       \
+    int _rc = (expr);        \
+    if (_rc != 0) return _rc; \
+  } while (0)
+
+static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------- RNG
+// Keyed counter hash; bit-exact twin of oracle/rng.py (see its docstring for the contract).
+enum RngStream : uint32_t {
+  S_INPUT = 1,
+  S_DET_DROP1 = 2,
+  S_DET_DROP2 = 3,
+  S_EPS = 4,
+  S_SCORER_DROP = 5,
+  S_DIRECT_DROP1 = 6,
+  S_DIRECT_DROP2 = 7,
+  S_MC_DROP1 = 8,
+  S_MC_DROP2 = 9,
+  S_A2_DROP_FC = 10,
+  S_A2_DROP_GRAPH = 11,
+  S_A2_PSEUDO = 12,
+  S_BBOX_DROP = 13,
+};
+
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// h1 depends only on (seed, stream, step): computed on the host once per launch.
+__host__ __device__ inline uint64_t rng_h1(uint64_t seed, uint32_t stream, uint64_t step) {
+  uint64_t h0 = mix64(seed + 0x9E3779B97F4A7C15ull * (uint64_t)(stream + 1));
+  return mix64(h0 ^ step);
+}
+
+__host__ __device__ inline uint64_t rng_hash(uint64_t h1, uint64_t row, uint64_t col) {
+  return mix64(h1 ^ ((row << 32) | col));
+}
+
+__host__ __device__ inline uint32_t rng_u24(uint64_t h1, uint64_t row, uint64_t col) {
+  return (uint32_t)(rng_hash(h1, row, col) >> 40);
+}
+
+// dropout: keep iff u24 >= thr, thr = floor(p * 2^24)
+static inline uint32_t drop_threshold(double p) { return (uint32_t)(p * 16777216.0); }
+
+__device__ inline float rng_normal(uint64_t h1, uint64_t row, uint64_t idx) {
+  double u1 = ((double)rng_u24(h1, row, 2 * idx) + 1.0) / 16777216.0;
+  double u2 = (double)rng_u24(h1, row, 2 * idx + 1) / 16777216.0;
+  return (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+}
+
+// ---------------------------------------------------------------- device math
+__device__ inline float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// f32-in / f32-acc MFMA 32x32x2: lane l supplies A[l&31][l>>5], B[l>>5][l&31];
+// D row = (r&3) + 8*(r>>2) + 4*(l>>5), col = l&31.
+__device__ inline f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+}  // namespace vad

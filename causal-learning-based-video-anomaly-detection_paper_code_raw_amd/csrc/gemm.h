@@ -1,0 +1,352 @@
+// Generic f32 MFMA GEMM for gfx950:  C[m][n] = sum_k A(m,k) * B(n,k)   (exact f32, v_mfma_f32_32x32x2_f32)
+//
+// Block = 256 threads = 4 waves arranged WM x WN; each wave owns TM x TN 32x32 accumulator tiles.
+// K is walked in BK=32 slices, register-prefetched one slice ahead into a double-buffered LDS tile.
+//
+// Every operand comes from a Loader policy that fills one of two LDS images:
+//   * K-contiguous (KC): lds[row][k], rows padded to 36 floats.  A lane reads 4 consecutive k with one
+//     ds_read_b128 and feeds 4 MFMAs; the k order inside an 8-wide sub-step is permuted so that lane
+//     half h supplies k = 8*kk + 4*h + s at MFMA s (both operands use the same map, so the sum is exact).
+//     The +4 float pad makes the 16-lane ds_read_b128 groups conflict-free (slot = 9*row mod 16).
+//   * K-major (KM): lds[k][row] (row contiguous); a lane reads one float (ds_read_b32) per MFMA.
+// Loaders: dense row-major KC/KM matrices, the NHWC conv patch gather (implicit GEMM with a tap table and
+// optional BN+ReLU applied on load), and the K-major patch gather used by the conv weight gradient.
+#pragma once
+#include "common.h"
+
+namespace vad {
+
+constexpr int BK = 32;
+constexpr int KC_STRIDE = BK + 4;
+
+template <int WM_, int WN_, int TM_, int TN_>
+struct TileCfg {
+  static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_;
+  static constexpr int BM = WM * TM * 32;
+  static constexpr int BN = WN * TN * 32;
+  static_assert(WM * WN == 4, "block is 4 waves");
+};
+
+template <bool KC, int R>
+struct LdsSize {
+  static constexpr int floats = KC ? R * KC_STRIDE : BK * R;
+};
+
+// ------------------------------------------------------------------ fragment reads
+template <int R>
+__device__ inline void frag_kc(const float* __restrict__ lds, int row, int kbase, float (&v)[4]) {
+  const f32x4 t = *reinterpret_cast<const f32x4*>(lds + row * KC_STRIDE + kbase);
+  v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+}
+template <int R>
+__device__ inline void frag_km(const float* __restrict__ lds, int row, int kbase, float (&v)[4]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) v[s] = lds[(kbase + s) * R + row];
+}
+
+// ------------------------------------------------------------------ dense loaders
+// Row-major matrix X[rows][ld] read as operand rows=r, k=c (K-contiguous).
+template <int R>
+struct DenseKC {
+  static constexpr bool KC = true;
+  static constexpr int NL = R / 32;  // float4 per thread per tile
+  struct Params { const float* p; int64_t ld; int rows; int kdim; };
+  const float* base; int64_t ld; int rows, kdim; int r0, tid;
+  f32x4 reg[NL];
+  __device__ void init(const Params& P, int r0_, int tid_) {
+    base = P.p; ld = P.ld; rows = P.rows; kdim = P.kdim; r0 = r0_; tid = tid_;
+  }
+  __device__ void load(int k0) {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int row = tid / 8 + 32 * j, kq = tid % 8;
+      const int r = r0 + row, k = k0 + kq * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (r < rows && k < kdim) {
+        const float* src = base + (int64_t)r * ld + k;
+        if (k + 3 < kdim && ((ld & 3) == 0)) v = *reinterpret_cast<const f32x4*>(src);
+        else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (k + e < kdim) ? src[e] : 0.f;
+        }
+      }
+      reg[j] = v;
+    }
+  }
+  __device__ void store(float* lds) const {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int row = tid / 8 + 32 * j, kq = tid % 8;
+      *reinterpret_cast<f32x4*>(lds + row * KC_STRIDE + kq * 4) = reg[j];
+    }
+  }
+};
+
+// Row-major matrix X[kdim][ld] read as operand k=row of X, r=column of X (K-major).
+// Optional virtual "ones" column at r == ones_col (used to fold bias grads into weight-grad GEMMs).
+template <int R>
+struct DenseKM {
+  static constexpr bool KC = false;
+  static constexpr int NL = R / 32;
+  struct Params { const float* p; int64_t ld; int rows; int kdim; int ones_col; };
+  const float* base; int64_t ld; int rows, kdim, ones_col; int r0, tid;
+  f32x4 reg[NL];
+  __device__ void init(const Params& P, int r0_, int tid_) {
+    base = P.p; ld = P.ld; rows = P.rows; kdim = P.kdim; ones_col = P.ones_col; r0 = r0_; tid = tid_;
+  }
+  __device__ void load(int k0) {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int q = tid + 256 * j;
+      const int kr = q / (R / 4), rq = q % (R / 4);
+      const int k = k0 + kr, r = r0 + rq * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (k < kdim) {
+        const float* src = base + (int64_t)k * ld + r;
+        if (r + 3 < rows && ((ld & 3) == 0)) v = *reinterpret_cast<const f32x4*>(src);
+        else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (r + e < rows) ? src[e] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (r + e == ones_col) v[e] = 1.f;
+      }
+      reg[j] = v;
+    }
+  }
+  __device__ void store(float* lds) const {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int q = tid + 256 * j;
+      const int kr = q / (R / 4), rq = q % (R / 4);
+      *reinterpret_cast<f32x4*>(lds + kr * R + rq * 4) = reg[j];
+    }
+  }
+};
+
+// ------------------------------------------------------------------ conv gathers
+// Tap table: for tap t, src pixel = (a*sa + dh[t], b*sb + dw[t]) where (a,b) is the GEMM row's position in
+// its destination grid.  Covers forward conv (dh = kh - pad), stride-1 transposed conv (dh = pad - kh) and
+// each stride-2 parity class of the transposed conv.
+struct TapTable {
+  int ntaps;
+  int8_t dh[9], dw[9];
+};
+
+struct ConvGeom {
+  int imgs;          // frames
+  int GA, GB;        // destination grid (rows of the GEMM = imgs*GA*GB)
+  int sa, sb;        // src step per grid step
+  int SH, SW, C;     // src spatial dims / channels (C % 32 == 0)
+};
+
+// A operand of forward / data-grad conv: row m = (img, a, b), k = tap*C + c; value = act(src[img][sh][sw][c]).
+template <int R>
+struct ConvGatherKC {
+  static constexpr bool KC = true;
+  static constexpr int NL = R / 32;
+  struct Params {
+    const float* src; ConvGeom g; TapTable taps;
+    const float* scale; const float* shift;  // BN+ReLU applied on load when scale != nullptr
+  };
+  const Params* P;
+  int tid;
+  int64_t pix_base[NL];  // img*SH*SW
+  int ya[NL], xb[NL];    // a*sa, b*sb  (ya < 0 marks an out-of-range row)
+  f32x4 reg[NL];
+  __device__ void init(const Params& Pp, int r0, int tid_) {
+    P = &Pp; tid = tid_;
+    const int M = Pp.g.imgs * Pp.g.GA * Pp.g.GB;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int m = r0 + tid / 8 + 32 * j;
+      if (m < M) {
+        const int img = m / (Pp.g.GA * Pp.g.GB);
+        const int rem = m - img * Pp.g.GA * Pp.g.GB;
+        const int a = rem / Pp.g.GB, b = rem - a * Pp.g.GB;
+        pix_base[j] = (int64_t)img * Pp.g.SH * Pp.g.SW;
+        ya[j] = a * Pp.g.sa;
+        xb[j] = b * Pp.g.sb;
+      } else {
+        pix_base[j] = 0; ya[j] = -100000; xb[j] = 0;
+      }
+    }
+  }
+  __device__ void load(int k0) {
+    const int C = P->g.C;
+    const int tap = k0 / C;
+    const int c = k0 - tap * C + (tid % 8) * 4;
+    const int dh = P->taps.dh[tap], dw = P->taps.dw[tap];
+    f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+    const bool bn = P->scale != nullptr;
+    if (bn) {
+      sc = *reinterpret_cast<const f32x4*>(P->scale + c);
+      sh = *reinterpret_cast<const f32x4*>(P->shift + c);
+    }
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int y = ya[j] + dh, x = xb[j] + dw;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (y >= 0 && y < P->g.SH && x >= 0 && x < P->g.SW) {
+        v = *reinterpret_cast<const f32x4*>(P->src + ((pix_base[j] + (int64_t)y * P->g.SW + x) * C + c));
+        if (bn) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
+        }
+      }
+      reg[j] = v;
+    }
+  }
+  __device__ void store(float* lds) const {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int row = tid / 8 + 32 * j, kq = tid % 8;
+      *reinterpret_cast<f32x4*>(lds + row * KC_STRIDE + kq * 4) = reg[j];
+    }
+  }
+};
+
+// B operand of the conv weight gradient (K-major over output pixels):
+//   k = output pixel p = (img, oh, ow) of the forward conv, r = tap*C + c,
+//   value = act(src[img][oh*s - pad + kh][ow*s - pad + kw][c]).
+template <int R>
+struct ConvPatchKM {
+  static constexpr bool KC = false;
+  static constexpr int NL = R / 32;
+  struct Params {
+    const float* src; int imgs, OH, OW, stride, pad, SH, SW, C, KW, rows;  // rows = taps*C
+    const float* scale; const float* shift;
+  };
+  const Params* P;
+  int r0, tid;
+  f32x4 reg[NL];
+  __device__ void init(const Params& Pp, int r0_, int tid_) { P = &Pp; r0 = r0_; tid = tid_; }
+  __device__ void load(int k0) {
+    const int npix = P->imgs * P->OH * P->OW;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int q = tid + 256 * j;
+      const int kr = q / (R / 4), rq = q % (R / 4);
+      const int p = k0 + kr, r = r0 + rq * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (p < npix && r < P->rows) {
+        const int tap = r / P->C, c = r - tap * P->C;
+        const int kh = tap / P->KW, kw = tap - kh * P->KW;
+        const int img = p / (P->OH * P->OW);
+        const int rem = p - img * P->OH * P->OW;
+        const int oh = rem / P->OW, ow = rem - oh * P->OW;
+        const int y = oh * P->stride - P->pad + kh, x = ow * P->stride - P->pad + kw;
+        if (y >= 0 && y < P->SH && x >= 0 && x < P->SW) {
+          v = *reinterpret_cast<const f32x4*>(P->src + (((int64_t)img * P->SH + y) * P->SW + x) * P->C + c);
+          if (P->scale) {
+            const f32x4 sc = *reinterpret_cast<const f32x4*>(P->scale + c);
+            const f32x4 sh = *reinterpret_cast<const f32x4*>(P->shift + c);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
+          }
+        }
+      }
+      reg[j] = v;
+    }
+  }
+  __device__ void store(float* lds) const {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int q = tid + 256 * j;
+      const int kr = q / (R / 4), rq = q % (R / 4);
+      *reinterpret_cast<f32x4*>(lds + kr * R + rq * 4) = reg[j];
+    }
+  }
+};
+
+// ------------------------------------------------------------------ the kernel body
+// Epi::apply(params, acc, m0, n0, wm, wn, lane, lds_scratch) writes the block's results.
+template <class Cfg, class LA, class LB, class Epi>
+__global__ __launch_bounds__(256) void gemm_kernel(const typename LA::Params pa, const typename LB::Params pb,
+                                                   const typename Epi::Params pe, int M, int N, int K,
+                                                   int k_per_split, const int* skip_if_zero) {
+  constexpr int BM = Cfg::BM, BN = Cfg::BN, TM = Cfg::TM, TN = Cfg::TN, WN = Cfg::WN;
+  constexpr int A_FL = LdsSize<LA::KC, BM>::floats, B_FL = LdsSize<LB::KC, BN>::floats;
+  constexpr int STAGE = A_FL + B_FL;
+  constexpr int TOTAL = 2 * STAGE > Epi::SCRATCH ? 2 * STAGE : Epi::SCRATCH;
+  __shared__ __attribute__((aligned(16))) float lds[TOTAL];
+  if (skip_if_zero != nullptr && *skip_if_zero == 0) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kbeg = blockIdx.z * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+
+  LA la; la.init(pa, m0, tid);
+  LB lb; lb.init(pb, n0, tid);
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (kbeg < kend) {
+    la.load(kbeg);
+    lb.load(kbeg);
+    la.store(lds);
+    lb.store(lds + A_FL);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+      const bool more = k0 + BK < kend;
+      if (more) {
+        la.load(k0 + BK);
+        lb.load(k0 + BK);
+      }
+      const float* As = lds + buf * STAGE;
+      const float* Bs = As + A_FL;
+#pragma unroll
+      for (int kk = 0; kk < BK / 8; ++kk) {
+        const int kb = kk * 8 + 4 * (lane >> 5);
+        float a[TM][4], b[TN][4];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = (wm * TM + i) * 32 + (lane & 31);
+          if constexpr (LA::KC) frag_kc<BM>(As, row, kb, a[i]);
+          else frag_km<BM>(As, row, kb, a[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int row = (wn * TN + j) * 32 + (lane & 31);
+          if constexpr (LB::KC) frag_kc<BN>(Bs, row, kb, b[j]);
+          else frag_km<BN>(Bs, row, kb, b[j]);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(a[i][s], b[j][s], acc[i][j]);
+      }
+      if (more) {
+        float* Ad = lds + (buf ^ 1) * STAGE;
+        la.store(Ad);
+        lb.store(Ad + A_FL);
+      }
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+  Epi::template apply<Cfg>(pe, acc, m0, n0, wm, wn, lane, M, N, lds);
+}
+
+// accumulator element -> (row, col) inside the block tile
+template <class Cfg>
+__device__ inline int acc_row(int wm, int i, int r, int lane) {
+  return (wm * Cfg::TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+}
+template <class Cfg>
+__device__ inline int acc_col(int wn, int j, int lane) {
+  return (wn * Cfg::TN + j) * 32 + (lane & 31);
+}
+
+}  // namespace vad

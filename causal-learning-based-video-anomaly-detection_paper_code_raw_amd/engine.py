@@ -1,0 +1,184 @@
+"""CadEngine: owns the flat device buffers of one CausalAnomalyDetector and drives libvadhip.
+
+Layout (all on the model's HIP device):
+  * params : one fp32 buffer, every nn.Parameter of the model is a view into it (slot order = state_dict order,
+             offsets from the library, 256-float aligned) -> state_dict / load_state_dict keep working;
+  * grads  : same layout + a 256-float tail whose first two floats are the "has grad" flags of the detector and
+             the structure learner (summed by the data-parallel all-reduce together with the grads);
+  * bufs   : BatchNorm running_mean / running_var, also viewed by the module buffers;
+  * nbt    : the nine num_batches_tracked counters (int64);
+  * exp_avg / exp_avg_sq / steps : AdamW state, created on the first optimizer step.
+One plan (+ workspace) per input shape (B, T, H, W).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native as nat
+
+GROUP_FROZEN, GROUP_ALWAYS, GROUP_DET, GROUP_STRUCT, GROUP_NEVER = range(5)
+
+
+class _Plan:
+    def __init__(self, engine, B, T, H, W):
+        L = nat.lib()
+        h = ctypes.c_void_p()
+        nat.check(L.vad_cad_create(B, T, H, W, ctypes.byref(h)))
+        self.h = h
+        self.shape = (B, T, H, W)
+        nbytes = L.vad_cad_workspace_bytes(h)
+        self.ws = torch.empty(int(nbytes) + 256, dtype=torch.uint8, device=engine.device)
+        base = (self.ws.data_ptr() + 255) // 256 * 256
+        e = engine
+        nat.check(L.vad_cad_bind(h, base, e.params.data_ptr(), e.grads.data_ptr(), e.bufs.data_ptr(),
+                                 e.nbt.data_ptr(), nat.ptr(e.exp_avg), nat.ptr(e.exp_avg_sq), nat.ptr(e.steps)))
+
+    def rebind(self, engine):
+        e = engine
+        base = (self.ws.data_ptr() + 255) // 256 * 256
+        nat.check(nat.lib().vad_cad_bind(self.h, base, e.params.data_ptr(), e.grads.data_ptr(), e.bufs.data_ptr(),
+                                         e.nbt.data_ptr(), nat.ptr(e.exp_avg), nat.ptr(e.exp_avg_sq),
+                                         nat.ptr(e.steps)))
+
+    def __del__(self):
+        try:
+            if self.h:
+                nat.lib().vad_cad_destroy(self.h)
+        except Exception:
+            pass
+
+
+class CadEngine:
+    def __init__(self, model: torch.nn.Module):
+        L = nat.lib()
+        self.model = model
+        p0 = next(model.parameters())
+        nat.require_hip(p0)
+        self.device = p0.device
+        n = L.vad_cad_num_slots()
+        self.slot_names = [L.vad_cad_slot_name(i).decode() for i in range(n)]
+        self.slot_numel = [L.vad_cad_slot_numel(i) for i in range(n)]
+        self.slot_offset = [L.vad_cad_slot_offset(i) for i in range(n)]
+        self.slot_group = [L.vad_cad_slot_group(i) for i in range(n)]
+        self.param_floats = L.vad_cad_param_floats()
+        named = list(model.named_parameters())
+        if [k for k, _ in named] != self.slot_names:
+            raise RuntimeError("model parameters do not match the libvadhip slot table")
+        for (k, p), nel in zip(named, self.slot_numel):
+            if p.numel() != nel:
+                raise RuntimeError(f"parameter {k}: {p.numel()} elements, library expects {nel}")
+        dev = self.device
+        self.params = torch.zeros(self.param_floats, dtype=torch.float32, device=dev)
+        self.grads = torch.zeros(self.param_floats + 256, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for (k, p), off in zip(named, self.slot_offset):
+                view = self.params[off:off + p.numel()].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+        nb = L.vad_cad_num_bufs()
+        self.buf_names = [L.vad_cad_buf_name(i).decode() for i in range(nb)]
+        self.buf_offset = [L.vad_cad_buf_offset(i) for i in range(nb)]
+        self.bufs = torch.zeros(L.vad_cad_buf_floats(), dtype=torch.float32, device=dev)
+        named_bufs = dict(model.named_buffers())
+        with torch.no_grad():
+            for k, off in zip(self.buf_names, self.buf_offset):
+                b = named_bufs[k]
+                view = self.bufs[off:off + b.numel()].view_as(b)
+                view.copy_(b)
+                _set_buffer(model, k, view)
+        nbt_names = [k for k in named_bufs if k.endswith("num_batches_tracked")]
+        if len(nbt_names) != L.vad_cad_num_bn():
+            raise RuntimeError("unexpected number of BatchNorm layers")
+        self.nbt = torch.zeros(len(nbt_names), dtype=torch.int64, device=dev)
+        with torch.no_grad():
+            for i, k in enumerate(nbt_names):
+                self.nbt[i].copy_(named_bufs[k].reshape(()))
+                _set_buffer(model, k, self.nbt[i])
+        self.exp_avg = self.exp_avg_sq = self.steps = None
+        self.plans = {}
+        self.generation = 0
+        self._last = None
+
+    # ------------------------------------------------------------------ bookkeeping
+    def is_bound(self) -> bool:
+        p = next(self.model.parameters())
+        return p.data_ptr() == self.params.data_ptr() and p.device == self.device
+
+    def init_optimizer_state(self):
+        if self.exp_avg is None:
+            self.exp_avg = torch.zeros_like(self.params)
+            self.exp_avg_sq = torch.zeros_like(self.params)
+            self.steps = torch.zeros(len(self.slot_names), dtype=torch.int32, device=self.device)
+            for p in self.plans.values():
+                p.rebind(self)
+
+    def plan(self, B, T, H, W) -> _Plan:
+        key = (B, T, H, W)
+        if key not in self.plans:
+            self.plans[key] = _Plan(self, B, T, H, W)
+        return self.plans[key]
+
+    def grad_view(self, i):
+        off = self.slot_offset[i]
+        return self.grads[off:off + self.slot_numel[i]]
+
+    # ------------------------------------------------------------------ compute
+    def forward(self, x: torch.Tensor, training: bool, seed: int, step: int, clip0: int, labels=None):
+        nat.require_hip(x)
+        if x.dim() != 5:
+            raise ValueError(f"Expected 5D tensor (B,T,C,H,W), got {tuple(x.shape)}")
+        B, T, C, H, W = x.shape
+        if C != 1:
+            raise ValueError("ResNetBackbone here takes single-channel frames (input_channels=1, cad:515)")
+        x = x.contiguous().float()
+        pl = self.plan(B, T, H, W)
+        dev = self.device
+        o = dict(
+            final=torch.empty(B, device=dev), probs=torch.empty(B, 2, device=dev),
+            causal=torch.empty(B, device=dev), kl=torch.empty(B, device=dev),
+            z=torch.empty(B, 5, 6, device=dev), adj=torch.empty(B, 6, 6, device=dev),
+            nmax=torch.empty(B, dtype=torch.int32, device=dev), boxes=torch.empty(B, T, 5, 4, device=dev),
+            counts=torch.empty(B, T, dtype=torch.int32, device=dev), losses=torch.empty(5, device=dev),
+            flags=torch.empty(2, dtype=torch.int32, device=dev))
+        lab = None
+        if labels is not None:
+            lab = labels.to(device=dev, dtype=torch.int64).contiguous()
+        nat.check(nat.lib().vad_cad_forward(
+            pl.h, x.data_ptr(), 1 if training else 0, seed & ((1 << 64) - 1), step, clip0, nat.ptr(lab),
+            o["final"].data_ptr(), o["probs"].data_ptr(), o["causal"].data_ptr(), o["kl"].data_ptr(),
+            o["z"].data_ptr(), o["adj"].data_ptr(), o["nmax"].data_ptr(), o["boxes"].data_ptr(),
+            o["counts"].data_ptr(), o["losses"].data_ptr(), o["flags"].data_ptr(), nat.stream_of(dev)))
+        self.generation += 1
+        self._last = (pl, lab, x)
+        return o
+
+    def backward(self, use_loss: bool, d_final=None, d_probs=None, d_causal=None, d_kl=None, d_z=None, d_adj=None):
+        pl, lab, _ = self._last
+        c = [t.contiguous() if t is not None else None for t in (d_final, d_probs, d_causal, d_kl, d_z, d_adj)]
+        nat.check(nat.lib().vad_cad_backward(pl.h, 1 if use_loss else 0, *[nat.ptr(t) for t in c],
+                                             nat.stream_of(self.device)))
+
+    def optimizer_step(self, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, max_norm=1.0, grad_scale=1.0,
+                       total_norm=None):
+        self.init_optimizer_state()
+        pl = self._last[0]
+        nat.check(nat.lib().vad_cad_optimizer_step(pl.h, lr, betas[0], betas[1], eps, weight_decay, max_norm,
+                                                   grad_scale, nat.ptr(total_norm), nat.stream_of(self.device)))
+
+
+def _set_buffer(model, dotted, tensor):
+    mod = model
+    parts = dotted.split(".")
+    for p in parts[:-1]:
+        mod = getattr(mod, p)
+    mod._buffers[parts[-1]] = tensor
+
+
+def engine_for(model) -> CadEngine:
+    eng = model.__dict__.get("_vad_engine")
+    if eng is None or not eng.is_bound():
+        eng = CadEngine(model)
+        model.__dict__["_vad_engine"] = eng
+    return eng

@@ -1,0 +1,131 @@
+"""train_model / test_model / apply_memory_efficient_training of causal_anomaly_detection.py (cad:592-835),
+driving the fused libvadhip step: forward + loss + backward + clip_grad_norm_(1.0) + AdamW in HIP kernels,
+with an optional data-parallel gradient all-reduce (RCCL) between backward and the optimizer.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.distributed as dist
+
+from .cad import CausalAnomalyDetector  # noqa: F401  (re-export for callers of this module)
+
+
+def apply_memory_efficient_training(model):
+    """Freeze backbone.conv1 / backbone.bn1 (cad:592-607)."""
+    for name, param in model.named_parameters():
+        if "backbone.conv1" in name or "backbone.bn1" in name:
+            param.requires_grad = False
+    total = sum(p.numel() for p in model.parameters())
+    trainable = sum(p.numel() for p in model.parameters() if p.requires_grad)
+    print(f"Total parameters: {total:,}")
+    print(f"Trainable parameters: {trainable:,}")
+    print(f"Frozen parameters: {total - trainable:,}")
+    return model
+
+
+class CadTrainer:
+    """One fused train step per call; the building block of train_model and bench.py.
+
+    Data parallel: one process per GPU; rank r processes global clips [r*B, (r+1)*B) of each step (RNG keyed by
+    global clip index), grads (+ has-grad flags) are summed with one all_reduce and scaled by 1/world inside the
+    optimizer kernel; BN running stats follow rank 0 (broadcast before each forward, DDP's broadcast_buffers).
+    """
+
+    def __init__(self, model, lr=3e-4, weight_decay=1e-5, eps=1e-8, betas=(0.9, 0.999), max_norm=1.0, seed=0,
+                 process_group=None):
+        self.model = model
+        self.eng = model.engine()
+        self.lr, self.wd, self.eps, self.betas, self.max_norm = lr, weight_decay, eps, betas, max_norm
+        self.seed = seed
+        self.step_idx = 0
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank(process_group) if self.world > 1 else 0
+        self.eng.init_optimizer_state()
+        if self.world > 1:
+            dist.broadcast(self.eng.params, 0, group=process_group)
+
+    def step(self, videos, labels, lr=None):
+        """One training step; returns the (device) loss vector [cls, anomaly, causal, kl, total]."""
+        eng = self.eng
+        B = videos.shape[0]
+        if self.world > 1:
+            dist.broadcast(eng.bufs, 0, group=self.pg)
+        o = eng.forward(videos, True, self.seed, self.step_idx, self.rank * B, labels)
+        eng.backward(True)
+        if self.world > 1:
+            dist.all_reduce(eng.grads, group=self.pg)
+        eng.optimizer_step(self.lr if lr is None else lr, self.betas, self.eps, self.wd, self.max_norm,
+                           1.0 / self.world)
+        self.step_idx += 1
+        return o["losses"]
+
+
+def _cosine_lr(base, epoch, t_max):
+    return 0.5 * base * (1 + math.cos(math.pi * epoch / t_max))
+
+
+def _eval_losses(model, videos, labels):
+    eng = model.engine()
+    o = eng.forward(videos, False, 0, 0, 0, labels)
+    return o
+
+
+def train_model(model, train_loader, val_loader, num_epochs=20, lr=3e-4):
+    """Training loop with the multi-objective loss (cad:609-790).  Returns (model, train_losses, val_losses)."""
+    model = apply_memory_efficient_training(model)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    model.to(dev)
+    trainer = CadTrainer(model, lr=lr)
+    train_losses, val_losses = [], []
+    print("Starting training with mixed precision: False")
+    for epoch in range(num_epochs):
+        model.train()
+        cur_lr = _cosine_lr(lr, epoch, num_epochs)
+        tot, nb = 0.0, 0
+        for batch_idx, (videos, labels) in enumerate(train_loader):
+            try:
+                losses = trainer.step(videos.to(dev), labels.to(dev), lr=cur_lr)
+                l = losses.tolist()
+                tot += l[4]
+                nb += 1
+                if batch_idx % 5 == 0:
+                    print(f"Epoch {epoch+1}/{num_epochs}, Batch {batch_idx+1}, Total: {l[4]:.6f}, Class: {l[0]:.6f}")
+            except RuntimeError as e:
+                if "out of memory" in str(e):
+                    print(f"CUDA out of memory at batch {batch_idx}. Skipping batch...")
+                    torch.cuda.empty_cache()
+                    continue
+                raise
+        model.eval()
+        vtot, vb, correct, total = 0.0, 0, 0, 0
+        with torch.no_grad():
+            for videos, labels in val_loader:
+                videos, labels = videos.to(dev), labels.to(dev)
+                o = _eval_losses(model, videos, labels)
+                vtot += o["losses"][4].item()
+                vb += 1
+                correct += (o["probs"].argmax(1) == labels).sum().item()
+                total += labels.numel()
+        train_losses.append(tot / max(nb, 1))
+        val_losses.append(vtot / max(vb, 1))
+        print(f"Epoch {epoch+1}/{num_epochs}, Train Loss: {train_losses[-1]:.6f}, Val Loss: {val_losses[-1]:.6f}, "
+              f"Val Accuracy: {correct / max(total, 1):.4f}")
+    return model, train_losses, val_losses
+
+
+def test_model(model, test_loader):
+    """Scores every clip (cad:796-835); returns (scores, labels, outputs)."""
+    model.eval()
+    dev = next(model.parameters()).device
+    scores, labels_all, outs = [], [], []
+    with torch.no_grad():
+        for videos, labels in test_loader:
+            out = model(videos.to(dev))
+            scores.extend(out["anomaly_scores"].cpu().tolist())
+            labels_all.extend(labels.tolist())
+            outs.append(out)
+    import numpy as np
+    return np.array(scores), np.array(labels_all), outs

@@ -1,0 +1,89 @@
+/*
+ * libvadhip — C ABI of the MI355X (gfx950) hot path of
+ * pvvkishore/Causal-Learning-Based-Video-Anomaly-Detection_Paper_Code_Raw.
+ *
+ * The reference exposes no FFI: its boundary is the Python nn.Module surface
+ * (SURVEY.md §8b).  Every entry point below replaces one piece of that surface;
+ * the Python package binds them with ctypes.
+ *
+ * Conventions
+ *   - all pointers are DEVICE pointers unless stated; fp32 unless stated;
+ *   - `stream` is a hipStream_t passed as void*; every call only enqueues work;
+ *   - return 0 on success, non-zero on error; vad_last_error() has the text
+ *     (the Python layer raises RuntimeError, mirroring cad:702-709);
+ *   - the caller (PyTorch) owns every buffer, including the workspace.
+ */
+#ifndef VAD_H_
+#define VAD_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VAD_ABI_VERSION 1
+
+int vad_abi_version(void);
+const char* vad_last_error(void);
+
+/* ------------------------------------------------------------------------------------------
+ * RNG (bit-exact twin of oracle/rng.py).  Replaces the torch CPU generator draws of
+ * nn.Dropout and torch.randn_like in the reference (cad:170,173,330,438,528,531).
+ * ------------------------------------------------------------------------------------------ */
+/* uint32 u24 draws for rows row0.. and cols 0..ncols-1 (testing the contract) */
+int vad_rng_u24(uint64_t seed, uint32_t stream_id, uint64_t step, int64_t row0, int64_t nrows, int64_t ncols,
+                uint32_t* out, void* stream);
+/* synthetic clips: x = (u8 - 0.5) / 0.5, u8 = hash >> 56 (UCSDped2Dataset + Normalize(0.5,0.5), cad:92-96) */
+int vad_synth_frames(uint64_t seed, uint64_t step, int64_t frame0, int64_t nframes, int64_t npix, int mode,
+                     float* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * causal_anomaly_detection.py — CausalAnomalyDetector (cad:508-586) + train_model step (cad:609-690)
+ * ------------------------------------------------------------------------------------------ */
+typedef struct vad_cad_plan vad_cad_plan;
+
+/* flat parameter layout: slot i = i-th entry of model.named_parameters() (state_dict order) */
+int vad_cad_num_slots(void);
+const char* vad_cad_slot_name(int i);
+int64_t vad_cad_slot_numel(int i);
+int64_t vad_cad_slot_offset(int i);
+/* 0 frozen (cad:596-598), 1 always has grad, 2 detector (grad iff any in-range box), 3 structure learner
+ * (grad iff some clip has >=2 trajectories), 4 never has grad (structure_params) */
+int vad_cad_slot_group(int i);
+int64_t vad_cad_param_floats(void);   /* flat params size; the grad buffer has 256 extra floats (flags) */
+int vad_cad_num_bufs(void);           /* BatchNorm running_mean / running_var tensors, state_dict order */
+const char* vad_cad_buf_name(int i);
+int64_t vad_cad_buf_numel(int i);
+int64_t vad_cad_buf_offset(int i);
+int64_t vad_cad_buf_floats(void);
+int vad_cad_num_bn(void);             /* num_batches_tracked counters (int64 array) */
+
+int vad_cad_create(int B, int T, int H, int W, vad_cad_plan** out);
+void vad_cad_destroy(vad_cad_plan* plan);
+int64_t vad_cad_workspace_bytes(const vad_cad_plan* plan);
+/* bind caller-owned buffers. exp_avg/exp_avg_sq/steps may be NULL when no optimizer step is used. */
+int vad_cad_bind(vad_cad_plan* plan, void* workspace, float* params, float* grads, float* bufs, int64_t* nbt,
+                 float* exp_avg, float* exp_avg_sq, int32_t* steps);
+
+/* CausalAnomalyDetector.forward.  training=1: batch-stat BN + running-stat update + dropout.
+ * labels (int64 [B], may be NULL) additionally computes the train_model loss terms.
+ * outputs: final [B], probs [B,2], causal [B], kl [B], z [B,5,6], adj [B,6,6], nmax int32 [B],
+ *          boxes [B,T,5,4], counts int32 [B,T], losses [5] (cls, anomaly, causal, kl, total), flags int32 [2] */
+int vad_cad_forward(vad_cad_plan* plan, const float* x, int training, uint64_t seed, uint64_t step, int64_t clip0,
+                    const int64_t* labels, float* final_scores, float* probs, float* causal, float* kl, float* z,
+                    float* adj, int32_t* nmax, float* boxes, int32_t* counts, float* losses, int32_t* flags,
+                    void* stream);
+/* backward of the last forward.  use_loss=1: upstream grads of the train_model loss (needs labels in forward);
+ * otherwise the given upstream grads (any may be NULL = zero).  Writes the flat grad buffer (all slots). */
+int vad_cad_backward(vad_cad_plan* plan, int use_loss, const float* d_final, const float* d_probs,
+                     const float* d_causal, const float* d_kl, const float* d_z, const float* d_adj, void* stream);
+/* clip_grad_norm_(max_norm) + AdamW over the flat buffers (torch.optim.AdamW semantics, per-slot steps,
+ * slots without a grad this step are skipped).  grad_scale multiplies grads first (1/world for DP).
+ * total_norm (device float [1], may be NULL) receives the pre-clip norm. */
+int vad_cad_optimizer_step(vad_cad_plan* plan, float lr, float beta1, float beta2, float eps, float weight_decay,
+                           float max_norm, float grad_scale, float* total_norm, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VAD_H_ */

@@ -1,0 +1,36 @@
+"""Golden-vector case table shared by make_golden.py and the tests (data only, no reference code)."""
+from __future__ import annotations
+
+import torch
+
+# "forced" detector setting: the reference init (cad:186-192) puts every box out of range so every
+# frame falls back to the constant box.  Forcing re-biases the last detector layer to
+# logits near the x/y validity thresholds and scales its weights, so that frames carry 1..5 valid
+# boxes and the detector / edge-MLP gradients are exercised.
+FORCED_A = dict(
+    bias=[-3.45, 0.0, 0.0, 0.0,     # det0: x near the low threshold (logit(10/360) = -3.56)
+          0.0, 0.0, 0.0, 0.0,       # det1: always valid
+          3.3, 0.3, 0.0, 0.0,       # det2: x near the high threshold
+          0.5, -2.9, 0.0, 0.0,      # det3: y near the low threshold (logit(10/240) = -3.14)
+          -3.58, 2.9, 0.0, 0.0],     # det4: both near thresholds
+    weight_scale=6.0,
+)
+
+
+def force_detector(sd: dict, forced: dict) -> None:
+    """Apply a forced-detection setting in place to a CausalAnomalyDetector state_dict."""
+    with torch.no_grad():
+        sd["detector.detector_net.10.bias"].copy_(torch.tensor(forced["bias"], dtype=torch.float32))
+        sd["detector.detector_net.10.weight"].mul_(forced["weight_scale"])
+
+
+CAD_CASES = [
+    dict(name="fallback_b2t4_64", B=2, T=4, H=64, W=64, seed=0, step=0, forced=None),
+    dict(name="forced_b2t4_64", B=2, T=4, H=64, W=64, seed=1, step=0, forced=FORCED_A),
+    dict(name="forced_b3t5_96x80", B=3, T=5, H=96, W=80, seed=2, step=3, forced=FORCED_A),
+    dict(name="fallback_b2t16_227", B=2, T=16, H=227, W=227, seed=3, step=0, forced=None),
+]
+
+MC_CASES = []
+A2_CASES = []
+BBOX_CASES = []
