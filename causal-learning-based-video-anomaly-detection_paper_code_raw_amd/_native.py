@@ -41,6 +41,13 @@ _SIGS = {
     "vad_cad_forward": (_I, [_P, _P, _I, _U64, _U64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vad_cad_backward": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "vad_cad_optimizer_step": (_I, [_P, _F, _F, _F, _F, _F, _F, _F, _P, _P]),
+    "vad_dense_forward": (_I, [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I64, _P]),
+    "vad_conv3x3_forward": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
+    "vad_conv3x3_dgrad": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, _P]),
+    "vad_cad_debug_buffer": (_I, [_P, ctypes.c_char_p, _I, ctypes.POINTER(_P), ctypes.POINTER(_I64)]),
+    "vad_cad_set_debug": (_I, [_P, ctypes.c_char_p, _I64]),
+    "vad_debug_d2h": (_I, [_P, _P, _I64]),
+    "vad_conv3x3_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I64, _P]),
 }
 
 

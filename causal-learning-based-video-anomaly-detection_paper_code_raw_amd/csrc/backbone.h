@@ -20,7 +20,7 @@ int bn_finalize(const float* partials, int P, int C, double count, const float* 
 int bn_bwd_reduce(const float* dA, const float* y, const float* stats, int M, int C, float* partials, int* nparts,
                   hipStream_t st);
 int bn_bwd_finalize(const float* partials, int P, int C, double count, const float* gamma, float* stats,
-                    float* dgamma, float* dbeta, hipStream_t st);
+                    float* dgamma, float* dbeta, int training, hipStream_t st);
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
                  int* nparts, hipStream_t st);
 int bn_rows_parts(int M, int C);

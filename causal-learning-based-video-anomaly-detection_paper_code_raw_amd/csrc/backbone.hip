@@ -228,7 +228,7 @@ int bn_bwd_reduce(const float* dA, const float* y, const float* stats, int M, in
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ partials, int P, int C,
                                                               double count, const float* __restrict__ gamma,
                                                               float* __restrict__ stats, float* dgamma,
-                                                              float* dbeta) {
+                                                              float* dbeta, int training) {
   const int c = blockIdx.x;
   __shared__ double red[2][256];
   double a = 0.0, b = 0.0;
@@ -251,15 +251,16 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
     if (dgamma) dgamma[c] = (float)sdzx;
     if (dbeta) dbeta[c] = (float)sdz;
     stats[4 * C + c] = gamma[c] * stats[C + c];
-    stats[5 * C + c] = (float)(sdz / count);
-    stats[6 * C + c] = (float)(sdzx / count);
+    // eval mode: BN is the affine map of the running stats, no batch-mean terms in its backward
+    stats[5 * C + c] = training ? (float)(sdz / count) : 0.f;
+    stats[6 * C + c] = training ? (float)(sdzx / count) : 0.f;
   }
 }
 
 int bn_bwd_finalize(const float* partials, int P, int C, double count, const float* gamma, float* stats,
-                    float* dgamma, float* dbeta, hipStream_t st) {
+                    float* dgamma, float* dbeta, int training, hipStream_t st) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partials, P, C, count, gamma, stats, dgamma,
-                     dbeta);
+                     dbeta, training);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -822,7 +823,7 @@ __global__ __launch_bounds__(256) void conv3_wgrad_reduce_kernel(const float* __
     for (int z = 0; z < S; ++z) s += part[(int64_t)z * Co * ldp + src];
     dW[i] = s;
   }
-  if (blockIdx.x == 0) {
+  if (blockIdx.x == 0 && db != nullptr) {
     for (int co = threadIdx.x; co < Co; co += 256) {
       float s = 0.f;
       for (int p = 0; p < NB; ++p) s += bparts[(int64_t)p * 2 * Co + co];

@@ -276,6 +276,7 @@ struct CadPlanImpl {
   int16_t* chunk_slot;
   int64_t parts_floats, dense_scratch_floats, wpart_floats, slab_len, act_max;
   int64_t clip0 = 0;
+  int debug_stop_layer = -1;  // backward returns after this backbone layer (debug introspection)
   int training = 1;
   bool have_labels = false;
   uint64_t seed = 0, step = 0;
@@ -510,13 +511,15 @@ struct CadPlanImpl {
       const int C = L[l].Co;
       int np = 0, nb = 0, ns = 0;
       VAD_TRY(bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st));
-      VAD_TRY(bn_bwd_finalize(parts, np, C, (double)M, P(LY.bn_w[l]), stats[l + 1], G(LY.bn_w[l]), G(LY.bn_b[l]), st));
+      VAD_TRY(bn_bwd_finalize(parts, np, C, (double)M, P(LY.bn_w[l]), stats[l + 1], G(LY.bn_w[l]), G(LY.bn_b[l]),
+                                training, st));
       VAD_TRY(bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dY, bparts, &nb, st));
       const float* src = l == 0 ? pool : y[l - 1];
       const float* sst = l == 0 ? nullptr : stats[l];
       VAD_TRY(conv3_wgrad(L[l], dY, src, sst, wpart, &ns, wpart_floats, st));
       VAD_TRY(conv3_wgrad_reduce(L[l], wpart, ns, bparts, nb, G(LY.conv_w[l]), G(LY.conv_b[l]), st));
       if (l > 0) VAD_TRY(conv3_dgrad(L[l], dY, wd[l], dA, st));
+      if (l == debug_stop_layer) return 0;
     }
     return 0;
   }
@@ -694,6 +697,41 @@ int vad_cad_optimizer_step(vad_cad_plan* plan, float lr, float beta1, float beta
   VAD_CHECK(plan != nullptr, "vad_cad_optimizer_step: null plan");
   return plan->impl.optimizer(lr, beta1, beta2, eps, weight_decay, max_norm, grad_scale, total_norm,
                               (hipStream_t)stream);
+}
+
+int vad_cad_debug_buffer(vad_cad_plan* plan, const char* name, int idx, void** ptr, int64_t* nfloats) {
+  VAD_CHECK(plan && name && ptr && nfloats, "vad_cad_debug_buffer: null argument");
+  CadPlanImpl& c = plan->impl;
+  const std::string n(name);
+  const int64_t NF = c.NF;
+  auto act = [&](int l) { return NF * c.L[l].OH * c.L[l].OW * c.L[l].Co; };
+  const int cs[9] = {32, 32, 32, 64, 64, 128, 128, 256, 256};
+  if (n == "y1") { *ptr = c.y1; *nfloats = NF * c.H1 * c.W1 * 32; }
+  else if (n == "pool") { *ptr = c.pool; *nfloats = NF * c.HP * c.WP * 32; }
+  else if (n == "y" && idx >= 0 && idx < 8) { *ptr = c.y[idx]; *nfloats = act(idx); }
+  else if (n == "stats" && idx >= 0 && idx < 9) { *ptr = c.stats[idx]; *nfloats = 7 * cs[idx]; }
+  else if (n == "feats") { *ptr = c.feats; *nfloats = NF * 6144; }
+  else if (n == "pooled") { *ptr = c.pooled; *nfloats = (int64_t)c.B * 6144; }
+  else if (n == "dA") { *ptr = c.dA; *nfloats = c.act_max; }
+  else if (n == "dY") { *ptr = c.dY; *nfloats = c.act_max; }
+  else if (n == "d_pooled") { *ptr = c.d_pooled; *nfloats = (int64_t)c.B * 6144; }
+  else if (n == "d_feat_det") { *ptr = c.d_feat_det; *nfloats = NF * 6144; }
+  else if (n == "det_logits") { *ptr = c.dlog; *nfloats = NF * 20; }
+  else { vad::set_error("vad_cad_debug_buffer: unknown buffer " + n); return 1; }
+  return 0;
+}
+
+int vad_cad_set_debug(vad_cad_plan* plan, const char* key, int64_t value) {
+  VAD_CHECK(plan && key, "vad_cad_set_debug: null argument");
+  if (std::string(key) == "stop_layer") plan->impl.debug_stop_layer = (int)value;
+  else { vad::set_error("vad_cad_set_debug: unknown key"); return 1; }
+  return 0;
+}
+
+int vad_debug_d2h(void* host, const void* dev, int64_t bytes) {
+  VAD_HIP(hipDeviceSynchronize());
+  VAD_HIP(hipMemcpy(host, dev, (size_t)bytes, hipMemcpyDeviceToHost));
+  return 0;
 }
 
 }  // extern "C"

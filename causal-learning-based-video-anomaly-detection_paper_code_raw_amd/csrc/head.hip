@@ -524,7 +524,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a, const float* 
         const float hp = w[L.hp + row * GH + u], ghn = w[L.ghn + row * GH + u];
         const float d = dh[idx];
         const float dn = d * (1.f - z);
-        const float dzg = d * (nv - hp);
+        const float dzg = d * (hp - nv);  // dh'/dz = h - n
         const float dan = dn * (1.f - nv * nv);
         const float dr = dan * ghn;
         const float daz = dzg * z * (1.f - z);

@@ -83,6 +83,32 @@ int vad_cad_backward(vad_cad_plan* plan, int use_loss, const float* d_final, con
 int vad_cad_optimizer_step(vad_cad_plan* plan, float lr, float beta1, float beta2, float eps, float weight_decay,
                            float max_norm, float grad_scale, float* total_norm, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Single building blocks (kernel unit tests; same kernels as the fused step)
+ * ------------------------------------------------------------------------------------------ */
+/* Y[M,N] = act(X[M,K] W[N,K]^T + b)  (nn.Linear + optional ReLU) */
+int vad_dense_forward(const float* X, int M, int K, const float* W, const float* b, int N, float* Y, int relu,
+                      float* scratch, int64_t scratch_floats, void* stream);
+/* nn.Conv2d(Ci, Co, 3, stride, padding=1) on NHWC activations; W in torch layout [Co][Ci][3][3].
+ * scratch: wf/wd 9*Ci*Co floats each, partials >= ceil(M/64)*2*Co floats (M = NF*OH*OW). */
+int vad_conv3x3_forward(const float* x_nhwc, int NF, int Ci, int IH, int IW, const float* w, const float* bias,
+                        int Co, int stride, float* y_nhwc, float* wf_scratch, float* wd_scratch, float* partials,
+                        void* stream);
+/* input gradient of the same conv (transposed conv; stride-2 split into four parity classes) */
+int vad_conv3x3_dgrad(const float* dy_nhwc, int NF, int Ci, int IH, int IW, const float* w, int Co, int stride,
+                      float* dx_nhwc, float* wf_scratch, float* wd_scratch, void* stream);
+/* weight gradient of the same conv: dW[Co][Ci][3][3] = sum over pixels dY x patches(x); split-K slabs in partial */
+int vad_conv3x3_wgrad(const float* x_nhwc, const float* dy_nhwc, int NF, int Ci, int IH, int IW, int Co, int stride,
+                      float* dW, float* partial, int64_t partial_floats, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Debug introspection (tests only): internal plan buffers, partial backward, device->host copy
+ * names: y1, pool, y[0..7], stats[0..8], feats, pooled, dA, dY, d_pooled, d_feat_det, det_logits
+ * ------------------------------------------------------------------------------------------ */
+int vad_cad_debug_buffer(vad_cad_plan* plan, const char* name, int idx, void** ptr, int64_t* nfloats);
+int vad_cad_set_debug(vad_cad_plan* plan, const char* key, int64_t value);  /* "stop_layer" */
+int vad_debug_d2h(void* host, const void* dev, int64_t bytes);
+
 #ifdef __cplusplus
 }
 #endif

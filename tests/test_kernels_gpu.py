@@ -1,0 +1,120 @@
+"""Single-kernel parity on the GPU: MFMA dense layer, implicit-GEMM 3x3 conv forward / transposed conv,
+and the device RNG — each against a plain fp32 reference of the same op (torch CPU / numpy)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import rng
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from vad_amd import _native
+    return _native
+
+
+@pytest.mark.parametrize("M,K,N,relu", [(128, 6144, 512, 1), (8, 6144, 512, 1), (37, 64, 20, 0), (5, 64, 2, 0),
+                                        (256, 96, 130, 1)])
+def test_dense_forward(M, K, N, relu):
+    nat = _lib()
+    g = torch.Generator().manual_seed(M * 1000 + N)
+    X = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    ref = X @ W.T + b
+    if relu:
+        ref = ref.clamp_min(0)
+    d = torch.device("cuda")
+    Y = torch.empty(M, N, device=d)
+    scratch = torch.empty(1 << 22, device=d)
+    Xd, Wd, bd = X.to(d), W.to(d), b.to(d)  # keep the device copies alive until the kernel ran
+    nat.check(nat.lib().vad_dense_forward(Xd.data_ptr(), M, K, Wd.data_ptr(), bd.data_ptr(), N,
+                                          Y.data_ptr(), relu, scratch.data_ptr(), scratch.numel(),
+                                          nat.stream_of(d)))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(Y.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+
+
+CONV_CASES = [(2, 32, 32, 19, 17, 1), (2, 32, 64, 29, 29, 2), (1, 64, 128, 15, 15, 2), (2, 128, 256, 8, 8, 1),
+              (3, 64, 64, 10, 7, 2), (1, 256, 256, 8, 8, 1)]
+
+
+@pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", CONV_CASES)
+def test_conv3x3_forward_and_dgrad(NF, Ci, Co, IH, IW, s):
+    nat = _lib()
+    g = torch.Generator().manual_seed(NF * 7 + Ci + Co + IH)
+    x = torch.randn(NF, Ci, IH, IW, generator=g)
+    w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
+    bias = torch.randn(Co, generator=g)
+    ref = F.conv2d(x, w, bias, stride=s, padding=1)
+    OH, OW = ref.shape[2:]
+    d = torch.device("cuda")
+    xh = x.permute(0, 2, 3, 1).contiguous().to(d)
+    y = torch.empty(NF, OH, OW, Co, device=d)
+    wf = torch.empty(9 * Ci * Co, device=d)
+    wd = torch.empty(9 * Ci * Co, device=d)
+    parts = torch.empty((NF * OH * OW // 64 + 2) * 2 * Co, device=d)
+    wdev = w.contiguous().to(d)
+    st = nat.stream_of(d)
+    bd = bias.to(d)
+    nat.check(nat.lib().vad_conv3x3_forward(xh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), bd.data_ptr(),
+                                            Co, s, y.data_ptr(), wf.data_ptr(), wd.data_ptr(), parts.data_ptr(), st))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(y.cpu().permute(0, 3, 1, 2).numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+    # transposed conv (input gradient)
+    dy = torch.randn(NF, Co, OH, OW, generator=g)
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, w, bias, stride=s, padding=1).backward(dy)
+    dx = torch.empty(NF, IH, IW, Ci, device=d)
+    dyh = dy.permute(0, 2, 3, 1).contiguous().to(d)
+    nat.check(nat.lib().vad_conv3x3_dgrad(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, s, dx.data_ptr(),
+                                          wf.data_ptr(), wd.data_ptr(), st))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(dx.cpu().permute(0, 3, 1, 2).numpy(), xr.grad.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("stream", [rng.S_DET_DROP1, rng.S_EPS, rng.S_INPUT])
+def test_device_rng_bitexact(stream):
+    nat = _lib()
+    d = torch.device("cuda")
+    out = torch.empty(37, 300, dtype=torch.int32, device=d)
+    nat.check(nat.lib().vad_rng_u24(12345, stream, 7, 1000, 37, 300, out.data_ptr(), nat.stream_of(d)))
+    ref = rng.u24(12345, stream, 7, np.arange(1000, 1037), np.arange(300))
+    np.testing.assert_array_equal(out.cpu().numpy().astype(np.int64), ref)
+
+
+def test_device_synth_frames_bitexact():
+    nat = _lib()
+    d = torch.device("cuda")
+    out = torch.empty(6, 51 * 40, device=d)
+    nat.check(nat.lib().vad_synth_frames(3, 1, 10, 6, 51 * 40, 0, out.data_ptr(), nat.stream_of(d)))
+    u8 = rng.pixels_u8(3, 1, 10, 6, 51 * 40).astype(np.float32)
+    np.testing.assert_array_equal(out.cpu().numpy(), (u8 - np.float32(0.5)) / np.float32(0.5))
+
+
+WGRAD_CASES = [(2, 32, 32, 19, 17, 1), (32, 256, 256, 8, 8, 1), (32, 128, 256, 15, 15, 2), (32, 32, 32, 57, 57, 1),
+               (8, 64, 64, 29, 29, 1), (3, 64, 128, 15, 15, 2)]
+
+
+@pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", WGRAD_CASES)
+def test_conv3x3_wgrad(NF, Ci, Co, IH, IW, s):
+    nat = _lib()
+    g = torch.Generator().manual_seed(NF * 5 + Ci + Co + IH)
+    x = torch.randn(NF, Ci, IH, IW, generator=g)
+    w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
+    wr = w.clone().requires_grad_(True)
+    y = F.conv2d(x, wr, None, stride=s, padding=1)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    d = torch.device("cuda")
+    xh = x.permute(0, 2, 3, 1).contiguous().to(d)
+    dyh = dy.permute(0, 2, 3, 1).contiguous().to(d)
+    dW = torch.empty(Co, Ci, 3, 3, device=d)
+    part = torch.empty(1 << 24, device=d)
+    nat.check(nat.lib().vad_conv3x3_wgrad(xh.data_ptr(), dyh.data_ptr(), NF, Ci, IH, IW, Co, s, dW.data_ptr(),
+                                          part.data_ptr(), part.numel(), nat.stream_of(d)))
+    torch.cuda.synchronize()
+    ref = wr.grad
+    np.testing.assert_allclose(dW.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4 * float(ref.abs().max()))
