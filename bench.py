@@ -1,0 +1,241 @@
+"""Training-throughput benchmark of the MI355X hot path (BASELINE.json config 2 / 3).
+
+One "step" = one fused train step of CausalAnomalyDetector (causal_anomaly_detection.py:669-690): forward
+(backbone, detector, causal head, direct classifier), the multi-term loss, backward, clip_grad_norm_(1.0) and
+AdamW — all in libvadhip kernels — on B=8 synthetic Avenue/UCSD-shaped clips of T=16 frames, 1x227x227, per GPU.
+Data parallel for --gpus N > 1 (launched by torch.distributed.run): 8 clips per rank, gradients summed over
+RCCL; value = all clips processed / max-over-ranks wall time (weak scaling).
+
+Prints ONE JSON line (rank 0).  `roofline` covers the dominant kernel family of the step, timed live with HIP
+events inside the timed region; `cpu_baseline` times the CPU oracle (oracle/cad_oracle.py, a port of the
+reference step) on this host's cores on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import io
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_METRIC = "training clips/sec (B×T frames) at 1/2/4/8 MI355X; frame-AUC parity vs CPU ref"
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector == FP32 matrix peak
+PEAK_HBM_GBPS = 8000.0     # MI355X_MICROARCH.md: HBM3E spec peak
+
+
+def conv_shapes(B, T, H, W):
+    """(NF, Ci, Co, OH, OW) of the eight 3x3 convs of ResNetBackbone (cad:121-139)."""
+    NF = B * T
+    h, w = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    h, w = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    out = []
+    for ci, co, s in [(32, 32, 1), (32, 32, 1), (32, 64, 2), (64, 64, 1), (64, 128, 2), (128, 128, 1),
+                      (128, 256, 2), (256, 256, 1)]:
+        h, w = (h - 1) // s + 1, (w - 1) // s + 1
+        out.append((NF, ci, co, h, w))
+    return out
+
+
+def algorithmic_work(label, B, T, H, W):
+    """(bound, amount) per launch of a labelled kernel: FLOPs for MFMA convs, HBM bytes for elementwise."""
+    fam, _, lay = label.partition("/L")
+    cs = conv_shapes(B, T, H, W)
+    if fam in ("conv_fwd", "conv_dgrad", "conv_wgrad"):
+        NF, ci, co, oh, ow = cs[int(lay)]
+        return "mfma", 2.0 * NF * oh * ow * co * ci * 9
+    if fam in ("bn_bwd_reduce", "bn_bwd_apply"):
+        NF, ci, co, oh, ow = cs[int(lay)]
+        n = NF * oh * ow * co * 4.0
+        return "hbm", (2 if fam == "bn_bwd_reduce" else 3) * n
+    if fam == "conv1":
+        NF = B * T
+        oh, ow = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        return "mfma", 2.0 * NF * oh * ow * 32 * 49
+    return None, None
+
+
+def run_gpu(args, rank, world, local_rank):
+    import torch
+    import torch.distributed as dist
+    from vad_amd import _native as nat
+    from vad_amd.cad import CausalAnomalyDetector
+    from vad_amd.train import CadTrainer, apply_memory_efficient_training
+
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    model = CausalAnomalyDetector()
+    with contextlib.redirect_stdout(io.StringIO()):
+        apply_memory_efficient_training(model)
+    model = model.to(dev)
+    trainer = CadTrainer(model, lr=3e-4, seed=1234)
+    B, T, H, W = args.batch, args.T, args.H, args.W
+    # synthetic clips resident in HBM before the timed region (device generator == oracle.rng.pixels_u8)
+    pool = []
+    for i in range(2):
+        x = torch.empty(B, T, 1, H, W, device=dev)
+        nat.check(nat.lib().vad_synth_frames(7, i, rank * B * T, B * T, H * W, 0, x.data_ptr(), nat.stream_of(dev)))
+        pool.append(x)
+    labels = torch.tensor([(rank * B + b) % 2 for b in range(B)], dtype=torch.int64, device=dev)
+
+    for i in range(args.warmup):
+        trainer.step(pool[i % 2], labels)
+    torch.cuda.synchronize()
+
+    # one instrumented step: per-label kernel times -> the dominant kernel family
+    eng = trainer.eng
+    eng.profile(True, "")
+    trainer.step(pool[0], labels)
+    torch.cuda.synchronize()
+    breakdown = eng.profile_read()
+    fam_time = {}
+    for lab, (ms, n) in breakdown.items():
+        fam = lab.split("/L")[0]
+        fam_time[fam] = fam_time.get(fam, 0.0) + ms
+    dominant = max(fam_time, key=fam_time.get)
+
+    # timed region: only the dominant family is bracketed by HIP events (on the plan's stream)
+    eng.profile(True, dominant)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        losses = trainer.step(pool[i % 2], labels)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    live = eng.profile_read()
+    eng.profile(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(losses[4].item())
+
+    # roofline of the dominant family, from the live events
+    bound, tot_work, tot_ms, launches = None, 0.0, 0.0, 0
+    for lab, (ms, n) in live.items():
+        bnd, work = algorithmic_work(lab, B, T, H, W)
+        if bnd is None:
+            continue
+        bound = bnd
+        tot_work += work * n
+        tot_ms += ms
+        launches += n
+    roof = None
+    if bound is not None and tot_ms > 0:
+        if bound == "mfma":
+            ach = tot_work / (tot_ms * 1e-3) / 1e12
+            roof = {"bound": "mfma", "kernel": dominant, "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None}
+        else:
+            ach = tot_work / (tot_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 1), "peak": PEAK_HBM_GBPS,
+                    "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 4), "traffic": None}
+        roof["launches_timed"] = launches
+        roof["avg_launch_us"] = round(1e3 * tot_ms / max(launches, 1), 2)
+    step_ms = 1e3 * elapsed / args.steps
+    # whole-step algorithmic FLOP rate (all 3x3 convs fwd/dgrad/wgrad + conv1 fwd), for context
+    conv_flops = sum(2.0 * NF * oh * ow * co * ci * 9 for NF, ci, co, oh, ow in conv_shapes(B, T, H, W))
+    dgrad_flops = conv_flops - 2.0 * B * T * conv_shapes(B, T, H, W)[0][3] * conv_shapes(B, T, H, W)[0][4] * 32 * 32 * 9
+    c1 = algorithmic_work("conv1", B, T, H, W)[1]
+    step_flops = 2 * conv_flops + dgrad_flops + c1
+    return dict(elapsed=elapsed, step_ms=step_ms, roof=roof, breakdown=breakdown, dominant=dominant,
+                final_loss=final_loss, step_tflops=step_flops / (step_ms * 1e-3) / 1e12)
+
+
+def cpu_baseline(args):
+    """The CPU oracle (a port of the reference step) on this host: bounded sample of the same workload."""
+    import torch
+    from oracle import cad_oracle as co
+    from vad_amd.cad import CausalAnomalyDetector
+    threads = torch.get_num_threads()
+    torch.manual_seed(0)
+    m = CausalAnomalyDetector()
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    params = {k: v for k, v in sd.items() if "running" not in k and "num_batches" not in k}
+    bufs = {k: v for k, v in sd.items() if "running" in k}
+    B, T, H, W = args.batch, args.T, args.H, args.W
+    x = co.synth_clips(7, 0, 0, B, T, H, W)
+    y = co.synth_labels(0, B)
+    state = {}
+    co.cad_train_step(params, bufs, state, x, y, co.CadDraws.make(1234, 0, 0, B, T))  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        co.cad_train_step(params, bufs, state, x, y, co.CadDraws.make(1234, n + 1, 0, B, T))
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or n >= 40:
+            break
+    return {"value": round(B * n / el, 3), "unit": "clips/s", "cores": threads, "kind": "port",
+            "sample": f"{n} train steps of B={B} clips x T={T} x 1x{H}x{W} (oracle/cad_oracle.py, torch CPU fp32, "
+                      f"{threads} threads), after 1 warm-up step"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8, help="clips per GPU")
+    ap.add_argument("--T", type=int, default=16)
+    ap.add_argument("--H", type=int, default=227)
+    ap.add_argument("--W", type=int, default=227)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--breakdown-out", default=None, help="write the per-kernel breakdown JSON here")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    r = run_gpu(args, rank, world, local_rank)
+    if rank == 0:
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
+        clips = world * args.batch * args.steps
+        out = {
+            "metric": BASELINE_METRIC,
+            "value": round(clips / r["elapsed"], 3),
+            "unit": "clips/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(r["step_ms"], 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (keyed-hash u8 pixels, Normalize(0.5,0.5)); random-init weights (torch.manual_seed(0))",
+            "config": {"workload": "causal_anomaly_detection.py train step (cad:669-690), BASELINE config "
+                                   + ("2" if world == 1 else "3"),
+                       "clips_per_gpu": args.batch, "global_batch": world * args.batch, "clip_len": args.T,
+                       "frame": f"1x{args.H}x{args.W}", "parallelism": f"dp{world}"},
+            "roofline": r["roof"],
+            "cpu_baseline": cpu,
+            "step_algorithmic_tflops": round(r["step_tflops"], 3),
+            "final_loss": r["final_loss"],
+        }
+        if args.breakdown_out:
+            with open(args.breakdown_out, "w") as f:
+                json.dump({"dominant": r["dominant"], "per_label_ms": r["breakdown"]}, f, indent=1)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

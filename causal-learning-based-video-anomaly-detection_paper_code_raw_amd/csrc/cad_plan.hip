@@ -239,6 +239,45 @@ __global__ void synth_kernel(uint64_t h1, int64_t frame0, int64_t nframes, int64
   }
 }
 
+// ------------------------------------------------------------------ HIP-event timing of labelled launches
+struct Profiler {
+  bool on = false;
+  std::string only;  // label prefix filter ("" = all)
+  struct Rec { std::string label; hipEvent_t a, b; };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  hipEvent_t get() {
+    if (used == pool.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      pool.push_back(e);
+    }
+    return pool[used++];
+  }
+  bool wants(const char* label) const { return on && std::string(label).rfind(only, 0) == 0; }
+  void reset() { recs.clear(); used = 0; }
+  ~Profiler() {
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+};
+
+#define TIMED(label, expr)                                       \
+  do {                                                           \
+    const bool _w = prof.wants(label);                           \
+    hipEvent_t _a = nullptr, _b = nullptr;                       \
+    if (_w) {                                                    \
+      _a = prof.get();                                           \
+      _b = prof.get();                                           \
+      VAD_HIP(hipEventRecord(_a, st));                           \
+    }                                                            \
+    VAD_TRY(expr);                                               \
+    if (_w) {                                                    \
+      VAD_HIP(hipEventRecord(_b, st));                           \
+      prof.recs.push_back({std::string(label), _a, _b});         \
+    }                                                            \
+  } while (0)
+
 // ------------------------------------------------------------------ the plan
 struct Ws {
   char* base = nullptr;
@@ -277,6 +316,12 @@ struct CadPlanImpl {
   int64_t parts_floats, dense_scratch_floats, wpart_floats, slab_len, act_max;
   int64_t clip0 = 0;
   int debug_stop_layer = -1;  // backward returns after this backbone layer (debug introspection)
+  Profiler prof;
+  char lbl[64];
+  const char* L_(const char* base, int l) {
+    snprintf(lbl, sizeof(lbl), "%s/L%d", base, l);
+    return lbl;
+  }
   int training = 1;
   bool have_labels = false;
   uint64_t seed = 0, step = 0;
@@ -390,22 +435,22 @@ struct CadPlanImpl {
 
   int forward(const float* x, hipStream_t st) {
     const CadLayout& LY = layout();
-    for (int l = 0; l < 8; ++l) VAD_TRY(conv3_prep_weights(P(LY.conv_w[l]), L[l], wf[l], wd[l], st));
+    for (int l = 0; l < 8; ++l) TIMED("prep", conv3_prep_weights(P(LY.conv_w[l]), L[l], wf[l], wd[l], st));
     int np = 0;
-    VAD_TRY(conv1_fwd(x, NF, H, W, P(LY.conv1_w), P(LY.conv1_b), y1, H1, W1, parts, &np, st));
-    VAD_TRY(bn_finalize(parts, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), RM(0), RV(0), 0.1f, 1e-5f,
-                        training, stats[0], st));
-    VAD_TRY(maxpool3s2_bnrelu(y1, stats[0], NF, H1, W1, 32, pool, HP, WP, st));
+    TIMED("conv1", conv1_fwd(x, NF, H, W, P(LY.conv1_w), P(LY.conv1_b), y1, H1, W1, parts, &np, st));
+    TIMED("bn_fin", bn_finalize(parts, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), RM(0), RV(0), 0.1f,
+                                1e-5f, training, stats[0], st));
+    TIMED("maxpool", maxpool3s2_bnrelu(y1, stats[0], NF, H1, W1, 32, pool, HP, WP, st));
     const float* src = pool;
     const float* sst = nullptr;
     for (int l = 0; l < 8; ++l) {
-      VAD_TRY(conv3_fwd(L[l], src, sst, wf[l], P(LY.conv_b[l]), y[l], parts, &np, st));
-      VAD_TRY(bn_finalize(parts, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]),
-                          RM(l + 1), RV(l + 1), 0.1f, 1e-5f, training, stats[l + 1], st));
+      TIMED(L_("conv_fwd", l), conv3_fwd(L[l], src, sst, wf[l], P(LY.conv_b[l]), y[l], parts, &np, st));
+      TIMED("bn_fin", bn_finalize(parts, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]),
+                                  RM(l + 1), RV(l + 1), 0.1f, 1e-5f, training, stats[l + 1], st));
       src = y[l];
       sst = stats[l + 1];
     }
-    VAD_TRY(avgpool_fwd(y[7], stats[8], B, T, HF, WF, 256, feats, pooled, st));
+    TIMED("avgpool", avgpool_fwd(y[7], stats[8], B, T, HF, WF, 256, feats, pooled, st));
     // detector_net (cad:167-179)
     const int64_t f0 = clip0 * T;
     const int dd[6] = {6144, 512, 256, 128, 64, 20};
@@ -414,8 +459,8 @@ struct CadPlanImpl {
       float* out = i < 4 ? dh[i] : dlog;
       const int sid = i == 0 ? S_DET_DROP1 : (i == 1 ? S_DET_DROP2 : 0);
       const double p = i == 0 ? 0.3 : 0.2;
-      VAD_TRY(dense_fwd(in, NF, dd[i], P(LY.det_w[i]), P(LY.det_b[i]), dd[i + 1], out, act(i < 4, sid, p, f0),
-                        dense_scratch, dense_scratch_floats, st));
+      TIMED("det_fwd", dense_fwd(in, NF, dd[i], P(LY.det_w[i]), P(LY.det_b[i]), dd[i + 1], out,
+                                 act(i < 4, sid, p, f0), dense_scratch, dense_scratch_floats, st));
       in = out;
     }
     // direct_classifier on the mean over T (cad:525-538, 568-570)
@@ -425,13 +470,13 @@ struct CadPlanImpl {
       float* out = i < 4 ? gh[i] : glog;
       const int sid = i == 0 ? S_DIRECT_DROP1 : (i == 1 ? S_DIRECT_DROP2 : 0);
       const double p = i == 0 ? 0.3 : 0.2;
-      VAD_TRY(dense_fwd(in, B, gd[i], P(LY.dir_w[i]), P(LY.dir_b[i]), gd[i + 1], out, act(i < 4, sid, p, clip0),
-                        dense_scratch, dense_scratch_floats, st));
+      TIMED("dir_fwd", dense_fwd(in, B, gd[i], P(LY.dir_w[i]), P(LY.dir_b[i]), gd[i + 1], out,
+                                 act(i < 4, sid, p, clip0), dense_scratch, dense_scratch_floats, st));
       in = out;
     }
-    VAD_TRY(head_fwd(head_args(), dlog, head_out(), st));
+    TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
     TailArgs t = tail_args(nullptr, nullptr, nullptr, nullptr);
-    VAD_TRY(cad_tail_fwd(t, st));
+    TIMED("tail", cad_tail_fwd(t, st));
     if (training && nbt) {
       hipLaunchKernelGGL(nbt_bump_kernel, dim3(1), dim3(64), 0, st, nbt, 9);
       VAD_LAUNCH_CHECK();
@@ -472,22 +517,22 @@ struct CadPlanImpl {
     VAD_HIP(hipMemsetAsync(grads, 0, sizeof(float) * LY.param_floats, st));
     TailArgs t = use_loss ? tail_args(nullptr, nullptr, nullptr, nullptr) : tail_args(dfin, dprobs, dcaus, dkl);
     if (!use_loss) t.labels = nullptr;
-    VAD_TRY(cad_tail_bwd(t, st));
+    TIMED("tail", cad_tail_bwd(t, st));
     HeadUp up{d_causal, d_kl, dz, dadj};
-    VAD_TRY(head_bwd(head_args(), dlog, head_out(), up, slabs, slab_len, d_dlog, st));
-    VAD_TRY(head_slab_reduce(slabs, B, slab_len, grads + LY.slots[LY.head0].offset, st));
+    TIMED("head_bwd", head_bwd(head_args(), dlog, head_out(), up, slabs, slab_len, d_dlog, st));
+    TIMED("head_bwd", head_slab_reduce(slabs, B, slab_len, grads + LY.slots[LY.head0].offset, st));
     // direct classifier chain
     const int gd[6] = {6144, 512, 256, 128, 64, 2};
     const double gp[5] = {0.3, 0.2, 0.0, 0.0, 0.0};
     const float* dcur = d_glog;
     for (int i = 4; i >= 0; --i) {
       const float* xin = i == 0 ? pooled : gh[i - 1];
-      VAD_TRY(dense_wgrad(dcur, B, gd[i + 1], xin, gd[i], G(LY.dir_w[i]), G(LY.dir_b[i]), dense_scratch,
-                          dense_scratch_floats, nullptr, st));
+      TIMED("dir_bwd", dense_wgrad(dcur, B, gd[i + 1], xin, gd[i], G(LY.dir_w[i]), G(LY.dir_b[i]), dense_scratch,
+                                   dense_scratch_floats, nullptr, st));
       float* dnext = i == 0 ? d_pooled : dg[i - 1];
       const float gs = (i >= 1 && training && gp[i - 1] > 0) ? (float)(1.0 / (1.0 - gp[i - 1])) : 1.f;
-      VAD_TRY(dense_dgrad(dcur, B, gd[i + 1], P(LY.dir_w[i]), gd[i], dnext, i == 0 ? nullptr : gh[i - 1], gs, nullptr,
-                          st));
+      TIMED("dir_bwd", dense_dgrad(dcur, B, gd[i + 1], P(LY.dir_w[i]), gd[i], dnext, i == 0 ? nullptr : gh[i - 1], gs,
+                                   nullptr, st));
       dcur = dnext;
     }
     // detector chain (skipped on device when no box was in range: no grads reach it, cad:221-226)
@@ -496,29 +541,30 @@ struct CadPlanImpl {
     dcur = d_dlog;
     for (int i = 4; i >= 0; --i) {
       const float* xin = i == 0 ? feats : dh[i - 1];
-      VAD_TRY(dense_wgrad(dcur, NF, dd[i + 1], xin, dd[i], G(LY.det_w[i]), G(LY.det_b[i]), dense_scratch,
-                          dense_scratch_floats, flags, st));
+      TIMED("det_bwd", dense_wgrad(dcur, NF, dd[i + 1], xin, dd[i], G(LY.det_w[i]), G(LY.det_b[i]), dense_scratch,
+                                   dense_scratch_floats, flags, st));
       float* dnext = i == 0 ? d_feat_det : ddh[i - 1];
       const float gs = (i >= 1 && training && gp[i - 1] > 0) ? (float)(1.0 / (1.0 - gp[i - 1])) : 1.f;
-      VAD_TRY(dense_dgrad(dcur, NF, dd[i + 1], P(LY.det_w[i]), dd[i], dnext, i == 0 ? nullptr : dh[i - 1], gs, flags,
-                          st));
+      TIMED("det_bwd", dense_dgrad(dcur, NF, dd[i + 1], P(LY.det_w[i]), dd[i], dnext, i == 0 ? nullptr : dh[i - 1],
+                                   gs, flags, st));
       dcur = dnext;
     }
     // backbone
-    VAD_TRY(avgpool_bwd(d_feat_det, d_pooled, B, T, HF, WF, 256, dA, st));
+    TIMED("avgpool_bwd", avgpool_bwd(d_feat_det, d_pooled, B, T, HF, WF, 256, dA, st));
     for (int l = 7; l >= 0; --l) {
       const int64_t M = (int64_t)NF * L[l].OH * L[l].OW;
       const int C = L[l].Co;
       int np = 0, nb = 0, ns = 0;
-      VAD_TRY(bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st));
-      VAD_TRY(bn_bwd_finalize(parts, np, C, (double)M, P(LY.bn_w[l]), stats[l + 1], G(LY.bn_w[l]), G(LY.bn_b[l]),
-                                training, st));
-      VAD_TRY(bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dY, bparts, &nb, st));
+      TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st));
+      TIMED("bn_bwd_fin", bn_bwd_finalize(parts, np, C, (double)M, P(LY.bn_w[l]), stats[l + 1], G(LY.bn_w[l]),
+                                          G(LY.bn_b[l]), training, st));
+      TIMED(L_("bn_bwd_apply", l), bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dY, bparts, &nb, st));
       const float* src = l == 0 ? pool : y[l - 1];
       const float* sst = l == 0 ? nullptr : stats[l];
-      VAD_TRY(conv3_wgrad(L[l], dY, src, sst, wpart, &ns, wpart_floats, st));
-      VAD_TRY(conv3_wgrad_reduce(L[l], wpart, ns, bparts, nb, G(LY.conv_w[l]), G(LY.conv_b[l]), st));
-      if (l > 0) VAD_TRY(conv3_dgrad(L[l], dY, wd[l], dA, st));
+      TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dY, src, sst, wpart, &ns, wpart_floats, st));
+      TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], wpart, ns, bparts, nb, G(LY.conv_w[l]), G(LY.conv_b[l]),
+                                                     st));
+      if (l > 0) TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dY, wd[l], dA, st));
       if (l == debug_stop_layer) return 0;
     }
     return 0;
@@ -528,6 +574,13 @@ struct CadPlanImpl {
                 hipStream_t st) {
     const CadLayout& LY = layout();
     VAD_CHECK(m && v && steps, "optimizer: state buffers not bound");
+    const bool pw = prof.wants("optimizer");
+    hipEvent_t pa = nullptr, pb = nullptr;
+    if (pw) {
+      pa = prof.get();
+      pb = prof.get();
+      VAD_HIP(hipEventRecord(pa, st));
+    }
     const int nb = 512;
     hipLaunchKernelGGL(sqsum_kernel, dim3(nb), dim3(256), 0, st, grads, LY.param_floats, gscale, sq_parts);
     VAD_LAUNCH_CHECK();
@@ -545,6 +598,10 @@ struct CadPlanImpl {
     hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)std::min<int64_t>(nchunks, 4096)), dim3(256), 0, st, params,
                        grads, m, v, chunk_slot, nchunks, slot_info, clip, gscale, lr, b1, b2, eps, wd_);
     VAD_LAUNCH_CHECK();
+    if (pw) {
+      VAD_HIP(hipEventRecord(pb, st));
+      prof.recs.push_back({"optimizer", pa, pb});
+    }
     return 0;
   }
 };
@@ -726,6 +783,46 @@ int vad_cad_set_debug(vad_cad_plan* plan, const char* key, int64_t value) {
   if (std::string(key) == "stop_layer") plan->impl.debug_stop_layer = (int)value;
   else { vad::set_error("vad_cad_set_debug: unknown key"); return 1; }
   return 0;
+}
+
+int vad_cad_profile(vad_cad_plan* plan, int enable, const char* only_prefix) {
+  VAD_CHECK(plan != nullptr, "vad_cad_profile: null plan");
+  Profiler& p = plan->impl.prof;
+  p.on = enable != 0;
+  p.only = only_prefix ? only_prefix : "";
+  p.reset();
+  return 0;
+}
+
+/* aggregates the recorded launches by label (after the stream has been synchronised). Returns the number of
+ * distinct labels; fills at most cap entries: labels (64 chars each), total ms, launch counts. */
+int vad_cad_profile_read(vad_cad_plan* plan, char* labels, double* total_ms, int* counts, int cap) {
+  VAD_CHECK(plan != nullptr, "vad_cad_profile_read: null plan");
+  Profiler& p = plan->impl.prof;
+  std::vector<std::string> names;
+  std::vector<double> tot;
+  std::vector<int> cnt;
+  for (auto& r : p.recs) {
+    float ms = 0.f;
+    VAD_HIP(hipEventSynchronize(r.b));
+    VAD_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+    size_t i = 0;
+    while (i < names.size() && names[i] != r.label) ++i;
+    if (i == names.size()) {
+      names.push_back(r.label);
+      tot.push_back(0.0);
+      cnt.push_back(0);
+    }
+    tot[i] += ms;
+    cnt[i] += 1;
+  }
+  for (size_t i = 0; i < names.size() && (int)i < cap; ++i) {
+    strncpy(labels + 64 * i, names[i].c_str(), 63);
+    labels[64 * i + 63] = 0;
+    total_ms[i] = tot[i];
+    counts[i] = cnt[i];
+  }
+  return (int)names.size();
 }
 
 int vad_debug_d2h(void* host, const void* dev, int64_t bytes) {

@@ -160,6 +160,27 @@ class CadEngine:
         nat.check(nat.lib().vad_cad_backward(pl.h, 1 if use_loss else 0, *[nat.ptr(t) for t in c],
                                              nat.stream_of(self.device)))
 
+    def profile(self, enable: bool, only_prefix: str = ""):
+        """HIP-event timing of the plan's labelled launches (all plans of this engine)."""
+        for pl in self.plans.values():
+            nat.check(nat.lib().vad_cad_profile(pl.h, 1 if enable else 0, only_prefix.encode()))
+
+    def profile_read(self, shape=None) -> dict:
+        """{label: (total_ms, launches)} recorded since profile(True) (synchronises the stream)."""
+        pl = self.plans[shape] if shape is not None else self._last[0]
+        cap = 256
+        labels = ctypes.create_string_buffer(64 * cap)
+        tot = (ctypes.c_double * cap)()
+        cnt = (ctypes.c_int * cap)()
+        n = nat.lib().vad_cad_profile_read(pl.h, labels, tot, cnt, cap)
+        if n < 0:
+            nat.check(1)
+        out = {}
+        for i in range(min(n, cap)):
+            lab = labels.raw[64 * i:64 * (i + 1)].split(b"\0", 1)[0].decode()
+            out[lab] = (tot[i], cnt[i])
+        return out
+
     def optimizer_step(self, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, max_norm=1.0, grad_scale=1.0,
                        total_norm=None):
         self.init_optimizer_state()

@@ -108,6 +108,10 @@ int vad_conv3x3_wgrad(const float* x_nhwc, const float* dy_nhwc, int NF, int Ci,
 int vad_cad_debug_buffer(vad_cad_plan* plan, const char* name, int idx, void** ptr, int64_t* nfloats);
 int vad_cad_set_debug(vad_cad_plan* plan, const char* key, int64_t value);  /* "stop_layer" */
 int vad_debug_d2h(void* host, const void* dev, int64_t bytes);
+/* HIP-event timing of labelled launches (conv_fwd/L<l>, conv_wgrad/L<l>, conv_dgrad/L<l>, bn_bwd_*, conv1,
+ * det_fwd, head_fwd, optimizer, ...).  enable=0 turns it off; only_prefix restricts the labels recorded. */
+int vad_cad_profile(vad_cad_plan* plan, int enable, const char* only_prefix);
+int vad_cad_profile_read(vad_cad_plan* plan, char* labels, double* total_ms, int* counts, int cap);
 
 #ifdef __cplusplus
 }
