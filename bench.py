@@ -95,6 +95,8 @@ def run_gpu(args, rank, world, local_rank):
     breakdown = eng.profile_read()
     fam_time = {}
     for lab, (ms, n) in breakdown.items():
+        if algorithmic_work(lab, B, T, H, W)[0] is None:
+            continue  # only families with a defined algorithmic work can carry a roofline
         fam = lab.split("/L")[0]
         fam_time[fam] = fam_time.get(fam, 0.0) + ms
     dominant = max(fam_time, key=fam_time.get)

@@ -8,13 +8,15 @@
 namespace vad {
 
 // =====================================================================================================
-// conv1: 1 -> 32 channels, 7x7, stride 2, pad 3.  One block = one frame x a band of RB output rows; the
-// zero-padded input band is staged in LDS, weights are wave-uniform (scalar loads), each thread owns whole
-// pixels (32 accumulators) so the NHWC store is 128 contiguous bytes.  BN statistics of the raw output are
-// reduced per block into partials (deterministic, no atomics).
+// conv1: 1 -> 32 channels, 7x7, stride 2, pad 3, as a K=49 (padded to 56) GEMM on f32 MFMA.
+// One block = one frame x a band of C1_RB output rows.  The zero-padded input band is staged in LDS; each wave
+// walks 32-pixel tiles of the band: lane (i, h) gathers its A operand patch[2*oy+kh][2*ox+kw] straight from LDS
+// (k = 8*kk + 4*h + s), its B operand (weights of channel lane&31) lives in 28 registers for the whole block.
+// Epilogue: +bias, NHWC store (one 128-B row per pixel), per-block BN partial sums (deterministic).
 // =====================================================================================================
 constexpr int C1_RB = 8;
 constexpr int C1_CO = 32;
+constexpr int C1_K = 56;  // 49 taps padded to 7 MFMA sub-steps of 8
 
 __global__ __launch_bounds__(256) void conv1_kernel(const float* __restrict__ x, int H, int W,
                                                     const float* __restrict__ w, const float* __restrict__ bias,
@@ -23,64 +25,69 @@ __global__ __launch_bounds__(256) void conv1_kernel(const float* __restrict__ x,
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int img = blockIdx.x / bands, band = blockIdx.x % bands;
   const int r0 = band * C1_RB;
-  const int PW = 2 * OW + 6;              // padded band width
+  const int PW = 2 * OW + 6;  // padded band width
   const int PH = 2 * C1_RB + 5;
-  float* patch = sm;                      // [PH][PW]
+  float* patch = sm;  // [PH][PW]
   const float* xi = x + (int64_t)img * H * W;
   for (int i = threadIdx.x; i < PH * PW; i += 256) {
     const int pr = i / PW, pc = i - pr * PW;
     const int ih = 2 * r0 - 3 + pr, iw = pc - 3;
     patch[i] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? xi[(int64_t)ih * W + iw] : 0.f;
   }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  // B operand: w[j][k] for k = 8*kk + 4*h + s, zero for k >= 49
+  float wr[28];
+  int koff[28];
+#pragma unroll
+  for (int kk = 0; kk < 7; ++kk)
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int k = kk * 8 + 4 * h + s4;
+      wr[kk * 4 + s4] = k < 49 ? w[j * 49 + k] : 0.f;
+      koff[kk * 4 + s4] = k < 49 ? (k / 7) * PW + (k % 7) : 0;
+    }
+  const float bj = bias[j];
   __syncthreads();
-  float s1[C1_CO], s2[C1_CO];
-#pragma unroll
-  for (int c = 0; c < C1_CO; ++c) s1[c] = s2[c] = 0.f;
   const int rows = min(C1_RB, OH - r0);
-  for (int p = threadIdx.x; p < rows * OW; p += 256) {
-    const int oy = p / OW, ox = p - oy * OW;
-    float acc[C1_CO];
-#pragma unroll
-    for (int c = 0; c < C1_CO; ++c) acc[c] = bias[c];
+  const int npix = rows * OW;
+  float s1 = 0.f, s2 = 0.f;
+  for (int t0 = wave * 32; t0 < npix; t0 += 4 * 32) {
+    // this lane's pixel for the A operand: i = lane & 31
+    const int pa = t0 + (lane & 31);
+    const int pac = pa < npix ? pa : npix - 1;
+    const int oy = pac / OW, ox = pac - oy * OW;
     const float* pp = patch + (2 * oy) * PW + 2 * ox;
+    f32x16 acc;
 #pragma unroll
-    for (int kh = 0; kh < 7; ++kh) {
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-      for (int kw = 0; kw < 7; ++kw) {
-        const float v = pp[kh * PW + kw];
+    for (int q = 0; q < 28; ++q) acc = mfma32(pp[koff[q]], wr[q], acc);
 #pragma unroll
-        for (int c = 0; c < C1_CO; ++c) acc[c] = fmaf(v, w[c * 49 + kh * 7 + kw], acc[c]);
+    for (int r = 0; r < 16; ++r) {
+      const int pi = t0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (pi < npix) {
+        const int py = pi / OW, px = pi - py * OW;
+        const float v = acc[r] + bj;
+        y[(((int64_t)img * OH + r0 + py) * OW + px) * C1_CO + j] = v;
+        s1 += v;
+        s2 = fmaf(v, v, s2);
       }
     }
-    float* dst = y + (((int64_t)img * OH + r0 + oy) * OW + ox) * C1_CO;
-#pragma unroll
-    for (int c = 0; c < C1_CO; c += 4) {
-      f32x4 v = {acc[c], acc[c + 1], acc[c + 2], acc[c + 3]};
-      *reinterpret_cast<f32x4*>(dst + c) = v;
-    }
-#pragma unroll
-    for (int c = 0; c < C1_CO; ++c) {
-      s1[c] += acc[c];
-      s2[c] = fmaf(acc[c], acc[c], s2[c]);
-    }
   }
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 32, 64);
   __syncthreads();
   float* red = sm;  // [4 waves][2][32]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int c = 0; c < C1_CO; ++c) {
-    const float a = wave_sum(s1[c]), b = wave_sum(s2[c]);
-    if (lane == 0) {
-      red[wave * 64 + c] = a;
-      red[wave * 64 + 32 + c] = b;
-    }
+  if (lane < 32) {
+    red[wave * 64 + lane] = s1;
+    red[wave * 64 + 32 + lane] = s2;
   }
   __syncthreads();
   if (threadIdx.x < 64) {
     const int t = threadIdx.x;
     const float v = red[t] + red[64 + t] + red[128 + t] + red[192 + t];
-    // partial layout [P][2*C]: sums then sums of squares
-    partials[(int64_t)blockIdx.x * 2 * C1_CO + t] = v;
+    partials[(int64_t)blockIdx.x * 2 * C1_CO + t] = v;  // [P][2*C]: sums then sums of squares
   }
 }
 
@@ -163,11 +170,17 @@ int bn_finalize(const float* partials, int P, int C, double count, const float* 
 //   apply: dY = k * (dZ - mean(dZ) - xhat*mean(dZ*xhat)), plus per-block sum(dY) for the conv bias grad
 // Thread layout over [M][C] rows: thread -> (row offset, channel quad); 1024 rows per block.
 // =====================================================================================================
-constexpr int BN_ROWS = 1024;
+// rows per block: 1024, lowered (down to 64) until the grid has >= 1024 blocks.  Callers size partial buffers for
+// the worst case ceil(M/64) blocks (CadPlanImpl::carve).
+static int bn_rows(int M) {
+  int r = 1024;
+  while (r > 64 && cdiv(M, r) < 1024) r >>= 1;
+  return r;
+}
 
 int bn_rows_parts(int M, int C) {
   (void)C;
-  return (int)cdiv(M, BN_ROWS);
+  return (int)cdiv(M, bn_rows(M));
 }
 
 __device__ inline void bn_block_reduce_store(float (&v)[2][4], int C, float* out) {
@@ -190,7 +203,7 @@ __device__ inline void bn_block_reduce_store(float (&v)[2][4], int C, float* out
 
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ dA, const float* __restrict__ y,
                                                             const float* __restrict__ stats, int M, int C,
-                                                            float* __restrict__ partials) {
+                                                            float* __restrict__ partials, int BN_ROWS) {
   const int nq = C / 4, groups = 256 / nq;
   const int q = threadIdx.x % nq, g = threadIdx.x / nq;
   const int c = q * 4;
@@ -219,7 +232,7 @@ int bn_bwd_reduce(const float* dA, const float* y, const float* stats, int M, in
                   hipStream_t st) {
   VAD_CHECK(C % 4 == 0 && C <= 1024 && 256 % (C / 4) == 0, "bn_bwd_reduce: unsupported C");
   const int P = bn_rows_parts(M, C);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(P), dim3(256), 0, st, dA, y, stats, M, C, partials);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(P), dim3(256), 0, st, dA, y, stats, M, C, partials, bn_rows(M));
   VAD_LAUNCH_CHECK();
   *nparts = P;
   return 0;
@@ -267,7 +280,8 @@ int bn_bwd_finalize(const float* partials, int P, int C, double count, const flo
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ dA, const float* __restrict__ y,
                                                            const float* __restrict__ stats, int M, int C,
-                                                           float* __restrict__ dY, float* __restrict__ bparts) {
+                                                           float* __restrict__ dY, float* __restrict__ bparts,
+                                                           int BN_ROWS) {
   const int nq = C / 4, groups = 256 / nq;
   const int q = threadIdx.x % nq, g = threadIdx.x / nq;
   const int c = q * 4;
@@ -301,7 +315,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
                  int* nparts, hipStream_t st) {
   const int P = bn_rows_parts(M, C);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(P), dim3(256), 0, st, dA, y, stats, M, C, dY, bias_partials);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(P), dim3(256), 0, st, dA, y, stats, M, C, dY, bias_partials,
+                     bn_rows(M));
   VAD_LAUNCH_CHECK();
   *nparts = P;
   return 0;
@@ -359,41 +374,46 @@ __device__ inline int ap_start(int i, int in, int out) { return (i * in) / out; 
 __device__ inline int ap_end(int i, int in, int out) { return ((i + 1) * in + out - 1) / out; }
 
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restrict__ y, const float* __restrict__ stats,
-                                                          int B, int T, int H, int W, int C,
-                                                          float* __restrict__ feats, float* __restrict__ pooled) {
-  const int b = blockIdx.y;
+                                                          int H, int W, int C, float* __restrict__ feats) {
+  const int img = blockIdx.y;
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   const float sc = stats[2 * C + c], sh = stats[3 * C + c];
-  float psum[24];
+  const float* yi = y + (int64_t)img * H * W * C;
 #pragma unroll
-  for (int k = 0; k < 24; ++k) psum[k] = 0.f;
-  for (int t = 0; t < T; ++t) {
-    const int img = b * T + t;
-    const float* yi = y + (int64_t)img * H * W * C;
+  for (int i = 0; i < 4; ++i) {
+    const int h0 = ap_start(i, H, 4), h1 = ap_end(i, H, 4);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int h0 = ap_start(i, H, 4), h1 = ap_end(i, H, 4);
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const int w0 = ap_start(j, W, 6), w1 = ap_end(j, W, 6);
-        float s = 0.f;
-        for (int hh = h0; hh < h1; ++hh)
-          for (int ww = w0; ww < w1; ++ww) s += fmaxf(fmaf(yi[((int64_t)hh * W + ww) * C + c], sc, sh), 0.f);
-        const float v = s / (float)((h1 - h0) * (w1 - w0));
-        feats[(int64_t)img * C * 24 + c * 24 + i * 6 + j] = v;
-        psum[i * 6 + j] += v;
-      }
+    for (int j = 0; j < 6; ++j) {
+      const int w0 = ap_start(j, W, 6), w1 = ap_end(j, W, 6);
+      float s = 0.f;
+      for (int hh = h0; hh < h1; ++hh)
+        for (int ww = w0; ww < w1; ++ww) s += fmaxf(fmaf(yi[((int64_t)hh * W + ww) * C + c], sc, sh), 0.f);
+      feats[(int64_t)img * C * 24 + c * 24 + i * 6 + j] = s / (float)((h1 - h0) * (w1 - w0));
     }
   }
-#pragma unroll
-  for (int k = 0; k < 24; ++k) pooled[(int64_t)b * C * 24 + c * 24 + k] = psum[k] / (float)T;
+}
+
+// features.mean(dim=1) (cad:568)
+__global__ __launch_bounds__(256) void temporal_mean_kernel(const float* __restrict__ feats, int B, int T, int D,
+                                                            float* __restrict__ pooled) {
+  const int64_t total = (int64_t)B * D;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i / D, d = i - b * D;
+    float s = 0.f;
+    for (int t = 0; t < T; ++t) s += feats[(b * T + t) * D + d];
+    pooled[i] = s / (float)T;
+  }
 }
 
 int avgpool_fwd(const float* y, const float* stats, int B, int T, int H, int W, int C, float* feats, float* pooled,
                 hipStream_t st) {
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((unsigned)cdiv(C, 256), B), dim3(256), 0, st, y, stats, B, T, H, W, C,
-                     feats, pooled);
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((unsigned)cdiv(C, 256), B * T), dim3(256), 0, st, y, stats, H, W, C,
+                     feats);
+  VAD_LAUNCH_CHECK();
+  const int64_t total = (int64_t)B * C * 24;
+  hipLaunchKernelGGL(temporal_mean_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 1024)), dim3(256), 0,
+                     st, feats, B, T, C * 24, pooled);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -795,7 +815,7 @@ int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const fl
   auto run = [&](auto cfg) -> int {
     using C = decltype(cfg);
     const int tiles = (int)(cdiv(M, C::BM) * cdiv(N, C::BN));
-    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(1024, tiles), cdiv(K, 4 * BK)));
+    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(1024, tiles), cdiv(K, 16 * BK)));
     while ((int64_t)splits * M * N > partial_cap && splits > 1) splits /= 2;
     typename DenseKM<C::BM>::Params pa{dY, L.Co, L.Co, K, -1};
     typename ConvPatchKM<C::BN>::Params pb{src, L.NF, L.OH, L.OW, L.stride, 1, L.IH, L.IW, L.Ci, 3, N,
@@ -808,36 +828,58 @@ int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const fl
   return run(T64x64{});
 }
 
+// Split-K slab reduction of the conv weight gradient.  Block = 32 consecutive slab elements x 8 split-lanes; each
+// lane sums every 8th slab with 4 independent accumulators, lanes are combined through LDS (fixed order).
+// Slab layout [S][co][t*Ci + ci]; dW is torch [co][ci][kh][kw].
 __global__ __launch_bounds__(256) void conv3_wgrad_reduce_kernel(const float* __restrict__ part, int S, int Co, int Ci,
                                                                  const float* __restrict__ bparts, int NB,
-                                                                 float* __restrict__ dW, float* __restrict__ db) {
-  const int64_t total = (int64_t)Co * Ci * 9;
+                                                                 float* __restrict__ dW, float* __restrict__ db,
+                                                                 int wblocks) {
+  __shared__ float red[8][33];
   const int64_t ldp = 9 * Ci;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    // i indexes dW[co][ci][t]
-    const int t = (int)(i % 9);
-    const int ci = (int)((i / 9) % Ci);
-    const int co = (int)(i / (9 * Ci));
-    const int64_t src = (int64_t)co * ldp + t * Ci + ci;
+  const int64_t total = (int64_t)Co * ldp;
+  if ((int)blockIdx.x >= wblocks) {  // conv bias: one block per channel, 256-way strided sum + tree
+    const int c = blockIdx.x - wblocks;
     float s = 0.f;
-    for (int z = 0; z < S; ++z) s += part[(int64_t)z * Co * ldp + src];
-    dW[i] = s;
+    for (int p = threadIdx.x; p < NB; p += 256) s += bparts[(int64_t)p * 2 * Co + c];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) db[c] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    return;
   }
-  if (blockIdx.x == 0 && db != nullptr) {
-    for (int co = threadIdx.x; co < Co; co += 256) {
-      float s = 0.f;
-      for (int p = 0; p < NB; ++p) s += bparts[(int64_t)p * 2 * Co + co];
-      db[co] = s;
+  const int e = threadIdx.x & 31, lane8 = threadIdx.x >> 5;
+  const int64_t i = (int64_t)blockIdx.x * 32 + e;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (i < total) {
+    int z = lane8;
+    for (; z + 24 < S; z += 32) {
+      a0 += part[(int64_t)z * total + i];
+      a1 += part[(int64_t)(z + 8) * total + i];
+      a2 += part[(int64_t)(z + 16) * total + i];
+      a3 += part[(int64_t)(z + 24) * total + i];
     }
+    for (; z < S; z += 8) a0 += part[(int64_t)z * total + i];
+  }
+  red[lane8][e] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (threadIdx.x < 32 && i < total) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += red[q][e];
+    const int64_t co = i / ldp, r = i - co * ldp;
+    const int t = (int)(r / Ci), ci = (int)(r - (int64_t)t * Ci);
+    dW[(co * Ci + ci) * 9 + t] = s;
   }
 }
 
 int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, const float* bias_partials,
                        int nbias_parts, float* dW, float* db, hipStream_t st) {
   const int64_t total = (int64_t)L.Co * L.Ci * 9;
-  const int grid = (int)std::min<int64_t>(cdiv(total, 256), 2048);
-  hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3(grid), dim3(256), 0, st, partial, nsplit, L.Co, L.Ci,
-                     bias_partials, nbias_parts, dW, db);
+  const int wblocks = (int)cdiv(total, 32);
+  const int bblocks = db ? L.Co : 0;
+  hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(256), 0, st, partial, nsplit,
+                     L.Co, L.Ci, bias_partials, nbias_parts, dW, db, wblocks);
   VAD_LAUNCH_CHECK();
   return 0;
 }

@@ -304,7 +304,7 @@ struct CadPlanImpl {
   // workspace carve
   float *y1, *pool, *y[8], *stats[9], *parts, *wf[8], *wd[8], *feats, *pooled;
   float *dh[5], *dlog, *gh[5], *glog;
-  float *head_ws;
+  float *head_ws, *head_rows;
   int* head_iws;
   float *probs, *finalv, *causal, *kl, *z, *adj, *boxes;
   int *counts, *nmax, *clip_flags, *flags;
@@ -355,6 +355,7 @@ struct CadPlanImpl {
     for (int i = 0; i < 4; ++i) gh[i] = w.take<float>((int64_t)B * gd[i]);
     glog = w.take<float>((int64_t)B * 2);
     head_ws = w.take<float>((int64_t)B * head_ws_floats(T));
+    head_rows = w.take<float>(head_rows_floats(B, T));
     head_iws = w.take<int>((int64_t)B * head_iws_ints(T));
     probs = w.take<float>(B * 2);
     finalv = w.take<float>(B);
@@ -385,7 +386,7 @@ struct CadPlanImpl {
     dense_scratch = w.take<float>(dense_scratch_floats);
     dA = w.take<float>(act_max);
     dY = w.take<float>(act_max);
-    bparts = w.take<float>(cdiv(act_max / 32, 1024) * 2 * 256 + 1024);
+    bparts = w.take<float>(parts_floats);  // same bound as parts: ceil(M/64) blocks x 2C per layer
     wpart_floats = 16ll << 20;
     wpart = w.take<float>(wpart_floats);
     sq_parts = w.take<float>(1024);
@@ -416,6 +417,8 @@ struct CadPlanImpl {
     a.ws_stride = head_ws_floats(T);
     a.iws = head_iws;
     a.iws_stride = head_iws_ints(T);
+    a.rows = head_rows;
+    a.grad = grads;
     return a;
   }
   HeadOut head_out() const { return HeadOut{causal, kl, z, adj, boxes, counts, nmax, clip_flags}; }
@@ -521,6 +524,7 @@ struct CadPlanImpl {
     HeadUp up{d_causal, d_kl, dz, dadj};
     TIMED("head_bwd", head_bwd(head_args(), dlog, head_out(), up, slabs, slab_len, d_dlog, st));
     TIMED("head_bwd", head_slab_reduce(slabs, B, slab_len, grads + LY.slots[LY.head0].offset, st));
+    TIMED("head_bwd", head_rows_wgrad(head_args(), st));
     // direct classifier chain
     const int gd[6] = {6144, 512, 256, 128, 64, 2};
     const double gp[5] = {0.3, 0.2, 0.0, 0.0, 0.0};

@@ -32,14 +32,17 @@ struct HeadArgs {
   const float* pbase;     // flat parameter buffer
   int64_t off[H_NUM];     // slot offsets into pbase / grad slabs (relative to head_begin for slabs)
   int64_t head_begin;
-  float* ws;              // per-clip workspace
+  float* ws;              // per-clip workspace (small per-clip tensors)
   int64_t ws_stride;
   int* iws;               // per-clip int workspace
   int64_t iws_stride;
+  float* rows;            // per-trajectory-row arrays, R = B*T*NMAX rows (see RowLayout in head.hip)
+  float* grad;            // flat grad buffer (GRU / ReID weight grads are written here directly)
 };
 
 int64_t head_ws_floats(int T);
 int64_t head_iws_ints(int T);
+int64_t head_rows_floats(int B, int T);
 
 // forward: det logits [B*T][20] -> per-clip outputs
 struct HeadOut {
@@ -64,6 +67,8 @@ struct HeadUp {
 int head_bwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, const HeadUp& up, float* slabs,
              int64_t slab_len, float* d_det_logits, hipStream_t st);
 int head_slab_reduce(const float* slabs, int B, int64_t slab_len, float* grad_head, hipStream_t st);
+// GRU / ReID weight grads over all trajectory rows, written to a.grad (run after head_slab_reduce)
+int head_rows_wgrad(const HeadArgs& a, hipStream_t st);
 
 // tail: softmax(direct logits), final score, optional loss + upstream grads, flag OR-reduce
 struct TailArgs {

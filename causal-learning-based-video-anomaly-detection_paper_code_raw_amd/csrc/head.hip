@@ -1,42 +1,64 @@
-// Fused causal head: one 256-thread block per clip runs every per-clip stage of CausalAnomalyDetector that the
-// reference executes as Python loops (cad:194-502): box decode + range filter + fallback, ReID MLP, zero-padded
-// trajectory tensor, GRU(68->64) over T for all trajectories at once, latent encoder, VAE + KL, pairwise edge
-// MLP -> 6x6 adjacency, (A z^T)^T dynamics MLP, three scorers and the 0.5/0.3/0.2 blend.  The backward kernel is
-// the hand-derived reverse of the same graph (BPTT through the GRU) writing a per-clip gradient slab, reduced
-// afterwards in a fixed clip order (deterministic, no atomics).
+// Causal head of CausalAnomalyDetector (cad:194-502) — the stages the reference runs as Python loops over clips,
+// frames, detections and trajectories — as five kernels:
+//   rows_fwd  (one block per frame)  : box decode + range filter + fallback (cad:198-228), ReID MLP on the real
+//                                      boxes, zero-padded trajectory rows x = [box, reid] (cad:248-274) and the GRU
+//                                      input projection W_ih x + b_ih for all 5 rows of the frame;
+//   seq_fwd   (one block per clip)   : the GRU recurrence over T for all trajectories at once (W_hh in LDS), encoder,
+//                                      VAE + KL, pairwise edge MLP, (A z^T)^T dynamics, three scorers (cad:287-502);
+//   seq_bwd   (one block per clip)   : reverse of seq_fwd incl. BPTT; small-layer weight grads into a per-clip slab;
+//   rows_bwd  (one block per frame)  : d x = W_ih^T d gates, ReID backward, d box -> d detector logits;
+//   rows_wgrad (output-parallel)     : GRU and ReID weight/bias grads as fixed-order reductions over all B*T*5 rows.
+// Trajectory row r = (b*T + t)*5 + j (j = compacted detection index in frame t = trajectory index n).
+// Deterministic: no atomics; per-clip slabs are reduced in clip order.
 #include "head.h"
 
 namespace vad {
 
-// ------------------------------------------------------------------ per-clip workspace layout
-struct HL {
-  int T;
-  int64_t boxes, x, rh1, rh2, gi, ghn, r, z, n, hp, hT, enc, ce1, ce2, mu, lv, zz, node, e, A, s, d1, d2, pred;
-  int64_t cur, prd, cs1, cs2, cs, ms1, ms2, ms, ts1, ts2, ts;
-  int64_t dgi, dgh, dx, dh, dtmp, dtmp2, dz, dnode, dA, dpred, ds, total;
-  __host__ __device__ HL(int T_) : T(T_) {
+constexpr int HT = 512;  // threads of the per-clip sequential kernels
+constexpr int G3 = 3 * GH;
+constexpr int WHH_LD = GH + 4;  // padded LDS row of W_hh (conflict-free ds_read_b128 over rows)
+
+// ------------------------------------------------------------------ per-row arrays (global, all clips)
+struct RowLayout {
+  int64_t R;
+  int64_t box, x, rh1, rh2, gi, r, z, n, ghn, hp, dgi, dgh, dp4, dp2, dp0, total;
+  __host__ __device__ explicit RowLayout(int64_t R_) : R(R_) {
     int64_t o = 0;
-    auto take = [&](int64_t n_) { int64_t r_ = o; o += (n_ + 3) & ~3ll; return r_; };
-    const int64_t TN = (int64_t)T * NMAX;
-    boxes = take(TN * 4); x = take(TN * GIN); rh1 = take(TN * 32); rh2 = take(TN * 64);
-    gi = take(TN * 3 * GH); ghn = take(TN * GH); r = take(TN * GH); z = take(TN * GH); n = take(TN * GH);
-    hp = take(TN * GH); hT = take(NMAX * GH); enc = take(NMAX * 32); ce1 = take(NMAX * 32); ce2 = take(NMAX * 32);
-    mu = take(NMAX * NF_); lv = take(NMAX * NF_); zz = take(NMAX * NF_); node = take(NMAX * 32);
-    e = take(NMAX * NMAX * 32); A = take(36); s = take(NMAX * NF_); d1 = take(NMAX * 32); d2 = take(NMAX * 32);
-    pred = take(NMAX * NF_); cur = take(8); prd = take(8); cs1 = take(64); cs2 = take(32); cs = take(4);
-    ms1 = take(32); ms2 = take(16); ms = take(4); ts1 = take(32); ts2 = take(16); ts = take(4);
-    dgi = take(TN * 3 * GH); dgh = take(TN * 3 * GH); dx = take(TN * GIN); dh = take(NMAX * GH);
-    dtmp = take(TN * 64 > 1024 ? TN * 64 : 1024); dtmp2 = take(TN * 64 > 512 ? TN * 64 : 512); dz = take(NMAX * NF_); dnode = take(NMAX * 32); dA = take(36);
-    dpred = take(NMAX * NF_); ds = take(NMAX * NF_);
+    auto take = [&](int64_t w) { int64_t r_ = o; o += (R * w + 63) & ~63ll; return r_; };
+    box = take(4); x = take(GIN); rh1 = take(32); rh2 = take(64); gi = take(G3);
+    r = take(GH); z = take(GH); n = take(GH); ghn = take(GH); hp = take(GH);
+    dgi = take(G3); dgh = take(G3); dp4 = take(64); dp2 = take(64); dp0 = take(32);
     total = o;
   }
 };
 
-int64_t head_ws_floats(int T) { return HL(T).total; }
+int64_t head_rows_floats(int B, int T) { return RowLayout((int64_t)B * T * NMAX).total; }
+
+// ------------------------------------------------------------------ per-clip small workspace
+struct HL {
+  int64_t hT, enc, ce1, ce2, mu, lv, zz, node, e, A, s, d1, d2, pred, cur, prd, cin, cs1, cs2, cs, ms1, ms2, ms, ts1,
+      ts2, ts, dh, dhn, scratch, dz, dnode, dA, dpred, ds, total;
+  __host__ __device__ HL() {
+    int64_t o = 0;
+    auto take = [&](int64_t n_) { int64_t r_ = o; o += (n_ + 3) & ~3ll; return r_; };
+    hT = take(NMAX * GH); enc = take(NMAX * 32); ce1 = take(NMAX * 32); ce2 = take(NMAX * 32);
+    mu = take(NMAX * NF_); lv = take(NMAX * NF_); zz = take(NMAX * NF_); node = take(NMAX * 32);
+    e = take(NMAX * NMAX * 32); A = take(36); s = take(NMAX * NF_); d1 = take(NMAX * 32); d2 = take(NMAX * 32);
+    pred = take(NMAX * NF_); cur = take(8); prd = take(8); cin = take(20); cs1 = take(64); cs2 = take(32);
+    cs = take(4); ms1 = take(32); ms2 = take(16); ms = take(4); ts1 = take(32); ts2 = take(16); ts = take(4);
+    dh = take(NMAX * GH); dhn = take(NMAX * GH); scratch = take(1024); dz = take(NMAX * NF_);
+    dnode = take(NMAX * 32); dA = take(36); dpred = take(NMAX * NF_); ds = take(NMAX * NF_);
+    total = o;
+  }
+};
+
+int64_t head_ws_floats(int T) {
+  (void)T;
+  return HL().total;
+}
 int64_t head_iws_ints(int T) { return (int64_t)T * (1 + NMAX) + 8; }
 
 // ------------------------------------------------------------------ block-wide small dense layers
-// out[r][o] = act(b[o] + sum_i W[o][i] * in[r][i])
 __device__ void lin_fwd(const float* in, int ldi, int R, int I, const float* __restrict__ W,
                         const float* __restrict__ b, int O, float* out, int ldo, bool relu) {
   for (int idx = threadIdx.x; idx < R * O; idx += blockDim.x) {
@@ -50,8 +72,7 @@ __device__ void lin_fwd(const float* in, int ldi, int R, int I, const float* __r
   __syncthreads();
 }
 
-// given dpre[r][o]: dW[o][i] += sum_r dpre[r][o] in[r][i]; db[o] += sum_r dpre[r][o];
-// din[r][i] (=, or += when acc) = sum_o W[o][i] dpre[r][o]
+// dW[o][i] += sum_r dpre[r][o] in[r][i]; db[o] += sum_r dpre[r][o]; din[r][i] (=|+=) sum_o W[o][i] dpre[r][o]
 __device__ void lin_bwd(const float* dpre, int ldd, const float* in, int ldi, int R, int I,
                         const float* __restrict__ W, int O, float* dW, float* db, float* din, int lddin, bool acc) {
   for (int idx = threadIdx.x; idx < O * I; idx += blockDim.x) {
@@ -79,7 +100,6 @@ __device__ void lin_bwd(const float* dpre, int ldd, const float* in, int ldi, in
   __syncthreads();
 }
 
-// relu gate in place: d[r][o] *= (out[r][o] > 0) * scale
 __device__ void relu_gate(float* d, int ldd, const float* out, int ldo, int R, int O, float scale) {
   for (int idx = threadIdx.x; idx < R * O; idx += blockDim.x) {
     const int r = idx / O, o = idx - r * O;
@@ -90,47 +110,136 @@ __device__ void relu_gate(float* d, int ldd, const float* out, int ldo, int R, i
 
 #define PW(slot) (a.pbase + a.off[slot])
 
-// ------------------------------------------------------------------ forward
-__global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, const float* __restrict__ logits, HeadOut o) {
-  const int b = blockIdx.x, T = a.T, tid = threadIdx.x;
-  const HL L(T);
-  float* w = a.ws + (int64_t)b * a.ws_stride;
+// ================================================================== forward
+__global__ __launch_bounds__(256) void head_rows_fwd_kernel(HeadArgs a, const float* __restrict__ logits, HeadOut o) {
+  const int f = blockIdx.x;  // frame b*T + t
+  const int b = f / a.T, t = f - b * a.T;
+  const int tid = threadIdx.x;
+  const RowLayout RL((int64_t)a.B * a.T * NMAX);
+  float* rows = a.rows;
   int* iw = a.iws + (int64_t)b * a.iws_stride;
-  int* cnt = iw;               // [T]
-  int* slot = iw + T;          // [T][5] original detection index of compacted row j (-1: fallback)
-  __shared__ int s_N, s_valid_any;
-  __shared__ float s_red[8];
-
-  // 1. box decode + range filter + fallback (cad:198-228)
-  if (tid < T) {
-    const int t = tid;
-    const float* lg = logits + ((int64_t)b * T + t) * 20;
-    float* bx = w + L.boxes + (int64_t)t * NMAX * 4;
+  __shared__ float sbox[NMAX][4];
+  __shared__ int svalid[NMAX];
+  __shared__ float sx[NMAX][GIN];
+  __shared__ float sh1[NMAX][32];
+  __shared__ float sh2[NMAX][64];
+  __shared__ int scnt;
+  if (tid < NMAX) {
+    const float* lg = logits + (int64_t)f * 20 + tid * 4;
+    const float X = sigmoidf_(lg[0]) * 360.f, Y = sigmoidf_(lg[1]) * 240.f;
+    const float Wd = sigmoidf_(lg[2]) * 80.f + 15.f, Hh = sigmoidf_(lg[3]) * 120.f + 25.f;
+    sbox[tid][0] = X; sbox[tid][1] = Y; sbox[tid][2] = Wd; sbox[tid][3] = Hh;
+    svalid[tid] = (X >= 10.f && X <= 350.f && Y >= 10.f && Y <= 230.f && Wd >= 10.f && Wd <= 100.f && Hh >= 20.f &&
+                   Hh <= 150.f) ? 1 : 0;
+  }
+  __syncthreads();
+  if (tid == 0) {
     int c = 0;
-    for (int k = 0; k < NMAX; ++k) {
-      const float X = sigmoidf_(lg[k * 4 + 0]) * 360.f;
-      const float Y = sigmoidf_(lg[k * 4 + 1]) * 240.f;
-      const float Wd = sigmoidf_(lg[k * 4 + 2]) * 80.f + 15.f;
-      const float Hh = sigmoidf_(lg[k * 4 + 3]) * 120.f + 25.f;
-      if (X >= 10.f && X <= 350.f && Y >= 10.f && Y <= 230.f && Wd >= 10.f && Wd <= 100.f && Hh >= 20.f &&
-          Hh <= 150.f) {
-        bx[c * 4 + 0] = X; bx[c * 4 + 1] = Y; bx[c * 4 + 2] = Wd; bx[c * 4 + 3] = Hh;
-        slot[t * NMAX + c] = k;
-        ++c;
+    int* slot = iw + a.T + t * NMAX;
+    float cb[NMAX][4];
+    for (int k = 0; k < NMAX; ++k)
+      if (svalid[k]) {
+        for (int q = 0; q < 4; ++q) cb[c][q] = sbox[k][q];
+        slot[c++] = k;
       }
-    }
     if (c == 0) {
-      bx[0] = 180.f; bx[1] = 120.f; bx[2] = 30.f; bx[3] = 60.f;
-      slot[t * NMAX] = -1;
+      cb[0][0] = 180.f; cb[0][1] = 120.f; cb[0][2] = 30.f; cb[0][3] = 60.f;  // fallback (cad:225)
+      slot[0] = -1;
       c = 1;
     }
     for (int j = c; j < NMAX; ++j) {
-      bx[j * 4 + 0] = bx[j * 4 + 1] = bx[j * 4 + 2] = bx[j * 4 + 3] = 0.f;
-      slot[t * NMAX + j] = -2;
+      for (int q = 0; q < 4; ++q) cb[j][q] = 0.f;
+      slot[j] = -2;
     }
-    cnt[t] = c;
+    for (int j = 0; j < NMAX; ++j)
+      for (int q = 0; q < 4; ++q) sbox[j][q] = cb[j][q];
+    iw[t] = c;
+    o.counts[f] = c;
+    scnt = c;
   }
   __syncthreads();
+  const int cnt = scnt;
+  const int64_t r0 = (int64_t)f * NMAX;
+  if (tid < NMAX * 4) {
+    const int j = tid / 4, q = tid % 4;
+    rows[RL.box + (r0 + j) * 4 + q] = sbox[j][q];
+    o.boxes[(int64_t)f * NMAX * 4 + tid] = sbox[j][q];
+  }
+  // ReID MLP 4 -> 32 -> 64 -> 64 on real rows (zeros elsewhere)
+  const float* W0 = PW(H_REID0_W);
+  const float* B0 = PW(H_REID0_B);
+  for (int idx = tid; idx < NMAX * 32; idx += 256) {
+    const int j = idx / 32, u = idx % 32;
+    float v = 0.f;
+    if (j < cnt) {
+      v = B0[u];
+      for (int q = 0; q < 4; ++q) v = fmaf(W0[u * 4 + q], sbox[j][q], v);
+      v = fmaxf(v, 0.f);
+    }
+    sh1[j][u] = v;
+    rows[RL.rh1 + (r0 + j) * 32 + u] = v;
+  }
+  __syncthreads();
+  const float* W2 = PW(H_REID2_W);
+  const float* B2 = PW(H_REID2_B);
+  for (int idx = tid; idx < NMAX * 64; idx += 256) {
+    const int j = idx / 64, u = idx % 64;
+    float v = 0.f;
+    if (j < cnt) {
+      v = B2[u];
+      for (int q = 0; q < 32; ++q) v = fmaf(W2[u * 32 + q], sh1[j][q], v);
+      v = fmaxf(v, 0.f);
+    }
+    sh2[j][u] = v;
+    rows[RL.rh2 + (r0 + j) * 64 + u] = v;
+  }
+  __syncthreads();
+  const float* W4 = PW(H_REID4_W);
+  const float* B4 = PW(H_REID4_B);
+  for (int idx = tid; idx < NMAX * GIN; idx += 256) {
+    const int j = idx / GIN, i = idx % GIN;
+    float v = 0.f;
+    if (j < cnt) {
+      if (i < 4) v = sbox[j][i];
+      else {
+        const int u = i - 4;
+        v = B4[u];
+        for (int q = 0; q < 64; ++q) v = fmaf(W4[u * 64 + q], sh2[j][q], v);
+      }
+    }
+    sx[j][i] = v;
+    rows[RL.x + (r0 + j) * GIN + i] = v;
+  }
+  __syncthreads();
+  // GRU input projection for all 5 rows (padded rows see x = 0)
+  const float* Wih = PW(H_GRU_WIH);
+  const float* bih = PW(H_GRU_BIH);
+  for (int idx = tid; idx < NMAX * G3; idx += 256) {
+    const int j = idx / G3, q = idx % G3;
+    float v = bih[q];
+    const float* wr = Wih + (int64_t)q * GIN;
+    for (int i = 0; i < GIN; ++i) v = fmaf(wr[i], sx[j][i], v);
+    rows[RL.gi + (r0 + j) * G3 + q] = v;
+  }
+}
+
+__global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o) {
+  const int b = blockIdx.x, T = a.T, tid = threadIdx.x;
+  const HL L;
+  const RowLayout RL((int64_t)a.B * T * NMAX);
+  float* rows = a.rows;
+  float* w = a.ws + (int64_t)b * a.ws_stride;
+  const int* iw = a.iws + (int64_t)b * a.iws_stride;
+  const int* cnt = iw;
+  const int* slot = iw + T;
+  __shared__ __attribute__((aligned(16))) float whh[G3 * WHH_LD];
+  __shared__ float hs[NMAX * GH];
+  __shared__ float ghs[NMAX * G3];
+  __shared__ int s_N, s_any;
+  __shared__ float s_red[4];
+  const float* Whh = PW(H_GRU_WHH);
+  for (int i = tid; i < G3 * GH; i += HT) whh[(i / GH) * WHH_LD + (i % GH)] = Whh[i];
+  for (int i = tid; i < NMAX * GH; i += HT) hs[i] = 0.f;
   if (tid == 0) {
     int N = 1, any = 0;
     for (int t = 0; t < T; ++t) {
@@ -138,68 +247,59 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, const float* 
       if (slot[t * NMAX] >= 0) any = 1;
     }
     s_N = N;
-    s_valid_any = any;
+    s_any = any;
   }
   __syncthreads();
   const int N = s_N;
-  // export detections
-  for (int i = tid; i < T * NMAX * 4; i += 256) o.boxes[(int64_t)b * T * NMAX * 4 + i] = w[L.boxes + i];
-  for (int t = tid; t < T; t += 256) o.counts[(int64_t)b * T + t] = cnt[t];
-
-  // 2. ReID MLP on every real row; trajectory rows x[t][j] = [box, reid] or zeros (cad:248-274)
-  //    rows are laid out [t][j] with j < NMAX; rows j >= cnt[t] are zero padding.
-  const int TN = T * NMAX;
-  lin_fwd(w + L.boxes, 4, TN, 4, PW(H_REID0_W), PW(H_REID0_B), 32, w + L.rh1, 32, true);
-  lin_fwd(w + L.rh1, 32, TN, 32, PW(H_REID2_W), PW(H_REID2_B), 64, w + L.rh2, 64, true);
-  lin_fwd(w + L.rh2, 64, TN, 64, PW(H_REID4_W), PW(H_REID4_B), 64, w + L.x + 4, GIN, false);
-  for (int idx = tid; idx < TN * GIN; idx += 256) {
-    const int row = idx / GIN, col = idx - row * GIN;
-    const int t = row / NMAX, j = row - t * NMAX;
-    float* xr = w + L.x + (int64_t)row * GIN;
-    if (j >= cnt[t]) xr[col] = 0.f;
-    else if (col < 4) xr[col] = w[L.boxes + (int64_t)row * 4 + col];
-  }
-  __syncthreads();
-
-  // 3. GRU input projections for all steps, then the recurrence (cad:284,298; gate order r,z,n)
-  lin_fwd(w + L.x, GIN, TN, GIN, PW(H_GRU_WIH), PW(H_GRU_BIH), 3 * GH, w + L.gi, 3 * GH, false);
-  float* h = w + L.hT;  // running hidden state, final value = h_T
-  for (int i = tid; i < NMAX * GH; i += 256) h[i] = 0.f;
-  __syncthreads();
-  const float* Whh = PW(H_GRU_WHH);
   const float* bhh = PW(H_GRU_BHH);
-  float* ghs = w + L.dtmp;  // scratch [N][192]
+  // GRU recurrence, gate order (r, z, n) (cad:284,298)
   for (int t = 0; t < T; ++t) {
-    for (int idx = tid; idx < N * 3 * GH; idx += 256) {
-      const int nn = idx / (3 * GH), g = idx - nn * 3 * GH;
-      float s = bhh[g];
-      const float* wr = Whh + (int64_t)g * GH;
-      const float* hv = h + nn * GH;
-      for (int j = 0; j < GH; ++j) s = fmaf(wr[j], hv[j], s);
+    for (int idx = tid; idx < N * G3; idx += HT) {
+      const int nn = idx / G3, q = idx - nn * G3;
+      const f32x4* wr = reinterpret_cast<const f32x4*>(whh + q * WHH_LD);
+      const float* hv = hs + nn * GH;
+      float s = bhh[q];
+#pragma unroll
+      for (int k = 0; k < GH / 4; ++k) {
+        const f32x4 wv = wr[k];
+        s = fmaf(wv[0], hv[4 * k], s);
+        s = fmaf(wv[1], hv[4 * k + 1], s);
+        s = fmaf(wv[2], hv[4 * k + 2], s);
+        s = fmaf(wv[3], hv[4 * k + 3], s);
+      }
       ghs[idx] = s;
     }
     __syncthreads();
-    for (int idx = tid; idx < N * GH; idx += 256) {
+    for (int idx = tid; idx < NMAX * GH; idx += HT) {
       const int nn = idx / GH, u = idx - nn * GH;
-      const int64_t row = (int64_t)t * NMAX + nn;
-      const float* gi = w + L.gi + row * 3 * GH;
-      const float* gh = ghs + nn * 3 * GH;
-      const float r = sigmoidf_(gi[u] + gh[u]);
-      const float z = sigmoidf_(gi[GH + u] + gh[GH + u]);
-      const float nv = tanhf(gi[2 * GH + u] + r * gh[2 * GH + u]);
-      const float hprev = h[idx];
-      w[L.r + row * GH + u] = r;
-      w[L.z + row * GH + u] = z;
-      w[L.n + row * GH + u] = nv;
-      w[L.ghn + row * GH + u] = gh[2 * GH + u];
-      w[L.hp + row * GH + u] = hprev;
-      h[idx] = (1.f - z) * nv + z * hprev;
+      const int64_t row = ((int64_t)b * T + t) * NMAX + nn;
+      if (nn < N) {
+        const float* gi = rows + RL.gi + row * G3;
+        const float* gh = ghs + nn * G3;
+        const float r = sigmoidf_(gi[u] + gh[u]);
+        const float z = sigmoidf_(gi[GH + u] + gh[GH + u]);
+        const float nv = tanhf(gi[2 * GH + u] + r * gh[2 * GH + u]);
+        const float hprev = hs[idx];
+        rows[RL.r + row * GH + u] = r;
+        rows[RL.z + row * GH + u] = z;
+        rows[RL.n + row * GH + u] = nv;
+        rows[RL.ghn + row * GH + u] = gh[2 * GH + u];
+        rows[RL.hp + row * GH + u] = hprev;
+        hs[idx] = (1.f - z) * nv + z * hprev;
+      } else {  // trajectory slots that do not exist in this clip
+        rows[RL.r + row * GH + u] = 0.f;
+        rows[RL.z + row * GH + u] = 0.f;
+        rows[RL.n + row * GH + u] = 0.f;
+        rows[RL.ghn + row * GH + u] = 0.f;
+        rows[RL.hp + row * GH + u] = 0.f;
+      }
     }
     __syncthreads();
   }
-
-  // 4. encoder + VAE (cad:299, 333-352)
-  lin_fwd(h, GH, N, GH, PW(H_ENC_W), PW(H_ENC_B), 32, w + L.enc, 32, false);
+  for (int i = tid; i < NMAX * GH; i += HT) w[L.hT + i] = hs[i];
+  __syncthreads();
+  // encoder + VAE (cad:299, 333-352)
+  lin_fwd(w + L.hT, GH, N, GH, PW(H_ENC_W), PW(H_ENC_B), 32, w + L.enc, 32, false);
   lin_fwd(w + L.enc, 32, N, 32, PW(H_CE0_W), PW(H_CE0_B), 32, w + L.ce1, 32, true);
   lin_fwd(w + L.ce1, 32, N, 32, PW(H_CE2_W), PW(H_CE2_B), 32, w + L.ce2, 32, true);
   lin_fwd(w + L.ce2, 32, N, 32, PW(H_MU_W), PW(H_MU_B), NF_, w + L.mu, NF_, false);
@@ -207,8 +307,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, const float* 
   if (tid < N * NF_) {
     const int nn = tid / NF_, f = tid - nn * NF_;
     const float eps = rng_normal(a.h1_eps, (uint64_t)(a.clip0 + b), (uint64_t)(nn * NF_ + f));
-    const float mu = w[L.mu + tid], lv = w[L.lv + tid];
-    w[L.zz + tid] = mu + eps * expf(0.5f * lv);
+    w[L.zz + tid] = w[L.mu + tid] + eps * expf(0.5f * w[L.lv + tid]);
   }
   __syncthreads();
   if (tid < 64) {
@@ -224,22 +323,20 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, const float* 
     s = wave_sum(s);
     if (tid == 0) s_red[0] = s / (float)N;
   }
-  // 5. structure learner (cad:371-398): node encoder + pairwise edge MLP for i != j < min(N,6)
+  // structure learner (cad:371-398)
   lin_fwd(w + L.zz, NF_, N, NF_, PW(H_NODE_W), PW(H_NODE_B), 32, w + L.node, 32, false);
   const int m = min(N, NF_);
   {
     const float* W0 = PW(H_EDGE0_W);
     const float* b0 = PW(H_EDGE0_B);
-    for (int idx = tid; idx < m * m * 32; idx += 256) {
+    for (int idx = tid; idx < m * m * 32; idx += HT) {
       const int pr = idx / 32, u = idx - pr * 32;
       const int i = pr / m, j = pr - i * m;
       if (i == j) continue;
       float s = b0[u];
       const float* wr = W0 + u * 64;
-      const float* ni = w + L.node + i * 32;
-      const float* nj = w + L.node + j * 32;
-      for (int q = 0; q < 32; ++q) s = fmaf(wr[q], ni[q], s);
-      for (int q = 0; q < 32; ++q) s = fmaf(wr[32 + q], nj[q], s);
+      for (int q = 0; q < 32; ++q) s = fmaf(wr[q], w[L.node + i * 32 + q], s);
+      for (int q = 0; q < 32; ++q) s = fmaf(wr[32 + q], w[L.node + j * 32 + q], s);
       w[L.e + (int64_t)(i * NMAX + j) * 32 + u] = fmaxf(s, 0.f);
     }
     __syncthreads();
@@ -249,15 +346,14 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, const float* 
       if (i != j && i < m && j < m) {
         const float* W2 = PW(H_EDGE2_W);
         float s = PW(H_EDGE2_B)[0];
-        const float* ev = w + L.e + (int64_t)(i * NMAX + j) * 32;
-        for (int q = 0; q < 32; ++q) s = fmaf(W2[q], ev[q], s);
+        for (int q = 0; q < 32; ++q) s = fmaf(W2[q], w[L.e + (int64_t)(i * NMAX + j) * 32 + q], s);
         v = sigmoidf_(s);
       }
       w[L.A + tid] = v;
     }
     __syncthreads();
   }
-  // 6. dynamics (cad:415-426): s[n][i] = sum_j A[i][j] z[n][j]
+  // dynamics (cad:415-426): s[n][i] = sum_j A[i][j] z[n][j]
   if (tid < N * NF_) {
     const int nn = tid / NF_, i = tid - nn * NF_;
     float s = 0.f;
@@ -268,8 +364,8 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, const float* 
   lin_fwd(w + L.s, NF_, N, NF_, PW(H_DYN0_W), PW(H_DYN0_B), 32, w + L.d1, 32, true);
   lin_fwd(w + L.d1, 32, N, 32, PW(H_DYN2_W), PW(H_DYN2_B), 32, w + L.d2, 32, true);
   lin_fwd(w + L.d2, 32, N, 32, PW(H_DYN4_W), PW(H_DYN4_B), NF_, w + L.pred, NF_, false);
-  // 7. scorer (cad:463-502)
-  float* cin = w + L.dtmp2;  // [cur(6) prd(6) diff(6)]
+  // scorer (cad:463-502)
+  float* cin = w + L.cin;
   if (tid < NF_) {
     float c = 0.f, p = 0.f;
     for (int nn = 0; nn < N; ++nn) {
@@ -305,48 +401,49 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, const float* 
     o.causal[b] = 0.5f * cs + 0.3f * ms + 0.2f * ts;
     o.kl[b] = s_red[0];
     o.nmax[b] = N;
-    o.clip_flags[b * 2 + 0] = s_valid_any;
+    o.clip_flags[b * 2 + 0] = s_any;
     o.clip_flags[b * 2 + 1] = m >= 2 ? 1 : 0;
   }
-  for (int i = tid; i < NMAX * NF_; i += 256) o.z[(int64_t)b * NMAX * NF_ + i] = (i < N * NF_) ? w[L.zz + i] : 0.f;
-  for (int i = tid; i < 36; i += 256) o.adj[(int64_t)b * 36 + i] = w[L.A + i];
+  for (int i = tid; i < NMAX * NF_; i += HT) o.z[(int64_t)b * NMAX * NF_ + i] = (i < N * NF_) ? w[L.zz + i] : 0.f;
+  for (int i = tid; i < 36; i += HT) o.adj[(int64_t)b * 36 + i] = w[L.A + i];
 }
 
 int head_fwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, hipStream_t st) {
-  VAD_CHECK(a.T <= 256, "head: T must be <= 256");
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(a.B), dim3(256), 0, st, a, det_logits, o);
+  VAD_CHECK(a.T <= 4096, "head: T too large");
+  hipLaunchKernelGGL(head_rows_fwd_kernel, dim3(a.B * a.T), dim3(256), 0, st, a, det_logits, o);
+  VAD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(head_seq_fwd_kernel, dim3(a.B), dim3(HT), 0, st, a, o);
   VAD_LAUNCH_CHECK();
   return 0;
 }
 
-// ------------------------------------------------------------------ backward
+// ================================================================== backward
 #define GW(slot) (g + (a.off[slot] - a.head_begin))
 
-__global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a, const float* __restrict__ logits, HeadOut o,
-                                                       HeadUp up, float* slabs, int64_t slab_len,
-                                                       float* __restrict__ dlog) {
+__global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o, HeadUp up, float* slabs,
+                                                          int64_t slab_len) {
   const int b = blockIdx.x, T = a.T, tid = threadIdx.x;
-  const HL L(T);
+  const HL L;
+  const RowLayout RL((int64_t)a.B * T * NMAX);
+  float* rows = a.rows;
   float* w = a.ws + (int64_t)b * a.ws_stride;
-  const int* iw = a.iws + (int64_t)b * a.iws_stride;
-  const int* cnt = iw;
-  const int* slot = iw + T;
   float* g = slabs + (int64_t)b * slab_len;
-  for (int64_t i = tid; i < slab_len; i += 256) g[i] = 0.f;
+  __shared__ __attribute__((aligned(16))) float whh[G3 * GH];  // [q][j], read by columns (conflict-free)
+  __shared__ float dgh_s[NMAX * G3];
+  const float* Whh = PW(H_GRU_WHH);
+  for (int i = tid; i < G3 * GH; i += HT) whh[i] = Whh[i];
+  for (int64_t i = tid; i < slab_len; i += HT) g[i] = 0.f;
   const int N = o.nmax[b];
   const int m = min(N, NF_);
   const float dscore = up.d_causal[b];
   const float dkl = up.d_kl[b];
+  float* cin = w + L.cin;
+  float* d1 = w + L.scratch;  // 1024-float scratch
+  float* dcin = w + L.scratch + 960;
+  for (int i = tid; i < 18; i += HT) dcin[i] = 0.f;
   __syncthreads();
-
   // ---- scorer (cad:485-497)
-  float* dcin = w + L.dtmp2 + 32;  // [18]
-  float* cin = w + L.dtmp2;
-  float* d1 = w + L.dtmp;          // scratch rows
-  for (int i = tid; i < 18; i += 256) dcin[i] = 0.f;
-  __syncthreads();
   {
-    // causal scorer: sigmoid -> L5 <- relu L3 <- dropout relu L0
     const float cs = w[L.cs + 1], ms = w[L.ms + 1], ts = w[L.ts + 1];
     if (tid == 0) {
       d1[0] = 0.5f * dscore * cs * (1.f - cs);
@@ -354,35 +451,34 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a, const float* 
       d1[2] = 0.2f * dscore * ts * (1.f - ts);
     }
     __syncthreads();
-    float* dcs2 = d1 + 8;   // [32]
-    float* dcs1 = d1 + 40;  // [64]
+    float* dcs2 = d1 + 8;
+    float* dcs1 = d1 + 40;
     lin_bwd(d1 + 0, 1, w + L.cs2, 32, 1, 32, PW(H_CS5_W), 1, GW(H_CS5_W), GW(H_CS5_B), dcs2, 32, false);
     relu_gate(dcs2, 32, w + L.cs2, 32, 1, 32, 1.f);
     lin_bwd(dcs2, 32, w + L.cs1, 64, 1, 64, PW(H_CS3_W), 32, GW(H_CS3_W), GW(H_CS3_B), dcs1, 64, false);
     relu_gate(dcs1, 64, w + L.cs1, 64, 1, 64, a.training ? 1.f / 0.8f : 1.f);
     lin_bwd(dcs1, 64, cin, 18, 1, 18, PW(H_CS0_W), 64, GW(H_CS0_W), GW(H_CS0_B), dcin, 18, true);
-    float* dms2 = d1 + 104;  // [16]
-    float* dms1 = d1 + 120;  // [32]
+    float* dms2 = d1 + 104;
+    float* dms1 = d1 + 120;
     lin_bwd(d1 + 1, 1, w + L.ms2, 16, 1, 16, PW(H_MS4_W), 1, GW(H_MS4_W), GW(H_MS4_B), dms2, 16, false);
     relu_gate(dms2, 16, w + L.ms2, 16, 1, 16, 1.f);
     lin_bwd(dms2, 16, w + L.ms1, 32, 1, 32, PW(H_MS2_W), 16, GW(H_MS2_W), GW(H_MS2_B), dms1, 32, false);
     relu_gate(dms1, 32, w + L.ms1, 32, 1, 32, 1.f);
     lin_bwd(dms1, 32, cin, 18, 1, 12, PW(H_MS0_W), 32, GW(H_MS0_W), GW(H_MS0_B), dcin, 18, true);
-    float* dts2 = d1 + 152;  // [16]
-    float* dts1 = d1 + 168;  // [32]
+    float* dts2 = d1 + 152;
+    float* dts1 = d1 + 168;
     lin_bwd(d1 + 2, 1, w + L.ts2, 16, 1, 16, PW(H_TS4_W), 1, GW(H_TS4_W), GW(H_TS4_B), dts2, 16, false);
     relu_gate(dts2, 16, w + L.ts2, 16, 1, 16, 1.f);
     lin_bwd(dts2, 16, w + L.ts1, 32, 1, 32, PW(H_TS2_W), 16, GW(H_TS2_W), GW(H_TS2_B), dts1, 32, false);
     relu_gate(dts1, 32, w + L.ts1, 32, 1, 32, 1.f);
     lin_bwd(dts1, 32, cin, 18, 1, 6, PW(H_TS0_W), 32, GW(H_TS0_W), GW(H_TS0_B), dcin, 18, true);
   }
-  // d cur / d prd including |cur - prd| (sign(0) = 0), then the means over N
   float* dz = w + L.dz;
   float* dpred = w + L.dpred;
   if (tid < NMAX * NF_) {
     const int nn = tid / NF_, f = tid - nn * NF_;
     const float c = w[L.cur + f], p = w[L.prd + f];
-    const float sg = c > p ? 1.f : (c < p ? -1.f : 0.f);
+    const float sg = c > p ? 1.f : (c < p ? -1.f : 0.f);  // d|c-p| (sign(0) = 0)
     const float dc = dcin[f] + dcin[12 + f] * sg;
     const float dp = dcin[6 + f] - dcin[12 + f] * sg;
     const bool live = nn < N;
@@ -390,11 +486,10 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a, const float* 
     dpred[tid] = live ? dp / (float)N : 0.f;
   }
   __syncthreads();
-
-  // ---- dynamics MLP backward -> d s
+  // ---- dynamics
   float* ds = w + L.ds;
   {
-    float* dd2 = d1;            // [N][32]
+    float* dd2 = d1;
     float* dd1 = d1 + NMAX * 32;
     lin_bwd(dpred, NF_, w + L.d2, 32, N, 32, PW(H_DYN4_W), NF_, GW(H_DYN4_W), GW(H_DYN4_B), dd2, 32, false);
     relu_gate(dd2, 32, w + L.d2, 32, N, 32, 1.f);
@@ -402,7 +497,6 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a, const float* 
     relu_gate(dd1, 32, w + L.d1, 32, N, 32, 1.f);
     lin_bwd(dd1, 32, w + L.s, NF_, N, NF_, PW(H_DYN0_W), 32, GW(H_DYN0_W), GW(H_DYN0_B), ds, NF_, false);
   }
-  // s = (A z^T)^T: dA[i][j] = sum_n ds[n][i] z[n][j] (+ external), dz[n][j] += sum_i A[i][j] ds[n][i]
   float* dA = w + L.dA;
   if (tid < 36) {
     const int i = tid / 6, j = tid - i * 6;
@@ -417,15 +511,13 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a, const float* 
     dz[q] += s;
   }
   __syncthreads();
-  // ---- structure learner backward (only when edges exist)
+  // ---- structure learner (only when edges exist)
   if (m >= 2) {
     float* dnode = w + L.dnode;
-    for (int i = tid; i < NMAX * 32; i += 256) dnode[i] = 0.f;
-    float* de = d1;  // [pairs][32] pre-activation grads
-    float* dW2 = GW(H_EDGE2_W);
-    __syncthreads();
+    for (int i = tid; i < NMAX * 32; i += HT) dnode[i] = 0.f;
+    float* de = d1;  // [pairs][32]
     const float* W2 = PW(H_EDGE2_W);
-    for (int idx = tid; idx < m * m * 32; idx += 256) {
+    for (int idx = tid; idx < m * m * 32; idx += HT) {
       const int pr = idx / 32, u = idx - pr * 32;
       const int i = pr / m, j = pr - i * m;
       float v = 0.f;
@@ -438,7 +530,6 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a, const float* 
       de[idx] = v;
     }
     __syncthreads();
-    // edge2 weight/bias grads
     if (tid < 33) {
       float s = 0.f;
       for (int i = 0; i < m; ++i)
@@ -448,12 +539,11 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a, const float* 
           const float da = dA[i * 6 + j] * Aij * (1.f - Aij);
           s += tid < 32 ? da * w[L.e + (int64_t)(i * NMAX + j) * 32 + tid] : da;
         }
-      if (tid < 32) dW2[tid] += s;
+      if (tid < 32) GW(H_EDGE2_W)[tid] += s;
       else GW(H_EDGE2_B)[0] += s;
     }
-    // edge0: input [node_i, node_j] (64)
     float* dW0 = GW(H_EDGE0_W);
-    for (int idx = tid; idx < 32 * 64; idx += 256) {
+    for (int idx = tid; idx < 32 * 64; idx += HT) {
       const int u = idx / 64, q = idx - u * 64;
       float s = 0.f;
       for (int i = 0; i < m; ++i)
@@ -470,7 +560,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a, const float* 
       GW(H_EDGE0_B)[tid] += s;
     }
     const float* W0 = PW(H_EDGE0_W);
-    for (int idx = tid; idx < m * 32; idx += 256) {
+    for (int idx = tid; idx < m * 32; idx += HT) {
       const int k = idx / 32, q = idx - k * 32;
       float s = 0.f;
       for (int j = 0; j < m; ++j) {
@@ -485,10 +575,10 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a, const float* 
     __syncthreads();
     lin_bwd(dnode, 32, w + L.zz, NF_, N, NF_, PW(H_NODE_W), 32, GW(H_NODE_W), GW(H_NODE_B), dz, NF_, true);
   }
-  // ---- VAE + KL backward (cad:328-347)
+  // ---- VAE + KL (cad:328-347)
   {
     float* dmu = d1;
-    float* dlv = d1 + NMAX * NF_;
+    float* dlv = d1 + 32;
     if (tid < N * NF_) {
       const int nn = tid / NF_, f = tid - nn * NF_;
       const float eps = rng_normal(a.h1_eps, (uint64_t)(a.clip0 + b), (uint64_t)(nn * NF_ + f));
@@ -499,139 +589,174 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a, const float* 
       dlv[tid] = dzz * eps * 0.5f * expf(0.5f * lv) + kls * 0.5f * (expf(lv) - 1.f);
     }
     __syncthreads();
-    float* dce2 = d1 + 64;   // [N][32]
-    float* dce1 = d1 + 256;  // [N][32]
+    float* dce2 = d1 + 64;
+    float* dce1 = d1 + 256;
     lin_bwd(dmu, NF_, w + L.ce2, 32, N, 32, PW(H_MU_W), NF_, GW(H_MU_W), GW(H_MU_B), dce2, 32, false);
     lin_bwd(dlv, NF_, w + L.ce2, 32, N, 32, PW(H_LV_W), NF_, GW(H_LV_W), GW(H_LV_B), dce2, 32, true);
     relu_gate(dce2, 32, w + L.ce2, 32, N, 32, 1.f);
     lin_bwd(dce2, 32, w + L.ce1, 32, N, 32, PW(H_CE2_W), 32, GW(H_CE2_W), GW(H_CE2_B), dce1, 32, false);
     relu_gate(dce1, 32, w + L.ce1, 32, N, 32, 1.f);
-    float* denc = d1 + 448;  // [N][32]
+    float* denc = d1 + 448;
     lin_bwd(dce1, 32, w + L.enc, 32, N, 32, PW(H_CE0_W), 32, GW(H_CE0_W), GW(H_CE0_B), denc, 32, false);
-    // encoder: enc = We h_T + be
     lin_bwd(denc, 32, w + L.hT, GH, N, GH, PW(H_ENC_W), 32, GW(H_ENC_W), GW(H_ENC_B), w + L.dh, GH, false);
   }
-  // ---- GRU backward through time
+  // ---- GRU backward through time (dh'/dz = h - n, dh'/dn = 1 - z)
   {
-    const float* Whh = PW(H_GRU_WHH);
     float* dh = w + L.dh;
-    float* dhn = w + L.dtmp2 + 64;  // [N][64] next dh
+    float* dhn = w + L.dhn;
     for (int t = T - 1; t >= 0; --t) {
-      for (int idx = tid; idx < N * GH; idx += 256) {
+      for (int idx = tid; idx < NMAX * GH; idx += HT) {
         const int nn = idx / GH, u = idx - nn * GH;
-        const int64_t row = (int64_t)t * NMAX + nn;
-        const float r = w[L.r + row * GH + u], z = w[L.z + row * GH + u], nv = w[L.n + row * GH + u];
-        const float hp = w[L.hp + row * GH + u], ghn = w[L.ghn + row * GH + u];
-        const float d = dh[idx];
-        const float dn = d * (1.f - z);
-        const float dzg = d * (hp - nv);  // dh'/dz = h - n
-        const float dan = dn * (1.f - nv * nv);
-        const float dr = dan * ghn;
-        const float daz = dzg * z * (1.f - z);
-        const float dar = dr * r * (1.f - r);
-        float* dgi = w + L.dgi + row * 3 * GH;
-        float* dgh = w + L.dgh + row * 3 * GH;
-        dgi[u] = dar; dgi[GH + u] = daz; dgi[2 * GH + u] = dan;
-        dgh[u] = dar; dgh[GH + u] = daz; dgh[2 * GH + u] = dan * r;
-        dhn[idx] = d * z;
+        const int64_t row = ((int64_t)b * T + t) * NMAX + nn;
+        float* dgi = rows + RL.dgi + row * G3;
+        float* dgh = rows + RL.dgh + row * G3;
+        if (nn < N) {
+          const float r = rows[RL.r + row * GH + u], z = rows[RL.z + row * GH + u];
+          const float nv = rows[RL.n + row * GH + u];
+          const float hp = rows[RL.hp + row * GH + u], ghn = rows[RL.ghn + row * GH + u];
+          const float d = dh[idx];
+          const float dan = d * (1.f - z) * (1.f - nv * nv);
+          const float daz = d * (hp - nv) * z * (1.f - z);
+          const float dar = dan * ghn * r * (1.f - r);
+          dgi[u] = dar; dgi[GH + u] = daz; dgi[2 * GH + u] = dan;
+          dgh[u] = dar; dgh[GH + u] = daz; dgh[2 * GH + u] = dan * r;
+          dgh_s[nn * G3 + u] = dar;
+          dgh_s[nn * G3 + GH + u] = daz;
+          dgh_s[nn * G3 + 2 * GH + u] = dan * r;
+          dhn[idx] = d * z;
+        } else {
+          dgi[u] = 0.f; dgi[GH + u] = 0.f; dgi[2 * GH + u] = 0.f;
+          dgh[u] = 0.f; dgh[GH + u] = 0.f; dgh[2 * GH + u] = 0.f;
+        }
       }
       __syncthreads();
-      for (int idx = tid; idx < N * GH; idx += 256) {
+      for (int idx = tid; idx < N * GH; idx += HT) {
         const int nn = idx / GH, j = idx - nn * GH;
-        const float* dgh = w + L.dgh + ((int64_t)t * NMAX + nn) * 3 * GH;
+        const float* dgv = dgh_s + nn * G3;
         float s = dhn[idx];
-        for (int q = 0; q < 3 * GH; ++q) s = fmaf(Whh[(int64_t)q * GH + j], dgh[q], s);
+        for (int q = 0; q < G3; ++q) s = fmaf(whh[q * GH + j], dgv[q], s);
         dh[idx] = s;
       }
       __syncthreads();
     }
-    // weight grads over all (t, n < N) rows; rows n >= N never ran
-    float* dWih = GW(H_GRU_WIH);
-    float* dWhh = GW(H_GRU_WHH);
-    for (int idx = tid; idx < 3 * GH * GIN; idx += 256) {
-      const int q = idx / GIN, i = idx - q * GIN;
-      float s = 0.f;
-      for (int t = 0; t < T; ++t)
-        for (int nn = 0; nn < N; ++nn) {
-          const int64_t row = (int64_t)t * NMAX + nn;
-          s = fmaf(w[L.dgi + row * 3 * GH + q], w[L.x + row * GIN + i], s);
-        }
-      dWih[idx] += s;
-    }
-    for (int idx = tid; idx < 3 * GH * GH; idx += 256) {
-      const int q = idx / GH, j = idx - q * GH;
-      float s = 0.f;
-      for (int t = 0; t < T; ++t)
-        for (int nn = 0; nn < N; ++nn) {
-          const int64_t row = (int64_t)t * NMAX + nn;
-          s = fmaf(w[L.dgh + row * 3 * GH + q], w[L.hp + row * GH + j], s);
-        }
-      dWhh[idx] += s;
-    }
-    for (int q = tid; q < 3 * GH; q += 256) {
-      float si = 0.f, sh = 0.f;
-      for (int t = 0; t < T; ++t)
-        for (int nn = 0; nn < N; ++nn) {
-          const int64_t row = (int64_t)t * NMAX + nn;
-          si += w[L.dgi + row * 3 * GH + q];
-          sh += w[L.dgh + row * 3 * GH + q];
-        }
-      GW(H_GRU_BIH)[q] += si;
-      GW(H_GRU_BHH)[q] += sh;
-    }
-    // d x for every real trajectory row (t, j < cnt[t])
-    const float* Wih = PW(H_GRU_WIH);
-    for (int idx = tid; idx < T * NMAX * GIN; idx += 256) {
-      const int row = idx / GIN, i = idx - row * GIN;
-      const int t = row / NMAX, j = row - t * NMAX;
-      float s = 0.f;
-      if (j < cnt[t]) {
-        const float* dgi = w + L.dgi + (int64_t)row * 3 * GH;
-        for (int q = 0; q < 3 * GH; ++q) s = fmaf(Wih[(int64_t)q * GIN + i], dgi[q], s);
-      }
-      w[L.dx + idx] = s;
-    }
-    __syncthreads();
   }
-  // ---- ReID MLP backward over real rows (padding rows carry zero d x and zero inputs -> contribute 0)
-  {
-    const int TN = T * NMAX;
-    float* dr2 = w + L.dtmp;  // [TN][64]
-    float* dr1 = w + L.dtmp2; // [TN][32] (dtmp2 is free now)
-    // layer 4 (no act): d pre = d x[:, 4:68] on real rows only
-    for (int idx = tid; idx < TN * 64; idx += 256) {
-      const int row = idx / 64, u = idx - row * 64;
-      const int t = row / NMAX, j = row - t * NMAX;
-      w[L.dgh + idx] = (j < cnt[t]) ? w[L.dx + (int64_t)row * GIN + 4 + u] : 0.f;  // reuse dgh as scratch
+}
+
+// per frame: d x = W_ih^T d gi for real rows, ReID backward, d box -> d detector logits
+__global__ __launch_bounds__(256) void head_rows_bwd_kernel(HeadArgs a, const float* __restrict__ logits,
+                                                            float* __restrict__ dlog) {
+  const int f = blockIdx.x;
+  const int b = f / a.T, t = f - b * a.T;
+  const int tid = threadIdx.x;
+  const RowLayout RL((int64_t)a.B * a.T * NMAX);
+  float* rows = a.rows;
+  const int* iw = a.iws + (int64_t)b * a.iws_stride;
+  const int cnt = iw[t];
+  const int* slot = iw + a.T + t * NMAX;
+  const int64_t r0 = (int64_t)f * NMAX;
+  __shared__ float sdx[NMAX][GIN];
+  __shared__ float sd2[NMAX][64];
+  __shared__ float sd1[NMAX][32];
+  const float* Wih = PW(H_GRU_WIH);
+  for (int idx = tid; idx < NMAX * GIN; idx += 256) {
+    const int j = idx / GIN, i = idx - j * GIN;
+    float s = 0.f;
+    if (j < cnt) {
+      const float* dgi = rows + RL.dgi + (r0 + j) * G3;
+      for (int q = 0; q < G3; ++q) s = fmaf(Wih[(int64_t)q * GIN + i], dgi[q], s);
     }
-    __syncthreads();
-    lin_bwd(w + L.dgh, 64, w + L.rh2, 64, TN, 64, PW(H_REID4_W), 64, GW(H_REID4_W), GW(H_REID4_B), dr2, 64, false);
-    relu_gate(dr2, 64, w + L.rh2, 64, TN, 64, 1.f);
-    lin_bwd(dr2, 64, w + L.rh1, 32, TN, 32, PW(H_REID2_W), 64, GW(H_REID2_W), GW(H_REID2_B), dr1, 32, false);
-    relu_gate(dr1, 32, w + L.rh1, 32, TN, 32, 1.f);
-    // box grads: d box = d x[:, 0:4] + W0^T dr1, then into the detector logits for valid boxes
-    float* dbox = w + L.dgi;  // [TN][4]
-    lin_bwd(dr1, 32, w + L.boxes, 4, TN, 4, PW(H_REID0_W), 32, GW(H_REID0_W), GW(H_REID0_B), dbox, 4, false);
-    for (int idx = tid; idx < TN * 4; idx += 256) {
-      const int row = idx / 4, c = idx - row * 4;
-      const int t = row / NMAX, j = row - t * NMAX;
-      if (j >= cnt[t]) continue;
-      const int k = slot[t * NMAX + j];
-      if (k < 0) continue;  // fallback box is a constant
-      const float dv = dbox[idx] + w[L.dx + (int64_t)row * GIN + c];
-      const float lg = logits[((int64_t)b * T + t) * 20 + k * 4 + c];
-      const float sg = sigmoidf_(lg);
+    sdx[j][i] = s;
+  }
+  __syncthreads();
+  // reid layer 4 (no activation): d pre = d x[4:68]
+  for (int idx = tid; idx < NMAX * 64; idx += 256) {
+    const int j = idx / 64, u = idx - j * 64;
+    rows[RL.dp4 + (r0 + j) * 64 + u] = sdx[j][4 + u];  // zero for padding rows
+  }
+  const float* W4 = PW(H_REID4_W);
+  for (int idx = tid; idx < NMAX * 64; idx += 256) {
+    const int j = idx / 64, k = idx - j * 64;
+    float s = 0.f;
+    if (j < cnt) {
+      for (int u = 0; u < 64; ++u) s = fmaf(W4[u * 64 + k], sdx[j][4 + u], s);
+      s = rows[RL.rh2 + (r0 + j) * 64 + k] > 0.f ? s : 0.f;
+    }
+    sd2[j][k] = s;
+    rows[RL.dp2 + (r0 + j) * 64 + k] = s;
+  }
+  __syncthreads();
+  const float* W2 = PW(H_REID2_W);
+  for (int idx = tid; idx < NMAX * 32; idx += 256) {
+    const int j = idx / 32, k = idx - j * 32;
+    float s = 0.f;
+    if (j < cnt) {
+      for (int u = 0; u < 64; ++u) s = fmaf(W2[u * 32 + k], sd2[j][u], s);
+      s = rows[RL.rh1 + (r0 + j) * 32 + k] > 0.f ? s : 0.f;
+    }
+    sd1[j][k] = s;
+    rows[RL.dp0 + (r0 + j) * 32 + k] = s;
+  }
+  __syncthreads();
+  const float* W0 = PW(H_REID0_W);
+  if (tid < NMAX * 4) {
+    const int j = tid / 4, c = tid % 4;
+    if (j < cnt && slot[j] >= 0) {  // the fallback box is a constant: no grad
+      float dv = sdx[j][c];
+      for (int u = 0; u < 32; ++u) dv = fmaf(W0[u * 4 + c], sd1[j][u], dv);
+      const int k = slot[j];
+      const float sg = sigmoidf_(logits[(int64_t)f * 20 + k * 4 + c]);
       const float sc = c == 0 ? 360.f : (c == 1 ? 240.f : (c == 2 ? 80.f : 120.f));
-      dlog[((int64_t)b * T + t) * 20 + k * 4 + c] = dv * sc * sg * (1.f - sg);
+      dlog[(int64_t)f * 20 + k * 4 + c] = dv * sc * sg * (1.f - sg);
     }
+  }
+}
+
+// GRU + ReID weight/bias grads: fixed-order reductions over all R rows, written into the flat grad buffer.
+// out[o][i] = sum_r A[r][o] * B[r][i]  (bias: sum_r A[r][o])
+struct WSeg {
+  int slot;
+  int64_t dA, dB;
+  int ldA, ldB, O, I;
+};
+
+__global__ __launch_bounds__(256) void head_rows_wgrad_kernel(HeadArgs a) {
+  const RowLayout RL((int64_t)a.B * a.T * NMAX);
+  const float* rows = a.rows;
+  const int64_t R = RL.R;
+  const WSeg segs[10] = {
+      {H_GRU_WIH, RL.dgi, RL.x, G3, GIN, G3, GIN},   {H_GRU_WHH, RL.dgh, RL.hp, G3, GH, G3, GH},
+      {H_GRU_BIH, RL.dgi, -1, G3, 0, G3, 1},         {H_GRU_BHH, RL.dgh, -1, G3, 0, G3, 1},
+      {H_REID4_W, RL.dp4, RL.rh2, 64, 64, 64, 64},   {H_REID4_B, RL.dp4, -1, 64, 0, 64, 1},
+      {H_REID2_W, RL.dp2, RL.rh1, 64, 32, 64, 32},   {H_REID2_B, RL.dp2, -1, 64, 0, 64, 1},
+      {H_REID0_W, RL.dp0, RL.box, 32, 4, 32, 4},     {H_REID0_B, RL.dp0, -1, 32, 0, 32, 1},
+  };
+  int64_t total = 0;
+  for (int s = 0; s < 10; ++s) total += (int64_t)segs[s].O * segs[s].I;
+  for (int64_t gidx = blockIdx.x * 256ll + threadIdx.x; gidx < total; gidx += (int64_t)gridDim.x * 256) {
+    int s = 0;
+    int64_t idx = gidx;
+    while (idx >= (int64_t)segs[s].O * segs[s].I) {
+      idx -= (int64_t)segs[s].O * segs[s].I;
+      ++s;
+    }
+    const WSeg& sg = segs[s];
+    const int o = (int)(idx / sg.I), i = (int)(idx - (int64_t)o * sg.I);
+    float acc = 0.f;
+    if (sg.dB >= 0) {
+      for (int64_t r = 0; r < R; ++r) acc = fmaf(rows[sg.dA + r * sg.ldA + o], rows[sg.dB + r * sg.ldB + i], acc);
+    } else {
+      for (int64_t r = 0; r < R; ++r) acc += rows[sg.dA + r * sg.ldA + o];
+    }
+    a.grad[a.off[sg.slot] + idx] = acc;
   }
 }
 
 int head_bwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, const HeadUp& up, float* slabs,
              int64_t slab_len, float* d_det_logits, hipStream_t st) {
   VAD_HIP(hipMemsetAsync(d_det_logits, 0, sizeof(float) * (size_t)a.B * a.T * 20, st));
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(a.B), dim3(256), 0, st, a, det_logits, o, up, slabs, slab_len,
-                     d_det_logits);
+  hipLaunchKernelGGL(head_seq_bwd_kernel, dim3(a.B), dim3(HT), 0, st, a, o, up, slabs, slab_len);
+  VAD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(head_rows_bwd_kernel, dim3(a.B * a.T), dim3(256), 0, st, a, det_logits, d_det_logits);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -651,7 +776,13 @@ int head_slab_reduce(const float* slabs, int B, int64_t slab_len, float* grad_he
   return 0;
 }
 
-// ------------------------------------------------------------------ tail: softmax, blend, losses
+int head_rows_wgrad(const HeadArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(head_rows_wgrad_kernel, dim3(128), dim3(256), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+// ================================================================== tail: softmax, blend, losses
 __global__ void cad_tail_fwd_kernel(TailArgs t) {
   const int B = t.B;
   __shared__ float red[4][256];
@@ -705,12 +836,12 @@ __global__ void cad_tail_fwd_kernel(TailArgs t) {
     }
     if (t.labels) {
       const float fB = (float)B;
-      const float c = red[0][0] / fB, a = red[1][0] / fB, ca2 = red[2][0] / fB, k = red[3][0] / fB;
+      const float c = red[0][0] / fB, an2 = red[1][0] / fB, ca2 = red[2][0] / fB, k = red[3][0] / fB;
       t.losses[0] = c;
-      t.losses[1] = a;
+      t.losses[1] = an2;
       t.losses[2] = ca2;
       t.losses[3] = k;
-      t.losses[4] = 0.4f * c + 0.3f * a + 0.2f * ca2 + 0.1f * k;
+      t.losses[4] = 0.4f * c + 0.3f * an2 + 0.2f * ca2 + 0.1f * k;
     }
   }
 }
@@ -734,7 +865,6 @@ __global__ void cad_tail_bwd_kernel(TailArgs t) {
       const float yf = (float)y;
       d_final = 0.3f * 2.f * (fin - yf) / fB;
       d_c = 0.2f * 2.f * (c - yf) / fB;
-      // d CE / d p = softmax(p) - onehot
       const float m2 = fmaxf(p0, p1);
       const float e0 = expf(p0 - m2), e1 = expf(p1 - m2);
       const float q0 = e0 / (e0 + e1), q1 = e1 / (e0 + e1);
@@ -750,8 +880,7 @@ __global__ void cad_tail_bwd_kernel(TailArgs t) {
     }
     d_c += 0.6f * d_final;
     dp1 += 0.4f * d_final;
-    // through softmax: dl = p * (dp - <p, dp>)
-    const float dot = p0 * dp0 + p1 * dp1;
+    const float dot = p0 * dp0 + p1 * dp1;  // through softmax: dl = p * (dp - <p, dp>)
     t.d_direct_logits[b * 2] = p0 * (dp0 - dot);
     t.d_direct_logits[b * 2 + 1] = p1 * (dp1 - dot);
     t.d_causal[b] = d_c;

@@ -100,6 +100,7 @@ class CadEngine:
         self.plans = {}
         self.generation = 0
         self._last = None
+        self._loss_buf = None
 
     # ------------------------------------------------------------------ bookkeeping
     def is_bound(self) -> bool:
@@ -125,7 +126,9 @@ class CadEngine:
         return self.grads[off:off + self.slot_numel[i]]
 
     # ------------------------------------------------------------------ compute
-    def forward(self, x: torch.Tensor, training: bool, seed: int, step: int, clip0: int, labels=None):
+    def forward(self, x: torch.Tensor, training: bool, seed: int, step: int, clip0: int, labels=None,
+                want_outputs: bool = True):
+        """Runs the fused forward.  want_outputs=False returns only the loss vector (no output copies)."""
         nat.require_hip(x)
         if x.dim() != 5:
             raise ValueError(f"Expected 5D tensor (B,T,C,H,W), got {tuple(x.shape)}")
@@ -135,6 +138,17 @@ class CadEngine:
         x = x.contiguous().float()
         pl = self.plan(B, T, H, W)
         dev = self.device
+        if not want_outputs:
+            if self._loss_buf is None:
+                self._loss_buf = torch.empty(5, device=dev)
+            lab = None if labels is None else labels.to(device=dev, dtype=torch.int64).contiguous()
+            nat.check(nat.lib().vad_cad_forward(
+                pl.h, x.data_ptr(), 1 if training else 0, seed & ((1 << 64) - 1), step, clip0, nat.ptr(lab),
+                None, None, None, None, None, None, None, None, None, self._loss_buf.data_ptr(), None,
+                nat.stream_of(dev)))
+            self.generation += 1
+            self._last = (pl, lab, x)
+            return {"losses": self._loss_buf}
         o = dict(
             final=torch.empty(B, device=dev), probs=torch.empty(B, 2, device=dev),
             causal=torch.empty(B, device=dev), kl=torch.empty(B, device=dev),

@@ -53,7 +53,7 @@ class CadTrainer:
         B = videos.shape[0]
         if self.world > 1:
             dist.broadcast(eng.bufs, 0, group=self.pg)
-        o = eng.forward(videos, True, self.seed, self.step_idx, self.rank * B, labels)
+        o = eng.forward(videos, True, self.seed, self.step_idx, self.rank * B, labels, want_outputs=False)
         eng.backward(True)
         if self.world > 1:
             dist.all_reduce(eng.grads, group=self.pg)
