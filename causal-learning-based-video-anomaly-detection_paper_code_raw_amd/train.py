@@ -34,9 +34,9 @@ class CadTrainer:
     """
 
     def __init__(self, model, lr=3e-4, weight_decay=1e-5, eps=1e-8, betas=(0.9, 0.999), max_norm=1.0, seed=0,
-                 process_group=None):
+                 process_group=None, engine=None):
         self.model = model
-        self.eng = model.engine()
+        self.eng = engine if engine is not None else model.engine()
         self.lr, self.wd, self.eps, self.betas, self.max_norm = lr, weight_decay, eps, betas, max_norm
         self.seed = seed
         self.step_idx = 0
@@ -46,6 +46,7 @@ class CadTrainer:
         self.eng.init_optimizer_state()
         if self.world > 1:
             dist.broadcast(self.eng.params, 0, group=process_group)
+            dist.broadcast(self.eng.bufs, 0, group=process_group)
 
     def step(self, videos, labels, lr=None):
         """One training step; returns the (device) loss vector [cls, anomaly, causal, kl, total]."""
