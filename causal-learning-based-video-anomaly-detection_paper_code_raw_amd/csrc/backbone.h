@@ -43,6 +43,12 @@ int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd
 int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats /*nullable: BN+ReLU on load*/,
               const float* wf, const float* bias, float* y, float* partials, int* nparts, hipStream_t st);
 int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
+// direct LDS-patch kernels (conv_patch.hip) for stride-1 layers; conv3_fwd / conv3_dgrad route there by default
+bool conv3_patch_supported(const Conv3Layer& L, bool fwd);
+int64_t conv3_patch_blocks(int NF, int OH, int OW);  // BN partial blocks of a patch forward
+int conv3_patch_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
+                    float* y, float* partials, int* nparts, hipStream_t st);
+int conv3_patch_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
                 int* nsplit, int64_t partial_cap, hipStream_t st);
 int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, const float* bias_partials,
@@ -66,5 +72,9 @@ int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX,
 // dW = dY^T X, db = colsum(dY) (written, not accumulated)
 int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW, float* db, float* scratch,
                 int64_t scratch_floats, const int* skip, hipStream_t st);
+
+// conv GEMM tuning knobs: conv_fwd_tile / conv_dgrad_tile / conv_wgrad_tile (tile id, -1 = heuristic),
+// conv_wgrad_blocks, conv_wgrad_min_ktiles
+int set_tuning(const char* key, int value);
 
 }  // namespace vad

@@ -652,6 +652,68 @@ using T64x64 = TileCfg<2, 2, 1, 1>;
 using T128x128 = TileCfg<2, 2, 2, 2>;
 using T32x128 = TileCfg<1, 4, 1, 1>;
 
+// runtime-selectable tile shapes for the conv GEMMs (tuning / sweeps); id -> TileCfg
+template <class F>
+static int with_tile(int id, F&& f) {
+  switch (id) {
+    case 0: return f(TileCfg<4, 1, 1, 1>{});  // 128 x 32
+    case 1: return f(TileCfg<4, 1, 2, 1>{});  // 256 x 32
+    case 2: return f(TileCfg<2, 2, 1, 1>{});  //  64 x 64
+    case 3: return f(TileCfg<2, 2, 2, 1>{});  // 128 x 64
+    case 4: return f(TileCfg<2, 2, 1, 2>{});  //  64 x 128
+    case 5: return f(TileCfg<2, 2, 2, 2>{});  // 128 x 128
+    case 6: return f(TileCfg<4, 1, 2, 2>{});  // 256 x 64
+    case 7: return f(TileCfg<1, 4, 1, 1>{});  //  32 x 128
+    case 8: return f(TileCfg<1, 4, 1, 2>{});  //  32 x 256
+    case 9: return f(TileCfg<2, 2, 1, 4>{});  //  64 x 256
+    default: set_error("unknown tile id"); return 1;
+  }
+}
+static int tile_bm(int id) {
+  static const int bm[10] = {128, 256, 64, 128, 64, 128, 256, 32, 32, 64};
+  return (id >= 0 && id < 10) ? bm[id] : 64;
+}
+
+struct ConvTuning {
+  int fwd = -1, dgrad = -1, wgrad = -1;  // forced tile ids (-1: heuristic)
+  int wgrad_blocks = 1024;               // target grid size of the split-K weight gradient
+  int wgrad_min_ktiles = 16;             // minimum BK-slices per split
+  int patch = 1;                         // stride-1 fwd/dgrad on the LDS-patch kernels
+};
+static ConvTuning g_tune;
+
+int set_tuning(const char* key, int value) {
+  const std::string k(key);
+  if (k == "conv_fwd_tile") g_tune.fwd = value;
+  else if (k == "conv_dgrad_tile") g_tune.dgrad = value;
+  else if (k == "conv_wgrad_tile") g_tune.wgrad = value;
+  else if (k == "conv_wgrad_blocks") g_tune.wgrad_blocks = value;
+  else if (k == "conv_wgrad_min_ktiles") g_tune.wgrad_min_ktiles = value;
+  else if (k == "conv_patch") g_tune.patch = value;
+  else {
+    set_error("unknown tuning key " + k);
+    return 1;
+  }
+  return 0;
+}
+
+// heuristics (fallback when no tile is forced); BM >= 64 keeps the forward BN partial count within bounds
+static int pick_fwd_tile(int M, int N) {
+  if (g_tune.fwd >= 0 && tile_bm(g_tune.fwd) >= 64) return g_tune.fwd;
+  if (N == 32) return 0;
+  return M >= 64 * 1024 ? 3 : 2;
+}
+static int pick_dgrad_tile(int M, int N) {
+  if (g_tune.dgrad >= 0) return g_tune.dgrad;
+  if (N == 32) return 0;
+  return M >= 64 * 1024 ? 3 : 2;
+}
+static int pick_wgrad_tile(int M, int N) {
+  (void)N;
+  if (g_tune.wgrad >= 0) return g_tune.wgrad;
+  return M == 32 ? 7 : 2;
+}
+
 // =====================================================================================================
 // 3x3 convs
 // =====================================================================================================
@@ -726,48 +788,42 @@ int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd
 int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
               float* y, float* partials, int* nparts, hipStream_t st) {
   VAD_CHECK(L.Ci % 32 == 0, "conv3_fwd: Ci must be a multiple of 32");
+  // (the patch grid may exceed ceil(M/64) BN partial blocks on tiny images: those stay on the GEMM path)
+  if (g_tune.patch && conv3_patch_supported(L, true) &&
+      conv3_patch_blocks(L.NF, L.OH, L.OW) <= cdiv((int64_t)L.NF * L.OH * L.OW, 64))
+    return conv3_patch_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st);
   ConvGeom g{L.NF, L.OH, L.OW, L.stride, L.stride, L.IH, L.IW, L.Ci};
   TapTable taps;
   fwd_taps(taps);
   const int M = L.NF * L.OH * L.OW, N = L.Co, K = 9 * L.Ci;
   EpiConvFwd::Params pe{y, bias, L.Co, partials};
-  if (L.Co == 32) {
-    using C = T128x32;
-    ConvGatherKC<C::BM>::Params pa{src, g, taps, src_stats ? src_stats + 2 * L.Ci : nullptr,
-                                   src_stats ? src_stats + 3 * L.Ci : nullptr};
-    DenseKC<C::BN>::Params pb{wf, K, N, K};
+  const int id = pick_fwd_tile(M, N);
+  return with_tile(id, [&](auto cfg) -> int {
+    using C = decltype(cfg);
+    typename ConvGatherKC<C::BM>::Params pa{src, g, taps, src_stats ? src_stats + 2 * L.Ci : nullptr,
+                                            src_stats ? src_stats + 3 * L.Ci : nullptr};
+    typename DenseKC<C::BN>::Params pb{wf, K, N, K};
     VAD_TRY((launch_gemm<C, ConvGatherKC, DenseKC, EpiConvFwd>(pa, pb, pe, M, N, K, 1, nullptr, st)));
     *nparts = (int)cdiv(M, C::BM);
-  } else if (M >= 64 * 1024) {
-    using C = T128x64;
-    ConvGatherKC<C::BM>::Params pa{src, g, taps, src_stats ? src_stats + 2 * L.Ci : nullptr,
-                                   src_stats ? src_stats + 3 * L.Ci : nullptr};
-    DenseKC<C::BN>::Params pb{wf, K, N, K};
-    VAD_TRY((launch_gemm<C, ConvGatherKC, DenseKC, EpiConvFwd>(pa, pb, pe, M, N, K, 1, nullptr, st)));
-    *nparts = (int)cdiv(M, C::BM);
-  } else {
-    using C = T64x64;
-    ConvGatherKC<C::BM>::Params pa{src, g, taps, src_stats ? src_stats + 2 * L.Ci : nullptr,
-                                   src_stats ? src_stats + 3 * L.Ci : nullptr};
-    DenseKC<C::BN>::Params pb{wf, K, N, K};
-    VAD_TRY((launch_gemm<C, ConvGatherKC, DenseKC, EpiConvFwd>(pa, pb, pe, M, N, K, 1, nullptr, st)));
-    *nparts = (int)cdiv(M, C::BM);
-  }
-  return 0;
+    return 0;
+  });
 }
 
-template <class C>
 static int dgrad_launch(const ConvGeom& g, const TapTable& taps, const float* dY, const float* wd, int N,
                         const EpiConvDgrad::Params& pe, hipStream_t st) {
   const int M = g.imgs * g.GA * g.GB, K = taps.ntaps * g.C;
-  typename ConvGatherKC<C::BM>::Params pa{dY, g, taps, nullptr, nullptr};
-  typename DenseKC<C::BN>::Params pb{wd, K, N, K};
-  return launch_gemm<C, ConvGatherKC, DenseKC, EpiConvDgrad>(pa, pb, pe, M, N, K, 1, nullptr, st);
+  return with_tile(pick_dgrad_tile(M, N), [&](auto cfg) -> int {
+    using C = decltype(cfg);
+    typename ConvGatherKC<C::BM>::Params pa{dY, g, taps, nullptr, nullptr};
+    typename DenseKC<C::BN>::Params pb{wd, K, N, K};
+    return launch_gemm<C, ConvGatherKC, DenseKC, EpiConvDgrad>(pa, pb, pe, M, N, K, 1, nullptr, st);
+  });
 }
 
 int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st) {
   VAD_CHECK(L.Co % 32 == 0, "conv3_dgrad: Co must be a multiple of 32");
   const int N = L.Ci;
+  if (g_tune.patch && conv3_patch_supported(L, false)) return conv3_patch_dgrad(L, dY, wd, dX, st);
   if (L.stride == 1) {
     ConvGeom g{L.NF, L.IH, L.IW, 1, 1, L.OH, L.OW, L.Co};
     TapTable taps;
@@ -777,10 +833,7 @@ int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX
       taps.dw[k] = (int8_t)(1 - k % 3);
     }
     EpiConvDgrad::Params pe{dX, L.IH, L.IW, 1, 0, 1, 0, L.IH, L.IW, L.Ci};
-    const int M = L.NF * L.IH * L.IW;
-    if (N == 32) return dgrad_launch<T128x32>(g, taps, dY, wd, N, pe, st);
-    if (M >= 64 * 1024) return dgrad_launch<T128x64>(g, taps, dY, wd, N, pe, st);
-    return dgrad_launch<T64x64>(g, taps, dY, wd, N, pe, st);
+    return dgrad_launch(g, taps, dY, wd, N, pe, st);
   }
   DgradClass cls[4];
   const int nc = dgrad_classes(2, cls);
@@ -797,11 +850,7 @@ int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX
         taps.dw[r * c.nct + q] = (int8_t)c.dw[q];
       }
     EpiConvDgrad::Params pe{dX, GA, GB, 2, c.ph, 2, c.pw, L.IH, L.IW, L.Ci};
-    const float* w = wd + off;
-    const int M = L.NF * GA * GB;
-    if (N == 32) VAD_TRY(dgrad_launch<T128x32>(g, taps, dY, w, N, pe, st));
-    else if (M >= 64 * 1024) VAD_TRY(dgrad_launch<T128x64>(g, taps, dY, w, N, pe, st));
-    else VAD_TRY(dgrad_launch<T64x64>(g, taps, dY, w, N, pe, st));
+    VAD_TRY(dgrad_launch(g, taps, dY, wd + off, N, pe, st));
     off += (int64_t)taps.ntaps * L.Ci * L.Co;
   }
   return 0;
@@ -810,12 +859,11 @@ int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
                 int* nsplit, int64_t partial_cap, hipStream_t st) {
   const int M = L.Co, N = 9 * L.Ci, K = L.NF * L.OH * L.OW;
-  ConvPatchKM<128>::Params dummy{};
-  (void)dummy;
-  auto run = [&](auto cfg) -> int {
+  return with_tile(pick_wgrad_tile(M, N), [&](auto cfg) -> int {
     using C = decltype(cfg);
     const int tiles = (int)(cdiv(M, C::BM) * cdiv(N, C::BN));
-    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(1024, tiles), cdiv(K, 16 * BK)));
+    int splits = (int)std::max<int64_t>(
+        1, std::min<int64_t>(cdiv(g_tune.wgrad_blocks, tiles), cdiv(K, (int64_t)g_tune.wgrad_min_ktiles * BK)));
     while ((int64_t)splits * M * N > partial_cap && splits > 1) splits /= 2;
     typename DenseKM<C::BM>::Params pa{dY, L.Co, L.Co, K, -1};
     typename ConvPatchKM<C::BN>::Params pb{src, L.NF, L.OH, L.OW, L.stride, 1, L.IH, L.IW, L.Ci, 3, N,
@@ -823,9 +871,7 @@ int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const fl
                                            src_stats ? src_stats + 3 * L.Ci : nullptr};
     EpiPartial::Params pe{partial, N};
     return launch_gemm<C, DenseKM, ConvPatchKM, EpiPartial>(pa, pb, pe, M, N, K, splits, nullptr, st, nsplit);
-  };
-  if (M == 32) return run(T32x128{});
-  return run(T64x64{});
+  });
 }
 
 // Split-K slab reduction of the conv weight gradient.  Block = 32 consecutive slab elements x 8 split-lanes; each

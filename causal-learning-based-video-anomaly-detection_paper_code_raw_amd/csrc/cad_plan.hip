@@ -344,6 +344,7 @@ struct CadPlanImpl {
     for (int l = 0; l < 8; ++l) {
       const int64_t M = nf * L[l].OH * L[l].OW;
       parts_floats = std::max<int64_t>(parts_floats, cdiv(M, 64) * 2 * L[l].Co);
+      parts_floats = std::max<int64_t>(parts_floats, conv3_patch_blocks(nf, L[l].OH, L[l].OW) * 2 * L[l].Co);
     }
     parts = w.take<float>(parts_floats);
     feats = w.take<float>(nf * 6144);

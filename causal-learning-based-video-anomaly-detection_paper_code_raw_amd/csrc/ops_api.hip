@@ -17,7 +17,7 @@ int vad_conv3x3_forward(const float* x_nhwc, int NF, int Ci, int IH, int IW, con
                         int Co, int stride, float* y_nhwc, float* wf_scratch, float* wd_scratch, float* partials,
                         void* stream) {
   Conv3Layer L{NF, Ci, Co, IH, IW, (IH - 1) / stride + 1, (IW - 1) / stride + 1, stride};
-  VAD_TRY(conv3_prep_weights(w, L, wf_scratch, wd_scratch, (hipStream_t)stream));
+  if (w) VAD_TRY(conv3_prep_weights(w, L, wf_scratch, wd_scratch, (hipStream_t)stream));  // w == NULL: prepared
   int np = 0;
   return conv3_fwd(L, x_nhwc, nullptr, wf_scratch, bias, y_nhwc, partials, &np, (hipStream_t)stream);
 }
@@ -25,7 +25,7 @@ int vad_conv3x3_forward(const float* x_nhwc, int NF, int Ci, int IH, int IW, con
 int vad_conv3x3_dgrad(const float* dy_nhwc, int NF, int Ci, int IH, int IW, const float* w, int Co, int stride,
                       float* dx_nhwc, float* wf_scratch, float* wd_scratch, void* stream) {
   Conv3Layer L{NF, Ci, Co, IH, IW, (IH - 1) / stride + 1, (IW - 1) / stride + 1, stride};
-  VAD_TRY(conv3_prep_weights(w, L, wf_scratch, wd_scratch, (hipStream_t)stream));
+  if (w) VAD_TRY(conv3_prep_weights(w, L, wf_scratch, wd_scratch, (hipStream_t)stream));  // w == NULL: prepared
   return conv3_dgrad(L, dy_nhwc, wd_scratch, dx_nhwc, (hipStream_t)stream);
 }
 
@@ -38,3 +38,5 @@ extern "C" int vad_conv3x3_wgrad(const float* x_nhwc, const float* dy_nhwc, int 
   VAD_TRY(conv3_wgrad(L, dy_nhwc, x_nhwc, nullptr, partial, &ns, partial_floats, (hipStream_t)stream));
   return conv3_wgrad_reduce(L, partial, ns, nullptr, 0, dW, nullptr, (hipStream_t)stream);
 }
+
+extern "C" int vad_set_tuning(const char* key, int value) { return vad::set_tuning(key, value); }

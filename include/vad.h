@@ -97,6 +97,9 @@ int vad_conv3x3_forward(const float* x_nhwc, int NF, int Ci, int IH, int IW, con
 /* input gradient of the same conv (transposed conv; stride-2 split into four parity classes) */
 int vad_conv3x3_dgrad(const float* dy_nhwc, int NF, int Ci, int IH, int IW, const float* w, int Co, int stride,
                       float* dx_nhwc, float* wf_scratch, float* wd_scratch, void* stream);
+/* kernel tuning knobs (sweeps): "conv_fwd_tile", "conv_dgrad_tile", "conv_wgrad_tile" (tile id 0..9, -1 = built-in
+ * choice), "conv_wgrad_blocks", "conv_wgrad_min_ktiles".  Process-global. */
+int vad_set_tuning(const char* key, int value);
 /* weight gradient of the same conv: dW[Co][Ci][3][3] = sum over pixels dY x patches(x); split-K slabs in partial */
 int vad_conv3x3_wgrad(const float* x_nhwc, const float* dy_nhwc, int NF, int Ci, int IH, int IW, int Co, int stride,
                       float* dW, float* partial, int64_t partial_floats, void* stream);

@@ -38,7 +38,10 @@ def test_dense_forward(M, K, N, relu):
 
 
 CONV_CASES = [(2, 32, 32, 19, 17, 1), (2, 32, 64, 29, 29, 2), (1, 64, 128, 15, 15, 2), (2, 128, 256, 8, 8, 1),
-              (3, 64, 64, 10, 7, 2), (1, 256, 256, 8, 8, 1)]
+              (3, 64, 64, 10, 7, 2), (1, 256, 256, 8, 8, 1),
+              # stride-1 shapes of the LDS-patch kernels: 2x8x8 tiles with odd NF, 8x16, 4x32 (57-wide, ragged)
+              (3, 32, 32, 8, 8, 1), (2, 64, 64, 15, 15, 1), (1, 32, 32, 57, 57, 1), (2, 128, 128, 29, 29, 1),
+              (2, 32, 64, 5, 3, 1)]
 
 
 @pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", CONV_CASES)
