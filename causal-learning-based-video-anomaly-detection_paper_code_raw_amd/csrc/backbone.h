@@ -49,6 +49,9 @@ int64_t conv3_patch_blocks(int NF, int OH, int OW);  // BN partial blocks of a p
 int conv3_patch_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
                     float* y, float* partials, int* nparts, hipStream_t st);
 int conv3_patch_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
+bool conv3_wgrad_patch_supported(const Conv3Layer& L);
+int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
+                      int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
                 int* nsplit, int64_t partial_cap, hipStream_t st);
 int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, const float* bias_partials,

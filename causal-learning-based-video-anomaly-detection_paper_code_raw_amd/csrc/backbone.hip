@@ -679,6 +679,8 @@ struct ConvTuning {
   int wgrad_blocks = 1024;               // target grid size of the split-K weight gradient
   int wgrad_min_ktiles = 16;             // minimum BK-slices per split
   int patch = 1;                         // stride-1 fwd/dgrad on the LDS-patch kernels
+  int wgrad_patch = 1;                   // weight gradients on the LDS-patch kernel: 1 stride-1 layers, 2 all
+  int wgrad_patch_blocks = 512;          // its target grid size
 };
 static ConvTuning g_tune;
 
@@ -690,6 +692,8 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_blocks") g_tune.wgrad_blocks = value;
   else if (k == "conv_wgrad_min_ktiles") g_tune.wgrad_min_ktiles = value;
   else if (k == "conv_patch") g_tune.patch = value;
+  else if (k == "conv_wgrad_patch") g_tune.wgrad_patch = value;
+  else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else {
     set_error("unknown tuning key " + k);
     return 1;
@@ -858,6 +862,8 @@ int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX
 
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
                 int* nsplit, int64_t partial_cap, hipStream_t st) {
+  if (g_tune.wgrad_patch && conv3_wgrad_patch_supported(L) && (L.stride == 1 || g_tune.wgrad_patch == 2))
+    return conv3_wgrad_patch(L, dY, src, src_stats, partial, nsplit, partial_cap, g_tune.wgrad_patch_blocks, st);
   const int M = L.Co, N = 9 * L.Ci, K = L.NF * L.OH * L.OW;
   return with_tile(pick_wgrad_tile(M, N), [&](auto cfg) -> int {
     using C = decltype(cfg);

@@ -7,6 +7,8 @@
 // every wave issues 9 x 4 x 4 = 144 MFMAs on its 32 pixels with only LDS reads in between (one ds_read_b128 of A
 // and one of B feed 4 MFMAs; rows padded to 36 / 292 floats so the 16-lane read groups are conflict-free).
 // Used for stride-1 forward convs (BN statistics in the epilogue) and stride-1 input gradients (flipped taps).
+#include <algorithm>
+
 #include "backbone.h"
 #include "gemm.h"
 
@@ -240,6 +242,209 @@ int conv3_patch_dgrad(const Conv3Layer& L, const float* dY, const float* wd, flo
   a.out = dX;
   a.NF = L.NF; a.IH = L.OH; a.IW = L.OW; a.C = L.Co; a.OH = L.IH; a.OW = L.IW; a.N = L.Ci;
   return dispatch_patch<false>(a, st, nullptr);
+}
+
+
+// =====================================================================================================
+// Weight gradient: dW[co][t][ci] = sum_p dY[p][co] * relu(bn(x))[p + off_t][ci].
+// Block = (32 co) x (9 taps x 32 ci) over a strided subset of 128-pixel tiles (split-K over pixels, split index
+// blockIdx.z).  Per tile it stages dY [128 px][32 co] and the input patch [patch px][32 ci] (BN+ReLU on load)
+// in LDS; wave w takes pixels [32w, 32w+32) as the MFMA K dimension (2 per step) and keeps all 9 tap tiles in
+// registers (one A read feeds 9 MFMAs).  The 4 waves are combined in a fixed order through LDS and the block's
+// sum lands in slab z of the [S][co][t*Ci + ci] split-K layout that conv3_wgrad_reduce consumes.
+// Stride 2: patch columns are stored de-interleaved by parity so consecutive output pixels read consecutive
+// patch rows (conflict-free b32 reads).
+// =====================================================================================================
+struct WgradPatchArgs {
+  const float* dY;     // [NF][OH][OW][Co]
+  const float* src;    // [NF][IH][IW][Ci]
+  const float* scale;  // BN+ReLU on load, nullable
+  const float* shift;
+  float* slab;         // [S][Co][9*Ci]
+  int NF, IH, IW, Ci, OH, OW, Co;
+  int tiles_h, tiles_w, ntiles;
+};
+
+template <int S, int NI, int TH, int TW>
+__global__ __launch_bounds__(256, S == 1 ? 2 : 1) void conv3x3_wgrad_patch_kernel(const WgradPatchArgs p) {
+  static_assert(NI * TH * TW == 128, "a tile holds 128 output pixels");
+  constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3, PROWS = NI * PH * PW;
+  constexpr int PWE = (PW + 1) / 2;  // stride 2: even columns first
+  constexpr int XF = PROWS * 32, YF = 128 * 32, RF = 2 * 9 * 16 * 64;
+  constexpr int LF = (XF + YF) > RF ? (XF + YF) : RF;
+  __shared__ __attribute__((aligned(16))) float sm[LF];
+  float* xs = sm;
+  float* ys = sm + XF;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int co0 = blockIdx.x * 32, ci0 = blockIdx.y * 32;
+  const int h = lane >> 5, j = lane & 31;
+  const int tiles_per_img = p.tiles_h * p.tiles_w;
+  const int c4 = (tid & 7) * 4;
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  constexpr int PIT = (PROWS * 8 + 255) / 256;
+  f32x4 pv[PIT], yv[4];
+  int img0 = 0, oy0 = 0, ox0 = 0;
+  auto tile_origin = [&](int tile, int& i0, int& y0, int& x0) {
+    i0 = (tile / tiles_per_img) * NI;
+    const int tr = tile % tiles_per_img;
+    y0 = (tr / p.tiles_w) * TH;
+    x0 = (tr % p.tiles_w) * TW;
+  };
+  auto fetch = [&](int tile) {
+    int i0, y0, x0;
+    tile_origin(tile, i0, y0, x0);
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int m = (tid >> 3) + it * 32;
+      const int mi = m / (TH * TW), mr = m % (TH * TW);
+      const int oy = y0 + mr / TW, ox = x0 + mr % TW, img = i0 + mi;
+      yv[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (img < p.NF && oy < p.OH && ox < p.OW)
+        yv[it] = *reinterpret_cast<const f32x4*>(p.dY + (((int64_t)img * p.OH + oy) * p.OW + ox) * p.Co + co0 + c4);
+    }
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int row = (tid >> 3) + it * 32;
+      const int im = row / (PH * PW), rr = row % (PH * PW);
+      const int iy = y0 * S - 1 + rr / PW, ix = x0 * S - 1 + rr % PW, img = i0 + im;
+      pv[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (row < PROWS && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
+        pv[it] = *reinterpret_cast<const f32x4*>(p.src + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.Ci + ci0 + c4);
+    }
+  };
+  f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+  if (p.scale) {
+    sc = *reinterpret_cast<const f32x4*>(p.scale + ci0 + c4);
+    sh = *reinterpret_cast<const f32x4*>(p.shift + ci0 + c4);
+  }
+  auto stash = [&]() {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) *reinterpret_cast<f32x4*>(ys + ((tid >> 3) + it * 32) * 32 + c4) = yv[it];
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int row = (tid >> 3) + it * 32;
+      if (row < PROWS) {
+        const int im = row / (PH * PW), rr = row % (PH * PW);
+        const int py = rr / PW, px = rr % PW;
+        const int iy = oy0 * S - 1 + py, ix = ox0 * S - 1 + px;
+        f32x4 v = pv[it];
+        if (p.scale && img0 + im < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
+        }
+        const int col = S == 1 ? px : ((px & 1) ? PWE + (px >> 1) : (px >> 1));
+        *reinterpret_cast<f32x4*>(xs + ((im * PH + py) * PW + col) * 32 + c4) = v;
+      }
+    }
+  };
+
+  int tile = blockIdx.z;
+  if (tile < p.ntiles) fetch(tile);
+  for (; tile < p.ntiles; tile += gridDim.z) {
+    tile_origin(tile, img0, oy0, ox0);
+    __syncthreads();
+    stash();
+    __syncthreads();
+    if (tile + (int)gridDim.z < p.ntiles) fetch(tile + gridDim.z);
+#pragma unroll 4
+    for (int s2 = 0; s2 < 16; ++s2) {
+      const int m = wave * 32 + 2 * s2 + h;
+      const int mi = m / (TH * TW), mr = m % (TH * TW);
+      const int py = mr / TW, px = mr % TW;
+      const float a = ys[m * 32 + j];
+      const float* xb = xs + ((mi * PH + py * S) * PW) * 32 + j;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int kh = t / 3, kw = t % 3;
+        const int col = S == 1 ? px + kw : ((kw & 1) ? PWE + px + (kw >> 1) : px + (kw >> 1));
+        const float b = xb[(kh * PW + col) * 32];
+        acc[t] = mfma32(a, b, acc[t]);
+      }
+    }
+  }
+
+  // fixed-order combine of the 4 waves: (2,3) -> (0,1), then 1 -> 0
+  __syncthreads();
+  float* red = sm;
+  if (wave >= 2) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[(((wave - 2) * 9 + t) * 16 + r) * 64 + lane] = acc[t][r];
+  }
+  __syncthreads();
+  if (wave < 2) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] += red[((wave * 9 + t) * 16 + r) * 64 + lane];
+  }
+  __syncthreads();
+  if (wave == 1) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[(t * 16 + r) * 64 + lane] = acc[t][r];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float* out = p.slab + (int64_t)blockIdx.z * p.Co * 9 * p.Ci;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        out[(int64_t)co * 9 * p.Ci + t * p.Ci + ci0 + j] = acc[t][r] + red[(t * 16 + r) * 64 + lane];
+      }
+  }
+}
+
+template <int S, int NI, int TH, int TW>
+static int launch_wgrad_patch(WgradPatchArgs a, int target_blocks, int64_t partial_cap, hipStream_t st,
+                              int* nsplit) {
+  a.tiles_h = (int)cdiv(a.OH, TH);
+  a.tiles_w = (int)cdiv(a.OW, TW);
+  a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);
+  const int pairs = (a.Co / 32) * (a.Ci / 32);
+  int64_t z = std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, pairs), a.ntiles));
+  z = std::min<int64_t>(z, std::max<int64_t>(1, partial_cap / ((int64_t)a.Co * 9 * a.Ci)));
+  dim3 grid((unsigned)(a.Co / 32), (unsigned)(a.Ci / 32), (unsigned)z);
+  hipLaunchKernelGGL((conv3x3_wgrad_patch_kernel<S, NI, TH, TW>), grid, dim3(256), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  *nsplit = (int)z;
+  return 0;
+}
+
+bool conv3_wgrad_patch_supported(const Conv3Layer& L) {
+  return (L.stride == 1 || L.stride == 2) && L.Ci % 32 == 0 && L.Co % 32 == 0;
+}
+
+int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
+                      int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st) {
+  VAD_CHECK(conv3_wgrad_patch_supported(L), "conv3_wgrad_patch: stride 1/2, Ci and Co multiples of 32");
+  VAD_CHECK(partial_cap >= (int64_t)L.Co * 9 * L.Ci, "conv3_wgrad_patch: slab capacity below one split");
+  WgradPatchArgs a{};
+  a.dY = dY;
+  a.src = src;
+  a.scale = src_stats ? src_stats + 2 * L.Ci : nullptr;
+  a.shift = src_stats ? src_stats + 3 * L.Ci : nullptr;
+  a.slab = slab;
+  a.NF = L.NF; a.IH = L.IH; a.IW = L.IW; a.Ci = L.Ci; a.OH = L.OH; a.OW = L.OW; a.Co = L.Co;
+  const int g = patch_geom(L.OH, L.OW);
+  if (L.stride == 1) {
+    if (g == 0) return launch_wgrad_patch<1, 2, 8, 8>(a, target_blocks, partial_cap, st, nsplit);
+    if (g == 1) return launch_wgrad_patch<1, 1, 8, 16>(a, target_blocks, partial_cap, st, nsplit);
+    return launch_wgrad_patch<1, 1, 4, 32>(a, target_blocks, partial_cap, st, nsplit);
+  }
+  if (g == 0) return launch_wgrad_patch<2, 2, 8, 8>(a, target_blocks, partial_cap, st, nsplit);
+  if (g == 1) return launch_wgrad_patch<2, 1, 8, 16>(a, target_blocks, partial_cap, st, nsplit);
+  return launch_wgrad_patch<2, 1, 4, 32>(a, target_blocks, partial_cap, st, nsplit);
 }
 
 }  // namespace vad

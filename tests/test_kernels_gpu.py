@@ -98,12 +98,16 @@ def test_device_synth_frames_bitexact():
 
 
 WGRAD_CASES = [(2, 32, 32, 19, 17, 1), (32, 256, 256, 8, 8, 1), (32, 128, 256, 15, 15, 2), (32, 32, 32, 57, 57, 1),
-               (8, 64, 64, 29, 29, 1), (3, 64, 128, 15, 15, 2)]
+               (8, 64, 64, 29, 29, 1), (3, 64, 128, 15, 15, 2),
+               # LDS-patch geometries: stride-2 4x32 tiles, 2x8x8 tiles with odd NF (both strides), tiny frames
+               (3, 32, 64, 57, 57, 2), (5, 64, 64, 8, 8, 1), (3, 128, 256, 15, 15, 2), (2, 32, 32, 5, 3, 1)]
 
 
+@pytest.mark.parametrize("patch", [1, 0, 2])
 @pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", WGRAD_CASES)
-def test_conv3x3_wgrad(NF, Ci, Co, IH, IW, s):
+def test_conv3x3_wgrad(NF, Ci, Co, IH, IW, s, patch):
     nat = _lib()
+    nat.lib().vad_set_tuning(b"conv_wgrad_patch", patch)
     g = torch.Generator().manual_seed(NF * 5 + Ci + Co + IH)
     x = torch.randn(NF, Ci, IH, IW, generator=g)
     w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
@@ -119,5 +123,6 @@ def test_conv3x3_wgrad(NF, Ci, Co, IH, IW, s):
     nat.check(nat.lib().vad_conv3x3_wgrad(xh.data_ptr(), dyh.data_ptr(), NF, Ci, IH, IW, Co, s, dW.data_ptr(),
                                           part.data_ptr(), part.numel(), nat.stream_of(d)))
     torch.cuda.synchronize()
+    nat.lib().vad_set_tuning(b"conv_wgrad_patch", 1)
     ref = wr.grad
     np.testing.assert_allclose(dW.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4 * float(ref.abs().max()))

@@ -67,10 +67,15 @@ def main():
         nat.check(L.vad_conv3x3_forward(x.data_ptr(), NF, ci, ih, iw, wt.data_ptr(), bias.data_ptr(), co, s,
                                         y.data_ptr(), wf.data_ptr(), wd.data_ptr(), parts.data_ptr(), st))
         if a.patch:
-            for op in ("fwd", "dgrad"):
+            for op in ("fwd", "dgrad", "wgrad"):
                 for on in (0, 1):
                     L.vad_set_tuning(b"conv_patch", on)
-                    if op == "fwd":
+                    L.vad_set_tuning(b"conv_wgrad_patch", on)
+                    if op == "wgrad":
+                        fn = lambda: nat.check(L.vad_conv3x3_wgrad(
+                            x.data_ptr(), dy.data_ptr(), NF, ci, ih, iw, co, s, dW.data_ptr(), part.data_ptr(),
+                            part.numel(), st))
+                    elif op == "fwd":
                         fn = lambda: nat.check(L.vad_conv3x3_forward(
                             x.data_ptr(), NF, ci, ih, iw, None, bias.data_ptr(), co, s, y.data_ptr(), wf.data_ptr(),
                             wd.data_ptr(), parts.data_ptr(), st))
@@ -82,6 +87,7 @@ def main():
                     r = dict(layer=li, op=op, patch=on, ms=round(ms, 4), tflops=round(flops / ms / 1e9, 2))
                     print(json.dumps(r), flush=True)
             L.vad_set_tuning(b"conv_patch", 1)
+            L.vad_set_tuning(b"conv_wgrad_patch", 1)
             continue
         for op in ("fwd", "dgrad", "wgrad"):
             ids = [0, 1, 2, 3, 4, 5, 6, 9] if op != "wgrad" else [2, 3, 4, 5, 7, 8, 9]
