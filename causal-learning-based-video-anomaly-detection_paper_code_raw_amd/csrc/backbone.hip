@@ -751,9 +751,9 @@ static int dgrad_classes(int stride, DgradClass* cls) {
   return n;
 }
 
-// dgrad weight images: stride 1 -> Wd[ci][t=kh*3+kw][co]; stride 2 -> per class, concatenated,
-// Wd_c[ci][ri*nct+cj][co] for taps (kh[ri], kw[cj]).
-__global__ void conv3_prep_kernel(const float* __restrict__ w, int Ci, int Co, int stride, float* __restrict__ wf,
+// dgrad weight images: stride 1 and the stride-2 patch kernel -> Wd[ci][t=kh*3+kw][co]; stride-2 GEMM path -> per
+// class, concatenated, Wd_c[ci][ri*nct+cj][co] for taps (kh[ri], kw[cj]).
+__global__ void conv3_prep_kernel(const float* __restrict__ w, int Ci, int Co, int classes, float* __restrict__ wf,
                                   float* __restrict__ wd) {
   const int64_t total = (int64_t)Co * Ci * 9;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
@@ -763,7 +763,7 @@ __global__ void conv3_prep_kernel(const float* __restrict__ w, int Ci, int Co, i
     const float v = w[i];
     wf[((int64_t)co * 9 + t) * Ci + ci] = v;
     const int kh = t / 3, kw = t % 3;
-    if (stride == 1) {
+    if (!classes) {
       wd[((int64_t)ci * 9 + t) * Co + co] = v;
     } else {
       // class (ph,pw): kh valid iff (ph+1-kh) even -> ph = (kh+1)&1; its index among the class's row taps
@@ -783,7 +783,8 @@ __global__ void conv3_prep_kernel(const float* __restrict__ w, int Ci, int Co, i
 
 int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd, hipStream_t st) {
   const int64_t total = (int64_t)L.Co * L.Ci * 9;
-  hipLaunchKernelGGL(conv3_prep_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, w, L.Ci, L.Co, L.stride,
+  const int classes = L.stride == 2 && !(g_tune.patch && conv3_patch_supported(L, false));
+  hipLaunchKernelGGL(conv3_prep_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, w, L.Ci, L.Co, classes,
                      wf, wd);
   VAD_LAUNCH_CHECK();
   return 0;

@@ -1,22 +1,23 @@
-// Direct 3x3 convolution over an LDS-resident input patch, on f32 MFMA (v_mfma_f32_32x32x2_f32).
+// Direct 3x3 convolutions over an LDS-resident input patch, on f32 MFMA (v_mfma_f32_32x32x2_f32).
 //
 // The implicit GEMM (gemm.h) re-gathers the input from L2 for every one of the 9 taps and synchronises every
 // 32-wide K slice.  Here a block owns 128 output pixels (NI images x TH x TW) x 32 output channels and walks the
-// reduction channels in chunks of 32: per chunk it stages the input patch (tile + 1-pixel halo, BN+ReLU of the
-// producing layer applied while staging, zero padding) and the 32 x (9 taps x 32) weight slice in LDS once, then
-// every wave issues 9 x 4 x 4 = 144 MFMAs on its 32 pixels with only LDS reads in between (one ds_read_b128 of A
-// and one of B feed 4 MFMAs; rows padded to 36 / 292 floats so the 16-lane read groups are conflict-free).
-// Used for stride-1 forward convs (BN statistics in the epilogue) and stride-1 input gradients (flipped taps).
+// reduction channels in chunks of PC: per chunk it stages the input patch (tile + halo, BN+ReLU of the producing
+// layer applied while staging, zero padding) and the 32 x (9 taps x PC) weight slice in LDS once, then every
+// wave issues 9 x PC/2 MFMAs on its 32 pixels with only LDS reads in between (one ds_read_b128 of A and one of
+// B feed 4 MFMAs; rows padded to PC+4 / 9PC+4 floats so the 16-lane read groups cover all 64 banks).
+// Global loads of chunk c+1 are issued into registers before chunk c is multiplied.
+//   conv3x3_patch_kernel        stride-1/2 forward (BN statistics in the epilogue), stride-1 input gradient
+//   conv3x3_dgrad_s2_kernel     stride-2 input gradient: 4 parity classes of a 16x16 dX tile share one dY patch
+//   conv3x3_wgrad_patch_kernel  weight gradient (split-K over pixel tiles)
+// Stride-2 patches store their columns de-interleaved by parity so consecutive output pixels read consecutive
+// patch rows.
 #include <algorithm>
 
 #include "backbone.h"
 #include "gemm.h"
 
 namespace vad {
-
-constexpr int PC = 32;            // reduction channels per chunk
-constexpr int PROW = PC + 4;      // patch row stride (floats)
-constexpr int WROW = 9 * PC + 4;  // weight row stride (floats)
 
 struct PatchArgs {
   const float* src;    // NHWC [NF][IH][IW][C]
@@ -30,10 +31,38 @@ struct PatchArgs {
   int tiles_h, tiles_w;
 };
 
-template <int NI, int TH, int TW, bool FWD>
+// Stage one chunk of a weight slice [32 n][9 taps][PC] into LDS rows of 9*PC+4 floats (tap order = LDS order;
+// FLIP reverses the taps, i.e. the stride-1 input gradient's rotated kernel).
+template <int PC, bool FLIP>
+struct WeightStage {
+  static constexpr int CQ = PC / 4, WQ = 32 * 9 * CQ, WIT = (WQ + 255) / 256, WROW = 9 * PC + 4;
+  f32x4 v[WIT];
+  __device__ void fetch(const PatchArgs& p, int n0, int c0, int tid) {
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int q = tid + it * 256;
+      const int n = q / (9 * CQ), t = (q % (9 * CQ)) / CQ, c4 = (q % CQ) * 4;
+      v[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (q < WQ && n0 + n < p.N)
+        v[it] = *reinterpret_cast<const f32x4*>(p.w + ((int64_t)(n0 + n) * 9 + (FLIP ? 8 - t : t)) * p.C + c0 + c4);
+    }
+  }
+  __device__ void stash(float* wl, int tid) const {
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int q = tid + it * 256;
+      const int n = q / (9 * CQ), t = (q % (9 * CQ)) / CQ, c4 = (q % CQ) * 4;
+      if (q < WQ) *reinterpret_cast<f32x4*>(wl + n * WROW + t * PC + c4) = v[it];
+    }
+  }
+};
+
+template <int S, int NI, int TH, int TW, int PC, bool FWD>
 __global__ __launch_bounds__(256, 2) void conv3x3_patch_kernel(const PatchArgs p) {
   static_assert(NI * TH * TW == 128, "a block owns 128 output pixels");
-  constexpr int PH = TH + 2, PW = TW + 2, PROWS = NI * PH * PW;
+  static_assert(FWD || S == 1, "strided input gradients use conv3x3_dgrad_s2_kernel");
+  constexpr int PROW = PC + 4, WROW = 9 * PC + 4, CQ = PC / 4;
+  constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3, PROWS = NI * PH * PW, PWE = (PW + 1) / 2;
   __shared__ __attribute__((aligned(16))) float sm[PROWS * PROW + 32 * WROW];
   float* patch = sm;
   float* wl = sm + PROWS * PROW;
@@ -48,42 +77,34 @@ __global__ __launch_bounds__(256, 2) void conv3x3_patch_kernel(const PatchArgs p
   const int m = wave * 32 + (lane & 31);
   const int mi = m / (TH * TW), mr = m % (TH * TW);
   const int py = mr / TW, px = mr % TW;
-  const int arow = (mi * PH + py) * PW + px;  // patch row of tap (0,0)
   const int h = lane >> 5;
   const int j = lane & 31;  // B column (output channel n0 + j)
+  const float* abase = patch + ((mi * PH + py * S) * PW + px) * PROW + 4 * h;
+  const float* bbase = wl + j * WROW + 4 * h;
 
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 
-  // staging: thread tid always handles channel quad c4 = (tid % 8) * 4 (256 % 8 == 0), so BN scale/shift are
-  // per-thread constants; all global loads of a chunk are issued back to back into registers, the chunk after
-  // the current one is fetched while the current one is multiplied.
-  constexpr int PQ = PROWS * (PC / 4), PIT = (PQ + 255) / 256;
-  constexpr int WQ = 32 * 9 * (PC / 4), WIT = WQ / 256;
-  static_assert(WQ % 256 == 0, "weight staging is exact");
-  const int c4 = (tid % (PC / 4)) * 4;
-  f32x4 pv[PIT], wv[WIT];
+  // staging: thread tid always handles channel quad c4 = (tid % CQ) * 4, so BN scale/shift are per-thread
+  // constants
+  constexpr int PQ = PROWS * CQ, PIT = (PQ + 255) / 256;
+  const int c4 = (tid % CQ) * 4;
+  f32x4 pv[PIT];
+  WeightStage<PC, !FWD> ws;
   auto fetch = [&](int c0) {
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
       const int q = tid + it * 256;
-      const int row = q / (PC / 4);
+      const int row = q / CQ;
       const int im = row / (PH * PW), rr = row % (PH * PW);
-      const int iy = oy0 - 1 + rr / PW, ix = ox0 - 1 + rr % PW;
+      const int iy = oy0 * S - 1 + rr / PW, ix = ox0 * S - 1 + rr % PW;
       const int img = img0 + im;
       pv[it] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (q < PQ && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
         pv[it] = *reinterpret_cast<const f32x4*>(p.src + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C + c0 + c4);
     }
-#pragma unroll
-    for (int it = 0; it < WIT; ++it) {
-      const int q = tid + it * 256;
-      const int n = q / (9 * PC / 4), t = (q % (9 * PC / 4)) / (PC / 4);
-      const int tw = FWD ? t : 8 - t;
-      wv[it] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (n0 + n < p.N) wv[it] = *reinterpret_cast<const f32x4*>(p.w + ((int64_t)(n0 + n) * 9 + tw) * p.C + c0 + c4);
-    }
+    ws.fetch(p, n0, c0, tid);
   };
   auto stash = [&](int c0) {
     f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
@@ -96,26 +117,23 @@ __global__ __launch_bounds__(256, 2) void conv3x3_patch_kernel(const PatchArgs p
     for (int it = 0; it < PIT; ++it) {
       const int q = tid + it * 256;
       if (q < PQ) {
-        const int row = q / (PC / 4);
+        const int row = q / CQ;
+        const int im = row / (PH * PW), rr = row % (PH * PW);
+        const int ry = rr / PW, rx = rr % PW;
         f32x4 v = pv[it];
         if (bn) {
           // zero padding stays zero: padded taps read 0 in the reference's relu(bn(y)) zero-padded input
-          const int im = row / (PH * PW), rr = row % (PH * PW);
-          const int iy = oy0 - 1 + rr / PW, ix = ox0 - 1 + rr % PW;
+          const int iy = oy0 * S - 1 + ry, ix = ox0 * S - 1 + rx;
           if (img0 + im < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
           }
         }
-        *reinterpret_cast<f32x4*>(patch + row * PROW + c4) = v;
+        const int col = S == 1 ? rx : ((rx & 1) ? PWE + (rx >> 1) : (rx >> 1));
+        *reinterpret_cast<f32x4*>(patch + ((im * PH + ry) * PW + col) * PROW + c4) = v;
       }
     }
-#pragma unroll
-    for (int it = 0; it < WIT; ++it) {
-      const int q = tid + it * 256;
-      const int n = q / (9 * PC / 4), t = (q % (9 * PC / 4)) / (PC / 4);
-      *reinterpret_cast<f32x4*>(wl + n * WROW + t * PC + c4) = wv[it];
-    }
+    ws.stash(wl, tid);
   };
 
   fetch(0);
@@ -124,25 +142,22 @@ __global__ __launch_bounds__(256, 2) void conv3x3_patch_kernel(const PatchArgs p
     stash(c0);
     __syncthreads();
     if (c0 + PC < p.C) fetch(c0 + PC);
-    // 36 steps of (one A quad, one B quad) -> 4 MFMAs; the next step's quads are read before this step's MFMAs
-    const float* abase = patch + arow * PROW + 4 * h;
-    const float* bbase = wl + j * WROW + 4 * h;
-    f32x4 a4 = *reinterpret_cast<const f32x4*>(abase);
-    f32x4 b4 = *reinterpret_cast<const f32x4*>(bbase);
+    // 9*PC/8 steps of (one A quad, one B quad) -> 4 MFMAs
 #pragma unroll
-    for (int s = 0; s < 36; ++s) {
-      f32x4 an = a4, bn = b4;
-      if (s + 1 < 36) {
-        const int t = (s + 1) >> 2, kk = (s + 1) & 3;
-        an = *reinterpret_cast<const f32x4*>(abase + ((t / 3) * PW + (t % 3)) * PROW + kk * 8);
-        bn = *reinterpret_cast<const f32x4*>(bbase + t * PC + kk * 8);
+    for (int t = 0; t < 9; ++t) {
+      const int kh = t / 3, kw = t % 3;
+      const int kwo = S == 1 ? kw : ((kw & 1) ? PWE + (kw >> 1) : (kw >> 1));
+      const float* ap = abase + (kh * PW + kwo) * PROW;
+      const float* bp = bbase + t * PC;
+#pragma unroll
+      for (int kk = 0; kk < PC / 8; ++kk) {
+        const f32x4 a4 = *reinterpret_cast<const f32x4*>(ap + kk * 8);
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(bp + kk * 8);
+        acc = mfma32(a4[0], b4[0], acc);
+        acc = mfma32(a4[1], b4[1], acc);
+        acc = mfma32(a4[2], b4[2], acc);
+        acc = mfma32(a4[3], b4[3], acc);
       }
-      acc = mfma32(a4[0], b4[0], acc);
-      acc = mfma32(a4[1], b4[1], acc);
-      acc = mfma32(a4[2], b4[2], acc);
-      acc = mfma32(a4[3], b4[3], acc);
-      a4 = an;
-      b4 = bn;
     }
   }
 
@@ -183,13 +198,114 @@ __global__ __launch_bounds__(256, 2) void conv3x3_patch_kernel(const PatchArgs p
   }
 }
 
-template <int NI, int TH, int TW, bool FWD>
+// Stride-2 input gradient.  dX pixel (2i+ph, 2j+pw) only sees the taps whose parity matches (ph, pw):
+// rows kh=1 (dY row i) for ph=0, kh=0 (row i+1) and kh=2 (row i) for ph=1; same for columns.  A block owns the
+// 16x16 dX tile of class pixels i in [i0, i0+8), j in [j0, j0+8): all four classes read the same 9x9 dY patch.
+// Work per (class, half of the 8x8 class tile) = its tap count (1/2/2/4 x 32 pixels); the waves take
+// (11,00), (11,00), (01,10), (01,10) pairs -> 5/5/4/4 taps.
+template <int PC, int CPH, int CPW>
+__device__ __forceinline__ void dgrad_s2_class(f32x16& acc, const float* pbase, const float* bbase) {
+  constexpr int PROW = PC + 4;
+#pragma unroll
+  for (int a = 0; a < (CPH ? 2 : 1); ++a) {
+    const int kh = CPH ? (a == 0 ? 0 : 2) : 1, dh = (CPH && a == 0) ? 1 : 0;
+#pragma unroll
+    for (int b = 0; b < (CPW ? 2 : 1); ++b) {
+      const int kw = CPW ? (b == 0 ? 0 : 2) : 1, dw = (CPW && b == 0) ? 1 : 0;
+      const float* ap = pbase + (dh * 9 + dw) * PROW;
+      const float* bp = bbase + (kh * 3 + kw) * PC;
+#pragma unroll
+      for (int kk = 0; kk < PC / 8; ++kk) {
+        const f32x4 a4 = *reinterpret_cast<const f32x4*>(ap + kk * 8);
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(bp + kk * 8);
+        acc = mfma32(a4[0], b4[0], acc);
+        acc = mfma32(a4[1], b4[1], acc);
+        acc = mfma32(a4[2], b4[2], acc);
+        acc = mfma32(a4[3], b4[3], acc);
+      }
+    }
+  }
+}
+
+// p.src = dY [NF][IH=OHy][IW=OWy][C=Co], p.w = Wd [Ci][9][Co], p.out = dX [NF][OH=XH][OW=XW][N=Ci]
+template <int PC>
+__global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2_kernel(const PatchArgs p) {
+  constexpr int PROW = PC + 4, WROW = 9 * PC + 4, CQ = PC / 4, PROWS = 81;
+  __shared__ __attribute__((aligned(16))) float sm[PROWS * PROW + 32 * WROW];
+  float* patch = sm;
+  float* wl = sm + PROWS * PROW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_per_img = p.tiles_h * p.tiles_w;
+  const int img = blockIdx.x / tiles_per_img;
+  const int trem = blockIdx.x % tiles_per_img;
+  const int i0 = (trem / p.tiles_w) * 8, j0 = (trem % p.tiles_w) * 8;
+  const int n0 = blockIdx.y * 32;
+  const int h = lane >> 5, j = lane & 31;
+  const int g = wave & 1;  // half of the 8x8 class tile (class rows 4g..4g+3)
+  const float* pbase = patch + ((4 * g + (lane & 31) / 8) * 9 + (lane & 31) % 8) * PROW + 4 * h;
+  const float* bbase = wl + j * WROW + 4 * h;
+
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+
+  constexpr int PQ = PROWS * CQ, PIT = (PQ + 255) / 256;
+  const int c4 = (tid % CQ) * 4;
+  f32x4 pv[PIT];
+  WeightStage<PC, false> ws;
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = tid + it * 256;
+      const int row = q / CQ;
+      const int y = i0 + row / 9, x = j0 + row % 9;
+      pv[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (q < PQ && y < p.IH && x < p.IW)
+        pv[it] = *reinterpret_cast<const f32x4*>(p.src + (((int64_t)img * p.IH + y) * p.IW + x) * p.C + c0 + c4);
+    }
+    ws.fetch(p, n0, c0, tid);
+  };
+  fetch(0);
+  for (int c0 = 0; c0 < p.C; c0 += PC) {
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = tid + it * 256;
+      if (q < PQ) *reinterpret_cast<f32x4*>(patch + (q / CQ) * PROW + c4) = pv[it];
+    }
+    ws.stash(wl, tid);
+    __syncthreads();
+    if (c0 + PC < p.C) fetch(c0 + PC);
+    if (wave < 2) {
+      dgrad_s2_class<PC, 1, 1>(acc0, pbase, bbase);
+      dgrad_s2_class<PC, 0, 0>(acc1, pbase, bbase);
+    } else {
+      dgrad_s2_class<PC, 0, 1>(acc0, pbase, bbase);
+      dgrad_s2_class<PC, 1, 0>(acc1, pbase, bbase);
+    }
+  }
+
+  const int col = n0 + j;
+  const int ph0 = wave < 2 ? 1 : 0, pw0 = 1;  // acc0 class: (1,1) or (0,1)
+  const int ph1 = wave < 2 ? 0 : 1, pw1 = 0;  // acc1 class: (0,0) or (1,0)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int pm = (r & 3) + 8 * (r >> 2) + 4 * h;
+    const int ci_ = i0 + 4 * g + pm / 8, cj = j0 + pm % 8;
+    const int y0 = 2 * ci_ + ph0, x0 = 2 * cj + pw0;
+    if (y0 < p.OH && x0 < p.OW && col < p.N) p.out[(((int64_t)img * p.OH + y0) * p.OW + x0) * p.N + col] = acc0[r];
+    const int y1 = 2 * ci_ + ph1, x1 = 2 * cj + pw1;
+    if (y1 < p.OH && x1 < p.OW && col < p.N) p.out[(((int64_t)img * p.OH + y1) * p.OW + x1) * p.N + col] = acc1[r];
+  }
+}
+
+template <int S, int NI, int TH, int TW, int PC, bool FWD>
 static int launch_patch(PatchArgs a, hipStream_t st, int* nparts) {
   a.tiles_h = (int)cdiv(a.OH, TH);
   a.tiles_w = (int)cdiv(a.OW, TW);
   const int64_t gx = cdiv(a.NF, NI) * a.tiles_h * a.tiles_w;
   dim3 grid((unsigned)gx, (unsigned)cdiv(a.N, 32));
-  hipLaunchKernelGGL((conv3x3_patch_kernel<NI, TH, TW, FWD>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv3x3_patch_kernel<S, NI, TH, TW, PC, FWD>), grid, dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   if (nparts) *nparts = (int)gx;
   return 0;
@@ -198,12 +314,14 @@ static int launch_patch(PatchArgs a, hipStream_t st, int* nparts) {
 // tile geometry per output size (128 pixels per block): 0 -> 2 images x 8x8, 1 -> 8x16, 2 -> 4x32
 static int patch_geom(int OH, int OW) { return (OH <= 8 && OW <= 8) ? 0 : (OW <= 16 ? 1 : 2); }
 
-template <bool FWD>
+// stride 1: 32-channel chunks; stride 2 (4x the patch pixels): 16-channel chunks keep 2 blocks per CU
+template <int S, bool FWD>
 static int dispatch_patch(const PatchArgs& a, hipStream_t st, int* nparts) {
+  constexpr int PC = S == 1 ? 32 : 16;
   switch (patch_geom(a.OH, a.OW)) {
-    case 0: return launch_patch<2, 8, 8, FWD>(a, st, nparts);
-    case 1: return launch_patch<1, 8, 16, FWD>(a, st, nparts);
-    default: return launch_patch<1, 4, 32, FWD>(a, st, nparts);
+    case 0: return launch_patch<S, 2, 8, 8, PC, FWD>(a, st, nparts);
+    case 1: return launch_patch<S, 1, 8, 16, PC, FWD>(a, st, nparts);
+    default: return launch_patch<S, 1, 4, 32, PC, FWD>(a, st, nparts);
   }
 }
 
@@ -216,12 +334,13 @@ int64_t conv3_patch_blocks(int NF, int OH, int OW) {
 }
 
 bool conv3_patch_supported(const Conv3Layer& L, bool fwd) {
-  return L.stride == 1 && (fwd ? L.Ci : L.Co) % PC == 0;
+  if (L.stride != 1 && L.stride != 2) return false;
+  return fwd ? L.Ci % 16 == 0 && (L.stride == 2 || L.Ci % 32 == 0) : L.Co % 32 == 0;
 }
 
 int conv3_patch_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
                     float* y, float* partials, int* nparts, hipStream_t st) {
-  VAD_CHECK(conv3_patch_supported(L, true), "conv3_patch_fwd: stride-1, Ci % 32 == 0 only");
+  VAD_CHECK(conv3_patch_supported(L, true), "conv3_patch_fwd: unsupported stride / channel count");
   PatchArgs a{};
   a.src = src;
   a.scale = src_stats ? src_stats + 2 * L.Ci : nullptr;
@@ -231,19 +350,26 @@ int conv3_patch_fwd(const Conv3Layer& L, const float* src, const float* src_stat
   a.out = y;
   a.partials = partials;
   a.NF = L.NF; a.IH = L.IH; a.IW = L.IW; a.C = L.Ci; a.OH = L.OH; a.OW = L.OW; a.N = L.Co;
-  return dispatch_patch<true>(a, st, nparts);
+  return L.stride == 1 ? dispatch_patch<1, true>(a, st, nparts) : dispatch_patch<2, true>(a, st, nparts);
 }
 
+// wd: [Ci][9][Co] with the original tap order (conv3_prep_weights writes this layout for every stride while the
+// patch path is on)
 int conv3_patch_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st) {
-  VAD_CHECK(conv3_patch_supported(L, false), "conv3_patch_dgrad: stride-1, Co % 32 == 0 only");
+  VAD_CHECK(conv3_patch_supported(L, false), "conv3_patch_dgrad: unsupported stride / channel count");
   PatchArgs a{};
   a.src = dY;
   a.w = wd;
   a.out = dX;
   a.NF = L.NF; a.IH = L.OH; a.IW = L.OW; a.C = L.Co; a.OH = L.IH; a.OW = L.IW; a.N = L.Ci;
-  return dispatch_patch<false>(a, st, nullptr);
+  if (L.stride == 1) return dispatch_patch<1, false>(a, st, nullptr);
+  a.tiles_h = (int)cdiv(cdiv(L.IH, 2), 8);
+  a.tiles_w = (int)cdiv(cdiv(L.IW, 2), 8);
+  dim3 grid((unsigned)((int64_t)L.NF * a.tiles_h * a.tiles_w), (unsigned)cdiv(L.Ci, 32));
+  hipLaunchKernelGGL((conv3x3_dgrad_s2_kernel<32>), grid, dim3(256), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  return 0;
 }
-
 
 // =====================================================================================================
 // Weight gradient: dW[co][t][ci] = sum_p dY[p][co] * relu(bn(x))[p + off_t][ci].

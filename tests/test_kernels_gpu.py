@@ -41,12 +41,16 @@ CONV_CASES = [(2, 32, 32, 19, 17, 1), (2, 32, 64, 29, 29, 2), (1, 64, 128, 15, 1
               (3, 64, 64, 10, 7, 2), (1, 256, 256, 8, 8, 1),
               # stride-1 shapes of the LDS-patch kernels: 2x8x8 tiles with odd NF, 8x16, 4x32 (57-wide, ragged)
               (3, 32, 32, 8, 8, 1), (2, 64, 64, 15, 15, 1), (1, 32, 32, 57, 57, 1), (2, 128, 128, 29, 29, 1),
-              (2, 32, 64, 5, 3, 1)]
+              (2, 32, 64, 5, 3, 1),
+              # stride-2 patch geometries (4x32 / 8x16 / 2x8x8 forward tiles, 16x16 dX parity tiles), odd sizes
+              (2, 32, 64, 57, 57, 2), (3, 128, 256, 16, 16, 2), (1, 64, 128, 31, 18, 2)]
 
 
+@pytest.mark.parametrize("patch", [1, 0])
 @pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", CONV_CASES)
-def test_conv3x3_forward_and_dgrad(NF, Ci, Co, IH, IW, s):
+def test_conv3x3_forward_and_dgrad(NF, Ci, Co, IH, IW, s, patch):
     nat = _lib()
+    nat.lib().vad_set_tuning(b"conv_patch", patch)
     g = torch.Generator().manual_seed(NF * 7 + Ci + Co + IH)
     x = torch.randn(NF, Ci, IH, IW, generator=g)
     w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
@@ -75,6 +79,7 @@ def test_conv3x3_forward_and_dgrad(NF, Ci, Co, IH, IW, s):
     nat.check(nat.lib().vad_conv3x3_dgrad(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, s, dx.data_ptr(),
                                           wf.data_ptr(), wd.data_ptr(), st))
     torch.cuda.synchronize()
+    nat.lib().vad_set_tuning(b"conv_patch", 1)
     np.testing.assert_allclose(dx.cpu().permute(0, 3, 1, 2).numpy(), xr.grad.numpy(), rtol=1e-4, atol=1e-4)
 
 

@@ -79,10 +79,10 @@ def main():
                         fn = lambda: nat.check(L.vad_conv3x3_forward(
                             x.data_ptr(), NF, ci, ih, iw, None, bias.data_ptr(), co, s, y.data_ptr(), wf.data_ptr(),
                             wd.data_ptr(), parts.data_ptr(), st))
-                    else:
+                    else:  # the dgrad weight layout depends on the path: re-prepare
                         fn = lambda: nat.check(L.vad_conv3x3_dgrad(
-                            dy.data_ptr(), NF, ci, ih, iw, None, co, s, dx.data_ptr(), wf.data_ptr(), wd.data_ptr(),
-                            st))
+                            dy.data_ptr(), NF, ci, ih, iw, wt.data_ptr(), co, s, dx.data_ptr(), wf.data_ptr(),
+                            wd.data_ptr(), st))
                     ms = timeit(fn)
                     r = dict(layer=li, op=op, patch=on, ms=round(ms, 4), tflops=round(flops / ms / 1e9, 2))
                     print(json.dumps(r), flush=True)
