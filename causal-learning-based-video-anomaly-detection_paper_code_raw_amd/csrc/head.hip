@@ -711,44 +711,73 @@ __global__ __launch_bounds__(256) void head_rows_bwd_kernel(HeadArgs a, const fl
   }
 }
 
-// GRU + ReID weight/bias grads: fixed-order reductions over all R rows, written into the flat grad buffer.
-// out[o][i] = sum_r A[r][o] * B[r][i]  (bias: sum_r A[r][o])
+// GRU + ReID weight/bias grads over all R trajectory rows (five Linear-style pairs):
+//   dW[o][i] = sum_r A[r][o] * X[r][i],  db[o] = sum_r A[r][o]   (X's extra column I == ones -> the bias)
+// One block per 32x32 tile of [O][I+1]; the 4 waves split the rows (f32 MFMA, 2 rows per step, operands straight
+// from L2: every A/X element is read by the (I+1)/32 / O/32 tiles that need it), then combine in a fixed order.
 struct WSeg {
-  int slot;
-  int64_t dA, dB;
-  int ldA, ldB, O, I;
+  int wslot, bslot;
+  int64_t dA, dX;
+  int O, I;
 };
 
 __global__ __launch_bounds__(256) void head_rows_wgrad_kernel(HeadArgs a) {
   const RowLayout RL((int64_t)a.B * a.T * NMAX);
   const float* rows = a.rows;
-  const int64_t R = RL.R;
-  const WSeg segs[10] = {
-      {H_GRU_WIH, RL.dgi, RL.x, G3, GIN, G3, GIN},   {H_GRU_WHH, RL.dgh, RL.hp, G3, GH, G3, GH},
-      {H_GRU_BIH, RL.dgi, -1, G3, 0, G3, 1},         {H_GRU_BHH, RL.dgh, -1, G3, 0, G3, 1},
-      {H_REID4_W, RL.dp4, RL.rh2, 64, 64, 64, 64},   {H_REID4_B, RL.dp4, -1, 64, 0, 64, 1},
-      {H_REID2_W, RL.dp2, RL.rh1, 64, 32, 64, 32},   {H_REID2_B, RL.dp2, -1, 64, 0, 64, 1},
-      {H_REID0_W, RL.dp0, RL.box, 32, 4, 32, 4},     {H_REID0_B, RL.dp0, -1, 32, 0, 32, 1},
+  const int R = (int)RL.R;
+  const WSeg segs[5] = {
+      {H_GRU_WIH, H_GRU_BIH, RL.dgi, RL.x, G3, GIN}, {H_GRU_WHH, H_GRU_BHH, RL.dgh, RL.hp, G3, GH},
+      {H_REID4_W, H_REID4_B, RL.dp4, RL.rh2, 64, 64}, {H_REID2_W, H_REID2_B, RL.dp2, RL.rh1, 64, 32},
+      {H_REID0_W, H_REID0_B, RL.dp0, RL.box, 32, 4},
   };
-  int64_t total = 0;
-  for (int s = 0; s < 10; ++s) total += (int64_t)segs[s].O * segs[s].I;
-  for (int64_t gidx = blockIdx.x * 256ll + threadIdx.x; gidx < total; gidx += (int64_t)gridDim.x * 256) {
-    int s = 0;
-    int64_t idx = gidx;
-    while (idx >= (int64_t)segs[s].O * segs[s].I) {
-      idx -= (int64_t)segs[s].O * segs[s].I;
-      ++s;
-    }
-    const WSeg& sg = segs[s];
-    const int o = (int)(idx / sg.I), i = (int)(idx - (int64_t)o * sg.I);
-    float acc = 0.f;
-    if (sg.dB >= 0) {
-      for (int64_t r = 0; r < R; ++r) acc = fmaf(rows[sg.dA + r * sg.ldA + o], rows[sg.dB + r * sg.ldB + i], acc);
-    } else {
-      for (int64_t r = 0; r < R; ++r) acc += rows[sg.dA + r * sg.ldA + o];
-    }
-    a.grad[a.off[sg.slot] + idx] = acc;
+  int s = 0, t = blockIdx.x;
+  for (; s < 5; ++s) {
+    const int n = ((segs[s].O + 31) / 32) * ((segs[s].I + 1 + 31) / 32);
+    if (t < n) break;
+    t -= n;
   }
+  if (s >= 5) return;
+  const WSeg sg = segs[s];
+  const int ti = (sg.I + 1 + 31) / 32;
+  const int o0 = (t / ti) * 32, i0 = (t % ti) * 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l = lane & 31;
+  const int o = o0 + l, i = i0 + l;
+  const float* A = rows + sg.dA;
+  const float* X = rows + sg.dX;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int per = (R + 3) / 4;
+  const int r0 = wave * per, r1 = min(R, r0 + per);
+  for (int rb = r0; rb < r1; rb += 2) {  // wave-uniform trip count; row rb + h, zero past the share
+    const int r = rb + h;
+    const bool ok = r < r1;
+    const float av = (ok && o < sg.O) ? A[(int64_t)r * sg.O + o] : 0.f;
+    const float xv = !ok ? 0.f : (i < sg.I ? X[(int64_t)r * sg.I + i] : (i == sg.I ? 1.f : 0.f));
+    acc = mfma32(av, xv, acc);
+  }
+  __shared__ float red[4][16][64];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[r];
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = (red[0][r][lane] + red[1][r][lane]) + (red[2][r][lane] + red[3][r][lane]);
+      const int oo = o0 + (r & 3) + 8 * (r >> 2) + 4 * h, ii = i0 + l;
+      if (oo < sg.O) {
+        if (ii < sg.I) a.grad[a.off[sg.wslot] + (int64_t)oo * sg.I + ii] = v;
+        else if (ii == sg.I) a.grad[a.off[sg.bslot] + oo] = v;
+      }
+    }
+  }
+}
+
+static int head_rows_wgrad_blocks() {
+  const int OI[5][2] = {{G3, GIN}, {G3, GH}, {64, 64}, {64, 32}, {32, 4}};
+  int n = 0;
+  for (auto& x : OI) n += ((x[0] + 31) / 32) * ((x[1] + 1 + 31) / 32);
+  return n;
 }
 
 int head_bwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, const HeadUp& up, float* slabs,
@@ -777,7 +806,7 @@ int head_slab_reduce(const float* slabs, int B, int64_t slab_len, float* grad_he
 }
 
 int head_rows_wgrad(const HeadArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(head_rows_wgrad_kernel, dim3(128), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(head_rows_wgrad_kernel, dim3(head_rows_wgrad_blocks()), dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   return 0;
 }
