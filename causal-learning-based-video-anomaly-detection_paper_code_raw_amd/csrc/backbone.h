@@ -68,7 +68,10 @@ struct DenseAct {
   int64_t row0 = 0;
 };
 int dense_fwd(const float* X, int M, int K, const float* W, const float* b, int N, float* Y, const DenseAct& act,
-              float* scratch, int64_t scratch_floats, hipStream_t st);
+              float* scratch, int64_t scratch_floats, hipStream_t st, int max_splits = 0);
+// split-K partials only: scratch[S][M][N] (finished by mlp_tail_fwd)
+int dense_fwd_splitk(const float* X, int M, int K, const float* W, int N, float* scratch, int64_t scratch_floats,
+                     int* nsplit, hipStream_t st);
 // dX = (dY W) * gate', where gate' = (gate > 0 ? gscale : 0) when gate != nullptr
 int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX, const float* gate, float gscale,
                 const int* skip, hipStream_t st);

@@ -941,13 +941,14 @@ int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, co
 // dense layers
 // =====================================================================================================
 int dense_fwd(const float* X, int M, int K, const float* W, const float* b, int N, float* Y, const DenseAct& act,
-              float* scratch, int64_t scratch_floats, hipStream_t st) {
+              float* scratch, int64_t scratch_floats, hipStream_t st, int max_splits) {
   using C = T64x64;
   DenseEpiArgs pe{Y, N, b, act.relu, act.drop, act.h1, act.thr, act.dscale, act.row0, nullptr, 1.f};
   DenseKC<C::BM>::Params pa{X, K, M, K};
   DenseKC<C::BN>::Params pb{W, K, N, K};
   const int tiles = (int)(cdiv(M, C::BM) * cdiv(N, C::BN));
   int splits = (int)std::min<int64_t>(cdiv(256, tiles), cdiv(K, 4 * BK));
+  if (max_splits > 0) splits = std::min(splits, max_splits);
   while (splits > 1 && (int64_t)splits * M * N > scratch_floats) splits /= 2;
   if (splits <= 1) return launch_gemm<C, DenseKC, DenseKC, EpiDense>(pa, pb, pe, M, N, K, 1, nullptr, st);
   EpiPartial::Params pp{scratch, N};
@@ -958,6 +959,19 @@ int dense_fwd(const float* X, int M, int K, const float* W, const float* b, int 
                      0, st, scratch, used, M, N, pe, nullptr);
   VAD_LAUNCH_CHECK();
   return 0;
+}
+
+int dense_fwd_splitk(const float* X, int M, int K, const float* W, int N, float* scratch, int64_t scratch_floats,
+                     int* nsplit, hipStream_t st) {
+  using C = T64x64;
+  DenseKC<C::BM>::Params pa{X, K, M, K};
+  DenseKC<C::BN>::Params pb{W, K, N, K};
+  const int tiles = (int)(cdiv(M, C::BM) * cdiv(N, C::BN));
+  int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(256, tiles), cdiv(K, 4 * BK)));
+  while (splits > 1 && (int64_t)splits * M * N > scratch_floats) splits /= 2;
+  VAD_CHECK((int64_t)M * N <= scratch_floats, "dense_fwd_splitk: scratch too small");
+  EpiPartial::Params pp{scratch, N};
+  return launch_gemm<C, DenseKC, DenseKC, EpiPartial>(pa, pb, pp, M, N, K, splits, nullptr, st, nsplit);
 }
 
 int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX, const float* gate, float gscale,

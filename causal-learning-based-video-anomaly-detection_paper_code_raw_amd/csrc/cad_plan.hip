@@ -8,6 +8,7 @@
 #include "../../include/vad.h"
 #include "backbone.h"
 #include "head.h"
+#include "mlp.h"
 
 namespace vad {
 
@@ -304,6 +305,7 @@ struct CadPlanImpl {
   // workspace carve
   float *y1, *pool, *y[8], *stats[9], *parts, *wf[8], *wd[8], *feats, *pooled;
   float *dh[5], *dlog, *gh[5], *glog;
+  float* wt[5] = {};  // transposed detector_net weights of layers 1-4 (mlp_tail_fwd)
   float *head_ws, *head_rows;
   int* head_iws;
   float *probs, *finalv, *causal, *kl, *z, *adj, *boxes;
@@ -355,6 +357,7 @@ struct CadPlanImpl {
     dlog = w.take<float>(nf * 20);
     for (int i = 0; i < 4; ++i) gh[i] = w.take<float>((int64_t)B * gd[i]);
     glog = w.take<float>((int64_t)B * 2);
+    for (int i = 1; i < 5; ++i) wt[i] = w.take<float>((int64_t)dd[i - 1] * dd[i]);
     head_ws = w.take<float>((int64_t)B * head_ws_floats(T));
     head_rows = w.take<float>(head_rows_floats(B, T));
     head_iws = w.take<int>((int64_t)B * head_iws_ints(T));
@@ -424,6 +427,79 @@ struct CadPlanImpl {
   }
   HeadOut head_out() const { return HeadOut{causal, kl, z, adj, boxes, counts, nmax, clip_flags}; }
 
+  // layers 1-4 of a 5-layer MLP chain (widths wd[0..5]) on top of h[0]; layer outputs h[1..3] and the logits
+  MlpTailArgs mlp_args(int M, int64_t row0, const int* wd, const int* wslot, const int* bslot, float* const* h,
+                       float* logits, int drop2, float* const* wtr) const {
+    MlpTailArgs m{};
+    m.M = M;
+    m.row0 = row0;
+    for (int i = 0; i < 5; ++i) {
+      const DenseAct a = act(i < 4, i == 1 ? drop2 : 0, 0.2, row0);
+      MlpLayer& L = m.L[i];
+      L.W = P(wslot[i]);
+      L.b = P(bslot[i]);
+      L.out = i < 4 ? h[i] : logits;
+      L.K = wd[i];
+      L.N = wd[i + 1];
+      L.relu = a.relu;
+      L.drop = a.drop;
+      L.h1 = a.h1;
+      L.thr = a.thr;
+      L.dscale = a.dscale;
+      m.WT[i] = i >= 1 ? wtr[i] : nullptr;
+    }
+    return m;
+  }
+  MlpTransposeArgs mlp_transpose_args() const {
+    const CadLayout& LY = layout();
+    const int dd[6] = {6144, 512, 256, 128, 64, 20};
+    MlpTransposeArgs t{};
+    for (int i = 1; i < 5; ++i, ++t.n) {
+      t.W[t.n] = P(LY.det_w[i]);
+      t.WT[t.n] = wt[i];
+      t.K[t.n] = dd[i];
+      t.N[t.n] = dd[i + 1];
+    }
+    return t;
+  }
+  // dropout after layers 0 and 1 (p = 0.3, 0.2): their gates carry the 1/(1-p) scale in training
+  MlpTailBwdArgs mlp_bwd_args(int M, const float* dout, const int* wd, const int* wslot, float* const* h,
+                              float* const* d, const int* skip) const {
+    MlpTailBwdArgs b{};
+    b.M = M;
+    b.dout = dout;
+    for (int i = 0; i < 5; ++i) {
+      b.W[i] = P(wslot[i]);
+      b.K[i] = wd[i];
+      b.N[i] = wd[i + 1];
+    }
+    const double gp[4] = {0.3, 0.2, 0.0, 0.0};
+    for (int i = 0; i < 4; ++i) {
+      b.h[i] = h[i];
+      b.d[i] = d[i];
+      b.gscale[i] = (training && gp[i] > 0) ? (float)(1.0 / (1.0 - gp[i])) : 1.f;
+    }
+    b.skip = skip;
+    return b;
+  }
+  RowsWgradArgs mlp_wgrad_args(int M, const float* dout, const int* wd, const int* wslot, const int* bslot,
+                               float* const* h, float* const* d, const int* skip) const {
+    RowsWgradArgs r{};
+    r.R = M;
+    r.nseg = 4;
+    for (int i = 4; i >= 1; --i) {
+      RowsWgradSeg& sg = r.seg[4 - i];
+      sg.dW = G(wslot[i]);
+      sg.db = G(bslot[i]);
+      sg.A = i == 4 ? dout : d[i];
+      sg.X = h[i - 1];
+      sg.O = wd[i + 1];
+      sg.I = wd[i];
+    }
+    r.skip = skip;
+    return r;
+  }
+
   DenseAct act(bool relu, int stream_id, double p, int64_t row0) const {
     DenseAct a;
     a.relu = relu ? 1 : 0;
@@ -455,27 +531,24 @@ struct CadPlanImpl {
       sst = stats[l + 1];
     }
     TIMED("avgpool", avgpool_fwd(y[7], stats[8], B, T, HF, WF, 256, feats, pooled, st));
-    // detector_net (cad:167-179)
+    // detector_net (cad:167-179): layer 0 as a split-K GEMM, layers 1-4 fused per row block
     const int64_t f0 = clip0 * T;
     const int dd[6] = {6144, 512, 256, 128, 64, 20};
-    const float* in = feats;
-    for (int i = 0; i < 5; ++i) {
-      float* out = i < 4 ? dh[i] : dlog;
-      const int sid = i == 0 ? S_DET_DROP1 : (i == 1 ? S_DET_DROP2 : 0);
-      const double p = i == 0 ? 0.3 : 0.2;
-      TIMED("det_fwd", dense_fwd(in, NF, dd[i], P(LY.det_w[i]), P(LY.det_b[i]), dd[i + 1], out,
-                                 act(i < 4, sid, p, f0), dense_scratch, dense_scratch_floats, st));
-      in = out;
-    }
-    // direct_classifier on the mean over T (cad:525-538, 568-570)
     const int gd[6] = {6144, 512, 256, 128, 64, 2};
+    TIMED("prep", mlp_transpose(mlp_transpose_args(), st));
+    const float* in = feats;
+    TIMED("det_fwd", dense_fwd(in, NF, 6144, P(LY.det_w[0]), P(LY.det_b[0]), 512, dh[0], act(true, S_DET_DROP1, 0.3, f0),
+                               dense_scratch, dense_scratch_floats, st));
+    TIMED("det_fwd", mlp_tail_fwd(mlp_args(NF, f0, dd, LY.det_w, LY.det_b, dh, dlog, S_DET_DROP2, wt), st));
+    // direct_classifier on the mean over T (cad:525-538, 568-570)
+    // (B rows only: one block per 64 columns, so the chain runs layer by layer on many CUs; layers 1-4 unsplit)
     in = pooled;
     for (int i = 0; i < 5; ++i) {
       float* out = i < 4 ? gh[i] : glog;
       const int sid = i == 0 ? S_DIRECT_DROP1 : (i == 1 ? S_DIRECT_DROP2 : 0);
-      const double p = i == 0 ? 0.3 : 0.2;
       TIMED("dir_fwd", dense_fwd(in, B, gd[i], P(LY.dir_w[i]), P(LY.dir_b[i]), gd[i + 1], out,
-                                 act(i < 4, sid, p, clip0), dense_scratch, dense_scratch_floats, st));
+                                 act(i < 4, sid, i == 0 ? 0.3 : 0.2, clip0), dense_scratch, dense_scratch_floats, st,
+                                 i == 0 ? 0 : 1));
       in = out;
     }
     TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
@@ -526,34 +599,31 @@ struct CadPlanImpl {
     TIMED("head_bwd", head_bwd(head_args(), dlog, head_out(), up, slabs, slab_len, d_dlog, st));
     TIMED("head_bwd", head_slab_reduce(slabs, B, slab_len, grads + LY.slots[LY.head0].offset, st));
     TIMED("head_bwd", head_rows_wgrad(head_args(), st));
-    // direct classifier chain
+    // direct classifier chain (B rows): per-layer input-gradient GEMMs spread over many CUs, the layer 1-4 weight
+    // grads in one launch, layer 0 GEMMs
     const int gd[6] = {6144, 512, 256, 128, 64, 2};
-    const double gp[5] = {0.3, 0.2, 0.0, 0.0, 0.0};
-    const float* dcur = d_glog;
-    for (int i = 4; i >= 0; --i) {
-      const float* xin = i == 0 ? pooled : gh[i - 1];
-      TIMED("dir_bwd", dense_wgrad(dcur, B, gd[i + 1], xin, gd[i], G(LY.dir_w[i]), G(LY.dir_b[i]), dense_scratch,
-                                   dense_scratch_floats, nullptr, st));
-      float* dnext = i == 0 ? d_pooled : dg[i - 1];
-      const float gs = (i >= 1 && training && gp[i - 1] > 0) ? (float)(1.0 / (1.0 - gp[i - 1])) : 1.f;
-      TIMED("dir_bwd", dense_dgrad(dcur, B, gd[i + 1], P(LY.dir_w[i]), gd[i], dnext, i == 0 ? nullptr : gh[i - 1], gs,
-                                   nullptr, st));
-      dcur = dnext;
+    const int dd[6] = {6144, 512, 256, 128, 64, 20};
+    {
+      const double gp[4] = {0.3, 0.2, 0.0, 0.0};
+      const float* dcur = d_glog;
+      for (int i = 4; i >= 1; --i) {
+        const float gs = (training && gp[i - 1] > 0) ? (float)(1.0 / (1.0 - gp[i - 1])) : 1.f;
+        TIMED("dir_bwd", dense_dgrad(dcur, B, gd[i + 1], P(LY.dir_w[i]), gd[i], dg[i - 1], gh[i - 1], gs, nullptr,
+                                     st));
+        dcur = dg[i - 1];
+      }
     }
+    TIMED("dir_bwd", rows_wgrad(mlp_wgrad_args(B, d_glog, gd, LY.dir_w, LY.dir_b, gh, dg, nullptr), st));
+    TIMED("dir_bwd", dense_wgrad(dg[0], B, 512, pooled, 6144, G(LY.dir_w[0]), G(LY.dir_b[0]), dense_scratch,
+                                 dense_scratch_floats, nullptr, st));
+    TIMED("dir_bwd", dense_dgrad(dg[0], B, 512, P(LY.dir_w[0]), 6144, d_pooled, nullptr, 1.f, nullptr, st));
     // detector chain (skipped on device when no box was in range: no grads reach it, cad:221-226)
     VAD_HIP(hipMemsetAsync(d_feat_det, 0, sizeof(float) * (size_t)NF * 6144, st));
-    const int dd[6] = {6144, 512, 256, 128, 64, 20};
-    dcur = d_dlog;
-    for (int i = 4; i >= 0; --i) {
-      const float* xin = i == 0 ? feats : dh[i - 1];
-      TIMED("det_bwd", dense_wgrad(dcur, NF, dd[i + 1], xin, dd[i], G(LY.det_w[i]), G(LY.det_b[i]), dense_scratch,
-                                   dense_scratch_floats, flags, st));
-      float* dnext = i == 0 ? d_feat_det : ddh[i - 1];
-      const float gs = (i >= 1 && training && gp[i - 1] > 0) ? (float)(1.0 / (1.0 - gp[i - 1])) : 1.f;
-      TIMED("det_bwd", dense_dgrad(dcur, NF, dd[i + 1], P(LY.det_w[i]), dd[i], dnext, i == 0 ? nullptr : dh[i - 1],
-                                   gs, flags, st));
-      dcur = dnext;
-    }
+    TIMED("det_bwd", mlp_tail_bwd(mlp_bwd_args(NF, d_dlog, dd, LY.det_w, dh, ddh, flags), st));
+    TIMED("det_bwd", rows_wgrad(mlp_wgrad_args(NF, d_dlog, dd, LY.det_w, LY.det_b, dh, ddh, flags), st));
+    TIMED("det_bwd", dense_wgrad(ddh[0], NF, 512, feats, 6144, G(LY.det_w[0]), G(LY.det_b[0]), dense_scratch,
+                                 dense_scratch_floats, flags, st));
+    TIMED("det_bwd", dense_dgrad(ddh[0], NF, 512, P(LY.det_w[0]), 6144, d_feat_det, nullptr, 1.f, flags, st));
     // backbone
     TIMED("avgpool_bwd", avgpool_bwd(d_feat_det, d_pooled, B, T, HF, WF, 256, dA, st));
     for (int l = 7; l >= 0; --l) {

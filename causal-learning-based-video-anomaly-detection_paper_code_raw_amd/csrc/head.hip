@@ -11,6 +11,7 @@
 // Trajectory row r = (b*T + t)*5 + j (j = compacted detection index in frame t = trajectory index n).
 // Deterministic: no atomics; per-clip slabs are reduced in clip order.
 #include "head.h"
+#include "mlp.h"
 
 namespace vad {
 
@@ -711,75 +712,6 @@ __global__ __launch_bounds__(256) void head_rows_bwd_kernel(HeadArgs a, const fl
   }
 }
 
-// GRU + ReID weight/bias grads over all R trajectory rows (five Linear-style pairs):
-//   dW[o][i] = sum_r A[r][o] * X[r][i],  db[o] = sum_r A[r][o]   (X's extra column I == ones -> the bias)
-// One block per 32x32 tile of [O][I+1]; the 4 waves split the rows (f32 MFMA, 2 rows per step, operands straight
-// from L2: every A/X element is read by the (I+1)/32 / O/32 tiles that need it), then combine in a fixed order.
-struct WSeg {
-  int wslot, bslot;
-  int64_t dA, dX;
-  int O, I;
-};
-
-__global__ __launch_bounds__(256) void head_rows_wgrad_kernel(HeadArgs a) {
-  const RowLayout RL((int64_t)a.B * a.T * NMAX);
-  const float* rows = a.rows;
-  const int R = (int)RL.R;
-  const WSeg segs[5] = {
-      {H_GRU_WIH, H_GRU_BIH, RL.dgi, RL.x, G3, GIN}, {H_GRU_WHH, H_GRU_BHH, RL.dgh, RL.hp, G3, GH},
-      {H_REID4_W, H_REID4_B, RL.dp4, RL.rh2, 64, 64}, {H_REID2_W, H_REID2_B, RL.dp2, RL.rh1, 64, 32},
-      {H_REID0_W, H_REID0_B, RL.dp0, RL.box, 32, 4},
-  };
-  int s = 0, t = blockIdx.x;
-  for (; s < 5; ++s) {
-    const int n = ((segs[s].O + 31) / 32) * ((segs[s].I + 1 + 31) / 32);
-    if (t < n) break;
-    t -= n;
-  }
-  if (s >= 5) return;
-  const WSeg sg = segs[s];
-  const int ti = (sg.I + 1 + 31) / 32;
-  const int o0 = (t / ti) * 32, i0 = (t % ti) * 32;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l = lane & 31;
-  const int o = o0 + l, i = i0 + l;
-  const float* A = rows + sg.dA;
-  const float* X = rows + sg.dX;
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  const int per = (R + 3) / 4;
-  const int r0 = wave * per, r1 = min(R, r0 + per);
-  for (int rb = r0; rb < r1; rb += 2) {  // wave-uniform trip count; row rb + h, zero past the share
-    const int r = rb + h;
-    const bool ok = r < r1;
-    const float av = (ok && o < sg.O) ? A[(int64_t)r * sg.O + o] : 0.f;
-    const float xv = !ok ? 0.f : (i < sg.I ? X[(int64_t)r * sg.I + i] : (i == sg.I ? 1.f : 0.f));
-    acc = mfma32(av, xv, acc);
-  }
-  __shared__ float red[4][16][64];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[r];
-  __syncthreads();
-  if (wave == 0) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float v = (red[0][r][lane] + red[1][r][lane]) + (red[2][r][lane] + red[3][r][lane]);
-      const int oo = o0 + (r & 3) + 8 * (r >> 2) + 4 * h, ii = i0 + l;
-      if (oo < sg.O) {
-        if (ii < sg.I) a.grad[a.off[sg.wslot] + (int64_t)oo * sg.I + ii] = v;
-        else if (ii == sg.I) a.grad[a.off[sg.bslot] + oo] = v;
-      }
-    }
-  }
-}
-
-static int head_rows_wgrad_blocks() {
-  const int OI[5][2] = {{G3, GIN}, {G3, GH}, {64, 64}, {64, 32}, {32, 4}};
-  int n = 0;
-  for (auto& x : OI) n += ((x[0] + 31) / 32) * ((x[1] + 1 + 31) / 32);
-  return n;
-}
-
 int head_bwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, const HeadUp& up, float* slabs,
              int64_t slab_len, float* d_det_logits, hipStream_t st) {
   VAD_HIP(hipMemsetAsync(d_det_logits, 0, sizeof(float) * (size_t)a.B * a.T * 20, st));
@@ -805,10 +737,21 @@ int head_slab_reduce(const float* slabs, int B, int64_t slab_len, float* grad_he
   return 0;
 }
 
+// GRU + ReID weight/bias grads over all R trajectory rows: five Linear-style (W, b) pairs, one rows_wgrad launch
 int head_rows_wgrad(const HeadArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(head_rows_wgrad_kernel, dim3(head_rows_wgrad_blocks()), dim3(256), 0, st, a);
-  VAD_LAUNCH_CHECK();
-  return 0;
+  const RowLayout RL((int64_t)a.B * a.T * NMAX);
+  RowsWgradArgs w{};
+  w.R = (int)RL.R;
+  w.nseg = 5;
+  auto seg = [&](int k, int ws, int bs, int64_t dA, int64_t dX, int O, int I) {
+    w.seg[k] = RowsWgradSeg{a.grad + a.off[ws], a.grad + a.off[bs], a.rows + dA, a.rows + dX, O, I};
+  };
+  seg(0, H_GRU_WIH, H_GRU_BIH, RL.dgi, RL.x, G3, GIN);
+  seg(1, H_GRU_WHH, H_GRU_BHH, RL.dgh, RL.hp, G3, GH);
+  seg(2, H_REID4_W, H_REID4_B, RL.dp4, RL.rh2, 64, 64);
+  seg(3, H_REID2_W, H_REID2_B, RL.dp2, RL.rh1, 64, 32);
+  seg(4, H_REID0_W, H_REID0_B, RL.dp0, RL.box, 32, 4);
+  return rows_wgrad(w, st);
 }
 
 // ================================================================== tail: softmax, blend, losses

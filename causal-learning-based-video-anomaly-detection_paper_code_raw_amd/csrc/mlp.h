@@ -1,0 +1,67 @@
+// Fused MLP chains (detector_net / direct_classifier) and the generic row-reduction weight gradient.
+#pragma once
+#include "common.h"
+
+namespace vad {
+
+constexpr int MLP_MAXW = 512;  // widest activation kept in LDS (layer-0 output)
+
+struct MlpLayer {
+  const float* W;  // [N][K]
+  const float* b;  // [N]
+  float* out;      // [M][N]
+  int K, N;
+  int relu, drop;
+  uint64_t h1;
+  uint32_t thr;
+  float dscale;
+};
+
+// layers 1-4 on top of layer 0's finished output L[0].out (only L[0].out / L[0].N are read)
+struct MlpTailArgs {
+  int M;
+  int64_t row0;        // global row of row 0 (dropout key)
+  MlpLayer L[5];
+  const float* WT[5];  // transposed weights WT[i][k][n] of layers 1-4
+};
+
+struct MlpTransposeArgs {
+  int n;
+  const float* W[8];
+  float* WT[8];
+  int K[8], N[8];
+};
+int mlp_transpose(const MlpTransposeArgs& a, hipStream_t st);
+
+// input-gradient chain: d[i-1] = (d_i W_i) * (h[i-1] > 0 ? gscale[i-1] : 0), d_4 = dout
+struct MlpTailBwdArgs {
+  int M;
+  const float* dout;  // [M][N[4]]
+  const float* W[5];
+  int K[5], N[5];
+  const float* h[4];   // forward outputs of layers 0..3 (post ReLU/dropout)
+  float gscale[4];
+  float* d[4];         // outputs: grads w.r.t. the pre-activations of layers 0..3
+  const int* skip;     // nullable device flag: 0 -> no-op
+};
+
+int mlp_tail_fwd(const MlpTailArgs& a, hipStream_t st);
+int mlp_tail_bwd(const MlpTailBwdArgs& a, hipStream_t st);
+
+// dW[o][i] = sum_r A[r][o] X[r][i], db[o] = sum_r A[r][o] for up to ROWS_WGRAD_MAXSEG Linear layers, one launch
+constexpr int ROWS_WGRAD_MAXSEG = 6;
+struct RowsWgradSeg {
+  float* dW;
+  float* db;  // nullable
+  const float* A;  // [R][O]
+  const float* X;  // [R][I]
+  int O, I;
+};
+struct RowsWgradArgs {
+  int R, nseg;
+  RowsWgradSeg seg[ROWS_WGRAD_MAXSEG];
+  const int* skip;
+};
+int rows_wgrad(const RowsWgradArgs& a, hipStream_t st);
+
+}  // namespace vad

@@ -1,0 +1,256 @@
+// The two 5-layer MLP chains of the model (detector_net cad:167-179 on every frame, direct_classifier
+// cad:525-538 on the clip mean), fused so each chain costs a handful of launches instead of ~25:
+//   forward   layer 0 (6144 -> 512) stays a split-K MFMA GEMM (its 12.6 MB weight needs the whole chip);
+//             mlp_tail_fwd_kernel sums its partials (+bias, ReLU, dropout) and runs layers 1-4 for RB rows per
+//             block with the activations in LDS (rows are independent through the chain).
+//   backward  mlp_tail_bwd_kernel walks the gated input-gradient chain 4 -> 0 for RB rows per block;
+//             rows_wgrad_kernel computes every layer-1..4 weight/bias gradient in one launch (f32 MFMA over the
+//             rows, 32x32 tiles, bias as a ones column, fixed-order combine of the 4 waves).
+// Dropout masks come from the keyed counter RNG (common.h), keyed by (stream, step, global row, column) exactly
+// like the unfused EpiDense path.
+#include "mlp.h"
+
+namespace vad {
+
+__device__ __forceinline__ float mlp_finish(const MlpLayer& L, int64_t grow, int col, float v) {
+  v += L.b[col];
+  if (L.relu) v = fmaxf(v, 0.f);
+  if (L.drop) v = (rng_u24(L.h1, (uint64_t)grow, (uint64_t)col) >= L.thr) ? v * L.dscale : 0.f;
+  return v;
+}
+
+// layers 1-4 for RB rows; h0 (layer-0 output, finished by the split-K reduce) is read from global.  Thread t of a
+// layer owns 4 consecutive outputs g = t % (N/4) over the K-slice p = t / (N/4): float4 loads of the transposed
+// weight WT[k][4g..4g+3] (coalesced across g), 8 in flight; the K-slices are combined in a fixed order in LDS.
+template <int RB>
+__global__ __launch_bounds__(256) void mlp_tail_fwd_kernel(const MlpTailArgs a) {
+  __shared__ __attribute__((aligned(16))) float buf[2][RB][MLP_MAXW];
+  __shared__ __attribute__((aligned(16))) float red[256 * 4 * RB];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * RB;
+  {
+    const int N = a.L[0].N;
+    for (int idx = tid; idx < RB * N; idx += 256) {
+      const int r = idx / N, n = idx % N, row = r0 + r;
+      buf[0][r][n] = row < a.M ? a.L[0].out[(int64_t)row * N + n] : 0.f;
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int i = 1; i < 5; ++i) {
+    const MlpLayer& L = a.L[i];
+    const float(*in)[MLP_MAXW] = buf[(i - 1) & 1];
+    float(*outb)[MLP_MAXW] = buf[i & 1];
+    const int K = L.K, N = L.N, NG = N / 4;
+    const int P = 256 / NG;
+    const int kper = ((K + P - 1) / P + 7) & ~7;
+    const float* WT = a.WT[i];
+    if (tid < NG * P) {
+      const int g = tid % NG, p = tid / NG;
+      const int k0 = p * kper, k1 = min(K, k0 + kper);
+      f32x4 acc[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int kb = k0; kb < k1; kb += 8) {  // K and kper are multiples of 8
+        f32x4 wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) wv[u] = *reinterpret_cast<const f32x4*>(WT + (int64_t)(kb + u) * N + 4 * g);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            const float x = in[r][kb + u];
+            acc[r][0] = fmaf(wv[u][0], x, acc[r][0]);
+            acc[r][1] = fmaf(wv[u][1], x, acc[r][1]);
+            acc[r][2] = fmaf(wv[u][2], x, acc[r][2]);
+            acc[r][3] = fmaf(wv[u][3], x, acc[r][3]);
+          }
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) *reinterpret_cast<f32x4*>(&red[(p * RB + r) * N + 4 * g]) = acc[r];
+    }
+    __syncthreads();
+    for (int idx = tid; idx < RB * N; idx += 256) {
+      const int r = idx / N, n = idx % N, row = r0 + r;
+      float sum = 0.f;
+      for (int p = 0; p < P; ++p) sum += red[(p * RB + r) * N + n];
+      float v = 0.f;
+      if (row < a.M) {
+        v = mlp_finish(L, a.row0 + row, n, sum);
+        L.out[(int64_t)row * N + n] = v;
+      }
+      outb[r][n] = v;
+    }
+    __syncthreads();
+  }
+}
+
+// WT[k][n] = W[n][k] for up to 8 matrices (the detector's layer-1..4 weights), once per step: 32x32 tiles through
+// LDS so both the read of W rows and the write of WT rows are coalesced.
+__global__ __launch_bounds__(256) void mlp_transpose_kernel(const MlpTransposeArgs a) {
+  __shared__ float tile[32][33];
+  int m = 0, t = blockIdx.x;
+  for (; m < a.n; ++m) {
+    const int nt = ((a.N[m] + 31) / 32) * ((a.K[m] + 31) / 32);
+    if (t < nt) break;
+    t -= nt;
+  }
+  if (m >= a.n) return;
+  const int K = a.K[m], N = a.N[m], tk = (K + 31) / 32;
+  const int n0 = (t / tk) * 32, k0 = (t % tk) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+#pragma unroll
+  for (int j = 0; j < 32; j += 8) {
+    const int n = n0 + ty + j, k = k0 + tx;
+    tile[ty + j][tx] = (n < N && k < K) ? a.W[m][(int64_t)n * K + k] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 32; j += 8) {
+    const int k = k0 + ty + j, n = n0 + tx;
+    if (k < K && n < N) a.WT[m][(int64_t)k * N + n] = tile[tx][ty + j];
+  }
+}
+
+int mlp_transpose(const MlpTransposeArgs& a, hipStream_t st) {
+  int blocks = 0;
+  for (int m = 0; m < a.n; ++m) blocks += (int)(cdiv(a.N[m], 32) * cdiv(a.K[m], 32));
+  hipLaunchKernelGGL(mlp_transpose_kernel, dim3(blocks), dim3(256), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+// d_{i-1}[r][k] = (sum_n d_i[r][n] W_i[n][k]) * (h_{i-1}[r][k] > 0 ? gscale_{i-1} : 0),  i = 4 .. 1
+template <int RB>
+__global__ __launch_bounds__(256) void mlp_tail_bwd_kernel(const MlpTailBwdArgs a) {
+  if (a.skip && *a.skip == 0) return;
+  __shared__ __attribute__((aligned(16))) float buf[2][RB][MLP_MAXW];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * RB;
+  {
+    const int N = a.N[4], N4 = (N + 3) & ~3;  // zero-filled to the 4-wide n-batches below
+    for (int idx = tid; idx < RB * N4; idx += 256) {
+      const int r = idx / N4, n = idx % N4, row = r0 + r;
+      buf[0][r][n] = (row < a.M && n < N) ? a.dout[(int64_t)row * N + n] : 0.f;
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int i = 4; i >= 1; --i) {
+    const float(*din)[MLP_MAXW] = buf[(4 - i) & 1];
+    float(*dout)[MLP_MAXW] = buf[(5 - i) & 1];
+    const float* W = a.W[i];
+    const int K = a.K[i], N = a.N[i];
+    const float* gate = a.h[i - 1];
+    const float gs = a.gscale[i - 1];
+    float* dst = a.d[i - 1];
+    for (int k = tid; k < K; k += 256) {
+      float acc[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) acc[r] = 0.f;
+      for (int n0 = 0; n0 < N; n0 += 4) {  // 4 coalesced weight loads in flight per batch
+        float wv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) wv[u] = n0 + u < N ? W[(int64_t)(n0 + u) * K + k] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int r = 0; r < RB; ++r) acc[r] = fmaf(din[r][n0 + u], wv[u], acc[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int row = r0 + r;
+        float v = 0.f;
+        if (row < a.M) {
+          v = gate[(int64_t)row * K + k] > 0.f ? acc[r] * gs : 0.f;
+          dst[(int64_t)row * K + k] = v;
+        }
+        dout[r][k] = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ generic row-reduction weight gradients
+__global__ __launch_bounds__(256) void rows_wgrad_kernel(const RowsWgradArgs a) {
+  if (a.skip && *a.skip == 0) return;
+  int s = 0, t = blockIdx.x;
+  for (; s < a.nseg; ++s) {
+    const int n = ((a.seg[s].O + 31) / 32) * ((a.seg[s].I + 1 + 31) / 32);
+    if (t < n) break;
+    t -= n;
+  }
+  if (s >= a.nseg) return;
+  const RowsWgradSeg sg = a.seg[s];
+  const int ti = (sg.I + 1 + 31) / 32;
+  const int o0 = (t / ti) * 32, i0 = (t % ti) * 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l = lane & 31;
+  const int o = o0 + l, i = i0 + l;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int R = a.R;
+  const int per = (R + 3) / 4;
+  const int r0 = wave * per, r1 = min(R, r0 + per);
+  for (int rb = r0; rb < r1; rb += 2) {  // wave-uniform trip count; row rb + h, zero past the share
+    const int r = rb + h;
+    const bool ok = r < r1;
+    const float av = (ok && o < sg.O) ? sg.A[(int64_t)r * sg.O + o] : 0.f;
+    const float xv = !ok ? 0.f : (i < sg.I ? sg.X[(int64_t)r * sg.I + i] : (i == sg.I ? 1.f : 0.f));
+    acc = mfma32(av, xv, acc);
+  }
+  __shared__ float red[4][16][64];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[r];
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = (red[0][r][lane] + red[1][r][lane]) + (red[2][r][lane] + red[3][r][lane]);
+      const int oo = o0 + (r & 3) + 8 * (r >> 2) + 4 * h, ii = i0 + l;
+      if (oo < sg.O) {
+        if (ii < sg.I) sg.dW[(int64_t)oo * sg.I + ii] = v;
+        else if (ii == sg.I && sg.db) sg.db[oo] = v;
+      }
+    }
+  }
+}
+
+int rows_wgrad(const RowsWgradArgs& a, hipStream_t st) {
+  VAD_CHECK(a.nseg >= 1 && a.nseg <= ROWS_WGRAD_MAXSEG, "rows_wgrad: bad segment count");
+  int blocks = 0;
+  for (int s = 0; s < a.nseg; ++s) blocks += (int)(cdiv(a.seg[s].O, 32) * cdiv(a.seg[s].I + 1, 32));
+  hipLaunchKernelGGL(rows_wgrad_kernel, dim3(blocks), dim3(256), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+static int mlp_rb(int M) { return M >= 64 ? 4 : 8; }
+
+int mlp_tail_fwd(const MlpTailArgs& a, hipStream_t st) {
+  for (int i = 1; i < 5; ++i)
+    VAD_CHECK(a.L[i].N <= MLP_MAXW && a.L[i].N % 4 == 0 && a.L[i].N / 4 <= 256 && a.L[i].K <= MLP_MAXW &&
+                  a.L[i].K % 8 == 0 && a.WT[i],
+              "mlp_tail_fwd: layer shape");
+  const int rb = mlp_rb(a.M);
+  if (rb == 4)
+    hipLaunchKernelGGL(mlp_tail_fwd_kernel<4>, dim3((unsigned)cdiv(a.M, 4)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(mlp_tail_fwd_kernel<8>, dim3((unsigned)cdiv(a.M, 8)), dim3(256), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int mlp_tail_bwd(const MlpTailBwdArgs& a, hipStream_t st) {
+  for (int i = 1; i < 5; ++i) VAD_CHECK(a.K[i] <= MLP_MAXW && a.N[i] <= MLP_MAXW, "mlp_tail_bwd: layer width");
+  const int rb = mlp_rb(a.M);
+  if (rb == 4)
+    hipLaunchKernelGGL(mlp_tail_bwd_kernel<4>, dim3((unsigned)cdiv(a.M, 4)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(mlp_tail_bwd_kernel<8>, dim3((unsigned)cdiv(a.M, 8)), dim3(256), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace vad
