@@ -51,6 +51,39 @@ _SIGS = {
     "vad_cad_profile_read": (_I, [_P, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I), _I]),
     "vad_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "vad_conv3x3_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I64, _P]),
+    # minicausal (config 1)
+    "vad_mc_create": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(_P)]),
+    "vad_mc_destroy": (None, [_P]),
+    "vad_mc_num_slots": (_I, [_P]),
+    "vad_mc_slot_name": (ctypes.c_char_p, [_P, _I]),
+    "vad_mc_slot_numel": (_I64, [_P, _I]),
+    "vad_mc_slot_offset": (_I64, [_P, _I]),
+    "vad_mc_param_floats": (_I64, [_P]),
+    "vad_mc_num_bufs": (_I, [_P]),
+    "vad_mc_buf_name": (ctypes.c_char_p, [_P, _I]),
+    "vad_mc_buf_numel": (_I64, [_P, _I]),
+    "vad_mc_buf_offset": (_I64, [_P, _I]),
+    "vad_mc_buf_floats": (_I64, [_P]),
+    "vad_mc_workspace_bytes": (_I64, [_P]),
+    "vad_mc_bind": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "vad_mc_forward": (_I, [_P, _P, _I, _U64, _U64, _I64, _P, _P, _P, _P, _P]),
+    "vad_mc_backward": (_I, [_P, _P, _P]),
+    "vad_mc_optimizer_step": (_I, [_P, _F, _F, _F, _F, _F, _F, _F, _P]),
+    # a2 (avenue_training_script2.py)
+    "vad_a2_num_slots": (_I, []),
+    "vad_a2_slot_name": (ctypes.c_char_p, [_I]),
+    "vad_a2_slot_numel": (_I64, [_I]),
+    "vad_a2_slot_offset": (_I64, [_I]),
+    "vad_a2_param_floats": (_I64, []),
+    "vad_a2_create": (_I, [_I, _I, _I, _I, ctypes.POINTER(_P)]),
+    "vad_a2_destroy": (None, [_P]),
+    "vad_a2_workspace_bytes": (_I64, [_P]),
+    "vad_a2_bind": (_I, [_P, _P, _P, _P, _P, _P, _P]),
+    "vad_a2_forward": (_I, [_P, _P, _I, _U64, _U64, _I64, _I, _P, _P, _P, _P, _P]),
+    "vad_a2_loss": (_I, [_P, _U64, _U64, _I64, _P, _P]),
+    "vad_a2_loss_grads": (_I, [_P, _P, _P, _P]),
+    "vad_a2_backward": (_I, [_P, _P, _P, _P, _P]),
+    "vad_a2_optimizer_step": (_I, [_P, _F, _F, _F, _F, _F, _F, _P]),
 }
 
 

@@ -1,0 +1,321 @@
+"""Drop-in for avenue_training_script2.py: the a2 CausalAnomalyDetector (a2:15-101) and ImprovedMiniCausalVAD
+(a2:107-297) with forward / loss / backward / AdamW on the HIP plan (``vad_a2_*`` in libvadhip.so).
+
+Same class names, constructor signatures, submodule names (state_dict keys ``feature_extractor.conv3d_1.weight``
+... so the reference's ``best_improved_model.pth`` loads strictly), initialisation order and forward return
+``(scores (B,1), causal_adj (B,16,16), features (B,16))``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _native as nat
+
+
+class CompactFeatureExtractor(nn.Module):
+    """a2:15-35"""
+
+    def __init__(self, input_channels=3, feature_dim=64):
+        super().__init__()
+        self.conv3d_1 = nn.Conv3d(input_channels, 16, (3, 3, 3), stride=(1, 2, 2), padding=1)
+        self.conv3d_2 = nn.Conv3d(16, 32, (3, 3, 3), stride=(2, 2, 2), padding=1)
+        self.conv3d_3 = nn.Conv3d(32, 64, (3, 3, 3), stride=(2, 2, 2), padding=1)
+        self.adaptive_pool = nn.AdaptiveAvgPool3d((4, 4, 4))
+        self.fc = nn.Linear(64 * 4 * 4 * 4, feature_dim)
+        self.dropout = nn.Dropout(0.3)
+
+
+class DifferentiableCausalDiscovery(nn.Module):
+    """a2:37-66"""
+
+    def __init__(self, num_variables=16, hidden_dim=32):
+        super().__init__()
+        self.num_variables = num_variables
+        self.causal_net = nn.Sequential(nn.Linear(num_variables, hidden_dim), nn.ReLU(),
+                                        nn.Linear(hidden_dim, num_variables * num_variables), nn.Sigmoid())
+
+    def acyclicity_constraint(self, adj_matrix):
+        """a2:62-66 (host-side helper, unchanged semantics)."""
+        m = adj_matrix.mean(dim=0)
+        return torch.trace(torch.matrix_power(m + 1e-8, 2))
+
+
+class CausalAnomalyDetector(nn.Module):
+    """a2:69-101.  forward(video_clips (B,3,T,H,W)) -> (anomaly_scores (B,1), causal_adj (B,16,16), features (B,16))."""
+
+    def __init__(self, feature_dim=64, causal_dim=16, hidden_dim=128):
+        super().__init__()
+        self.feature_extractor = CompactFeatureExtractor(feature_dim=causal_dim)
+        self.causal_discovery = DifferentiableCausalDiscovery(num_variables=causal_dim)
+        self.graph_encoder = nn.Sequential(nn.Linear(causal_dim * causal_dim, hidden_dim), nn.ReLU(), nn.Dropout(0.3),
+                                           nn.Linear(hidden_dim, 64))
+        self.anomaly_predictor = nn.Sequential(nn.Linear(causal_dim + 64, 32), nn.ReLU(), nn.Linear(32, 1),
+                                               nn.Sigmoid())
+        self._engine = None
+        self._step = 0
+
+    def engine(self, x: torch.Tensor) -> "A2Engine":
+        e = self._engine
+        if e is None or e.device != x.device:
+            e = A2Engine(self, x.device)
+            self._engine = e
+        e.sync_from_module()
+        e.use_shape(tuple(x.shape))
+        return e
+
+    def forward(self, video_clips, *, seed=None, step=None, clip0=0):
+        if video_clips.dim() != 5 or video_clips.shape[1] != 3:
+            raise ValueError(f"Expected (B,3,T,H,W) clips, got {tuple(video_clips.shape)}")
+        nat.require_hip(video_clips)
+        x = video_clips.float().contiguous()
+        e = self.engine(x)
+        if seed is None:
+            seed = e.seed
+        if step is None:
+            step = self._step
+            if self.training:
+                self._step += 1
+        e.last_keys = (seed, step, clip0)
+        params = [p for _, p in self.named_parameters()]
+        return _A2Function.apply(x, e, self.training, seed, step, clip0, *params)
+
+
+class _A2Function(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, e, training, seed, step, clip0, *params):
+        s, adj, f = e.forward(x, training, seed, step, clip0, with_loss=False)
+        ctx.e = e
+        return s.view(-1, 1).clone(), adj.clone(), f.clone()
+
+    @staticmethod
+    def backward(ctx, d_s, d_adj, d_f):
+        e = ctx.e
+        e.backward(None if d_s is None else d_s.reshape(-1).contiguous().float(),
+                   None if d_adj is None else d_adj.contiguous().float(),
+                   None if d_f is None else d_f.contiguous().float())
+        return (None, None, None, None, None, None, *e.grad_clones())
+
+
+class _A2LossFunction(torch.autograd.Function):
+    """compute_improved_loss on the engine's last forward; backward hands d total / d (scores, adj) upstream."""
+
+    @staticmethod
+    def forward(ctx, scores, adj, e, seed, step, clip0):
+        e.loss(seed, step, clip0)
+        ctx.e = e
+        return e.losses[0].clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        ds, dadj = ctx.e.loss_grads()
+        return (ds.view(-1, 1) * g, dadj * g, None, None, None, None)
+
+
+class _A2Plan:
+    def __init__(self, e, shape):
+        lib = nat.lib()
+        B, C, T, H, W = shape
+        plan = ctypes.c_void_p()
+        nat.check(lib.vad_a2_create(B, T, H, W, ctypes.byref(plan)))
+        self.plan = plan
+        self.B = B
+        self.ws = torch.empty(lib.vad_a2_workspace_bytes(plan) + 256, dtype=torch.uint8, device=e.device)
+        base = (self.ws.data_ptr() + 255) // 256 * 256
+        nat.check(lib.vad_a2_bind(plan, ctypes.c_void_p(base), nat.ptr(e.params), nat.ptr(e.grads),
+                                  nat.ptr(e.exp_avg), nat.ptr(e.exp_avg_sq), nat.ptr(e.steps)))
+        f = dict(dtype=torch.float32, device=e.device)
+        self.scores, self.adj, self.feats = torch.zeros(B, **f), torch.zeros(B, 16, 16, **f), torch.zeros(B, 16, **f)
+        self.d_s, self.d_adj = torch.zeros(B, **f), torch.zeros(B, 16, 16, **f)
+
+    def __del__(self):
+        try:
+            if getattr(self, "plan", None):
+                nat.lib().vad_a2_destroy(self.plan)
+        except Exception:
+            pass
+
+
+class A2Engine:
+    """Flat device buffers (params / grads / AdamW state, named_parameters order) shared by per-shape plans."""
+
+    def __init__(self, model, device):
+        lib = nat.lib()
+        self.device, self.model, self.seed = device, model, 1234
+        self.slots = [(lib.vad_a2_slot_name(i).decode(), lib.vad_a2_slot_offset(i), lib.vad_a2_slot_numel(i))
+                      for i in range(lib.vad_a2_num_slots())]
+        names = [n for n, _ in model.named_parameters()]
+        if names != [s[0] for s in self.slots]:
+            raise NotImplementedError("the HIP a2 plan supports the reference dims (feature_dim=64, causal_dim=16, "
+                                      "hidden_dim=128) only")
+        n = lib.vad_a2_param_floats()
+        f = dict(dtype=torch.float32, device=device)
+        self.params, self.grads = torch.zeros(n, **f), torch.zeros(n, **f)
+        self.exp_avg, self.exp_avg_sq = torch.zeros(n, **f), torch.zeros(n, **f)
+        self.steps = torch.zeros(len(self.slots), dtype=torch.int32, device=device)
+        self.losses = torch.zeros(10, **f)
+        sd = dict(model.named_parameters())
+        self.param_views = [self.params[o:o + k].view_as(sd[nm]) for nm, o, k in self.slots]
+        self._bound = False
+        self.plans, self.cur, self.last_keys = {}, None, (0, 0, 0)
+
+    def use_shape(self, shape):
+        if shape not in self.plans:
+            self.plans[shape] = _A2Plan(self, shape)
+        self.cur = self.plans[shape]
+
+    def sync_from_module(self):
+        if self._bound:
+            return
+        m = self.model
+        with torch.no_grad():
+            sd = dict(m.named_parameters())
+            for (name, o, k), view in zip(self.slots, self.param_views):
+                view.copy_(sd[name].detach().to(self.device))
+                mod_name, attr = name.rsplit(".", 1)
+                setattr(m.get_submodule(mod_name), attr, nn.Parameter(view, requires_grad=sd[name].requires_grad))
+        self._bound = True
+
+    def stream(self):
+        return nat.stream_of(self.device)
+
+    def forward(self, x, training, seed, step, clip0, with_loss):
+        p = self.cur
+        nat.check(nat.lib().vad_a2_forward(p.plan, nat.ptr(x), int(training), ctypes.c_uint64(seed),
+                                           ctypes.c_uint64(step), ctypes.c_int64(clip0), int(with_loss),
+                                           nat.ptr(p.scores), nat.ptr(p.adj), nat.ptr(p.feats),
+                                           nat.ptr(self.losses) if with_loss else None, self.stream()))
+        return p.scores, p.adj, p.feats
+
+    def loss(self, seed, step, clip0):
+        nat.check(nat.lib().vad_a2_loss(self.cur.plan, ctypes.c_uint64(seed), ctypes.c_uint64(step),
+                                        ctypes.c_int64(clip0), nat.ptr(self.losses), self.stream()))
+
+    def loss_grads(self):
+        p = self.cur
+        nat.check(nat.lib().vad_a2_loss_grads(p.plan, nat.ptr(p.d_s), nat.ptr(p.d_adj), self.stream()))
+        return p.d_s.clone(), p.d_adj.clone()
+
+    def backward(self, d_s=None, d_adj=None, d_f=None):
+        nat.check(nat.lib().vad_a2_backward(self.cur.plan, nat.ptr(d_s) if d_s is not None else None,
+                                            nat.ptr(d_adj) if d_adj is not None else None,
+                                            nat.ptr(d_f) if d_f is not None else None, self.stream()))
+
+    def grad_clones(self):
+        return [self.grads[o:o + k].view_as(v).clone() for (_, o, k), v in zip(self.slots, self.param_views)]
+
+    def optimizer_step(self, lr, weight_decay, max_norm, betas=(0.9, 0.999), eps=1e-8):
+        nat.check(nat.lib().vad_a2_optimizer_step(self.cur.plan, ctypes.c_float(lr), ctypes.c_float(betas[0]),
+                                                  ctypes.c_float(betas[1]), ctypes.c_float(eps),
+                                                  ctypes.c_float(weight_decay), ctypes.c_float(max_norm),
+                                                  self.stream()))
+
+
+class _ParamGroups:
+    """The slice of the torch optimizer surface the reference's driver reads (param_groups[0]['lr'])."""
+
+    def __init__(self, lr, weight_decay):
+        self.param_groups = [{"lr": lr, "weight_decay": weight_decay, "betas": (0.9, 0.999), "eps": 1e-8}]
+
+
+class _Plateau:
+    """ReduceLROnPlateau(mode='min', factor=0.5, patience=5) semantics (torch defaults: rel threshold 1e-4)."""
+
+    def __init__(self, opt, factor=0.5, patience=5, threshold=1e-4, min_lr=0.0, eps=1e-8):
+        self.opt, self.factor, self.patience, self.threshold, self.min_lr, self.eps = (
+            opt, factor, patience, threshold, min_lr, eps)
+        self.best, self.bad = float("inf"), 0
+
+    def step(self, metric):
+        if metric < self.best * (1 - self.threshold):
+            self.best, self.bad = metric, 0
+        else:
+            self.bad += 1
+        if self.bad > self.patience:
+            for g in self.opt.param_groups:
+                new = max(g["lr"] * self.factor, self.min_lr)
+                if g["lr"] - new > self.eps:
+                    g["lr"] = new
+            self.bad = 0
+
+
+LOSS_KEYS = ("anomaly_loss", "acyclicity_loss", "sparsity_loss", "consistency_loss", "structure_loss", "edge_count",
+             "sparsity_ratio")
+
+
+class ImprovedMiniCausalVAD:
+    """a2:107-297 on the HIP plan: model / optimizer / scheduler attributes, compute_improved_loss,
+    train_epoch_improved, evaluate_improved."""
+
+    def __init__(self, device="cuda"):
+        self.device = device
+        self.model = CausalAnomalyDetector().to(device)
+        self.optimizer = _ParamGroups(lr=0.0005, weight_decay=0.001)
+        self.anomaly_weight, self.causal_weight, self.sparsity_weight, self.consistency_weight = 1.0, 0.01, 0.001, 0.01
+        self.scheduler = _Plateau(self.optimizer, factor=0.5, patience=5)
+        self.seed = 1234
+        self.global_step = 0
+        self.clip0 = 0
+
+    def compute_improved_loss(self, anomaly_scores, causal_adj, targets, features):
+        """Loss of the model's last forward (the labels are ignored: pseudo-labels, a2:139-141).  Returns
+        (total loss tensor with autograd into the model's backward, components dict)."""
+        e = self.model._engine
+        seed, step, clip0 = e.last_keys
+        total = _A2LossFunction.apply(anomaly_scores, causal_adj, e, seed, step, clip0)
+        vals = e.losses.cpu().tolist()
+        return total, dict(zip(LOSS_KEYS, vals[1:8]))
+
+    def train_step(self, videos, labels):
+        """One a2:218-245 iteration fused on device (forward + loss + backward + clip + AdamW)."""
+        videos = videos.to(self.device, dtype=torch.float32).contiguous()
+        self.model.train()
+        e = self.model.engine(videos)
+        g = self.optimizer.param_groups[0]
+        e.forward(videos, True, self.seed, self.global_step, self.clip0, with_loss=True)
+        vals = e.losses.cpu().tolist()
+        comps = dict(zip(LOSS_KEYS, vals[1:8]))
+        stepped = not np.isnan(vals[0])
+        if stepped:
+            e.backward()
+            e.optimizer_step(g["lr"], g["weight_decay"], max_norm=0.5)
+        self.global_step += 1
+        self.clip0 += videos.shape[0]
+        return vals[0], comps, stepped
+
+    def train_epoch_improved(self, dataloader):
+        total_loss = 0.0
+        comps_sum = {k: 0.0 for k in LOSS_KEYS}
+        for videos, labels in dataloader:
+            loss, comps, stepped = self.train_step(videos, labels)
+            if not stepped:
+                continue
+            total_loss += loss
+            for k, v in comps.items():
+                comps_sum[k] += v
+        n = len(dataloader)
+        avg = total_loss / n
+        self.scheduler.step(avg)
+        return avg, {k: v / n for k, v in comps_sum.items()}
+
+    def evaluate_improved(self, dataloader):
+        self.model.eval()
+        preds, graphs = [], []
+        with torch.no_grad():
+            for videos, _ in dataloader:
+                videos = videos.to(self.device, dtype=torch.float32).contiguous()
+                s, adj, f = self.model(videos)
+                preds.extend(s.squeeze().cpu().numpy().reshape(-1).tolist())
+                graphs.append(adj.cpu().numpy())
+        preds = np.array(preds, dtype=np.float32)
+        graphs = np.vstack(graphs)
+        e = np.sum(graphs > 0.1, axis=(1, 2))
+        metrics = {"mean_score": float(np.mean(preds)), "std_score": float(np.std(preds)),
+                   "min_score": float(np.min(preds)), "max_score": float(np.max(preds)),
+                   "score_range": float(np.max(preds) - np.min(preds)), "avg_edges": float(np.mean(e)),
+                   "avg_sparsity": float(np.mean(e / 256)),
+                   "unique_graphs": len(np.unique(graphs.reshape(len(graphs), -1), axis=0))}
+        return preds, graphs, metrics

@@ -1,0 +1,698 @@
+// avenue_training_script2.py: the a2 CausalAnomalyDetector (a2:15-101), compute_improved_loss (a2:135-205) and
+// the ImprovedMiniCausalVAD train step (a2:218-245) as one device plan.
+//
+//   forward   3 x [im2col3d -> f32 MFMA GEMM with fused bias+ReLU] (strides (1,2,2), 2, 2) -> AdaptiveAvgPool3d(4,4,4)
+//             -> fc GEMM (4096 -> 16) with the keyed Dropout(0.3) -> one block-wide kernel for the causal-discovery
+//             MLP (sigmoid adjacency, zero diagonal), graph encoder (Dropout .3) and predictor -> the loss kernel
+//             (compute_improved_loss and its gradients w.r.t. scores and adjacency)
+//   backward  loss + head backward in the same block-wide style (weight grads as fixed-order sums over the batch),
+//             fc weight / input grads as GEMMs, avg-pool backward, then per stage ReLU gate -> weight+bias grad GEMM
+//             over the saved columns -> input grad GEMM + col2im
+//   update    clip_grad_norm_(0.5) (norm of per-parameter norms) -> AdamW (decoupled weight decay)
+// losses[]: 0 total, 1 anomaly(focal), 2 acyclicity, 3 sparsity, 4 consistency, 5 structure, 6 edge_count,
+//           7 sparsity_ratio, 8 grad total norm, 9 status (0 skipped: NaN loss, 2 stepped)
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/vad.h"
+#include "backbone.h"
+#include "conv3d.h"
+#include "plan_util.h"
+
+namespace vad {
+
+constexpr int A2_NSLOT = 20;
+constexpr int A2_CO[3] = {16, 32, 64};
+constexpr int A2_MAXB = 256;
+
+struct A2Slot {
+  const char* name;
+  int64_t numel;
+};
+static const A2Slot A2_SLOTS[A2_NSLOT] = {
+    {"feature_extractor.conv3d_1.weight", 16 * 3 * 27}, {"feature_extractor.conv3d_1.bias", 16},
+    {"feature_extractor.conv3d_2.weight", 32 * 16 * 27}, {"feature_extractor.conv3d_2.bias", 32},
+    {"feature_extractor.conv3d_3.weight", 64 * 32 * 27}, {"feature_extractor.conv3d_3.bias", 64},
+    {"feature_extractor.fc.weight", 16 * 4096},          {"feature_extractor.fc.bias", 16},
+    {"causal_discovery.causal_net.0.weight", 32 * 16},   {"causal_discovery.causal_net.0.bias", 32},
+    {"causal_discovery.causal_net.2.weight", 256 * 32},  {"causal_discovery.causal_net.2.bias", 256},
+    {"graph_encoder.0.weight", 128 * 256},               {"graph_encoder.0.bias", 128},
+    {"graph_encoder.3.weight", 64 * 128},                {"graph_encoder.3.bias", 64},
+    {"anomaly_predictor.0.weight", 32 * 80},             {"anomaly_predictor.0.bias", 32},
+    {"anomaly_predictor.2.weight", 32},                  {"anomaly_predictor.2.bias", 1},
+};
+enum {
+  S_C1W, S_C1B, S_C2W, S_C2B, S_C3W, S_C3B, S_FCW, S_FCB, S_CN0W, S_CN0B, S_CN2W, S_CN2B,
+  S_GE0W, S_GE0B, S_GE3W, S_GE3B, S_AP0W, S_AP0B, S_AP2W, S_AP2B
+};
+
+struct A2Offsets {
+  int64_t off[A2_NSLOT];
+  int64_t total;
+  A2Offsets() {
+    total = 0;
+    for (int i = 0; i < A2_NSLOT; ++i) {
+      off[i] = total;
+      total += (A2_SLOTS[i].numel + 255) / 256 * 256;
+    }
+  }
+};
+static const A2Offsets& a2_offsets() {
+  static const A2Offsets o;
+  return o;
+}
+
+// ------------------------------------------------------------------ head: block-wide dense helper
+// out[b][n] = act(sum_k in[b][k] W[n][k] + bias[n]); act 0 none, 1 relu, 2 sigmoid
+__device__ void blk_dense(const float* in, int K, const float* W, const float* bias, int N, float* out, int B,
+                          int act) {
+  for (int idx = threadIdx.x; idx < B * N; idx += blockDim.x) {
+    const int b = idx / N, n = idx % N;
+    const float* x = in + (int64_t)b * K;
+    const float* w = W + (int64_t)n * K;
+    float z = bias[n];
+    for (int k = 0; k < K; ++k) z = fmaf(w[k], x[k], z);
+    out[idx] = act == 1 ? relu_nan(z) : (act == 2 ? 1.f / (1.f + expf(-z)) : z);
+  }
+}
+
+struct A2HeadArgs {
+  int B, training, with_loss;
+  int64_t clip0;
+  const float* P;  // params base
+  const int64_t* off;
+  float *f, *hc0, *sig, *adj, *g1, *g1d, *g2, *cat, *hp0, *s;  // saved activations
+  uint64_t h_graph, h_pseudo;
+  uint32_t thr_graph;
+  float s_graph;
+  float* losses;
+  float* pseudo;  // [B]
+  float* d_s;     // [B]  upstream grads written by the loss
+  float* d_adj;   // [B][256]
+  float* red;     // [256] scratch
+};
+
+__global__ __launch_bounds__(512) void a2_head_fwd_kernel(A2HeadArgs a) {
+  const int B = a.B;
+  const float* P = a.P;
+  const int64_t* o = a.off;
+  blk_dense(a.f, 16, P + o[S_CN0W], P + o[S_CN0B], 32, a.hc0, B, 1);
+  __syncthreads();
+  blk_dense(a.hc0, 32, P + o[S_CN2W], P + o[S_CN2B], 256, a.sig, B, 2);
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < B * 256; idx += blockDim.x) {
+    const int e = idx % 256;
+    a.adj[idx] = (e / 16 == e % 16) ? a.sig[idx] * 0.f : a.sig[idx];  // * (1 - eye)
+  }
+  __syncthreads();
+  blk_dense(a.adj, 256, P + o[S_GE0W], P + o[S_GE0B], 128, a.g1, B, 1);
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < B * 128; idx += blockDim.x) {
+    float v = a.g1[idx];
+    if (a.training) {
+      const int b = idx / 128, n = idx % 128;
+      v = rng_u24(a.h_graph, (uint64_t)(a.clip0 + b), (uint64_t)n) >= a.thr_graph ? v * a.s_graph : 0.f;
+    }
+    a.g1d[idx] = v;
+  }
+  __syncthreads();
+  blk_dense(a.g1d, 128, P + o[S_GE3W], P + o[S_GE3B], 64, a.g2, B, 0);
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < B * 80; idx += blockDim.x) {
+    const int b = idx / 80, c = idx % 80;
+    a.cat[idx] = c < 16 ? a.f[b * 16 + c] : a.g2[b * 64 + c - 16];
+  }
+  __syncthreads();
+  blk_dense(a.cat, 80, P + o[S_AP0W], P + o[S_AP0B], 32, a.hp0, B, 1);
+  __syncthreads();
+  blk_dense(a.hp0, 32, P + o[S_AP2W], P + o[S_AP2B], 1, a.s, B, 2);
+}
+
+// compute_improved_loss (a2:135-205) on the saved scores / adjacency, plus d total / d scores and d total / d adj
+__global__ __launch_bounds__(512) void a2_loss_kernel(A2HeadArgs a) {
+  const int B = a.B;
+  __shared__ float sh[512];
+  __shared__ float sh2[512];
+  __shared__ int nnormal_s, npairs_s;
+  __shared__ float avg_s;
+  const int t = threadIdx.x;
+  if (t < B) {
+    const float u = (float)rng_u24(a.h_pseudo, (uint64_t)(a.clip0 + t), 0) * (1.0f / 16777216.0f);
+    a.pseudo[t] = u > 0.95f ? 1.f : 0.f;
+  }
+  __syncthreads();
+  // focal BCE (mean over the batch) and its derivative w.r.t. the scores
+  float focal = 0.f;
+  for (int b = t; b < B; b += blockDim.x) {
+    const float sv = a.s[b], p = a.pseudo[b];
+    const float ce = -(p * fmaxf(logf(sv), -100.f) + (1.f - p) * fmaxf(log1pf(-sv), -100.f));
+    const float pt = expf(-ce);
+    focal += 0.25f * (1.f - pt) * (1.f - pt) * ce;
+    const float dfdce = 0.25f * ((1.f - pt) * (1.f - pt) + 2.f * (1.f - pt) * pt * ce);
+    const float dce = (sv - p) / fmaxf((1.f - sv) * sv, 1e-12f);
+    a.d_s[b] = dfdce * dce / (float)B;
+  }
+  // mean adjacency, sparsity counts
+  float acyc_part = 0.f, cnt = 0.f;
+  for (int e = t; e < 256; e += blockDim.x) {
+    float m = 0.f, mt = 0.f;
+    const int i = e / 16, j = e % 16, et = j * 16 + i;
+    for (int b = 0; b < B; ++b) {
+      m += a.adj[b * 256 + e];
+      mt += a.adj[b * 256 + et];
+    }
+    m /= (float)B;
+    mt /= (float)B;
+    a.red[e] = mt;  // mean_adj^T, for the acyclicity gradient
+    acyc_part += m * mt;
+  }
+  for (int idx = t; idx < B * 256; idx += blockDim.x) cnt += a.adj[idx] > 0.1f ? 1.f : 0.f;
+  sh[t] = focal + 0.f;
+  sh2[t] = acyc_part;
+  __syncthreads();
+  for (int k = blockDim.x / 2; k > 0; k >>= 1) {
+    if (t < k) {
+      sh[t] += sh[t + k];
+      sh2[t] += sh2[t + k];
+    }
+    __syncthreads();
+  }
+  const float focal_sum = sh[0], acyc = sh2[0];
+  __syncthreads();
+  sh[t] = cnt;
+  __syncthreads();
+  for (int k = blockDim.x / 2; k > 0; k >>= 1) {
+    if (t < k) sh[t] += sh[t + k];
+    __syncthreads();
+  }
+  const float edges = sh[0];
+  __syncthreads();
+  // consistency over the pseudo-normal clips: mean over pairs i<j of mean|A_i - A_j|
+  if (t == 0) {
+    int nn = 0;
+    for (int b = 0; b < B; ++b) nn += a.pseudo[b] == 0.f;
+    nnormal_s = nn;
+    npairs_s = nn * (nn - 1) / 2;
+  }
+  __syncthreads();
+  const int np = npairs_s;
+  float pd = 0.f;
+  if (nnormal_s > 1) {
+    for (int q = t; q < B * B; q += blockDim.x) {
+      const int i = q / B, j = q % B;
+      if (i < j && a.pseudo[i] == 0.f && a.pseudo[j] == 0.f) {
+        float d = 0.f;
+        for (int e = 0; e < 256; ++e) d += fabsf(a.adj[i * 256 + e] - a.adj[j * 256 + e]);
+        pd += d / 256.f;
+      }
+    }
+  }
+  sh[t] = pd;
+  __syncthreads();
+  for (int k = blockDim.x / 2; k > 0; k >>= 1) {
+    if (t < k) sh[t] += sh[t + k];
+    __syncthreads();
+  }
+  if (t == 0) avg_s = np > 0 ? sh[0] / (float)np : 0.f;
+  __syncthreads();
+  const float avg = avg_s;
+  const float consistency = np > 0 ? fabsf(avg - 0.1f) : 0.f;
+  const float csign = np > 0 ? (avg > 0.1f ? 1.f : (avg < 0.1f ? -1.f : 0.f)) : 0.f;
+  // d total / d adj: 0.01 * d acyc + 0.01 * d consistency  (sparsity / structure carry no gradient)
+  for (int idx = t; idx < B * 256; idx += blockDim.x) {
+    const int b = idx / 256, e = idx % 256;
+    float g = 0.01f * 2.f * a.red[e] / (float)B;
+    if (np > 0 && a.pseudo[b] == 0.f) {
+      float sg = 0.f;
+      for (int j = 0; j < B; ++j) {
+        if (j == b || a.pseudo[j] != 0.f) continue;
+        const float d = a.adj[idx] - a.adj[j * 256 + e];
+        sg += d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+      }
+      g += 0.01f * csign * sg / ((float)np * 256.f);
+    }
+    a.d_adj[idx] = g;
+  }
+  if (t == 0) {
+    const float anomaly = focal_sum / (float)B;
+    const float ratio = edges / (float)(B * 256);
+    const float sparsity = fabsf(ratio - 0.3f);
+    float structure = 0.f;
+    if (edges < 10.f) structure = (10.f - edges) * 0.01f;
+    else if (edges > 40.f) structure = (edges - 40.f) * 0.01f;
+    const float total = anomaly + 0.01f * acyc + 0.001f * sparsity + 0.01f * consistency + 0.01f * structure;
+    float* L = a.losses;
+    L[0] = total; L[1] = anomaly; L[2] = acyc; L[3] = sparsity; L[4] = consistency; L[5] = structure;
+    L[6] = edges; L[7] = ratio; L[8] = 0.f;
+    L[9] = isnan(total) ? 0.f : 2.f;
+  }
+}
+
+struct A2HeadBwdArgs {
+  A2HeadArgs f;
+  const float* d_s;    // [B]
+  const float* d_adj;  // [B][256] (nullable)
+  const float* d_f;    // [B][16] external features grad (nullable)
+  float* G;            // grads base
+  float *dz_ap2, *dz_ap0, *dg2, *dz_ge0, *dz_cn2, *dz_cn0, *dfeat;  // scratch; dfeat = grad w.r.t. fc output
+  uint64_t h_fc;
+  uint32_t thr_fc;
+  float s_fc;
+};
+
+__global__ __launch_bounds__(512) void a2_head_bwd_kernel(A2HeadBwdArgs a) {
+  const A2HeadArgs& f = a.f;
+  const int B = f.B, t = threadIdx.x, T = blockDim.x;
+  const float* P = f.P;
+  const int64_t* o = f.off;
+  // predictor: s = sigmoid(W2 hp0 + b), hp0 = relu(W0 cat + b)
+  for (int b = t; b < B; b += T) a.dz_ap2[b] = a.d_s[b] * f.s[b] * (1.f - f.s[b]);
+  __syncthreads();
+  for (int idx = t; idx < B * 32; idx += T) {
+    const int b = idx / 32, k = idx % 32;
+    a.dz_ap0[idx] = f.hp0[idx] > 0.f ? a.dz_ap2[b] * P[o[S_AP2W] + k] : 0.f;
+  }
+  __syncthreads();
+  // d cat -> d g2 (64) and the predictor's share of d features (16, kept in dfeat)
+  for (int idx = t; idx < B * 80; idx += T) {
+    const int b = idx / 80, c = idx % 80;
+    float d = 0.f;
+    for (int k = 0; k < 32; ++k) d = fmaf(a.dz_ap0[b * 32 + k], P[o[S_AP0W] + k * 80 + c], d);
+    if (c < 16) a.dfeat[b * 16 + c] = d + (a.d_f ? a.d_f[b * 16 + c] : 0.f);
+    else a.dg2[b * 64 + c - 16] = d;
+  }
+  __syncthreads();
+  // graph encoder: g2 = W3 g1d + b; g1d = drop(relu(W0 adj + b))
+  for (int idx = t; idx < B * 128; idx += T) {
+    const int b = idx / 128, n = idx % 128;
+    float d = 0.f;
+    for (int k = 0; k < 64; ++k) d = fmaf(a.dg2[b * 64 + k], P[o[S_GE3W] + k * 128 + n], d);
+    if (f.training) d = rng_u24(f.h_graph, (uint64_t)(f.clip0 + b), (uint64_t)n) >= f.thr_graph ? d * f.s_graph : 0.f;
+    a.dz_ge0[idx] = f.g1[idx] > 0.f ? d : 0.f;
+  }
+  __syncthreads();
+  // d adj (graph encoder + loss) -> d sig (zero diagonal) -> dz_cn2
+  for (int idx = t; idx < B * 256; idx += T) {
+    const int b = idx / 256, e = idx % 256;
+    float d = a.d_adj ? a.d_adj[idx] : 0.f;
+    for (int k = 0; k < 128; ++k) d = fmaf(a.dz_ge0[b * 128 + k], P[o[S_GE0W] + k * 256 + e], d);
+    const float sg = f.sig[idx];
+    a.dz_cn2[idx] = (e / 16 == e % 16) ? 0.f : d * sg * (1.f - sg);
+  }
+  __syncthreads();
+  for (int idx = t; idx < B * 32; idx += T) {
+    const int b = idx / 32, k = idx % 32;
+    float d = 0.f;
+    for (int e = 0; e < 256; ++e) d = fmaf(a.dz_cn2[b * 256 + e], P[o[S_CN2W] + e * 32 + k], d);
+    a.dz_cn0[idx] = f.hc0[idx] > 0.f ? d : 0.f;
+  }
+  __syncthreads();
+  // d features (fc output after dropout) += W_cn0^T dz_cn0, then the fc dropout backward (in place)
+  for (int idx = t; idx < B * 16; idx += T) {
+    const int b = idx / 16, c = idx % 16;
+    float d = a.dfeat[idx];
+    for (int k = 0; k < 32; ++k) d = fmaf(a.dz_cn0[b * 32 + k], P[o[S_CN0W] + k * 16 + c], d);
+    if (f.training) d = rng_u24(a.h_fc, (uint64_t)(f.clip0 + b), (uint64_t)c) >= a.thr_fc ? d * a.s_fc : 0.f;
+    a.dfeat[idx] = d;
+  }
+  // head weight grads: fixed-order sums over the batch
+  struct Seg { int w, bias, N, K; const float* dz; const float* x; };
+  const Seg segs[6] = {
+      {S_AP2W, S_AP2B, 1, 32, a.dz_ap2, f.hp0},  {S_AP0W, S_AP0B, 32, 80, a.dz_ap0, f.cat},
+      {S_GE3W, S_GE3B, 64, 128, a.dg2, f.g1d},   {S_GE0W, S_GE0B, 128, 256, a.dz_ge0, f.adj},
+      {S_CN2W, S_CN2B, 256, 32, a.dz_cn2, f.hc0}, {S_CN0W, S_CN0B, 32, 16, a.dz_cn0, f.f},
+  };
+  for (int s = 0; s < 6; ++s) {
+    const Seg& g = segs[s];
+    const int tot = g.N * (g.K + 1);
+    for (int idx = t; idx < tot; idx += T) {
+      const int n = idx / (g.K + 1), k = idx % (g.K + 1);
+      float acc = 0.f;
+      if (k < g.K) {
+        for (int b = 0; b < B; ++b) acc = fmaf(g.dz[b * g.N + n], g.x[b * g.K + k], acc);
+        a.G[o[g.w] + n * g.K + k] = acc;
+      } else {
+        for (int b = 0; b < B; ++b) acc += g.dz[b * g.N + n];
+        a.G[o[g.bias] + n] = acc;
+      }
+    }
+  }
+}
+
+__global__ void relu_gate_kernel(float* __restrict__ d, const float* __restrict__ y, int64_t n) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    if (!(y[i] > 0.f)) d[i] = 0.f;
+}
+static int relu_gate(float* d, const float* y, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(relu_gate_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 8192)), dim3(256), 0, st, d, y,
+                     n);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+// ------------------------------------------------------------------ AdamW with clip_grad_norm_(max_norm)
+struct A2SlotTab {
+  int64_t off[A2_NSLOT], numel[A2_NSLOT];
+};
+__global__ __launch_bounds__(256) void a2_sqsum_kernel(const float* __restrict__ g, A2SlotTab t, float* norms) {
+  const int s = blockIdx.x;
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < t.numel[s]; i += 256) {
+    const float v = g[t.off[s] + i];
+    acc += (double)v * (double)v;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) norms[s] = (float)sqrt(red[0]);
+}
+// ctrl: [0] step?, [1] clip coefficient, [2] -lr/bc1, [3] sqrt(bc2), [4] 1 - lr*wd
+__global__ void a2_opt_prepare_kernel(const float* norms, float* losses, int32_t* steps, float lr, float b1, float b2,
+                                      float wd, float max_norm, float* ctrl) {
+  if (threadIdx.x != 0) return;
+  ctrl[0] = 0.f;
+  if (losses[9] < 1.f) return;
+  double tot = 0.0;
+  for (int s = 0; s < A2_NSLOT; ++s) tot += (double)norms[s] * (double)norms[s];
+  const float total = (float)sqrt(tot);
+  losses[8] = total;
+  ctrl[1] = fminf(1.f, max_norm / (total + 1e-6f));
+  const int step = steps[0] + 1;
+  for (int s = 0; s < A2_NSLOT; ++s) steps[s] = step;
+  const double bc1 = 1.0 - pow((double)b1, step), bc2 = 1.0 - pow((double)b2, step);
+  ctrl[2] = (float)(-(double)lr / bc1);
+  ctrl[3] = (float)sqrt(bc2);
+  ctrl[4] = (float)(1.0 - (double)lr * (double)wd);
+  ctrl[0] = 1.f;
+}
+__global__ __launch_bounds__(256) void a2_adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                       const float* ctrl, float b1, float b2, float eps) {
+  if (ctrl[0] == 0.f) return;
+  const float coef = ctrl[1], step_size = ctrl[2], bc2s = ctrl[3], decay = ctrl[4];
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float gv = g[i] * coef;
+    const float pv = p[i] * decay;  // param.mul_(1 - lr * weight_decay)
+    const float mv = m[i] + (1.f - b1) * (gv - m[i]);
+    const float vv = fmaf(v[i], b2, (1.f - b2) * gv * gv);
+    m[i] = mv;
+    v[i] = vv;
+    p[i] = fmaf(step_size, mv / (sqrtf(vv) / bc2s + eps), pv);
+  }
+}
+
+// ------------------------------------------------------------------ the plan
+struct A2PlanImpl {
+  int B, T, H, W;
+  Conv3dGeom g[3];
+  int64_t ws_bytes = 0;
+  float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr;
+  int32_t* steps = nullptr;
+  float *cols[3], *y[3], *pooled, *f, *hc0, *sig, *adj, *g1, *g1d, *g2, *cat, *hp0, *s, *losses, *pseudo, *d_s,
+      *d_adj, *red, *dz_ap2, *dz_ap0, *dg2, *dz_ge0, *dz_cn2, *dz_cn0, *dfeat, *dpooled, *dA, *dcols, *scratch,
+      *norms, *ctrl;
+  int64_t* off_dev;
+  int64_t scratch_floats = 0;
+  int training = 1, with_loss = 0;
+  uint64_t seed = 0, step = 0;
+  int64_t clip0 = 0;
+
+  A2PlanImpl(int B_, int T_, int H_, int W_) : B(B_), T(T_), H(H_), W(W_) {
+    Vol5 in{B, 3, T, H, W};
+    const int sd[3] = {1, 2, 2};
+    for (int s = 0; s < 3; ++s) {
+      g[s] = conv3d_geom(in, A2_CO[s], 3, sd[s], 2, 2, 1);
+      in = g[s].out();
+    }
+  }
+  float* P(int s) const { return params + a2_offsets().off[s]; }
+  float* G(int s) const { return grads + a2_offsets().off[s]; }
+
+  void carve(Ws& w) {
+    int64_t max_y = 0, max_dcols = 1;
+    for (int s = 0; s < 3; ++s) {
+      cols[s] = w.take<float>(g[s].rows() * g[s].K());
+      y[s] = w.take<float>(g[s].out().numel());
+      max_y = std::max(max_y, g[s].out().numel());
+      if (s > 0) max_dcols = std::max(max_dcols, g[s].rows() * g[s].K());
+    }
+    const int64_t b = B;
+    pooled = w.take<float>(b * 4096);
+    f = w.take<float>(b * 16);
+    hc0 = w.take<float>(b * 32);
+    sig = w.take<float>(b * 256);
+    adj = w.take<float>(b * 256);
+    g1 = w.take<float>(b * 128);
+    g1d = w.take<float>(b * 128);
+    g2 = w.take<float>(b * 64);
+    cat = w.take<float>(b * 80);
+    hp0 = w.take<float>(b * 32);
+    s = w.take<float>(b);
+    losses = w.take<float>(16);
+    pseudo = w.take<float>(b);
+    d_s = w.take<float>(b);
+    d_adj = w.take<float>(b * 256);
+    red = w.take<float>(256);
+    dz_ap2 = w.take<float>(b);
+    dz_ap0 = w.take<float>(b * 32);
+    dg2 = w.take<float>(b * 64);
+    dz_ge0 = w.take<float>(b * 128);
+    dz_cn2 = w.take<float>(b * 256);
+    dz_cn0 = w.take<float>(b * 32);
+    dfeat = w.take<float>(b * 16);
+    dpooled = w.take<float>(b * 4096);
+    dA = w.take<float>(max_y);
+    dcols = w.take<float>(max_dcols);
+    scratch_floats = 8ll << 20;
+    scratch = w.take<float>(scratch_floats);
+    norms = w.take<float>(A2_NSLOT);
+    ctrl = w.take<float>(8);
+    off_dev = w.take<int64_t>(A2_NSLOT);
+  }
+
+  A2HeadArgs head_args() const {
+    A2HeadArgs a{};
+    a.B = B;
+    a.training = training;
+    a.with_loss = with_loss;
+    a.clip0 = clip0;
+    a.P = params;
+    a.off = off_dev;
+    a.f = f; a.hc0 = hc0; a.sig = sig; a.adj = adj; a.g1 = g1; a.g1d = g1d; a.g2 = g2; a.cat = cat; a.hp0 = hp0;
+    a.s = s;
+    a.h_graph = rng_h1(seed, S_A2_DROP_GRAPH, step);
+    a.h_pseudo = rng_h1(seed, S_A2_PSEUDO, step);
+    a.thr_graph = drop_threshold(0.3);
+    a.s_graph = 1.0f / (float)(1.0 - 0.3);
+    a.losses = losses;
+    a.pseudo = pseudo;
+    a.d_s = d_s;
+    a.d_adj = d_adj;
+    a.red = red;
+    return a;
+  }
+
+  int forward(const float* x, hipStream_t st) {
+    for (int s3 = 0; s3 < 3; ++s3) {
+      const float* src = s3 == 0 ? x : y[s3 - 1];
+      const Strides5 str = s3 == 0 ? ncdhw_strides(g[0].in) : ndhwc_strides(g[s3].in);
+      VAD_TRY(im2col3d(src, str, g[s3], nullptr, nullptr, 0, cols[s3], st));
+      DenseAct relu;
+      relu.relu = 1;
+      VAD_TRY(dense_fwd(cols[s3], (int)g[s3].rows(), g[s3].K(), P(2 * s3), P(2 * s3 + 1), A2_CO[s3], y[s3], relu,
+                        scratch, scratch_floats, st));
+    }
+    VAD_TRY(adaptive_avgpool3d_fwd(y[2], nullptr, 0, g[2].out(), 4, 4, 4, pooled, st));
+    DenseAct fc;
+    if (training) {
+      fc.drop = 1;
+      fc.h1 = rng_h1(seed, S_A2_DROP_FC, step);
+      fc.thr = drop_threshold(0.3);
+      fc.dscale = 1.0f / (float)(1.0 - 0.3);
+      fc.row0 = clip0;
+    }
+    VAD_TRY(dense_fwd(pooled, B, 4096, P(S_FCW), P(S_FCB), 16, f, fc, scratch, scratch_floats, st));
+    hipLaunchKernelGGL(a2_head_fwd_kernel, dim3(1), dim3(512), 0, st, head_args());
+    VAD_LAUNCH_CHECK();
+    if (with_loss) VAD_TRY(loss(st));
+    return 0;
+  }
+
+  int loss(hipStream_t st) {
+    with_loss = 1;
+    hipLaunchKernelGGL(a2_loss_kernel, dim3(1), dim3(512), 0, st, head_args());
+    VAD_LAUNCH_CHECK();
+    return 0;
+  }
+
+  int backward(const float* ext_ds, const float* ext_dadj, const float* ext_df, hipStream_t st) {
+    const bool from_loss = !ext_ds && !ext_dadj && !ext_df;
+    VAD_CHECK(!from_loss || with_loss, "vad_a2_backward: the forward computed no loss and no upstream grads given");
+    if (!from_loss) {
+      // external upstream grads replace the loss ones (zeros where absent)
+      VAD_HIP(hipMemsetAsync(d_s, 0, sizeof(float) * B, st));
+      VAD_HIP(hipMemsetAsync(d_adj, 0, sizeof(float) * B * 256, st));
+      if (ext_ds) VAD_HIP(hipMemcpyAsync(d_s, ext_ds, sizeof(float) * B, hipMemcpyDeviceToDevice, st));
+      if (ext_dadj) VAD_HIP(hipMemcpyAsync(d_adj, ext_dadj, sizeof(float) * B * 256, hipMemcpyDeviceToDevice, st));
+    }
+    A2HeadBwdArgs hb{};
+    hb.f = head_args();
+    hb.d_s = d_s;
+    hb.d_adj = d_adj;
+    hb.d_f = from_loss ? nullptr : ext_df;
+    hb.G = grads;
+    hb.dz_ap2 = dz_ap2; hb.dz_ap0 = dz_ap0; hb.dg2 = dg2; hb.dz_ge0 = dz_ge0; hb.dz_cn2 = dz_cn2; hb.dz_cn0 = dz_cn0;
+    hb.dfeat = dfeat;
+    hb.h_fc = rng_h1(seed, S_A2_DROP_FC, step);
+    hb.thr_fc = drop_threshold(0.3);
+    hb.s_fc = 1.0f / (float)(1.0 - 0.3);
+    hipLaunchKernelGGL(a2_head_bwd_kernel, dim3(1), dim3(512), 0, st, hb);
+    VAD_LAUNCH_CHECK();
+    VAD_TRY(dense_wgrad(dfeat, B, 16, pooled, 4096, G(S_FCW), G(S_FCB), scratch, scratch_floats, nullptr, st));
+    VAD_TRY(dense_dgrad(dfeat, B, 16, P(S_FCW), 4096, dpooled, nullptr, 1.f, nullptr, st));
+    VAD_TRY(adaptive_avgpool3d_bwd(dpooled, g[2].out(), 4, 4, 4, dA, st));
+    for (int s3 = 2; s3 >= 0; --s3) {
+      const int64_t rows = g[s3].rows();
+      VAD_TRY(relu_gate(dA, y[s3], rows * A2_CO[s3], st));
+      VAD_TRY(dense_wgrad(dA, (int)rows, A2_CO[s3], cols[s3], g[s3].K(), G(2 * s3), G(2 * s3 + 1), scratch,
+                          scratch_floats, nullptr, st));
+      if (s3 > 0) {
+        VAD_TRY(dense_dgrad(dA, (int)rows, A2_CO[s3], P(2 * s3), g[s3].K(), dcols, nullptr, 1.f, nullptr, st));
+        VAD_TRY(col2im3d(dcols, g[s3], dA, st));
+      }
+    }
+    return 0;
+  }
+
+  int optimizer(float lr, float b1, float b2, float eps, float wd, float max_norm, hipStream_t st) {
+    A2SlotTab t{};
+    for (int i = 0; i < A2_NSLOT; ++i) {
+      t.off[i] = a2_offsets().off[i];
+      t.numel[i] = A2_SLOTS[i].numel;
+    }
+    hipLaunchKernelGGL(a2_sqsum_kernel, dim3(A2_NSLOT), dim3(256), 0, st, grads, t, norms);
+    VAD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(a2_opt_prepare_kernel, dim3(1), dim3(64), 0, st, norms, losses, steps, lr, b1, b2, wd,
+                       max_norm, ctrl);
+    VAD_LAUNCH_CHECK();
+    const int64_t n = a2_offsets().total;
+    hipLaunchKernelGGL(a2_adamw_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 1024)), dim3(256), 0, st,
+                       params, grads, m, v, n, ctrl, b1, b2, eps);
+    VAD_LAUNCH_CHECK();
+    return 0;
+  }
+};
+
+}  // namespace vad
+
+using namespace vad;
+
+struct vad_a2_plan {
+  vad_a2_plan(int B, int T, int H, int W) : impl(B, T, H, W) {}
+  A2PlanImpl impl;
+  float* user_losses = nullptr;
+};
+
+extern "C" {
+
+int vad_a2_num_slots(void) { return A2_NSLOT; }
+const char* vad_a2_slot_name(int i) { return (i >= 0 && i < A2_NSLOT) ? A2_SLOTS[i].name : nullptr; }
+int64_t vad_a2_slot_numel(int i) { return (i >= 0 && i < A2_NSLOT) ? A2_SLOTS[i].numel : -1; }
+int64_t vad_a2_slot_offset(int i) { return (i >= 0 && i < A2_NSLOT) ? a2_offsets().off[i] : -1; }
+int64_t vad_a2_param_floats(void) { return a2_offsets().total; }
+
+int vad_a2_create(int B, int T, int H, int W, vad_a2_plan** out) {
+  VAD_CHECK(out != nullptr, "vad_a2_create: out is null");
+  VAD_CHECK(B >= 2 && B <= A2_MAXB && T >= 1 && H >= 4 && W >= 4,
+            "vad_a2_create: unsupported shape (2 <= B <= 256: the loss squeezes the scores to (B,))");
+  auto* p = new vad_a2_plan(B, T, H, W);
+  Ws ws;
+  p->impl.carve(ws);
+  p->impl.ws_bytes = ws.off + 256;
+  *out = p;
+  return 0;
+}
+
+void vad_a2_destroy(vad_a2_plan* plan) { delete plan; }
+int64_t vad_a2_workspace_bytes(const vad_a2_plan* p) { return p ? p->impl.ws_bytes : -1; }
+
+int vad_a2_bind(vad_a2_plan* plan, void* workspace, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                int32_t* steps) {
+  VAD_CHECK(plan && workspace && params && grads && exp_avg && exp_avg_sq && steps, "vad_a2_bind: null argument");
+  VAD_CHECK((reinterpret_cast<uintptr_t>(workspace) & 255) == 0, "vad_a2_bind: workspace must be 256-B aligned");
+  A2PlanImpl& c = plan->impl;
+  Ws ws;
+  ws.base = reinterpret_cast<char*>(workspace);
+  ws.dry = false;
+  c.carve(ws);
+  c.params = params; c.grads = grads; c.m = exp_avg; c.v = exp_avg_sq; c.steps = steps;
+  VAD_HIP(hipMemcpy(c.off_dev, a2_offsets().off, sizeof(int64_t) * A2_NSLOT, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int vad_a2_forward(vad_a2_plan* plan, const float* x, int training, uint64_t seed, uint64_t step, int64_t clip0,
+                   int with_loss, float* scores, float* adj, float* features, float* losses, void* stream) {
+  VAD_CHECK(plan && x, "vad_a2_forward: null argument");
+  A2PlanImpl& c = plan->impl;
+  VAD_CHECK(c.params != nullptr, "vad_a2_forward: plan not bound");
+  hipStream_t st = (hipStream_t)stream;
+  c.training = training;
+  c.seed = seed;
+  c.step = step;
+  c.clip0 = clip0;
+  c.with_loss = with_loss;
+  VAD_TRY(c.forward(x, st));
+  const int B = c.B;
+  if (scores) VAD_HIP(hipMemcpyAsync(scores, c.s, sizeof(float) * B, hipMemcpyDeviceToDevice, st));
+  if (adj) VAD_HIP(hipMemcpyAsync(adj, c.adj, sizeof(float) * B * 256, hipMemcpyDeviceToDevice, st));
+  if (features) VAD_HIP(hipMemcpyAsync(features, c.f, sizeof(float) * B * 16, hipMemcpyDeviceToDevice, st));
+  plan->user_losses = losses;
+  if (losses && with_loss) VAD_HIP(hipMemcpyAsync(losses, c.losses, sizeof(float) * 10, hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+
+int vad_a2_loss(vad_a2_plan* plan, uint64_t seed, uint64_t step, int64_t clip0, float* losses, void* stream) {
+  VAD_CHECK(plan != nullptr, "vad_a2_loss: null plan");
+  A2PlanImpl& c = plan->impl;
+  hipStream_t st = (hipStream_t)stream;
+  c.seed = seed;
+  c.step = step;
+  c.clip0 = clip0;
+  VAD_TRY(c.loss(st));
+  plan->user_losses = losses;
+  if (losses) VAD_HIP(hipMemcpyAsync(losses, c.losses, sizeof(float) * 10, hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+
+int vad_a2_loss_grads(vad_a2_plan* plan, float* d_scores, float* d_adj, void* stream) {
+  VAD_CHECK(plan != nullptr, "vad_a2_loss_grads: null plan");
+  A2PlanImpl& c = plan->impl;
+  hipStream_t st = (hipStream_t)stream;
+  if (d_scores) VAD_HIP(hipMemcpyAsync(d_scores, c.d_s, sizeof(float) * c.B, hipMemcpyDeviceToDevice, st));
+  if (d_adj) VAD_HIP(hipMemcpyAsync(d_adj, c.d_adj, sizeof(float) * c.B * 256, hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+
+int vad_a2_backward(vad_a2_plan* plan, const float* d_scores, const float* d_adj, const float* d_features,
+                    void* stream) {
+  VAD_CHECK(plan != nullptr, "vad_a2_backward: null plan");
+  return plan->impl.backward(d_scores, d_adj, d_features, (hipStream_t)stream);
+}
+
+int vad_a2_optimizer_step(vad_a2_plan* plan, float lr, float beta1, float beta2, float eps, float weight_decay,
+                          float max_norm, void* stream) {
+  VAD_CHECK(plan != nullptr, "vad_a2_optimizer_step: null plan");
+  A2PlanImpl& c = plan->impl;
+  hipStream_t st = (hipStream_t)stream;
+  VAD_TRY(c.optimizer(lr, beta1, beta2, eps, weight_decay, max_norm, st));
+  if (plan->user_losses)
+    VAD_HIP(hipMemcpyAsync(plan->user_losses, c.losses, sizeof(float) * 10, hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+
+}  // extern "C"

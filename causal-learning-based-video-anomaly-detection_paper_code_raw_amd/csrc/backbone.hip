@@ -570,7 +570,7 @@ struct DenseEpiArgs {
 
 __device__ inline float dense_finish(const DenseEpiArgs& P, int row, int col, float v) {
   if (P.bias) v += P.bias[col];
-  if (P.relu) v = fmaxf(v, 0.f);
+  if (P.relu) v = relu_nan(v);
   if (P.drop) v = (rng_u24(P.h1, (uint64_t)(P.row0 + row), (uint64_t)col) >= P.thr) ? v * P.dscale : 0.f;
   if (P.gate) v = P.gate[(int64_t)row * P.ldc + col] > 0.f ? v * P.gscale : 0.f;
   return v;

@@ -9,6 +9,7 @@
 #include "backbone.h"
 #include "head.h"
 #include "mlp.h"
+#include "plan_util.h"
 
 namespace vad {
 
@@ -280,19 +281,6 @@ struct Profiler {
   } while (0)
 
 // ------------------------------------------------------------------ the plan
-struct Ws {
-  char* base = nullptr;
-  int64_t off = 0;
-  bool dry = true;
-  template <class T>
-  T* take(int64_t n) {
-    off = (off + 255) / 256 * 256;
-    T* p = dry ? nullptr : reinterpret_cast<T*>(base + off);
-    off += n * (int64_t)sizeof(T);
-    return p;
-  }
-};
-
 struct CadPlanImpl {
   int B, T, H, W, NF;
   int H1, W1, HP, WP, HF, WF;

@@ -99,6 +99,10 @@ __device__ inline float wave_sum(float v) {
 
 // f32-in / f32-acc MFMA 32x32x2: lane l supplies A[l&31][l>>5], B[l>>5][l&31];
 // D row = (r&3) + 8*(r>>2) + 4*(l>>5), col = l&31.
+// torch.relu semantics: NaN propagates (fmaxf(NaN, 0) would return 0 and hide a non-finite batch from the
+// trainers' NaN checks, mc:281 / a2:230)
+__device__ inline float relu_nan(float v) { return v > 0.f ? v : (v == v ? 0.f : v); }
+
 __device__ inline f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }

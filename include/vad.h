@@ -105,6 +105,75 @@ int vad_conv3x3_wgrad(const float* x_nhwc, const float* dy_nhwc, int NF, int Ci,
                       float* dW, float* partial, int64_t partial_floats, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * minicausal_vad_complete3.py — SimpleVideoAnomalyDetector (mc:25-102) + StableTrainer step (mc:249-330)
+ * replaces: model(data) (mc:272), criterion(outputs, targets) (mc:284), loss.backward() (mc:292), the grad
+ * NaN check / norm / conditional clip (mc:294-306) and optimizer.step() (mc:308, Adam lr 1e-3 wd 1e-5, mc:229-234)
+ * ------------------------------------------------------------------------------------------ */
+typedef struct vad_mc_plan vad_mc_plan;
+
+/* x: (B, C, T, H, W) fp32 NCDHW (torch layout) */
+int vad_mc_create(int B, int C, int T, int H, int W, vad_mc_plan** out);
+void vad_mc_destroy(vad_mc_plan* plan);
+/* slot i = i-th entry of model.named_parameters(); buffers = BatchNorm3d running stats (state_dict order) */
+int vad_mc_num_slots(const vad_mc_plan* plan);
+const char* vad_mc_slot_name(const vad_mc_plan* plan, int i);
+int64_t vad_mc_slot_numel(const vad_mc_plan* plan, int i);
+int64_t vad_mc_slot_offset(const vad_mc_plan* plan, int i);
+int64_t vad_mc_param_floats(const vad_mc_plan* plan);
+int vad_mc_num_bufs(const vad_mc_plan* plan);
+const char* vad_mc_buf_name(const vad_mc_plan* plan, int i);
+int64_t vad_mc_buf_numel(const vad_mc_plan* plan, int i);
+int64_t vad_mc_buf_offset(const vad_mc_plan* plan, int i);
+int64_t vad_mc_buf_floats(const vad_mc_plan* plan);
+int64_t vad_mc_workspace_bytes(const vad_mc_plan* plan);
+/* nbt: int64[3] num_batches_tracked; steps: int32[num_slots] Adam step counters */
+int vad_mc_bind(vad_mc_plan* plan, void* workspace, float* params, float* grads, float* bufs, int64_t* nbt,
+                float* exp_avg, float* exp_avg_sq, int32_t* steps);
+/* scores: (B,) sigmoid outputs.  labels (B,) fp32 nullable -> BCE.  losses (nullable, float[4]): bce, grad norm,
+ * clipped (0/1), status (0 skipped: non-finite outputs/loss; 1 counted, no step: non-finite grads; 2 stepped) —
+ * the last three are filled by vad_mc_optimizer_step.  Dropout keys: (seed, step, clip0 + b). */
+int vad_mc_forward(vad_mc_plan* plan, const float* x, int training, uint64_t seed, uint64_t step, int64_t clip0,
+                   const float* labels, float* scores, float* losses, int32_t* flags, void* stream);
+/* d_scores (B,) nullable: NULL = backward of the forward's BCE (requires labels) */
+int vad_mc_backward(vad_mc_plan* plan, const float* d_scores, void* stream);
+/* grad norm (float64 sum of per-param norm^2); clip_grad_norm_(max_norm) only when norm > clip_above; Adam */
+int vad_mc_optimizer_step(vad_mc_plan* plan, float lr, float beta1, float beta2, float eps, float weight_decay,
+                          float clip_above, float max_norm, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * avenue_training_script2.py — a2 CausalAnomalyDetector (a2:15-101), compute_improved_loss (a2:135-205) and the
+ * ImprovedMiniCausalVAD step (a2:218-245).  replaces: self.model(videos) (a2:224), compute_improved_loss (a2:227),
+ * loss.backward() (a2:235), clip_grad_norm_(0.5) (a2:236), AdamW(lr 5e-4, wd 1e-3).step() (a2:115-119, 238)
+ * ------------------------------------------------------------------------------------------ */
+typedef struct vad_a2_plan vad_a2_plan;
+
+int vad_a2_num_slots(void);            /* 20 = model.named_parameters() order (188,849 parameters) */
+const char* vad_a2_slot_name(int i);
+int64_t vad_a2_slot_numel(int i);
+int64_t vad_a2_slot_offset(int i);
+int64_t vad_a2_param_floats(void);
+/* x: (B, 3, T, H, W) fp32 NCDHW, 2 <= B <= 256 */
+int vad_a2_create(int B, int T, int H, int W, vad_a2_plan** out);
+void vad_a2_destroy(vad_a2_plan* plan);
+int64_t vad_a2_workspace_bytes(const vad_a2_plan* plan);
+int vad_a2_bind(vad_a2_plan* plan, void* workspace, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                int32_t* steps);
+/* outputs (nullable): scores (B,), adj (B,16,16), features (B,16).  with_loss: compute_improved_loss with
+ * pseudo-labels keyed (seed, step, clip0 + b); losses float[10]: total, anomaly, acyclicity, sparsity,
+ * consistency, structure, edge_count, sparsity_ratio, grad norm (optimizer), status (0 NaN skip, 2 stepped) */
+int vad_a2_forward(vad_a2_plan* plan, const float* x, int training, uint64_t seed, uint64_t step, int64_t clip0,
+                   int with_loss, float* scores, float* adj, float* features, float* losses, void* stream);
+/* compute_improved_loss alone, on the last forward's scores / adjacency (pseudo-labels keyed by seed/step/clip0);
+ * vad_a2_loss_grads copies d total / d scores (B,) and d total / d adj (B,16,16) of that loss */
+int vad_a2_loss(vad_a2_plan* plan, uint64_t seed, uint64_t step, int64_t clip0, float* losses, void* stream);
+int vad_a2_loss_grads(vad_a2_plan* plan, float* d_scores, float* d_adj, void* stream);
+/* all upstream grads NULL: backward of the forward's loss; else the given (nullable) output grads */
+int vad_a2_backward(vad_a2_plan* plan, const float* d_scores, const float* d_adj, const float* d_features,
+                    void* stream);
+int vad_a2_optimizer_step(vad_a2_plan* plan, float lr, float beta1, float beta2, float eps, float weight_decay,
+                          float max_norm, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Debug introspection (tests only): internal plan buffers, partial backward, device->host copy
  * names: y1, pool, y[0..7], stats[0..8], feats, pooled, dA, dY, d_pooled, d_feat_det, det_logits
  * ------------------------------------------------------------------------------------------ */

@@ -31,6 +31,18 @@ CAD_CASES = [
     dict(name="fallback_b2t16_227", B=2, T=16, H=227, W=227, seed=3, step=0, forced=None),
 ]
 
-MC_CASES = []
-A2_CASES = []
+# minicausal (config 1 family): scale > 1 multiplies the last classifier layer so the pre-clip grad norm exceeds 10
+# and StableTrainer's clip branch (mc:304-306) runs
+MC_CASES = [
+    dict(name="b4t8_32", B=4, T=8, H=32, W=32, seed=10, step=0, scale=1.0),
+    dict(name="b8t16_64", B=8, T=16, H=64, W=64, seed=11, step=2, scale=1.0),
+    dict(name="clip_b4t8_32x48", B=4, T=8, H=32, W=48, seed=12, step=1, scale=12000.0),
+]
+# a2 (avenue_training_script2.py): "ckpt" starts from the reference's shipped best_improved_model.pth (stored as
+# tests/golden/a2_best_improved_model.npz); seeds/steps chosen so both pseudo-label classes occur (a2:139-141)
+A2_CASES = [
+    dict(name="ckpt_b4t8_64", B=4, T=8, H=64, W=64, seed=22, step=0, ckpt=True),
+    dict(name="ckpt_b6t8_64_pseudo", B=6, T=8, H=64, W=64, seed=21, step=0, ckpt=True),
+    dict(name="init_b6t8_48x40_pseudo", B=6, T=8, H=48, W=40, seed=25, step=2, ckpt=False),
+]
 BBOX_CASES = []

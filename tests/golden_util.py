@@ -6,6 +6,8 @@ import numpy as np
 import torch
 
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+# the reference's shipped a2 checkpoint (best_improved_model.pth, model_state_dict) exported as a safe .npz
+A2_CKPT = "a2_best_improved_model.npz"
 
 
 def load(name):

@@ -1,0 +1,84 @@
+"""a2 (avenue_training_script2.py) on the GPU: the HIP plan (vad_a2_*) against the reference fixtures (incl. the
+shipped checkpoint) and the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import a2_oracle as ao
+from tests.golden.cases import A2_CASES
+from tests.golden_util import load
+from tests.test_a2_oracle import make_a2_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _vad(case):
+    from vad_amd.a2 import ImprovedMiniCausalVAD
+    vad = ImprovedMiniCausalVAD(device="cuda")
+    vad.model = make_a2_model(case).to("cuda")
+    vad.seed, vad.global_step, vad.clip0 = case["seed"], case["step"], 0
+    return vad
+
+
+@pytest.mark.parametrize("case", A2_CASES, ids=[c["name"] for c in A2_CASES])
+def test_a2_step_matches_reference(case):
+    g = load(f"a2_{case['name']}.npz")
+    vad = _vad(case)
+    B, T, H, W = case["B"], case["T"], case["H"], case["W"]
+    x = ao.synth_clips(case["seed"], case["step"], 0, B, T, H, W)
+    avg, comps = vad.train_epoch_improved([(x, ao.synth_labels(0, B))])
+    e = vad.model._engine
+    p = e.cur
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(p.scores.cpu().numpy(), g["out/scores"].reshape(-1), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(p.adj.cpu().numpy(), g["out/adj"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(p.feats.cpu().numpy(), g["out/features"], rtol=1e-4, atol=1e-5)
+    assert avg == pytest.approx(float(g["loss/total"]), rel=1e-4)
+    for k, v in comps.items():
+        assert v == pytest.approx(float(g[f"loss/{k}"]), rel=1e-4, abs=1e-6), k
+    assert float(e.losses[8]) == pytest.approx(float(g["grad_total_norm"]), rel=1e-3)
+    sd = dict(vad.model.named_parameters())
+    for name, off, n in e.slots:
+        gf = e.grads[off:off + n].cpu().numpy()
+        ref = float(g[f"grad_norm/{name}"])
+        assert float(np.linalg.norm(gf.astype(np.float64))) == pytest.approx(ref, rel=2e-3, abs=1e-12), name
+        np.testing.assert_allclose(gf[g[f"idx/{name}"]], g[f"grad/{name}"], rtol=2e-3,
+                                   atol=2e-4 * ref / np.sqrt(n) + 1e-12, err_msg=name)
+        np.testing.assert_allclose(sd[name].detach().cpu().numpy().reshape(-1)[g[f"idx/{name}"]], g[f"post/{name}"],
+                                   rtol=1e-6, atol=2.5e-5, err_msg=name)
+    x2 = ao.synth_clips(case["seed"], case["step"] + 1, B, B, T, H, W)
+    preds, graphs, metrics = vad.evaluate_improved([(x2, ao.synth_labels(B, B))])
+    np.testing.assert_allclose(preds, g["eval/preds"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(graphs, g["eval/graphs"], rtol=1e-4, atol=1e-6)
+    for k, v in metrics.items():
+        if k == "unique_graphs":
+            assert v == int(g[f"eval/{k}"])
+        elif k in ("avg_edges", "avg_sparsity"):
+            assert v == pytest.approx(float(g[f"eval/{k}"]), abs=1e-9), k  # counts of adj > 0.1
+        else:
+            assert v == pytest.approx(float(g[f"eval/{k}"]), rel=1e-4, abs=1e-6), k
+
+
+def test_a2_autograd_loss_path_matches_oracle():
+    """model(x) -> compute_improved_loss -> loss.backward() through torch autograd (the reference's own call
+    sequence, a2:224-235) against the oracle's autograd."""
+    case = dict(B=5, T=6, H=40, W=48, seed=23, step=0, ckpt=True)
+    vad = _vad(case)
+    x = ao.synth_clips(23, 0, 0, 5, 6, 40, 48)
+    vad.model.train()
+    s, adj, f = vad.model(x.cuda(), seed=23, step=0, clip0=0)
+    loss, comps = vad.compute_improved_loss(s, adj, torch.zeros(5, device="cuda"), f)
+    loss.backward()
+    m = make_a2_model(case)
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    draws = ao.A2Draws.make(23, 0, 0, 5)
+    rs, radj, rf = ao.a2_forward(leaves, x, draws, True)
+    rtot, rcomps, _ = ao.a2_loss(rs, radj, draws.u_pseudo)
+    rtot.backward()
+    assert float(loss) == pytest.approx(float(rtot), rel=1e-4)
+    for k in rcomps:
+        assert comps[k] == pytest.approx(rcomps[k], rel=1e-4, abs=1e-6), k
+    for n, p in vad.model.named_parameters():
+        gr, gref = p.grad.cpu().numpy(), leaves[n].grad.numpy()
+        scale = float(np.abs(gref).max()) + 1e-12
+        np.testing.assert_allclose(gr, gref, rtol=2e-3, atol=2e-4 * scale, err_msg=n)
