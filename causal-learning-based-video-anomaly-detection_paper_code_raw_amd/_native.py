@@ -84,6 +84,17 @@ _SIGS = {
     "vad_a2_loss_grads": (_I, [_P, _P, _P, _P]),
     "vad_a2_backward": (_I, [_P, _P, _P, _P, _P]),
     "vad_a2_optimizer_step": (_I, [_P, _F, _F, _F, _F, _F, _F, _P]),
+    # bbox clip scorer (config 5)
+    "vad_bbox_num_slots": (_I, []),
+    "vad_bbox_slot_name": (ctypes.c_char_p, [_I]),
+    "vad_bbox_slot_numel": (_I64, [_I]),
+    "vad_bbox_slot_offset": (_I64, [_I]),
+    "vad_bbox_param_floats": (_I64, []),
+    "vad_bbox_create": (_I, [_I, _I, _I, _I, ctypes.POINTER(_P)]),
+    "vad_bbox_destroy": (None, [_P]),
+    "vad_bbox_workspace_bytes": (_I64, [_P]),
+    "vad_bbox_bind": (_I, [_P, _P, _P]),
+    "vad_bbox_forward": (_I, [_P, _P, _P, _P, _P, _P]),
 }
 
 

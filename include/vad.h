@@ -174,6 +174,25 @@ int vad_a2_optimizer_step(vad_a2_plan* plan, float lr, float beta1, float beta2,
                           float max_norm, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * avenue_training_script_bbox.py — CausalAnomalyDetector forward (bbox:51-101), eval mode, as run by
+ * AnomalyVisualizer.predict_anomaly_for_clip (bbox:339-368).  replaces: self.model(video_tensor) (bbox:357)
+ * ------------------------------------------------------------------------------------------ */
+typedef struct vad_bbox_plan vad_bbox_plan;
+
+int vad_bbox_num_slots(void);          /* 12 = model.named_parameters() order */
+const char* vad_bbox_slot_name(int i);
+int64_t vad_bbox_slot_numel(int i);
+int64_t vad_bbox_slot_offset(int i);
+int64_t vad_bbox_param_floats(void);
+/* x: (B, 3, T, H, W) fp32 NCDHW, one clip length per plan (mixed-T batches: one plan per T) */
+int vad_bbox_create(int B, int T, int H, int W, vad_bbox_plan** out);
+void vad_bbox_destroy(vad_bbox_plan* plan);
+int64_t vad_bbox_workspace_bytes(const vad_bbox_plan* plan);
+int vad_bbox_bind(vad_bbox_plan* plan, void* workspace, const float* params);
+/* scores (B,), adj (B,16,16), features (B,1024, nullable) */
+int vad_bbox_forward(vad_bbox_plan* plan, const float* x, float* scores, float* adj, float* features, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Debug introspection (tests only): internal plan buffers, partial backward, device->host copy
  * names: y1, pool, y[0..7], stats[0..8], feats, pooled, dA, dY, d_pooled, d_feat_det, det_logits
  * ------------------------------------------------------------------------------------------ */

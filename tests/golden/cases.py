@@ -45,4 +45,9 @@ A2_CASES = [
     dict(name="ckpt_b6t8_64_pseudo", B=6, T=8, H=64, W=64, seed=21, step=0, ckpt=True),
     dict(name="init_b6t8_48x40_pseudo", B=6, T=8, H=48, W=40, seed=25, step=2, ckpt=False),
 ]
-BBOX_CASES = []
+# bbox clip scorer (config 5): eval mode, one case per clip length of the mixed-T packing
+BBOX_CASES = [
+    dict(name="t8", B=3, T=8, H=64, W=64, seed=30, step=0),
+    dict(name="t16", B=2, T=16, H=64, W=64, seed=31, step=0),
+    dict(name="t32_48x56", B=2, T=32, H=48, W=56, seed=32, step=0),
+]

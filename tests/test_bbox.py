@@ -1,0 +1,70 @@
+"""bbox clip scorer (config 5): the CPU oracle against the reference's own predict_anomaly_for_clip fixtures, and
+(GPU) the HIP plan against both, including mixed-T packing."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import bbox_oracle as bo
+from tests.golden.cases import BBOX_CASES
+from tests.golden_util import load
+
+
+def make_bbox_model(case):
+    from vad_amd.bbox import CausalAnomalyDetector
+    torch.manual_seed(case["seed"])
+    return CausalAnomalyDetector().eval()
+
+
+@pytest.mark.parametrize("case", BBOX_CASES, ids=[c["name"] for c in BBOX_CASES])
+def test_bbox_init_and_oracle_match_reference(case):
+    g = load(f"bbox_{case['name']}.npz")
+    m = make_bbox_model(case)
+    for n, t in m.state_dict().items():
+        assert np.float64(t.double().sum()) == g[f"init_sum/{n}"], n
+        assert np.float64((t.double() ** 2).sum()) == g[f"init_sq/{n}"], n
+    p = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    x = bo.synth_clips(case["seed"], case["step"], 0, case["B"], case["T"], case["H"], case["W"])
+    with torch.no_grad():
+        s, adj, f = bo.bbox_forward(p, x)
+    np.testing.assert_allclose(s.numpy(), g["out/scores"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(adj.numpy(), g["out/adj"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(f.numpy(), g["out/features"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(s.numpy(), g["batch/scores"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", BBOX_CASES, ids=[c["name"] for c in BBOX_CASES])
+def test_bbox_hip_matches_reference(case):
+    g = load(f"bbox_{case['name']}.npz")
+    from vad_amd.bbox import AnomalyVisualizer
+    vis = AnomalyVisualizer(None, device="cuda")
+    vis.model = make_bbox_model(case).cuda()
+    x = bo.synth_clips(case["seed"], case["step"], 0, case["B"], case["T"], case["H"], case["W"])
+    for b in range(case["B"]):
+        s, adj, f = vis.predict_anomaly_for_clip(x[b].numpy())
+        assert s == pytest.approx(float(g["out/scores"][b]), rel=1e-4, abs=1e-6)
+        np.testing.assert_allclose(adj, g["out/adj"][b], rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(f, g["out/features"][b], rtol=1e-4, atol=1e-5)
+    with torch.no_grad():
+        s, adj, f = vis.model(x.cuda())
+    np.testing.assert_allclose(s.cpu().numpy(), g["batch/scores"], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_bbox_mixed_t_packing_matches_oracle():
+    """Clips of T in {8,16,32} scored in one call (one packed batch per T) equal per-clip oracle results."""
+    from vad_amd.bbox import AnomalyVisualizer
+    case = dict(seed=33)
+    vis = AnomalyVisualizer(None, device="cuda")
+    vis.model = make_bbox_model(case).cuda()
+    p = {k: v.detach().cpu().clone() for k, v in make_bbox_model(case).state_dict().items()}
+    clips = []
+    for i, T in enumerate([8, 32, 16, 8, 16, 32, 8]):
+        clips.append(bo.synth_clips(33, 0, i, 1, T, 64, 64)[0].numpy())
+    res = vis.predict_clips(clips)
+    for c, (s, adj, f) in zip(clips, res):
+        with torch.no_grad():
+            rs, radj, rf = bo.bbox_forward(p, torch.from_numpy(c)[None])
+        assert s == pytest.approx(float(rs), rel=1e-4, abs=1e-6)
+        np.testing.assert_allclose(adj, radj[0].numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(f, rf[0].numpy(), rtol=1e-4, atol=1e-5)

@@ -26,6 +26,7 @@ def _trainer(case, model):
 def test_mc_step_matches_reference(case):
     g = load(f"mc_{case['name']}.npz")
     model = make_mc_model(case)
+    init = {n: p.detach().clone().numpy().reshape(-1) for n, p in model.named_parameters()}
     tr = _trainer(case, model)
     avg_loss, acc = tr.train_epoch()
     e = model._engine
@@ -48,15 +49,21 @@ def test_mc_step_matches_reference(case):
             wn = float(g[f"grad_norm/{name[:-4]}weight"])
             assert float(np.abs(gf).max()) <= 1e-5 * wn + 1e-9, name
             continue
-        assert float(np.linalg.norm(gf.astype(np.float64))) == pytest.approx(ref, rel=2e-3, abs=1e-12), name
+        rel = 1e-2 if name.startswith("features.") else 2e-3
+        assert float(np.linalg.norm(gf.astype(np.float64))) == pytest.approx(ref, rel=rel, abs=1e-12), name
         # conv weight grads are sums over up to 5e5 voxels with heavy cancellation (BN-backward dY): the GPU's and
         # the reference CPU's summation orders agree to ~1e-3 of the vector norm, not per tiny element
+        # (the 0.01-std classifier init makes the feature-stack grads ~1e-7 against O(1) summed terms: 2e-2 there)
         sampled, want = gf[g[f"idx/{name}"]].astype(np.float64), g[f"grad/{name}"].astype(np.float64)
-        assert np.linalg.norm(sampled - want) <= 5e-3 * np.linalg.norm(want) + 1e-12, name
-        # Adam's first update is lr * g / (|g| + eps): for |g| well above eps (1e-8) it is +-lr whatever the
-        # rounding; for |g| within ~100 eps a rounding-level grad difference moves it by up to lr (1e-3)
+        tol = 2e-2 if name.startswith("features.") else 5e-3
+        assert np.linalg.norm(sampled - want) <= tol * np.linalg.norm(want) + 1e-12, name
+        # Adam's first update is lr * g' / (|g'| + eps) with g' = clip_coef * g + wd * p (coupled L2): for |g'| well
+        # above eps (1e-8) it is +-lr whatever the rounding; for |g'| within ~100 eps (incl. g and wd * p cancelling)
+        # a rounding-level grad difference moves it by up to lr (1e-3)
         got = sd[name].detach().cpu().numpy().reshape(-1)[g[f"idx/{name}"]]
-        near_eps = np.abs(g[f"grad/{name}"]) < 1e-6
+        coef = min(1.0, 1.0 / (float(g["grad_norm"]) + 1e-6)) if int(g["clipped"]) else 1.0
+        g_eff = coef * g[f"grad/{name}"] + 1e-5 * init[name][g[f"idx/{name}"]]
+        near_eps = np.abs(g_eff) < 1e-6
         np.testing.assert_allclose(got[~near_eps], g[f"post/{name}"][~near_eps], rtol=1e-6, atol=5e-5, err_msg=name)
         np.testing.assert_allclose(got[near_eps], g[f"post/{name}"][near_eps], rtol=0, atol=1.01e-3, err_msg=name)
     for name, t in sd.items():
