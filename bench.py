@@ -59,6 +59,21 @@ def algorithmic_work(label, B, T, H, W):
     return None, None
 
 
+def pmc_traffic(family):
+    """HBM bytes per launch of a conv family from the latest committed PMC summary (tools/pmc_traffic.py over two
+    rocprofv3 --pmc passes of this bench), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    fam = d.get("families", {}).get(family)
+    if not fam:
+        return None, None
+    return fam["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def run_gpu(args, rank, world, local_rank):
     import torch
     import torch.distributed as dist
@@ -144,6 +159,11 @@ def run_gpu(args, rank, world, local_rank):
                     "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 4), "traffic": None}
         roof["launches_timed"] = launches
         roof["avg_launch_us"] = round(1e3 * tot_ms / max(launches, 1), 2)
+        traffic, src = pmc_traffic(dominant)
+        if traffic is not None:
+            roof["traffic"] = round(traffic)
+            roof["traffic_unit"] = "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE)"
+            roof["traffic_source"] = src
     step_ms = 1e3 * elapsed / args.steps
     # whole-step algorithmic FLOP rate (all 3x3 convs fwd/dgrad/wgrad + conv1 fwd), for context
     conv_flops = sum(2.0 * NF * oh * ow * co * ci * 9 for NF, ci, co, oh, ow in conv_shapes(B, T, H, W))

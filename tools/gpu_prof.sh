@@ -1,5 +1,8 @@
+# rocprofv3 passes for profiles/: kernel stats, then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
 set -o pipefail
 mkdir -p gpurun_out
 ROOT=$(pwd)
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $ROOT/gpurun_out/prof -o run -- python3 $ROOT/bench.py --no-cpu-baseline --steps 20 > $ROOT/gpurun_out/prof_bench.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/prof -o run -- python3 $ROOT/bench.py --no-cpu-baseline --steps 20 > $ROOT/gpurun_out/prof_bench.log 2>&1 && \
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $ROOT/gpurun_out/pmc_fetch -o run -- python3 $ROOT/bench.py --no-cpu-baseline --steps 3 --warmup 2 > $ROOT/gpurun_out/pmc_fetch.log 2>&1 && \
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $ROOT/gpurun_out/pmc_write -o run -- python3 $ROOT/bench.py --no-cpu-baseline --steps 3 --warmup 2 > $ROOT/gpurun_out/pmc_write.log 2>&1

@@ -1,0 +1,64 @@
+"""Summarise two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; tools/gpu_prof.sh) into HBM bytes per launch for
+the conv kernel families that bench.py can name as dominant.
+
+Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE / WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports
+half the bytes of 16-B-per-lane streaming reads (all conv kernels stage with 16-B loads), so it is doubled;
+WRITE_SIZE is exact for 16-B stores and taken as is for the 4-B epilogue stores (uncalibrated, noted).
+Usage: python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/<round>_pmc_traffic.json
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def family(name):
+    if "conv3x3_wgrad_patch_kernel" in name or ("gemm_kernel" in name and "ConvPatchKM" in name):
+        return "conv_wgrad"
+    if "conv3x3_patch_kernel" in name:
+        return "conv_fwd" if ", true>" in name else "conv_dgrad"
+    if "conv3x3_dgrad_s2_kernel" in name or ("gemm_kernel" in name and "EpiConvDgrad" in name):
+        return "conv_dgrad"
+    if "gemm_kernel" in name and "EpiConvFwd" in name:
+        return "conv_fwd"
+    return None
+
+
+def per_kernel(path, counter):
+    rows = [r for r in csv.DictReader(open(os.path.join(path, "run_counter_collection.csv")))
+            if r["Counter_Name"] == counter]
+    return {int(r["Dispatch_Id"]): (r["Kernel_Name"], float(r["Counter_Value"]) * 1024.0) for r in rows}
+
+
+def main():
+    fetch, write = per_kernel(sys.argv[1], "FETCH_SIZE"), per_kernel(sys.argv[2], "WRITE_SIZE")
+    fam = collections.defaultdict(lambda: {"launches": 0, "fetch": 0.0, "write": 0.0})
+    # the two passes ran the same program: pair dispatches by kernel name in order
+    wq = collections.defaultdict(list)
+    for d in sorted(write):
+        wq[write[d][0]].append(write[d][1])
+    used = collections.Counter()
+    for d in sorted(fetch):
+        name, fb = fetch[d]
+        f = family(name)
+        k = used[name]
+        used[name] += 1
+        if f is None or k >= len(wq[name]):
+            continue
+        a = fam[f]
+        a["launches"] += 1
+        a["fetch"] += 2.0 * fb
+        a["write"] += wq[name][k]
+    out = {"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace only); "
+                     "FETCH_SIZE doubled (gfx950 16-B/lane reads), KiB -> bytes",
+           "families": {}}
+    for f, a in sorted(fam.items()):
+        n = a["launches"]
+        out["families"][f] = {"launches": n, "hbm_bytes_per_launch": (a["fetch"] + a["write"]) / n,
+                              "read_bytes_per_launch": a["fetch"] / n, "write_bytes_per_launch": a["write"] / n}
+    json.dump(out, sys.stdout, indent=1)
+
+
+if __name__ == "__main__":
+    main()
