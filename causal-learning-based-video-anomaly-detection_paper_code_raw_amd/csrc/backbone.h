@@ -45,6 +45,7 @@ int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats /*nu
 int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
 // direct LDS-patch kernels (conv_patch.hip) for stride-1 layers; conv3_fwd / conv3_dgrad route there by default
 bool conv3_patch_supported(const Conv3Layer& L, bool fwd);
+extern int g_patch_persist;  // single-chunk (C == 32) stride-1 layers on the persistent patch kernel
 int64_t conv3_patch_blocks(int NF, int OH, int OW);  // BN partial blocks of a patch forward
 int conv3_patch_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
                     float* y, float* partials, int* nparts, hipStream_t st);

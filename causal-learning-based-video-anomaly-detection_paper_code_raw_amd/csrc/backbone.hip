@@ -692,6 +692,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_blocks") g_tune.wgrad_blocks = value;
   else if (k == "conv_wgrad_min_ktiles") g_tune.wgrad_min_ktiles = value;
   else if (k == "conv_patch") g_tune.patch = value;
+  else if (k == "conv_patch_persist") g_patch_persist = value;
   else if (k == "conv_wgrad_patch") g_tune.wgrad_patch = value;
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else {

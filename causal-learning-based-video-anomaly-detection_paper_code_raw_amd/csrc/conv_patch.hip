@@ -299,6 +299,161 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2_kernel(const PatchArg
   }
 }
 
+// Single-chunk stride-1 layers (C == 32: layer1.0 / layer1.1 forward, layer1.1 input gradient).  The weight slice
+// is the same for every pixel tile, so a persistent block stages it once, then walks a contiguous range of tiles
+// (neighbours share halo rows in the same L2): the next tile's patch is loaded into registers while the current
+// one is multiplied, and the BN partial sums accumulate across the block's tiles (one partial row per block).
+template <int NI, int TH, int TW, bool FWD>
+__global__ __launch_bounds__(256, 2) void conv3x3_patch_persist_kernel(const PatchArgs p, int tpb, int ntiles) {
+  constexpr int PC = 32, PROW = PC + 4, WROW = 9 * PC + 4, CQ = PC / 4;
+  constexpr int PH = TH + 2, PW = TW + 2, PROWS = NI * PH * PW;
+  __shared__ __attribute__((aligned(16))) float sm[PROWS * PROW + 32 * WROW];
+  float* patch = sm;
+  float* wl = sm + PROWS * PROW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_per_img = p.tiles_h * p.tiles_w;
+  const int n0 = blockIdx.y * 32;
+  const int t0 = blockIdx.x * tpb, t1 = min(ntiles, t0 + tpb);
+  const int m = wave * 32 + (lane & 31);
+  const int mi = m / (TH * TW), mr = m % (TH * TW);
+  const int py = mr / TW, px = mr % TW;
+  const int h = lane >> 5, j = lane & 31;
+  const float* abase = patch + ((mi * PH + py) * PW + px) * PROW + 4 * h;
+  const float* bbase = wl + j * WROW + 4 * h;
+  const int c4 = (tid % CQ) * 4;
+  constexpr int PQ = PROWS * CQ, PIT = (PQ + 255) / 256;
+
+  {  // the weight slice, once
+    WeightStage<PC, !FWD> ws;
+    ws.fetch(p, n0, 0, tid);
+    ws.stash(wl, tid);
+  }
+  f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+  const bool bn = FWD && p.scale;
+  if (bn) {
+    sc = *reinterpret_cast<const f32x4*>(p.scale + c4);
+    sh = *reinterpret_cast<const f32x4*>(p.shift + c4);
+  }
+  f32x4 pv[PIT];
+  auto origin = [&](int tile, int& img0, int& oy0, int& ox0) {
+    img0 = (tile / tiles_per_img) * NI;
+    const int tr = tile % tiles_per_img;
+    oy0 = (tr / p.tiles_w) * TH;
+    ox0 = (tr % p.tiles_w) * TW;
+  };
+  auto fetch = [&](int tile) {
+    int img0, oy0, ox0;
+    origin(tile, img0, oy0, ox0);
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = tid + it * 256;
+      const int row = q / CQ;
+      const int im = row / (PH * PW), rr = row % (PH * PW);
+      const int iy = oy0 - 1 + rr / PW, ix = ox0 - 1 + rr % PW, img = img0 + im;
+      pv[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (q < PQ && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
+        pv[it] = *reinterpret_cast<const f32x4*>(p.src + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C + c4);
+    }
+  };
+  auto stash = [&](int tile) {
+    int img0, oy0, ox0;
+    origin(tile, img0, oy0, ox0);
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = tid + it * 256;
+      if (q < PQ) {
+        const int row = q / CQ;
+        f32x4 v = pv[it];
+        if (bn) {
+          const int im = row / (PH * PW), rr = row % (PH * PW);
+          const int iy = oy0 - 1 + rr / PW, ix = ox0 - 1 + rr % PW;
+          if (img0 + im < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = relu_nan(fmaf(v[e], sc[e], sh[e]));
+          }
+        }
+        *reinterpret_cast<f32x4*>(patch + row * PROW + c4) = v;
+      }
+    }
+  };
+
+  const int col = n0 + j;
+  const float bj = (FWD && col < p.N) ? p.bias[col] : 0.f;
+  float s1 = 0.f, s2 = 0.f;
+  if (t0 < t1) fetch(t0);
+  for (int tile = t0; tile < t1; ++tile) {
+    __syncthreads();  // weights staged / the previous tile's reads of the patch are done
+    stash(tile);
+    __syncthreads();
+    if (tile + 1 < t1) fetch(tile + 1);
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float* ap = abase + ((t / 3) * PW + (t % 3)) * PROW;
+      const float* bp = bbase + t * PC;
+#pragma unroll
+      for (int kk = 0; kk < PC / 8; ++kk) {
+        const f32x4 a4 = *reinterpret_cast<const f32x4*>(ap + kk * 8);
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(bp + kk * 8);
+        acc = mfma32(a4[0], b4[0], acc);
+        acc = mfma32(a4[1], b4[1], acc);
+        acc = mfma32(a4[2], b4[2], acc);
+        acc = mfma32(a4[3], b4[3], acc);
+      }
+    }
+    int img0, oy0, ox0;
+    origin(tile, img0, oy0, ox0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int pm = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int qi = pm / (TH * TW), qr = pm % (TH * TW);
+      const int oy = oy0 + qr / TW, ox = ox0 + qr % TW, img = img0 + qi;
+      if (img < p.NF && oy < p.OH && ox < p.OW && col < p.N) {
+        const float v = acc[r] + bj;
+        p.out[(((int64_t)img * p.OH + oy) * p.OW + ox) * p.N + col] = v;
+        if (FWD) {
+          s1 += v;
+          s2 = fmaf(v, v, s2);
+        }
+      }
+    }
+  }
+  if (FWD) {
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    __syncthreads();
+    float* red = sm;
+    if (lane < 32) {
+      red[wave * 64 + lane] = s1;
+      red[wave * 64 + 32 + lane] = s2;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const int c = tid & 31, which = tid >> 5;
+      const float v = red[which * 32 + c] + red[64 + which * 32 + c] + red[128 + which * 32 + c] +
+                      red[192 + which * 32 + c];
+      if (n0 + c < p.N) p.partials[(int64_t)blockIdx.x * 2 * p.N + which * p.N + n0 + c] = v;
+    }
+  }
+}
+
+template <int NI, int TH, int TW, bool FWD>
+static int launch_patch_persist(PatchArgs a, hipStream_t st, int* nparts) {
+  a.tiles_h = (int)cdiv(a.OH, TH);
+  a.tiles_w = (int)cdiv(a.OW, TW);
+  const int ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);
+  const int ny = (int)cdiv(a.N, 32);
+  const int target = std::max(1, 512 / ny);  // 2 resident blocks per CU over 256 CUs
+  const int tpb = (int)cdiv(ntiles, target);
+  const int gx = (int)cdiv(ntiles, tpb);
+  hipLaunchKernelGGL((conv3x3_patch_persist_kernel<NI, TH, TW, FWD>), dim3(gx, ny), dim3(256), 0, st, a, tpb, ntiles);
+  VAD_LAUNCH_CHECK();
+  if (nparts) *nparts = gx;
+  return 0;
+}
+
 template <int S, int NI, int TH, int TW, int PC, bool FWD>
 static int launch_patch(PatchArgs a, hipStream_t st, int* nparts) {
   a.tiles_h = (int)cdiv(a.OH, TH);
@@ -311,6 +466,8 @@ static int launch_patch(PatchArgs a, hipStream_t st, int* nparts) {
   return 0;
 }
 
+int g_patch_persist = 1;  // tuning knob "conv_patch_persist"
+
 // tile geometry per output size (128 pixels per block): 0 -> 2 images x 8x8, 1 -> 8x16, 2 -> 4x32
 static int patch_geom(int OH, int OW) { return (OH <= 8 && OW <= 8) ? 0 : (OW <= 16 ? 1 : 2); }
 
@@ -318,6 +475,13 @@ static int patch_geom(int OH, int OW) { return (OH <= 8 && OW <= 8) ? 0 : (OW <=
 template <int S, bool FWD>
 static int dispatch_patch(const PatchArgs& a, hipStream_t st, int* nparts) {
   constexpr int PC = S == 1 ? 32 : 16;
+  if (S == 1 && a.C == 32 && g_patch_persist) {
+    switch (patch_geom(a.OH, a.OW)) {
+      case 0: return launch_patch_persist<2, 8, 8, FWD>(a, st, nparts);
+      case 1: return launch_patch_persist<1, 8, 16, FWD>(a, st, nparts);
+      default: return launch_patch_persist<1, 4, 32, FWD>(a, st, nparts);
+    }
+  }
   switch (patch_geom(a.OH, a.OW)) {
     case 0: return launch_patch<S, 2, 8, 8, PC, FWD>(a, st, nparts);
     case 1: return launch_patch<S, 1, 8, 16, PC, FWD>(a, st, nparts);

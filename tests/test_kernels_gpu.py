@@ -46,11 +46,14 @@ CONV_CASES = [(2, 32, 32, 19, 17, 1), (2, 32, 64, 29, 29, 2), (1, 64, 128, 15, 1
               (2, 32, 64, 57, 57, 2), (3, 128, 256, 16, 16, 2), (1, 64, 128, 31, 18, 2)]
 
 
-@pytest.mark.parametrize("patch", [1, 0])
+@pytest.mark.parametrize("patch", [1, 0, 2])
 @pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", CONV_CASES)
 def test_conv3x3_forward_and_dgrad(NF, Ci, Co, IH, IW, s, patch):
+    """patch 1: LDS-patch kernels (persistent variant for 32-channel stride-1 layers), 2: patch kernels without the
+    persistent variant, 0: implicit-GEMM path."""
     nat = _lib()
-    nat.lib().vad_set_tuning(b"conv_patch", patch)
+    nat.lib().vad_set_tuning(b"conv_patch", 1 if patch else 0)
+    nat.lib().vad_set_tuning(b"conv_patch_persist", 0 if patch == 2 else 1)
     g = torch.Generator().manual_seed(NF * 7 + Ci + Co + IH)
     x = torch.randn(NF, Ci, IH, IW, generator=g)
     w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
@@ -80,6 +83,7 @@ def test_conv3x3_forward_and_dgrad(NF, Ci, Co, IH, IW, s, patch):
                                           wf.data_ptr(), wd.data_ptr(), st))
     torch.cuda.synchronize()
     nat.lib().vad_set_tuning(b"conv_patch", 1)
+    nat.lib().vad_set_tuning(b"conv_patch_persist", 1)
     np.testing.assert_allclose(dx.cpu().permute(0, 3, 1, 2).numpy(), xr.grad.numpy(), rtol=1e-4, atol=1e-4)
 
 
