@@ -555,12 +555,13 @@ struct WgradPatchArgs {
   int tiles_h, tiles_w, ntiles;
 };
 
-template <int S, int NI, int TH, int TW>
-__global__ __launch_bounds__(256, S == 1 ? 2 : 1) void conv3x3_wgrad_patch_kernel(const WgradPatchArgs p) {
-  static_assert(NI * TH * TW == 128, "a tile holds 128 output pixels");
+template <int S, int NI, int TH, int TW, int WPX>
+__global__ __launch_bounds__(256, 2) void conv3x3_wgrad_patch_kernel(const WgradPatchArgs p) {
+  static_assert(NI * TH * TW == 4 * WPX, "a tile holds 4 waves x WPX output pixels");
+  constexpr int TPX = 4 * WPX;  // pixels per tile
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3, PROWS = NI * PH * PW;
   constexpr int PWE = (PW + 1) / 2;  // stride 2: even columns first
-  constexpr int XF = PROWS * 32, YF = 128 * 32, RF = 2 * 9 * 16 * 64;
+  constexpr int XF = PROWS * 32, YF = TPX * 32, RF = 2 * 9 * 16 * 64;
   constexpr int LF = (XF + YF) > RF ? (XF + YF) : RF;
   __shared__ __attribute__((aligned(16))) float sm[LF];
   float* xs = sm;
@@ -577,8 +578,8 @@ __global__ __launch_bounds__(256, S == 1 ? 2 : 1) void conv3x3_wgrad_patch_kerne
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
-  constexpr int PIT = (PROWS * 8 + 255) / 256;
-  f32x4 pv[PIT], yv[4];
+  constexpr int PIT = (PROWS * 8 + 255) / 256, YIT = TPX * 8 / 256;
+  f32x4 pv[PIT], yv[YIT];
   int img0 = 0, oy0 = 0, ox0 = 0;
   auto tile_origin = [&](int tile, int& i0, int& y0, int& x0) {
     i0 = (tile / tiles_per_img) * NI;
@@ -590,7 +591,7 @@ __global__ __launch_bounds__(256, S == 1 ? 2 : 1) void conv3x3_wgrad_patch_kerne
     int i0, y0, x0;
     tile_origin(tile, i0, y0, x0);
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
+    for (int it = 0; it < YIT; ++it) {
       const int m = (tid >> 3) + it * 32;
       const int mi = m / (TH * TW), mr = m % (TH * TW);
       const int oy = y0 + mr / TW, ox = x0 + mr % TW, img = i0 + mi;
@@ -615,7 +616,7 @@ __global__ __launch_bounds__(256, S == 1 ? 2 : 1) void conv3x3_wgrad_patch_kerne
   }
   auto stash = [&]() {
 #pragma unroll
-    for (int it = 0; it < 4; ++it) *reinterpret_cast<f32x4*>(ys + ((tid >> 3) + it * 32) * 32 + c4) = yv[it];
+    for (int it = 0; it < YIT; ++it) *reinterpret_cast<f32x4*>(ys + ((tid >> 3) + it * 32) * 32 + c4) = yv[it];
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
       const int row = (tid >> 3) + it * 32;
@@ -643,8 +644,8 @@ __global__ __launch_bounds__(256, S == 1 ? 2 : 1) void conv3x3_wgrad_patch_kerne
     __syncthreads();
     if (tile + (int)gridDim.z < p.ntiles) fetch(tile + gridDim.z);
 #pragma unroll 4
-    for (int s2 = 0; s2 < 16; ++s2) {
-      const int m = wave * 32 + 2 * s2 + h;
+    for (int s2 = 0; s2 < WPX / 2; ++s2) {
+      const int m = wave * WPX + 2 * s2 + h;
       const int mi = m / (TH * TW), mr = m % (TH * TW);
       const int py = mr / TW, px = mr % TW;
       const float a = ys[m * 32 + j];
@@ -695,7 +696,7 @@ __global__ __launch_bounds__(256, S == 1 ? 2 : 1) void conv3x3_wgrad_patch_kerne
   }
 }
 
-template <int S, int NI, int TH, int TW>
+template <int S, int NI, int TH, int TW, int WPX = 32>
 static int launch_wgrad_patch(WgradPatchArgs a, int target_blocks, int64_t partial_cap, hipStream_t st,
                               int* nsplit) {
   a.tiles_h = (int)cdiv(a.OH, TH);
@@ -705,7 +706,7 @@ static int launch_wgrad_patch(WgradPatchArgs a, int target_blocks, int64_t parti
   int64_t z = std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, pairs), a.ntiles));
   z = std::min<int64_t>(z, std::max<int64_t>(1, partial_cap / ((int64_t)a.Co * 9 * a.Ci)));
   dim3 grid((unsigned)(a.Co / 32), (unsigned)(a.Ci / 32), (unsigned)z);
-  hipLaunchKernelGGL((conv3x3_wgrad_patch_kernel<S, NI, TH, TW>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv3x3_wgrad_patch_kernel<S, NI, TH, TW, WPX>), grid, dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   *nsplit = (int)z;
   return 0;
@@ -732,9 +733,10 @@ int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, co
     if (g == 1) return launch_wgrad_patch<1, 1, 8, 16>(a, target_blocks, partial_cap, st, nsplit);
     return launch_wgrad_patch<1, 1, 4, 32>(a, target_blocks, partial_cap, st, nsplit);
   }
-  if (g == 0) return launch_wgrad_patch<2, 2, 8, 8>(a, target_blocks, partial_cap, st, nsplit);
-  if (g == 1) return launch_wgrad_patch<2, 1, 8, 16>(a, target_blocks, partial_cap, st, nsplit);
-  return launch_wgrad_patch<2, 1, 4, 32>(a, target_blocks, partial_cap, st, nsplit);
+  // stride 2: 64-pixel tiles (16 per wave) keep the ~4x larger input patch at 2 waves per SIMD
+  if (g == 0) return launch_wgrad_patch<2, 1, 8, 8, 16>(a, target_blocks, partial_cap, st, nsplit);
+  if (g == 1) return launch_wgrad_patch<2, 1, 4, 16, 16>(a, target_blocks, partial_cap, st, nsplit);
+  return launch_wgrad_patch<2, 1, 2, 32, 16>(a, target_blocks, partial_cap, st, nsplit);
 }
 
 }  // namespace vad

@@ -253,50 +253,59 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
   __syncthreads();
   const int N = s_N;
   const float* bhh = PW(H_GRU_BHH);
-  // GRU recurrence, gate order (r, z, n) (cad:284,298)
-  for (int t = 0; t < T; ++t) {
-    for (int idx = tid; idx < N * G3; idx += HT) {
-      const int nn = idx / G3, q = idx - nn * G3;
-      const f32x4* wr = reinterpret_cast<const f32x4*>(whh + q * WHH_LD);
-      const float* hv = hs + nn * GH;
-      float s = bhh[q];
+  // GRU recurrence, gate order (r, z, n) (cad:284,298): one wave per trajectory slot, lane u owns hidden unit u
+  // and computes exactly its three gate pre-activations (W_hh rows u, GH+u, 2GH+u from LDS), so a time step
+  // needs no block barrier -- only the wave's own LDS copy of h is exchanged between steps.
+  static_assert(NMAX * 64 <= HT && GH == 64, "one wave per trajectory, one lane per hidden unit");
+  {
+    const int nn = tid >> 6, u = tid & 63;
+    if (nn < NMAX) {
+      float h = 0.f;
+      const bool live = nn < N;
+      const float br = bhh[u], bz = bhh[GH + u], bn = bhh[2 * GH + u];
+      const f32x4* wr = reinterpret_cast<const f32x4*>(whh + u * WHH_LD);
+      const f32x4* wz = reinterpret_cast<const f32x4*>(whh + (GH + u) * WHH_LD);
+      const f32x4* wn = reinterpret_cast<const f32x4*>(whh + (2 * GH + u) * WHH_LD);
+      const f32x4* hv = reinterpret_cast<const f32x4*>(hs + nn * GH);
+      for (int t = 0; t < T; ++t) {
+        const int64_t row = ((int64_t)b * T + t) * NMAX + nn;
+        if (live) {
+          const float* gi = rows + RL.gi + row * G3;
+          const float gi_r = gi[u], gi_z = gi[GH + u], gi_n = gi[2 * GH + u];
+          float ar = br, az = bz, an = bn;
 #pragma unroll
-      for (int k = 0; k < GH / 4; ++k) {
-        const f32x4 wv = wr[k];
-        s = fmaf(wv[0], hv[4 * k], s);
-        s = fmaf(wv[1], hv[4 * k + 1], s);
-        s = fmaf(wv[2], hv[4 * k + 2], s);
-        s = fmaf(wv[3], hv[4 * k + 3], s);
-      }
-      ghs[idx] = s;
-    }
-    __syncthreads();
-    for (int idx = tid; idx < NMAX * GH; idx += HT) {
-      const int nn = idx / GH, u = idx - nn * GH;
-      const int64_t row = ((int64_t)b * T + t) * NMAX + nn;
-      if (nn < N) {
-        const float* gi = rows + RL.gi + row * G3;
-        const float* gh = ghs + nn * G3;
-        const float r = sigmoidf_(gi[u] + gh[u]);
-        const float z = sigmoidf_(gi[GH + u] + gh[GH + u]);
-        const float nv = tanhf(gi[2 * GH + u] + r * gh[2 * GH + u]);
-        const float hprev = hs[idx];
-        rows[RL.r + row * GH + u] = r;
-        rows[RL.z + row * GH + u] = z;
-        rows[RL.n + row * GH + u] = nv;
-        rows[RL.ghn + row * GH + u] = gh[2 * GH + u];
-        rows[RL.hp + row * GH + u] = hprev;
-        hs[idx] = (1.f - z) * nv + z * hprev;
-      } else {  // trajectory slots that do not exist in this clip
-        rows[RL.r + row * GH + u] = 0.f;
-        rows[RL.z + row * GH + u] = 0.f;
-        rows[RL.n + row * GH + u] = 0.f;
-        rows[RL.ghn + row * GH + u] = 0.f;
-        rows[RL.hp + row * GH + u] = 0.f;
+          for (int k = 0; k < GH / 4; ++k) {
+            const f32x4 x = hv[k], a0 = wr[k], a1 = wz[k], a2 = wn[k];
+            ar = fmaf(a0[0], x[0], ar); ar = fmaf(a0[1], x[1], ar); ar = fmaf(a0[2], x[2], ar); ar = fmaf(a0[3], x[3], ar);
+            az = fmaf(a1[0], x[0], az); az = fmaf(a1[1], x[1], az); az = fmaf(a1[2], x[2], az); az = fmaf(a1[3], x[3], az);
+            an = fmaf(a2[0], x[0], an); an = fmaf(a2[1], x[1], an); an = fmaf(a2[2], x[2], an); an = fmaf(a2[3], x[3], an);
+          }
+          const float r = sigmoidf_(gi_r + ar);
+          const float z = sigmoidf_(gi_z + az);
+          const float nv = tanhf(gi_n + r * an);
+          rows[RL.r + row * GH + u] = r;
+          rows[RL.z + row * GH + u] = z;
+          rows[RL.n + row * GH + u] = nv;
+          rows[RL.ghn + row * GH + u] = an;
+          rows[RL.hp + row * GH + u] = h;
+          h = (1.f - z) * nv + z * h;
+          // every lane's reads of the old h are done (lockstep wave) before the new h is published
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          hs[nn * GH + u] = h;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+        } else {  // trajectory slots that do not exist in this clip
+          rows[RL.r + row * GH + u] = 0.f;
+          rows[RL.z + row * GH + u] = 0.f;
+          rows[RL.n + row * GH + u] = 0.f;
+          rows[RL.ghn + row * GH + u] = 0.f;
+          rows[RL.hp + row * GH + u] = 0.f;
+        }
       }
     }
-    __syncthreads();
   }
+  __syncthreads();
   for (int i = tid; i < NMAX * GH; i += HT) w[L.hT + i] = hs[i];
   __syncthreads();
   // encoder + VAE (cad:299, 333-352)
@@ -604,41 +613,44 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
   // ---- GRU backward through time (dh'/dz = h - n, dh'/dn = 1 - z)
   {
     float* dh = w + L.dh;
-    float* dhn = w + L.dhn;
-    for (int t = T - 1; t >= 0; --t) {
-      for (int idx = tid; idx < NMAX * GH; idx += HT) {
-        const int nn = idx / GH, u = idx - nn * GH;
+    // one wave per trajectory slot, lane u owns hidden unit u: the 3 gate grads of unit u are computed in-lane,
+    // published to the wave's LDS row, and dh_prev[u] = dh[u] z[u] + sum_q W_hh[q][u] dgh[q] reads them back --
+    // no block barrier inside the time loop
+    static_assert(NMAX * 64 <= HT && GH == 64, "one wave per trajectory, one lane per hidden unit");
+    __syncthreads();
+    const int nn = tid >> 6, u = tid & 63;
+    if (nn < NMAX) {
+      const bool live = nn < N;
+      float d = live ? dh[nn * GH + u] : 0.f;
+      float* dgv = dgh_s + nn * G3;
+      for (int t = T - 1; t >= 0; --t) {
         const int64_t row = ((int64_t)b * T + t) * NMAX + nn;
         float* dgi = rows + RL.dgi + row * G3;
         float* dgh = rows + RL.dgh + row * G3;
-        if (nn < N) {
+        if (live) {
           const float r = rows[RL.r + row * GH + u], z = rows[RL.z + row * GH + u];
           const float nv = rows[RL.n + row * GH + u];
           const float hp = rows[RL.hp + row * GH + u], ghn = rows[RL.ghn + row * GH + u];
-          const float d = dh[idx];
           const float dan = d * (1.f - z) * (1.f - nv * nv);
           const float daz = d * (hp - nv) * z * (1.f - z);
           const float dar = dan * ghn * r * (1.f - r);
           dgi[u] = dar; dgi[GH + u] = daz; dgi[2 * GH + u] = dan;
           dgh[u] = dar; dgh[GH + u] = daz; dgh[2 * GH + u] = dan * r;
-          dgh_s[nn * G3 + u] = dar;
-          dgh_s[nn * G3 + GH + u] = daz;
-          dgh_s[nn * G3 + 2 * GH + u] = dan * r;
-          dhn[idx] = d * z;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          dgv[u] = dar;
+          dgv[GH + u] = daz;
+          dgv[2 * GH + u] = dan * r;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          float s = d * z;
+          for (int q = 0; q < G3; ++q) s = fmaf(whh[q * GH + u], dgv[q], s);
+          d = s;
         } else {
           dgi[u] = 0.f; dgi[GH + u] = 0.f; dgi[2 * GH + u] = 0.f;
           dgh[u] = 0.f; dgh[GH + u] = 0.f; dgh[2 * GH + u] = 0.f;
         }
       }
-      __syncthreads();
-      for (int idx = tid; idx < N * GH; idx += HT) {
-        const int nn = idx / GH, j = idx - nn * GH;
-        const float* dgv = dgh_s + nn * G3;
-        float s = dhn[idx];
-        for (int q = 0; q < G3; ++q) s = fmaf(whh[q * GH + j], dgv[q], s);
-        dh[idx] = s;
-      }
-      __syncthreads();
     }
   }
 }

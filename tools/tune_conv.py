@@ -68,8 +68,8 @@ def main():
                                         y.data_ptr(), wf.data_ptr(), wd.data_ptr(), parts.data_ptr(), st))
         if a.patch:
             for op in ("fwd", "dgrad", "wgrad"):
-                for on in (0, 1):
-                    L.vad_set_tuning(b"conv_patch", on)
+                for on in ((0, 1, 2) if op == "wgrad" else (0, 1)):
+                    L.vad_set_tuning(b"conv_patch", min(on, 1))
                     L.vad_set_tuning(b"conv_wgrad_patch", on)
                     if op == "wgrad":
                         fn = lambda: nat.check(L.vad_conv3x3_wgrad(
