@@ -50,6 +50,14 @@ int64_t conv3_patch_blocks(int NF, int OH, int OW);  // BN partial blocks of a p
 int conv3_patch_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
                     float* y, float* partials, int* nparts, hipStream_t st);
 int conv3_patch_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
+// split-bf16 patch kernels (conv_x3.hip): fp32 operands as three bf16 planes, six bf16 MFMA products per K step
+extern int g_conv_split;  // 0 disables them (f32 MFMA patch kernels)
+extern int g_x3_nt;       // output channels per block: 0 auto, 1 -> 32, 2 -> 64
+extern int g_x3_dbg;      // measurement-only bits (X3Args::dbg)
+bool conv3_x3_supported(const Conv3Layer& L, bool fwd);
+int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
+                 float* y, float* partials, int* nparts, hipStream_t st);
+int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
 bool conv3_wgrad_patch_supported(const Conv3Layer& L);
 int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
                       int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);

@@ -693,6 +693,9 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_min_ktiles") g_tune.wgrad_min_ktiles = value;
   else if (k == "conv_patch") g_tune.patch = value;
   else if (k == "conv_patch_persist") g_patch_persist = value;
+  else if (k == "conv_split") g_conv_split = value;
+  else if (k == "conv_split_nt") g_x3_nt = value;
+  else if (k == "conv_split_dbg") g_x3_dbg = value;
   else if (k == "conv_wgrad_patch") g_tune.wgrad_patch = value;
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else {
@@ -795,9 +798,10 @@ int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, con
               float* y, float* partials, int* nparts, hipStream_t st) {
   VAD_CHECK(L.Ci % 32 == 0, "conv3_fwd: Ci must be a multiple of 32");
   // (the patch grid may exceed ceil(M/64) BN partial blocks on tiny images: those stay on the GEMM path)
-  if (g_tune.patch && conv3_patch_supported(L, true) &&
-      conv3_patch_blocks(L.NF, L.OH, L.OW) <= cdiv((int64_t)L.NF * L.OH * L.OW, 64))
-    return conv3_patch_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st);
+  if (g_tune.patch && conv3_patch_blocks(L.NF, L.OH, L.OW) <= cdiv((int64_t)L.NF * L.OH * L.OW, 64)) {
+    if (conv3_x3_supported(L, true)) return conv3_x3_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st);
+    if (conv3_patch_supported(L, true)) return conv3_patch_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st);
+  }
   ConvGeom g{L.NF, L.OH, L.OW, L.stride, L.stride, L.IH, L.IW, L.Ci};
   TapTable taps;
   fwd_taps(taps);
@@ -829,6 +833,7 @@ static int dgrad_launch(const ConvGeom& g, const TapTable& taps, const float* dY
 int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st) {
   VAD_CHECK(L.Co % 32 == 0, "conv3_dgrad: Co must be a multiple of 32");
   const int N = L.Ci;
+  if (g_tune.patch && conv3_x3_supported(L, false)) return conv3_x3_dgrad(L, dY, wd, dX, st);
   if (g_tune.patch && conv3_patch_supported(L, false)) return conv3_patch_dgrad(L, dY, wd, dX, st);
   if (L.stride == 1) {
     ConvGeom g{L.NF, L.IH, L.IW, 1, 1, L.OH, L.OW, L.Co};

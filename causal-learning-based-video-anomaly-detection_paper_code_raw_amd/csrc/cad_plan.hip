@@ -405,6 +405,9 @@ struct CadPlanImpl {
     a.pbase = params;
     for (int i = 0; i < H_NUM; ++i) a.off[i] = LY.slots[LY.head0 + i].offset;
     a.head_begin = LY.slots[LY.head0].offset;
+    int64_t numel[H_NUM];
+    for (int i = 0; i < H_NUM; ++i) numel[i] = LY.slots[LY.head0 + i].numel;
+    head_pack_weights(a, numel);  // sizes are fixed by the architecture; checked once in create()
     a.ws = head_ws;
     a.ws_stride = head_ws_floats(T);
     a.iws = head_iws;
@@ -724,6 +727,12 @@ int vad_cad_num_bn(void) { return 9; }
 int vad_cad_create(int B, int T, int H, int W, vad_cad_plan** out) {
   VAD_CHECK(out != nullptr, "vad_cad_create: out is null");
   VAD_CHECK(B >= 1 && T >= 1 && T <= 256 && H >= 16 && W >= 16, "vad_cad_create: unsupported shape");
+  {
+    HeadArgs probe{};
+    int64_t numel[H_NUM];
+    for (int i = 0; i < H_NUM; ++i) numel[i] = layout().slots[layout().head0 + i].numel;
+    VAD_CHECK(head_pack_weights(probe, numel) == 0, "vad_cad_create: head weight image exceeds its LDS capacity");
+  }
   auto* p = new vad_cad_plan();
   CadPlanImpl& c = p->impl;
   c.B = B; c.T = T; c.H = H; c.W = W; c.NF = B * T;

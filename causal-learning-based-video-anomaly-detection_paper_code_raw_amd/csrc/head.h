@@ -32,6 +32,7 @@ struct HeadArgs {
   const float* pbase;     // flat parameter buffer
   int64_t off[H_NUM];     // slot offsets into pbase / grad slabs (relative to head_begin for slabs)
   int64_t head_begin;
+  int lw_len;             // floats of the parameter range [off[H_ENC_W], end of the last slot) staged in LDS
   float* ws;              // per-clip workspace (small per-clip tensors)
   int64_t ws_stride;
   int* iws;               // per-clip int workspace
@@ -39,6 +40,10 @@ struct HeadArgs {
   float* rows;            // per-trajectory-row arrays, R = B*T*NMAX rows (see RowLayout in head.hip)
   float* grad;            // flat grad buffer (GRU / ReID weight grads are written here directly)
 };
+
+constexpr int HW_LDS = 20480;  // capacity (floats) of the sequence kernels' LDS weight image
+// sets lw_len from a.off and the last slot's size; nonzero if the image does not fit or a slot is not 16-B aligned
+int head_pack_weights(HeadArgs& a, const int64_t* numel);
 
 int64_t head_ws_floats(int T);
 int64_t head_iws_ints(int T);

@@ -37,9 +37,10 @@ int64_t head_rows_floats(int B, int T) { return RowLayout((int64_t)B * T * NMAX)
 
 // ------------------------------------------------------------------ per-clip small workspace
 struct HL {
-  int64_t hT, enc, ce1, ce2, mu, lv, zz, node, e, A, s, d1, d2, pred, cur, prd, cin, cs1, cs2, cs, ms1, ms2, ms, ts1,
-      ts2, ts, dh, dhn, scratch, dz, dnode, dA, dpred, ds, total;
-  __host__ __device__ HL() {
+  int64_t hT = 0, enc = 0, ce1 = 0, ce2 = 0, mu = 0, lv = 0, zz = 0, node = 0, e = 0, A = 0, s = 0, d1 = 0, d2 = 0,
+          pred = 0, cur = 0, prd = 0, cin = 0, cs1 = 0, cs2 = 0, cs = 0, ms1 = 0, ms2 = 0, ms = 0, ts1 = 0, ts2 = 0,
+          ts = 0, dh = 0, dhn = 0, scratch = 0, dz = 0, dnode = 0, dA = 0, dpred = 0, ds = 0, total = 0;
+  __host__ __device__ constexpr HL() {
     int64_t o = 0;
     auto take = [&](int64_t n_) { int64_t r_ = o; o += (n_ + 3) & ~3ll; return r_; };
     hT = take(NMAX * GH); enc = take(NMAX * 32); ce1 = take(NMAX * 32); ce2 = take(NMAX * 32);
@@ -52,6 +53,23 @@ struct HL {
     total = o;
   }
 };
+
+// the per-clip workspace lives in LDS inside the two sequence kernels; [0, dh) is handed from forward to backward
+// through global memory
+constexpr int HL_TOTAL = (int)HL().total;
+constexpr int HL_HANDOFF = (int)HL().dh;
+static_assert(HL_TOTAL % 4 == 0 && HL_HANDOFF % 4 == 0, "float4 copies");
+// LDS image of the head's small-MLP weights (slots H_ENC_W .. H_NUM-1, packed at HeadArgs::lw_off); it shares its
+// LDS with W_hh, which the recurrences need before (forward) or after (backward) the MLP phases
+constexpr int HF_BIG = HW_LDS > G3 * WHH_LD ? HW_LDS : G3 * WHH_LD;
+
+int head_pack_weights(HeadArgs& a, const int64_t* numel) {
+  const int64_t len = a.off[H_NUM - 1] + numel[H_NUM - 1] - a.off[H_ENC_W];
+  a.lw_len = (int)((len + 3) & ~3ll);
+  for (int i = H_ENC_W; i < H_NUM; ++i)
+    if (a.off[i] % 4) return 1;
+  return a.lw_len <= HW_LDS ? 0 : 1;
+}
 
 int64_t head_ws_floats(int T) {
   (void)T;
@@ -67,26 +85,31 @@ __device__ void lin_fwd(const float* in, int ldi, int R, int I, const float* __r
     float s = b ? b[o] : 0.f;
     const float* w = W + (int64_t)o * I;
     const float* v = in + (int64_t)r * ldi;
-    for (int i = 0; i < I; ++i) s = fmaf(w[i], v[i], s);
+    // W lives in LDS: rotating the start column by o spreads the lanes of one row block over the banks
+    int i = o % I;
+    for (int k = 0; k < I; ++k) {
+      s = fmaf(w[i], v[i], s);
+      i = i + 1 == I ? 0 : i + 1;
+    }
     out[(int64_t)r * ldo + o] = relu ? fmaxf(s, 0.f) : s;
   }
   __syncthreads();
 }
 
-// dW[o][i] += sum_r dpre[r][o] in[r][i]; db[o] += sum_r dpre[r][o]; din[r][i] (=|+=) sum_o W[o][i] dpre[r][o]
+// dW[o][i] = sum_r dpre[r][o] in[r][i]; db[o] += sum_r dpre[r][o]; din[r][i] (=|+=) sum_o W[o][i] dpre[r][o]
 __device__ void lin_bwd(const float* dpre, int ldd, const float* in, int ldi, int R, int I,
                         const float* __restrict__ W, int O, float* dW, float* db, float* din, int lddin, bool acc) {
   for (int idx = threadIdx.x; idx < O * I; idx += blockDim.x) {
     const int o = idx / I, i = idx - o * I;
     float s = 0.f;
     for (int r = 0; r < R; ++r) s = fmaf(dpre[(int64_t)r * ldd + o], in[(int64_t)r * ldi + i], s);
-    dW[idx] += s;
+    dW[idx] = s;  // every head slot is produced by exactly one layer call
   }
   if (db) {
     for (int o = threadIdx.x; o < O; o += blockDim.x) {
       float s = 0.f;
       for (int r = 0; r < R; ++r) s += dpre[(int64_t)r * ldd + o];
-      db[o] += s;
+      db[o] = s;
     }
   }
   if (din) {
@@ -110,6 +133,33 @@ __device__ void relu_gate(float* d, int ldd, const float* out, int ldo, int R, i
 }
 
 #define PW(slot) (a.pbase + a.off[slot])
+#define PL(slot) (sW + (a.off[slot] - a.off[H_ENC_W]))  // LDS weight image
+
+// block-wide copy of n4 float4s (dst index remapped by map): every thread issues U loads before its LDS stores,
+// so a copy costs one memory latency per U*blockDim float4s instead of one per blockDim
+template <int U, typename Map>
+__device__ void block_copy4(float* dst, const float* src, int n4, Map map) {
+  for (int base = 0; base < n4; base += U * (int)blockDim.x) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * (int)blockDim.x + (int)threadIdx.x;
+      if (i < n4) v[u] = reinterpret_cast<const f32x4*>(src)[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * (int)blockDim.x + (int)threadIdx.x;
+      if (i < n4) reinterpret_cast<f32x4*>(dst)[map(i)] = v[u];
+    }
+  }
+}
+struct Ident {
+  __device__ int operator()(int i) const { return i; }
+};
+
+__device__ void stage_head_weights(const HeadArgs& a, float* sW) {
+  block_copy4<12>(sW, a.pbase + a.off[H_ENC_W], a.lw_len / 4, Ident{});
+}
 
 // ================================================================== forward
 __global__ __launch_bounds__(256) void head_rows_fwd_kernel(HeadArgs a, const float* __restrict__ logits, HeadOut o) {
@@ -229,17 +279,20 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
   const HL L;
   const RowLayout RL((int64_t)a.B * T * NMAX);
   float* rows = a.rows;
-  float* w = a.ws + (int64_t)b * a.ws_stride;
+  float* wg = a.ws + (int64_t)b * a.ws_stride;
   const int* iw = a.iws + (int64_t)b * a.iws_stride;
   const int* cnt = iw;
   const int* slot = iw + T;
-  __shared__ __attribute__((aligned(16))) float whh[G3 * WHH_LD];
+  __shared__ __attribute__((aligned(16))) float big[HF_BIG];  // W_hh during the recurrence, then the MLP weights
+  __shared__ __attribute__((aligned(16))) float sw[HL_TOTAL];
   __shared__ float hs[NMAX * GH];
-  __shared__ float ghs[NMAX * G3];
+  float* whh = big;
+  float* sW = big;
+  float* w = sw;
   __shared__ int s_N, s_any;
   __shared__ float s_red[4];
   const float* Whh = PW(H_GRU_WHH);
-  for (int i = tid; i < G3 * GH; i += HT) whh[(i / GH) * WHH_LD + (i % GH)] = Whh[i];
+  block_copy4<6>(whh, Whh, G3 * GH / 4, [](int i) { return (i >> 4) * (WHH_LD / 4) + (i & 15); });
   for (int i = tid; i < NMAX * GH; i += HT) hs[i] = 0.f;
   if (tid == 0) {
     int N = 1, any = 0;
@@ -267,11 +320,20 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
       const f32x4* wz = reinterpret_cast<const f32x4*>(whh + (GH + u) * WHH_LD);
       const f32x4* wn = reinterpret_cast<const f32x4*>(whh + (2 * GH + u) * WHH_LD);
       const f32x4* hv = reinterpret_cast<const f32x4*>(hs + nn * GH);
+      // the input projections of step t+1 are loaded while step t computes
+      float gi_r = 0.f, gi_z = 0.f, gi_n = 0.f;
+      if (live) {
+        const float* gi = rows + RL.gi + ((int64_t)b * T * NMAX + nn) * G3;
+        gi_r = gi[u]; gi_z = gi[GH + u]; gi_n = gi[2 * GH + u];
+      }
       for (int t = 0; t < T; ++t) {
         const int64_t row = ((int64_t)b * T + t) * NMAX + nn;
         if (live) {
-          const float* gi = rows + RL.gi + row * G3;
-          const float gi_r = gi[u], gi_z = gi[GH + u], gi_n = gi[2 * GH + u];
+          float nx_r = 0.f, nx_z = 0.f, nx_n = 0.f;
+          if (t + 1 < T) {
+            const float* gi = rows + RL.gi + (row + NMAX) * G3;
+            nx_r = gi[u]; nx_z = gi[GH + u]; nx_n = gi[2 * GH + u];
+          }
           float ar = br, az = bz, an = bn;
 #pragma unroll
           for (int k = 0; k < GH / 4; ++k) {
@@ -295,6 +357,7 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
           hs[nn * GH + u] = h;
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           __builtin_amdgcn_wave_barrier();
+          gi_r = nx_r; gi_z = nx_z; gi_n = nx_n;
         } else {  // trajectory slots that do not exist in this clip
           rows[RL.r + row * GH + u] = 0.f;
           rows[RL.z + row * GH + u] = 0.f;
@@ -305,15 +368,16 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
       }
     }
   }
-  __syncthreads();
+  __syncthreads();  // W_hh is dead: its LDS now takes the MLP weight image
+  stage_head_weights(a, sW);
   for (int i = tid; i < NMAX * GH; i += HT) w[L.hT + i] = hs[i];
   __syncthreads();
   // encoder + VAE (cad:299, 333-352)
-  lin_fwd(w + L.hT, GH, N, GH, PW(H_ENC_W), PW(H_ENC_B), 32, w + L.enc, 32, false);
-  lin_fwd(w + L.enc, 32, N, 32, PW(H_CE0_W), PW(H_CE0_B), 32, w + L.ce1, 32, true);
-  lin_fwd(w + L.ce1, 32, N, 32, PW(H_CE2_W), PW(H_CE2_B), 32, w + L.ce2, 32, true);
-  lin_fwd(w + L.ce2, 32, N, 32, PW(H_MU_W), PW(H_MU_B), NF_, w + L.mu, NF_, false);
-  lin_fwd(w + L.ce2, 32, N, 32, PW(H_LV_W), PW(H_LV_B), NF_, w + L.lv, NF_, false);
+  lin_fwd(w + L.hT, GH, N, GH, PL(H_ENC_W), PL(H_ENC_B), 32, w + L.enc, 32, false);
+  lin_fwd(w + L.enc, 32, N, 32, PL(H_CE0_W), PL(H_CE0_B), 32, w + L.ce1, 32, true);
+  lin_fwd(w + L.ce1, 32, N, 32, PL(H_CE2_W), PL(H_CE2_B), 32, w + L.ce2, 32, true);
+  lin_fwd(w + L.ce2, 32, N, 32, PL(H_MU_W), PL(H_MU_B), NF_, w + L.mu, NF_, false);
+  lin_fwd(w + L.ce2, 32, N, 32, PL(H_LV_W), PL(H_LV_B), NF_, w + L.lv, NF_, false);
   if (tid < N * NF_) {
     const int nn = tid / NF_, f = tid - nn * NF_;
     const float eps = rng_normal(a.h1_eps, (uint64_t)(a.clip0 + b), (uint64_t)(nn * NF_ + f));
@@ -334,19 +398,22 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
     if (tid == 0) s_red[0] = s / (float)N;
   }
   // structure learner (cad:371-398)
-  lin_fwd(w + L.zz, NF_, N, NF_, PW(H_NODE_W), PW(H_NODE_B), 32, w + L.node, 32, false);
+  lin_fwd(w + L.zz, NF_, N, NF_, PL(H_NODE_W), PL(H_NODE_B), 32, w + L.node, 32, false);
   const int m = min(N, NF_);
   {
-    const float* W0 = PW(H_EDGE0_W);
-    const float* b0 = PW(H_EDGE0_B);
+    const float* W0 = PL(H_EDGE0_W);
+    const float* b0 = PL(H_EDGE0_B);
     for (int idx = tid; idx < m * m * 32; idx += HT) {
       const int pr = idx / 32, u = idx - pr * 32;
       const int i = pr / m, j = pr - i * m;
       if (i == j) continue;
       float s = b0[u];
       const float* wr = W0 + u * 64;
-      for (int q = 0; q < 32; ++q) s = fmaf(wr[q], w[L.node + i * 32 + q], s);
-      for (int q = 0; q < 32; ++q) s = fmaf(wr[32 + q], w[L.node + j * 32 + q], s);
+      for (int k = 0; k < 32; ++k) {  // start column rotated by u: conflict-free LDS weight reads
+        const int q = (k + u) & 31;
+        s = fmaf(wr[q], w[L.node + i * 32 + q], s);
+        s = fmaf(wr[32 + q], w[L.node + j * 32 + q], s);
+      }
       w[L.e + (int64_t)(i * NMAX + j) * 32 + u] = fmaxf(s, 0.f);
     }
     __syncthreads();
@@ -354,8 +421,8 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
       const int i = tid / 6, j = tid - i * 6;
       float v = 0.f;
       if (i != j && i < m && j < m) {
-        const float* W2 = PW(H_EDGE2_W);
-        float s = PW(H_EDGE2_B)[0];
+        const float* W2 = PL(H_EDGE2_W);
+        float s = PL(H_EDGE2_B)[0];
         for (int q = 0; q < 32; ++q) s = fmaf(W2[q], w[L.e + (int64_t)(i * NMAX + j) * 32 + q], s);
         v = sigmoidf_(s);
       }
@@ -371,9 +438,9 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
     w[L.s + tid] = s;
   }
   __syncthreads();
-  lin_fwd(w + L.s, NF_, N, NF_, PW(H_DYN0_W), PW(H_DYN0_B), 32, w + L.d1, 32, true);
-  lin_fwd(w + L.d1, 32, N, 32, PW(H_DYN2_W), PW(H_DYN2_B), 32, w + L.d2, 32, true);
-  lin_fwd(w + L.d2, 32, N, 32, PW(H_DYN4_W), PW(H_DYN4_B), NF_, w + L.pred, NF_, false);
+  lin_fwd(w + L.s, NF_, N, NF_, PL(H_DYN0_W), PL(H_DYN0_B), 32, w + L.d1, 32, true);
+  lin_fwd(w + L.d1, 32, N, 32, PL(H_DYN2_W), PL(H_DYN2_B), 32, w + L.d2, 32, true);
+  lin_fwd(w + L.d2, 32, N, 32, PL(H_DYN4_W), PL(H_DYN4_B), NF_, w + L.pred, NF_, false);
   // scorer (cad:463-502)
   float* cin = w + L.cin;
   if (tid < NF_) {
@@ -391,20 +458,20 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
     cin[12 + tid] = fabsf(c - p);
   }
   __syncthreads();
-  lin_fwd(cin, 18, 1, 18, PW(H_CS0_W), PW(H_CS0_B), 64, w + L.cs1, 64, true);
+  lin_fwd(cin, 18, 1, 18, PL(H_CS0_W), PL(H_CS0_B), 64, w + L.cs1, 64, true);
   if (a.training && tid < 64) {
     const bool keep = rng_u24(a.h1_drop, (uint64_t)(a.clip0 + b), (uint64_t)tid) >= a.thr_drop;
     w[L.cs1 + tid] = keep ? w[L.cs1 + tid] * (1.0f / 0.8f) : 0.f;
   }
   __syncthreads();
-  lin_fwd(w + L.cs1, 64, 1, 64, PW(H_CS3_W), PW(H_CS3_B), 32, w + L.cs2, 32, true);
-  lin_fwd(w + L.cs2, 32, 1, 32, PW(H_CS5_W), PW(H_CS5_B), 1, w + L.cs, 1, false);
-  lin_fwd(cin, 18, 1, 12, PW(H_MS0_W), PW(H_MS0_B), 32, w + L.ms1, 32, true);
-  lin_fwd(w + L.ms1, 32, 1, 32, PW(H_MS2_W), PW(H_MS2_B), 16, w + L.ms2, 16, true);
-  lin_fwd(w + L.ms2, 16, 1, 16, PW(H_MS4_W), PW(H_MS4_B), 1, w + L.ms, 1, false);
-  lin_fwd(cin, 18, 1, 6, PW(H_TS0_W), PW(H_TS0_B), 32, w + L.ts1, 32, true);
-  lin_fwd(w + L.ts1, 32, 1, 32, PW(H_TS2_W), PW(H_TS2_B), 16, w + L.ts2, 16, true);
-  lin_fwd(w + L.ts2, 16, 1, 16, PW(H_TS4_W), PW(H_TS4_B), 1, w + L.ts, 1, false);
+  lin_fwd(w + L.cs1, 64, 1, 64, PL(H_CS3_W), PL(H_CS3_B), 32, w + L.cs2, 32, true);
+  lin_fwd(w + L.cs2, 32, 1, 32, PL(H_CS5_W), PL(H_CS5_B), 1, w + L.cs, 1, false);
+  lin_fwd(cin, 18, 1, 12, PL(H_MS0_W), PL(H_MS0_B), 32, w + L.ms1, 32, true);
+  lin_fwd(w + L.ms1, 32, 1, 32, PL(H_MS2_W), PL(H_MS2_B), 16, w + L.ms2, 16, true);
+  lin_fwd(w + L.ms2, 16, 1, 16, PL(H_MS4_W), PL(H_MS4_B), 1, w + L.ms, 1, false);
+  lin_fwd(cin, 18, 1, 6, PL(H_TS0_W), PL(H_TS0_B), 32, w + L.ts1, 32, true);
+  lin_fwd(w + L.ts1, 32, 1, 32, PL(H_TS2_W), PL(H_TS2_B), 16, w + L.ts2, 16, true);
+  lin_fwd(w + L.ts2, 16, 1, 16, PL(H_TS4_W), PL(H_TS4_B), 1, w + L.ts, 1, false);
   if (tid == 0) {
     const float cs = sigmoidf_(w[L.cs]), ms = sigmoidf_(w[L.ms]), ts = sigmoidf_(w[L.ts]);
     w[L.cs + 1] = cs; w[L.ms + 1] = ms; w[L.ts + 1] = ts;
@@ -416,6 +483,9 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
   }
   for (int i = tid; i < NMAX * NF_; i += HT) o.z[(int64_t)b * NMAX * NF_ + i] = (i < N * NF_) ? w[L.zz + i] : 0.f;
   for (int i = tid; i < 36; i += HT) o.adj[(int64_t)b * 36 + i] = w[L.A + i];
+  __syncthreads();
+  // hand the activations to the backward kernel
+  block_copy4<3>(wg, sw, HL_HANDOFF / 4, Ident{});
 }
 
 int head_fwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, hipStream_t st) {
@@ -436,13 +506,18 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
   const HL L;
   const RowLayout RL((int64_t)a.B * T * NMAX);
   float* rows = a.rows;
-  float* w = a.ws + (int64_t)b * a.ws_stride;
+  const float* wg = a.ws + (int64_t)b * a.ws_stride;
   float* g = slabs + (int64_t)b * slab_len;
-  __shared__ __attribute__((aligned(16))) float whh[G3 * GH];  // [q][j], read by columns (conflict-free)
+  __shared__ __attribute__((aligned(16))) float big[HF_BIG];  // MLP weight image, then W_hh [q][j] for BPTT
+  __shared__ __attribute__((aligned(16))) float sw[HL_TOTAL];
   __shared__ float dgh_s[NMAX * G3];
-  const float* Whh = PW(H_GRU_WHH);
-  for (int i = tid; i < G3 * GH; i += HT) whh[i] = Whh[i];
-  for (int64_t i = tid; i < slab_len; i += HT) g[i] = 0.f;
+  float* sW = big;
+  float* w = sw;
+  stage_head_weights(a, sW);
+  block_copy4<3>(sw, wg, HL_HANDOFF / 4, Ident{});
+  // slots the layer calls below may not write (structure learner without edges, the sparsity weight) read as 0;
+  // GRU / ReID slots are overwritten by head_rows_wgrad
+  for (int64_t i = tid; i < slab_len / 4; i += HT) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int N = o.nmax[b];
   const int m = min(N, NF_);
   const float dscore = up.d_causal[b];
@@ -463,25 +538,25 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
     __syncthreads();
     float* dcs2 = d1 + 8;
     float* dcs1 = d1 + 40;
-    lin_bwd(d1 + 0, 1, w + L.cs2, 32, 1, 32, PW(H_CS5_W), 1, GW(H_CS5_W), GW(H_CS5_B), dcs2, 32, false);
+    lin_bwd(d1 + 0, 1, w + L.cs2, 32, 1, 32, PL(H_CS5_W), 1, GW(H_CS5_W), GW(H_CS5_B), dcs2, 32, false);
     relu_gate(dcs2, 32, w + L.cs2, 32, 1, 32, 1.f);
-    lin_bwd(dcs2, 32, w + L.cs1, 64, 1, 64, PW(H_CS3_W), 32, GW(H_CS3_W), GW(H_CS3_B), dcs1, 64, false);
+    lin_bwd(dcs2, 32, w + L.cs1, 64, 1, 64, PL(H_CS3_W), 32, GW(H_CS3_W), GW(H_CS3_B), dcs1, 64, false);
     relu_gate(dcs1, 64, w + L.cs1, 64, 1, 64, a.training ? 1.f / 0.8f : 1.f);
-    lin_bwd(dcs1, 64, cin, 18, 1, 18, PW(H_CS0_W), 64, GW(H_CS0_W), GW(H_CS0_B), dcin, 18, true);
+    lin_bwd(dcs1, 64, cin, 18, 1, 18, PL(H_CS0_W), 64, GW(H_CS0_W), GW(H_CS0_B), dcin, 18, true);
     float* dms2 = d1 + 104;
     float* dms1 = d1 + 120;
-    lin_bwd(d1 + 1, 1, w + L.ms2, 16, 1, 16, PW(H_MS4_W), 1, GW(H_MS4_W), GW(H_MS4_B), dms2, 16, false);
+    lin_bwd(d1 + 1, 1, w + L.ms2, 16, 1, 16, PL(H_MS4_W), 1, GW(H_MS4_W), GW(H_MS4_B), dms2, 16, false);
     relu_gate(dms2, 16, w + L.ms2, 16, 1, 16, 1.f);
-    lin_bwd(dms2, 16, w + L.ms1, 32, 1, 32, PW(H_MS2_W), 16, GW(H_MS2_W), GW(H_MS2_B), dms1, 32, false);
+    lin_bwd(dms2, 16, w + L.ms1, 32, 1, 32, PL(H_MS2_W), 16, GW(H_MS2_W), GW(H_MS2_B), dms1, 32, false);
     relu_gate(dms1, 32, w + L.ms1, 32, 1, 32, 1.f);
-    lin_bwd(dms1, 32, cin, 18, 1, 12, PW(H_MS0_W), 32, GW(H_MS0_W), GW(H_MS0_B), dcin, 18, true);
+    lin_bwd(dms1, 32, cin, 18, 1, 12, PL(H_MS0_W), 32, GW(H_MS0_W), GW(H_MS0_B), dcin, 18, true);
     float* dts2 = d1 + 152;
     float* dts1 = d1 + 168;
-    lin_bwd(d1 + 2, 1, w + L.ts2, 16, 1, 16, PW(H_TS4_W), 1, GW(H_TS4_W), GW(H_TS4_B), dts2, 16, false);
+    lin_bwd(d1 + 2, 1, w + L.ts2, 16, 1, 16, PL(H_TS4_W), 1, GW(H_TS4_W), GW(H_TS4_B), dts2, 16, false);
     relu_gate(dts2, 16, w + L.ts2, 16, 1, 16, 1.f);
-    lin_bwd(dts2, 16, w + L.ts1, 32, 1, 32, PW(H_TS2_W), 16, GW(H_TS2_W), GW(H_TS2_B), dts1, 32, false);
+    lin_bwd(dts2, 16, w + L.ts1, 32, 1, 32, PL(H_TS2_W), 16, GW(H_TS2_W), GW(H_TS2_B), dts1, 32, false);
     relu_gate(dts1, 32, w + L.ts1, 32, 1, 32, 1.f);
-    lin_bwd(dts1, 32, cin, 18, 1, 6, PW(H_TS0_W), 32, GW(H_TS0_W), GW(H_TS0_B), dcin, 18, true);
+    lin_bwd(dts1, 32, cin, 18, 1, 6, PL(H_TS0_W), 32, GW(H_TS0_W), GW(H_TS0_B), dcin, 18, true);
   }
   float* dz = w + L.dz;
   float* dpred = w + L.dpred;
@@ -501,11 +576,11 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
   {
     float* dd2 = d1;
     float* dd1 = d1 + NMAX * 32;
-    lin_bwd(dpred, NF_, w + L.d2, 32, N, 32, PW(H_DYN4_W), NF_, GW(H_DYN4_W), GW(H_DYN4_B), dd2, 32, false);
+    lin_bwd(dpred, NF_, w + L.d2, 32, N, 32, PL(H_DYN4_W), NF_, GW(H_DYN4_W), GW(H_DYN4_B), dd2, 32, false);
     relu_gate(dd2, 32, w + L.d2, 32, N, 32, 1.f);
-    lin_bwd(dd2, 32, w + L.d1, 32, N, 32, PW(H_DYN2_W), 32, GW(H_DYN2_W), GW(H_DYN2_B), dd1, 32, false);
+    lin_bwd(dd2, 32, w + L.d1, 32, N, 32, PL(H_DYN2_W), 32, GW(H_DYN2_W), GW(H_DYN2_B), dd1, 32, false);
     relu_gate(dd1, 32, w + L.d1, 32, N, 32, 1.f);
-    lin_bwd(dd1, 32, w + L.s, NF_, N, NF_, PW(H_DYN0_W), 32, GW(H_DYN0_W), GW(H_DYN0_B), ds, NF_, false);
+    lin_bwd(dd1, 32, w + L.s, NF_, N, NF_, PL(H_DYN0_W), 32, GW(H_DYN0_W), GW(H_DYN0_B), ds, NF_, false);
   }
   float* dA = w + L.dA;
   if (tid < 36) {
@@ -526,7 +601,7 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
     float* dnode = w + L.dnode;
     for (int i = tid; i < NMAX * 32; i += HT) dnode[i] = 0.f;
     float* de = d1;  // [pairs][32]
-    const float* W2 = PW(H_EDGE2_W);
+    const float* W2 = PL(H_EDGE2_W);
     for (int idx = tid; idx < m * m * 32; idx += HT) {
       const int pr = idx / 32, u = idx - pr * 32;
       const int i = pr / m, j = pr - i * m;
@@ -549,8 +624,8 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
           const float da = dA[i * 6 + j] * Aij * (1.f - Aij);
           s += tid < 32 ? da * w[L.e + (int64_t)(i * NMAX + j) * 32 + tid] : da;
         }
-      if (tid < 32) GW(H_EDGE2_W)[tid] += s;
-      else GW(H_EDGE2_B)[0] += s;
+      if (tid < 32) GW(H_EDGE2_W)[tid] = s;
+      else GW(H_EDGE2_B)[0] = s;
     }
     float* dW0 = GW(H_EDGE0_W);
     for (int idx = tid; idx < 32 * 64; idx += HT) {
@@ -562,14 +637,14 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
           const float in = q < 32 ? w[L.node + i * 32 + q] : w[L.node + j * 32 + q - 32];
           s = fmaf(de[(i * m + j) * 32 + u], in, s);
         }
-      dW0[idx] += s;
+      dW0[idx] = s;
     }
     if (tid < 32) {
       float s = 0.f;
       for (int pr = 0; pr < m * m; ++pr) s += de[pr * 32 + tid];
-      GW(H_EDGE0_B)[tid] += s;
+      GW(H_EDGE0_B)[tid] = s;
     }
-    const float* W0 = PW(H_EDGE0_W);
+    const float* W0 = PL(H_EDGE0_W);
     for (int idx = tid; idx < m * 32; idx += HT) {
       const int k = idx / 32, q = idx - k * 32;
       float s = 0.f;
@@ -583,7 +658,7 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
       dnode[idx] = s;
     }
     __syncthreads();
-    lin_bwd(dnode, 32, w + L.zz, NF_, N, NF_, PW(H_NODE_W), 32, GW(H_NODE_W), GW(H_NODE_B), dz, NF_, true);
+    lin_bwd(dnode, 32, w + L.zz, NF_, N, NF_, PL(H_NODE_W), 32, GW(H_NODE_W), GW(H_NODE_B), dz, NF_, true);
   }
   // ---- VAE + KL (cad:328-347)
   {
@@ -601,14 +676,14 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
     __syncthreads();
     float* dce2 = d1 + 64;
     float* dce1 = d1 + 256;
-    lin_bwd(dmu, NF_, w + L.ce2, 32, N, 32, PW(H_MU_W), NF_, GW(H_MU_W), GW(H_MU_B), dce2, 32, false);
-    lin_bwd(dlv, NF_, w + L.ce2, 32, N, 32, PW(H_LV_W), NF_, GW(H_LV_W), GW(H_LV_B), dce2, 32, true);
+    lin_bwd(dmu, NF_, w + L.ce2, 32, N, 32, PL(H_MU_W), NF_, GW(H_MU_W), GW(H_MU_B), dce2, 32, false);
+    lin_bwd(dlv, NF_, w + L.ce2, 32, N, 32, PL(H_LV_W), NF_, GW(H_LV_W), GW(H_LV_B), dce2, 32, true);
     relu_gate(dce2, 32, w + L.ce2, 32, N, 32, 1.f);
-    lin_bwd(dce2, 32, w + L.ce1, 32, N, 32, PW(H_CE2_W), 32, GW(H_CE2_W), GW(H_CE2_B), dce1, 32, false);
+    lin_bwd(dce2, 32, w + L.ce1, 32, N, 32, PL(H_CE2_W), 32, GW(H_CE2_W), GW(H_CE2_B), dce1, 32, false);
     relu_gate(dce1, 32, w + L.ce1, 32, N, 32, 1.f);
     float* denc = d1 + 448;
-    lin_bwd(dce1, 32, w + L.enc, 32, N, 32, PW(H_CE0_W), 32, GW(H_CE0_W), GW(H_CE0_B), denc, 32, false);
-    lin_bwd(denc, 32, w + L.hT, GH, N, GH, PW(H_ENC_W), 32, GW(H_ENC_W), GW(H_ENC_B), w + L.dh, GH, false);
+    lin_bwd(dce1, 32, w + L.enc, 32, N, 32, PL(H_CE0_W), 32, GW(H_CE0_W), GW(H_CE0_B), denc, 32, false);
+    lin_bwd(denc, 32, w + L.hT, GH, N, GH, PL(H_ENC_W), 32, GW(H_ENC_W), GW(H_ENC_B), w + L.dh, GH, false);
   }
   // ---- GRU backward through time (dh'/dz = h - n, dh'/dn = 1 - z)
   {
@@ -617,20 +692,35 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
     // published to the wave's LDS row, and dh_prev[u] = dh[u] z[u] + sum_q W_hh[q][u] dgh[q] reads them back --
     // no block barrier inside the time loop
     static_assert(NMAX * 64 <= HT && GH == 64, "one wave per trajectory, one lane per hidden unit");
+    static_assert(G3 * GH <= HF_BIG, "W_hh fits the weight image's LDS");
+    __syncthreads();  // the MLP weight image is dead: load W_hh [q][j] (read by columns, conflict-free)
+    float* whh = big;
+    const float* Whh = PW(H_GRU_WHH);
+    block_copy4<6>(whh, Whh, G3 * GH / 4, Ident{});
     __syncthreads();
     const int nn = tid >> 6, u = tid & 63;
     if (nn < NMAX) {
       const bool live = nn < N;
       float d = live ? dh[nn * GH + u] : 0.f;
       float* dgv = dgh_s + nn * G3;
+      // the saved gates of step t-1 are loaded while step t computes
+      float r = 0.f, z = 0.f, nv = 0.f, hp = 0.f, ghn = 0.f;
+      if (live) {
+        const int64_t row = ((int64_t)b * T + T - 1) * NMAX + nn;
+        r = rows[RL.r + row * GH + u]; z = rows[RL.z + row * GH + u]; nv = rows[RL.n + row * GH + u];
+        hp = rows[RL.hp + row * GH + u]; ghn = rows[RL.ghn + row * GH + u];
+      }
       for (int t = T - 1; t >= 0; --t) {
         const int64_t row = ((int64_t)b * T + t) * NMAX + nn;
         float* dgi = rows + RL.dgi + row * G3;
         float* dgh = rows + RL.dgh + row * G3;
         if (live) {
-          const float r = rows[RL.r + row * GH + u], z = rows[RL.z + row * GH + u];
-          const float nv = rows[RL.n + row * GH + u];
-          const float hp = rows[RL.hp + row * GH + u], ghn = rows[RL.ghn + row * GH + u];
+          float nr = 0.f, nz = 0.f, nn_ = 0.f, nhp = 0.f, nghn = 0.f;
+          if (t > 0) {
+            const int64_t pr = row - NMAX;
+            nr = rows[RL.r + pr * GH + u]; nz = rows[RL.z + pr * GH + u]; nn_ = rows[RL.n + pr * GH + u];
+            nhp = rows[RL.hp + pr * GH + u]; nghn = rows[RL.ghn + pr * GH + u];
+          }
           const float dan = d * (1.f - z) * (1.f - nv * nv);
           const float daz = d * (hp - nv) * z * (1.f - z);
           const float dar = dan * ghn * r * (1.f - r);
@@ -646,6 +736,7 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
           float s = d * z;
           for (int q = 0; q < G3; ++q) s = fmaf(whh[q * GH + u], dgv[q], s);
           d = s;
+          r = nr; z = nz; nv = nn_; hp = nhp; ghn = nghn;
         } else {
           dgi[u] = 0.f; dgi[GH + u] = 0.f; dgi[2 * GH + u] = 0.f;
           dgh[u] = 0.f; dgh[GH + u] = 0.f; dgh[2 * GH + u] = 0.f;

@@ -46,14 +46,26 @@ CONV_CASES = [(2, 32, 32, 19, 17, 1), (2, 32, 64, 29, 29, 2), (1, 64, 128, 15, 1
               (2, 32, 64, 57, 57, 2), (3, 128, 256, 16, 16, 2), (1, 64, 128, 31, 18, 2)]
 
 
-@pytest.mark.parametrize("patch", [1, 0, 2])
-@pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", CONV_CASES)
-def test_conv3x3_forward_and_dgrad(NF, Ci, Co, IH, IW, s, patch):
-    """patch 1: LDS-patch kernels (persistent variant for 32-channel stride-1 layers), 2: patch kernels without the
-    persistent variant, 0: implicit-GEMM path."""
-    nat = _lib()
+def _conv_path(nat, patch):
     nat.lib().vad_set_tuning(b"conv_patch", 1 if patch else 0)
     nat.lib().vad_set_tuning(b"conv_patch_persist", 0 if patch == 2 else 1)
+    nat.lib().vad_set_tuning(b"conv_split", 1 if patch == 3 else 0)
+
+
+def _conv_default(nat):
+    nat.lib().vad_set_tuning(b"conv_patch", 1)
+    nat.lib().vad_set_tuning(b"conv_patch_persist", 1)
+    nat.lib().vad_set_tuning(b"conv_split", 1)
+
+
+@pytest.mark.parametrize("patch", [3, 1, 0, 2])
+@pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", CONV_CASES)
+def test_conv3x3_forward_and_dgrad(NF, Ci, Co, IH, IW, s, patch):
+    """patch 3: split-bf16 patch kernels (conv_x3.hip; stride-2 input gradients stay on the f32 parity kernel),
+    1: f32 LDS-patch kernels (persistent variant for 32-channel stride-1 layers), 2: f32 patch kernels without the
+    persistent variant, 0: implicit-GEMM path."""
+    nat = _lib()
+    _conv_path(nat, patch)
     g = torch.Generator().manual_seed(NF * 7 + Ci + Co + IH)
     x = torch.randn(NF, Ci, IH, IW, generator=g)
     w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
@@ -82,9 +94,42 @@ def test_conv3x3_forward_and_dgrad(NF, Ci, Co, IH, IW, s, patch):
     nat.check(nat.lib().vad_conv3x3_dgrad(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, s, dx.data_ptr(),
                                           wf.data_ptr(), wd.data_ptr(), st))
     torch.cuda.synchronize()
-    nat.lib().vad_set_tuning(b"conv_patch", 1)
-    nat.lib().vad_set_tuning(b"conv_patch_persist", 1)
+    _conv_default(nat)
     np.testing.assert_allclose(dx.cpu().permute(0, 3, 1, 2).numpy(), xr.grad.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", [(2, 64, 64, 29, 29, 1), (2, 32, 64, 57, 57, 2), (1, 256, 256, 8, 8, 1)])
+def test_conv3x3_split_accuracy_matches_f32(NF, Ci, Co, IH, IW, s):
+    """The split-bf16 kernels (three bf16 planes per fp32 operand, six products per K step) against an fp64
+    reference: their worst error, relative to sum |x||w| of each output, is within 2x that of the exact-f32 MFMA
+    patch kernels (both are ~1e-7; a plain bf16 conv would sit near 4e-3)."""
+    nat = _lib()
+    g = torch.Generator().manual_seed(5 + Ci + IH)
+    x = torch.randn(NF, Ci, IH, IW, generator=g)
+    w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
+    bias = torch.zeros(Co)
+    ref = F.conv2d(x.double(), w.double(), bias.double(), stride=s, padding=1)
+    mag = F.conv2d(x.double().abs(), w.double().abs(), None, stride=s, padding=1)
+    OH, OW = ref.shape[2:]
+    d = torch.device("cuda")
+    xh = x.permute(0, 2, 3, 1).contiguous().to(d)
+    wdev, bd = w.contiguous().to(d), bias.to(d)
+    errs = {}
+    for patch in (1, 3):
+        _conv_path(nat, patch)
+        y = torch.empty(NF, OH, OW, Co, device=d)
+        wf = torch.empty(9 * Ci * Co, device=d)
+        wd = torch.empty(9 * Ci * Co, device=d)
+        parts = torch.empty((NF * OH * OW // 64 + 2) * 2 * Co, device=d)
+        nat.check(nat.lib().vad_conv3x3_forward(xh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), bd.data_ptr(), Co, s,
+                                                y.data_ptr(), wf.data_ptr(), wd.data_ptr(), parts.data_ptr(),
+                                                nat.stream_of(d)))
+        torch.cuda.synchronize()
+        out = y.cpu().permute(0, 3, 1, 2).double()
+        errs[patch] = float(((out - ref).abs() / mag).max())
+    _conv_default(nat)
+    assert errs[3] < 1e-6, errs
+    assert errs[3] <= 2.0 * errs[1] + 1e-8, errs
 
 
 @pytest.mark.parametrize("stream", [rng.S_DET_DROP1, rng.S_EPS, rng.S_INPUT])
