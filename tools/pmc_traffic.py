@@ -16,7 +16,9 @@ import sys
 def family(name):
     if "conv3x3_wgrad_patch_kernel" in name or ("gemm_kernel" in name and "ConvPatchKM" in name):
         return "conv_wgrad"
-    if "conv3x3_patch_kernel" in name:
+    if "conv3x3_wgrad_x3_kernel" in name:
+        return "conv_wgrad"
+    if "conv3x3_patch_kernel" in name or "conv3x3_x3_kernel" in name:
         return "conv_fwd" if ", true>" in name else "conv_dgrad"
     if "conv3x3_dgrad_s2_kernel" in name or ("gemm_kernel" in name and "EpiConvDgrad" in name):
         return "conv_dgrad"
