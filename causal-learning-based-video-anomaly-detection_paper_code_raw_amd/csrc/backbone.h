@@ -40,6 +40,9 @@ struct Conv3Layer {
 };
 // weight relayout: W[co][ci][3][3] -> Wf[co][9][ci] and per-parity-class dgrad images Wd[ci][taps][co]
 int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd, hipStream_t st);
+// the same for n <= 8 layers in one launch
+int conv3_prep_weights_all(int n, const float* const* w, const Conv3Layer* L, float* const* wf, float* const* wd,
+                           hipStream_t st);
 int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats /*nullable: BN+ReLU on load*/,
               const float* wf, const float* bias, float* y, float* partials, int* nparts, hipStream_t st);
 int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
@@ -58,6 +61,10 @@ bool conv3_x3_supported(const Conv3Layer& L, bool fwd);
 int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
                  float* y, float* partials, int* nparts, hipStream_t st);
 int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
+extern int g_wgrad_split;  // stride-1 weight gradients on the split-bf16 kernel (knob "conv_wgrad_split")
+bool conv3_wgrad_x3_supported(const Conv3Layer& L);
+int conv3_wgrad_x3(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
+                   int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);
 bool conv3_wgrad_patch_supported(const Conv3Layer& L);
 int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
                       int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);

@@ -99,7 +99,7 @@ int conv1_fwd(const float* x, int NF, int H, int W, const float* w, const float*
   const int bands = (int)cdiv(OH, C1_RB);
   const size_t lds = (size_t)(2 * C1_RB + 5) * (2 * OW + 6) * sizeof(float);
   VAD_CHECK(lds <= 160 * 1024, "conv1: frame too wide for the LDS band");
-  hipLaunchKernelGGL(conv1_kernel, dim3(NF * bands), dim3(256), lds, st, x, H, W, w, b, y, OH, OW, bands, partials);
+  VAD_KLAUNCH(conv1_kernel, dim3(NF * bands), dim3(256), lds, st, x, H, W, w, b, y, OH, OW, bands, partials);
   VAD_LAUNCH_CHECK();
   *nparts = NF * bands;
   return 0;
@@ -639,7 +639,7 @@ static int launch_gemm(const typename LA<Cfg::BM>::Params& pa, const typename LB
   splits = (int)cdiv(K, kps);
   if (splits < 1) splits = 1;
   dim3 grid((unsigned)cdiv(M, Cfg::BM), (unsigned)cdiv(N, Cfg::BN), (unsigned)splits);
-  hipLaunchKernelGGL((gemm_kernel<Cfg, LA<Cfg::BM>, LB<Cfg::BN>, Epi>), grid, dim3(256), 0, st, pa, pb, pe, M, N, K,
+  VAD_KLAUNCH((gemm_kernel<Cfg, LA<Cfg::BM>, LB<Cfg::BN>, Epi>), grid, dim3(256), 0, st, pa, pb, pe, M, N, K,
                      kps, skip);
   VAD_LAUNCH_CHECK();
   if (used_splits) *used_splits = splits;
@@ -697,6 +697,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_split_nt") g_x3_nt = value;
   else if (k == "conv_split_dbg") g_x3_dbg = value;
   else if (k == "conv_wgrad_patch") g_tune.wgrad_patch = value;
+  else if (k == "conv_wgrad_split") g_wgrad_split = value;
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else {
     set_error("unknown tuning key " + k);
@@ -785,6 +786,67 @@ __global__ void conv3_prep_kernel(const float* __restrict__ w, int Ci, int Co, i
   }
 }
 
+struct PrepTab {
+  const float* w[8];
+  float* wf[8];
+  float* wd[8];
+  int Ci[8], Co[8], classes[8];
+  int64_t end[8];  // inclusive prefix sums of Co*Ci*9
+  int n;
+};
+
+__global__ void conv3_prep_all_kernel(const PrepTab t) {
+  const int64_t total = t.end[t.n - 1];
+  for (int64_t g = blockIdx.x * 256ll + threadIdx.x; g < total; g += (int64_t)gridDim.x * 256) {
+    int l = 0;
+    while (g >= t.end[l]) ++l;
+    const int64_t i = g - (l ? t.end[l - 1] : 0);
+    const int Ci = t.Ci[l], Co = t.Co[l];
+    const int tap = (int)(i % 9);
+    const int ci = (int)((i / 9) % Ci);
+    const int co = (int)(i / (9 * Ci));
+    const float v = t.w[l][i];
+    t.wf[l][((int64_t)co * 9 + tap) * Ci + ci] = v;
+    if (!t.classes[l]) {
+      t.wd[l][((int64_t)ci * 9 + tap) * Co + co] = v;
+    } else {
+      const int kh = tap / 3, kw = tap % 3;
+      const int ph = (kh + 1) & 1, pw = (kw + 1) & 1;
+      const int ri = (ph == 0) ? 0 : (kh == 0 ? 0 : 1);
+      const int cj = (pw == 0) ? 0 : (kw == 0 ? 0 : 1);
+      const int nrt = ph == 0 ? 1 : 2, nct = pw == 0 ? 1 : 2;
+      int64_t off = 0;
+      for (int c = 0; c < ph * 2 + pw; ++c) {
+        const int r = (c >> 1) == 0 ? 1 : 2, q = (c & 1) == 0 ? 1 : 2;
+        off += (int64_t)r * q * Ci * Co;
+      }
+      t.wd[l][off + ((int64_t)ci * (nrt * nct) + ri * nct + cj) * Co + co] = v;
+    }
+  }
+}
+
+int conv3_prep_weights_all(int n, const float* const* w, const Conv3Layer* L, float* const* wf, float* const* wd,
+                           hipStream_t st) {
+  VAD_CHECK(n >= 1 && n <= 8, "conv3_prep_weights_all: 1..8 layers");
+  PrepTab t{};
+  t.n = n;
+  int64_t acc = 0;
+  for (int l = 0; l < n; ++l) {
+    t.w[l] = w[l];
+    t.wf[l] = wf[l];
+    t.wd[l] = wd[l];
+    t.Ci[l] = L[l].Ci;
+    t.Co[l] = L[l].Co;
+    t.classes[l] = L[l].stride == 2 && !(g_tune.patch && conv3_patch_supported(L[l], false));
+    acc += (int64_t)L[l].Co * L[l].Ci * 9;
+    t.end[l] = acc;
+  }
+  hipLaunchKernelGGL(conv3_prep_all_kernel, dim3((unsigned)std::min<int64_t>(cdiv(acc, 256), 4096)), dim3(256), 0, st,
+                     t);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
 int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd, hipStream_t st) {
   const int64_t total = (int64_t)L.Co * L.Ci * 9;
   const int classes = L.stride == 2 && !(g_tune.patch && conv3_patch_supported(L, false));
@@ -869,6 +931,8 @@ int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX
 
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
                 int* nsplit, int64_t partial_cap, hipStream_t st) {
+  if (g_tune.wgrad_patch && conv3_wgrad_x3_supported(L))
+    return conv3_wgrad_x3(L, dY, src, src_stats, partial, nsplit, partial_cap, g_tune.wgrad_patch_blocks, st);
   if (g_tune.wgrad_patch && conv3_wgrad_patch_supported(L) && (L.stride == 1 || g_tune.wgrad_patch == 2))
     return conv3_wgrad_patch(L, dY, src, src_stats, partial, nsplit, partial_cap, g_tune.wgrad_patch_blocks, st);
   const int M = L.Co, N = 9 * L.Ci, K = L.NF * L.OH * L.OW;
@@ -946,10 +1010,157 @@ int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, co
 // =====================================================================================================
 // dense layers
 // =====================================================================================================
+// Few-row layers (M <= 16: the direct classifier runs on the B clips of a rank, cad:568-570) are bound by the weight
+// read and by launch latency, not by FLOPs: they use row-streaming kernels instead of the MFMA GEMM tiles, whose K
+// loop over 64-row tiles would leave most of the chip idle.
+constexpr int kSkinnyRows = 16;
+static bool skinny_ok(int M, int K) { return M >= 1 && M <= kSkinnyRows && K % 4 == 0; }
+
+// Y[m][n] = finish(sum_k X[m][k] W[n][k]): a block owns 4 output columns; its 512 threads stride over K in float4
+// steps (coalesced W rows, X from L2) with the loads of up to 4 steps in flight, then the 4*MR partial sums are
+// combined through LDS in a fixed order.
+template <int MR>
+__global__ __launch_bounds__(512) void skinny_fwd_kernel(const float* __restrict__ X, int M, int K,
+                                                         const float* __restrict__ W, int N, DenseEpiArgs P) {
+  constexpr int NT = 512, NO = 4 * MR, G = NT / NO, U = 4;
+  __shared__ float red[NT][NO + 1];
+  const int tid = threadIdx.x, n0 = blockIdx.x * 4, K4 = K / 4;
+  float acc[4][MR];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int m = 0; m < MR; ++m) acc[c][m] = 0.f;
+  for (int kb = 0; kb < K4; kb += NT * U) {
+    f32x4 w[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k4 = kb + u * NT + tid;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        w[u][c] = (k4 < K4 && n0 + c < N) ? *reinterpret_cast<const f32x4*>(W + (int64_t)(n0 + c) * K + 4 * k4)
+                                          : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k4 = kb + u * NT + tid;
+      if (k4 >= K4) break;
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        if (m < M) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(X + (int64_t)m * K + 4 * k4);
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            acc[c][m] = fmaf(x[3], w[u][c][3], fmaf(x[2], w[u][c][2], fmaf(x[1], w[u][c][1], fmaf(x[0], w[u][c][0], acc[c][m]))));
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int m = 0; m < MR; ++m) red[tid][c * MR + m] = acc[c][m];
+  __syncthreads();
+  const int o = tid / G, part = tid % G;
+  float v = 0.f;
+  for (int r = part; r < NT; r += G) v += red[r][o];
+#pragma unroll
+  for (int off = 1; off < G; off <<= 1) v += __shfl_xor(v, off, 64);
+  const int c = o / MR, m = o % MR;
+  if (part == 0 && m < M && n0 + c < N) P.out[(int64_t)m * P.ldc + n0 + c] = dense_finish(P, m, n0 + c, v);
+}
+
+// dX[m][k] = gate(sum_n dY[m][n] W[n][k]): a block owns 64 consecutive k (one per lane), its 16 waves split N (8 W
+// loads in flight per lane); dY is staged in LDS as [n][MR] (broadcast reads), the waves are combined in a fixed order.
+template <int MR>
+__global__ __launch_bounds__(1024) void skinny_dgrad_kernel(const float* __restrict__ dY, int M, int N,
+                                                            const float* __restrict__ W, int K, DenseEpiArgs P,
+                                                            const int* skip) {
+  if (skip && *skip == 0) return;
+  constexpr int NW = 16, U = 8;
+  extern __shared__ __attribute__((aligned(16))) float dsm[];  // [N][MR] then [NW][MR][64]
+  float* dys = dsm;
+  float* red = dsm + (int64_t)N * MR;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < N * MR; i += 64 * NW) {
+    const int n = i / MR, m = i % MR;
+    dys[i] = m < M ? dY[(int64_t)m * N + n] : 0.f;
+  }
+  __syncthreads();
+  const int k = blockIdx.x * 64 + lane;
+  const int nq = (N + NW - 1) / NW, nb = wave * nq, ne = min(N, nb + nq);
+  float acc[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) acc[m] = 0.f;
+  if (k < K) {
+    for (int n0 = nb; n0 < ne; n0 += U) {
+      float w[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) w[u] = n0 + u < ne ? W[(int64_t)(n0 + u) * K + k] : 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (n0 + u >= ne) break;
+#pragma unroll
+        for (int m4 = 0; m4 < MR; m4 += 4) {
+          const f32x4 d = *reinterpret_cast<const f32x4*>(dys + (n0 + u) * MR + m4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[m4 + e] = fmaf(d[e], w[u], acc[m4 + e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MR; ++m) red[(wave * MR + m) * 64 + lane] = acc[m];
+  __syncthreads();
+  if (wave == 0 && k < K) {
+    for (int m = 0; m < M; ++m) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) v += red[(q * MR + m) * 64 + lane];
+      P.out[(int64_t)m * P.ldc + k] = dense_finish(P, m, k, v);
+    }
+  }
+}
+
+// dW[n][k] = sum_m dY[m][n] X[m][k] (written), db[n] = sum_m dY[m][n]: a thread owns 4 columns n x one float4 of k.
+__global__ __launch_bounds__(256) void skinny_wgrad_kernel(const float* __restrict__ dY, int M, int N,
+                                                           const float* __restrict__ X, int K, float* __restrict__ dW,
+                                                           float* __restrict__ db, const int* skip) {
+  if (skip && *skip == 0) return;
+  const int k4 = blockIdx.x * 256 + threadIdx.x, n0 = blockIdx.y * 4;
+  if (db && blockIdx.x == 0 && threadIdx.x < 4 && n0 + (int)threadIdx.x < N) {
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) s += dY[(int64_t)m * N + n0 + threadIdx.x];
+    db[n0 + threadIdx.x] = s;
+  }
+  if (k4 >= K / 4) return;
+  f32x4 acc[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < M; ++m) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(X + (int64_t)m * K + 4 * k4);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float d = n0 + c < N ? dY[(int64_t)m * N + n0 + c] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[c][e] = fmaf(d, x[e], acc[c][e]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (n0 + c < N) *reinterpret_cast<f32x4*>(dW + (int64_t)(n0 + c) * K + 4 * k4) = acc[c];
+}
+
 int dense_fwd(const float* X, int M, int K, const float* W, const float* b, int N, float* Y, const DenseAct& act,
               float* scratch, int64_t scratch_floats, hipStream_t st, int max_splits) {
   using C = T64x64;
   DenseEpiArgs pe{Y, N, b, act.relu, act.drop, act.h1, act.thr, act.dscale, act.row0, nullptr, 1.f};
+  if (skinny_ok(M, K)) {
+    const dim3 grid((unsigned)cdiv(N, 4));
+    if (M <= 8) hipLaunchKernelGGL(skinny_fwd_kernel<8>, grid, dim3(512), 0, st, X, M, K, W, N, pe);
+    else hipLaunchKernelGGL(skinny_fwd_kernel<16>, grid, dim3(512), 0, st, X, M, K, W, N, pe);
+    VAD_LAUNCH_CHECK();
+    return 0;
+  }
   DenseKC<C::BM>::Params pa{X, K, M, K};
   DenseKC<C::BN>::Params pb{W, K, N, K};
   const int tiles = (int)(cdiv(M, C::BM) * cdiv(N, C::BN));
@@ -985,6 +1196,17 @@ int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX,
   // dX[m][k] = sum_n dY[m][n] W[n][k]: A = dY (KC over n), B(row k, red n) = W[n][k] (KM, ld K)
   using C = T64x64;
   DenseEpiArgs pe{dX, K, nullptr, 0, 0, 0, 0, 1.f, 0, gate, gscale};
+  if (skinny_ok(M, N) && (int64_t)(N + 1024) * (M <= 8 ? 8 : 16) * 4 <= 65536) {  // dY + combine buffer in LDS
+    const dim3 grid((unsigned)cdiv(K, 64));
+    if (M <= 8)
+      hipLaunchKernelGGL(skinny_dgrad_kernel<8>, grid, dim3(1024), sizeof(float) * (N * 8 + 16 * 8 * 64), st, dY, M, N,
+                         W, K, pe, skip);
+    else
+      hipLaunchKernelGGL(skinny_dgrad_kernel<16>, grid, dim3(1024), sizeof(float) * (N * 16 + 16 * 16 * 64), st, dY, M,
+                         N, W, K, pe, skip);
+    VAD_LAUNCH_CHECK();
+    return 0;
+  }
   DenseKC<C::BM>::Params pa{dY, N, M, N};
   DenseKM<C::BN>::Params pb{W, K, K, N, -1};
   return launch_gemm<C, DenseKC, DenseKM, EpiDense>(pa, pb, pe, M, K, N, 1, skip, st);
@@ -994,6 +1216,12 @@ int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW,
                 int64_t scratch_floats, const int* skip, hipStream_t st) {
   // GEMM rows = out feature n, cols = in feature k (+ ones column for the bias), reduction over m
   using C = T64x64;
+  if (skinny_ok(M, K)) {
+    hipLaunchKernelGGL(skinny_wgrad_kernel, dim3((unsigned)cdiv(K / 4, 256), (unsigned)cdiv(N, 4)), dim3(256), 0, st, dY,
+                       M, N, X, K, dW, db, skip);
+    VAD_LAUNCH_CHECK();
+    return 0;
+  }
   const int GN = K + 1;
   DenseKM<C::BM>::Params pa{dY, N, N, M, -1};
   DenseKM<C::BN>::Params pb{X, K, K, M, K};

@@ -252,7 +252,9 @@ struct Profiler {
   hipEvent_t get() {
     if (used == pool.size()) {
       hipEvent_t e;
-      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      // timing-only events: no system-scope fence (an L2 writeback per record would cost ~6 us of GPU time
+      // and slow the next kernel)
+      if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
       pool.push_back(e);
     }
     return pool[used++];
@@ -264,17 +266,29 @@ struct Profiler {
   }
 };
 
+// Labelled launch timing.  Breakdown mode (all labels): hipEventRecord around the op.  Family mode (a label
+// prefix, bench.py's live roofline of the conv families): the op's kernel is dispatched with the events itself
+// (VAD_KLAUNCH), so the timed steps carry no extra marker packets.
 #define TIMED(label, expr)                                       \
   do {                                                           \
     const bool _w = prof.wants(label);                           \
+    const bool _k = _w && !prof.only.empty();                    \
     hipEvent_t _a = nullptr, _b = nullptr;                       \
     if (_w) {                                                    \
       _a = prof.get();                                           \
       _b = prof.get();                                           \
-      VAD_HIP(hipEventRecord(_a, st));                           \
+      if (_k) {                                                  \
+        ktimer().a = _a;                                         \
+        ktimer().b = _b;                                         \
+      } else {                                                   \
+        VAD_HIP(hipEventRecord(_a, st));                         \
+      }                                                          \
     }                                                            \
     VAD_TRY(expr);                                               \
-    if (_w) {                                                    \
+    if (_k) {                                                    \
+      if (ktimer().a == nullptr) prof.recs.push_back({std::string(label), _a, _b}); \
+      ktimer().a = ktimer().b = nullptr;                         \
+    } else if (_w) {                                             \
       VAD_HIP(hipEventRecord(_b, st));                           \
       prof.recs.push_back({std::string(label), _a, _b});         \
     }                                                            \
@@ -506,7 +520,11 @@ struct CadPlanImpl {
 
   int forward(const float* x, hipStream_t st) {
     const CadLayout& LY = layout();
-    for (int l = 0; l < 8; ++l) TIMED("prep", conv3_prep_weights(P(LY.conv_w[l]), L[l], wf[l], wd[l], st));
+    {
+      const float* w8[8];
+      for (int l = 0; l < 8; ++l) w8[l] = P(LY.conv_w[l]);
+      TIMED("prep", conv3_prep_weights_all(8, w8, L, wf, wd, st));
+    }
     int np = 0;
     TIMED("conv1", conv1_fwd(x, NF, H, W, P(LY.conv1_w), P(LY.conv1_b), y1, H1, W1, parts, &np, st));
     TIMED("bn_fin", bn_finalize(parts, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), RM(0), RV(0), 0.1f,
@@ -860,9 +878,10 @@ int vad_cad_set_debug(vad_cad_plan* plan, const char* key, int64_t value) {
 int vad_cad_profile(vad_cad_plan* plan, int enable, const char* only_prefix) {
   VAD_CHECK(plan != nullptr, "vad_cad_profile: null plan");
   Profiler& p = plan->impl.prof;
+  // enable: 0 off (records kept), 1 on after clearing the records, 2 on, appending to the records
   p.on = enable != 0;
-  p.only = only_prefix ? only_prefix : "";
-  p.reset();
+  if (enable) p.only = only_prefix ? only_prefix : "";
+  if (enable == 1) p.reset();
   return 0;
 }
 

@@ -1,5 +1,6 @@
 // Shared device/host helpers for libvadhip (gfx950 / CDNA4 only).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
@@ -32,6 +33,24 @@ const char* last_error();
   } while (0)
 
 #define VAD_LAUNCH_CHECK() VAD_HIP(hipGetLastError())
+
+// Kernel-timing hook for live roofline measurement: when armed, the next VAD_KLAUNCH (the conv kernels) is
+// dispatched with hipExtLaunchKernel's start/stop events, which take their timestamps from the dispatch itself
+// (no marker packets between kernels, unlike hipEventRecord around the launch).
+struct KTimer {
+  hipEvent_t a = nullptr, b = nullptr;
+};
+KTimer& ktimer();
+#define VAD_KLAUNCH(kernel, grid, block, shm, st, ...)                                                       \
+  do {                                                                                                     \
+    ::vad::KTimer& _kt = ::vad::ktimer();                                                                   \
+    if (_kt.a) {                                                                                           \
+      hipExtLaunchKernelGGL(kernel, grid, block, shm, st, _kt.a, _kt.b, 0, __VA_ARGS__);                   \
+      _kt.a = _kt.b = nullptr;                                                                             \
+    } else {                                                                                               \
+      hipLaunchKernelGGL(kernel, grid, block, shm, st, __VA_ARGS__);                                       \
+    }                                                                                                      \
+  } while (0)
 
 #define VAD_TRY(expr)        \
   do {                       \

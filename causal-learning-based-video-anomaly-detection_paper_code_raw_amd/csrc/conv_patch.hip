@@ -448,7 +448,7 @@ static int launch_patch_persist(PatchArgs a, hipStream_t st, int* nparts) {
   const int target = std::max(1, 512 / ny);  // 2 resident blocks per CU over 256 CUs
   const int tpb = (int)cdiv(ntiles, target);
   const int gx = (int)cdiv(ntiles, tpb);
-  hipLaunchKernelGGL((conv3x3_patch_persist_kernel<NI, TH, TW, FWD>), dim3(gx, ny), dim3(256), 0, st, a, tpb, ntiles);
+  VAD_KLAUNCH((conv3x3_patch_persist_kernel<NI, TH, TW, FWD>), dim3(gx, ny), dim3(256), 0, st, a, tpb, ntiles);
   VAD_LAUNCH_CHECK();
   if (nparts) *nparts = gx;
   return 0;
@@ -460,7 +460,7 @@ static int launch_patch(PatchArgs a, hipStream_t st, int* nparts) {
   a.tiles_w = (int)cdiv(a.OW, TW);
   const int64_t gx = cdiv(a.NF, NI) * a.tiles_h * a.tiles_w;
   dim3 grid((unsigned)gx, (unsigned)cdiv(a.N, 32));
-  hipLaunchKernelGGL((conv3x3_patch_kernel<S, NI, TH, TW, PC, FWD>), grid, dim3(256), 0, st, a);
+  VAD_KLAUNCH((conv3x3_patch_kernel<S, NI, TH, TW, PC, FWD>), grid, dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   if (nparts) *nparts = (int)gx;
   return 0;
@@ -530,7 +530,7 @@ int conv3_patch_dgrad(const Conv3Layer& L, const float* dY, const float* wd, flo
   a.tiles_h = (int)cdiv(cdiv(L.IH, 2), 8);
   a.tiles_w = (int)cdiv(cdiv(L.IW, 2), 8);
   dim3 grid((unsigned)((int64_t)L.NF * a.tiles_h * a.tiles_w), (unsigned)cdiv(L.Ci, 32));
-  hipLaunchKernelGGL((conv3x3_dgrad_s2_kernel<32>), grid, dim3(256), 0, st, a);
+  VAD_KLAUNCH((conv3x3_dgrad_s2_kernel<32>), grid, dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -706,7 +706,7 @@ static int launch_wgrad_patch(WgradPatchArgs a, int target_blocks, int64_t parti
   int64_t z = std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, pairs), a.ntiles));
   z = std::min<int64_t>(z, std::max<int64_t>(1, partial_cap / ((int64_t)a.Co * 9 * a.Ci)));
   dim3 grid((unsigned)(a.Co / 32), (unsigned)(a.Ci / 32), (unsigned)z);
-  hipLaunchKernelGGL((conv3x3_wgrad_patch_kernel<S, NI, TH, TW, WPX>), grid, dim3(256), 0, st, a);
+  VAD_KLAUNCH((conv3x3_wgrad_patch_kernel<S, NI, TH, TW, WPX>), grid, dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   *nsplit = (int)z;
   return 0;

@@ -302,7 +302,7 @@ static int launch_x3(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   a.tpb = (int)cdiv(a.ntiles, target);
   a.dbg = g_x3_dbg;
   const int gx = (int)cdiv(a.ntiles, a.tpb);
-  hipLaunchKernelGGL((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD>), dim3(gx, ny), dim3(256), 0, st, a);
+  VAD_KLAUNCH((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD>), dim3(gx, ny), dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   if (nparts) *nparts = gx;
   return 0;
@@ -363,6 +363,278 @@ int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float*
   a.out = dX;
   a.NF = L.NF; a.IH = L.OH; a.IW = L.OW; a.C = L.Co; a.OH = L.IH; a.OW = L.IW; a.N = L.Ci;
   return dispatch_x3<1, false>(a, 1 << 20, st, nullptr);
+}
+
+// =====================================================================================================
+// Stride-1 weight gradient on the split-bf16 MFMA: dW[co][t][ci] = sum_p dY[p][co] * relu(bn(x))[p + off_t][ci].
+// GEMM view per tap: M = 32 co (A = dY^T), N = 32 ci (B = shifted input), K = output pixels.  A K step is 16
+// consecutive tile pixels; lane half h holds 8 of them, which lie in one tile row (TW % 8 == 0).  LDS holds
+//   Ys[co][plane][pixel]           (the dY tile, 3 bf16 planes, pixels contiguous)
+//   Xs[ci][plane][patch row][col]  (input patch incl. halo, BN+ReLU on load, cols padded to TW + 8)
+// so the A fragment is one b128 read per plane and, per kernel row kh, two aligned b128 reads per plane give
+// columns ox..ox+15 from which the kw = 0 / 2 fragments are dword-aligned subsets and kw = 1 is assembled with
+// v_alignbyte (a 2-byte shift): no unaligned LDS access.  Every wave owns KS K steps of each tile and all 9 tap
+// accumulators; the 4 waves are combined in a fixed order at the end ((0+2) + (1+3)), and the block's sum lands
+// in slab blockIdx.z of the [S][co][t*Ci + ci] split-K layout that conv3_wgrad_reduce consumes.
+// =====================================================================================================
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+struct WgX3Args {
+  const float* dY;     // [NF][OH][OW][Co]
+  const float* src;    // [NF][IH][IW][Ci]
+  const float* scale;  // BN+ReLU on load, nullable
+  const float* shift;
+  float* slab;         // [S][Co][9*Ci]
+  int NF, IH, IW, Ci, OH, OW, Co;
+  int tiles_h, tiles_w, ntiles;
+  int dbg;  // measurement only (knob "conv_split_dbg"): 2 no split, 4 no MFMA, 8 no global loads
+};
+
+// LDS row pitch (elements, a multiple of 8) with an odd number of 16-B units: the 16 lanes of a b128 read phase
+// hit distinct bank quads
+constexpr int odd16_pitch(int n) { return ((n / 8) & 1) ? n : n + 8; }
+
+template <int NI, int TH, int TW, bool PF>
+__global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args p) {
+  constexpr int TPX = NI * TH * TW, KS = TPX / 64;
+  static_assert(TPX % 64 == 0 && TW % 8 == 0, "whole 16-pixel K steps per wave, 8-pixel row runs");
+  constexpr int PH = TH + 2, PW = TW + 2, PWP = TW + 8, NCG = PWP / 4;
+  constexpr int PLANE = NI * PH * PWP, CIP = odd16_pitch(3 * PLANE), DYP = odd16_pitch(3 * TPX);
+  constexpr int XE = 32 * CIP, YE = 32 * DYP, RE = 2 * 3 * 16 * 64 * 2;  // RE: the combine buffer (floats x2)
+  __shared__ __attribute__((aligned(16))) __bf16 sm[(XE + YE) > RE ? (XE + YE) : RE];
+  __bf16* xs = sm;
+  __bf16* ys = sm + XE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, j = lane & 31;
+  const int co0 = blockIdx.x * 32, ci0 = blockIdx.y * 32;
+  const int tiles_per_img = p.tiles_h * p.tiles_w;
+  const int c4 = tid & 7;  // staging: this thread's 4-channel group
+
+  constexpr int XQ = NI * PH * NCG * 8, XIT = (XQ + 255) / 256;
+  constexpr int YQ = TPX / 4 * 8, YIT = (YQ + 255) / 256;
+  f32x4 xv[XIT][4], yv[YIT][4];
+  auto origin = [&](int tile, int& i0, int& y0, int& x0) {
+    i0 = (tile / tiles_per_img) * NI;
+    const int tr = tile % tiles_per_img;
+    y0 = (tr / p.tiles_w) * TH;
+    x0 = (tr % p.tiles_w) * TW;
+  };
+  auto fetch = [&](int tile) {
+    int i0, y0, x0;
+    origin(tile, i0, y0, x0);
+#pragma unroll
+    for (int it = 0; it < YIT; ++it) {
+      const int q = tid + it * 256, lin = (q >> 3) * 4;
+      const int mi = lin / (TH * TW), mr = lin % (TH * TW);
+      const int oy = y0 + mr / TW, ox = x0 + mr % TW, img = i0 + mi;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        yv[it][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!(p.dbg & 8) && q < YQ && img < p.NF && oy < p.OH && ox + e < p.OW)
+          yv[it][e] = *reinterpret_cast<const f32x4*>(p.dY + (((int64_t)img * p.OH + oy) * p.OW + ox + e) * p.Co +
+                                                      co0 + c4 * 4);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < XIT; ++it) {
+      const int q = tid + it * 256, g = q >> 3;
+      const int row = g / NCG, cg = g % NCG;
+      const int mi = row / PH, iy = y0 - 1 + row % PH, img = i0 + mi;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int px = cg * 4 + e, ix = x0 - 1 + px;
+        xv[it][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!(p.dbg & 8) && q < XQ && px < PW && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
+          xv[it][e] = *reinterpret_cast<const f32x4*>(p.src + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.Ci +
+                                                      ci0 + c4 * 4);
+      }
+    }
+  };
+  f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+  if (p.scale) {
+    sc = *reinterpret_cast<const f32x4*>(p.scale + ci0 + c4 * 4);
+    sh = *reinterpret_cast<const f32x4*>(p.shift + ci0 + c4 * 4);
+  }
+  // 4 channels x 4 consecutive pixels -> per channel and plane one 8-B LDS store
+  auto put4 = [&](__bf16* dst, int pitch, int plane_stride, const f32x4* v) {
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 hi, mid, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = v[e][cc];
+        const __bf16 a = (__bf16)x;
+        if (p.dbg & 2) {
+          hi[e] = mid[e] = lo[e] = a;
+          continue;
+        }
+        const float r = x - (float)a;
+        const __bf16 b = (__bf16)r;
+        hi[e] = a;
+        mid[e] = b;
+        lo[e] = (__bf16)(r - (float)b);
+      }
+      __bf16* d = dst + (c4 * 4 + cc) * pitch;
+      *reinterpret_cast<bf16x4*>(d) = hi;
+      *reinterpret_cast<bf16x4*>(d + plane_stride) = mid;
+      *reinterpret_cast<bf16x4*>(d + 2 * plane_stride) = lo;
+    }
+  };
+  auto stash = [&](int tile) {
+    int i0, y0, x0;
+    origin(tile, i0, y0, x0);
+#pragma unroll
+    for (int it = 0; it < YIT; ++it) {
+      const int q = tid + it * 256;
+      if (q < YQ) put4(ys + (q >> 3) * 4, DYP, TPX, yv[it]);
+    }
+#pragma unroll
+    for (int it = 0; it < XIT; ++it) {
+      const int q = tid + it * 256, g = q >> 3;
+      if (q < XQ) {
+        const int row = g / NCG, cg = g % NCG;
+        const int mi = row / PH, iy = y0 - 1 + row % PH;
+        f32x4 v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = xv[it][e];
+          const int ix = x0 - 1 + cg * 4 + e;
+          // zero padding stays zero: padded taps read 0 in the reference's zero-padded relu(bn(y))
+          if (p.scale && i0 + mi < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW && cg * 4 + e < PW) {
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) v[e][cc] = relu_nan(fmaf(v[e][cc], sc[cc], sh[cc]));
+          }
+        }
+        put4(xs + row * PWP + cg * 4, CIP, PLANE, v);
+      }
+    }
+  };
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  int tile = blockIdx.z;
+  if (PF && tile < p.ntiles) fetch(tile);
+  for (; tile < p.ntiles; tile += gridDim.z) {
+    if (!PF) fetch(tile);  // (no register prefetch: the co-resident block hides the load latency)
+    __syncthreads();  // the previous tile's fragment reads are done
+    stash(tile);
+    __syncthreads();
+    if (PF && tile + (int)gridDim.z < p.ntiles) fetch(tile + gridDim.z);
+#pragma unroll
+    for (int ks = 0; ks < ((p.dbg & 4) ? 0 : KS); ++ks) {
+      const int lin = (wave * KS + ks) * 16 + 8 * h;
+      const int mi = lin / (TH * TW), mr = lin % (TH * TW);
+      const int oy = mr / TW, ox = mr % TW;
+      bf16x8 a[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const bf16x8*>(ys + j * DYP + q * TPX + lin);
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const __bf16* xb = xs + j * CIP + (mi * PH + oy + kh) * PWP + ox;
+        // B planes smallest first: lo (x a.hi), mid (x a.mid, a.hi), hi (x a.lo, a.mid, a.hi)
+#pragma unroll
+        for (int q = 2; q >= 0; --q) {
+          const u32x4 d0 = *reinterpret_cast<const u32x4*>(xb + q * PLANE);
+          const u32x4 d1 = *reinterpret_cast<const u32x4*>(xb + q * PLANE + 8);
+          const u32x4 s1 = {__builtin_amdgcn_alignbyte(d0[1], d0[0], 2), __builtin_amdgcn_alignbyte(d0[2], d0[1], 2),
+                            __builtin_amdgcn_alignbyte(d0[3], d0[2], 2), __builtin_amdgcn_alignbyte(d1[0], d0[3], 2)};
+          const u32x4 s2 = {d0[1], d0[2], d0[3], d1[0]};
+          const bf16x8 b0 = __builtin_bit_cast(bf16x8, d0);
+          const bf16x8 b1 = __builtin_bit_cast(bf16x8, s1);
+          const bf16x8 b2 = __builtin_bit_cast(bf16x8, s2);
+#pragma unroll
+          for (int qa = 2 - q; qa >= 0; --qa) {
+            acc[kh * 3 + 0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[qa], b0, acc[kh * 3 + 0], 0, 0, 0);
+            acc[kh * 3 + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[qa], b1, acc[kh * 3 + 1], 0, 0, 0);
+            acc[kh * 3 + 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[qa], b2, acc[kh * 3 + 2], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+
+  // fixed-order combine of the 4 waves, 3 taps at a time: (2,3) -> (0,1), then 1 -> 0
+  float* red = reinterpret_cast<float*>(sm);
+  float* out = p.slab + (int64_t)blockIdx.z * p.Co * 9 * p.Ci;
+#pragma unroll
+  for (int tc = 0; tc < 3; ++tc) {
+    __syncthreads();
+    if (wave >= 2) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(((wave - 2) * 3 + u) * 16 + r) * 64 + lane] = acc[tc * 3 + u][r];
+    }
+    __syncthreads();
+    if (wave < 2) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[tc * 3 + u][r] += red[((wave * 3 + u) * 16 + r) * 64 + lane];
+    }
+    __syncthreads();
+    if (wave == 1) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(u * 16 + r) * 64 + lane] = acc[tc * 3 + u][r];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * h, t = tc * 3 + u;
+          out[(int64_t)co * 9 * p.Ci + t * p.Ci + ci0 + j] = acc[t][r] + red[(u * 16 + r) * 64 + lane];
+        }
+    }
+  }
+}
+
+template <int NI, int TH, int TW, bool PF = false>
+static int launch_wgrad_x3(WgX3Args a, int target_blocks, int64_t partial_cap, hipStream_t st, int* nsplit) {
+  a.tiles_h = (int)cdiv(a.OH, TH);
+  a.tiles_w = (int)cdiv(a.OW, TW);
+  a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);
+  const int pairs = (a.Co / 32) * (a.Ci / 32);
+  int64_t z = std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, pairs), a.ntiles));
+  z = std::min<int64_t>(z, std::max<int64_t>(1, partial_cap / ((int64_t)a.Co * 9 * a.Ci)));
+  dim3 grid((unsigned)(a.Co / 32), (unsigned)(a.Ci / 32), (unsigned)z);
+  VAD_KLAUNCH((conv3x3_wgrad_x3_kernel<NI, TH, TW, PF>), grid, dim3(256), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  *nsplit = (int)z;
+  return 0;
+}
+
+int g_wgrad_split = 1;  // tuning knob "conv_wgrad_split": stride-1 weight gradients on the split-bf16 kernel
+
+bool conv3_wgrad_x3_supported(const Conv3Layer& L) {
+  // (8x8 frames: 64-pixel tiles carry too little MFMA work per staged patch; the f32 patch kernel is faster there)
+  return g_conv_split && g_wgrad_split && L.stride == 1 && L.Ci % 32 == 0 && L.Co % 32 == 0 &&
+         (L.OH > 8 || L.OW > 8 || g_wgrad_split == 2);
+}
+
+int conv3_wgrad_x3(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
+                   int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st) {
+  VAD_CHECK(conv3_wgrad_x3_supported(L), "conv3_wgrad_x3: stride 1, Ci and Co multiples of 32");
+  VAD_CHECK(partial_cap >= (int64_t)L.Co * 9 * L.Ci, "conv3_wgrad_x3: slab capacity below one split");
+  WgX3Args a{};
+  a.dY = dY;
+  a.src = src;
+  a.scale = src_stats ? src_stats + 2 * L.Ci : nullptr;
+  a.shift = src_stats ? src_stats + 3 * L.Ci : nullptr;
+  a.slab = slab;
+  a.NF = L.NF; a.IH = L.IH; a.IW = L.IW; a.Ci = L.Ci; a.OH = L.OH; a.OW = L.OW; a.Co = L.Co;
+  a.dbg = g_x3_dbg;
+  if (L.OH <= 8 && L.OW <= 8) return launch_wgrad_x3<1, 8, 8>(a, target_blocks, partial_cap, st, nsplit);
+  if (L.OW <= 16) return launch_wgrad_x3<1, 8, 16>(a, target_blocks, partial_cap, st, nsplit);
+  return launch_wgrad_x3<1, 4, 32>(a, target_blocks, partial_cap, st, nsplit);
 }
 
 }  // namespace vad

@@ -174,10 +174,12 @@ class CadEngine:
         nat.check(nat.lib().vad_cad_backward(pl.h, 1 if use_loss else 0, *[nat.ptr(t) for t in c],
                                              nat.stream_of(self.device)))
 
-    def profile(self, enable: bool, only_prefix: str = ""):
-        """HIP-event timing of the plan's labelled launches (all plans of this engine)."""
+    def profile(self, enable: bool, only_prefix: str = "", reset: bool = True):
+        """HIP-event timing of the plan's labelled launches (all plans of this engine).  enable=False pauses (the
+        records are kept); enable=True clears them first unless reset=False."""
+        code = (1 if reset else 2) if enable else 0
         for pl in self.plans.values():
-            nat.check(nat.lib().vad_cad_profile(pl.h, 1 if enable else 0, only_prefix.encode()))
+            nat.check(nat.lib().vad_cad_profile(pl.h, code, only_prefix.encode()))
 
     def profile_read(self, shape=None) -> dict:
         """{label: (total_ms, launches)} recorded since profile(True) (synchronises the stream)."""

@@ -200,7 +200,9 @@ int vad_cad_debug_buffer(vad_cad_plan* plan, const char* name, int idx, void** p
 int vad_cad_set_debug(vad_cad_plan* plan, const char* key, int64_t value);  /* "stop_layer" */
 int vad_debug_d2h(void* host, const void* dev, int64_t bytes);
 /* HIP-event timing of labelled launches (conv_fwd/L<l>, conv_wgrad/L<l>, conv_dgrad/L<l>, bn_bwd_*, conv1,
- * det_fwd, head_fwd, optimizer, ...).  enable=0 turns it off; only_prefix restricts the labels recorded. */
+ * det_fwd, head_fwd, optimizer, ...).  enable: 0 pauses (records kept), 1 clears the records and starts, 2 starts
+ * appending.  only_prefix restricts the labels recorded; with a non-empty prefix the labelled conv kernels are
+ * dispatched with their own start/stop events (hipExtLaunchKernel) instead of event records around the launch. */
 int vad_cad_profile(vad_cad_plan* plan, int enable, const char* only_prefix);
 int vad_cad_profile_read(vad_cad_plan* plan, char* labels, double* total_ms, int* counts, int cap);
 

@@ -157,11 +157,18 @@ WGRAD_CASES = [(2, 32, 32, 19, 17, 1), (32, 256, 256, 8, 8, 1), (32, 128, 256, 1
                (3, 32, 64, 57, 57, 2), (5, 64, 64, 8, 8, 1), (3, 128, 256, 15, 15, 2), (2, 32, 32, 5, 3, 1)]
 
 
-@pytest.mark.parametrize("patch", [1, 0, 2])
+def _wgrad_path(nat, patch):
+    """3: split-bf16 kernel for stride-1 layers (default), 1: f32 LDS-patch kernel for stride-1 layers,
+    2: f32 LDS-patch kernel for all strides, 0: implicit-GEMM path."""
+    nat.lib().vad_set_tuning(b"conv_wgrad_patch", 1 if patch == 3 else patch)
+    nat.lib().vad_set_tuning(b"conv_wgrad_split", 1 if patch == 3 else 0)
+
+
+@pytest.mark.parametrize("patch", [3, 1, 0, 2])
 @pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", WGRAD_CASES)
 def test_conv3x3_wgrad(NF, Ci, Co, IH, IW, s, patch):
     nat = _lib()
-    nat.lib().vad_set_tuning(b"conv_wgrad_patch", patch)
+    _wgrad_path(nat, patch)
     g = torch.Generator().manual_seed(NF * 5 + Ci + Co + IH)
     x = torch.randn(NF, Ci, IH, IW, generator=g)
     w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
@@ -177,6 +184,34 @@ def test_conv3x3_wgrad(NF, Ci, Co, IH, IW, s, patch):
     nat.check(nat.lib().vad_conv3x3_wgrad(xh.data_ptr(), dyh.data_ptr(), NF, Ci, IH, IW, Co, s, dW.data_ptr(),
                                           part.data_ptr(), part.numel(), nat.stream_of(d)))
     torch.cuda.synchronize()
-    nat.lib().vad_set_tuning(b"conv_wgrad_patch", 1)
+    _wgrad_path(nat, 3)
     ref = wr.grad
     np.testing.assert_allclose(dW.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4 * float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("NF,Ci,Co,IH,IW", [(8, 32, 32, 57, 57), (4, 64, 64, 29, 29), (16, 256, 256, 8, 8),
+                                            (6, 128, 128, 15, 15)])
+def test_conv3x3_wgrad_split_accuracy_matches_f32(NF, Ci, Co, IH, IW):
+    """Split-bf16 weight gradient against an fp64 reference: worst error relative to sum_p |dy||x| of each weight
+    within 2x that of the exact-f32 MFMA patch kernel (a plain bf16 product would sit near 4e-3)."""
+    nat = _lib()
+    g = torch.Generator().manual_seed(11 + Ci + IH)
+    x = torch.randn(NF, Ci, IH, IW, generator=g)
+    dy = torch.randn(NF, Co, IH, IW, generator=g)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (Co, Ci, 3, 3), dy.double(), stride=1, padding=1)
+    mag = torch.nn.grad.conv2d_weight(x.double().abs(), (Co, Ci, 3, 3), dy.double().abs(), stride=1, padding=1)
+    d = torch.device("cuda")
+    xh = x.permute(0, 2, 3, 1).contiguous().to(d)
+    dyh = dy.permute(0, 2, 3, 1).contiguous().to(d)
+    part = torch.empty(1 << 24, device=d)
+    errs = {}
+    for patch in (1, 3):
+        _wgrad_path(nat, patch)
+        dW = torch.empty(Co, Ci, 3, 3, device=d)
+        nat.check(nat.lib().vad_conv3x3_wgrad(xh.data_ptr(), dyh.data_ptr(), NF, Ci, IH, IW, Co, 1, dW.data_ptr(),
+                                              part.data_ptr(), part.numel(), nat.stream_of(d)))
+        torch.cuda.synchronize()
+        errs[patch] = float(((dW.cpu().double() - ref).abs() / mag).max())
+    _wgrad_path(nat, 3)
+    assert errs[3] < 1e-6, errs
+    assert errs[3] <= 2.0 * errs[1] + 1e-8, errs

@@ -1,0 +1,8 @@
+# GPU tests, bench line, then a kernel-trace pass of a short bench run
+set -o pipefail
+mkdir -p gpurun_out
+ROOT=$(pwd)
+timeout -k 10 500 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gt.log 2>&1 && \
+timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench.log 2>&1 && \
+cd /tmp && export TMPDIR=/tmp && \
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $ROOT/gpurun_out/tr -o run -- python3 $ROOT/bench.py --no-cpu-baseline --steps 5 --warmup 2 > $ROOT/gpurun_out/tr_bench.log 2>&1
