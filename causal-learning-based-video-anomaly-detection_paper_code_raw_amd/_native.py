@@ -46,6 +46,8 @@ _SIGS = {
     "vad_conv3x3_dgrad": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, _P]),
     "vad_cad_debug_buffer": (_I, [_P, ctypes.c_char_p, _I, ctypes.POINTER(_P), ctypes.POINTER(_I64)]),
     "vad_cad_set_debug": (_I, [_P, ctypes.c_char_p, _I64]),
+    "vad_cad_set_option": (_I, [_P, ctypes.c_char_p, _I64]),
+    "vad_cad_conv_path": (_I, [_P, _I, _I]),
     "vad_debug_d2h": (_I, [_P, _P, _I64]),
     "vad_cad_profile": (_I, [_P, _I, ctypes.c_char_p]),
     "vad_cad_profile_read": (_I, [_P, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I), _I]),

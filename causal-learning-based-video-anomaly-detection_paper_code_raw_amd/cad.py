@@ -187,7 +187,19 @@ class CausalAnomalyDetector(nn.Module):
     def engine(self) -> _eng.CadEngine:
         eng = _eng.engine_for(self)
         eng.model_param_shapes = [p.shape for p in self.parameters()]
+        dt = getattr(self, "_compute_dtype", torch.float32)
+        if eng.compute_dtype != dt:
+            eng.compute_dtype = dt
         return eng
+
+    def set_compute_dtype(self, dtype):
+        """torch.float32 (default, fp32 numerics) or torch.bfloat16: the backbone's 3x3 convs take bf16 operands
+        with fp32 accumulation (BASELINE config 4); BN, heads, losses and AdamW stay fp32.  An extension of the
+        reference surface (which runs fp32 on CPU and fp16 autocast on CUDA, cad:644-668)."""
+        if dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"compute dtype must be torch.float32 or torch.bfloat16, got {dtype}")
+        self._compute_dtype = dtype
+        return self
 
     def forward(self, video_frames, *, seed=None, step=0, clip0=0):
         """video_frames: (B, T, 1, H, W) on a HIP device.  Returns the reference's output dict."""

@@ -57,6 +57,14 @@ int conv3_patch_dgrad(const Conv3Layer& L, const float* dY, const float* wd, flo
 extern int g_conv_split;  // 0 disables them (f32 MFMA patch kernels)
 extern int g_x3_nt;       // output channels per block: 0 auto, 1 -> 32, 2 -> 64
 extern int g_x3_dbg;      // measurement-only bits (X3Args::dbg)
+// bf16-operand mode of the split kernels (one plane, one bf16 product per K step, fp32 accumulation): BASELINE
+// config 4's bf16 compute.  Thread-local, set for the duration of a plan call by ConvPrecision.
+extern thread_local int g_conv_bf16;
+struct ConvPrecision {
+  int saved;
+  explicit ConvPrecision(int bf16) : saved(g_conv_bf16) { g_conv_bf16 = bf16; }
+  ~ConvPrecision() { g_conv_bf16 = saved; }
+};
 bool conv3_x3_supported(const Conv3Layer& L, bool fwd);
 int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
                  float* y, float* partials, int* nparts, hipStream_t st);
@@ -68,6 +76,9 @@ int conv3_wgrad_x3(const Conv3Layer& L, const float* dY, const float* src, const
 bool conv3_wgrad_patch_supported(const Conv3Layer& L);
 int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
                       int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);
+// which kernel family conv3_fwd (kind 0) / conv3_dgrad (1) / conv3_wgrad (2) dispatches to for this layer under the
+// current knobs: 6 = split-bf16 (six bf16 products per K step), 1 = bf16 operands, 0 = f32 MFMA kernels
+int conv3_path(const Conv3Layer& L, int kind);
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
                 int* nsplit, int64_t partial_cap, hipStream_t st);
 int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, const float* bias_partials,

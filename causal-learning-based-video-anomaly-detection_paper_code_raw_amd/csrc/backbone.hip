@@ -698,6 +698,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_split_dbg") g_x3_dbg = value;
   else if (k == "conv_wgrad_patch") g_tune.wgrad_patch = value;
   else if (k == "conv_wgrad_split") g_wgrad_split = value;
+  else if (k == "conv_bf16") g_conv_bf16 = value;  // ops API only (calling thread); plans use their own option
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else {
     set_error("unknown tuning key " + k);
@@ -927,6 +928,18 @@ int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX
     off += (int64_t)taps.ntaps * L.Ci * L.Co;
   }
   return 0;
+}
+
+int conv3_path(const Conv3Layer& L, int kind) {
+  bool x3 = false;
+  if (kind == 0)
+    x3 = g_tune.patch && conv3_patch_blocks(L.NF, L.OH, L.OW) <= cdiv((int64_t)L.NF * L.OH * L.OW, 64) &&
+         conv3_x3_supported(L, true);
+  else if (kind == 1)
+    x3 = g_tune.patch && conv3_x3_supported(L, false);
+  else
+    x3 = g_tune.wgrad_patch && conv3_wgrad_x3_supported(L);
+  return x3 ? (g_conv_bf16 ? 1 : 6) : 0;
 }
 
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,

@@ -518,7 +518,10 @@ struct CadPlanImpl {
     return a;
   }
 
+  int conv_bf16 = 0;  // option "conv_bf16": 3x3 convs on bf16 operands (BASELINE config 4)
+
   int forward(const float* x, hipStream_t st) {
+    ConvPrecision prec(conv_bf16);
     const CadLayout& LY = layout();
     {
       const float* w8[8];
@@ -562,11 +565,11 @@ struct CadPlanImpl {
     }
     TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
     TailArgs t = tail_args(nullptr, nullptr, nullptr, nullptr);
-    TIMED("tail", cad_tail_fwd(t, st));
-    if (training && nbt) {
-      hipLaunchKernelGGL(nbt_bump_kernel, dim3(1), dim3(64), 0, st, nbt, 9);
-      VAD_LAUNCH_CHECK();
+    if (training && nbt) {  // num_batches_tracked of the 9 BN layers (bumped by the tail kernel)
+      t.nbt = nbt;
+      t.nbt_n = 9;
     }
+    TIMED("tail", cad_tail_fwd(t, st));
     return 0;
   }
 
@@ -596,6 +599,7 @@ struct CadPlanImpl {
 
   int backward(bool use_loss, const float* dfin, const float* dprobs, const float* dcaus, const float* dkl,
                const float* dz, const float* dadj, hipStream_t st) {
+    ConvPrecision prec(conv_bf16);
     const CadLayout& LY = layout();
     VAD_CHECK(grads != nullptr, "backward: grads not bound");
     VAD_CHECK(!use_loss || labels != nullptr, "backward(use_loss): forward ran without labels");
@@ -873,6 +877,22 @@ int vad_cad_set_debug(vad_cad_plan* plan, const char* key, int64_t value) {
   if (std::string(key) == "stop_layer") plan->impl.debug_stop_layer = (int)value;
   else { vad::set_error("vad_cad_set_debug: unknown key"); return 1; }
   return 0;
+}
+
+int vad_cad_set_option(vad_cad_plan* plan, const char* key, int64_t value) {
+  VAD_CHECK(plan && key, "vad_cad_set_option: null argument");
+  if (std::string(key) == "conv_bf16") plan->impl.conv_bf16 = value ? 1 : 0;
+  else { vad::set_error("vad_cad_set_option: unknown key"); return 1; }
+  return 0;
+}
+
+int vad_cad_conv_path(vad_cad_plan* plan, int layer, int kind) {
+  if (!plan || layer < 0 || layer >= 8 || kind < 0 || kind > 2) {
+    vad::set_error("vad_cad_conv_path: bad argument");
+    return -1;
+  }
+  ConvPrecision prec(plan->impl.conv_bf16);
+  return conv3_path(plan->impl.L[layer], kind);
 }
 
 int vad_cad_profile(vad_cad_plan* plan, int enable, const char* only_prefix) {

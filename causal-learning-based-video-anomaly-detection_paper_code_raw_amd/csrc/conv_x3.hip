@@ -59,15 +59,33 @@ __device__ __forceinline__ f32x16 mfma_x3(const bf16x8* a, const bf16x8* b, f32x
   return c;
 }
 
-template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD>
+// stores 8 fp32 values as NP bf16 planes (hi[, mid, lo]) at d, d + pitch, d + 2 pitch
+template <int NP>
+__device__ __forceinline__ void put_planes(__bf16* d, int pitch, const float* v, bool hi_only) {
+  bf16x8 hi, mid, lo;
+  if (NP == 1 || hi_only) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) hi[e] = mid[e] = lo[e] = (__bf16)v[e];
+  } else {
+    split3(v, hi, mid, lo);
+  }
+  *reinterpret_cast<bf16x8*>(d) = hi;
+  if constexpr (NP == 3) {
+    *reinterpret_cast<bf16x8*>(d + pitch) = mid;
+    *reinterpret_cast<bf16x8*>(d + 2 * pitch) = lo;
+  }
+}
+
+template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP>
 __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
+  static_assert(NP == 3 || NP == 1, "three split planes (fp32 numerics) or one (bf16 operands)");
   static_assert(NI * TH * TW == 128, "a block owns 128 output pixels");
   static_assert(FWD || S == 1, "stride-2 input gradients use conv3x3_dgrad_s2_kernel");
   static_assert(PC % 16 == 0, "16-deep K steps");
   constexpr int NC = 32 * NT, G8 = PC / 8;
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3, PROWS = NI * PH * PW, PWE = (PW + 1) / 2;
-  constexpr int RP = 3 * PC + 8;   // patch row: 3 planes x PC + 16 B pad (odd number of 16-B units)
-  constexpr int WP = 27 * PC + 8;  // weight row: 9 taps x 3 planes x PC + pad
+  constexpr int RP = NP * PC + 8;      // patch row: NP planes x PC + 16 B pad (odd number of 16-B units)
+  constexpr int WP = 9 * NP * PC + 8;  // weight row: 9 taps x NP planes x PC + pad
   static_assert(((RP * 2 / 16) & 1) && ((WP * 2 / 16) & 1), "odd 16-B row pitch");
   __shared__ __attribute__((aligned(16))) __bf16 sm[PROWS * RP + NC * WP];
   __bf16* patch = sm;
@@ -163,17 +181,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
           }
         }
         const int col = S == 1 ? rx : ((rx & 1) ? PWE + (rx >> 1) : (rx >> 1));
-        bf16x8 hi, mid, lo;
-        if (p.dbg & 2) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) hi[e] = mid[e] = lo[e] = (__bf16)v[e];
-        } else {
-          split3(v, hi, mid, lo);
-        }
         __bf16* d = patch + ((im * PH + ry) * PW + col) * RP + g8 * 8;
-        *reinterpret_cast<bf16x8*>(d) = hi;
-        *reinterpret_cast<bf16x8*>(d + PC) = mid;
-        *reinterpret_cast<bf16x8*>(d + 2 * PC) = lo;
+        put_planes<NP>(d, PC, v, p.dbg & 2);
       }
     }
     if (weights) {
@@ -188,12 +197,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
             v[e] = wv[it][0][e];
             v[4 + e] = wv[it][1][e];
           }
-          bf16x8 hi, mid, lo;
-          split3(v, hi, mid, lo);
-          __bf16* d = wl + n * WP + t * 3 * PC + g8 * 8;
-          *reinterpret_cast<bf16x8*>(d) = hi;
-          *reinterpret_cast<bf16x8*>(d + PC) = mid;
-          *reinterpret_cast<bf16x8*>(d + 2 * PC) = lo;
+          put_planes<NP>(wl + n * WP + t * NP * PC + g8 * 8, PC, v, false);
         }
       }
     }
@@ -232,16 +236,19 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
       const __bf16* ap = patch + (arow0 + kh * PW + col) * RP + 8 * h;
 #pragma unroll
       for (int kk = 0; kk < PC / 16; ++kk) {
-        bf16x8 a[3], b[NT][3];
+        bf16x8 a[NP], b[NT][NP];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const bf16x8*>(ap + q * PC + kk * 16);
+        for (int q = 0; q < NP; ++q) a[q] = *reinterpret_cast<const bf16x8*>(ap + q * PC + kk * 16);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-          for (int q = 0; q < 3; ++q)
-            b[nt][q] = *reinterpret_cast<const bf16x8*>(bbase + nt * 32 * WP + (t * 3 + q) * PC + kk * 16);
+          for (int q = 0; q < NP; ++q)
+            b[nt][q] = *reinterpret_cast<const bf16x8*>(bbase + nt * 32 * WP + (t * NP + q) * PC + kk * 16);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma_x3(a, b[nt], acc[nt]);
+        for (int nt = 0; nt < NT; ++nt) {
+          if constexpr (NP == 3) acc[nt] = mfma_x3(a, b[nt], acc[nt]);
+          else acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[nt][0], acc[nt], 0, 0, 0);
+        }
       }
     }
     if (ch == nch - 1) {
@@ -292,8 +299,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
   }
 }
 
-template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD>
-static int launch_x3(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
+template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP>
+static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   a.tiles_h = (int)cdiv(a.OH, TH);
   a.tiles_w = (int)cdiv(a.OW, TW);
   a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);
@@ -302,15 +309,23 @@ static int launch_x3(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   a.tpb = (int)cdiv(a.ntiles, target);
   a.dbg = g_x3_dbg;
   const int gx = (int)cdiv(a.ntiles, a.tpb);
-  VAD_KLAUNCH((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD>), dim3(gx, ny), dim3(256), 0, st, a);
+  VAD_KLAUNCH((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD, NP>), dim3(gx, ny), dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   if (nparts) *nparts = gx;
   return 0;
 }
 
 int g_conv_split = 1;  // tuning knob "conv_split": 1 = split-bf16 patch kernels where supported, 0 = f32 MFMA
+thread_local int g_conv_bf16 = 0;  // bf16-operand convs (one plane, one product; set per plan, see ConvPrecision)
 int g_x3_nt = 0;       // tuning knob "conv_split_nt": 0 = auto, 1 / 2 = force 32 / 64 output channels per block
 int g_x3_dbg = 0;      // knob "conv_split_dbg" (measurement only, see X3Args::dbg)
+
+template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD>
+static int launch_x3(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
+  if (g_conv_bf16) return launch_np<S, NI, TH, TW, NT, PC, FWD, 1>(a, max_blocks, st, nparts);
+  return launch_np<S, NI, TH, TW, NT, PC, FWD, 3>(a, max_blocks, st, nparts);
+}
+
 
 template <int S, bool FWD, int NT>
 static int dispatch_x3_nt(const X3Args& a, int max_blocks, hipStream_t st, int* nparts) {
@@ -326,7 +341,8 @@ static int dispatch_x3(const X3Args& a, int max_blocks, hipStream_t st, int* npa
   if (nt == 0) {
     // 64 channels per block halves the fragment reads per MFMA; keep 32 when that would leave the chip underfull
     const int64_t tiles = conv3_patch_blocks(a.NF, a.OH, a.OW);
-    nt = (a.N % 64 == 0 && tiles * (a.N / 64) >= 512) ? 2 : 1;
+    // (stride 2: the 4x larger input patch per tile makes sharing it over 64 channels pay even on a small grid)
+    nt = (a.N % 64 == 0 && (S == 2 || tiles * (a.N / 64) >= 512)) ? 2 : 1;
   }
   return nt == 2 ? dispatch_x3_nt<S, FWD, 2>(a, max_blocks, st, nparts)
                  : dispatch_x3_nt<S, FWD, 1>(a, max_blocks, st, nparts);
@@ -394,12 +410,12 @@ struct WgX3Args {
 // hit distinct bank quads
 constexpr int odd16_pitch(int n) { return ((n / 8) & 1) ? n : n + 8; }
 
-template <int NI, int TH, int TW, bool PF>
+template <int NI, int TH, int TW, bool PF, int NP>
 __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args p) {
   constexpr int TPX = NI * TH * TW, KS = TPX / 64;
   static_assert(TPX % 64 == 0 && TW % 8 == 0, "whole 16-pixel K steps per wave, 8-pixel row runs");
   constexpr int PH = TH + 2, PW = TW + 2, PWP = TW + 8, NCG = PWP / 4;
-  constexpr int PLANE = NI * PH * PWP, CIP = odd16_pitch(3 * PLANE), DYP = odd16_pitch(3 * TPX);
+  constexpr int PLANE = NI * PH * PWP, CIP = odd16_pitch(NP * PLANE), DYP = odd16_pitch(NP * TPX);
   constexpr int XE = 32 * CIP, YE = 32 * DYP, RE = 2 * 3 * 16 * 64 * 2;  // RE: the combine buffer (floats x2)
   __shared__ __attribute__((aligned(16))) __bf16 sm[(XE + YE) > RE ? (XE + YE) : RE];
   __bf16* xs = sm;
@@ -465,7 +481,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
       for (int e = 0; e < 4; ++e) {
         const float x = v[e][cc];
         const __bf16 a = (__bf16)x;
-        if (p.dbg & 2) {
+        if (NP == 1 || (p.dbg & 2)) {
           hi[e] = mid[e] = lo[e] = a;
           continue;
         }
@@ -477,8 +493,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
       }
       __bf16* d = dst + (c4 * 4 + cc) * pitch;
       *reinterpret_cast<bf16x4*>(d) = hi;
-      *reinterpret_cast<bf16x4*>(d + plane_stride) = mid;
-      *reinterpret_cast<bf16x4*>(d + 2 * plane_stride) = lo;
+      if constexpr (NP == 3) {
+        *reinterpret_cast<bf16x4*>(d + plane_stride) = mid;
+        *reinterpret_cast<bf16x4*>(d + 2 * plane_stride) = lo;
+      }
     }
   };
   auto stash = [&](int tile) {
@@ -530,15 +548,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
       const int lin = (wave * KS + ks) * 16 + 8 * h;
       const int mi = lin / (TH * TW), mr = lin % (TH * TW);
       const int oy = mr / TW, ox = mr % TW;
-      bf16x8 a[3];
+      bf16x8 a[NP];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const bf16x8*>(ys + j * DYP + q * TPX + lin);
+      for (int q = 0; q < NP; ++q) a[q] = *reinterpret_cast<const bf16x8*>(ys + j * DYP + q * TPX + lin);
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
         const __bf16* xb = xs + j * CIP + (mi * PH + oy + kh) * PWP + ox;
         // B planes smallest first: lo (x a.hi), mid (x a.mid, a.hi), hi (x a.lo, a.mid, a.hi)
 #pragma unroll
-        for (int q = 2; q >= 0; --q) {
+        for (int q = NP - 1; q >= 0; --q) {
           const u32x4 d0 = *reinterpret_cast<const u32x4*>(xb + q * PLANE);
           const u32x4 d1 = *reinterpret_cast<const u32x4*>(xb + q * PLANE + 8);
           const u32x4 s1 = {__builtin_amdgcn_alignbyte(d0[1], d0[0], 2), __builtin_amdgcn_alignbyte(d0[2], d0[1], 2),
@@ -548,7 +566,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
           const bf16x8 b1 = __builtin_bit_cast(bf16x8, s1);
           const bf16x8 b2 = __builtin_bit_cast(bf16x8, s2);
 #pragma unroll
-          for (int qa = 2 - q; qa >= 0; --qa) {
+          for (int qa = NP - 1 - q; qa >= 0; --qa) {
             acc[kh * 3 + 0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[qa], b0, acc[kh * 3 + 0], 0, 0, 0);
             acc[kh * 3 + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[qa], b1, acc[kh * 3 + 1], 0, 0, 0);
             acc[kh * 3 + 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[qa], b2, acc[kh * 3 + 2], 0, 0, 0);
@@ -606,7 +624,8 @@ static int launch_wgrad_x3(WgX3Args a, int target_blocks, int64_t partial_cap, h
   int64_t z = std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, pairs), a.ntiles));
   z = std::min<int64_t>(z, std::max<int64_t>(1, partial_cap / ((int64_t)a.Co * 9 * a.Ci)));
   dim3 grid((unsigned)(a.Co / 32), (unsigned)(a.Ci / 32), (unsigned)z);
-  VAD_KLAUNCH((conv3x3_wgrad_x3_kernel<NI, TH, TW, PF>), grid, dim3(256), 0, st, a);
+  if (g_conv_bf16) VAD_KLAUNCH((conv3x3_wgrad_x3_kernel<NI, TH, TW, PF, 1>), grid, dim3(256), 0, st, a);
+  else VAD_KLAUNCH((conv3x3_wgrad_x3_kernel<NI, TH, TW, PF, 3>), grid, dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   *nsplit = (int)z;
   return 0;
@@ -617,7 +636,7 @@ int g_wgrad_split = 1;  // tuning knob "conv_wgrad_split": stride-1 weight gradi
 bool conv3_wgrad_x3_supported(const Conv3Layer& L) {
   // (8x8 frames: 64-pixel tiles carry too little MFMA work per staged patch; the f32 patch kernel is faster there)
   return g_conv_split && g_wgrad_split && L.stride == 1 && L.Ci % 32 == 0 && L.Co % 32 == 0 &&
-         (L.OH > 8 || L.OW > 8 || g_wgrad_split == 2);
+         (L.OH > 8 || L.OW > 8 || g_wgrad_split == 2 || g_conv_bf16);
 }
 
 int conv3_wgrad_x3(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,

@@ -97,6 +97,8 @@ struct TailArgs {
   float* d_causal;              // [B]
   float* d_kl;                  // [B]
   float* d_direct_logits;       // [B][2]
+  int64_t* nbt;                 // forward: BN num_batches_tracked counters bumped (train mode) or null
+  int nbt_n;
 };
 int cad_tail_fwd(const TailArgs& t, hipStream_t st);
 int cad_tail_bwd(const TailArgs& t, hipStream_t st);

@@ -860,6 +860,7 @@ int head_rows_wgrad(const HeadArgs& a, hipStream_t st) {
 // ================================================================== tail: softmax, blend, losses
 __global__ void cad_tail_fwd_kernel(TailArgs t) {
   const int B = t.B;
+  if (t.nbt && (int)threadIdx.x < t.nbt_n) t.nbt[threadIdx.x] += 1;
   __shared__ float red[4][256];
   float cls = 0.f, an = 0.f, ca = 0.f, kl = 0.f;
   int fdet = 0, fst = 0;

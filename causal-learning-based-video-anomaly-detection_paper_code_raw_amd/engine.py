@@ -27,6 +27,7 @@ class _Plan:
         h = ctypes.c_void_p()
         nat.check(L.vad_cad_create(B, T, H, W, ctypes.byref(h)))
         self.h = h
+        nat.check(L.vad_cad_set_option(h, b"conv_bf16", 1 if engine.compute_dtype == torch.bfloat16 else 0))
         self.shape = (B, T, H, W)
         nbytes = L.vad_cad_workspace_bytes(h)
         self.ws = torch.empty(int(nbytes) + 256, dtype=torch.uint8, device=engine.device)
@@ -97,12 +98,27 @@ class CadEngine:
                 self.nbt[i].copy_(named_bufs[k].reshape(()))
                 _set_buffer(model, k, self.nbt[i])
         self.exp_avg = self.exp_avg_sq = self.steps = None
+        self._compute_dtype = torch.float32
         self.plans = {}
         self.generation = 0
         self._last = None
         self._loss_buf = None
 
     # ------------------------------------------------------------------ bookkeeping
+    @property
+    def compute_dtype(self):
+        """torch.float32 (default: fp32 numerics) or torch.bfloat16 (backbone 3x3 convs on bf16 operands with fp32
+        accumulation, BASELINE config 4; everything else stays fp32)."""
+        return self._compute_dtype
+
+    @compute_dtype.setter
+    def compute_dtype(self, dt):
+        if dt not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"compute_dtype must be torch.float32 or torch.bfloat16, got {dt}")
+        self._compute_dtype = dt
+        for p in self.plans.values():
+            nat.check(nat.lib().vad_cad_set_option(p.h, b"conv_bf16", 1 if dt == torch.bfloat16 else 0))
+
     def is_bound(self) -> bool:
         p = next(self.model.parameters())
         return p.data_ptr() == self.params.data_ptr() and p.device == self.device

@@ -34,8 +34,10 @@ class CadTrainer:
     """
 
     def __init__(self, model, lr=3e-4, weight_decay=1e-5, eps=1e-8, betas=(0.9, 0.999), max_norm=1.0, seed=0,
-                 process_group=None, engine=None):
+                 process_group=None, engine=None, compute_dtype=None):
         self.model = model
+        if compute_dtype is not None:
+            model.set_compute_dtype(compute_dtype)
         self.eng = engine if engine is not None else model.engine()
         self.lr, self.wd, self.eps, self.betas, self.max_norm = lr, weight_decay, eps, betas, max_norm
         self.seed = seed

@@ -192,6 +192,15 @@ int vad_bbox_bind(vad_bbox_plan* plan, void* workspace, const float* params);
 /* scores (B,), adj (B,16,16), features (B,1024, nullable) */
 int vad_bbox_forward(vad_bbox_plan* plan, const float* x, float* scores, float* adj, float* features, void* stream);
 
+/* Plan options.  "conv_bf16" (0/1): the 3x3 convs of the backbone run on bf16 operands with fp32 accumulation
+ * (BASELINE config 4's bf16 compute; BN, pooling, heads, losses and the optimizer stay fp32).  Default 0: fp32
+ * numerics (split-bf16 products). */
+int vad_cad_set_option(vad_cad_plan* plan, const char* key, int64_t value);
+/* Kernel family of backbone 3x3 conv `layer` (0..7) for kind 0 forward / 1 input gradient / 2 weight gradient:
+ * 6 = split-bf16 (fp32 numerics, six bf16 MFMA products per K step), 1 = bf16 operands, 0 = f32 MFMA; -1 on error.
+ * (bench.py prices each launch against the peak of the instruction mix it runs.) */
+int vad_cad_conv_path(vad_cad_plan* plan, int layer, int kind);
+
 /* ------------------------------------------------------------------------------------------
  * Debug introspection (tests only): internal plan buffers, partial backward, device->host copy
  * names: y1, pool, y[0..7], stats[0..8], feats, pooled, dA, dY, d_pooled, d_feat_det, det_logits

@@ -193,3 +193,37 @@ def test_hip_backward_matches_oracle_full_size():
         mine = gr[eng.slot_offset[i]:eng.slot_offset[i] + eng.slot_numel[i]].astype(np.float64)
         rel = np.linalg.norm(mine - r) / max(np.linalg.norm(r), 1e-30)
         assert rel < 3e-2, f"{n}: relative L2 error {rel:.3g}"
+
+
+@pytest.mark.parametrize("B,T,H,W", [(2, 32, 256, 256)])
+def test_config4_shape_fp32_and_bf16(B, T, H, W):
+    """BASELINE config 4 shape (T=32, 256x256; 2 clips per rank here to bound the oracle's CPU time).
+    fp32 mode: scores / loss within the north-star 1e-4 of the CPU oracle.  bf16 mode (conv_bf16: the 3x3 convs
+    on bf16 operands, fp32 accumulation, everything else fp32): the outputs move by bf16 rounding of the conv
+    operands only -- scores and probabilities (bounded in [0, 1]) within 2e-2 absolute, the total loss within 2e-2
+    relative, the global gradient norm within 5 % (tolerance stated for bf16 compute: unit roundoff 2^-8)."""
+    case = dict(name="cfg4", B=B, T=T, H=H, W=W, seed=9, step=1, forced=None)
+    x = co.synth_clips(9, 1, 0, B, T, H, W)
+    y = co.synth_labels(0, B)
+    mc = make_cad_model(case)
+    sd = {k: v.clone() for k, v in mc.state_dict().items()}
+    params = {k: v for k, v in sd.items() if "running" not in k and "num_batches" not in k}
+    bufs = {k: v for k, v in sd.items() if "running" in k}
+    res = co.cad_train_step(params, bufs, {}, x, y, co.CadDraws.make(9, 1, 0, B, T))
+    ref_norm = float(res["total_norm"])
+    for dt in (torch.float32, torch.bfloat16):
+        m = make_cad_model(case).cuda().set_compute_dtype(dt)
+        eng = m.engine()
+        o = eng.forward(x.cuda(), True, 9, 1, 0, y.cuda())
+        eng.backward(True)
+        torch.cuda.synchronize()
+        g = eng.grads[:eng.param_floats].double()
+        fp32 = dt == torch.float32
+        atol = 1e-5 if fp32 else 2e-2
+        np.testing.assert_allclose(o["final"].cpu().numpy(), res["out"]["anomaly_scores"].detach().numpy(),
+                                   rtol=1e-4 if fp32 else 0, atol=atol)
+        np.testing.assert_allclose(o["probs"].cpu().numpy(), res["out"]["direct_predictions"].detach().numpy(),
+                                   rtol=1e-4 if fp32 else 0, atol=atol)
+        assert float(o["losses"][4]) == pytest.approx(float(res["losses"]["total"]), rel=1e-4 if fp32 else 2e-2)
+        # (frozen-stem / no-grad slots are zero in both)
+        assert float(g.norm()) == pytest.approx(ref_norm, rel=5e-3 if fp32 else 5e-2)

@@ -215,3 +215,60 @@ def test_conv3x3_wgrad_split_accuracy_matches_f32(NF, Ci, Co, IH, IW):
     _wgrad_path(nat, 3)
     assert errs[3] < 1e-6, errs
     assert errs[3] <= 2.0 * errs[1] + 1e-8, errs
+
+
+def _bf16(t):
+    return t.bfloat16().double()
+
+
+@pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", [(2, 64, 64, 29, 29, 1), (2, 32, 64, 57, 57, 2), (3, 128, 128, 15, 15, 1),
+                                              (2, 256, 256, 8, 8, 1), (2, 128, 256, 15, 15, 2)])
+def test_conv3x3_bf16_mode_matches_rounded_fp64(NF, Ci, Co, IH, IW, s):
+    """conv_bf16 (BASELINE config 4): operands rounded to bf16, products exact, fp32 accumulation.  Against an fp64
+    conv of the bf16-rounded operands the error stays at fp32 accumulation level (< 1e-5 of sum |a||b|); stride-1
+    input and weight gradients take the same path (stride-2 ones stay on the fp32 kernels)."""
+    nat = _lib()
+    nat.lib().vad_set_tuning(b"conv_bf16", 1)
+    try:
+        g = torch.Generator().manual_seed(3 + Ci + IH)
+        x = torch.randn(NF, Ci, IH, IW, generator=g)
+        w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
+        bias = torch.zeros(Co)
+        ref = F.conv2d(_bf16(x), _bf16(w), None, stride=s, padding=1)
+        mag = F.conv2d(_bf16(x).abs(), _bf16(w).abs(), None, stride=s, padding=1)
+        OH, OW = ref.shape[2:]
+        d = torch.device("cuda")
+        xh = x.permute(0, 2, 3, 1).contiguous().to(d)
+        wdev, bd = w.contiguous().to(d), bias.to(d)
+        y = torch.empty(NF, OH, OW, Co, device=d)
+        wf = torch.empty(9 * Ci * Co, device=d)
+        wd = torch.empty(9 * Ci * Co, device=d)
+        parts = torch.empty((NF * OH * OW // 64 + 2) * 2 * Co, device=d)
+        st = nat.stream_of(d)
+        nat.check(nat.lib().vad_conv3x3_forward(xh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), bd.data_ptr(), Co, s,
+                                                y.data_ptr(), wf.data_ptr(), wd.data_ptr(), parts.data_ptr(), st))
+        torch.cuda.synchronize()
+        err = float(((y.cpu().permute(0, 3, 1, 2).double() - ref).abs() / (mag + 1e-30)).max())
+        assert err < 1e-5, err
+        # the result differs from the fp32 conv by bf16 rounding, not more
+        assert float((y.cpu().permute(0, 3, 1, 2) - F.conv2d(x, w, None, stride=s, padding=1)).abs().max()) < 5e-2
+        if s != 1:
+            return
+        dy = torch.randn(NF, Co, OH, OW, generator=g)
+        dyh = dy.permute(0, 2, 3, 1).contiguous().to(d)
+        dx = torch.empty(NF, IH, IW, Ci, device=d)
+        nat.check(nat.lib().vad_conv3x3_dgrad(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, s, dx.data_ptr(),
+                                              wf.data_ptr(), wd.data_ptr(), st))
+        dW = torch.empty(Co, Ci, 3, 3, device=d)
+        part = torch.empty(1 << 24, device=d)
+        nat.check(nat.lib().vad_conv3x3_wgrad(xh.data_ptr(), dyh.data_ptr(), NF, Ci, IH, IW, Co, 1, dW.data_ptr(),
+                                              part.data_ptr(), part.numel(), st))
+        torch.cuda.synchronize()
+        rdx = torch.nn.grad.conv2d_input(x.shape, _bf16(w), _bf16(dy), stride=1, padding=1)
+        mdx = torch.nn.grad.conv2d_input(x.shape, _bf16(w).abs(), _bf16(dy).abs(), stride=1, padding=1)
+        assert float(((dx.cpu().permute(0, 3, 1, 2).double() - rdx).abs() / (mdx + 1e-30)).max()) < 1e-5
+        rdw = torch.nn.grad.conv2d_weight(_bf16(x), w.shape, _bf16(dy), stride=1, padding=1)
+        mdw = torch.nn.grad.conv2d_weight(_bf16(x).abs(), w.shape, _bf16(dy).abs(), stride=1, padding=1)
+        assert float(((dW.cpu().double() - rdw).abs() / (mdw + 1e-30)).max()) < 1e-5
+    finally:
+        nat.lib().vad_set_tuning(b"conv_bf16", 0)
