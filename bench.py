@@ -188,13 +188,47 @@ def run_gpu(args, rank, world, local_rank):
             roof["traffic_unit"] = "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE)"
             roof["traffic_source"] = src
     step_ms = 1e3 * elapsed / args.steps
+    # parity probe (rank 0): one more forward on the first batch with the trained weights; the CPU leg re-runs it on
+    # the oracle (cpu_baseline) and reports the score difference and the frame-AUC of both
+    probe = None
+    if rank == 0:
+        o = eng.forward(pool[0], True, 777, 0, 0, labels)
+        torch.cuda.synchronize()
+        probe = dict(state={k: v.detach().cpu().clone() for k, v in model.state_dict().items()},
+                     final=o["final"].cpu(), probs=o["probs"].cpu(), loss=float(o["losses"][4]))
     # whole-step algorithmic FLOP rate (all 3x3 convs fwd/dgrad/wgrad + conv1 fwd), for context
     conv_flops = sum(2.0 * NF * oh * ow * co * ci * 9 for NF, ci, co, oh, ow in conv_shapes(B, T, H, W))
     dgrad_flops = conv_flops - 2.0 * B * T * conv_shapes(B, T, H, W)[0][3] * conv_shapes(B, T, H, W)[0][4] * 32 * 32 * 9
     c1 = algorithmic_work("conv1", B, T, H, W)[1]
     step_flops = 2 * conv_flops + dgrad_flops + c1
     return dict(elapsed=elapsed, step_ms=step_ms, roof=roof, breakdown=breakdown, dominant=dominant,
-                final_loss=final_loss, step_tflops=step_flops / (step_ms * 1e-3) / 1e12)
+                final_loss=final_loss, step_tflops=step_flops / (step_ms * 1e-3) / 1e12, probe=probe)
+
+
+def parity_check(args, probe):
+    """CPU leg of the parity probe: the oracle forward (fp32, CPU) on the same clips, weights, BN state and draws
+    as the GPU probe; max |score difference| (north star: 1e-4) and frame-AUC of both score sets (clip labels
+    i mod 2 broadcast to the T frames of each clip)."""
+    import torch
+    from oracle import cad_oracle as co
+    from vad_amd.evaluate import frame_auc
+    B, T, H, W = args.batch, args.T, args.H, args.W
+    sd = probe["state"]
+    params = {k: v for k, v in sd.items() if "running" not in k and "num_batches" not in k}
+    bufs = {k: v.clone() for k, v in sd.items() if "running" in k}
+    x = co.synth_clips(7, 0, 0, B, T, H, W)
+    y = co.synth_labels(0, B)
+    with torch.no_grad():
+        ref = co.cad_forward(params, bufs, x, co.CadDraws.make(777, 0, 0, B, T), training=True)
+        rl = co.cad_losses(ref, y)
+    gpu_s, cpu_s = probe["final"].double(), ref["anomaly_scores"].double()
+    return {"max_abs_score_diff": float((gpu_s - cpu_s).abs().max()),
+            "max_abs_prob_diff": float((probe["probs"].double() - ref["direct_predictions"].double()).abs().max()),
+            "loss_rel_diff": abs(probe["loss"] - float(rl["total"])) / max(abs(float(rl["total"])), 1e-12),
+            "frame_auc_gpu": frame_auc(gpu_s.numpy(), y.numpy(), T),
+            "frame_auc_cpu": frame_auc(cpu_s.numpy(), y.numpy(), T),
+            "tolerance": 1e-4 if args.dtype == "fp32" else 2e-2,
+            "sample": f"one train-mode forward of B={B} clips x T={T} x 1x{H}x{W} after the timed steps"}
 
 
 def cpu_baseline(args):
@@ -225,13 +259,91 @@ def cpu_baseline(args):
                       f"{threads} threads), after 1 warm-up step"}
 
 
+def run_bbox(args, rank, world, local_rank):
+    """BASELINE config 5 (avenue_training_script_bbox.py scorer, bbox:339-368): 64 RGB 64x64 clips per rank with T
+    drawn from {8, 16, 32}, scored in one packed batch per T (bbox.AnomalyVisualizer.predict_clips packing, the
+    clips already resident in HBM).  A step scores every clip of the rank once."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from vad_amd import _native as nat
+    from vad_amd.bbox import CausalAnomalyDetector as BboxDetector
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    model = BboxDetector().to(dev).eval()
+    n = args.batch
+    Ts = np.random.default_rng(5).choice([8, 16, 32], size=n * world)[rank * n:(rank + 1) * n]
+    groups = {}
+    for T in (8, 16, 32):
+        k = int((Ts == T).sum())
+        if k:
+            x = torch.empty(k, 3, T, 64, 64, device=dev)
+            nat.check(nat.lib().vad_synth_frames(11, 0, (rank * n) * 3 * 32, k * 3 * T, 64 * 64, 1, x.data_ptr(),
+                                                 nat.stream_of(dev)))
+            groups[T] = x
+
+    def step():
+        with torch.no_grad():
+            return [model(x) for x in groups.values()]
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    frames = int(sum(x.shape[0] * x.shape[2] for x in groups.values()))
+    probe = {T: (x[:2].cpu(), o[0].reshape(-1)[:2].cpu()) for (T, x), o in zip(groups.items(), out)}
+    return dict(elapsed=elapsed, step_ms=1e3 * elapsed / args.steps, frames=frames, Ts=Ts.tolist(),
+                state={k: v.detach().cpu().clone() for k, v in model.state_dict().items()}, probe=probe)
+
+
+def bbox_cpu(args, r):
+    """CPU leg of config 5: the oracle scorer (oracle/bbox_oracle.py) on a bounded sample, and parity of the GPU
+    scores of the first two clips of every T bucket."""
+    import torch
+    from oracle import bbox_oracle as bo
+    threads = torch.get_num_threads()
+    p = r["state"]
+    diff = 0.0
+    with torch.no_grad():
+        for T, (x, s) in r["probe"].items():
+            rs, _, _ = bo.bbox_forward(p, x)
+            diff = max(diff, float((rs.reshape(-1) - s).abs().max()))
+        x = bo.synth_clips(11, 0, 0, 4, 16, 64, 64)
+        bo.bbox_forward(p, x)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            bo.bbox_forward(p, x)
+            n += 1
+            if time.perf_counter() - t0 >= min(args.cpu_seconds, 6.0) or n >= 200:
+                break
+        el = time.perf_counter() - t0
+    return ({"value": round(4 * n / el, 3), "unit": "clips/s", "cores": threads, "kind": "port",
+             "sample": f"{n} forwards of 4 RGB clips x T=16 x 64x64 (oracle/bbox_oracle.py, torch CPU fp32, "
+                       f"{threads} threads)"},
+            {"max_abs_score_diff": diff, "tolerance": 1e-4, "sample": "first two clips of each T bucket"})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 4),
-                    help="BASELINE config: 2 = T=16 227x227 fp32 (default), 4 = T=32 256x256 bf16 convs")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
+                    help="BASELINE config: 2 = T=16 227x227 fp32 (default), 4 = T=32 256x256 bf16 convs, "
+                         "5 = bbox clip scorer, mixed T (inference)")
     ap.add_argument("--batch", type=int, default=8, help="clips per GPU")
     ap.add_argument("--T", type=int, default=None)
     ap.add_argument("--H", type=int, default=None)
@@ -243,7 +355,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--breakdown-out", default=None, help="write the per-kernel breakdown JSON here")
     args = ap.parse_args()
-    preset = {2: (16, 227, 227, "fp32"), 4: (32, 256, 256, "bf16")}[args.config]
+    preset = {2: (16, 227, 227, "fp32"), 4: (32, 256, 256, "bf16"), 5: (0, 64, 64, "fp32")}[args.config]
+    if args.config == 5 and args.batch == 8:
+        args.batch = 64  # clips per rank
     args.T = args.T or preset[0]
     args.H = args.H or preset[1]
     args.W = args.W or preset[2]
@@ -257,9 +371,29 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    if args.config == 5:
+        r = run_bbox(args, rank, world, local_rank)
+        if rank == 0:
+            cpu, parity = (None, None) if (args.no_cpu_baseline or world > 1) else bbox_cpu(args, r)
+            clips = world * args.batch * args.steps
+            print(json.dumps({
+                "metric": BASELINE_METRIC, "value": round(clips / r["elapsed"], 3), "unit": "clips/s",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["step_ms"], 4),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+                "data": "synthetic RGB clips (keyed-hash u8 / 255), random-init weights (torch.manual_seed(0))",
+                "config": {"workload": "avenue_training_script_bbox.py clip scorer (bbox:339-368), BASELINE config 5 "
+                                       "(inference)", "clips_per_gpu": args.batch, "clip_len": "8/16/32 mixed",
+                           "frame": "3x64x64", "packing": "one batch per T", "parallelism": f"dp{world}",
+                           "frames_per_step_per_gpu": r["frames"]},
+                "roofline": None, "cpu_baseline": cpu, "parity": parity}), flush=True)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
     r = run_gpu(args, rank, world, local_rank)
     if rank == 0:
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
+        parity = None if (args.no_cpu_baseline or world > 1 or r.get("probe") is None) else parity_check(args, r["probe"])
         clips = world * args.batch * args.steps
         out = {
             "metric": BASELINE_METRIC,
@@ -280,6 +414,7 @@ def main():
                        "frame": f"1x{args.H}x{args.W}", "parallelism": f"dp{world}"},
             "roofline": r["roof"],
             "cpu_baseline": cpu,
+            "parity": parity,
             "step_algorithmic_tflops": round(r["step_tflops"], 3),
             "final_loss": r["final_loss"],
         }

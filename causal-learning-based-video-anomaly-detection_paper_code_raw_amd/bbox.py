@@ -132,19 +132,35 @@ class AnomalyVisualizer:
             s, adj, f = self.model(t.to(self.device))
         return float(s.squeeze().cpu().numpy()), adj.squeeze().cpu().numpy(), f.squeeze().cpu().numpy()
 
-    def predict_clips(self, clips):
-        """Score clips of mixed lengths: one packed batch per T; results in input order."""
+    def predict_clips(self, clips, process_group=None):
+        """Score clips of mixed lengths: one packed batch per T; results in input order.
+
+        Data parallel (BASELINE config 5): with an initialised process group of world size P every rank passes the
+        same clip list, scores the clips of each length group at positions r, r+P, ... (an even share of every T
+        bucket), and the (score, graph, features) triples are exchanged with one all_gather_object at the end;
+        no layer couples clips, so the result equals the single-process one."""
+        import torch.distributed as dist
+        world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        rank = dist.get_rank(process_group) if world > 1 else 0
         groups = defaultdict(list)
         for i, c in enumerate(clips):
             t = torch.from_numpy(c).float() if isinstance(c, np.ndarray) else c.float()
             groups[tuple(t.shape)].append((i, t))
-        out = [None] * len(clips)
+        mine = {}
         with torch.no_grad():
             for shape, items in groups.items():
+                items = items[rank::world]
+                if not items:
+                    continue
                 x = torch.stack([t for _, t in items]).to(self.device)
                 s, adj, f = self.model(x)
                 s = s.reshape(-1).cpu().numpy()
                 adj, f = adj.cpu().numpy(), f.cpu().numpy()
                 for k, (i, _) in enumerate(items):
-                    out[i] = (float(s[k]), adj[k], f[k])
-        return out
+                    mine[i] = (float(s[k]), adj[k], f[k])
+        if world > 1:
+            parts = [None] * world
+            dist.all_gather_object(parts, mine, group=process_group)
+            for p in parts:
+                mine.update(p)
+        return [mine[i] for i in range(len(clips))]

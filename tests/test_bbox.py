@@ -68,3 +68,45 @@ def test_bbox_mixed_t_packing_matches_oracle():
         assert s == pytest.approx(float(rs), rel=1e-4, abs=1e-6)
         np.testing.assert_allclose(adj, radj[0].numpy(), rtol=1e-4, atol=1e-6)
         np.testing.assert_allclose(f, rf[0].numpy(), rtol=1e-4, atol=1e-5)
+
+
+def _bbox_dp_worker(rank, world, port, out_path):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vad_amd.bbox import AnomalyVisualizer
+        vis = AnomalyVisualizer(None, device="cuda")
+        vis.model = make_bbox_model(dict(seed=44)).cuda()
+        clips = [bo.synth_clips(44, 0, i, 1, T, 64, 64)[0].numpy() for i, T in enumerate([8, 32, 16, 8, 16, 32, 8])]
+        res = vis.predict_clips(clips)
+        if rank == 0:
+            torch.save({"s": torch.tensor([r[0] for r in res]), "f": torch.tensor(np.stack([r[2] for r in res]))},
+                       out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_bbox_data_parallel_two_ranks(tmp_path):
+    """Config 5 sharding: two gloo ranks (sharing cuda:0) each score their share of every T bucket; the gathered
+    results equal single-process scoring (clips are independent; only the split-K reduction order of the 3-D conv
+    GEMMs depends on the batch size, so features agree to fp32 rounding)."""
+    import socket
+    import torch.multiprocessing as mp
+    from vad_amd.bbox import AnomalyVisualizer
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "r0.pt")
+    mp.spawn(_bbox_dp_worker, args=(2, port, out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    vis = AnomalyVisualizer(None, device="cuda")
+    vis.model = make_bbox_model(dict(seed=44)).cuda()
+    clips = [bo.synth_clips(44, 0, i, 1, T, 64, 64)[0].numpy() for i, T in enumerate([8, 32, 16, 8, 16, 32, 8])]
+    ref = vis.predict_clips(clips)
+    np.testing.assert_allclose(got["s"].numpy(), np.array([r[0] for r in ref], dtype=np.float32), rtol=1e-6,
+                               atol=1e-7)
+    np.testing.assert_allclose(got["f"].numpy(), np.stack([r[2] for r in ref]), rtol=1e-5, atol=1e-6)
