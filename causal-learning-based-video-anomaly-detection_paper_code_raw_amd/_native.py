@@ -48,6 +48,8 @@ _SIGS = {
     "vad_cad_set_debug": (_I, [_P, ctypes.c_char_p, _I64]),
     "vad_cad_set_option": (_I, [_P, ctypes.c_char_p, _I64]),
     "vad_cad_conv_path": (_I, [_P, _I, _I]),
+    "vad_u8_to_clip": (_I, [_P, _I64, _I, _P, _P]),
+    "vad_resize_u8": (_I, [_P, _I, _I, _P, _I, _I]),
     "vad_debug_d2h": (_I, [_P, _P, _I64]),
     "vad_cad_profile": (_I, [_P, _I, ctypes.c_char_p]),
     "vad_cad_profile_read": (_I, [_P, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I), _I]),

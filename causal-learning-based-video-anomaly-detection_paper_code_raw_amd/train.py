@@ -10,6 +10,7 @@ import torch
 import torch.distributed as dist
 
 from .cad import CausalAnomalyDetector  # noqa: F401  (re-export for callers of this module)
+from .data import ClipStager, prefetch
 
 
 def apply_memory_efficient_training(model):
@@ -82,15 +83,18 @@ def train_model(model, train_loader, val_loader, num_epochs=20, lr=3e-4):
     dev = torch.device("cuda", torch.cuda.current_device())
     model.to(dev)
     trainer = CadTrainer(model, lr=lr)
+    stager = ClipStager(dev, mode=0)
     train_losses, val_losses = [], []
     print("Starting training with mixed precision: False")
     for epoch in range(num_epochs):
         model.train()
         cur_lr = _cosine_lr(lr, epoch, num_epochs)
         tot, nb = 0.0, 0
-        for batch_idx, (videos, labels) in enumerate(train_loader):
+        # u8 clips (vad_amd.data datasets) are staged through pinned memory and normalised on the device, one batch
+        # ahead of the step; float clips (the reference's datasets) are copied as they are
+        for batch_idx, (videos, labels) in enumerate(prefetch(train_loader, stager)):
             try:
-                losses = trainer.step(videos.to(dev), labels.to(dev), lr=cur_lr)
+                losses = trainer.step(videos, labels, lr=cur_lr)
                 l = losses.tolist()
                 tot += l[4]
                 nb += 1
@@ -105,8 +109,7 @@ def train_model(model, train_loader, val_loader, num_epochs=20, lr=3e-4):
         model.eval()
         vtot, vb, correct, total = 0.0, 0, 0, 0
         with torch.no_grad():
-            for videos, labels in val_loader:
-                videos, labels = videos.to(dev), labels.to(dev)
+            for videos, labels in prefetch(val_loader, stager):
                 o = _eval_losses(model, videos, labels)
                 vtot += o["losses"][4].item()
                 vb += 1
@@ -125,10 +128,10 @@ def test_model(model, test_loader):
     dev = next(model.parameters()).device
     scores, labels_all, outs = [], [], []
     with torch.no_grad():
-        for videos, labels in test_loader:
-            out = model(videos.to(dev))
+        for videos, labels in prefetch(test_loader, ClipStager(dev, mode=0)):
+            out = model(videos)
             scores.extend(out["anomaly_scores"].cpu().tolist())
-            labels_all.extend(labels.tolist())
+            labels_all.extend(labels.cpu().tolist())
             outs.append(out)
     import numpy as np
     return np.array(scores), np.array(labels_all), outs

@@ -51,3 +51,30 @@ BBOX_CASES = [
     dict(name="t16", B=2, T=16, H=64, W=64, seed=31, step=0),
     dict(name="t32_48x56", B=2, T=32, H=48, W=56, seed=32, step=0),
 ]
+
+
+# frame-folder tree for the dataset-enumeration fixture (tests/golden/make_dataset_golden.py): folder -> frame count
+# (UCSD Ped2 layout: TrainNNN / TestNNN folders of .tif frames, TestNNN_gt folders of .bmp masks)
+DATASET_TREE = {
+    "Train/Train001": 40, "Train/Train002": 23, "Train/Train003": 16, "Train/Train004": 7,
+    "Test/Test001": 50, "Test/Test002": 33, "Test/Test003": 17, "Test/Test004": 64, "Test/Test005": 12,
+    "Test/Test011": 45, "Test/Test001_gt": 50,
+}
+
+
+def build_dataset_tree(root, empty=True, frame_hw=(24, 36), seed=0):
+    """Create DATASET_TREE under root: empty files (enumeration only) or small random grayscale .tif frames."""
+    import os
+    import numpy as np
+    rs = np.random.default_rng(seed)
+    for folder, n in DATASET_TREE.items():
+        d = os.path.join(root, folder)
+        os.makedirs(d, exist_ok=True)
+        ext = ".bmp" if folder.endswith("_gt") else ".tif"
+        for i in range(n):
+            path = os.path.join(d, f"{i + 1:03d}{ext}")
+            if empty:
+                open(path, "wb").close()
+            else:
+                from PIL import Image
+                Image.fromarray(rs.integers(0, 256, size=frame_hw, dtype=np.uint8)).save(path)
