@@ -336,14 +336,92 @@ def bbox_cpu(args, r):
             {"max_abs_score_diff": diff, "tolerance": 1e-4, "sample": "first two clips of each T bucket"})
 
 
+def ae_flops_per_clip(T):
+    """Algorithmic FLOPs of one cad1 autoencoder train clip (SURVEY §8d counting: 2 per MAC, backward = 2x forward
+    minus the first conv's input gradient).  Encoder per frame: convs 1.05 + 16.8 + 16.8 + 8.4 MFLOP + Linear 0.26;
+    LSTM per frame 2 x 2 x 64 x 256; decoder once per clip (its T calls are identical): Linear 0.26 + transposed
+    convs 8.4 + 16.8 + 16.8 + 1.05 MFLOP."""
+    enc, lstm, dec, first = 43_253_760, 65_536, 43_253_760, 1_048_576
+    return 3 * (T * (enc + lstm) + dec) - T * first
+
+
+def run_ae(args, rank, world, local_rank):
+    """cad1 (causal_anomaly_detection1.py) memory autoencoder, SURVEY §8f: one step = the fused train_model
+    iteration (cad1:378-431: forward, MSE, memory-ring update, backward, NaN-grad check, clip_grad_norm_(0.1), Adam)
+    on args.batch normal clips of T x 1x64x64 per rank, already resident in HBM."""
+    import torch
+    from vad_amd import _native as nat
+    from vad_amd.ae import AeTrainer, VideoAutoEncoder
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    model = VideoAutoEncoder().to(dev)
+    tr = AeTrainer(model, lr=1e-6)
+    B, T = args.batch, args.T
+    x = torch.empty(B, T, 1, 64, 64, device=dev)
+    nat.check(nat.lib().vad_synth_frames(13, 0, rank * B * T, B * T, 64 * 64, 1, x.data_ptr(), nat.stream_of(dev)))
+    x.clamp_(0.001, 0.999)  # the dataset's clamp (cad1:110-114)
+    for _ in range(args.warmup):
+        tr.step(x)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        losses = tr.step(x)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    lv = losses.cpu().tolist()
+    ev = tr.eval_batch(x[:4])
+    probe = {"x": x[:4].cpu(), "recon_error": ev["recon_error"].cpu(), "score": ev["anomaly_score"].cpu(),
+             "state": {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}}
+    return dict(elapsed=elapsed, step_ms=1e3 * elapsed / args.steps, loss=lv[0], status=lv[3], probe=probe)
+
+
+def ae_cpu(args, r):
+    """CPU leg of the cad1 line: parity of the GPU eval scores against the oracle (same weights / ring), and the
+    oracle train step (oracle/ae_oracle.py) timed on a bounded sample."""
+    import torch
+    from oracle import ae_oracle as ae
+    threads = torch.get_num_threads()
+    params, bufs, mem = ae.split_state(r["probe"]["state"])
+    ev = ae.ae_eval_batch(params, bufs, mem, r["probe"]["x"])
+    parity = {"max_abs_recon_error_diff": float((ev["recon_error"] - r["probe"]["recon_error"]).abs().max()),
+              "max_abs_memory_score_diff": float((ev["outputs"]["anomaly_score"] - r["probe"]["score"]).abs().max()),
+              "tolerance": 1e-4, "sample": "eval forward of 4 clips after the timed steps"}
+    B, T = args.batch, args.T
+    x = ae.synth_clips(13, 0, 0, B, T)
+    y = torch.zeros(B, dtype=torch.int64)
+    state = {}
+    ae.ae_train_step(params, bufs, mem, state, x, y, lr=1e-6)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        ae.ae_train_step(params, bufs, mem, state, x, y, lr=1e-6)
+        n += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds or n >= 100:
+            break
+    el = time.perf_counter() - t0
+    return ({"value": round(B * n / el, 3), "unit": "clips/s", "cores": threads, "kind": "port",
+             "sample": f"{n} train steps of B={B} clips x T={T} x 1x64x64 (oracle/ae_oracle.py, torch CPU fp32, "
+                       f"{threads} threads), after 1 warm-up step"}, parity)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
+    ap.add_argument("--config", default="2", choices=("2", "4", "5", "cad1"),
                     help="BASELINE config: 2 = T=16 227x227 fp32 (default), 4 = T=32 256x256 bf16 convs, "
-                         "5 = bbox clip scorer, mixed T (inference)")
+                         "5 = bbox clip scorer, mixed T (inference); cad1 = the causal_anomaly_detection1.py "
+                         "memory autoencoder train step (SURVEY §8f, not a BASELINE config)")
     ap.add_argument("--batch", type=int, default=8, help="clips per GPU")
     ap.add_argument("--T", type=int, default=None)
     ap.add_argument("--H", type=int, default=None)
@@ -355,9 +433,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--breakdown-out", default=None, help="write the per-kernel breakdown JSON here")
     args = ap.parse_args()
-    preset = {2: (16, 227, 227, "fp32"), 4: (32, 256, 256, "bf16"), 5: (0, 64, 64, "fp32")}[args.config]
+    args.config = args.config if args.config == "cad1" else int(args.config)
+    preset = {2: (16, 227, 227, "fp32"), 4: (32, 256, 256, "bf16"), 5: (0, 64, 64, "fp32"),
+              "cad1": (16, 64, 64, "fp32")}[args.config]
     if args.config == 5 and args.batch == 8:
         args.batch = 64  # clips per rank
+    if args.config == "cad1" and args.batch == 8:
+        args.batch = 32
     args.T = args.T or preset[0]
     args.H = args.H or preset[1]
     args.W = args.W or preset[2]
@@ -371,6 +453,32 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    if args.config == "cad1":
+        r = run_ae(args, rank, world, local_rank)
+        if rank == 0:
+            cpu, parity = (None, None) if (args.no_cpu_baseline or world > 1) else ae_cpu(args, r)
+            clips = world * args.batch * args.steps
+            tflops = ae_flops_per_clip(args.T) * args.batch / (r["step_ms"] * 1e-3) / 1e12
+            print(json.dumps({
+                "metric": BASELINE_METRIC, "value": round(clips / r["elapsed"], 3), "unit": "clips/s",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["step_ms"], 4),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+                "data": "synthetic grayscale clips (keyed-hash u8 / 255, clamped to [0.001, 0.999]); random-init "
+                        "weights (torch.manual_seed(0))",
+                "config": {"workload": "causal_anomaly_detection1.py memory-autoencoder train_model step "
+                                       "(cad1:378-431), SURVEY §8f", "clips_per_gpu": args.batch,
+                           "global_batch": world * args.batch, "clip_len": args.T, "frame": "1x64x64",
+                           "parallelism": f"dp{world}"},
+                "roofline": {"bound": "mfma", "kernel": "whole step", "achieved": round(tflops, 3),
+                             "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_FP32_TFLOPS, 4),
+                             "traffic": None,
+                             "basis": f"{ae_flops_per_clip(args.T)} algorithmic FLOP per clip x clips / step time"},
+                "cpu_baseline": cpu, "parity": parity, "final_loss": r["loss"], "final_status": r["status"]}),
+                flush=True)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
     if args.config == 5:
         r = run_bbox(args, rank, world, local_rank)
         if rank == 0:

@@ -99,6 +99,26 @@ _SIGS = {
     "vad_bbox_workspace_bytes": (_I64, [_P]),
     "vad_bbox_bind": (_I, [_P, _P, _P]),
     "vad_bbox_forward": (_I, [_P, _P, _P, _P, _P, _P]),
+    # cad1 memory autoencoder (causal_anomaly_detection1.py)
+    "vad_ae_num_slots": (_I, []),
+    "vad_ae_slot_name": (ctypes.c_char_p, [_I]),
+    "vad_ae_slot_numel": (_I64, [_I]),
+    "vad_ae_slot_offset": (_I64, [_I]),
+    "vad_ae_param_floats": (_I64, []),
+    "vad_ae_num_bufs": (_I, []),
+    "vad_ae_buf_name": (ctypes.c_char_p, [_I]),
+    "vad_ae_buf_numel": (_I64, [_I]),
+    "vad_ae_buf_offset": (_I64, [_I]),
+    "vad_ae_buf_floats": (_I64, []),
+    "vad_ae_create": (_I, [_I, _I, ctypes.POINTER(_P)]),
+    "vad_ae_destroy": (None, [_P]),
+    "vad_ae_workspace_bytes": (_I64, [_P]),
+    "vad_ae_bind": (_I, [_P] * 11),
+    "vad_ae_forward": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "vad_ae_backward": (_I, [_P, _I, _P, _P, _P, _P]),
+    "vad_ae_optimizer_step": (_I, [_P, _F, _F, _F, _F, _F, _F, _F, _P]),
+    "vad_ae_update_memory": (_I, [_P, _P, _P, _I, _P]),
+    "vad_ae_memory_score": (_I, [_P, _P, _P, _I, _P, _P]),
 }
 
 

@@ -621,7 +621,7 @@ __global__ __launch_bounds__(256) void dense_wgrad_reduce_kernel(const float* __
     for (int z = 0; z < S; ++z) s += part[z * total + i];
     const int row = (int)(i / ld), col = (int)(i % ld);
     if (col < K) dW[(int64_t)row * K + col] = s;
-    else db[row] = s;
+    else if (db) db[row] = s;
   }
 }
 

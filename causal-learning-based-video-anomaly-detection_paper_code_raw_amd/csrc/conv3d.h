@@ -40,8 +40,9 @@ Conv3dGeom conv3d_geom(const Vol5& in, int Co, int k, int s_d, int s_h, int s_w,
 // cols[rows][K]; optional relu(scale*x + shift) / relu(x) of the source applied on load (scale nullable)
 int im2col3d(const float* src, const Strides5& s, const Conv3dGeom& g, const float* scale, const float* shift,
              int relu, float* cols, hipStream_t st);
-// dsrc (NDHWC, in dims) = col2im(dcols)   (written, not accumulated)
-int col2im3d(const float* dcols, const Conv3dGeom& g, float* dsrc, hipStream_t st);
+// dsrc (NDHWC, in dims) = col2im(dcols) (+ bias[c] when bias != nullptr: a transposed conv's output)   (written,
+// not accumulated)
+int col2im3d(const float* dcols, const Conv3dGeom& g, float* dsrc, hipStream_t st, const float* bias = nullptr);
 
 // Non-overlapping MaxPool3d (kernel == stride, floor mode) over act(y) where act = relu(scale*y + shift) when
 // stats != nullptr (stats layout of bn_finalize) or relu(y) when relu, else identity.  out NDHWC.

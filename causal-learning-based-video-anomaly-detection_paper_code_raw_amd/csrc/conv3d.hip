@@ -66,7 +66,7 @@ int im2col3d(const float* src, const Strides5& s, const Conv3dGeom& g, const flo
 
 // one thread per source element (NDHWC): gather the taps that read it
 __global__ __launch_bounds__(256) void col2im3d_kernel(const float* __restrict__ dcols, Conv3dGeom g,
-                                                       float* __restrict__ dsrc) {
+                                                       const float* __restrict__ bias, float* __restrict__ dsrc) {
   const int K = g.K(), taps = g.kd * g.kh * g.kw, C = g.in.C;
   const int64_t total = g.in.numel();
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
@@ -99,15 +99,15 @@ __global__ __launch_bounds__(256) void col2im3d_kernel(const float* __restrict__
         }
       }
     }
-    dsrc[i] = acc;
+    dsrc[i] = bias ? acc + bias[c] : acc;
   }
 }
 
-int col2im3d(const float* dcols, const Conv3dGeom& g, float* dsrc, hipStream_t st) {
+int col2im3d(const float* dcols, const Conv3dGeom& g, float* dsrc, hipStream_t st, const float* bias) {
   const int64_t total = g.in.numel();
   if (total == 0) return 0;
   hipLaunchKernelGGL(col2im3d_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 16384)), dim3(256), 0, st,
-                     dcols, g, dsrc);
+                     dcols, g, bias, dsrc);
   VAD_LAUNCH_CHECK();
   return 0;
 }

@@ -192,6 +192,56 @@ int vad_bbox_bind(vad_bbox_plan* plan, void* workspace, const float* params);
 /* scores (B,), adj (B,16,16), features (B,1024, nullable) */
 int vad_bbox_forward(vad_bbox_plan* plan, const float* x, float* scores, float* adj, float* features, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * causal_anomaly_detection1.py — memory-bank VideoAutoEncoder (cad1:124-321) and the train_model iteration
+ * (cad1:372-431).  replaces: model(videos) (cad1:392), reconstruction_loss (cad1:400), model.update_memory
+ * (cad1:407), total_loss.backward() (cad1:411), the NaN-grad check + clip_grad_norm_(0.1) + Adam.step()
+ * (cad1:413-425), and the eval forwards of the validation / calculate_anomaly_scores loops (cad1:460, 542-552)
+ * ------------------------------------------------------------------------------------------ */
+typedef struct vad_ae_plan vad_ae_plan;
+
+int vad_ae_num_slots(void);            /* 38 = model.named_parameters() order */
+const char* vad_ae_slot_name(int i);
+int64_t vad_ae_slot_numel(int i);
+int64_t vad_ae_slot_offset(int i);
+int64_t vad_ae_param_floats(void);
+int vad_ae_num_bufs(void);             /* 14 BatchNorm running_mean / running_var tensors, state_dict order */
+const char* vad_ae_buf_name(int i);
+int64_t vad_ae_buf_numel(int i);
+int64_t vad_ae_buf_offset(int i);
+int64_t vad_ae_buf_floats(void);
+/* clips (B, T, 1, 64, 64) fp32 (the encoder's Linear(128*4*4) fixes 64x64 frames), 1 <= B <= 500 */
+int vad_ae_create(int B, int T, vad_ae_plan** out);
+void vad_ae_destroy(vad_ae_plan* plan);
+int64_t vad_ae_workspace_bytes(const vad_ae_plan* plan);
+/* nbt: int64[7] num_batches_tracked (encoder.1/4/7/10, decoder.4/7/10); memory: float[500*64] normal_memory;
+ * memory_ptr: int64[1]; exp_avg / exp_avg_sq / steps (int32[num_slots]) may be NULL until an optimizer step */
+int vad_ae_bind(vad_ae_plan* plan, void* workspace, float* params, float* grads, float* bufs, int64_t* nbt,
+                float* memory, int64_t* memory_ptr, float* exp_avg, float* exp_avg_sq, int32_t* steps);
+/* stages: 3 = forward() (encode_sequence + decode_sequence + compute_anomaly_score), 1 = encode_sequence only,
+ * 2 = decode_sequence of seq_in (B, 64) over T frames.  loss_mode (stages 3): 0 none; 1 the reconstruction MSE
+ * against x and per-clip errors (eval loops); 2 the train_model iteration: MSE and its gradient, a non-finite input
+ * skips the batch without touching BN running stats / counters / the ring (cad1:385-387), a valid batch's sequence
+ * features enter the ring after the scores (cad1:407).  Outputs (nullable): recon (B,T,1,64,64), seq (B,64),
+ * frame_feats (B,T,64), scores (B,), recon_err (B,) (loss_mode > 0).  losses float[4]: mse, grad norm, clipped,
+ * status (0 skipped, 1 non-finite grads, 2 stepped; the middle two and the final status from the optimizer) */
+int vad_ae_forward(vad_ae_plan* plan, const float* x, const float* seq_in, int stages, int training, int loss_mode,
+                   float* recon, float* seq, float* frame_feats, float* scores, float* recon_err, float* losses,
+                   void* stream);
+/* backward of the last full forward: use_loss = 1 -> of its train_model MSE, else the given output grads
+ * (nullable = zero).  Writes every slot of the flat grad buffer. */
+int vad_ae_backward(vad_ae_plan* plan, int use_loss, const float* d_recon, const float* d_seq,
+                    const float* d_frame_feats, void* stream);
+/* non-finite-grad skip, clip_grad_norm_(max_norm) and Adam with coupled L2 weight decay (cad1:350-351, 413-425);
+ * grad_scale multiplies the grads first (1/world after a data-parallel sum) */
+int vad_ae_optimizer_step(vad_ae_plan* plan, float lr, float beta1, float beta2, float eps, float weight_decay,
+                          float max_norm, float grad_scale, void* stream);
+/* the memory ring of any VideoAutoEncoder: update_memory (cad1:201-219; n <= 500 features (n, 64)) and
+ * compute_anomaly_score (cad1:262-301; n sequence features -> scores (n,)) */
+int vad_ae_update_memory(float* memory, int64_t* memory_ptr, const float* features, int n, void* stream);
+int vad_ae_memory_score(const float* memory, const int64_t* memory_ptr, const float* seq, int n, float* scores,
+                        void* stream);
+
 /* Host data path.
  * vad_u8_to_clip: n u8 pixels (already in HBM) -> fp32; mode 0: (u8 - 0.5) / 0.5 (UCSDped2Dataset + Normalize,
  *   cad:85-104, 1177-1179), mode 1: u8 / 255 (ToTensor, mc:120 / bbox:411).  src 4-byte, dst 16-byte aligned.

@@ -52,6 +52,19 @@ BBOX_CASES = [
     dict(name="t32_48x56", B=2, T=32, H=48, W=56, seed=32, step=0),
 ]
 
+# cad1 memory autoencoder (causal_anomaly_detection1.py): one epoch of the reference's train_model over the label rows
+# (only label-0 clips train, cad1:373-378), its validation pass and calculate_anomaly_scores.  mem: the ring state
+# before training, (rows prefilled, memory_ptr) or None -- ptr >= 10 exercises the score, 498 + 3 clips the
+# wrap-around of update_memory (cad1:212-219); an all-anomalous first batch exercises the skip.
+AE_CASES = [
+    dict(name="b4t8", B=4, T=8, seed=40, lr=1e-5, labels=[[0, 0, 1, 0], [0, 0, 0, 0], [0, 1, 0, 0]],
+         val_labels=[0, 1, 0], test_labels=[0, 1, 0, 1], mem=None),
+    dict(name="b3t5_wrap", B=3, T=5, seed=41, lr=5e-7, labels=[[0, 0, 0], [1, 0, 0]], val_labels=[0, 0],
+         test_labels=[1, 0, 0], mem=(500, 498)),
+    dict(name="b2t16_skip", B=2, T=16, seed=42, lr=2e-5, labels=[[1, 1], [0, 0]], val_labels=[0, 1],
+         test_labels=[0, 1], mem=(20, 20)),
+]
+
 
 # frame-folder tree for the dataset-enumeration fixture (tests/golden/make_dataset_golden.py): folder -> frame count
 # (UCSD Ped2 layout: TrainNNN / TestNNN folders of .tif frames, TestNNN_gt folders of .bmp masks)

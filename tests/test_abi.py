@@ -51,6 +51,26 @@ def test_slot_table_matches_module():
     assert groups["detector.detector_net.0.weight"] == 2 and groups["structure_learner.node_encoder.weight"] == 3
 
 
+def test_ae_slot_table_matches_module():
+    """cad1 VideoAutoEncoder: library slots = named_parameters(), buffers = the BN running stats in state_dict order."""
+    from vad_amd import _native
+    from vad_amd.ae import VideoAutoEncoder
+    L = _native.lib()
+    torch.manual_seed(0)
+    m = VideoAutoEncoder()
+    named = list(m.named_parameters())
+    assert L.vad_ae_num_slots() == len(named)
+    for i, (k, p) in enumerate(named):
+        assert L.vad_ae_slot_name(i).decode() == k
+        assert L.vad_ae_slot_numel(i) == p.numel()
+        assert L.vad_ae_slot_offset(i) % 256 == 0
+    assert [L.vad_ae_buf_name(i).decode() for i in range(L.vad_ae_num_bufs())] == \
+        [k for k in m.state_dict() if "running" in k]
+    h = ctypes.c_void_p()
+    assert L.vad_ae_create(501, 8, ctypes.byref(h)) != 0  # update_memory writes B rows of the 500-row ring
+    assert b"unsupported shape" in L.vad_last_error()
+
+
 def test_error_codes_and_text():
     from vad_amd import _native
     L = _native.lib()
