@@ -215,10 +215,62 @@ class A2Engine:
 
 
 class _ParamGroups:
-    """The slice of the torch optimizer surface the reference's driver reads (param_groups[0]['lr'])."""
+    """The slice of the torch optimizer surface the reference's driver reads (param_groups[0]['lr']) and writes into
+    its checkpoints (a2:438-455: ``optimizer.state_dict()``).  The AdamW moments live in the engine's flat device
+    buffers; ``state_dict`` exports them in torch.optim.AdamW's layout (one entry per parameter, named_parameters
+    order) so a checkpoint written here loads into the reference's optimizer and vice versa."""
 
-    def __init__(self, lr, weight_decay):
+    def __init__(self, lr, weight_decay, model_ref=None):
         self.param_groups = [{"lr": lr, "weight_decay": weight_decay, "betas": (0.9, 0.999), "eps": 1e-8}]
+        self._model_ref = model_ref
+
+    def _engine(self):
+        m = self._model_ref() if self._model_ref is not None else None
+        return getattr(m, "_engine", None)
+
+    def state_dict(self):
+        g = dict(self.param_groups[0])
+        e = self._engine()
+        n = len(list(self._model_ref().parameters())) if self._model_ref is not None else 0
+        state = {}
+        if e is not None:
+            steps = e.steps.cpu().tolist()
+            for i, (_, o, k) in enumerate(e.slots):
+                if steps[i] > 0:
+                    shape = e.param_views[i].shape
+                    state[i] = {"step": torch.tensor(float(steps[i])),
+                                "exp_avg": e.exp_avg[o:o + k].view(shape).detach().cpu().clone(),
+                                "exp_avg_sq": e.exp_avg_sq[o:o + k].view(shape).detach().cpu().clone()}
+        g.update(amsgrad=False, maximize=False, foreach=None, capturable=False, differentiable=False, fused=None,
+                 params=list(range(n)))
+        return {"state": state, "param_groups": [g]}
+
+    def load_state_dict(self, sd):
+        g = sd["param_groups"][0]
+        for k in ("lr", "weight_decay", "betas", "eps"):
+            if k in g:
+                self.param_groups[0][k] = tuple(g[k]) if k == "betas" else float(g[k])
+        self._pending = sd.get("state", {})
+        e = self._engine()
+        if e is not None:
+            self.push_state(e)
+
+    def push_state(self, e):
+        """Copy loaded moments into the engine's device buffers (called once the engine exists)."""
+        st = getattr(self, "_pending", None)
+        if not st:
+            return
+        steps = [0] * len(e.slots)
+        with torch.no_grad():
+            for i, (_, o, k) in enumerate(e.slots):
+                s = st.get(i, st.get(str(i)))
+                if s is None:
+                    continue
+                e.exp_avg[o:o + k].copy_(s["exp_avg"].reshape(-1).to(e.exp_avg))
+                e.exp_avg_sq[o:o + k].copy_(s["exp_avg_sq"].reshape(-1).to(e.exp_avg_sq))
+                steps[i] = int(float(s["step"]))
+            e.steps.copy_(torch.tensor(steps, dtype=torch.int32))
+        self._pending = None
 
 
 class _Plateau:
@@ -228,6 +280,17 @@ class _Plateau:
         self.opt, self.factor, self.patience, self.threshold, self.min_lr, self.eps = (
             opt, factor, patience, threshold, min_lr, eps)
         self.best, self.bad = float("inf"), 0
+
+    def state_dict(self):
+        return {"factor": self.factor, "patience": self.patience, "threshold": self.threshold,
+                "min_lrs": [self.min_lr], "eps": self.eps, "best": self.best, "num_bad_epochs": self.bad,
+                "mode": "min", "threshold_mode": "rel", "cooldown": 0, "cooldown_counter": 0}
+
+    def load_state_dict(self, sd):
+        self.factor, self.patience = float(sd["factor"]), int(sd["patience"])
+        self.threshold, self.eps = float(sd["threshold"]), float(sd["eps"])
+        self.min_lr = float(sd.get("min_lrs", [0.0])[0])
+        self.best, self.bad = float(sd["best"]), int(sd["num_bad_epochs"])
 
     def step(self, metric):
         if metric < self.best * (1 - self.threshold):
@@ -253,7 +316,7 @@ class ImprovedMiniCausalVAD:
     def __init__(self, device="cuda"):
         self.device = device
         self.model = CausalAnomalyDetector().to(device)
-        self.optimizer = _ParamGroups(lr=0.0005, weight_decay=0.001)
+        self.optimizer = _ParamGroups(lr=0.0005, weight_decay=0.001, model_ref=lambda: self.model)
         self.anomaly_weight, self.causal_weight, self.sparsity_weight, self.consistency_weight = 1.0, 0.01, 0.001, 0.01
         self.scheduler = _Plateau(self.optimizer, factor=0.5, patience=5)
         self.seed = 1234
@@ -274,6 +337,7 @@ class ImprovedMiniCausalVAD:
         videos = videos.to(self.device, dtype=torch.float32).contiguous()
         self.model.train()
         e = self.model.engine(videos)
+        self.optimizer.push_state(e)
         g = self.optimizer.param_groups[0]
         e.forward(videos, True, self.seed, self.global_step, self.clip0, with_loss=True)
         vals = e.losses.cpu().tolist()
@@ -319,3 +383,60 @@ class ImprovedMiniCausalVAD:
                    "avg_sparsity": float(np.mean(e / 256)),
                    "unique_graphs": len(np.unique(graphs.reshape(len(graphs), -1), axis=0))}
         return preds, graphs, metrics
+
+    def save_checkpoint(self, path, **extra):
+        """The a2:438-455 checkpoint dict: model / optimizer (/ scheduler) state plus caller extras (epoch, ...)."""
+        ck = {"model_state_dict": self.model.state_dict(), "optimizer_state_dict": self.optimizer.state_dict(),
+              "scheduler_state_dict": self.scheduler.state_dict()}
+        ck.update(extra)
+        torch.save(ck, str(path))
+
+    def load_checkpoint(self, path):
+        """Load an a2-format checkpoint (incl. the shipped best_improved_model.pth) or a bare state_dict.  Only
+        tensors and plain containers are read (weights_only=True)."""
+        ck = torch.load(str(path), map_location="cpu", weights_only=True)
+        sd = ck.get("model_state_dict", ck) if isinstance(ck, dict) else ck
+        self.model.load_state_dict(sd)
+        if isinstance(ck, dict) and "optimizer_state_dict" in ck:
+            self.optimizer.load_state_dict(ck["optimizer_state_dict"])
+        if isinstance(ck, dict) and "scheduler_state_dict" in ck:
+            self.scheduler.load_state_dict(ck["scheduler_state_dict"])
+        return ck
+
+
+class MiniCausalVAD(ImprovedMiniCausalVAD):
+    """The ``MiniCausalVAD`` surface avenue_training_script1.py drives (a1:19,104,141,160,180-181,187,210): ``.model``
+    (whose forward returns the (scores, adj, features) 3-tuple, a1:51), ``.device``, ``.optimizer.param_groups``
+    (a1:107-108), ``train_epoch(loader) -> (loss, components)`` with the anomaly/acyclicity/sparsity/consistency
+    keys (a1:141-154), ``evaluate(loader) -> (predictions, labels, causal_graphs)`` (a1:160,187) and
+    ``save_model/load_model(path)`` (a1:180-181,205,210).  The module a1 imports it from (``minicausal_vad``,
+    a1:20) is not in the reference repo, so this restates it on the a2 model and loss it shares its 16x16 causal
+    graph and loss keys with; the default lr 1e-3 is the one a1:107 treats as the constructor's.  Semantics beyond
+    a1's call sites are parity unpinned."""
+
+    def __init__(self, device="cuda", learning_rate=0.001):
+        super().__init__(device)
+        self.optimizer.param_groups[0]["lr"] = learning_rate
+
+    def train_epoch(self, dataloader):
+        return self.train_epoch_improved(dataloader)
+
+    def evaluate(self, dataloader):
+        self.model.eval()
+        preds, labels, graphs = [], [], []
+        with torch.no_grad():
+            for videos, y in dataloader:
+                videos = videos.to(self.device, dtype=torch.float32).contiguous()
+                s, adj, _ = self.model(videos)
+                preds.append(s.reshape(-1).cpu().numpy())
+                labels.append(np.asarray(torch.as_tensor(y).reshape(-1).cpu().numpy(), dtype=np.float32))
+                graphs.append(adj.cpu().numpy())
+        return np.concatenate(preds), np.concatenate(labels), np.concatenate(graphs)
+
+    def save_model(self, path):
+        self.save_checkpoint(path, global_step=self.global_step)
+
+    def load_model(self, path):
+        ck = self.load_checkpoint(path)
+        if isinstance(ck, dict) and "global_step" in ck:
+            self.global_step = int(ck["global_step"])
