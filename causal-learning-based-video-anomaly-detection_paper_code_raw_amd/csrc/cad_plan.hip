@@ -804,6 +804,22 @@ int vad_cad_bind(vad_cad_plan* plan, void* workspace, float* params, float* grad
   return 0;
 }
 
+namespace {
+struct CopyList {
+  uint32_t* dst[10];
+  const uint32_t* src[10];
+  int words[10];
+  int n;
+};
+// one block per entry; every entry is a whole number of 4-byte words (fp32 / int32 arrays)
+__global__ void __launch_bounds__(256) copy_list_kernel(CopyList L) {
+  const int e = blockIdx.x;
+  uint32_t* d = L.dst[e];
+  const uint32_t* s = L.src[e];
+  for (int i = threadIdx.x; i < L.words[e]; i += 256) d[i] = s[i];
+}
+}  // namespace
+
 int vad_cad_forward(vad_cad_plan* plan, const float* x, int training, uint64_t seed, uint64_t step, int64_t clip0,
                     const int64_t* labels, float* final_scores, float* probs, float* causal, float* kl, float* z,
                     float* adj, int32_t* nmax, float* boxes, int32_t* counts, float* losses, int32_t* flags,
@@ -819,21 +835,30 @@ int vad_cad_forward(vad_cad_plan* plan, const float* x, int training, uint64_t s
   c.labels = labels;
   c.losses_ptr = losses ? losses : c.sq_parts;  // scratch when not requested
   VAD_TRY(c.forward(x, st));
-  auto cp = [&](void* dst, const void* src, size_t bytes) -> int {
-    if (dst) VAD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
-    return 0;
-  };
+  // the ten small result arrays leave the plan in one launch (one block per array) instead of ten copy kernels
   const int B = c.B, NF = c.NF;
-  VAD_TRY(cp(final_scores, c.finalv, B * 4));
-  VAD_TRY(cp(probs, c.probs, B * 8));
-  VAD_TRY(cp(causal, c.causal, B * 4));
-  VAD_TRY(cp(kl, c.kl, B * 4));
-  VAD_TRY(cp(z, c.z, B * 30 * 4));
-  VAD_TRY(cp(adj, c.adj, B * 36 * 4));
-  VAD_TRY(cp(nmax, c.nmax, B * 4));
-  VAD_TRY(cp(boxes, c.boxes, (size_t)NF * 80));
-  VAD_TRY(cp(counts, c.counts, (size_t)NF * 4));
-  VAD_TRY(cp(flags, c.flags, 8));
+  CopyList L{};
+  auto cp = [&](void* dst, const void* src, size_t bytes) {
+    if (!dst) return;
+    L.dst[L.n] = (uint32_t*)dst;
+    L.src[L.n] = (const uint32_t*)src;
+    L.words[L.n] = (int)(bytes / 4);
+    ++L.n;
+  };
+  cp(final_scores, c.finalv, B * 4);
+  cp(probs, c.probs, B * 8);
+  cp(causal, c.causal, B * 4);
+  cp(kl, c.kl, B * 4);
+  cp(z, c.z, B * 30 * 4);
+  cp(adj, c.adj, B * 36 * 4);
+  cp(nmax, c.nmax, B * 4);
+  cp(boxes, c.boxes, (size_t)NF * 80);
+  cp(counts, c.counts, (size_t)NF * 4);
+  cp(flags, c.flags, 8);
+  if (L.n > 0) {
+    hipLaunchKernelGGL(copy_list_kernel, dim3(L.n), dim3(256), 0, st, L);
+    VAD_HIP(hipGetLastError());
+  }
   return 0;
 }
 
