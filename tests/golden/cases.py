@@ -29,6 +29,9 @@ CAD_CASES = [
     dict(name="forced_b2t4_64", B=2, T=4, H=64, W=64, seed=1, step=0, forced=FORCED_A),
     dict(name="forced_b3t5_96x80", B=3, T=5, H=96, W=80, seed=2, step=3, forced=FORCED_A),
     dict(name="fallback_b2t16_227", B=2, T=16, H=227, W=227, seed=3, step=0, forced=None),
+    # edge shapes: a single clip (batch statistics over T frames only) and single-frame clips (GRU over one step)
+    dict(name="forced_b1t3_64", B=1, T=3, H=64, W=64, seed=4, step=1, forced=FORCED_A),
+    dict(name="forced_b2t1_64", B=2, T=1, H=64, W=64, seed=5, step=0, forced=FORCED_A),
 ]
 
 # minicausal (config 1 family): scale > 1 multiplies the last classifier layer so the pre-clip grad norm exceeds 10
