@@ -309,6 +309,14 @@ LOSS_KEYS = ("anomaly_loss", "acyclicity_loss", "sparsity_loss", "consistency_lo
              "sparsity_ratio")
 
 
+def _check_batch(B):
+    """A single-clip batch fails in the reference: ``anomaly_scores.squeeze()`` is 0-d while the pseudo-targets are
+    (1,), and ``F.binary_cross_entropy`` raises (a2:139-147; reproduced by running the reference on B=1)."""
+    if B == 1:
+        raise ValueError("Using a target size (torch.Size([1])) that is different to the input size "
+                         "(torch.Size([])) is deprecated. Please ensure they have the same size.")
+
+
 class ImprovedMiniCausalVAD:
     """a2:107-297 on the HIP plan: model / optimizer / scheduler attributes, compute_improved_loss,
     train_epoch_improved, evaluate_improved."""
@@ -326,6 +334,7 @@ class ImprovedMiniCausalVAD:
     def compute_improved_loss(self, anomaly_scores, causal_adj, targets, features):
         """Loss of the model's last forward (the labels are ignored: pseudo-labels, a2:139-141).  Returns
         (total loss tensor with autograd into the model's backward, components dict)."""
+        _check_batch(anomaly_scores.shape[0])
         e = self.model._engine
         seed, step, clip0 = e.last_keys
         total = _A2LossFunction.apply(anomaly_scores, causal_adj, e, seed, step, clip0)
@@ -334,6 +343,7 @@ class ImprovedMiniCausalVAD:
 
     def train_step(self, videos, labels):
         """One a2:218-245 iteration fused on device (forward + loss + backward + clip + AdamW)."""
+        _check_batch(videos.shape[0])
         videos = videos.to(self.device, dtype=torch.float32).contiguous()
         self.model.train()
         e = self.model.engine(videos)

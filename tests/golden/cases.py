@@ -53,6 +53,8 @@ BBOX_CASES = [
     dict(name="t8", B=3, T=8, H=64, W=64, seed=30, step=0),
     dict(name="t16", B=2, T=16, H=64, W=64, seed=31, step=0),
     dict(name="t32_48x56", B=2, T=32, H=48, W=56, seed=32, step=0),
+    # a single clip: the reference's .squeeze() returns a 0-d score (bbox:101)
+    dict(name="t8_b1", B=1, T=8, H=64, W=64, seed=33, step=0),
 ]
 
 # cad1 memory autoencoder (causal_anomaly_detection1.py): one epoch of the reference's train_model over the label rows

@@ -89,3 +89,13 @@ def test_resume_equals_continue_gpu(tmp_path):
     preds, labels, graphs = b.evaluate([(xs[0], ys[0])])
     assert preds.shape == (B,) and labels.shape == (B,) and graphs.shape == (B, 16, 16)
     assert np.all(np.isfinite(preds))
+
+
+def test_single_clip_batch_raises_like_reference():
+    """B=1: the reference's BCE on a 0-d squeezed score vs (1,) pseudo-targets raises ValueError (a2:146)."""
+    from vad_amd.a2 import ImprovedMiniCausalVAD
+    vad = ImprovedMiniCausalVAD(device="cpu")
+    with pytest.raises(ValueError, match="target size"):
+        vad.train_step(torch.zeros(1, 3, 8, 64, 64), torch.zeros(1))
+    with pytest.raises(ValueError, match="target size"):
+        vad.compute_improved_loss(torch.zeros(1, 1), torch.zeros(1, 16, 16), torch.zeros(1), torch.zeros(1, 16))
