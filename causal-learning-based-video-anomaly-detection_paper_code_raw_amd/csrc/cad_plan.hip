@@ -597,12 +597,17 @@ struct CadPlanImpl {
   }
   float* losses_ptr = nullptr;
 
+  // stage -1: the whole backward.  stage 0: loss tail, causal head, direct classifier and detector (every
+  // non-backbone grad is final when it returns); stage 1: the backbone.  Splitting lets a data-parallel caller
+  // all-reduce the head grads while the backbone backward runs.
   int backward(bool use_loss, const float* dfin, const float* dprobs, const float* dcaus, const float* dkl,
-               const float* dz, const float* dadj, hipStream_t st) {
+               const float* dz, const float* dadj, hipStream_t st, int stage = -1) {
     ConvPrecision prec(conv_bf16);
     const CadLayout& LY = layout();
     VAD_CHECK(grads != nullptr, "backward: grads not bound");
     VAD_CHECK(!use_loss || labels != nullptr, "backward(use_loss): forward ran without labels");
+    VAD_CHECK(stage >= -1 && stage <= 1, "backward: stage must be -1, 0 or 1");
+    if (stage != 1) {
     // grads of frozen / never-used slots stay zero
     VAD_HIP(hipMemsetAsync(grads, 0, sizeof(float) * LY.param_floats, st));
     TailArgs t = use_loss ? tail_args(nullptr, nullptr, nullptr, nullptr) : tail_args(dfin, dprobs, dcaus, dkl);
@@ -637,6 +642,8 @@ struct CadPlanImpl {
     TIMED("det_bwd", dense_wgrad(ddh[0], NF, 512, feats, 6144, G(LY.det_w[0]), G(LY.det_b[0]), dense_scratch,
                                  dense_scratch_floats, flags, st));
     TIMED("det_bwd", dense_dgrad(ddh[0], NF, 512, P(LY.det_w[0]), 6144, d_feat_det, nullptr, 1.f, flags, st));
+    }
+    if (stage == 0) return 0;
     // backbone
     TIMED("avgpool_bwd", avgpool_bwd(d_feat_det, d_pooled, B, T, HF, WF, 256, dA, st));
     for (int l = 7; l >= 0; --l) {
@@ -866,6 +873,14 @@ int vad_cad_backward(vad_cad_plan* plan, int use_loss, const float* d_final, con
                      const float* d_causal, const float* d_kl, const float* d_z, const float* d_adj, void* stream) {
   VAD_CHECK(plan != nullptr, "vad_cad_backward: null plan");
   return plan->impl.backward(use_loss != 0, d_final, d_probs, d_causal, d_kl, d_z, d_adj, (hipStream_t)stream);
+}
+
+int vad_cad_backward_stage(vad_cad_plan* plan, int stage, int use_loss, const float* d_final, const float* d_probs,
+                           const float* d_causal, const float* d_kl, const float* d_z, const float* d_adj,
+                           void* stream) {
+  VAD_CHECK(plan != nullptr, "vad_cad_backward_stage: null plan");
+  return plan->impl.backward(use_loss != 0, d_final, d_probs, d_causal, d_kl, d_z, d_adj, (hipStream_t)stream,
+                             stage);
 }
 
 int vad_cad_optimizer_step(vad_cad_plan* plan, float lr, float beta1, float beta2, float eps, float weight_decay,

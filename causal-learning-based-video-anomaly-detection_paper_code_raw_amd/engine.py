@@ -184,11 +184,23 @@ class CadEngine:
         self._last = (pl, lab, x)
         return o
 
-    def backward(self, use_loss: bool, d_final=None, d_probs=None, d_causal=None, d_kl=None, d_z=None, d_adj=None):
+    def backward(self, use_loss: bool, d_final=None, d_probs=None, d_causal=None, d_kl=None, d_z=None, d_adj=None,
+                 stage: int = -1):
+        """stage -1: whole backward; 0: everything but the backbone (grads outside [0, backbone_floats) final);
+        1: the backbone (after stage 0)."""
         pl, lab, _ = self._last
         c = [t.contiguous() if t is not None else None for t in (d_final, d_probs, d_causal, d_kl, d_z, d_adj)]
-        nat.check(nat.lib().vad_cad_backward(pl.h, 1 if use_loss else 0, *[nat.ptr(t) for t in c],
-                                             nat.stream_of(self.device)))
+        if stage == -1:
+            nat.check(nat.lib().vad_cad_backward(pl.h, 1 if use_loss else 0, *[nat.ptr(t) for t in c],
+                                                 nat.stream_of(self.device)))
+        else:
+            nat.check(nat.lib().vad_cad_backward_stage(pl.h, stage, 1 if use_loss else 0, *[nat.ptr(t) for t in c],
+                                                       nat.stream_of(self.device)))
+
+    @property
+    def backbone_floats(self) -> int:
+        """Length of the backbone's leading run of slots in the flat buffers (named_parameters order)."""
+        return next(o for n, o in zip(self.slot_names, self.slot_offset) if not n.startswith("backbone."))
 
     def profile(self, enable: bool, only_prefix: str = "", reset: bool = True):
         """HIP-event timing of the plan's labelled launches (all plans of this engine).  enable=False pauses (the

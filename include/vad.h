@@ -77,6 +77,14 @@ int vad_cad_forward(vad_cad_plan* plan, const float* x, int training, uint64_t s
  * otherwise the given upstream grads (any may be NULL = zero).  Writes the flat grad buffer (all slots). */
 int vad_cad_backward(vad_cad_plan* plan, int use_loss, const float* d_final, const float* d_probs,
                      const float* d_causal, const float* d_kl, const float* d_z, const float* d_adj, void* stream);
+/* vad_cad_backward in two calls (same arguments; stage 0 then stage 1, both on the same stream): stage 0 runs the
+ * loss tail, the causal head, the direct classifier and the detector and zeroes the grad buffer first, so every
+ * grad outside the backbone slots is final when it returns; stage 1 runs the backbone (cad:141-158).  Replaces
+ * the single `total_loss.backward()` (cad:688) when a data-parallel caller overlaps the head-grad all-reduce with
+ * the backbone backward (DDP's bucketed reduce during backward). */
+int vad_cad_backward_stage(vad_cad_plan* plan, int stage, int use_loss, const float* d_final, const float* d_probs,
+                           const float* d_causal, const float* d_kl, const float* d_z, const float* d_adj,
+                           void* stream);
 /* clip_grad_norm_(max_norm) + AdamW over the flat buffers (torch.optim.AdamW semantics, per-slot steps,
  * slots without a grad this step are skipped).  grad_scale multiplies grads first (1/world for DP).
  * total_norm (device float [1], may be NULL) receives the pre-clip norm. */

@@ -227,3 +227,22 @@ def test_config4_shape_fp32_and_bf16(B, T, H, W):
         assert float(o["losses"][4]) == pytest.approx(float(res["losses"]["total"]), rel=1e-4 if fp32 else 2e-2)
         # (frozen-stem / no-grad slots are zero in both)
         assert float(g.norm()) == pytest.approx(ref_norm, rel=5e-3 if fp32 else 5e-2)
+
+
+def test_staged_backward_equals_whole_backward():
+    """vad_cad_backward_stage 0 then 1 (the DP overlap path) writes the same grads, bit for bit, as one backward;
+    after stage 0 every non-backbone grad is already final."""
+    case = CASES[1]
+    m, eng, o, grads, tn = _hip_step(case, step_opt=False)
+    B, T, H, W = case["B"], case["T"], case["H"], case["W"]
+    x = co.synth_clips(case["seed"], case["step"], 0, B, T, H, W).cuda()
+    y = co.synth_labels(0, B).cuda()
+    eng.forward(x, True, case["seed"], case["step"], 0, y)
+    eng.backward(True, stage=0)
+    torch.cuda.synchronize()
+    nb = eng.backbone_floats
+    assert 0 < nb < eng.param_floats
+    assert torch.equal(eng.grads[nb:eng.param_floats + 2], grads[nb:eng.param_floats + 2])
+    eng.backward(True, stage=1)
+    torch.cuda.synchronize()
+    assert torch.equal(eng.grads[:eng.param_floats + 2], grads[:eng.param_floats + 2])
