@@ -431,6 +431,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--prof-every", type=int, default=4, help="instrument every k-th timed step (roofline events)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="nccl (= RCCL over xGMI) for measurement; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--breakdown-out", default=None, help="write the per-kernel breakdown JSON here")
     args = ap.parse_args()
     args.config = args.config if args.config == "cad1" else int(args.config)
@@ -451,8 +453,14 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
+        if args.dist_backend == "gloo":
+            # rehearsal of the multi-rank path on fewer GPUs than ranks (ranks share devices round-robin)
+            local_rank %= torch.cuda.device_count()
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
     if args.config == "cad1":
         r = run_ae(args, rank, world, local_rank)
         if rank == 0:
