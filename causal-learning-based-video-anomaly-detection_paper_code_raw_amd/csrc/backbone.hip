@@ -14,7 +14,7 @@ namespace vad {
 // (k = 8*kk + 4*h + s), its B operand (weights of channel lane&31) lives in 28 registers for the whole block.
 // Epilogue: +bias, NHWC store (one 128-B row per pixel), per-block BN partial sums (deterministic).
 // =====================================================================================================
-constexpr int C1_RB = 8;
+constexpr int C1_RB = 6;  // 114 output rows at 227x227 = 19 full bands; 2432 blocks balance over 256 CUs
 constexpr int C1_CO = 32;
 constexpr int C1_K = 56;  // 49 taps padded to 7 MFMA sub-steps of 8
 
@@ -63,13 +63,14 @@ __global__ __launch_bounds__(256) void conv1_kernel(const float* __restrict__ x,
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
     for (int q = 0; q < 28; ++q) acc = mfma32(pp[koff[q]], wr[q], acc);
+    // the band's output pixels are contiguous in NHWC: the store address is linear in pi (no per-element divide)
+    float* yb = y + (((int64_t)img * OH + r0) * OW) * C1_CO + j;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int pi = t0 + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (pi < npix) {
-        const int py = pi / OW, px = pi - py * OW;
         const float v = acc[r] + bj;
-        y[(((int64_t)img * OH + r0 + py) * OW + px) * C1_CO + j] = v;
+        yb[(int64_t)pi * C1_CO] = v;
         s1 += v;
         s2 = fmaf(v, v, s2);
       }
