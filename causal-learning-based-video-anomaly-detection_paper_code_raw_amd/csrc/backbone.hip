@@ -36,16 +36,16 @@ __global__ __launch_bounds__(256) void conv1_kernel(const float* __restrict__ x,
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int j = lane & 31, h = lane >> 5;
-  // B operand: w[j][k] for k = 8*kk + 4*h + s, zero for k >= 49
+  // B operand: w[j][k] for k = 8*kk + 4*h + s, zero for k >= 49.  The A operand's patch offset of tap k,
+  // (k/7)*PW + k%7, is rebuilt per MFMA from compile-time row/col constants selected by h (no 28-register
+  // offset table: 4 instead of 3 waves per SIMD)
   float wr[28];
-  int koff[28];
 #pragma unroll
   for (int kk = 0; kk < 7; ++kk)
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       const int k = kk * 8 + 4 * h + s4;
       wr[kk * 4 + s4] = k < 49 ? w[j * 49 + k] : 0.f;
-      koff[kk * 4 + s4] = k < 49 ? (k / 7) * PW + (k % 7) : 0;
     }
   const float bj = bias[j];
   __syncthreads();
@@ -62,7 +62,12 @@ __global__ __launch_bounds__(256) void conv1_kernel(const float* __restrict__ x,
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-    for (int q = 0; q < 28; ++q) acc = mfma32(pp[koff[q]], wr[q], acc);
+    for (int q = 0; q < 28; ++q) {
+      const int k0 = (q >> 2) * 8 + (q & 3), k1 = k0 + 4;  // tap of lane half 0 / 1
+      const int kr = h ? (k1 < 49 ? k1 / 7 : 0) : (k0 < 49 ? k0 / 7 : 0);
+      const int kc = h ? (k1 < 49 ? k1 % 7 : 0) : (k0 < 49 ? k0 % 7 : 0);
+      acc = mfma32(pp[kr * PW + kc], wr[q], acc);
+    }
     // the band's output pixels are contiguous in NHWC: the store address is linear in pi (no per-element divide)
     float* yb = y + (((int64_t)img * OH + r0) * OW) * C1_CO + j;
 #pragma unroll
