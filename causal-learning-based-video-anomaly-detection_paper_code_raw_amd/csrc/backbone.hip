@@ -386,8 +386,8 @@ __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restric
   if (c >= C) return;
   const float sc = stats[2 * C + c], sh = stats[3 * C + c];
   const float* yi = y + (int64_t)img * H * W * C;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  {  // one output row i per blockIdx.z: 4x the blocks of a per-image grid, a quarter of the serial sums
+    const int i = blockIdx.z;
     const int h0 = ap_start(i, H, 4), h1 = ap_end(i, H, 4);
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
@@ -414,8 +414,8 @@ __global__ __launch_bounds__(256) void temporal_mean_kernel(const float* __restr
 
 int avgpool_fwd(const float* y, const float* stats, int B, int T, int H, int W, int C, float* feats, float* pooled,
                 hipStream_t st) {
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((unsigned)cdiv(C, 256), B * T), dim3(256), 0, st, y, stats, H, W, C,
-                     feats);
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((unsigned)cdiv(C, 256), B * T, 4), dim3(256), 0, st, y, stats, H, W,
+                     C, feats);
   VAD_LAUNCH_CHECK();
   const int64_t total = (int64_t)B * C * 24;
   hipLaunchKernelGGL(temporal_mean_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 1024)), dim3(256), 0,
