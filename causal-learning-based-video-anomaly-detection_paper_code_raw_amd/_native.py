@@ -16,6 +16,9 @@ _I64 = ctypes.c_int64
 _U64 = ctypes.c_uint64
 _U32 = ctypes.c_uint32
 _F = ctypes.c_float
+# int (*vad_bn_sync_fn)(void* user, int bn_layer, int phase, int64_t n, void* stream)
+BN_SYNC_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                              ctypes.c_void_p)
 
 _SIGS = {
     "vad_abi_version": (_I, []),
@@ -49,6 +52,7 @@ _SIGS = {
     "vad_cad_set_debug": (_I, [_P, ctypes.c_char_p, _I64]),
     "vad_cad_set_option": (_I, [_P, ctypes.c_char_p, _I64]),
     "vad_cad_conv_path": (_I, [_P, _I, _I]),
+    "vad_cad_set_bn_sync": (_I, [_P, BN_SYNC_FN, _P, _I]),
     "vad_u8_to_clip": (_I, [_P, _I64, _I, _P, _P]),
     "vad_resize_u8": (_I, [_P, _I, _I, _P, _I, _I]),
     "vad_debug_d2h": (_I, [_P, _P, _I64]),

@@ -24,6 +24,13 @@ int bn_bwd_finalize(const float* partials, int P, int C, double count, const flo
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
                  int* nparts, hipStream_t st);
 int bn_rows_parts(int M, int C);
+// SyncBatchNorm: [P][2C] partials -> [2C] double sums (+ optional float copies of the two halves); finalize from
+// (all-reduced) sums over `count` elements of the whole process group
+int bn_sum_partials(const float* partials, int P, int C, double* sums, float* a_out, float* b_out, hipStream_t st);
+int bn_finalize_sums(const double* sums, int C, double count, const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, float momentum, float eps, float* stats,
+                     hipStream_t st);
+int bn_bwd_finalize_sums(const double* sums, int C, double count, const float* gamma, float* stats, hipStream_t st);
 
 // ---------------------------------------------------------------- pools
 int maxpool3s2_bnrelu(const float* y, const float* stats, int NF, int H, int W, int C, float* out, int OH, int OW,

@@ -115,7 +115,8 @@ int conv1_fwd(const float* x, int NF, int H, int W, const float* w, const float*
 // BatchNorm finalize: combine partial sums in double; batch stats, affine folding, running-stat update
 // (momentum 0.1, unbiased variance for running_var; nn.BatchNorm2d train semantics).
 // =====================================================================================================
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ partials, int P, int C,
+template <typename PT>
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const PT* __restrict__ partials, int P, int C,
                                                           double count, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* running_mean,
                                                           float* running_var, float momentum, float eps,
@@ -163,8 +164,53 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
 int bn_finalize(const float* partials, int P, int C, double count, const float* gamma, const float* beta,
                 float* running_mean, float* running_var, float momentum, float eps, int training, float* stats,
                 hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, partials, P, C, count, gamma, beta,
+  hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3(C), dim3(256), 0, st, partials, P, C, count, gamma, beta,
                      running_mean, running_var, momentum, eps, training, stats);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int bn_finalize_sums(const double* sums, int C, double count, const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, float momentum, float eps, float* stats,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel<double>, dim3(C), dim3(256), 0, st, sums, 1, C, count, gamma, beta,
+                     running_mean, running_var, momentum, eps, 1, stats);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+// SyncBatchNorm support: fold a layer's [P][2C] float partials into [2C] double sums (the buffer the caller
+// all-reduces across ranks); optionally also writes them as float to a_out / b_out (the local dbeta / dgamma)
+__global__ __launch_bounds__(256) void bn_sum_partials_kernel(const float* __restrict__ partials, int P, int C,
+                                                              double* __restrict__ sums, float* a_out,
+                                                              float* b_out) {
+  const int c = blockIdx.x;
+  __shared__ double red[2][256];
+  double a = 0.0, b = 0.0;
+  for (int p = threadIdx.x; p < P; p += 256) {
+    a += (double)partials[(int64_t)p * 2 * C + c];
+    b += (double)partials[(int64_t)p * 2 * C + C + c];
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    sums[c] = red[0][0];
+    sums[C + c] = red[1][0];
+    if (a_out) a_out[c] = (float)red[0][0];
+    if (b_out) b_out[c] = (float)red[1][0];
+  }
+}
+
+int bn_sum_partials(const float* partials, int P, int C, double* sums, float* a_out, float* b_out, hipStream_t st) {
+  hipLaunchKernelGGL(bn_sum_partials_kernel, dim3(C), dim3(256), 0, st, partials, P, C, sums, a_out, b_out);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -244,7 +290,8 @@ int bn_bwd_reduce(const float* dA, const float* y, const float* stats, int M, in
   return 0;
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ partials, int P, int C,
+template <typename PT>
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const PT* __restrict__ partials, int P, int C,
                                                               double count, const float* __restrict__ gamma,
                                                               float* __restrict__ stats, float* dgamma,
                                                               float* dbeta, int training) {
@@ -278,8 +325,15 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
 
 int bn_bwd_finalize(const float* partials, int P, int C, double count, const float* gamma, float* stats,
                     float* dgamma, float* dbeta, int training, hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partials, P, C, count, gamma, stats, dgamma,
-                     dbeta, training);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3(C), dim3(256), 0, st, partials, P, C, count, gamma, stats,
+                     dgamma, dbeta, training);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int bn_bwd_finalize_sums(const double* sums, int C, double count, const float* gamma, float* stats, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, sums, 1, C, count, gamma, stats,
+                     nullptr, nullptr, 1);
   VAD_LAUNCH_CHECK();
   return 0;
 }

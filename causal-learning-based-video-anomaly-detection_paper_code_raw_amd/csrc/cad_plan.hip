@@ -319,6 +319,15 @@ struct CadPlanImpl {
   int16_t* chunk_slot;
   int64_t parts_floats, dense_scratch_floats, wpart_floats, slab_len, act_max;
   int64_t clip0 = 0;
+  // SyncBatchNorm (option): per-layer [2C] double sums are handed to the caller's callback (an all-reduce over the
+  // process group) between the partial-sum reduction and the finalize, forward and backward
+  vad_bn_sync_fn sync_fn = nullptr;
+  void* sync_user = nullptr;
+  int sync_world = 1;
+  double* bnsync = nullptr;
+  // backward-stage bookkeeping: forward resets it, stage 0 (or the whole backward) sets it; stage 1 requires it
+  // (stage 1 reads d_feat_det / d_pooled and the zeroed grads that stage 0 leaves)
+  int bwd_state = 0;
   int debug_stop_layer = -1;  // backward returns after this backbone layer (debug introspection)
   Profiler prof;
   char lbl[64];
@@ -396,6 +405,7 @@ struct CadPlanImpl {
     wpart_floats = 16ll << 20;
     wpart = w.take<float>(wpart_floats);
     sq_parts = w.take<float>(1024);
+    bnsync = w.take<double>(2 * 256);
     slot_info = w.take<float>(4 * 160);
     clip = w.take<float>(4);
     chunk_slot = w.take<int16_t>(LY.param_floats / 256 + 1);
@@ -520,6 +530,34 @@ struct CadPlanImpl {
 
   int conv_bf16 = 0;  // option "conv_bf16": 3x3 convs on bf16 operands (BASELINE config 4)
 
+  // batch statistics of BN layer i (0 = bn1) from the `np` partials in `parts`: local (default) or, with a sync
+  // callback in training mode, over the whole process group (torch.nn.SyncBatchNorm semantics)
+  int bn_fwd_stats(int i, int np, int C, double count, const float* gamma, const float* beta, hipStream_t st) {
+    if (sync_fn == nullptr || !training) {
+      TIMED("bn_fin", bn_finalize(parts, np, C, count, gamma, beta, RM(i), RV(i), 0.1f, 1e-5f, training, stats[i],
+                                  st));
+      return 0;
+    }
+    TIMED("bn_fin", bn_sum_partials(parts, np, C, bnsync, nullptr, nullptr, st));
+    VAD_CHECK(sync_fn(sync_user, i, 0, 2 * C, st) == 0, "BatchNorm sync callback failed (forward)");
+    TIMED("bn_fin", bn_finalize_sums(bnsync, C, count * sync_world, gamma, beta, RM(i), RV(i), 0.1f, 1e-5f, stats[i],
+                                     st));
+    return 0;
+  }
+  // backward of BN layer i: dgamma/dbeta from this rank's sums (the grad all-reduce adds the ranks), the mean terms
+  // from the group's sums when synchronised
+  int bn_bwd_stats(int i, int np, int C, double count, const float* gamma, float* dgamma, float* dbeta,
+                   hipStream_t st) {
+    if (sync_fn == nullptr || !training) {
+      TIMED("bn_bwd_fin", bn_bwd_finalize(parts, np, C, count, gamma, stats[i], dgamma, dbeta, training, st));
+      return 0;
+    }
+    TIMED("bn_bwd_fin", bn_sum_partials(parts, np, C, bnsync, dbeta, dgamma, st));
+    VAD_CHECK(sync_fn(sync_user, i, 1, 2 * C, st) == 0, "BatchNorm sync callback failed (backward)");
+    TIMED("bn_bwd_fin", bn_bwd_finalize_sums(bnsync, C, count * sync_world, gamma, stats[i], st));
+    return 0;
+  }
+
   int forward(const float* x, hipStream_t st) {
     ConvPrecision prec(conv_bf16);
     const CadLayout& LY = layout();
@@ -529,16 +567,15 @@ struct CadPlanImpl {
       TIMED("prep", conv3_prep_weights_all(8, w8, L, wf, wd, st));
     }
     int np = 0;
+    bwd_state = 0;
     TIMED("conv1", conv1_fwd(x, NF, H, W, P(LY.conv1_w), P(LY.conv1_b), y1, H1, W1, parts, &np, st));
-    TIMED("bn_fin", bn_finalize(parts, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), RM(0), RV(0), 0.1f,
-                                1e-5f, training, stats[0], st));
+    VAD_TRY(bn_fwd_stats(0, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), st));
     TIMED("maxpool", maxpool3s2_bnrelu(y1, stats[0], NF, H1, W1, 32, pool, HP, WP, st));
     const float* src = pool;
     const float* sst = nullptr;
     for (int l = 0; l < 8; ++l) {
       TIMED(L_("conv_fwd", l), conv3_fwd(L[l], src, sst, wf[l], P(LY.conv_b[l]), y[l], parts, &np, st));
-      TIMED("bn_fin", bn_finalize(parts, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]),
-                                  RM(l + 1), RV(l + 1), 0.1f, 1e-5f, training, stats[l + 1], st));
+      VAD_TRY(bn_fwd_stats(l + 1, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]), st));
       src = y[l];
       sst = stats[l + 1];
     }
@@ -607,6 +644,7 @@ struct CadPlanImpl {
     VAD_CHECK(grads != nullptr, "backward: grads not bound");
     VAD_CHECK(!use_loss || labels != nullptr, "backward(use_loss): forward ran without labels");
     VAD_CHECK(stage >= -1 && stage <= 1, "backward: stage must be -1, 0 or 1");
+    VAD_CHECK(bwd_state != 0 || stage != 1, "backward stage 1: stage 0 has not run for the current forward");
     if (stage != 1) {
     // grads of frozen / never-used slots stay zero
     VAD_HIP(hipMemsetAsync(grads, 0, sizeof(float) * LY.param_floats, st));
@@ -643,6 +681,7 @@ struct CadPlanImpl {
                                  dense_scratch_floats, flags, st));
     TIMED("det_bwd", dense_dgrad(ddh[0], NF, 512, P(LY.det_w[0]), 6144, d_feat_det, nullptr, 1.f, flags, st));
     }
+    bwd_state = 1;
     if (stage == 0) return 0;
     // backbone
     TIMED("avgpool_bwd", avgpool_bwd(d_feat_det, d_pooled, B, T, HF, WF, 256, dA, st));
@@ -651,8 +690,7 @@ struct CadPlanImpl {
       const int C = L[l].Co;
       int np = 0, nb = 0, ns = 0;
       TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st));
-      TIMED("bn_bwd_fin", bn_bwd_finalize(parts, np, C, (double)M, P(LY.bn_w[l]), stats[l + 1], G(LY.bn_w[l]),
-                                          G(LY.bn_b[l]), training, st));
+      VAD_TRY(bn_bwd_stats(l + 1, np, C, (double)M, P(LY.bn_w[l]), G(LY.bn_w[l]), G(LY.bn_b[l]), st));
       TIMED(L_("bn_bwd_apply", l), bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dY, bparts, &nb, st));
       const float* src = l == 0 ? pool : y[l - 1];
       const float* sst = l == 0 ? nullptr : stats[l];
@@ -908,6 +946,7 @@ int vad_cad_debug_buffer(vad_cad_plan* plan, const char* name, int idx, void** p
   else if (n == "d_pooled") { *ptr = c.d_pooled; *nfloats = (int64_t)c.B * 6144; }
   else if (n == "d_feat_det") { *ptr = c.d_feat_det; *nfloats = NF * 6144; }
   else if (n == "det_logits") { *ptr = c.dlog; *nfloats = NF * 20; }
+  else if (n == "bn_sync") { *ptr = c.bnsync; *nfloats = 2 * 2 * 256; }  // double [2*256]: 1024 float words
   else { vad::set_error("vad_cad_debug_buffer: unknown buffer " + n); return 1; }
   return 0;
 }
@@ -923,6 +962,15 @@ int vad_cad_set_option(vad_cad_plan* plan, const char* key, int64_t value) {
   VAD_CHECK(plan && key, "vad_cad_set_option: null argument");
   if (std::string(key) == "conv_bf16") plan->impl.conv_bf16 = value ? 1 : 0;
   else { vad::set_error("vad_cad_set_option: unknown key"); return 1; }
+  return 0;
+}
+
+int vad_cad_set_bn_sync(vad_cad_plan* plan, vad_bn_sync_fn fn, void* user, int world) {
+  VAD_CHECK(plan != nullptr, "vad_cad_set_bn_sync: null plan");
+  VAD_CHECK(fn == nullptr || world >= 1, "vad_cad_set_bn_sync: world must be >= 1");
+  plan->impl.sync_fn = fn;
+  plan->impl.sync_user = user;
+  plan->impl.sync_world = fn ? world : 1;
   return 0;
 }
 

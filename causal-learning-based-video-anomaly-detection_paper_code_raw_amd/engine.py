@@ -35,6 +35,34 @@ class _Plan:
         e = engine
         nat.check(L.vad_cad_bind(h, base, e.params.data_ptr(), e.grads.data_ptr(), e.bufs.data_ptr(),
                                  e.nbt.data_ptr(), nat.ptr(e.exp_avg), nat.ptr(e.exp_avg_sq), nat.ptr(e.steps)))
+        self._sync_cb = None
+        self.apply_bn_sync(engine)
+
+    def apply_bn_sync(self, engine):
+        """Install (or clear) the SyncBatchNorm callback: an all-reduce of the plan's [2C] double sums buffer over
+        the engine's process group, on the current stream."""
+        L = nat.lib()
+        if engine.bn_sync is None:
+            self._sync_cb = None
+            nat.check(L.vad_cad_set_bn_sync(self.h, nat.BN_SYNC_FN(), None, 1))
+            return
+        import torch.distributed as dist
+        group, world = engine.bn_sync
+        p, n = ctypes.c_void_p(), ctypes.c_int64()
+        nat.check(L.vad_cad_debug_buffer(self.h, b"bn_sync", 0, ctypes.byref(p), ctypes.byref(n)))
+        off = p.value - self.ws.data_ptr()
+        sums = self.ws[off:off + 4 * n.value].view(torch.float64)
+
+        def _cb(user, bn_layer, phase, count, stream):
+            try:
+                dist.all_reduce(sums[:count], group=group)
+                return 0
+            except Exception as exc:  # reported through the library's error path
+                print(f"vad bn sync (layer {bn_layer}, phase {phase}) failed: {exc!r}")
+                return 1
+
+        self._sync_cb = nat.BN_SYNC_FN(_cb)  # kept alive as long as the plan
+        nat.check(L.vad_cad_set_bn_sync(self.h, self._sync_cb, None, world))
 
     def rebind(self, engine):
         e = engine
@@ -98,6 +126,7 @@ class CadEngine:
                 self.nbt[i].copy_(named_bufs[k].reshape(()))
                 _set_buffer(model, k, self.nbt[i])
         self.exp_avg = self.exp_avg_sq = self.steps = None
+        self.bn_sync = None  # (process_group, world) in SyncBatchNorm mode
         self._compute_dtype = torch.float32
         self.plans = {}
         self.generation = 0
@@ -118,6 +147,20 @@ class CadEngine:
         self._compute_dtype = dt
         for p in self.plans.values():
             nat.check(nat.lib().vad_cad_set_option(p.h, b"conv_bf16", 1 if dt == torch.bfloat16 else 0))
+
+    def set_bn_sync(self, process_group=None, enable: bool = True):
+        """SyncBatchNorm mode: in training forwards every BatchNorm layer normalises with the statistics of the whole
+        process group's batch (and its backward uses the group's mean terms), so an N-rank step of B clips per rank
+        equals the reference's single-process step on the N*B-clip batch (cad:116,131,136 normalise over all B*T
+        frames).  enable=False restores per-rank statistics (DDP's default)."""
+        import torch.distributed as dist
+        if enable:
+            world = dist.get_world_size(process_group)
+            self.bn_sync = (process_group, world)
+        else:
+            self.bn_sync = None
+        for p in self.plans.values():
+            p.apply_bn_sync(self)
 
     def is_bound(self) -> bool:
         p = next(self.model.parameters())

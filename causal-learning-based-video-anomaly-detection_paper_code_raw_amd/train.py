@@ -32,10 +32,15 @@ class CadTrainer:
     Data parallel: one process per GPU; rank r processes global clips [r*B, (r+1)*B) of each step (RNG keyed by
     global clip index), grads (+ has-grad flags) are summed with one all_reduce and scaled by 1/world inside the
     optimizer kernel; BN running stats follow rank 0 (broadcast before each forward, DDP's broadcast_buffers).
+
+    sync_bn=True (world > 1): SyncBatchNorm semantics -- every BN layer normalises over the whole group's batch
+    (per-layer sums all-reduced in forward and backward), so the N-rank step equals the reference's single-process
+    step on the global batch (BASELINE config 3: batch 64 over 8 GPUs); running stats then agree on every rank and
+    are not broadcast.
     """
 
     def __init__(self, model, lr=3e-4, weight_decay=1e-5, eps=1e-8, betas=(0.9, 0.999), max_norm=1.0, seed=0,
-                 process_group=None, engine=None, compute_dtype=None):
+                 process_group=None, engine=None, compute_dtype=None, sync_bn=False):
         self.model = model
         if compute_dtype is not None:
             model.set_compute_dtype(compute_dtype)
@@ -47,17 +52,25 @@ class CadTrainer:
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if self.world > 1 else 0
         self.eng.init_optimizer_state()
+        self.sync_bn = bool(sync_bn) and self.world > 1
         if self.world > 1:
             dist.broadcast(self.eng.params, 0, group=process_group)
             dist.broadcast(self.eng.bufs, 0, group=process_group)
+        if self.sync_bn:
+            # the statistics travel on a communicator of their own, so on RCCL they are not queued behind the
+            # head-grad all-reduce that overlaps the backbone backward (_backward_overlapped)
+            ranks = dist.get_process_group_ranks(process_group) if process_group is not None else None
+            self._bn_pg = dist.new_group(ranks=ranks)
+            self.eng.set_bn_sync(self._bn_pg)
 
-    def step(self, videos, labels, lr=None):
-        """One training step; returns the (device) loss vector [cls, anomaly, causal, kl, total]."""
+    def step(self, videos, labels, lr=None, want_outputs=False):
+        """One training step; returns the (device) loss vector [cls, anomaly, causal, kl, total] (want_outputs: the
+        forward's output dict, see CadEngine.forward)."""
         eng = self.eng
         B = videos.shape[0]
-        if self.world > 1:
+        if self.world > 1 and not self.sync_bn:
             dist.broadcast(eng.bufs, 0, group=self.pg)
-        o = eng.forward(videos, True, self.seed, self.step_idx, self.rank * B, labels, want_outputs=False)
+        o = eng.forward(videos, True, self.seed, self.step_idx, self.rank * B, labels, want_outputs=want_outputs)
         if self.world > 1 and eng.grads.is_cuda:
             self._backward_overlapped()
         else:
@@ -67,7 +80,7 @@ class CadTrainer:
         eng.optimizer_step(self.lr if lr is None else lr, self.betas, self.eps, self.wd, self.max_norm,
                            1.0 / self.world)
         self.step_idx += 1
-        return o["losses"]
+        return o if want_outputs else o["losses"]
 
 
     def _backward_overlapped(self):

@@ -90,6 +90,15 @@ int vad_cad_backward_stage(vad_cad_plan* plan, int stage, int use_loss, const fl
  * total_norm (device float [1], may be NULL) receives the pre-clip norm. */
 int vad_cad_optimizer_step(vad_cad_plan* plan, float lr, float beta1, float beta2, float eps, float weight_decay,
                            float max_norm, float grad_scale, float* total_norm, void* stream);
+/* SyncBatchNorm mode (BASELINE config 3 parity with the reference's single-process global batch: its BatchNorm2d
+ * layers normalise over all B*T frames, cad:116,131,136).  In training mode each of the nine BN layers folds its
+ * partial sums into a per-plan double buffer `sums` ([2*C]: forward sum(x) | sum(x^2); backward sum(dZ) |
+ * sum(dZ*xhat)) and calls fn(user, bn_layer 0..8, phase 0 fwd / 1 bwd, n_doubles, stream); fn must replace the
+ * buffer by its sum over the process group (an all-reduce ordered on `stream`) and return 0.  Statistics then use
+ * world * local count.  The buffer's address: vad_cad_debug_buffer(plan, "bn_sync").  fn NULL = per-rank BN
+ * (DDP default). */
+typedef int (*vad_bn_sync_fn)(void* user, int bn_layer, int phase, int64_t n, void* stream);
+int vad_cad_set_bn_sync(vad_cad_plan* plan, vad_bn_sync_fn fn, void* user, int world);
 
 /* ------------------------------------------------------------------------------------------
  * Single building blocks (kernel unit tests; same kernels as the fused step)

@@ -29,6 +29,11 @@ class OracleEngine:
         self.bufs = torch.cat([sd[k].reshape(-1).clone() for k in self.buf_names])
         self.exp_avg = self.exp_avg_sq = self.steps = None
         self._last = None
+        self.bn_sync = None
+
+    def set_bn_sync(self, process_group=None, enable=True):
+        import torch.distributed as dist
+        self.bn_sync = (process_group if process_group is not None else dist.group.WORLD) if enable else None
 
     def _pdict(self):
         return {k: self.params[o:o + n].view(self.shapes[k]) for k, o, n in
@@ -54,7 +59,7 @@ class OracleEngine:
         p = {k: v.detach().clone().requires_grad_(not k.startswith(co.FROZEN_PREFIXES)) for k, v in self._pdict().items()}
         bufs = self._bdict()
         draws = co.CadDraws.make(seed, step, clip0, B, T)
-        out = co.cad_forward(p, bufs, x, draws, training=training)
+        out = co.cad_forward(p, bufs, x, draws, training=training, sync_group=self.bn_sync)
         losses = co.cad_losses(out, labels)
         self._last = (p, losses, out)
         lv = torch.stack([losses[k].detach() for k in ("classification", "anomaly", "causal", "kl", "total")])

@@ -32,6 +32,8 @@ CAD_CASES = [
     # edge shapes: a single clip (batch statistics over T frames only) and single-frame clips (GRU over one step)
     dict(name="forced_b1t3_64", B=1, T=3, H=64, W=64, seed=4, step=1, forced=FORCED_A),
     dict(name="forced_b2t1_64", B=2, T=1, H=64, W=64, seed=5, step=0, forced=FORCED_A),
+    # config-2 frame size with live detections (N>1 trajectories, detector and edge-MLP grads)
+    dict(name="forced_b2t16_227", B=2, T=16, H=227, W=227, seed=6, step=0, forced=FORCED_A),
 ]
 
 # minicausal (config 1 family): scale > 1 multiplies the last classifier layer so the pre-clip grad norm exceeds 10

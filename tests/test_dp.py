@@ -48,6 +48,47 @@ def _worker(rank, world, port, use_gpu, out_path):
         dist.destroy_process_group()
 
 
+def _sync_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vad_amd.cad import CausalAnomalyDetector
+        from vad_amd.train import CadTrainer
+        torch.manual_seed(0)
+        m = CausalAnomalyDetector()
+        x, y = make_batches(world, **SHAPE)[rank]
+        tr = CadTrainer(m, lr=3e-4, seed=0, engine=OracleEngine(m), sync_bn=True)
+        losses = tr.step(x, y)
+        torch.save({"losses": losses, "grads": tr.eng.grads.clone(), "bufs": tr.eng.bufs.clone()},
+                   f"{out_path}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_syncbn_protocol_cpu_gloo(tmp_path):
+    """CadTrainer(sync_bn=True) over 2 gloo ranks (oracle engine with its differentiable SyncBatchNorm) equals the
+    single-process step on the 2x-larger batch: mean of the ranks' losses, grads summed over ranks = 2 x the global
+    batch's grads, running stats identical on both ranks and equal to the global batch's."""
+    out = str(tmp_path / "sync")
+    mp.spawn(_sync_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = [torch.load(f"{out}.{r}", weights_only=True) for r in range(2)]
+    from vad_amd.cad import CausalAnomalyDetector
+    from oracle import cad_oracle as co
+    torch.manual_seed(0)
+    m = CausalAnomalyDetector()
+    eng = OracleEngine(m)
+    bt = make_batches(2, **SHAPE)
+    x = torch.cat([b[0] for b in bt])
+    y = torch.cat([b[1] for b in bt])
+    lv = eng.forward(x, True, 0, 0, 0, y)["losses"]
+    eng.backward(True)
+    np.testing.assert_allclose(((got[0]["losses"] + got[1]["losses"]) / 2).numpy(), lv.numpy(), rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(got[0]["grads"][:eng.param_floats].numpy(), 2 * eng.grads[:eng.param_floats].numpy(),
+                               rtol=1e-4, atol=2e-6)
+    for r in range(2):
+        np.testing.assert_allclose(got[r]["bufs"].numpy(), eng.bufs.numpy(), rtol=1e-5, atol=1e-6)
+
+
 def _run(use_gpu, tmp_path):
     out = str(tmp_path / "rank0.pt")
     mp.spawn(_worker, args=(2, _free_port(), use_gpu, out), nprocs=2, join=True)
@@ -77,3 +118,101 @@ def test_dp_hip_engine_gloo_two_ranks(tmp_path):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(got["params"].numpy(), eng.params.cpu().numpy())
     np.testing.assert_array_equal(got["bufs"].numpy(), eng.bufs.cpu().numpy())
+
+
+# ---------------------------------------------------------------- BASELINE config 3 per-rank shape, vs the oracle
+CFG3 = dict(B=8, T=16, H=227, W=227)
+
+
+def _cfg3_worker(rank, world, port, sync_bn, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import io
+        import contextlib
+        from vad_amd.cad import CausalAnomalyDetector
+        from vad_amd.train import CadTrainer, apply_memory_efficient_training
+        from tests.golden_util import hip_relu_masks
+        torch.manual_seed(0)
+        m = CausalAnomalyDetector()
+        with contextlib.redirect_stdout(io.StringIO()):
+            apply_memory_efficient_training(m)
+        m = m.cuda()
+        x, y = make_batches(world, **CFG3)[rank]
+        tr = CadTrainer(m, lr=3e-4, seed=0, sync_bn=sync_bn)
+        o = tr.step(x.cuda(), y.cuda(), want_outputs=True)
+        torch.cuda.synchronize()
+        masks = hip_relu_masks(tr.eng, CFG3["B"] * CFG3["T"])
+        torch.save({"final": o["final"].cpu(), "probs": o["probs"].cpu(), "losses": o["losses"].cpu(),
+                    "grads": tr.eng.grads.cpu(), "bufs": tr.eng.bufs.cpu(), "params": tr.eng.params.cpu(),
+                    "masks": [mk.clone() for mk in masks]}, f"{out_path}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def _cfg3_run(sync_bn, tmp_path):
+    out = str(tmp_path / "cfg3")
+    mp.spawn(_cfg3_worker, args=(2, _free_port(), sync_bn, out), nprocs=2, join=True)
+    return [torch.load(f"{out}.{r}", weights_only=True) for r in range(2)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sync_bn", [False, True], ids=["ddp", "syncbn"])
+def test_dp_config3_shape_vs_oracle(sync_bn, tmp_path):
+    """Two ranks on cuda:0 (gloo), 8 clips x T=16 x 227x227 per rank: BASELINE config 3's per-rank workload.
+    ddp: per-rank BatchNorm statistics (DDP default) vs the oracle run on each rank's micro-batch, grads summed.
+    syncbn: SyncBatchNorm mode vs the oracle's single-process step on the 16-clip global batch (the reference's
+    semantics at batch 64: BN over all B*T frames, cad:116,131,136).  Scores and losses within 1e-4; the summed
+    gradients within relative L2 1e-4 of the mask-pinned float64 oracle (ReLU decisions of the ranks' forwards);
+    running stats within 1e-4."""
+    from tests.golden_util import check_running_stats, pinned_oracle_grads, rel_l2
+    from tests.test_oracle_golden import is_pre_bn_bias
+    from oracle import cad_oracle as co
+    from vad_amd.cad import CausalAnomalyDetector
+    got = _cfg3_run(sync_bn, tmp_path)
+    batches = make_batches(2, **CFG3)
+    torch.manual_seed(0)
+    sd = {k: v.clone() for k, v in CausalAnomalyDetector().state_dict().items()}
+    B, T = CFG3["B"], CFG3["T"]
+    if sync_bn:
+        x = torch.cat([b[0] for b in batches])
+        y = torch.cat([b[1] for b in batches])
+        masks = [torch.cat([got[0]["masks"][l], got[1]["masks"][l]]) for l in range(8)]
+        grads, losses, res = pinned_oracle_grads(sd, x, y, co.CadDraws.make(0, 0, 0, 2 * B, T), masks)
+        scores = res["out"]["anomaly_scores"].detach()
+        np.testing.assert_allclose(torch.cat([g["final"] for g in got]).numpy(), scores.numpy(), rtol=1e-4, atol=1e-5)
+        mean_losses = (got[0]["losses"].double() + got[1]["losses"].double()) / 2
+        for i, k in enumerate(("classification", "anomaly", "causal", "kl", "total")):
+            assert float(mean_losses[i]) == pytest.approx(float(losses[k]), rel=1e-4, abs=1e-6), k
+        ref_g = grads
+        scale = 2.0  # sum over ranks of per-rank means = 2 x the gradient of the global mean
+        for r in range(2):  # every rank holds the group's running stats
+            check_running_stats(got[r]["bufs"], res["bufs"])
+    else:
+        ref_g, scale = {}, 1.0
+        for r in range(2):
+            x, y = batches[r]
+            grads, losses, res = pinned_oracle_grads(sd, x, y, co.CadDraws.make(0, 0, r * B, B, T), got[r]["masks"])
+            np.testing.assert_allclose(got[r]["final"].numpy(), res["out"]["anomaly_scores"].detach().numpy(),
+                                       rtol=1e-4, atol=1e-5)
+            for i, k in enumerate(("classification", "anomaly", "causal", "kl", "total")):
+                assert float(got[r]["losses"][i]) == pytest.approx(float(losses[k]), rel=1e-4, abs=1e-6), k
+            for n, gv in grads.items():
+                if gv is not None:
+                    ref_g[n] = ref_g.get(n, 0) + gv
+            if r == 0:  # running stats follow rank 0 (DDP broadcast_buffers)
+                check_running_stats(got[0]["bufs"], res["bufs"])
+    # the summed grads (what the all-reduce left on the ranks; identical on both)
+    from vad_amd import _native as nat
+    L = nat.lib()
+    names = [L.vad_cad_slot_name(i).decode() for i in range(L.vad_cad_num_slots())]
+    offs = [L.vad_cad_slot_offset(i) for i in range(len(names))]
+    nels = [L.vad_cad_slot_numel(i) for i in range(len(names))]
+    assert torch.equal(got[0]["grads"], got[1]["grads"])
+    gr = got[0]["grads"].numpy()
+    for n, o, k in zip(names, offs, nels):
+        ref = ref_g.get(n)
+        if ref is None or is_pre_bn_bias(n):
+            continue
+        e = rel_l2(gr[o:o + k], scale * ref.numpy())
+        assert e <= 1e-4, f"{n}: relative L2 {e:.3g}"
