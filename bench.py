@@ -78,6 +78,24 @@ def pmc_traffic(family):
     return fam["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
+def host_cpu_info(threads):
+    """Threads the CPU leg used, plus the host's logical CPU count and this process's affinity mask size."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"cores": threads, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff}
+
+
+def pmc_mfma_util(family):
+    """MFMA utilisation of a conv family from the latest committed rocprofv3 counter summary (tools/pmc_mfma.py:
+    SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_mfma.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        fam = json.load(f).get("families", {}).get(family)
+    return (round(fam["mfma_util"], 4), os.path.relpath(files[-1], ROOT)) if fam else (None, None)
+
+
 def run_gpu(args, rank, world, local_rank):
     import torch
     import torch.distributed as dist
@@ -93,7 +111,8 @@ def run_gpu(args, rank, world, local_rank):
         apply_memory_efficient_training(model)
     model = model.to(dev)
     trainer = CadTrainer(model, lr=3e-4, seed=1234,
-                         compute_dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32)
+                         compute_dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32,
+                         sync_bn=args.sync_bn)
     B, T, H, W = args.batch, args.T, args.H, args.W
     # synthetic clips resident in HBM before the timed region (device generator == oracle.rng.pixels_u8)
     pool = []
@@ -187,6 +206,10 @@ def run_gpu(args, rank, world, local_rank):
             roof["traffic"] = round(traffic)
             roof["traffic_unit"] = "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE)"
             roof["traffic_source"] = src
+        util, usrc = pmc_mfma_util(dominant)
+        if util is not None:
+            roof["mfma_util"] = util
+            roof["mfma_util_source"] = usrc
     step_ms = 1e3 * elapsed / args.steps
     # parity probe (rank 0): one more forward on the first batch with the trained weights; the CPU leg re-runs it on
     # the oracle (cpu_baseline) and reports the score difference and the frame-AUC of both
@@ -196,13 +219,39 @@ def run_gpu(args, rank, world, local_rank):
         torch.cuda.synchronize()
         probe = dict(state={k: v.detach().cpu().clone() for k, v in model.state_dict().items()},
                      final=o["final"].cpu(), probs=o["probs"].cpu(), loss=float(o["losses"][4]))
+    # input-inclusive leg (rank 0, N=1): the same step fed from pinned host u8 clips through ClipStager (H2D on a
+    # copy stream, batch k+1's copy overlapping step k, u8 -> fp32 on the device); never the headline value
+    h2d = None
+    if rank == 0 and world == 1 and args.h2d_steps > 0:
+        from vad_amd.data import ClipStager
+        stager = ClipStager(dev, mode=0)
+        u8 = [torch.randint(0, 256, (B, T, 1, H, W), dtype=torch.uint8).pin_memory() for _ in range(2)]
+        h = stager.issue(u8[0])
+        for i in range(2):  # warm-up
+            x = stager.finish(h)
+            h = stager.issue(u8[(i + 1) % 2])
+            trainer.step(x, labels)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.h2d_steps):
+            x = stager.finish(h)
+            h = stager.issue(u8[(i + 1) % 2])
+            trainer.step(x, labels)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        stager.finish(h)
+        torch.cuda.synchronize()
+        h2d = {"value": round(B * args.h2d_steps / el, 3), "unit": "clips/s", "steps": args.h2d_steps,
+               "ms_per_step": round(1e3 * el / args.h2d_steps, 4),
+               "bytes_h2d_per_step": B * T * H * W,
+               "path": "pinned u8 host clips -> ClipStager.issue (H2D, copy stream) -> finish (u8->fp32 on device)"}
     # whole-step algorithmic FLOP rate (all 3x3 convs fwd/dgrad/wgrad + conv1 fwd), for context
     conv_flops = sum(2.0 * NF * oh * ow * co * ci * 9 for NF, ci, co, oh, ow in conv_shapes(B, T, H, W))
     dgrad_flops = conv_flops - 2.0 * B * T * conv_shapes(B, T, H, W)[0][3] * conv_shapes(B, T, H, W)[0][4] * 32 * 32 * 9
     c1 = algorithmic_work("conv1", B, T, H, W)[1]
     step_flops = 2 * conv_flops + dgrad_flops + c1
     return dict(elapsed=elapsed, step_ms=step_ms, roof=roof, breakdown=breakdown, dominant=dominant,
-                final_loss=final_loss, step_tflops=step_flops / (step_ms * 1e-3) / 1e12, probe=probe)
+                final_loss=final_loss, step_tflops=step_flops / (step_ms * 1e-3) / 1e12, probe=probe, h2d=h2d)
 
 
 def parity_check(args, probe):
@@ -254,9 +303,10 @@ def cpu_baseline(args):
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds or n >= 40:
             break
-    return {"value": round(B * n / el, 3), "unit": "clips/s", "cores": threads, "kind": "port",
+    return {"value": round(B * n / el, 3), "unit": "clips/s", **host_cpu_info(threads), "kind": "port",
             "sample": f"{n} train steps of B={B} clips x T={T} x 1x{H}x{W} (oracle/cad_oracle.py, torch CPU fp32, "
-                      f"{threads} threads), after 1 warm-up step"}
+                      f"{threads} threads), after 1 warm-up step",
+            "validated": "profiles/r02_cpu_baseline_check.json (oracle vs the imported reference, same host)"}
 
 
 def run_bbox(args, rank, world, local_rank):
@@ -330,10 +380,103 @@ def bbox_cpu(args, r):
             if time.perf_counter() - t0 >= min(args.cpu_seconds, 6.0) or n >= 200:
                 break
         el = time.perf_counter() - t0
-    return ({"value": round(4 * n / el, 3), "unit": "clips/s", "cores": threads, "kind": "port",
+    return ({"value": round(4 * n / el, 3), "unit": "clips/s", **host_cpu_info(threads), "kind": "port",
              "sample": f"{n} forwards of 4 RGB clips x T=16 x 64x64 (oracle/bbox_oracle.py, torch CPU fp32, "
                        f"{threads} threads)"},
             {"max_abs_score_diff": diff, "tolerance": 1e-4, "sample": "first two clips of each T bucket"})
+
+
+BBOX_FLOP_PER_FRAME = 2 * 4096 * 32 * 81 + 2 * 1024 * 64 * 864 // 2  # conv3d 3->32 @64^2 + 32->64 @32^2 (T/2)
+BBOX_BYTES_PER_FRAME = 4 * (3 * 4096 + 2 * 32 * 4096 + 2 * 32 * 1024 // 2 + 2 * 64 * 1024 // 2)
+
+
+def bbox_roofline(frames_per_s):
+    """Config 5 (inference) against both ceilings SURVEY §8d names: fp32 FLOPs (the two Conv3d layers) and HBM bytes
+    (per-layer compulsory fp32 I/O: the clip, conv1's output written and read by the pool, the pool output written
+    and read by conv2, conv2's output written and read by the adaptive pool), per frame of a clip."""
+    tf = frames_per_s * BBOX_FLOP_PER_FRAME / 1e12
+    gbs = frames_per_s * BBOX_BYTES_PER_FRAME / 1e9
+    f_mfma, f_hbm = tf / PEAK_FP32_TFLOPS, gbs / PEAK_HBM_GBPS
+    gov = "mfma" if f_mfma >= f_hbm else "hbm"
+    return {"bound": gov, "kernel": "whole step",
+            "achieved": round(tf if gov == "mfma" else gbs, 3), "peak": PEAK_FP32_TFLOPS if gov == "mfma" else PEAK_HBM_GBPS,
+            "unit": "TFLOP/s" if gov == "mfma" else "GB/s", "frac": round(max(f_mfma, f_hbm), 4), "traffic": None,
+            "other_ceiling": {"unit": "GB/s" if gov == "mfma" else "TFLOP/s",
+                              "achieved": round(gbs if gov == "mfma" else tf, 3),
+                              "frac": round(f_hbm if gov == "mfma" else f_mfma, 4)},
+            "basis": f"{BBOX_FLOP_PER_FRAME} FLOP and {BBOX_BYTES_PER_FRAME} B (per-layer compulsory fp32 I/O) per frame"
+                     " x frames scored per second; governing = the ceiling with the larger fraction"}
+
+
+MC_TRAIN_FLOP_PER_CLIP = 566.3e6  # SURVEY §8d: minicausal train step, T=16, 64x64
+
+
+def run_mc(args, rank, world, local_rank):
+    """BASELINE config 1 (minicausal_vad_complete3.py): StableTrainer.train_epoch over 32 clips (T=16, 1x64x64,
+    x ~ U[0,1), labels alternating, batch 8: mc:503-599) on the HIP plan; one step = one epoch (4 iterations, with
+    the reference's per-iteration host reads of loss / NaN status / accuracy)."""
+    import torch
+    from vad_amd import _native as nat
+    from vad_amd.mc import SimpleVideoAnomalyDetector, StableTrainer
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    model = SimpleVideoAnomalyDetector(input_channels=1, temporal_frames=args.T, spatial_size=args.H)
+    n, bs = args.batch, 8
+    batches = []
+    for k in range(n // bs):
+        x = torch.empty(bs, 1, args.T, args.H, args.W, device=dev)
+        nat.check(nat.lib().vad_synth_frames(0, 0, (rank * n + k * bs) * args.T, bs * args.T, args.H * args.W, 1,
+                                             x.data_ptr(), nat.stream_of(dev)))
+        y = torch.tensor([1.0 if (rank * n + k * bs + b) % 2 == 0 else 0.0 for b in range(bs)], device=dev)
+        batches.append((x, y))
+    tr = StableTrainer(model, batches, [], dev, lr=1e-3)
+    for _ in range(args.warmup):
+        tr.train_epoch()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss, acc = tr.train_epoch()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    model.eval()
+    with torch.no_grad():
+        probe = model(batches[0][0]).reshape(-1).cpu()
+    state = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    return dict(elapsed=elapsed, step_ms=1e3 * elapsed / args.steps, loss=loss, probe=probe, state=state,
+                x0=batches[0][0].cpu())
+
+
+def mc_cpu(args, r):
+    """CPU leg of config 1: parity of the GPU eval scores (first batch, trained weights) against the oracle, and the
+    oracle's StableTrainer iteration (oracle/mc_oracle.py) over the 4 batches of an epoch, timed."""
+    import torch
+    from oracle import mc_oracle as mo
+    threads = torch.get_num_threads()
+    sd = r["state"]
+    params = {k: v for k, v in sd.items() if "running" not in k and "num_batches" not in k}
+    bufs = {k: v.clone() for k, v in sd.items() if "running" in k}
+    with torch.no_grad():
+        ref = mo.mc_forward(params, bufs, r["x0"], None, False).reshape(-1)
+    parity = {"max_abs_score_diff": float((ref - r["probe"]).abs().max()), "tolerance": 1e-4,
+              "sample": "eval forward of the first batch (8 clips) after the timed epochs"}
+    bs, T = 8, args.T
+    batches = [(mo.synth_clips(0, 0, k * bs, bs, T, args.H, args.W), mo.synth_labels(k * bs, bs))
+               for k in range(args.batch // bs)]
+    state = {}
+    p = {k: v.clone() for k, v in params.items()}
+    mo.mc_train_step(p, bufs, state, *batches[0], mo.McDraws.make(1, 0, 0, bs))
+    n, t0 = 0, time.perf_counter()
+    while True:
+        for k, (x, y) in enumerate(batches):
+            mo.mc_train_step(p, bufs, state, x, y, mo.McDraws.make(1, n + 1, k * bs, bs))
+        n += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds or n >= 50:
+            break
+    el = time.perf_counter() - t0
+    return ({"value": round(args.batch * n / el, 3), "unit": "clips/s", **host_cpu_info(threads), "kind": "port",
+             "sample": f"{n} epochs of {args.batch} clips (batch {bs}) x T={T} x 1x{args.H}x{args.W} "
+                       f"(oracle/mc_oracle.py mc_train_step, torch CPU fp32, {threads} threads)"}, parity)
 
 
 def ae_flops_per_clip(T):
@@ -408,7 +551,7 @@ def ae_cpu(args, r):
         if time.perf_counter() - t0 >= args.cpu_seconds or n >= 100:
             break
     el = time.perf_counter() - t0
-    return ({"value": round(B * n / el, 3), "unit": "clips/s", "cores": threads, "kind": "port",
+    return ({"value": round(B * n / el, 3), "unit": "clips/s", **host_cpu_info(threads), "kind": "port",
              "sample": f"{n} train steps of B={B} clips x T={T} x 1x64x64 (oracle/ae_oracle.py, torch CPU fp32, "
                        f"{threads} threads), after 1 warm-up step"}, parity)
 
@@ -418,8 +561,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="2", choices=("2", "4", "5", "cad1"),
-                    help="BASELINE config: 2 = T=16 227x227 fp32 (default), 4 = T=32 256x256 bf16 convs, "
+    ap.add_argument("--config", default="2", choices=("1", "2", "4", "5", "cad1"),
+                    help="BASELINE config: 1 = minicausal StableTrainer epoch over 32 clips T=16 64x64, "
+                         "2 = T=16 227x227 fp32 (default), 4 = T=32 256x256 bf16 convs, "
                          "5 = bbox clip scorer, mixed T (inference); cad1 = the causal_anomaly_detection1.py "
                          "memory autoencoder train step (SURVEY §8f, not a BASELINE config)")
     ap.add_argument("--batch", type=int, default=8, help="clips per GPU")
@@ -434,10 +578,16 @@ def main():
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="nccl (= RCCL over xGMI) for measurement; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--breakdown-out", default=None, help="write the per-kernel breakdown JSON here")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="N>1: SyncBatchNorm mode (BN over the global batch = the reference's single-process step)")
+    ap.add_argument("--h2d-steps", type=int, default=10,
+                    help="steps of the input-inclusive leg (pinned u8 clips through ClipStager; 0 = skip)")
     args = ap.parse_args()
     args.config = args.config if args.config == "cad1" else int(args.config)
-    preset = {2: (16, 227, 227, "fp32"), 4: (32, 256, 256, "bf16"), 5: (0, 64, 64, "fp32"),
+    preset = {1: (16, 64, 64, "fp32"), 2: (16, 227, 227, "fp32"), 4: (32, 256, 256, "bf16"), 5: (0, 64, 64, "fp32"),
               "cad1": (16, 64, 64, "fp32")}[args.config]
+    if args.config == 1 and args.batch == 8:
+        args.batch = 32  # clips per epoch per rank (BASELINE config 1)
     if args.config == 5 and args.batch == 8:
         args.batch = 64  # clips per rank
     if args.config == "cad1" and args.batch == 8:
@@ -461,6 +611,27 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group("gloo")
+    if args.config == 1:
+        r = run_mc(args, rank, world, local_rank)
+        if rank == 0:
+            cpu, parity = (None, None) if (args.no_cpu_baseline or world > 1) else mc_cpu(args, r)
+            clips = world * args.batch * args.steps
+            tflops = MC_TRAIN_FLOP_PER_CLIP * clips / r["elapsed"] / 1e12
+            print(json.dumps({
+                "metric": BASELINE_METRIC, "value": round(clips / r["elapsed"], 3), "unit": "clips/s",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["step_ms"], 4),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+                "data": "synthetic grayscale clips (keyed-hash u8 / 255), labels alternating; random-init weights "
+                        "(torch.manual_seed(0))",
+                "config": {"workload": "minicausal_vad_complete3.py StableTrainer epoch (mc:249-330), BASELINE "
+                                       "config 1", "clips_per_gpu": args.batch, "batch": 8, "clip_len": args.T,
+                           "frame": f"1x{args.H}x{args.W}", "parallelism": f"dp{world}",
+                           "step": "one epoch (4 iterations)"},
+                "roofline": {"bound": "mfma", "kernel": "whole step", "achieved": round(tflops, 3),
+                             "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_FP32_TFLOPS, 4),
+                             "traffic": None, "basis": "566.3 MFLOP per train clip (SURVEY §8d) x clips / time"},
+                "cpu_baseline": cpu, "parity": parity, "final_loss": r["loss"]}), flush=True)
+        return
     if args.config == "cad1":
         r = run_ae(args, rank, world, local_rank)
         if rank == 0:
@@ -501,7 +672,8 @@ def main():
                                        "(inference)", "clips_per_gpu": args.batch, "clip_len": "8/16/32 mixed",
                            "frame": "3x64x64", "packing": "one batch per T", "parallelism": f"dp{world}",
                            "frames_per_step_per_gpu": r["frames"]},
-                "roofline": None, "cpu_baseline": cpu, "parity": parity}), flush=True)
+                "roofline": bbox_roofline(world * r["frames"] / (r["step_ms"] * 1e-3)),
+                "cpu_baseline": cpu, "parity": parity}), flush=True)
         if world > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
@@ -531,6 +703,8 @@ def main():
             "roofline": r["roof"],
             "cpu_baseline": cpu,
             "parity": parity,
+            "h2d_inclusive": r.get("h2d"),
+            "bn_stats": "group (SyncBatchNorm)" if (args.sync_bn and world > 1) else "per rank",
             "step_algorithmic_tflops": round(r["step_tflops"], 3),
             "final_loss": r["final_loss"],
         }

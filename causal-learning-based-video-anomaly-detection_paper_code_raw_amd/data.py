@@ -141,8 +141,11 @@ class FrameFolderClipsMC(torch.utils.data.Dataset):
 class ClipStager:
     """Pinned u8 staging ring + H2D copies on a dedicated stream + on-device u8 -> fp32 conversion.
 
-    ``stage(batch_u8)`` returns the fp32 device tensor (same shape) ready on the current stream; the copy of the
-    next batch can be issued while the current step runs.  mode 0: (u8 - 0.5) / 0.5 (cad), 1: u8 / 255 (mc/bbox)."""
+    Two halves, so the copy of batch k+1 overlaps step k: ``issue(batch_u8)`` puts the batch into a pinned ring slot
+    (skipped when the batch is already pinned) and enqueues its H2D copy on the copy stream, ordered only after the
+    previous conversion out of the same device slot (not after the compute stream's other work); ``finish(handle)``
+    makes the current stream wait for that copy and converts it to the fp32 device clip.  ``stage(batch)`` =
+    ``finish(issue(batch))``.  mode 0: (u8 - 0.5) / 0.5 (cad), 1: u8 / 255 (mc/bbox)."""
 
     def __init__(self, device, mode=0, depth=2):
         self.device = torch.device(device)
@@ -150,52 +153,72 @@ class ClipStager:
         self.mode = mode
         self.depth = depth
         self.copy_stream = torch.cuda.Stream(self.device)
-        self._ring = []  # (pinned u8, device u8, copy-done event)
+        self._ring = []  # [pinned u8, device u8, copy-done event, read-done event]
         self._k = 0
 
     def _slot(self, shape):
         if len(self._ring) <= self._k or tuple(self._ring[self._k][0].shape) != tuple(shape):
-            slot = (torch.empty(shape, dtype=torch.uint8, pin_memory=True),
-                    torch.empty(shape, dtype=torch.uint8, device=self.device), torch.cuda.Event())
+            slot = [torch.empty(shape, dtype=torch.uint8, pin_memory=True),
+                    torch.empty(shape, dtype=torch.uint8, device=self.device), torch.cuda.Event(), torch.cuda.Event()]
             if len(self._ring) <= self._k:
                 self._ring.append(slot)
             else:
                 self._ring[self._k] = slot
         return self._ring[self._k]
 
-    def stage(self, batch_u8: torch.Tensor) -> torch.Tensor:
+    def issue(self, batch_u8: torch.Tensor):
+        """Start the H2D copy of one u8 batch; returns the handle for finish()."""
         if batch_u8.dtype != torch.uint8:
-            raise TypeError("ClipStager.stage expects a uint8 batch")
-        pinned, dev, done = self._slot(batch_u8.shape)
-        done.synchronize()  # the previous copy out of this pinned buffer has finished
-        pinned.copy_(batch_u8)
-        cur = torch.cuda.current_stream(self.device)
-        self.copy_stream.wait_stream(cur)  # the device buffer's previous reader (u8 -> fp32) is done
+            raise TypeError("ClipStager.issue expects a uint8 batch")
+        slot = self._slot(batch_u8.shape)
+        pinned, dev, copied, read = slot
+        if batch_u8.is_pinned():
+            src = batch_u8
+        else:
+            copied.synchronize()  # the previous H2D out of this pinned buffer has finished
+            pinned.copy_(batch_u8)
+            src = pinned
+        self.copy_stream.wait_event(read)  # the previous u8 -> fp32 conversion out of this device slot is done
         with torch.cuda.stream(self.copy_stream):
-            dev.copy_(pinned, non_blocking=True)
-            done.record(self.copy_stream)
-        cur.wait_event(done)
-        out = torch.empty(batch_u8.shape, dtype=torch.float32, device=self.device)
+            dev.copy_(src, non_blocking=True)
+            copied.record(self.copy_stream)
+        self._k = (self._k + 1) % self.depth
+        return slot
+
+    def finish(self, handle) -> torch.Tensor:
+        """The fp32 device clip of an issued batch, ready on the current stream."""
+        _, dev, copied, read = handle
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(copied)
+        out = torch.empty(dev.shape, dtype=torch.float32, device=self.device)
         nat.check(nat.lib().vad_u8_to_clip(dev.data_ptr(), dev.numel(), self.mode, out.data_ptr(),
                                            nat.stream_of(self.device)))
-        self._k = (self._k + 1) % self.depth
+        read.record(cur)
         return out
+
+    def stage(self, batch_u8: torch.Tensor) -> torch.Tensor:
+        return self.finish(self.issue(batch_u8))
 
 
 def prefetch(loader, stager: ClipStager):
-    """Iterate (device clips, device labels) one batch ahead: batch k+1 is staged before batch k is yielded.
-    uint8 batches go through the stager; float batches (the reference's own datasets) are copied as they are."""
-    def put(x, y):
-        xd = stager.stage(x) if x.dtype == torch.uint8 else x.to(stager.device, non_blocking=True)
+    """Iterate (device clips, device labels) one batch ahead: the H2D copy of batch k+1 is issued before batch k is
+    yielded (it runs on the copy stream while step k computes) and converted when batch k+1 is yielded.  uint8
+    batches go through the stager; float batches (the reference's own datasets) are copied as they are."""
+    def issue(x, y):
+        h = stager.issue(x) if x.dtype == torch.uint8 else x
+        return h, y
+
+    def finish(h, y):
+        xd = stager.finish(h) if not isinstance(h, torch.Tensor) else h.to(stager.device, non_blocking=True)
         return xd, y.to(stager.device, non_blocking=True)
 
     it = iter(loader)
     try:
-        nxt = put(*next(it))
+        pending = issue(*next(it))
     except StopIteration:
         return
     for x, y in it:
-        cur = nxt
-        nxt = put(x, y)
+        cur = finish(*pending)
+        pending = issue(x, y)
         yield cur
-    yield nxt
+    yield finish(*pending)

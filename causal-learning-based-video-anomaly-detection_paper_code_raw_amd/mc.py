@@ -207,26 +207,74 @@ class McEngine:
                                                   self.stream()))
 
 
+class _AdamSurface:
+    """The torch.optim.Adam surface StableTrainer exposes (mc:229-234): ``param_groups[0]['lr']`` is the live learning
+    rate the device step uses (the reference's driver prints it every epoch, mc:414) and may be written; the Adam
+    moments themselves live in the engine's flat device buffers.  ``zero_grad`` is a no-op (the fused step writes
+    every grad)."""
+
+    def __init__(self, lr, weight_decay=1e-5, eps=1e-8, betas=(0.9, 0.999)):
+        self.param_groups = [{"lr": lr, "initial_lr": lr, "weight_decay": weight_decay, "eps": eps, "betas": betas}]
+        self.defaults = dict(self.param_groups[0])
+
+    def zero_grad(self, set_to_none=True):
+        pass
+
+
+class _StepLRSurface:
+    """optim.lr_scheduler.StepLR(optimizer, step_size=15, gamma=0.7) (mc:237): ``step()`` once per epoch."""
+
+    def __init__(self, optimizer, step_size=15, gamma=0.7):
+        self.optimizer, self.step_size, self.gamma = optimizer, step_size, gamma
+        self.base_lrs = [g["initial_lr"] for g in optimizer.param_groups]
+        self.last_epoch = 0
+
+    def step(self):
+        self.last_epoch += 1
+        for g, b in zip(self.optimizer.param_groups, self.base_lrs):
+            g["lr"] = b * self.gamma ** (self.last_epoch // self.step_size)
+
+    def get_last_lr(self):
+        return [g["lr"] for g in self.optimizer.param_groups]
+
+    def state_dict(self):
+        return {"step_size": self.step_size, "gamma": self.gamma, "base_lrs": list(self.base_lrs),
+                "last_epoch": self.last_epoch, "_last_lr": self.get_last_lr()}
+
+    def load_state_dict(self, sd):
+        self.step_size, self.gamma = sd["step_size"], sd["gamma"]
+        self.base_lrs, self.last_epoch = list(sd["base_lrs"]), sd["last_epoch"]
+
+
 class StableTrainer:
     """mc:218-420 with the train step on the HIP plan.  ``train_epoch`` / ``evaluate`` / ``train_model`` keep the
-    reference's return values and history keys."""
+    reference's return values and history keys; ``optimizer`` / ``scheduler`` / ``criterion`` keep its attributes
+    (Adam lr/wd 1e-5/eps 1e-8, StepLR(15, 0.7), BCELoss; mc:229-240)."""
 
     def __init__(self, model, train_loader, test_loader, device, lr=0.001):
         self.model = model.to(device)
         self.train_loader = train_loader
         self.test_loader = test_loader
         self.device = torch.device(device)
-        self.lr = lr
-        self.base_lr = lr
-        self.epoch = 0
+        self.optimizer = _AdamSurface(lr, weight_decay=1e-5, eps=1e-8)
+        self.scheduler = _StepLRSurface(self.optimizer, step_size=15, gamma=0.7)
+        self.criterion = nn.BCELoss()
         self.history = {"train_loss": [], "test_loss": [], "test_auc": [], "train_acc": [], "test_acc": []}
         self.best_auc = 0.0
         self.seed = 1234
         self.global_step = 0
         self.clip0 = 0
 
+    @property
+    def lr(self):
+        return self.optimizer.param_groups[0]["lr"]
+
+    @property
+    def epoch(self):
+        return self.scheduler.last_epoch
+
     def _lr(self):
-        return self.base_lr * (0.7 ** (self.epoch // 15))  # StepLR(step_size=15, gamma=0.7) per epoch (mc:238)
+        return self.optimizer.param_groups[0]["lr"]
 
     def train_step(self, data, targets):
         """One mc:259-318 iteration on device; returns (loss, correct, n, counted) as host numbers."""
@@ -236,7 +284,8 @@ class StableTrainer:
         e = self.model.engine(data)
         e.forward(data, True, self.seed, self.global_step, self.clip0, labels=targets)
         e.backward()
-        e.optimizer_step(self._lr())
+        g = self.optimizer.param_groups[0]
+        e.optimizer_step(self._lr(), wd=g["weight_decay"], b1=g["betas"][0], b2=g["betas"][1], eps=g["eps"])
         self.global_step += 1
         self.clip0 += data.shape[0]
         out = e.scores
@@ -291,7 +340,7 @@ class StableTrainer:
         for epoch in range(epochs):
             train_loss, train_acc = self.train_epoch()
             test_loss, test_auc, test_acc = self.evaluate()
-            self.epoch += 1
+            self.scheduler.step()
             for k, v in zip(("train_loss", "test_loss", "test_auc", "train_acc", "test_acc"),
                             (train_loss, test_loss, test_auc, train_acc, test_acc)):
                 self.history[k].append(v)

@@ -13,13 +13,22 @@ import os
 import sys
 
 
+def _targs(name):
+    """Template arguments of a demangled kernel name, e.g. 'k<1, 2, true, 3>(...)' -> ['1', '2', 'true', '3']."""
+    a = name.find("<")
+    b = name.find(">", a)
+    return [t.strip() for t in name[a + 1:b].split(",")] if a >= 0 and b > a else []
+
+
 def family(name):
     if "conv3x3_wgrad_patch_kernel" in name or ("gemm_kernel" in name and "ConvPatchKM" in name):
         return "conv_wgrad"
     if "conv3x3_wgrad_x3_kernel" in name:
         return "conv_wgrad"
-    if "conv3x3_patch_kernel" in name or "conv3x3_x3_kernel" in name:
-        return "conv_fwd" if ", true>" in name else "conv_dgrad"
+    if "conv3x3_x3_kernel" in name:  # <S, NI, TH, TW, NT, PC, FWD, NP>
+        return "conv_fwd" if _targs(name)[6:7] == ["true"] else "conv_dgrad"
+    if "conv3x3_patch_kernel" in name:
+        return "conv_fwd" if "true" in _targs(name) else "conv_dgrad"
     if "conv3x3_dgrad_s2_kernel" in name or ("gemm_kernel" in name and "EpiConvDgrad" in name):
         return "conv_dgrad"
     if "gemm_kernel" in name and "EpiConvFwd" in name:
