@@ -15,12 +15,15 @@ int conv1_num_parts(int NF, int OH);
 int bn_finalize(const float* partials, int P, int C, double count, const float* gamma, const float* beta,
                 float* running_mean, float* running_var, float momentum, float eps, int training, float* stats,
                 hipStream_t st);
-// stats layout per layer: [0:C) mean, [C:2C) invstd, [2C:3C) scale, [3C:4C) shift, [4C:5C) k (bwd),
-//                         [5C:6C) mean(dZ), [6C:7C) mean(dZ*xhat)
+// stats layout per layer (BN_STATS_PER_C = 7): [0:C) mean, [C:2C) invstd, [2C:3C) scale, [3C:4C) shift,
+//   [4C:5C) k (bwd), [5C:6C) mean(dZ), [6C:7C) mean(dZ*xhat)
 int bn_bwd_reduce(const float* dA, const float* y, const float* stats, int M, int C, float* partials, int* nparts,
                   hipStream_t st);
+// when dbias is given, also the gradient of the conv bias in front of the BN: the sum over pixels of dY (zero up to
+// rounding in training mode)
 int bn_bwd_finalize(const float* partials, int P, int C, double count, const float* gamma, float* stats,
-                    float* dgamma, float* dbeta, int training, hipStream_t st);
+                    float* dgamma, float* dbeta, int training, hipStream_t st, float* dbias = nullptr);
+// bias_partials may be null (the conv bias grad then comes from bn_bwd_finalize's dbias)
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
                  int* nparts, hipStream_t st);
 int bn_rows_parts(int M, int C);
@@ -30,7 +33,8 @@ int bn_sum_partials(const float* partials, int P, int C, double* sums, float* a_
 int bn_finalize_sums(const double* sums, int C, double count, const float* gamma, const float* beta,
                      float* running_mean, float* running_var, float momentum, float eps, float* stats,
                      hipStream_t st);
-int bn_bwd_finalize_sums(const double* sums, int C, double count, const float* gamma, float* stats, hipStream_t st);
+int bn_bwd_finalize_sums(const double* sums, int C, double count, const float* gamma, float* stats, hipStream_t st,
+                         float* dbias = nullptr);
 
 // ---------------------------------------------------------------- pools
 int maxpool3s2_bnrelu(const float* y, const float* stats, int NF, int H, int W, int C, float* out, int OH, int OW,

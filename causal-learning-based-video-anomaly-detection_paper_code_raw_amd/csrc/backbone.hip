@@ -294,7 +294,7 @@ template <typename PT>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const PT* __restrict__ partials, int P, int C,
                                                               double count, const float* __restrict__ gamma,
                                                               float* __restrict__ stats, float* dgamma,
-                                                              float* dbeta, int training) {
+                                                              float* dbeta, int training, float* dbias) {
   const int c = blockIdx.x;
   __shared__ double red[2][256];
   double a = 0.0, b = 0.0;
@@ -316,24 +316,31 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const PT* __restri
     const double sdz = red[0][0], sdzx = red[1][0];
     if (dgamma) dgamma[c] = (float)sdzx;
     if (dbeta) dbeta[c] = (float)sdz;
+    const double inv = stats[C + c];
+    const double k = (double)gamma[c] * inv;
     stats[4 * C + c] = gamma[c] * stats[C + c];
     // eval mode: BN is the affine map of the running stats, no batch-mean terms in its backward
-    stats[5 * C + c] = training ? (float)(sdz / count) : 0.f;
-    stats[6 * C + c] = training ? (float)(sdzx / count) : 0.f;
+    const double mdz = training ? sdz / count : 0.0, mdzx = training ? sdzx / count : 0.0;
+    stats[5 * C + c] = (float)mdz;
+    stats[6 * C + c] = (float)mdzx;
+    // conv bias grad = sum of dY = k (sum dZ - count mean(dZ)) - k invstd mean(dZ xhat) sum(y - mean); the last
+    // sum is zero by the definition of the mean, the first vanishes in training mode up to rounding
+    if (dbias) dbias[c] = (float)(k * (sdz - count * mdz));
   }
 }
 
 int bn_bwd_finalize(const float* partials, int P, int C, double count, const float* gamma, float* stats,
-                    float* dgamma, float* dbeta, int training, hipStream_t st) {
+                    float* dgamma, float* dbeta, int training, hipStream_t st, float* dbias) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3(C), dim3(256), 0, st, partials, P, C, count, gamma, stats,
-                     dgamma, dbeta, training);
+                     dgamma, dbeta, training, dbias);
   VAD_LAUNCH_CHECK();
   return 0;
 }
 
-int bn_bwd_finalize_sums(const double* sums, int C, double count, const float* gamma, float* stats, hipStream_t st) {
+int bn_bwd_finalize_sums(const double* sums, int C, double count, const float* gamma, float* stats, hipStream_t st,
+                         float* dbias) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, sums, 1, C, count, gamma, stats,
-                     nullptr, nullptr, 1);
+                     nullptr, nullptr, 1, dbias);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -369,7 +376,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     }
     *reinterpret_cast<f32x4*>(dY + (int64_t)r * C + c) = o;
   }
-  bn_block_reduce_store(v, C, bparts + (int64_t)blockIdx.x * 2 * C);
+  if (bparts) bn_block_reduce_store(v, C, bparts + (int64_t)blockIdx.x * 2 * C);
 }
 
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,

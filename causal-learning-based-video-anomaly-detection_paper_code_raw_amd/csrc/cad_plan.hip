@@ -314,7 +314,7 @@ struct CadPlanImpl {
   int *counts, *nmax, *clip_flags, *flags;
   float *d_causal, *d_kl, *d_glog, *d_dlog, *slabs, *d_feat_det, *d_pooled, *dense_scratch;
   float *dg[5], *ddh[5];
-  float *dA, *dY, *bparts, *wpart;
+  float *dA, *dY, *wpart;
   float *sq_parts, *slot_info, *clip;
   int16_t* chunk_slot;
   int64_t parts_floats, dense_scratch_floats, wpart_floats, slab_len, act_max;
@@ -352,7 +352,7 @@ struct CadPlanImpl {
       act_max = std::max<int64_t>(act_max, nf * L[l].OH * L[l].OW * L[l].Co);
     }
     const int cs[9] = {32, 32, 32, 64, 64, 128, 128, 256, 256};
-    for (int l = 0; l < 9; ++l) stats[l] = w.take<float>(7 * cs[l]);
+    for (int l = 0; l < 9; ++l) stats[l] = w.take<float>(BN_STATS_PER_C * cs[l]);
     parts_floats = std::max<int64_t>((int64_t)conv1_num_parts(NF, H1) * 64, 1024);
     for (int l = 0; l < 8; ++l) {
       const int64_t M = nf * L[l].OH * L[l].OW;
@@ -401,7 +401,6 @@ struct CadPlanImpl {
     dense_scratch = w.take<float>(dense_scratch_floats);
     dA = w.take<float>(act_max);
     dY = w.take<float>(act_max);
-    bparts = w.take<float>(parts_floats);  // same bound as parts: ceil(M/64) blocks x 2C per layer
     wpart_floats = 16ll << 20;
     wpart = w.take<float>(wpart_floats);
     sq_parts = w.take<float>(1024);
@@ -547,14 +546,14 @@ struct CadPlanImpl {
   // backward of BN layer i: dgamma/dbeta from this rank's sums (the grad all-reduce adds the ranks), the mean terms
   // from the group's sums when synchronised
   int bn_bwd_stats(int i, int np, int C, double count, const float* gamma, float* dgamma, float* dbeta,
-                   hipStream_t st) {
+                   float* dbias, hipStream_t st) {
     if (sync_fn == nullptr || !training) {
-      TIMED("bn_bwd_fin", bn_bwd_finalize(parts, np, C, count, gamma, stats[i], dgamma, dbeta, training, st));
+      TIMED("bn_bwd_fin", bn_bwd_finalize(parts, np, C, count, gamma, stats[i], dgamma, dbeta, training, st, dbias));
       return 0;
     }
     TIMED("bn_bwd_fin", bn_sum_partials(parts, np, C, bnsync, dbeta, dgamma, st));
     VAD_CHECK(sync_fn(sync_user, i, 1, 2 * C, st) == 0, "BatchNorm sync callback failed (backward)");
-    TIMED("bn_bwd_fin", bn_bwd_finalize_sums(bnsync, C, count * sync_world, gamma, stats[i], st));
+    TIMED("bn_bwd_fin", bn_bwd_finalize_sums(bnsync, C, count * sync_world, gamma, stats[i], st, dbias));
     return 0;
   }
 
@@ -683,20 +682,20 @@ struct CadPlanImpl {
     }
     bwd_state = 1;
     if (stage == 0) return 0;
-    // backbone
+    // backbone (BatchNorm backward as streaming passes: the conv kernels are MFMA/LDS-bound and slowed down more by
+    // extra loads than the separate 6 TB/s passes cost -- DESIGN.md §6, BN-backward fusion experiment)
     TIMED("avgpool_bwd", avgpool_bwd(d_feat_det, d_pooled, B, T, HF, WF, 256, dA, st));
     for (int l = 7; l >= 0; --l) {
       const int64_t M = (int64_t)NF * L[l].OH * L[l].OW;
       const int C = L[l].Co;
       int np = 0, nb = 0, ns = 0;
       TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st));
-      VAD_TRY(bn_bwd_stats(l + 1, np, C, (double)M, P(LY.bn_w[l]), G(LY.bn_w[l]), G(LY.bn_b[l]), st));
-      TIMED(L_("bn_bwd_apply", l), bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dY, bparts, &nb, st));
+      VAD_TRY(bn_bwd_stats(l + 1, np, C, (double)M, P(LY.bn_w[l]), G(LY.bn_w[l]), G(LY.bn_b[l]), G(LY.conv_b[l]), st));
+      TIMED(L_("bn_bwd_apply", l), bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dY, nullptr, &nb, st));
       const float* src = l == 0 ? pool : y[l - 1];
       const float* sst = l == 0 ? nullptr : stats[l];
       TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dY, src, sst, wpart, &ns, wpart_floats, st));
-      TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], wpart, ns, bparts, nb, G(LY.conv_w[l]), G(LY.conv_b[l]),
-                                                     st));
+      TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], wpart, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
       if (l > 0) TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dY, wd[l], dA, st));
       if (l == debug_stop_layer) return 0;
     }
@@ -938,7 +937,7 @@ int vad_cad_debug_buffer(vad_cad_plan* plan, const char* name, int idx, void** p
   if (n == "y1") { *ptr = c.y1; *nfloats = NF * c.H1 * c.W1 * 32; }
   else if (n == "pool") { *ptr = c.pool; *nfloats = NF * c.HP * c.WP * 32; }
   else if (n == "y" && idx >= 0 && idx < 8) { *ptr = c.y[idx]; *nfloats = act(idx); }
-  else if (n == "stats" && idx >= 0 && idx < 9) { *ptr = c.stats[idx]; *nfloats = 7 * cs[idx]; }
+  else if (n == "stats" && idx >= 0 && idx < 9) { *ptr = c.stats[idx]; *nfloats = BN_STATS_PER_C * cs[idx]; }
   else if (n == "feats") { *ptr = c.feats; *nfloats = NF * 6144; }
   else if (n == "pooled") { *ptr = c.pooled; *nfloats = (int64_t)c.B * 6144; }
   else if (n == "dA") { *ptr = c.dA; *nfloats = c.act_max; }

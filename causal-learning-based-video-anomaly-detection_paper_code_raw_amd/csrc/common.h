@@ -122,6 +122,9 @@ __device__ inline float wave_sum(float v) {
 // trainers' NaN checks, mc:281 / a2:230)
 __device__ inline float relu_nan(float v) { return v > 0.f ? v : (v == v ? 0.f : v); }
 
+// BatchNorm state per layer: [7C] floats (backbone.h: mean | invstd | scale | shift | k | mean(dZ) | mean(dZ xhat))
+constexpr int BN_STATS_PER_C = 7;
+
 __device__ inline f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }

@@ -356,7 +356,7 @@ struct McPlanImpl {
       cols[s] = w.take<float>(g[s].rows() * g[s].K());
       y[s] = w.take<float>(V * Co);
       pooled[s] = w.take<float>(pooled_vol[s].numel());
-      stats[s] = w.take<float>(7 * Co);
+      stats[s] = w.take<float>(BN_STATS_PER_C * Co);
       max_y = std::max(max_y, V * Co);
       max_pool = std::max(max_pool, pooled_vol[s].numel());
       if (s > 0) max_dcols = std::max(max_dcols, g[s].rows() * g[s].K());

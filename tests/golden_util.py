@@ -77,7 +77,7 @@ def hip_relu_masks(eng, NF):
     masks = []
     for l in range(8):
         st = read_debug(pl, "stats", l + 1)
-        C = st.size // 7
+        C = st.size // 7  # BN stats layout [7C] (csrc/common.h BN_STATS_PER_C)
         y = read_debug(pl, "y", l).astype(np.float64).reshape(NF, -1, C)
         z = y * st[2 * C:3 * C].astype(np.float64) + st[3 * C:4 * C].astype(np.float64)
         masks.append(torch.from_numpy(z > 0).permute(0, 2, 1))  # (NF, C, OH*OW); pinned_oracle_grads reshapes
