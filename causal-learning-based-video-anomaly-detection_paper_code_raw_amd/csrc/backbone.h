@@ -68,6 +68,7 @@ int conv3_patch_dgrad(const Conv3Layer& L, const float* dY, const float* wd, flo
 extern int g_conv_split;  // 0 disables them (f32 MFMA patch kernels)
 extern int g_x3_nt;       // output channels per block: 0 auto, 1 -> 32, 2 -> 64
 extern int g_x3_dbg;      // measurement-only bits (X3Args::dbg)
+extern int g_x3_wres;     // 32-channel stride-1 layers: all split weights resident in LDS (1, default) or restaged
 // bf16-operand mode of the split kernels (one plane, one bf16 product per K step, fp32 accumulation): BASELINE
 // config 4's bf16 compute.  Thread-local, set for the duration of a plan call by ConvPrecision.
 extern thread_local int g_conv_bf16;

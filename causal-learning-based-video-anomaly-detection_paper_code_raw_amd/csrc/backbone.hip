@@ -763,6 +763,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_split") g_conv_split = value;
   else if (k == "conv_split_nt") g_x3_nt = value;
   else if (k == "conv_split_dbg") g_x3_dbg = value;
+  else if (k == "conv_split_wres") g_x3_wres = value;
   else if (k == "conv_wgrad_patch") g_tune.wgrad_patch = value;
   else if (k == "conv_wgrad_split") g_wgrad_split = value;
   else if (k == "conv_bf16") g_conv_bf16 = value;  // ops API only (calling thread); plans use their own option

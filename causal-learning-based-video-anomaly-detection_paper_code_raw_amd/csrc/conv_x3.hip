@@ -76,7 +76,10 @@ __device__ __forceinline__ void put_planes(__bf16* d, int pitch, const float* v,
   }
 }
 
-template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP>
+// WCH > 1: the block keeps the split weights of all WCH reduction chunks resident in LDS (staged during its first
+// tile, p.C == WCH * PC) instead of restaging the chunk's slice for every (tile, chunk) item -- the weight split is
+// most of the staging VALU of the 32-channel layers
+template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1>
 __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
   static_assert(NP == 3 || NP == 1, "three split planes (fp32 numerics) or one (bf16 operands)");
   static_assert(NI * TH * TW == 128, "a block owns 128 output pixels");
@@ -85,7 +88,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
   constexpr int NC = 32 * NT, G8 = PC / 8;
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3, PROWS = NI * PH * PW, PWE = (PW + 1) / 2;
   constexpr int RP = NP * PC + 8;      // patch row: NP planes x PC + 16 B pad (odd number of 16-B units)
-  constexpr int WP = 9 * NP * PC + 8;  // weight row: 9 taps x NP planes x PC + pad
+  constexpr int WCS = 9 * NP * PC;      // one chunk's weight row segment: 9 taps x NP planes x PC
+  constexpr int WP = WCH * WCS + 8;     // weight row: WCH segments + pad
   static_assert(((RP * 2 / 16) & 1) && ((WP * 2 / 16) & 1), "odd 16-B row pitch");
   __shared__ __attribute__((aligned(16))) __bf16 sm[PROWS * RP + NC * WP];
   __bf16* patch = sm;
@@ -197,7 +201,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
             v[e] = wv[it][0][e];
             v[4 + e] = wv[it][1][e];
           }
-          put_planes<NP>(wl + n * WP + t * NP * PC + g8 * 8, PC, v, false);
+          put_planes<NP>(wl + n * WP + (WCH > 1 ? (c0 / PC) * WCS : 0) + t * NP * PC + g8 * 8, PC, v, false);
         }
       }
     }
@@ -215,13 +219,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
   if (nitems > 0) fetch(t0, 0, true);
   for (int item = 0; item < nitems; ++item) {
     const int tile = t0 + item / nch, ch = item % nch, c0 = ch * PC;
-    const bool wnow = (nch > 1 && !(p.dbg & 1)) || item == 0;
+    const bool wnow = WCH > 1 ? item < nch : ((nch > 1 && !(p.dbg & 1)) || item == 0);
+    const int wseg = WCH > 1 ? ch * WCS : 0;
     __syncthreads();  // the previous item's fragment reads are done
     stash(tile, c0, wnow);
     __syncthreads();
     if (item + 1 < nitems) {
       const int nx = item + 1;
-      fetch(t0 + nx / nch, (nx % nch) * PC, nch > 1 && !(p.dbg & 1));
+      fetch(t0 + nx / nch, (nx % nch) * PC, WCH > 1 ? nx < nch : (nch > 1 && !(p.dbg & 1)));
     }
     if (ch == 0) {
 #pragma unroll
@@ -243,7 +248,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
           for (int q = 0; q < NP; ++q)
-            b[nt][q] = *reinterpret_cast<const bf16x8*>(bbase + nt * 32 * WP + (t * NP + q) * PC + kk * 16);
+            b[nt][q] = *reinterpret_cast<const bf16x8*>(bbase + nt * 32 * WP + wseg + (t * NP + q) * PC + kk * 16);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
           if constexpr (NP == 3) acc[nt] = mfma_x3(a, b[nt], acc[nt]);
@@ -299,8 +304,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
   }
 }
 
-template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP>
+template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1>
 static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
+  VAD_CHECK(WCH == 1 || a.C == WCH * PC, "conv3x3_x3: resident weights need C == WCH * PC");
   a.tiles_h = (int)cdiv(a.OH, TH);
   a.tiles_w = (int)cdiv(a.OW, TW);
   a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);
@@ -309,7 +315,7 @@ static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   a.tpb = (int)cdiv(a.ntiles, target);
   a.dbg = g_x3_dbg;
   const int gx = (int)cdiv(a.ntiles, a.tpb);
-  VAD_KLAUNCH((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD, NP>), dim3(gx, ny), dim3(256), 0, st, a);
+  VAD_KLAUNCH((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD, NP, WCH>), dim3(gx, ny), dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   if (nparts) *nparts = gx;
   return 0;
@@ -320,8 +326,16 @@ thread_local int g_conv_bf16 = 0;  // bf16-operand convs (one plane, one product
 int g_x3_nt = 0;       // tuning knob "conv_split_nt": 0 = auto, 1 / 2 = force 32 / 64 output channels per block
 int g_x3_dbg = 0;      // knob "conv_split_dbg" (measurement only, see X3Args::dbg)
 
+int g_x3_wres = 1;  // knob "conv_split_wres": 32-channel stride-1 layers keep all split weights resident in LDS
+
 template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD>
 static int launch_x3(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
+  if constexpr (S == 1 && NT == 1) {
+    if (g_x3_wres && a.C == 2 * PC) {
+      if (g_conv_bf16) return launch_np<S, NI, TH, TW, NT, PC, FWD, 1, 2>(a, max_blocks, st, nparts);
+      return launch_np<S, NI, TH, TW, NT, PC, FWD, 3, 2>(a, max_blocks, st, nparts);
+    }
+  }
   if (g_conv_bf16) return launch_np<S, NI, TH, TW, NT, PC, FWD, 1>(a, max_blocks, st, nparts);
   return launch_np<S, NI, TH, TW, NT, PC, FWD, 3>(a, max_blocks, st, nparts);
 }
