@@ -146,21 +146,21 @@ class _CadFunction(torch.autograd.Function):
         o = engine.forward(x, training, seed, step, clip0)
         ctx.engine = engine
         ctx.generation = engine.generation
-        ctx.mark_non_differentiable(o["nmax"], o["boxes"], o["counts"])
+        ctx.mark_non_differentiable(o["nmax"], o["counts"])
         return o["final"], o["probs"], o["causal"], o["kl"], o["z"], o["adj"], o["nmax"], o["boxes"], o["counts"]
 
     @staticmethod
-    def backward(ctx, d_final, d_probs, d_causal, d_kl, d_z, d_adj, *_):
+    def backward(ctx, d_final, d_probs, d_causal, d_kl, d_z, d_adj, d_nmax, d_boxes, d_counts):
         eng = ctx.engine
         if eng.generation != ctx.generation:
             raise RuntimeError("libvadhip keeps the activations of the most recent forward only: call backward "
                                "before running the model again")
-        eng.backward(False, d_final, d_probs, d_causal, d_kl, d_z, d_adj)
+        eng.backward(False, d_final, d_probs, d_causal, d_kl, d_z, d_adj, d_boxes=d_boxes)
         flags = eng.grads[eng.param_floats:eng.param_floats + 2].tolist()
         grads = []
         for i, g in enumerate(eng.slot_group):
             live = (g == _eng.GROUP_ALWAYS or (g == _eng.GROUP_DET and flags[0] > 0)
-                    or (g == _eng.GROUP_STRUCT and flags[1] > 0))
+                    or (g == _eng.GROUP_STRUCT and flags[1] > 0) or (g == _eng.GROUP_FROZEN and eng.stem_grad_on))
             grads.append(eng.grad_view(i).view(eng.model_param_shapes[i]).clone() if live else None)
         return (None, None, None, None, None, None, *grads)
 

@@ -9,6 +9,12 @@ namespace vad {
 int conv1_fwd(const float* x, int NF, int H, int W, const float* w, const float* b, float* y, int OH, int OW,
               float* partials, int* nparts, hipStream_t st);
 int conv1_num_parts(int NF, int OH);
+// stem backward: conv1 weight gradient (dW [32][49] torch layout; slab >= NF * ceil(OH/6) * 32 * 49 floats of
+// per-block partials) and the MaxPool2d(3,2,1) backward over relu(bn1(y)) (first-maximum rule)
+int conv1_wgrad(const float* x, int NF, int H, int W, const float* dy, int OH, int OW, float* slab,
+                int64_t slab_cap, float* dw, hipStream_t st);
+int maxpool3s2_bwd(const float* y, const float* stats, const float* dpool, int NF, int H, int W, int C, int OH,
+                   int OW, float* dA, hipStream_t st);
 
 // ---------------------------------------------------------------- BatchNorm (training mode)
 // partials: [P][2*C] (sum | sumsq).  Writes mean/invstd/scale/shift [C] and updates running stats.

@@ -99,6 +99,160 @@ __global__ __launch_bounds__(256) void conv1_kernel(const float* __restrict__ x,
 
 int conv1_num_parts(int NF, int OH) { return NF * (int)cdiv(OH, C1_RB); }
 
+// =====================================================================================================
+// Stem backward (only when backbone.conv1 / bn1 train: the module API without apply_memory_efficient_training,
+// cad:115-116,145-147; train_model freezes them, cad:592-598)
+// =====================================================================================================
+// conv1 weight gradient: dW[c][tap] = sum over output pixels of dY[p][c] * xpad[patch_p + tap], as f32 MFMA with
+// M = 32 channels, K = pixels (two per MFMA), N = taps (two tiles: 0..31, 32..48).  One block per (frame, band of
+// C1_RB output rows), the zero-padded input band staged in LDS as in the forward; the 4 waves take interleaved
+// pixel pairs and are combined in a fixed order; each block writes its [32][49] partial to slab[blockIdx.x].
+__global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restrict__ x, int H, int W,
+                                                          const float* __restrict__ dy, int OH, int OW, int bands,
+                                                          float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int img = blockIdx.x / bands, band = blockIdx.x % bands;
+  const int r0 = band * C1_RB;
+  const int PW = 2 * OW + 6, PH = 2 * C1_RB + 5;
+  float* patch = sm;
+  float* red = sm + ((PH * PW + 3) & ~3);  // [4 waves][2 tiles][16][64]
+  const float* xi = x + (int64_t)img * H * W;
+  for (int i = threadIdx.x; i < PH * PW; i += 256) {
+    const int pr = i / PW, pc = i - pr * PW;
+    const int ih = 2 * r0 - 3 + pr, iw = pc - 3;
+    patch[i] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? xi[(int64_t)ih * W + iw] : 0.f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int rows = min(C1_RB, OH - r0), npix = rows * OW;
+  const float* dyb = dy + (((int64_t)img * OH + r0) * OW) * C1_CO;
+  const int t1 = 32 + j;
+  const int off0 = (j / 7) * PW + j % 7;
+  const int off1 = t1 < 49 ? (t1 / 7) * PW + t1 % 7 : 0;
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+  for (int p0 = wave * 2; p0 < npix; p0 += 8) {
+    const int p = p0 + h;
+    const bool ok = p < npix;
+    const int pc = ok ? p : npix - 1;
+    const float a = ok ? dyb[(int64_t)pc * C1_CO + j] : 0.f;  // A[c = j][k = h]
+    const int oy = pc / OW, ox = pc - oy * OW;
+    const float* pp = patch + (2 * oy) * PW + 2 * ox;
+    acc0 = mfma32(a, pp[off0], acc0);
+    acc1 = mfma32(a, t1 < 49 ? pp[off1] : 0.f, acc1);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    red[((wave * 2 + 0) * 16 + r) * 64 + lane] = acc0[r];
+    red[((wave * 2 + 1) * 16 + r) * 64 + lane] = acc1[r];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 2 * 16 * 64; e += 256) {
+    const int tile = e / 1024, r = (e / 64) % 16, l = e % 64;
+    const float v = (red[((0 * 2 + tile) * 16 + r) * 64 + l] + red[((1 * 2 + tile) * 16 + r) * 64 + l]) +
+                    (red[((2 * 2 + tile) * 16 + r) * 64 + l] + red[((3 * 2 + tile) * 16 + r) * 64 + l]);
+    const int c = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), tap = tile * 32 + (l & 31);
+    if (tap < 49) slab[(int64_t)blockIdx.x * 32 * 49 + c * 49 + tap] = v;
+  }
+}
+
+// dW (torch [32][1][7][7]) = sum of the blocks' partials, fixed order: 64 elements x 4 slab lanes per block
+__global__ __launch_bounds__(256) void conv1_wgrad_reduce_kernel(const float* __restrict__ slab, int S,
+                                                                 float* __restrict__ dw) {
+  __shared__ float red[4][64];
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+  float s0 = 0.f, s1 = 0.f;
+  if (e < 32 * 49) {
+    int s = g;
+    for (; s + 4 < S; s += 8) {
+      s0 += slab[(int64_t)s * 32 * 49 + e];
+      s1 += slab[(int64_t)(s + 4) * 32 * 49 + e];
+    }
+    for (; s < S; s += 4) s0 += slab[(int64_t)s * 32 * 49 + e];
+  }
+  red[g][threadIdx.x & 63] = s0 + s1;
+  __syncthreads();
+  if (threadIdx.x < 64 && e < 32 * 49)
+    dw[e] = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+int conv1_wgrad(const float* x, int NF, int H, int W, const float* dy, int OH, int OW, float* slab,
+                int64_t slab_cap, float* dw, hipStream_t st) {
+  const int bands = (int)cdiv(OH, C1_RB);
+  const int S = NF * bands;
+  VAD_CHECK((int64_t)S * 32 * 49 <= slab_cap, "conv1_wgrad: slab buffer too small");
+  const size_t patch = ((size_t)(2 * C1_RB + 5) * (2 * OW + 6) + 3) & ~(size_t)3;
+  const size_t lds = (patch + 4 * 2 * 16 * 64) * sizeof(float);
+  VAD_CHECK(lds <= 160 * 1024, "conv1_wgrad: frame too wide for the LDS band");
+  hipLaunchKernelGGL(conv1_wgrad_kernel, dim3(S), dim3(256), lds, st, x, H, W, dy, OH, OW, bands, slab);
+  VAD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(conv1_wgrad_reduce_kernel, dim3((unsigned)cdiv(32 * 49, 64)), dim3(256), 0, st, slab, S, dw);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+// MaxPool2d(3, 2, 1) backward over relu(bn1(y)): dA[p] = sum of dpool over the (1, 2 or 4) windows whose first
+// maximum in scan order (torch CPU max_pool2d's index rule) is p; recomputed from y instead of stored indices.
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ y, const float* __restrict__ stats,
+                                                          const float* __restrict__ dpool, int NF, int H, int W,
+                                                          int C, int OH, int OW, float* __restrict__ dA) {
+  const int nq = C / 4;
+  const int64_t total = (int64_t)NF * H * W * nq;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int q = (int)(i % nq);
+    int64_t p = i / nq;
+    const int ix = (int)(p % W);
+    p /= W;
+    const int iy = (int)(p % H);
+    const int img = (int)(p / H);
+    const int c = q * 4;
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(stats + 2 * C + c);
+    const f32x4 sh = *reinterpret_cast<const f32x4*>(stats + 3 * C + c);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int oy0 = max(0, iy / 2), oy1 = min(OH - 1, (iy + 1) / 2);
+    const int ox0 = max(0, ix / 2), ox1 = min(OW - 1, (ix + 1) / 2);
+    for (int oy = oy0; oy <= oy1; ++oy)
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        f32x4 best = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        int first[4] = {-1, -1, -1, -1};
+        for (int dyy = -1; dyy <= 1; ++dyy) {
+          const int yy = 2 * oy + dyy;
+          if (yy < 0 || yy >= H) continue;
+          for (int dxx = -1; dxx <= 1; ++dxx) {
+            const int xx = 2 * ox + dxx;
+            if (xx < 0 || xx >= W) continue;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(y + (((int64_t)img * H + yy) * W + xx) * C + c);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float z = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
+              if (z > best[e]) {
+                best[e] = z;
+                first[e] = yy * W + xx;
+              }
+            }
+          }
+        }
+        const f32x4 g = *reinterpret_cast<const f32x4*>(dpool + (((int64_t)img * OH + oy) * OW + ox) * C + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (first[e] == iy * W + ix) acc[e] += g[e];
+      }
+    *reinterpret_cast<f32x4*>(dA + (((int64_t)img * H + iy) * W + ix) * C + c) = acc;
+  }
+}
+
+int maxpool3s2_bwd(const float* y, const float* stats, const float* dpool, int NF, int H, int W, int C, int OH,
+                   int OW, float* dA, hipStream_t st) {
+  VAD_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && C % 4 == 0, "maxpool_bwd: bad dims");
+  const int64_t total = (int64_t)NF * H * W * (C / 4);
+  const int grid = (int)std::min<int64_t>(cdiv(total, 256), 16384);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid), dim3(256), 0, st, y, stats, dpool, NF, H, W, C, OH, OW, dA);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
 int conv1_fwd(const float* x, int NF, int H, int W, const float* w, const float* b, float* y, int OH, int OW,
               float* partials, int* nparts, hipStream_t st) {
   VAD_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1, "conv1: bad output dims");

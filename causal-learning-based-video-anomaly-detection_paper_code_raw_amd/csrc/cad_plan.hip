@@ -135,12 +135,33 @@ static const CadLayout& layout() {
 constexpr int64_t FLAG_FLOATS = 256;  // grad buffer tail: [0] det flag, [1] struct flag (summed under DP)
 
 // ------------------------------------------------------------------ optimizer kernels
-__global__ __launch_bounds__(256) void sqsum_kernel(const float* __restrict__ g, int64_t n, float scale,
-                                                    float* __restrict__ partials) {
-  double s = 0.0;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float v = g[i] * scale;
-    s += (double)v * v;
+struct SlotTab {
+  int64_t off[160];
+  int32_t group[160];
+  int nslots;
+};
+
+__device__ inline bool slot_active(int g, const float* flags, int stem) {
+  return g == G_ALWAYS || (g == G_DET && flags[0] > 0.f) || (g == G_STRUCT && flags[1] > 0.f) ||
+         (g == G_FROZEN && stem);
+}
+
+// sum of squared (scaled) grads: one 256-float chunk (slots are 256-aligned) per wave iteration, float4 per lane;
+// chunks of slots without a grad this step (frozen, or the detector / structure learner when their flag is 0: zero)
+// are skipped.  Per-lane float sums, block combine in double.
+__global__ __launch_bounds__(256) void sqsum_kernel(const float* __restrict__ g, const int16_t* __restrict__ chunk_slot,
+                                                    int64_t nchunks, SlotTab tab, const float* __restrict__ flags,
+                                                    float scale, float* __restrict__ partials, int stem) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float s = 0.f;
+  for (int64_t c = (int64_t)blockIdx.x * 4 + wave; c < nchunks; c += (int64_t)gridDim.x * 4) {
+    const int sl = chunk_slot[c];
+    if (sl < 0 || !slot_active(tab.group[sl], flags, stem)) continue;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(g + c * 256 + lane * 4) * scale;
+    s = fmaf(v[0], v[0], s);
+    s = fmaf(v[1], v[1], s);
+    s = fmaf(v[2], v[2], s);
+    s = fmaf(v[3], v[3], s);
   }
   __shared__ double red[256];
   red[threadIdx.x] = s;
@@ -152,17 +173,11 @@ __global__ __launch_bounds__(256) void sqsum_kernel(const float* __restrict__ g,
   if (threadIdx.x == 0) partials[blockIdx.x] = (float)red[0];
 }
 
-struct SlotTab {
-  int64_t off[160];
-  int32_t group[160];
-  int nslots;
-};
-
 // per-slot step bump + bias corrections; clip coefficient (torch clip_grad_norm_: coef = max/(norm+1e-6) <= 1)
 __global__ void opt_prepare_kernel(const float* __restrict__ partials, int np, const float* __restrict__ flags,
                                    SlotTab tab, int32_t* steps, float beta1, float beta2, float max_norm,
                                    float* __restrict__ slot_info /* [nslots][4] */, float* clip_out,
-                                   float* total_norm_out) {
+                                   float* total_norm_out, int stem) {
   __shared__ double red[256];
   double s = 0.0;
   for (int i = threadIdx.x; i < np; i += 256) s += partials[i];
@@ -180,7 +195,7 @@ __global__ void opt_prepare_kernel(const float* __restrict__ partials, int np, c
   }
   for (int i = threadIdx.x; i < tab.nslots; i += 256) {
     const int g = tab.group[i];
-    bool active = g == G_ALWAYS || (g == G_DET && flags[0] > 0.f) || (g == G_STRUCT && flags[1] > 0.f);
+    const bool active = slot_active(g, flags, stem);
     float st = 0.f, bc1 = 1.f, bc2s = 1.f;
     if (active) {
       const int step = steps[i] + 1;
@@ -312,9 +327,9 @@ struct CadPlanImpl {
   int* head_iws;
   float *probs, *finalv, *causal, *kl, *z, *adj, *boxes;
   int *counts, *nmax, *clip_flags, *flags;
-  float *d_causal, *d_kl, *d_glog, *d_dlog, *slabs, *d_feat_det, *d_pooled, *dense_scratch;
+  float *d_causal, *d_kl, *d_glog, *d_dlog, *slabs, *d_feat_det, *d_pooled, *dense_scratch, *dense_scratch2;
   float *dg[5], *ddh[5];
-  float *dA, *dY, *wpart;
+  float *dA, *dY, *wpart, *stem_d;  // stem_d: [NF][H1][W1][32], the stem backward's dA / dY (stem_grad only)
   float *sq_parts, *slot_info, *clip;
   int16_t* chunk_slot;
   int64_t parts_floats, dense_scratch_floats, wpart_floats, slab_len, act_max;
@@ -330,6 +345,33 @@ struct CadPlanImpl {
   int bwd_state = 0;
   int debug_stop_layer = -1;  // backward returns after this backbone layer (debug introspection)
   Profiler prof;
+  // side stream: the detector + causal head chain runs beside the direct classifier (forward and backward); the
+  // two chains share only their inputs (features / the loss tail's upstream grads) and meet again at the loss tail
+  // and at the backbone backward (fork / join through events on the caller's stream)
+  hipStream_t st2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_det = nullptr;
+  int fork(hipStream_t st) {
+    if (!st2) {
+      VAD_HIP(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
+      VAD_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+      VAD_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+      VAD_HIP(hipEventCreateWithFlags(&ev_det, hipEventDisableTiming));
+    }
+    VAD_HIP(hipEventRecord(ev_fork, st));
+    VAD_HIP(hipStreamWaitEvent(st2, ev_fork, 0));
+    return 0;
+  }
+  int join(hipStream_t st) {
+    VAD_HIP(hipEventRecord(ev_join, st2));
+    VAD_HIP(hipStreamWaitEvent(st, ev_join, 0));
+    return 0;
+  }
+  ~CadPlanImpl() {
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (ev_det) (void)hipEventDestroy(ev_det);
+    if (st2) (void)hipStreamDestroy(st2);
+  }
   char lbl[64];
   const char* L_(const char* base, int l) {
     snprintf(lbl, sizeof(lbl), "%s/L%d", base, l);
@@ -399,8 +441,10 @@ struct CadPlanImpl {
     dense_scratch_floats = std::max<int64_t>(512ll * 6145, 16ll * nf * 512);
     dense_scratch_floats = std::max<int64_t>(dense_scratch_floats, 16ll * B * 512);
     dense_scratch = w.take<float>(dense_scratch_floats);
+    dense_scratch2 = w.take<float>(dense_scratch_floats);  // the side stream's (detector) split-K scratch
     dA = w.take<float>(act_max);
     dY = w.take<float>(act_max);
+    stem_d = w.take<float>(nf * H1 * W1 * 32);
     wpart_floats = 16ll << 20;
     wpart = w.take<float>(wpart_floats);
     sq_parts = w.take<float>(1024);
@@ -528,6 +572,9 @@ struct CadPlanImpl {
   }
 
   int conv_bf16 = 0;  // option "conv_bf16": 3x3 convs on bf16 operands (BASELINE config 4)
+  // option "stem_grad": backbone.conv1 / bn1 train (the reference's module without apply_memory_efficient_training);
+  // stem_active: the last backward wrote their grads (the fused optimizer then steps them too)
+  int stem_grad = 0, stem_active = 0;
 
   // batch statistics of BN layer i (0 = bn1) from the `np` partials in `parts`: local (default) or, with a sync
   // callback in training mode, over the whole process group (torch.nn.SyncBatchNorm semantics)
@@ -557,8 +604,11 @@ struct CadPlanImpl {
     return 0;
   }
 
+  const float* x_last = nullptr;  // the last forward's input (the stem backward's conv1 weight gradient reads it)
+
   int forward(const float* x, hipStream_t st) {
     ConvPrecision prec(conv_bf16);
+    x_last = x;
     const CadLayout& LY = layout();
     {
       const float* w8[8];
@@ -579,18 +629,22 @@ struct CadPlanImpl {
       sst = stats[l + 1];
     }
     TIMED("avgpool", avgpool_fwd(y[7], stats[8], B, T, HF, WF, 256, feats, pooled, st));
-    // detector_net (cad:167-179): layer 0 as a split-K GEMM, layers 1-4 fused per row block
     const int64_t f0 = clip0 * T;
     const int dd[6] = {6144, 512, 256, 128, 64, 20};
     const int gd[6] = {6144, 512, 256, 128, 64, 2};
-    TIMED("prep", mlp_transpose(mlp_transpose_args(), st));
-    const float* in = feats;
-    TIMED("det_fwd", dense_fwd(in, NF, 6144, P(LY.det_w[0]), P(LY.det_b[0]), 512, dh[0], act(true, S_DET_DROP1, 0.3, f0),
-                               dense_scratch, dense_scratch_floats, st));
-    TIMED("det_fwd", mlp_tail_fwd(mlp_args(NF, f0, dd, LY.det_w, LY.det_b, dh, dlog, S_DET_DROP2, wt), st));
+    // (launch order: the side stream's first long kernels are queued before the direct classifier's short chain so
+    // the host's launch latency overlaps GPU work on both streams)
+    VAD_TRY(fork(st));
+    {  // side stream: detector_net (cad:167-179; layer 0 as a split-K GEMM, layers 1-4 fused per row block)
+      hipStream_t st = st2;
+      TIMED("prep", mlp_transpose(mlp_transpose_args(), st));
+      TIMED("det_fwd", dense_fwd(feats, NF, 6144, P(LY.det_w[0]), P(LY.det_b[0]), 512, dh[0],
+                                 act(true, S_DET_DROP1, 0.3, f0), dense_scratch2, dense_scratch_floats, st));
+      TIMED("det_fwd", mlp_tail_fwd(mlp_args(NF, f0, dd, LY.det_w, LY.det_b, dh, dlog, S_DET_DROP2, wt), st));
+    }
     // direct_classifier on the mean over T (cad:525-538, 568-570)
     // (B rows only: one block per 64 columns, so the chain runs layer by layer on many CUs; layers 1-4 unsplit)
-    in = pooled;
+    const float* in = pooled;
     for (int i = 0; i < 5; ++i) {
       float* out = i < 4 ? gh[i] : glog;
       const int sid = i == 0 ? S_DIRECT_DROP1 : (i == 1 ? S_DIRECT_DROP2 : 0);
@@ -599,7 +653,14 @@ struct CadPlanImpl {
                                  i == 0 ? 0 : 1));
       in = out;
     }
-    TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
+    // the detector's input gradient buffer is zero unless its backward writes it (the backward skips it on device when
+    // no box was in range); cleared here, where the main stream has slack
+    VAD_HIP(hipMemsetAsync(d_feat_det, 0, sizeof(float) * (size_t)NF * 6144, st));
+    {  // side stream: the causal head on the detections
+      hipStream_t st = st2;
+      TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
+    }
+    VAD_TRY(join(st));
     TailArgs t = tail_args(nullptr, nullptr, nullptr, nullptr);
     if (training && nbt) {  // num_batches_tracked of the 9 BN layers (bumped by the tail kernel)
       t.nbt = nbt;
@@ -637,7 +698,7 @@ struct CadPlanImpl {
   // non-backbone grad is final when it returns); stage 1: the backbone.  Splitting lets a data-parallel caller
   // all-reduce the head grads while the backbone backward runs.
   int backward(bool use_loss, const float* dfin, const float* dprobs, const float* dcaus, const float* dkl,
-               const float* dz, const float* dadj, hipStream_t st, int stage = -1) {
+               const float* dz, const float* dadj, hipStream_t st, int stage = -1, const float* dboxes = nullptr) {
     ConvPrecision prec(conv_bf16);
     const CadLayout& LY = layout();
     VAD_CHECK(grads != nullptr, "backward: grads not bound");
@@ -650,14 +711,17 @@ struct CadPlanImpl {
     TailArgs t = use_loss ? tail_args(nullptr, nullptr, nullptr, nullptr) : tail_args(dfin, dprobs, dcaus, dkl);
     if (!use_loss) t.labels = nullptr;
     TIMED("tail", cad_tail_bwd(t, st));
-    HeadUp up{d_causal, d_kl, dz, dadj};
-    TIMED("head_bwd", head_bwd(head_args(), dlog, head_out(), up, slabs, slab_len, d_dlog, st));
-    TIMED("head_bwd", head_slab_reduce(slabs, B, slab_len, grads + LY.slots[LY.head0].offset, st));
-    TIMED("head_bwd", head_rows_wgrad(head_args(), st));
-    // direct classifier chain (B rows): per-layer input-gradient GEMMs spread over many CUs, the layer 1-4 weight
-    // grads in one launch, layer 0 GEMMs
     const int gd[6] = {6144, 512, 256, 128, 64, 2};
     const int dd[6] = {6144, 512, 256, 128, 64, 20};
+    VAD_TRY(fork(st));
+    {  // side stream: causal head backward, then the detector chain (skipped on device when no box was in range: no
+       // grads reach it, cad:221-226)
+      hipStream_t st = st2;
+      HeadUp up{d_causal, d_kl, dz, dadj, dboxes};
+      TIMED("head_bwd", head_bwd(head_args(), dlog, head_out(), up, slabs, slab_len, d_dlog, st));
+    }
+    // direct classifier chain (B rows): per-layer input-gradient GEMMs spread over many CUs, the layer 1-4 weight
+    // grads in one launch, layer 0 GEMMs
     {
       const double gp[4] = {0.3, 0.2, 0.0, 0.0};
       const float* dcur = d_glog;
@@ -672,13 +736,20 @@ struct CadPlanImpl {
     TIMED("dir_bwd", dense_wgrad(dg[0], B, 512, pooled, 6144, G(LY.dir_w[0]), G(LY.dir_b[0]), dense_scratch,
                                  dense_scratch_floats, nullptr, st));
     TIMED("dir_bwd", dense_dgrad(dg[0], B, 512, P(LY.dir_w[0]), 6144, d_pooled, nullptr, 1.f, nullptr, st));
-    // detector chain (skipped on device when no box was in range: no grads reach it, cad:221-226)
-    VAD_HIP(hipMemsetAsync(d_feat_det, 0, sizeof(float) * (size_t)NF * 6144, st));
-    TIMED("det_bwd", mlp_tail_bwd(mlp_bwd_args(NF, d_dlog, dd, LY.det_w, dh, ddh, flags), st));
-    TIMED("det_bwd", rows_wgrad(mlp_wgrad_args(NF, d_dlog, dd, LY.det_w, LY.det_b, dh, ddh, flags), st));
-    TIMED("det_bwd", dense_wgrad(ddh[0], NF, 512, feats, 6144, G(LY.det_w[0]), G(LY.det_b[0]), dense_scratch,
-                                 dense_scratch_floats, flags, st));
-    TIMED("det_bwd", dense_dgrad(ddh[0], NF, 512, P(LY.det_w[0]), 6144, d_feat_det, nullptr, 1.f, flags, st));
+    {  // side stream, continued: the detector chain (it feeds the backbone: event ev_det), then the head's weight
+       // grads, which only the optimizer / the grad all-reduce wait for
+      hipStream_t st = st2;
+      TIMED("det_bwd", mlp_tail_bwd(mlp_bwd_args(NF, d_dlog, dd, LY.det_w, dh, ddh, flags), st));
+      TIMED("det_bwd", rows_wgrad(mlp_wgrad_args(NF, d_dlog, dd, LY.det_w, LY.det_b, dh, ddh, flags), st));
+      TIMED("det_bwd", dense_wgrad(ddh[0], NF, 512, feats, 6144, G(LY.det_w[0]), G(LY.det_b[0]), dense_scratch2,
+                                   dense_scratch_floats, flags, st));
+      TIMED("det_bwd", dense_dgrad(ddh[0], NF, 512, P(LY.det_w[0]), 6144, d_feat_det, nullptr, 1.f, flags, st));
+      VAD_HIP(hipEventRecord(ev_det, st));
+      TIMED("head_bwd", head_slab_reduce(slabs, B, slab_len, grads + LY.slots[LY.head0].offset, st));
+      TIMED("head_bwd", head_rows_wgrad(head_args(), st));
+    }
+    if (stage == 0) VAD_TRY(join(st));  // every non-backbone grad is final when stage 0 returns
+    else VAD_HIP(hipStreamWaitEvent(st, ev_det, 0));
     }
     bwd_state = 1;
     if (stage == 0) return 0;
@@ -697,8 +768,23 @@ struct CadPlanImpl {
       TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dY, src, sst, wpart, &ns, wpart_floats, st));
       TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], wpart, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
       if (l > 0) TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dY, wd[l], dA, st));
-      if (l == debug_stop_layer) return 0;
+      if (l == debug_stop_layer) break;
     }
+    stem_active = 0;
+    if (stem_grad && debug_stop_layer < 0) {
+      // the stem (cad:145-147): input gradient of layer1.0 into the pooled map, MaxPool2d backward, bn1 backward (in
+      // place), conv1 weight gradient (its bias gradient comes from the bn1 finalize)
+      TIMED("stem_bwd", conv3_dgrad(L[0], dY, wd[0], dA, st));
+      TIMED("stem_bwd", maxpool3s2_bwd(y1, stats[0], dA, NF, H1, W1, 32, HP, WP, stem_d, st));
+      const int64_t M1 = (int64_t)NF * H1 * W1;
+      int np = 0, nb = 0;
+      TIMED("stem_bwd", bn_bwd_reduce(stem_d, y1, stats[0], (int)M1, 32, parts, &np, st));
+      VAD_TRY(bn_bwd_stats(0, np, 32, (double)M1, P(LY.bn1_w), G(LY.bn1_w), G(LY.bn1_b), G(LY.conv1_b), st));
+      TIMED("stem_bwd", bn_bwd_apply(stem_d, y1, stats[0], (int)M1, 32, stem_d, nullptr, &nb, st));
+      TIMED("stem_bwd", conv1_wgrad(x_last, NF, H, W, stem_d, H1, W1, wpart, wpart_floats, G(LY.conv1_w), st));
+      stem_active = 1;
+    }
+    if (stage == -1) VAD_TRY(join(st));  // the head's weight grads (side stream)
     return 0;
   }
 
@@ -713,9 +799,6 @@ struct CadPlanImpl {
       pb = prof.get();
       VAD_HIP(hipEventRecord(pa, st));
     }
-    const int nb = 512;
-    hipLaunchKernelGGL(sqsum_kernel, dim3(nb), dim3(256), 0, st, grads, LY.param_floats, gscale, sq_parts);
-    VAD_LAUNCH_CHECK();
     SlotTab tab{};
     tab.nslots = (int)LY.slots.size();
     VAD_CHECK(tab.nslots <= 160, "too many slots");
@@ -723,8 +806,12 @@ struct CadPlanImpl {
       tab.off[i] = LY.slots[i].offset;
       tab.group[i] = LY.slots[i].group;
     }
+    const int nb = 1024;  // (<= the 1024-float sq_parts)
+    hipLaunchKernelGGL(sqsum_kernel, dim3(nb), dim3(256), 0, st, grads, chunk_slot, LY.param_floats / 256, tab,
+                       grads + LY.param_floats, gscale, sq_parts, stem_active);
+    VAD_LAUNCH_CHECK();
     hipLaunchKernelGGL(opt_prepare_kernel, dim3(1), dim3(256), 0, st, sq_parts, nb, grads + LY.param_floats, tab,
-                       steps, b1, b2, max_norm, slot_info, clip, tn);
+                       steps, b1, b2, max_norm, slot_info, clip, tn, stem_active);
     VAD_LAUNCH_CHECK();
     const int64_t nchunks = LY.param_floats / 256;
     hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)std::min<int64_t>(nchunks, 4096)), dim3(256), 0, st, params,
@@ -920,6 +1007,14 @@ int vad_cad_backward_stage(vad_cad_plan* plan, int stage, int use_loss, const fl
                              stage);
 }
 
+int vad_cad_backward_ext(vad_cad_plan* plan, int stage, int use_loss, const float* d_final, const float* d_probs,
+                         const float* d_causal, const float* d_kl, const float* d_z, const float* d_adj,
+                         const float* d_boxes, void* stream) {
+  VAD_CHECK(plan != nullptr, "vad_cad_backward_ext: null plan");
+  return plan->impl.backward(use_loss != 0, d_final, d_probs, d_causal, d_kl, d_z, d_adj, (hipStream_t)stream,
+                             stage, d_boxes);
+}
+
 int vad_cad_optimizer_step(vad_cad_plan* plan, float lr, float beta1, float beta2, float eps, float weight_decay,
                            float max_norm, float grad_scale, float* total_norm, void* stream) {
   VAD_CHECK(plan != nullptr, "vad_cad_optimizer_step: null plan");
@@ -960,6 +1055,7 @@ int vad_cad_set_debug(vad_cad_plan* plan, const char* key, int64_t value) {
 int vad_cad_set_option(vad_cad_plan* plan, const char* key, int64_t value) {
   VAD_CHECK(plan && key, "vad_cad_set_option: null argument");
   if (std::string(key) == "conv_bf16") plan->impl.conv_bf16 = value ? 1 : 0;
+  else if (std::string(key) == "stem_grad") plan->impl.stem_grad = value ? 1 : 0;
   else { vad::set_error("vad_cad_set_option: unknown key"); return 1; }
   return 0;
 }

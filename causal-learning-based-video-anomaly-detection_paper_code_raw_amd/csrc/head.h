@@ -68,6 +68,7 @@ struct HeadUp {
   const float* d_kl;      // [B]
   const float* d_z;       // [B][5][6] or null
   const float* d_adj;     // [B][6][6] or null
+  const float* d_boxes;   // [B][T][5][4] or null: grads of the compacted per-frame detections (HeadOut::boxes)
 };
 int head_bwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, const HeadUp& up, float* slabs,
              int64_t slab_len, float* d_det_logits, hipStream_t st);

@@ -320,50 +320,63 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
       const f32x4* wz = reinterpret_cast<const f32x4*>(whh + (GH + u) * WHH_LD);
       const f32x4* wn = reinterpret_cast<const f32x4*>(whh + (2 * GH + u) * WHH_LD);
       const f32x4* hv = reinterpret_cast<const f32x4*>(hs + nn * GH);
-      // the input projections of step t+1 are loaded while step t computes
-      float gi_r = 0.f, gi_z = 0.f, gi_n = 0.f;
-      if (live) {
-        const float* gi = rows + RL.gi + ((int64_t)b * T * NMAX + nn) * G3;
-        gi_r = gi[u]; gi_z = gi[GH + u]; gi_n = gi[2 * GH + u];
-      }
-      for (int t = 0; t < T; ++t) {
-        const int64_t row = ((int64_t)b * T + t) * NMAX + nn;
-        if (live) {
-          float nx_r = 0.f, nx_z = 0.f, nx_n = 0.f;
-          if (t + 1 < T) {
-            const float* gi = rows + RL.gi + (row + NMAX) * G3;
-            nx_r = gi[u]; nx_z = gi[GH + u]; nx_n = gi[2 * GH + u];
-          }
-          float ar = br, az = bz, an = bn;
+      // the input projections are loaded TC steps at a time, one chunk ahead (double-buffered in registers): a
+      // per-step prefetch would be waited for together with the previous step's stores (vmcnt counts both)
+      constexpr int TC = 8;
+      float gc[TC][3], gn[TC][3];
+      auto load_gi = [&](int t0, float (&g)[TC][3]) {
 #pragma unroll
-          for (int k = 0; k < GH / 4; ++k) {
-            const f32x4 x = hv[k], a0 = wr[k], a1 = wz[k], a2 = wn[k];
-            ar = fmaf(a0[0], x[0], ar); ar = fmaf(a0[1], x[1], ar); ar = fmaf(a0[2], x[2], ar); ar = fmaf(a0[3], x[3], ar);
-            az = fmaf(a1[0], x[0], az); az = fmaf(a1[1], x[1], az); az = fmaf(a1[2], x[2], az); az = fmaf(a1[3], x[3], az);
-            an = fmaf(a2[0], x[0], an); an = fmaf(a2[1], x[1], an); an = fmaf(a2[2], x[2], an); an = fmaf(a2[3], x[3], an);
+        for (int k = 0; k < TC; ++k) {
+          g[k][0] = g[k][1] = g[k][2] = 0.f;
+          if (t0 + k < T) {
+            const float* gi = rows + RL.gi + (((int64_t)b * T + t0 + k) * NMAX + nn) * G3;
+            g[k][0] = gi[u]; g[k][1] = gi[GH + u]; g[k][2] = gi[2 * GH + u];
           }
-          const float r = sigmoidf_(gi_r + ar);
-          const float z = sigmoidf_(gi_z + az);
-          const float nv = tanhf(gi_n + r * an);
-          rows[RL.r + row * GH + u] = r;
-          rows[RL.z + row * GH + u] = z;
-          rows[RL.n + row * GH + u] = nv;
-          rows[RL.ghn + row * GH + u] = an;
-          rows[RL.hp + row * GH + u] = h;
-          h = (1.f - z) * nv + z * h;
-          // every lane's reads of the old h are done (lockstep wave) before the new h is published
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          hs[nn * GH + u] = h;
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          gi_r = nx_r; gi_z = nx_z; gi_n = nx_n;
-        } else {  // trajectory slots that do not exist in this clip
-          rows[RL.r + row * GH + u] = 0.f;
-          rows[RL.z + row * GH + u] = 0.f;
-          rows[RL.n + row * GH + u] = 0.f;
-          rows[RL.ghn + row * GH + u] = 0.f;
-          rows[RL.hp + row * GH + u] = 0.f;
+        }
+      };
+      if (live) load_gi(0, gc);
+      for (int t0 = 0; t0 < T; t0 += TC) {
+        if (live && t0 + TC < T) load_gi(t0 + TC, gn);
+#pragma unroll
+        for (int k = 0; k < TC; ++k) {
+          const int t = t0 + k;
+          if (t >= T) break;
+          const int64_t row = ((int64_t)b * T + t) * NMAX + nn;
+          if (live) {
+            float ar = br, az = bz, an = bn;
+#pragma unroll
+            for (int kk = 0; kk < GH / 4; ++kk) {
+              const f32x4 x = hv[kk], a0 = wr[kk], a1 = wz[kk], a2 = wn[kk];
+              ar = fmaf(a0[0], x[0], ar); ar = fmaf(a0[1], x[1], ar); ar = fmaf(a0[2], x[2], ar); ar = fmaf(a0[3], x[3], ar);
+              az = fmaf(a1[0], x[0], az); az = fmaf(a1[1], x[1], az); az = fmaf(a1[2], x[2], az); az = fmaf(a1[3], x[3], az);
+              an = fmaf(a2[0], x[0], an); an = fmaf(a2[1], x[1], an); an = fmaf(a2[2], x[2], an); an = fmaf(a2[3], x[3], an);
+            }
+            const float r = sigmoidf_(gc[k][0] + ar);
+            const float z = sigmoidf_(gc[k][1] + az);
+            const float nv = tanhf(gc[k][2] + r * an);
+            rows[RL.r + row * GH + u] = r;
+            rows[RL.z + row * GH + u] = z;
+            rows[RL.n + row * GH + u] = nv;
+            rows[RL.ghn + row * GH + u] = an;
+            rows[RL.hp + row * GH + u] = h;
+            h = (1.f - z) * nv + z * h;
+            // every lane's reads of the old h are done (lockstep wave) before the new h is published
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            hs[nn * GH + u] = h;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+          } else {  // trajectory slots that do not exist in this clip
+            rows[RL.r + row * GH + u] = 0.f;
+            rows[RL.z + row * GH + u] = 0.f;
+            rows[RL.n + row * GH + u] = 0.f;
+            rows[RL.ghn + row * GH + u] = 0.f;
+            rows[RL.hp + row * GH + u] = 0.f;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < TC; ++k) {
+          gc[k][0] = gn[k][0]; gc[k][1] = gn[k][1]; gc[k][2] = gn[k][2];
         }
       }
     }
@@ -703,44 +716,58 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
       const bool live = nn < N;
       float d = live ? dh[nn * GH + u] : 0.f;
       float* dgv = dgh_s + nn * G3;
-      // the saved gates of step t-1 are loaded while step t computes
-      float r = 0.f, z = 0.f, nv = 0.f, hp = 0.f, ghn = 0.f;
-      if (live) {
-        const int64_t row = ((int64_t)b * T + T - 1) * NMAX + nn;
-        r = rows[RL.r + row * GH + u]; z = rows[RL.z + row * GH + u]; nv = rows[RL.n + row * GH + u];
-        hp = rows[RL.hp + row * GH + u]; ghn = rows[RL.ghn + row * GH + u];
-      }
-      for (int t = T - 1; t >= 0; --t) {
-        const int64_t row = ((int64_t)b * T + t) * NMAX + nn;
-        float* dgi = rows + RL.dgi + row * G3;
-        float* dgh = rows + RL.dgh + row * G3;
-        if (live) {
-          float nr = 0.f, nz = 0.f, nn_ = 0.f, nhp = 0.f, nghn = 0.f;
-          if (t > 0) {
-            const int64_t pr = row - NMAX;
-            nr = rows[RL.r + pr * GH + u]; nz = rows[RL.z + pr * GH + u]; nn_ = rows[RL.n + pr * GH + u];
-            nhp = rows[RL.hp + pr * GH + u]; nghn = rows[RL.ghn + pr * GH + u];
+      // the saved gates are loaded TC steps at a time, one chunk ahead (double-buffered in registers; see the
+      // forward recurrence)
+      constexpr int TC = 8;
+      float sc_[TC][5], sn_[TC][5];  // r, z, n, h_prev, W_hn h_prev + b_hn of steps t0, t0-1, ...
+      auto load_gates = [&](int t0, float (&g)[TC][5]) {
+#pragma unroll
+        for (int k = 0; k < TC; ++k) {
+          g[k][0] = g[k][1] = g[k][2] = g[k][3] = g[k][4] = 0.f;
+          if (t0 - k >= 0) {
+            const int64_t row = ((int64_t)b * T + t0 - k) * NMAX + nn;
+            g[k][0] = rows[RL.r + row * GH + u]; g[k][1] = rows[RL.z + row * GH + u];
+            g[k][2] = rows[RL.n + row * GH + u]; g[k][3] = rows[RL.hp + row * GH + u];
+            g[k][4] = rows[RL.ghn + row * GH + u];
           }
-          const float dan = d * (1.f - z) * (1.f - nv * nv);
-          const float daz = d * (hp - nv) * z * (1.f - z);
-          const float dar = dan * ghn * r * (1.f - r);
-          dgi[u] = dar; dgi[GH + u] = daz; dgi[2 * GH + u] = dan;
-          dgh[u] = dar; dgh[GH + u] = daz; dgh[2 * GH + u] = dan * r;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          dgv[u] = dar;
-          dgv[GH + u] = daz;
-          dgv[2 * GH + u] = dan * r;
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          float s = d * z;
-          for (int q = 0; q < G3; ++q) s = fmaf(whh[q * GH + u], dgv[q], s);
-          d = s;
-          r = nr; z = nz; nv = nn_; hp = nhp; ghn = nghn;
-        } else {
-          dgi[u] = 0.f; dgi[GH + u] = 0.f; dgi[2 * GH + u] = 0.f;
-          dgh[u] = 0.f; dgh[GH + u] = 0.f; dgh[2 * GH + u] = 0.f;
         }
+      };
+      if (live) load_gates(T - 1, sc_);
+      for (int t0 = T - 1; t0 >= 0; t0 -= TC) {
+        if (live && t0 - TC >= 0) load_gates(t0 - TC, sn_);
+#pragma unroll
+        for (int k = 0; k < TC; ++k) {
+          const int t = t0 - k;
+          if (t < 0) break;
+          const int64_t row = ((int64_t)b * T + t) * NMAX + nn;
+          float* dgi = rows + RL.dgi + row * G3;
+          float* dgh = rows + RL.dgh + row * G3;
+          if (live) {
+            const float r = sc_[k][0], z = sc_[k][1], nv = sc_[k][2], hp = sc_[k][3], ghn = sc_[k][4];
+            const float dan = d * (1.f - z) * (1.f - nv * nv);
+            const float daz = d * (hp - nv) * z * (1.f - z);
+            const float dar = dan * ghn * r * (1.f - r);
+            dgi[u] = dar; dgi[GH + u] = daz; dgi[2 * GH + u] = dan;
+            dgh[u] = dar; dgh[GH + u] = daz; dgh[2 * GH + u] = dan * r;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            dgv[u] = dar;
+            dgv[GH + u] = daz;
+            dgv[2 * GH + u] = dan * r;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            float s = d * z;
+            for (int q = 0; q < G3; ++q) s = fmaf(whh[q * GH + u], dgv[q], s);
+            d = s;
+          } else {
+            dgi[u] = 0.f; dgi[GH + u] = 0.f; dgi[2 * GH + u] = 0.f;
+            dgh[u] = 0.f; dgh[GH + u] = 0.f; dgh[2 * GH + u] = 0.f;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < TC; ++k)
+#pragma unroll
+          for (int e = 0; e < 5; ++e) sc_[k][e] = sn_[k][e];
       }
     }
   }
@@ -748,7 +775,8 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
 
 // per frame: d x = W_ih^T d gi for real rows, ReID backward, d box -> d detector logits
 __global__ __launch_bounds__(256) void head_rows_bwd_kernel(HeadArgs a, const float* __restrict__ logits,
-                                                            float* __restrict__ dlog) {
+                                                            float* __restrict__ dlog,
+                                                            const float* __restrict__ dboxes) {
   const int f = blockIdx.x;
   const int b = f / a.T, t = f - b * a.T;
   const int tid = threadIdx.x;
@@ -807,6 +835,9 @@ __global__ __launch_bounds__(256) void head_rows_bwd_kernel(HeadArgs a, const fl
     if (j < cnt && slot[j] >= 0) {  // the fallback box is a constant: no grad
       float dv = sdx[j][c];
       for (int u = 0; u < 32; ++u) dv = fmaf(W0[u * 4 + c], sd1[j][u], dv);
+      // a loss on the returned detections (the reference's boxes are slices of the rescaled detector output,
+      // cad:201-222): its grad enters at the same compacted slot
+      if (dboxes) dv += dboxes[(int64_t)f * NMAX * 4 + j * 4 + c];
       const int k = slot[j];
       const float sg = sigmoidf_(logits[(int64_t)f * 20 + k * 4 + c]);
       const float sc = c == 0 ? 360.f : (c == 1 ? 240.f : (c == 2 ? 80.f : 120.f));
@@ -820,7 +851,8 @@ int head_bwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, const
   VAD_HIP(hipMemsetAsync(d_det_logits, 0, sizeof(float) * (size_t)a.B * a.T * 20, st));
   hipLaunchKernelGGL(head_seq_bwd_kernel, dim3(a.B), dim3(HT), 0, st, a, o, up, slabs, slab_len);
   VAD_LAUNCH_CHECK();
-  hipLaunchKernelGGL(head_rows_bwd_kernel, dim3(a.B * a.T), dim3(256), 0, st, a, det_logits, d_det_logits);
+  hipLaunchKernelGGL(head_rows_bwd_kernel, dim3(a.B * a.T), dim3(256), 0, st, a, det_logits, d_det_logits,
+                     up.d_boxes);
   VAD_LAUNCH_CHECK();
   return 0;
 }

@@ -228,17 +228,37 @@ class CadEngine:
         return o
 
     def backward(self, use_loss: bool, d_final=None, d_probs=None, d_causal=None, d_kl=None, d_z=None, d_adj=None,
-                 stage: int = -1):
+                 stage: int = -1, d_boxes=None):
         """stage -1: whole backward; 0: everything but the backbone (grads outside [0, backbone_floats) final);
-        1: the backbone (after stage 0)."""
+        1: the backbone (after stage 0).  d_boxes: grad of the (B, T, 5, 4) detections output."""
         pl, lab, _ = self._last
+        self._set_stem_grad(pl)
         c = [t.contiguous() if t is not None else None for t in (d_final, d_probs, d_causal, d_kl, d_z, d_adj)]
+        if d_boxes is not None:
+            nat.check(nat.lib().vad_cad_backward_ext(pl.h, stage, 1 if use_loss else 0, *[nat.ptr(t) for t in c],
+                                                     nat.ptr(d_boxes.contiguous().float()),
+                                                     nat.stream_of(self.device)))
+            return
         if stage == -1:
             nat.check(nat.lib().vad_cad_backward(pl.h, 1 if use_loss else 0, *[nat.ptr(t) for t in c],
                                                  nat.stream_of(self.device)))
         else:
             nat.check(nat.lib().vad_cad_backward_stage(pl.h, stage, 1 if use_loss else 0, *[nat.ptr(t) for t in c],
                                                        nat.stream_of(self.device)))
+
+    STEM = ("backbone.conv1.weight", "backbone.conv1.bias", "backbone.bn1.weight", "backbone.bn1.bias")
+
+    def stem_trains(self) -> bool:
+        """backbone.conv1 / bn1 take grads unless frozen (apply_memory_efficient_training, cad:592-598)."""
+        named = dict(self.model.named_parameters())
+        return any(named[n].requires_grad for n in self.STEM)
+
+    def _set_stem_grad(self, pl):
+        on = self.stem_trains()
+        if getattr(pl, "stem_grad", None) != on:
+            nat.check(nat.lib().vad_cad_set_option(pl.h, b"stem_grad", 1 if on else 0))
+            pl.stem_grad = on
+        self.stem_grad_on = on
 
     @property
     def backbone_floats(self) -> int:

@@ -85,6 +85,12 @@ int vad_cad_backward(vad_cad_plan* plan, int use_loss, const float* d_final, con
 int vad_cad_backward_stage(vad_cad_plan* plan, int stage, int use_loss, const float* d_final, const float* d_probs,
                            const float* d_causal, const float* d_kl, const float* d_z, const float* d_adj,
                            void* stream);
+/* vad_cad_backward_stage with one more upstream grad: d_boxes [B,T,5,4] (may be NULL), the grad of a loss on the
+ * forward's compacted per-frame detections (boxes output of vad_cad_forward; the reference's detections are slices
+ * of the rescaled detector output and carry autograd, cad:201-222).  The constant fallback box takes no grad. */
+int vad_cad_backward_ext(vad_cad_plan* plan, int stage, int use_loss, const float* d_final, const float* d_probs,
+                         const float* d_causal, const float* d_kl, const float* d_z, const float* d_adj,
+                         const float* d_boxes, void* stream);
 /* clip_grad_norm_(max_norm) + AdamW over the flat buffers (torch.optim.AdamW semantics, per-slot steps,
  * slots without a grad this step are skipped).  grad_scale multiplies grads first (1/world for DP).
  * total_norm (device float [1], may be NULL) receives the pre-clip norm. */

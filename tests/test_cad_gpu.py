@@ -22,6 +22,14 @@ pytestmark = pytest.mark.gpu
 CASES = cad_cases()
 
 
+def _frozen(m):
+    from vad_amd.train import apply_memory_efficient_training
+    import io, contextlib
+    with contextlib.redirect_stdout(io.StringIO()):
+        apply_memory_efficient_training(m)
+    return m
+
+
 def _hip_step(case, step_opt=True, keep_pre=False):
     from vad_amd.train import apply_memory_efficient_training
     import io, contextlib
@@ -168,9 +176,7 @@ def test_module_api_forward_backward():
     lref.backward()
     for n, p in m.named_parameters():
         pr = params[n]
-        if n.startswith(("backbone.conv1", "backbone.bn1")):
-            assert p.grad is None, n  # the stem is frozen in this build (cad:596-598)
-            continue
+        # (the stem trains here: no apply_memory_efficient_training, so conv1 / bn1 get grads as in the reference)
         if pr.grad is None or float(pr.grad.abs().max()) == 0.0:
             assert p.grad is None or float(p.grad.abs().max()) < 1e-9, n
             continue
@@ -208,7 +214,7 @@ def test_hip_backward_matches_oracle_full_size():
     <= 1e-4, and the loss terms within 1e-4."""
     B, T, H, W = 8, 16, 227, 227
     case = dict(name="cfg2", B=B, T=T, H=H, W=W, seed=6, step=0, forced=None)
-    m = make_cad_model(case).cuda()
+    m = _frozen(make_cad_model(case)).cuda()  # train_model's frozen stem (cad:592-598), as the oracle step
     eng = m.engine()
     x = co.synth_clips(6, 0, 0, B, T, H, W)
     y = co.synth_labels(0, B)
@@ -241,7 +247,7 @@ def test_config4_shape_fp32_and_bf16(B, T, H, W):
     res = co.cad_train_step(params, bufs, {}, x, y, co.CadDraws.make(9, 1, 0, B, T))
     ref_norm = float(res["total_norm"])
     for dt in (torch.float32, torch.bfloat16):
-        m = make_cad_model(case).cuda().set_compute_dtype(dt)
+        m = _frozen(make_cad_model(case)).cuda().set_compute_dtype(dt)
         eng = m.engine()
         o = eng.forward(x.cuda(), True, 9, 1, 0, y.cuda())
         eng.backward(True)
@@ -275,3 +281,39 @@ def test_staged_backward_equals_whole_backward():
     eng.backward(True, stage=1)
     torch.cuda.synchronize()
     assert torch.equal(eng.grads[:eng.param_floats + 2], grads[:eng.param_floats + 2])
+
+
+def test_module_api_detection_grads():
+    """Detections carry autograd as in the reference (cad:201-222: each frame's boxes are slices of the rescaled
+    detector output; the fallback box is a constant): a loss on out["detections"] trains the detector and the
+    backbone under it.  Forced-detection weights (valid boxes), eval mode; every grad vs the oracle."""
+    from tests.golden.cases import CAD_CASES
+    case = dict(next(c for c in CAD_CASES if c["name"] == "forced_b2t4_64"))
+    m = make_cad_model(case).cuda()
+    m.eval()
+    B, T = case["B"], case["T"]
+    x = co.synth_clips(case["seed"], 0, 0, B, T, case["H"], case["W"])
+    coef = torch.tensor([1.0, -0.5, 0.25, 2.0])
+    out = m(x.cuda())
+    loss = sum((d * coef.cuda()).sum() for fr in out["detections"] for d in fr) + out["anomaly_scores"].sum()
+    loss.backward()
+    mc = make_cad_model(case)
+    sd = {k: v.clone() for k, v in mc.state_dict().items()}
+    params = {k: v.requires_grad_(True) for k, v in sd.items() if "running" not in k and "num_batches" not in k}
+    bufs = {k: v for k, v in sd.items() if "running" in k}
+    ref = co.cad_forward(params, bufs, x, co.CadDraws.make(0, 0, 0, B, T), training=False)
+    assert sum(int(d.shape[0]) for fr in ref["detections"] for d in fr) > B * T  # live boxes (forced regime)
+    lref = sum((d * coef).sum() for fr in ref["detections"] for d in fr) + ref["anomaly_scores"].sum()
+    lref.backward()
+    det_grad = 0.0
+    for n, p in m.named_parameters():
+        pr = params[n]
+        if pr.grad is None or float(pr.grad.abs().max()) == 0.0:
+            assert p.grad is None or float(p.grad.abs().max()) < 1e-9, n
+            continue
+        if n.startswith("detector."):
+            det_grad = max(det_grad, float(pr.grad.abs().max()))
+        ref_norm = float(pr.grad.norm())
+        np.testing.assert_allclose(p.grad.cpu().numpy(), pr.grad.numpy(), rtol=3e-3,
+                                   atol=1e-7 + 2e-4 * ref_norm / np.sqrt(pr.numel()), err_msg=n)
+    assert det_grad > 0.0

@@ -3,4 +3,4 @@ set -o pipefail
 mkdir -p gpurun_out
 ROOT=$(pwd)
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $ROOT/gpurun_out/tr -o run -- python3 $ROOT/bench.py --no-cpu-baseline --steps 5 --warmup 2 > $ROOT/gpurun_out/tr_bench.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $ROOT/gpurun_out/tr -o run -- python3 $ROOT/bench.py --no-cpu-baseline --steps 5 --warmup 2 --h2d-steps 0 > $ROOT/gpurun_out/tr_bench.log 2>&1
