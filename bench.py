@@ -582,7 +582,14 @@ def main():
                     help="N>1: SyncBatchNorm mode (BN over the global batch = the reference's single-process step)")
     ap.add_argument("--h2d-steps", type=int, default=10,
                     help="steps of the input-inclusive leg (pinned u8 clips through ClipStager; 0 = skip)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KNOB=V",
+                    help="measurement only: set a libvadhip tuning knob (vad_set_tuning) before the run")
     args = ap.parse_args()
+    if args.tune:
+        from vad_amd import _native as nat
+        for kv in args.tune:
+            k, v = kv.split("=")
+            nat.check(nat.lib().vad_set_tuning(k.encode(), int(v)))
     args.config = args.config if args.config == "cad1" else int(args.config)
     preset = {1: (16, 64, 64, "fp32"), 2: (16, 227, 227, "fp32"), 4: (32, 256, 256, "bf16"), 5: (0, 64, 64, "fp32"),
               "cad1": (16, 64, 64, "fp32")}[args.config]

@@ -87,7 +87,10 @@ bool conv3_x3_supported(const Conv3Layer& L, bool fwd);
 int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
                  float* y, float* partials, int* nparts, hipStream_t st);
 int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
-extern int g_wgrad_split;  // stride-1 weight gradients on the split-bf16 kernel (knob "conv_wgrad_split")
+extern int g_wgrad_split;     // stride-1 weight gradients on the split-bf16 kernel (knob "conv_wgrad_split")
+extern int g_wgrad_s1_nt, g_wgrad_s1_nt_blocks, g_wgrad_s1_nt_wide;  // knobs "conv_wgrad_s1_nt", "conv_wgrad_s1_nt_blocks"
+extern int g_wgrad_s2_blocks;  // their target grid size (knob "conv_wgrad_s2_blocks")
+extern int g_wgrad_split_s2;  // stride-2 weight gradients on the split-bf16 kernel (knob "conv_wgrad_split_s2")
 bool conv3_wgrad_x3_supported(const Conv3Layer& L);
 int conv3_wgrad_x3(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
                    int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);

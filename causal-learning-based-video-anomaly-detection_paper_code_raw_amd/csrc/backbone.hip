@@ -920,6 +920,11 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_split_wres") g_x3_wres = value;
   else if (k == "conv_wgrad_patch") g_tune.wgrad_patch = value;
   else if (k == "conv_wgrad_split") g_wgrad_split = value;
+  else if (k == "conv_wgrad_split_s2") g_wgrad_split_s2 = value;
+  else if (k == "conv_wgrad_s2_blocks") g_wgrad_s2_blocks = value;
+  else if (k == "conv_wgrad_s1_nt") g_wgrad_s1_nt = value;
+  else if (k == "conv_wgrad_s1_nt_wide") g_wgrad_s1_nt_wide = value;
+  else if (k == "conv_wgrad_s1_nt_blocks") g_wgrad_s1_nt_blocks = value;
   else if (k == "conv_bf16") g_conv_bf16 = value;  // ops API only (calling thread); plans use their own option
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else {
@@ -1186,14 +1191,16 @@ int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const fl
   });
 }
 
-// Split-K slab reduction of the conv weight gradient.  Block = 32 consecutive slab elements x 8 split-lanes; each
-// lane sums every 8th slab with 4 independent accumulators, lanes are combined through LDS (fixed order).
-// Slab layout [S][co][t*Ci + ci]; dW is torch [co][ci][kh][kw].
+// Split-K slab reduction of the conv weight gradient.  Block = 64 consecutive slab elements (16 float4 columns) x 16
+// split-lanes; each lane sums every 16th slab with 2 independent float4 accumulators (a wave reads 4 slabs x 256 B
+// contiguous per load), lanes are combined through LDS in a fixed order.  (16-way split lanes: the 32-channel layers
+// have few elements and up to 512 slabs.)  Slab layout [S][co][t*Ci + ci]; dW is torch
+// [co][ci][kh][kw].
 __global__ __launch_bounds__(256) void conv3_wgrad_reduce_kernel(const float* __restrict__ part, int S, int Co, int Ci,
                                                                  const float* __restrict__ bparts, int NB,
                                                                  float* __restrict__ dW, float* __restrict__ db,
                                                                  int wblocks) {
-  __shared__ float red[8][33];
+  __shared__ f32x4 red[16][17];
   const int64_t ldp = 9 * Ci;
   const int64_t total = (int64_t)Co * ldp;
   if ((int)blockIdx.x >= wblocks) {  // conv bias: one block per channel, 256-way strided sum + tree
@@ -1201,40 +1208,42 @@ __global__ __launch_bounds__(256) void conv3_wgrad_reduce_kernel(const float* __
     float s = 0.f;
     for (int p = threadIdx.x; p < NB; p += 256) s += bparts[(int64_t)p * 2 * Co + c];
     s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = s;
+    float* r0 = reinterpret_cast<float*>(&red[0][0]);
+    if ((threadIdx.x & 63) == 0) r0[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) db[c] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    if (threadIdx.x == 0) db[c] = (r0[0] + r0[1]) + (r0[2] + r0[3]);
     return;
   }
-  const int e = threadIdx.x & 31, lane8 = threadIdx.x >> 5;
-  const int64_t i = (int64_t)blockIdx.x * 32 + e;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  const int e = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int64_t i = ((int64_t)blockIdx.x * 16 + e) * 4;  // total % 4 == 0 (Ci % 4 == 0)
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
   if (i < total) {
-    int z = lane8;
-    for (; z + 24 < S; z += 32) {
-      a0 += part[(int64_t)z * total + i];
-      a1 += part[(int64_t)(z + 8) * total + i];
-      a2 += part[(int64_t)(z + 16) * total + i];
-      a3 += part[(int64_t)(z + 24) * total + i];
+    int z = sl;
+    for (; z + 16 < S; z += 32) {
+      a0 += *reinterpret_cast<const f32x4*>(part + (int64_t)z * total + i);
+      a1 += *reinterpret_cast<const f32x4*>(part + (int64_t)(z + 16) * total + i);
     }
-    for (; z < S; z += 8) a0 += part[(int64_t)z * total + i];
+    if (z < S) a0 += *reinterpret_cast<const f32x4*>(part + (int64_t)z * total + i);
   }
-  red[lane8][e] = (a0 + a1) + (a2 + a3);
+  red[sl][e] = a0 + a1;
   __syncthreads();
-  if (threadIdx.x < 32 && i < total) {
-    float s = 0.f;
+  if (threadIdx.x < 16 && i < total) {
+    f32x4 q[4];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) s += red[q][e];
+    for (int u = 0; u < 4; ++u) q[u] = (red[4 * u][e] + red[4 * u + 1][e]) + (red[4 * u + 2][e] + red[4 * u + 3][e]);
+    const f32x4 s = (q[0] + q[1]) + (q[2] + q[3]);
     const int64_t co = i / ldp, r = i - co * ldp;
     const int t = (int)(r / Ci), ci = (int)(r - (int64_t)t * Ci);
-    dW[(co * Ci + ci) * 9 + t] = s;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dW[(co * Ci + ci + u) * 9 + t] = s[u];
   }
 }
 
 int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, const float* bias_partials,
                        int nbias_parts, float* dW, float* db, hipStream_t st) {
   const int64_t total = (int64_t)L.Co * L.Ci * 9;
-  const int wblocks = (int)cdiv(total, 32);
+  VAD_CHECK(L.Ci % 4 == 0, "conv3_wgrad_reduce: Ci % 4");
+  const int wblocks = (int)cdiv(total, 64);
   const int bblocks = db ? L.Co : 0;
   hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(256), 0, st, partial, nsplit,
                      L.Co, L.Ci, bias_partials, nbias_parts, dW, db, wblocks);

@@ -424,6 +424,9 @@ struct WgX3Args {
 // hit distinct bank quads
 constexpr int odd16_pitch(int n) { return ((n / 8) & 1) ? n : n + 8; }
 
+__device__ __forceinline__ void wgrad_combine_store(f32x16 (&acc)[9], __bf16* sm, float* out, int co0, int ci0,
+                                                    int Ci);
+
 template <int NI, int TH, int TW, bool PF, int NP>
 __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args p) {
   constexpr int TPX = NI * TH * TW, KS = TPX / 64;
@@ -590,9 +593,16 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
     }
   }
 
-  // fixed-order combine of the 4 waves, 3 taps at a time: (2,3) -> (0,1), then 1 -> 0
+  wgrad_combine_store(acc, sm, p.slab + (int64_t)blockIdx.z * p.Co * 9 * p.Ci, co0, ci0, p.Ci);
+}
+
+// fixed-order combine of the 4 waves' tap accumulators, 3 taps at a time: (2,3) -> (0,1), then 1 -> 0; wave 0
+// writes the block's [32 co][9 taps][32 ci] sum into its slab (LDS: 2*3*16*64 floats)
+__device__ __forceinline__ void wgrad_combine_store(f32x16 (&acc)[9], __bf16* sm, float* out, int co0, int ci0,
+                                                    int Ci) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, j = lane & 31;
   float* red = reinterpret_cast<float*>(sm);
-  float* out = p.slab + (int64_t)blockIdx.z * p.Co * 9 * p.Ci;
 #pragma unroll
   for (int tc = 0; tc < 3; ++tc) {
     __syncthreads();
@@ -623,9 +633,222 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * h, t = tc * 3 + u;
-          out[(int64_t)co * 9 * p.Ci + t * p.Ci + ci0 + j] = acc[t][r] + red[(u * 16 + r) * 64 + lane];
+          out[(int64_t)co * 9 * Ci + t * Ci + ci0 + j] = acc[t][r] + red[(u * 16 + r) * 64 + lane];
         }
     }
+  }
+}
+
+// Multi-co-tile weight gradient (same GEMM view: M = co, N = ci, K = output pixels) for the layers whose staged
+// patch is large against the tile's MFMA work: stride 2 (the patch is ~4x the tile's pixel count) and 8x8 frames
+// (the halo is 56% of the tile).  The block amortises one patch over 32*NT output channels (NT = 2 or 4) of a
+// TPX-pixel tile: wave w owns co tile w % NT and KSW = TPX/16*NT/4 consecutive K steps; the 4/NT waves of a co tile
+// are summed in a fixed order at the end (none for NT = 4).
+// Stride 1: patch rows of TW+8 columns, the kw shifts are a 2-byte v_alignbyte (kw = 1) and a dword shift (kw = 2)
+// of two aligned reads.  Stride 2: output pixel ox reads input columns 2ox-1+kw, so each patch row (2TH+1 rows x
+// 2TW+1 columns incl. halo) is stored parity-split as [E: even patch columns, TW+8 slots][O: odd ones, TW slots];
+// the 8 consecutive output pixels of a lane half need E[ox..ox+7] (kw = 0), O[ox..ox+7] (kw = 1) and E[ox+1..ox+8]
+// (kw = 2, the 2-byte shift): every fragment is an aligned b128 read per plane, no strided LDS access.
+template <int S, int TH, int TW, int NT, int NP>
+__global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Args p) {
+  constexpr int TPX = TH * TW, NC = 32 * NT, KT = TPX / 16, KSW = KT * NT / 4;
+  static_assert((TPX == 32 || TPX == 64) && TW % 8 == 0 && (NT == 2 || NT == 4) && (S == 1 || S == 2),
+                "whole K steps per wave, 8-pixel row runs");
+  constexpr int PH = S * (TH - 1) + 3, PW = S * (TW - 1) + 3, EW = TW + 8, PWP = S == 1 ? TW + 8 : EW + TW;
+  constexpr int NCG = PWP / 4;
+  constexpr int PLANE = PH * PWP, CIP = odd16_pitch(NP * PLANE), DYP = odd16_pitch(NP * TPX);
+  constexpr int XE = 32 * CIP, YE = NC * DYP, RE = 2 * 3 * 16 * 64 * 2;
+  __shared__ __attribute__((aligned(16))) __bf16 sm[(XE + YE) > RE ? (XE + YE) : RE];
+  __bf16* xs = sm;
+  __bf16* ys = sm + XE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, j = lane & 31;
+  const int co0 = blockIdx.x * NC, ci0 = blockIdx.y * 32;
+  const int c4 = tid & 7;  // patch staging: this thread's 4-channel group of the 32 ci
+  constexpr int YG = NC / 4, YQ = TPX / 4 * YG, YIT = (YQ + 255) / 256;  // dY staging: 4 pixels x 4 co per item
+  static_assert(256 % YG == 0 && (YQ <= 256 || YQ % 256 == 0), "whole dY staging passes");
+  const int yc = tid % YG;
+
+  constexpr int XQ = PH * NCG * 8, XIT = (XQ + 255) / 256;
+  static_assert(XIT <= 2, "patch staged in one register pass");
+  f32x4 xv[XIT][4], yv[YIT][4];
+  // patch column (0 = input column S*x0 - 1) held by LDS column c of a row
+  auto pcol = [](int c) { return S == 1 ? c : (c < EW ? 2 * c : 2 * (c - EW) + 1); };
+  auto origin = [&](int tile, int& img, int& y0, int& x0) {
+    const int tpi = p.tiles_h * p.tiles_w, tr = tile % tpi;
+    img = tile / tpi;
+    y0 = (tr / p.tiles_w) * TH;
+    x0 = (tr % p.tiles_w) * TW;
+  };
+  auto fetch = [&](int tile) {
+    int img, y0, x0;
+    origin(tile, img, y0, x0);
+#pragma unroll
+    for (int it = 0; it < YIT; ++it) {
+      const int yp = ((tid + it * 256) / YG) * 4, oy = y0 + yp / TW, ox = x0 + yp % TW;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        yv[it][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!(p.dbg & 8) && tid + it * 256 < YQ && oy < p.OH && ox + e < p.OW)
+          yv[it][e] = *reinterpret_cast<const f32x4*>(p.dY + (((int64_t)img * p.OH + oy) * p.OW + ox + e) * p.Co +
+                                                      co0 + yc * 4);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < XIT; ++it) {
+      const int q = tid + it * 256, g = q >> 3;
+      const int row = g / NCG, cg = g % NCG, iy = S * y0 - 1 + row;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int pc = pcol(cg * 4 + e), ix = S * x0 - 1 + pc;
+        xv[it][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!(p.dbg & 8) && q < XQ && pc < PW && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
+          xv[it][e] = *reinterpret_cast<const f32x4*>(p.src + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.Ci + ci0 +
+                                                      c4 * 4);
+      }
+    }
+  };
+  f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+  if (p.scale) {
+    sc = *reinterpret_cast<const f32x4*>(p.scale + ci0 + c4 * 4);
+    sh = *reinterpret_cast<const f32x4*>(p.shift + ci0 + c4 * 4);
+  }
+  // 4 channels (rows ch0..ch0+3 of pitch `pitch`) x 4 consecutive columns -> per channel and plane one 8-B store
+  auto put4 = [&](__bf16* dst, int pitch, int plane_stride, const f32x4* v) {
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 hi, mid, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = v[e][cc];
+        const __bf16 a = (__bf16)x;
+        if (NP == 1 || (p.dbg & 2)) {
+          hi[e] = mid[e] = lo[e] = a;
+          continue;
+        }
+        const float r = x - (float)a;
+        const __bf16 b = (__bf16)r;
+        hi[e] = a;
+        mid[e] = b;
+        lo[e] = (__bf16)(r - (float)b);
+      }
+      __bf16* d = dst + cc * pitch;
+      *reinterpret_cast<bf16x4*>(d) = hi;
+      if constexpr (NP == 3) {
+        *reinterpret_cast<bf16x4*>(d + plane_stride) = mid;
+        *reinterpret_cast<bf16x4*>(d + 2 * plane_stride) = lo;
+      }
+    }
+  };
+  auto stash = [&](int tile) {
+    int img, y0, x0;
+    origin(tile, img, y0, x0);
+#pragma unroll
+    for (int it = 0; it < YIT; ++it)
+      if (tid + it * 256 < YQ) put4(ys + yc * 4 * DYP + ((tid + it * 256) / YG) * 4, DYP, TPX, yv[it]);
+#pragma unroll
+    for (int it = 0; it < XIT; ++it) {
+      const int q = tid + it * 256, g = q >> 3;
+      if (q < XQ) {
+        const int row = g / NCG, cg = g % NCG, iy = S * y0 - 1 + row;
+        f32x4 v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = xv[it][e];
+          const int pc = pcol(cg * 4 + e), ix = S * x0 - 1 + pc;
+          // zero padding stays zero (the reference pads relu(bn(y)) with zeros)
+          if (p.scale && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW && pc < PW) {
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) v[e][cc] = relu_nan(fmaf(v[e][cc], sc[cc], sh[cc]));
+          }
+        }
+        put4(xs + c4 * 4 * CIP + row * PWP + cg * 4, CIP, PLANE, v);
+      }
+    }
+  };
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  const int ct = wave % NT, ks0 = (wave / NT) * KSW;  // this wave's co tile and first K step
+  for (int tile = blockIdx.z; tile < p.ntiles; tile += gridDim.z) {
+    fetch(tile);
+    __syncthreads();  // the previous tile's fragment reads are done
+    stash(tile);
+    __syncthreads();
+    if (p.dbg & 4) continue;
+#pragma unroll
+    for (int k = 0; k < KSW; ++k) {
+      const int lin = (ks0 + k) * 16 + 8 * h, oyr = lin / TW, oxr = lin % TW;
+      bf16x8 a[NP];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) a[q] = *reinterpret_cast<const bf16x8*>(ys + (ct * 32 + j) * DYP + q * TPX + lin);
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const __bf16* xb = xs + j * CIP + (S * oyr + kh) * PWP + oxr;
+#pragma unroll
+        for (int q = NP - 1; q >= 0; --q) {
+          const u32x4 d0 = *reinterpret_cast<const u32x4*>(xb + q * PLANE);
+          const u32x4 d1 = *reinterpret_cast<const u32x4*>(xb + q * PLANE + 8);
+          const u32x4 s1 = {__builtin_amdgcn_alignbyte(d0[1], d0[0], 2), __builtin_amdgcn_alignbyte(d0[2], d0[1], 2),
+                            __builtin_amdgcn_alignbyte(d0[3], d0[2], 2), __builtin_amdgcn_alignbyte(d1[0], d0[3], 2)};
+          bf16x8 b0 = __builtin_bit_cast(bf16x8, d0), b1, b2;
+          if constexpr (S == 1) {
+            const u32x4 s2 = {d0[1], d0[2], d0[3], d1[0]};
+            b1 = __builtin_bit_cast(bf16x8, s1);
+            b2 = __builtin_bit_cast(bf16x8, s2);
+          } else {
+            b1 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(xb + q * PLANE + EW));
+            b2 = __builtin_bit_cast(bf16x8, s1);
+          }
+#pragma unroll
+          for (int qa = NP - 1 - q; qa >= 0; --qa) {
+            acc[kh * 3 + 0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[qa], b0, acc[kh * 3 + 0], 0, 0, 0);
+            acc[kh * 3 + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[qa], b1, acc[kh * 3 + 1], 0, 0, 0);
+            acc[kh * 3 + 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[qa], b2, acc[kh * 3 + 2], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+
+  float* out = p.slab + (int64_t)blockIdx.z * p.Co * 9 * p.Ci;
+  const int cob = co0 + ct * 32;
+  if constexpr (NT == 2) {
+    // waves w and w + 2 hold the two K steps of co tile w: (w) + (w + 2), 3 taps at a time
+    float* red = reinterpret_cast<float*>(sm);
+#pragma unroll
+    for (int tc = 0; tc < 3; ++tc) {
+      __syncthreads();
+      if (wave >= 2) {
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) red[(((wave - 2) * 3 + u) * 16 + r) * 64 + lane] = acc[tc * 3 + u][r];
+      }
+      __syncthreads();
+      if (wave < 2) {
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int co = cob + (r & 3) + 8 * (r >> 2) + 4 * h, t = tc * 3 + u;
+            out[(int64_t)co * 9 * p.Ci + t * p.Ci + ci0 + j] = acc[t][r] + red[((wave * 3 + u) * 16 + r) * 64 + lane];
+          }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = cob + (r & 3) + 8 * (r >> 2) + 4 * h;
+        out[(int64_t)co * 9 * p.Ci + t * p.Ci + ci0 + j] = acc[t][r];
+      }
   }
 }
 
@@ -645,17 +868,47 @@ static int launch_wgrad_x3(WgX3Args a, int target_blocks, int64_t partial_cap, h
   return 0;
 }
 
-int g_wgrad_split = 1;  // tuning knob "conv_wgrad_split": stride-1 weight gradients on the split-bf16 kernel
+template <int S, int TH, int TW, int NT>
+static int launch_wgrad_x3nt(WgX3Args a, int target_blocks, int64_t partial_cap, hipStream_t st, int* nsplit) {
+  a.tiles_h = (int)cdiv(a.OH, TH);
+  a.tiles_w = (int)cdiv(a.OW, TW);
+  a.ntiles = (int)((int64_t)a.NF * a.tiles_h * a.tiles_w);
+  const int pairs = (a.Co / (32 * NT)) * (a.Ci / 32);
+  int64_t z = std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, pairs), a.ntiles));
+  z = std::min<int64_t>(z, std::max<int64_t>(1, partial_cap / ((int64_t)a.Co * 9 * a.Ci)));
+  dim3 grid((unsigned)(a.Co / (32 * NT)), (unsigned)(a.Ci / 32), (unsigned)z);
+  if (g_conv_bf16) VAD_KLAUNCH((conv3x3_wgrad_x3nt_kernel<S, TH, TW, NT, 1>), grid, dim3(256), 0, st, a);
+  else VAD_KLAUNCH((conv3x3_wgrad_x3nt_kernel<S, TH, TW, NT, 3>), grid, dim3(256), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  *nsplit = (int)z;
+  return 0;
+}
+
+template <int S, int TH, int TW>
+static int launch_wgrad_x3nt_co(WgX3Args a, int nt, int target_blocks, int64_t partial_cap, hipStream_t st,
+                                int* nsplit) {
+  if (nt == 4 && a.Co % 128 == 0) return launch_wgrad_x3nt<S, TH, TW, 4>(a, target_blocks, partial_cap, st, nsplit);
+  return launch_wgrad_x3nt<S, TH, TW, 2>(a, target_blocks, partial_cap, st, nsplit);
+}
+
+int g_wgrad_split = 1;     // tuning knob "conv_wgrad_split": stride-1 weight gradients on the split-bf16 kernel
+int g_wgrad_split_s2 = 1;  // tuning knob "conv_wgrad_split_s2": stride-2 weight gradients on the split-bf16 kernel
+int g_wgrad_s2_blocks = 512;  // tuning knob "conv_wgrad_s2_blocks": their target grid size
+int g_wgrad_s1_nt = 2;  // tuning knob "conv_wgrad_s1_nt": stride-1 frames <= 16 wide on the multi-co-tile kernel (2|4)
+int g_wgrad_s1_nt_wide = 0;  // knob "conv_wgrad_s1_nt_wide": wider stride-1 frames too (2x32 tiles)
+int g_wgrad_s1_nt_blocks = 512;  // knob "conv_wgrad_s1_nt_blocks"
 
 bool conv3_wgrad_x3_supported(const Conv3Layer& L) {
+  if (!g_conv_split || L.Ci % 32 != 0 || L.Co % 32 != 0) return false;
+  if (L.stride == 2) return g_wgrad_split_s2 != 0 && L.Co % 64 == 0;
   // (8x8 frames: 64-pixel tiles carry too little MFMA work per staged patch; the f32 patch kernel is faster there)
-  return g_conv_split && g_wgrad_split && L.stride == 1 && L.Ci % 32 == 0 && L.Co % 32 == 0 &&
-         (L.OH > 8 || L.OW > 8 || g_wgrad_split == 2 || g_conv_bf16);
+  return L.stride == 1 && g_wgrad_split &&
+         (L.OH > 8 || L.OW > 8 || g_wgrad_split == 2 || g_conv_bf16 || (g_wgrad_s1_nt && L.Co % 64 == 0));
 }
 
 int conv3_wgrad_x3(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
                    int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st) {
-  VAD_CHECK(conv3_wgrad_x3_supported(L), "conv3_wgrad_x3: stride 1, Ci and Co multiples of 32");
+  VAD_CHECK(conv3_wgrad_x3_supported(L), "conv3_wgrad_x3: Ci and Co multiples of 32");
   VAD_CHECK(partial_cap >= (int64_t)L.Co * 9 * L.Ci, "conv3_wgrad_x3: slab capacity below one split");
   WgX3Args a{};
   a.dY = dY;
@@ -665,6 +918,19 @@ int conv3_wgrad_x3(const Conv3Layer& L, const float* dY, const float* src, const
   a.slab = slab;
   a.NF = L.NF; a.IH = L.IH; a.IW = L.IW; a.Ci = L.Ci; a.OH = L.OH; a.OW = L.OW; a.Co = L.Co;
   a.dbg = g_x3_dbg;
+  if (L.stride == 2) {
+    VAD_CHECK(L.IH >= 2 * L.OH - 1 && L.IW >= 2 * L.OW - 1, "conv3_wgrad_x3: stride-2 geometry");
+    target_blocks = g_wgrad_s2_blocks;
+    if (L.OW > 16) return launch_wgrad_x3nt_co<2, 1, 32>(a, 4, target_blocks, partial_cap, st, nsplit);
+    if (L.OW > 8) return launch_wgrad_x3nt_co<2, 2, 16>(a, 4, target_blocks, partial_cap, st, nsplit);
+    return launch_wgrad_x3nt_co<2, 4, 8>(a, 4, target_blocks, partial_cap, st, nsplit);
+  }
+  if (g_wgrad_s1_nt && L.Co % 64 == 0 && (L.OW <= 16 || g_wgrad_s1_nt_wide)) {
+    if (L.OW > 16) return launch_wgrad_x3nt_co<1, 2, 32>(a, g_wgrad_s1_nt, g_wgrad_s1_nt_blocks, partial_cap, st, nsplit);
+    if (L.OW <= 8 && L.OH <= 8)
+      return launch_wgrad_x3nt_co<1, 8, 8>(a, g_wgrad_s1_nt, g_wgrad_s1_nt_blocks, partial_cap, st, nsplit);
+    return launch_wgrad_x3nt_co<1, 4, 16>(a, g_wgrad_s1_nt, g_wgrad_s1_nt_blocks, partial_cap, st, nsplit);
+  }
   if (L.OH <= 8 && L.OW <= 8) return launch_wgrad_x3<1, 8, 8>(a, target_blocks, partial_cap, st, nsplit);
   if (L.OW <= 16) return launch_wgrad_x3<1, 8, 16>(a, target_blocks, partial_cap, st, nsplit);
   return launch_wgrad_x3<1, 4, 32>(a, target_blocks, partial_cap, st, nsplit);
