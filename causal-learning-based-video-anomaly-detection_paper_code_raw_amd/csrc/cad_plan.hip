@@ -575,6 +575,9 @@ struct CadPlanImpl {
   // option "stem_grad": backbone.conv1 / bn1 train (the reference's module without apply_memory_efficient_training);
   // stem_active: the last backward wrote their grads (the fused optimizer then steps them too)
   int stem_grad = 0, stem_active = 0;
+  int y1_fresh = 0;  // the last forward wrote conv1's output y1 (the stem backward reads it)
+  // BN state layer1.0 applies on load to `pool`: bn1's (fused stem: `pool` holds the raw pooled conv1 output) or none
+  const float* pool_stats = nullptr;
 
   // batch statistics of BN layer i (0 = bn1) from the `np` partials in `parts`: local (default) or, with a sync
   // callback in training mode, over the whole process group (torch.nn.SyncBatchNorm semantics)
@@ -617,11 +620,23 @@ struct CadPlanImpl {
     }
     int np = 0;
     bwd_state = 0;
-    TIMED("conv1", conv1_fwd(x, NF, H, W, P(LY.conv1_w), P(LY.conv1_b), y1, H1, W1, parts, &np, st));
-    VAD_TRY(bn_fwd_stats(0, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), st));
-    TIMED("maxpool", maxpool3s2_bnrelu(y1, stats[0], NF, H1, W1, 32, pool, HP, WP, st));
+    y1_fresh = !(g_stem_fused && !stem_grad && stem_fused_ok(W1));
+    if (!y1_fresh) {
+      // frozen stem (the training default): conv1 + BN sums + pooling of the raw output in one pass (stem.hip);
+      // `pool` then holds the pooled conv1 output and layer1.0 applies bn1 + ReLU on load
+      TIMED("conv1", stem_fused(x, NF, H, W, P(LY.conv1_w), P(LY.conv1_b), P(LY.bn1_w), H1, W1, pool, HP, WP, parts,
+                                &np, st));
+      VAD_TRY(bn_fwd_stats(0, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), st));
+      pool_stats = stats[0];
+    } else {
+      // training stem: the backward's MaxPool / bn1 / conv1 gradients read conv1's output y1
+      TIMED("conv1", conv1_fwd(x, NF, H, W, P(LY.conv1_w), P(LY.conv1_b), y1, H1, W1, parts, &np, st));
+      VAD_TRY(bn_fwd_stats(0, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), st));
+      TIMED("maxpool", maxpool3s2_bnrelu(y1, stats[0], NF, H1, W1, 32, pool, HP, WP, st));
+      pool_stats = nullptr;
+    }
     const float* src = pool;
-    const float* sst = nullptr;
+    const float* sst = pool_stats;
     for (int l = 0; l < 8; ++l) {
       TIMED(L_("conv_fwd", l), conv3_fwd(L[l], src, sst, wf[l], P(LY.conv_b[l]), y[l], parts, &np, st));
       VAD_TRY(bn_fwd_stats(l + 1, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]), st));
@@ -764,7 +779,7 @@ struct CadPlanImpl {
       VAD_TRY(bn_bwd_stats(l + 1, np, C, (double)M, P(LY.bn_w[l]), G(LY.bn_w[l]), G(LY.bn_b[l]), G(LY.conv_b[l]), st));
       TIMED(L_("bn_bwd_apply", l), bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dY, nullptr, &nb, st));
       const float* src = l == 0 ? pool : y[l - 1];
-      const float* sst = l == 0 ? nullptr : stats[l];
+      const float* sst = l == 0 ? pool_stats : stats[l];
       TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dY, src, sst, wpart, &ns, wpart_floats, st));
       TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], wpart, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
       if (l > 0) TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dY, wd[l], dA, st));
@@ -772,6 +787,7 @@ struct CadPlanImpl {
     }
     stem_active = 0;
     if (stem_grad && debug_stop_layer < 0) {
+      VAD_CHECK(y1_fresh, "stem backward: the forward ran with the stem frozen (set option stem_grad before it)");
       // the stem (cad:145-147): input gradient of layer1.0 into the pooled map, MaxPool2d backward, bn1 backward (in
       // place), conv1 weight gradient (its bias gradient comes from the bn1 finalize)
       TIMED("stem_bwd", conv3_dgrad(L[0], dY, wd[0], dA, st));

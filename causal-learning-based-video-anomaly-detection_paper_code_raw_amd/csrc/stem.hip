@@ -1,0 +1,252 @@
+// Frozen-stem forward without the conv1 activation round trip (the training default: train_model freezes
+// backbone.conv1 / bn1, cad:592-598, so nothing downstream needs conv1's output, only maxpool(relu(bn1(.))).
+//
+// One pass: conv1 (1 -> 32, 7x7, s2, p3) + bias, the BN partial sums, and the 3x3 / stride-2 pooling of the RAW
+// output y, taken per channel as a max where bn1's gamma >= 0 and as a min where gamma < 0.  bn1+ReLU is applied
+// on load by layer1.0's kernels (as for every other layer): z = relu(fma(y, scale, shift)) is monotone in y,
+// non-decreasing for scale = gamma * invstd >= 0 and non-increasing for scale < 0, so
+//   maxpool(relu(fma(y, s, t))) == relu(fma(gamma >= 0 ? maxpool(y) : minpool(y), s, t))
+// exactly (rounding is monotone too), while the batch statistics that set s and t are still being accumulated.
+// The 114x114x32 activation (213 MB at config 2) is neither written nor read: the stem reads the input once
+// (26 MB) and writes the pooled map (53 MB).
+//
+// conv1 runs on the bf16 MFMA with both operands split three ways (hi + mid + lo, six products: fp32-class
+// numerics, see conv_x3.hip) as a GEMM M = 32 output pixels, N = 32 channels, K = 8 kernel rows x 8 columns (row 7
+// and column 7 zero): K step ks covers kernel rows 2ks (lane half 0) and 2ks+1 (half 1), so a lane's 8 A values are
+// input columns 2ox-3 .. 2ox+4 of one input row -- four consecutive dwords of a bf16 LDS row (x is staged once per
+// band as 3 bf16 planes).  The weights live in 48 registers.  A wave's 32 pixels are conv columns c0-1 .. c0+30 of
+// one row (c0 = 30 * tile): after swapping the lane halves every lane holds all 32 values of its channel and takes
+// the 15 horizontal windows (columns 2px-1 .. 2px+1) in registers; the block keeps the horizontally pooled rows in
+// LDS and pools vertically at the end.
+#include <algorithm>
+
+#include "backbone.h"
+
+namespace vad {
+
+typedef __bf16 bf16x8s __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+
+namespace {
+
+__device__ __forceinline__ void split3s(float v, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)v;
+  const float r = v - (float)h;
+  m = (__bf16)r;
+  l = (__bf16)(r - (float)m);
+}
+
+// B fragments: w[co = lane & 31][kh = 2ks + (lane >> 5)][kw = 0..7], zero outside the 7x7 kernel
+__device__ __forceinline__ void stem_weights(const float* __restrict__ w, bf16x8s (&b)[4][3]) {
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int kh = 2 * ks + h;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = (kh < 7 && e < 7) ? w[j * 49 + kh * 7 + e] : 0.f;
+      __bf16 hi, mid, lo;
+      split3s(v, hi, mid, lo);
+      b[ks][0][e] = hi;
+      b[ks][1][e] = mid;
+      b[ks][2][e] = lo;
+    }
+  }
+}
+
+// staging of input rows [2*c0 - 3, 2*c0 - 3 + rows) x columns [-3, PWb - 3) of a frame as 3 bf16 planes (zero
+// padding), in two halves so the global loads of the next band can be in flight during the current one's MFMAs:
+// item q = column pair m of row pr, held by thread q % 256 in register slot q / 256
+template <int N>  // register slots: rows * PWb / 2 <= N * 256
+struct StemRegs {
+  static constexpr int items = N;
+  float v[N][2];
+};
+
+template <class R>
+__device__ __forceinline__ void stem_fetch(const float* __restrict__ xi, int H, int W, int c0, int rows, int PWb,
+                                           R& r) {
+  constexpr int ST_ITEMS = R::items;
+  const int half = PWb / 2;
+#pragma unroll
+  for (int k = 0; k < ST_ITEMS; ++k) {
+    const int q = threadIdx.x + k * 256;
+    const int pr = q / half, m = q - pr * half;
+    const int ih = 2 * c0 - 3 + pr, iw = 2 * m - 3;
+    r.v[k][0] = r.v[k][1] = 0.f;
+    if (pr < rows && ih >= 0 && ih < H) {
+      if (iw >= 0 && iw < W) r.v[k][0] = xi[(int64_t)ih * W + iw];
+      if (iw + 1 >= 0 && iw + 1 < W) r.v[k][1] = xi[(int64_t)ih * W + iw + 1];
+    }
+  }
+}
+
+template <class R>
+__device__ __forceinline__ void stem_store(const R& r, int rows, int PWb, __bf16* xs) {
+  constexpr int ST_ITEMS = R::items;
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const int half = PWb / 2, plane2 = rows * half;  // plane stride in bf16 pairs
+  bf16x2* d = reinterpret_cast<bf16x2*>(xs);
+#pragma unroll
+  for (int k = 0; k < ST_ITEMS; ++k) {
+    const int q = threadIdx.x + k * 256;
+    if (q < rows * half) {
+      __bf16 h0, m0, l0, h1, m1, l1;
+      split3s(r.v[k][0], h0, m0, l0);
+      split3s(r.v[k][1], h1, m1, l1);
+      const bf16x2 hi = {h0, h1}, mid = {m0, m1}, lo = {l0, l1};
+      d[q] = hi;  // q = pr * half + m
+      d[q + plane2] = mid;
+      d[q + 2 * plane2] = lo;
+    }
+  }
+}
+
+// block = (frame, band of ST_PB pooled rows): conv rows 2*py0-1 .. 2*py1-1 (the first one is the previous band's
+// last and is recomputed; rows 2*py0 .. 2*py1-1 are this band's own for the BN sums), per conv row ceil(WP/15)
+// tiles of 32 columns.
+constexpr int ST_PB = 3;
+constexpr int ST_SLOTS = 12;  // input staging register slots: (2 * (2 * ST_PB + 1) + 6) rows * PWb / 2 <= 12 * 256
+
+__global__ __launch_bounds__(256, 2) void stem_fused_kernel(const float* __restrict__ x, int H, int W,
+                                                            const float* __restrict__ w,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ gamma, int OH, int OW, int HP,
+                                                            int WP, int nbands, int PWb, float* __restrict__ pool,
+                                                            float* __restrict__ partials) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
+  constexpr int C = 32;
+  const int img = blockIdx.x / nbands, band = blockIdx.x % nbands;
+  const int py0 = band * ST_PB, py1 = min(HP, py0 + ST_PB);
+  const int c_lo = max(2 * py0 - 1, 0), c_hi = min(2 * py1 - 1, OH - 1), n = c_hi - c_lo + 1;
+  const int rows = 2 * n + 6;
+  float* hrow = reinterpret_cast<float*>(smb);  // [n][WP][32] horizontally pooled rows
+  __bf16* xs = smb + 2 * (2 * ST_PB + 1) * WP * C;
+  bf16x8s b[4][3];
+  stem_weights(w, b);
+  {
+    StemRegs<ST_SLOTS> sr;
+    stem_fetch(x + (int64_t)img * H * W, H, W, c_lo, rows, PWb, sr);
+    stem_store(sr, rows, PWb, xs);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
+  const float bj = bias[j];
+  const bool neg = gamma[j] < 0.f;  // this channel pools the minimum (as the maximum of -y)
+  const int ntr = (WP + 14) / 15;   // tiles per conv row
+  __syncthreads();
+  float s1 = 0.f, s2 = 0.f;
+  for (int t = wave; t < n * ntr; t += 4) {
+    const int rl = t / ntr, c0 = 30 * (t - rl * ntr);
+    const int crow = c_lo + rl;
+    // lane pixel: conv column c0 - 1 + (lane & 31) of conv row crow (address clamped; out-of-map columns excluded)
+    const int col = c0 - 1 + (lane & 31), colc = min(max(col, 0), OW - 1);
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int plane2 = rows * PWb / 2;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const unsigned* rowp = reinterpret_cast<const unsigned*>(xs + (2 * rl + 2 * ks + h) * PWb) + colc;
+      bf16x8s a[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const unsigned* sp = rowp + q * plane2;
+        const u32x4s d = {sp[0], sp[1], sp[2], sp[3]};
+        a[q] = __builtin_bit_cast(bf16x8s, d);
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[ks][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[ks][1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[ks][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][0], acc, 0, 0, 0);
+    }
+    // D row i (pixel = column c0 - 1 + i) of register r in lane half h: i = (r & 3) + 8 (r >> 2) + 4 h
+    const bool own_row = crow >= 2 * py0;
+    float v[16], o[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = (r & 3) + 8 * (r >> 2) + 4 * h, c = c0 - 1 + i;
+      const float y = acc[r] + bj;
+      const bool ok = c >= 0 && c < OW;
+      if (ok && own_row && i >= 1 && i <= 30) {  // column c0-1 / c0+30 belong to the neighbouring tiles
+        s1 += y;
+        s2 = fmaf(y, y, s2);
+      }
+      v[r] = ok ? (neg ? -y : y) : -INFINITY;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = __shfl_xor(v[r], 32, 64);
+    // value of pixel i: lane half (i >> 2) & 1 holds it in register (i & 3) + 4 (i >> 3)
+    auto val = [&](int i) { return (((i >> 2) & 1) == h) ? v[(i & 3) + 4 * (i >> 3)] : o[(i & 3) + 4 * (i >> 3)]; };
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+      const float m = fmaxf(fmaxf(val(2 * k), val(2 * k + 1)), val(2 * k + 2));
+      const int px = 15 * (c0 / 30) + k;
+      if ((h == 0 ? k < 8 : k >= 8) && px < WP) hrow[(rl * WP + px) * C + j] = m;
+    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < (py1 - py0) * WP * (C / 4); q += blockDim.x) {
+    const int pyl = q / (WP * (C / 4)), rem = q - pyl * (WP * (C / 4));
+    const int px = rem / (C / 4), c = (rem % (C / 4)) * 4, py = py0 + pyl;
+    f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int cr = 2 * py + dy;
+      if (cr < 0 || cr >= OH) continue;
+      const f32x4 u = *reinterpret_cast<const f32x4*>(hrow + ((cr - c_lo) * WP + px) * C + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], u[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (gamma[c + e] < 0.f) m[e] = -m[e];
+    *reinterpret_cast<f32x4*>(pool + (((int64_t)img * HP + py) * WP + px) * C + c) = m;
+  }
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  __syncthreads();
+  float* red = hrow;  // [4 waves][2][32]
+  if (lane < 32) {
+    red[wave * 64 + lane] = s1;
+    red[wave * 64 + 32 + lane] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int t = threadIdx.x;
+    partials[(int64_t)blockIdx.x * 64 + t] = (red[t] + red[64 + t]) + (red[128 + t] + red[192 + t]);
+  }
+}
+
+}  // namespace
+
+int g_stem_fused = 1;  // tuning knob "stem_fused": the frozen stem's forward without the conv1 activation
+
+static int stem_pitch(int OW) { return (int)cdiv(2 * OW + 6, 8) * 8; }
+static size_t stem_lds(int OW) {
+  const int WP = (OW - 1) / 2 + 1;
+  return (size_t)(2 * ST_PB + 1) * WP * 32 * sizeof(float) +
+         (size_t)3 * (2 * (2 * ST_PB + 1) + 6) * stem_pitch(OW) * sizeof(__bf16);
+}
+
+bool stem_fused_ok(int OW) {
+  return OW >= 2 && (2 * (2 * ST_PB + 1) + 6) * stem_pitch(OW) / 2 <= ST_SLOTS * 256 && stem_lds(OW) <= 160 * 1024;
+}
+
+int stem_fused(const float* x, int NF, int H, int W, const float* w, const float* b, const float* gamma, int OH,
+               int OW, float* pool, int HP, int WP, float* partials, int* nparts, hipStream_t st) {
+  VAD_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && HP == (OH - 1) / 2 + 1 && WP == (OW - 1) / 2 + 1,
+            "stem_fused: bad dims");
+  VAD_CHECK(stem_fused_ok(OW), "stem_fused: frame width");
+  const int nbands = (int)cdiv(HP, ST_PB);
+  // (the partial rows fit the conv1_fwd layout: ceil(ceil(OH/2)/3) == ceil(OH/6))
+  VAD_CHECK(nbands == (int)cdiv(OH, 6) && (int64_t)NF * nbands == conv1_num_parts(NF, OH), "stem_fused: partials");
+  VAD_KLAUNCH(stem_fused_kernel, dim3(NF * nbands), dim3(256), stem_lds(OW), st, x, H, W, w, b, gamma, OH, OW, HP,
+              WP, nbands, stem_pitch(OW), pool, partials);
+  VAD_LAUNCH_CHECK();
+  *nparts = NF * nbands;
+  return 0;
+}
+
+}  // namespace vad

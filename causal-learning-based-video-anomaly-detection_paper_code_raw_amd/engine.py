@@ -196,6 +196,8 @@ class CadEngine:
             raise ValueError("ResNetBackbone here takes single-channel frames (input_channels=1, cad:515)")
         x = x.contiguous().float()
         pl = self.plan(B, T, H, W)
+        # (before the forward: a training stem needs conv1's activation stored, a frozen one is recomputed in place)
+        self._set_stem_grad(pl)
         dev = self.device
         if not want_outputs:
             if self._loss_buf is None:

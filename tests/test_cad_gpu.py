@@ -230,6 +230,59 @@ def test_hip_backward_matches_oracle_full_size():
     print(f"worst per-tensor relative L2 vs the mask-pinned oracle: {worst:.3g}")
 
 
+@pytest.mark.parametrize("B,T,H,W", [(2, 8, 227, 227), (1, 4, 256, 256), (1, 3, 64, 80)])
+def test_fused_stem_matches_float64_stem(B, T, H, W):
+    """Frozen stem (stem.hip: conv1 + BN sums + 3x3/s2 pooling of the raw output -- max where gamma >= 0, min where
+    gamma < 0 -- in one pass, bn1 + ReLU applied on load by layer1.0) against the float64 stem
+    maxpool(relu(bn1_train(conv1(x)))) and against the stored-activation path (knob stem_fused=0); bn1's running
+    statistics too.  One bn1 gamma is made negative so both pooling directions are exercised."""
+    from tests.golden_util import read_debug
+    from vad_amd import _native as nat
+    case = dict(name="stem", B=B, T=T, H=H, W=W, seed=9, step=1, forced=None)
+    x = co.synth_clips(9, 1, 0, B, T, H, W)
+    y = co.synth_labels(0, B)
+    pools, rstats = [], []
+    for fused in (1, 0):
+        nat.check(nat.lib().vad_set_tuning(b"stem_fused", fused))
+        try:
+            m = _frozen(make_cad_model(case))
+            with torch.no_grad():
+                m.backbone.bn1.weight[3] = -0.75
+            m = m.cuda()
+            eng = m.engine()
+            eng.forward(x.cuda(), True, 9, 1, 0, y.cuda())
+            torch.cuda.synchronize()
+            pool = read_debug(eng._last[0], "pool").astype(np.float64)
+            if fused:  # raw pooled conv1 output: bn1 + ReLU as layer1.0 applies them on load
+                st = read_debug(eng._last[0], "stats", 0).astype(np.float64)
+                pool = np.maximum(pool.reshape(-1, 32) * st[64:96] + st[96:128], 0.0).reshape(-1)
+            pools.append(pool)
+            bufs = dict(m.named_buffers())
+            rstats.append([bufs[k].cpu().numpy() for k in ("backbone.bn1.running_mean", "backbone.bn1.running_var")])
+        finally:
+            nat.check(nat.lib().vad_set_tuning(b"stem_fused", 1))
+    sd = make_cad_model(case).state_dict()
+    sd["backbone.bn1.weight"] = sd["backbone.bn1.weight"].clone()
+    sd["backbone.bn1.weight"][3] = -0.75
+    xd = x.reshape(B * T, 1, H, W).double()
+    c = torch.nn.functional.conv2d(xd, sd["backbone.conv1.weight"].double(), sd["backbone.conv1.bias"].double(),
+                                   stride=2, padding=3)
+    mean, var = c.mean(dim=(0, 2, 3)), c.var(dim=(0, 2, 3), unbiased=False)
+    z = (c - mean[None, :, None, None]) / torch.sqrt(var[None, :, None, None] + 1e-5)
+    z = z * sd["backbone.bn1.weight"].double()[None, :, None, None] + sd["backbone.bn1.bias"].double()[None, :, None, None]
+    ref = torch.nn.functional.max_pool2d(torch.relu(z), 3, 2, 1).permute(0, 2, 3, 1).reshape(-1).numpy()
+    scale = float(np.abs(ref).max())
+    for got in pools:
+        assert got.shape == ref.shape
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5 * scale)
+    np.testing.assert_allclose(pools[0], pools[1], rtol=1e-5, atol=1e-6 * scale)
+    rm = 0.9 * sd["backbone.bn1.running_mean"].double() + 0.1 * mean
+    rv = 0.9 * sd["backbone.bn1.running_var"].double() + 0.1 * c.var(dim=(0, 2, 3), unbiased=True)
+    for got_m, got_v in rstats:
+        np.testing.assert_allclose(got_m, rm.numpy(), rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(got_v, rv.numpy(), rtol=1e-5, atol=1e-7)
+
+
 @pytest.mark.parametrize("B,T,H,W", [(2, 32, 256, 256)])
 def test_config4_shape_fp32_and_bf16(B, T, H, W):
     """BASELINE config 4 shape (T=32, 256x256; 2 clips per rank here to bound the oracle's CPU time).
