@@ -16,8 +16,8 @@
 // input columns 2ox-3 .. 2ox+4 of one input row -- four consecutive dwords of a bf16 LDS row (x is staged once per
 // band as 3 bf16 planes).  The weights live in 48 registers.  A wave's 32 pixels are conv columns c0-1 .. c0+30 of
 // one row (c0 = 30 * tile): after swapping the lane halves every lane holds all 32 values of its channel and takes
-// the 15 horizontal windows (columns 2px-1 .. 2px+1) in registers; the block keeps the horizontally pooled rows in
-// LDS and pools vertically at the end.
+// the 15 horizontal windows (columns 2px-1 .. 2px+1) in registers; the block folds them into its pooled rows in LDS
+// (ds_max_f32) and writes them at the end.
 #include <algorithm>
 
 #include "backbone.h"
@@ -108,7 +108,7 @@ __device__ __forceinline__ void stem_store(const R& r, int rows, int PWb, __bf16
 constexpr int ST_PB = 3;
 constexpr int ST_SLOTS = 12;  // input staging register slots: (2 * (2 * ST_PB + 1) + 6) rows * PWb / 2 <= 12 * 256
 
-__global__ __launch_bounds__(256, 2) void stem_fused_kernel(const float* __restrict__ x, int H, int W,
+__global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restrict__ x, int H, int W,
                                                             const float* __restrict__ w,
                                                             const float* __restrict__ bias,
                                                             const float* __restrict__ gamma, int OH, int OW, int HP,
@@ -120,8 +120,11 @@ __global__ __launch_bounds__(256, 2) void stem_fused_kernel(const float* __restr
   const int py0 = band * ST_PB, py1 = min(HP, py0 + ST_PB);
   const int c_lo = max(2 * py0 - 1, 0), c_hi = min(2 * py1 - 1, OH - 1), n = c_hi - c_lo + 1;
   const int rows = 2 * n + 6;
-  float* hrow = reinterpret_cast<float*>(smb);  // [n][WP][32] horizontally pooled rows
-  __bf16* xs = smb + 2 * (2 * ST_PB + 1) * WP * C;
+  // [ST_PB][WP][32] pooled rows: each conv row's horizontal window maxima are folded in with LDS max atomics
+  // (exact and order-independent), conv row 2py+1 into pooled rows py and py+1
+  float* hpool = reinterpret_cast<float*>(smb);
+  __bf16* xs = smb + 2 * ST_PB * WP * C;
+  for (int q = threadIdx.x; q < ST_PB * WP * C; q += blockDim.x) hpool[q] = -INFINITY;
   bf16x8s b[4][3];
   stem_weights(w, b);
   {
@@ -161,44 +164,51 @@ __global__ __launch_bounds__(256, 2) void stem_fused_kernel(const float* __restr
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][1], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][0], acc, 0, 0, 0);
     }
-    // D row i (pixel = column c0 - 1 + i) of register r in lane half h: i = (r & 3) + 8 (r >> 2) + 4 h
-    const bool own_row = crow >= 2 * py0;
-    float v[16], o[16];
+    // D row i (pixel = column c0 - 1 + i) of register r in lane half h: i = (r & 3) + 8 (r >> 2) + 4 h.  Valid
+    // columns are i <= ihi (and i >= 1 on the first tile); this tile's own columns for the BN sums are i = 1 .. 30
+    const int ihi = min(30, OW - c0), ilo = c0 == 0 ? 1 : 0;
+    const float own = crow >= 2 * py0 ? 1.f : 0.f, sgn = neg ? -1.f : 1.f;
+    float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int i = (r & 3) + 8 * (r >> 2) + 4 * h, c = c0 - 1 + i;
+      const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
       const float y = acc[r] + bj;
-      const bool ok = c >= 0 && c < OW;
-      if (ok && own_row && i >= 1 && i <= 30) {  // column c0-1 / c0+30 belong to the neighbouring tiles
-        s1 += y;
-        s2 = fmaf(y, y, s2);
-      }
-      v[r] = ok ? (neg ? -y : y) : -INFINITY;
+      const float m = (i >= 1 && i <= ihi) ? own : 0.f;
+      s1 = fmaf(y, m, s1);
+      s2 = fmaf(y * y, m, s2);
+      v[r] = (i >= ilo && i <= ihi) ? y * sgn : -INFINITY;  // pooled as a max of y (gamma >= 0) or of -y
     }
+    // v_permlane32_swap of (v[r], v[r+8]): lane half 0 gets pixels 0..15 in X/Y (its windows 0..7 also need pixel
+    // 16 = its own v[8], kept aside), lane half 1 pixels 16..31 -- the same registers for local pixel 16h + l:
+    // l -> ((l >> 2) & 1 ? Y : X)[(l & 3) + 4 (l >> 3)], so both halves run one window code path
+    const float p16 = v[8];
+    float X[8], Y[8];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o[r] = __shfl_xor(v[r], 32, 64);
-    // value of pixel i: lane half (i >> 2) & 1 holds it in register (i & 3) + 4 (i >> 3)
-    auto val = [&](int i) { return (((i >> 2) & 1) == h) ? v[(i & 3) + 4 * (i >> 3)] : o[(i & 3) + 4 * (i >> 3)]; };
+    for (int r = 0; r < 8; ++r) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[r]), __float_as_uint(v[r + 8]), false, false);
+      X[r] = __uint_as_float(sw[0]);
+      Y[r] = __uint_as_float(sw[1]);
+    }
+    auto loc = [&](int l) { return l == 16 ? p16 : (((l >> 2) & 1) ? Y : X)[(l & 3) + 4 * (l >> 3)]; };
+    const int pxb = 15 * (c0 / 30) + 8 * h;  // window k of this half = pooled column pxb + k
+    const int pa = crow >> 1, pb = (crow + 1) >> 1;  // the pooled rows this conv row belongs to (equal if even)
+    float* ha = hpool + ((pa - py0) * WP + pxb) * C + j;
+    float* hb = hpool + ((pb - py0) * WP + pxb) * C + j;
+    const bool wa = pa >= py0, wb = pb != pa && pb < py1;
 #pragma unroll
-    for (int k = 0; k < 15; ++k) {
-      const float m = fmaxf(fmaxf(val(2 * k), val(2 * k + 1)), val(2 * k + 2));
-      const int px = 15 * (c0 / 30) + k;
-      if ((h == 0 ? k < 8 : k >= 8) && px < WP) hrow[(rl * WP + px) * C + j] = m;
+    for (int k = 0; k < 8; ++k) {
+      const float m = fmaxf(fmaxf(loc(2 * k), loc(2 * k + 1)), loc(2 * k + 2));
+      if (k < 8 - h && pxb + k < WP) {
+        if (wa) __hip_atomic_fetch_max(ha + k * C, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (wb) __hip_atomic_fetch_max(hb + k * C, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
   }
   __syncthreads();
   for (int q = threadIdx.x; q < (py1 - py0) * WP * (C / 4); q += blockDim.x) {
     const int pyl = q / (WP * (C / 4)), rem = q - pyl * (WP * (C / 4));
     const int px = rem / (C / 4), c = (rem % (C / 4)) * 4, py = py0 + pyl;
-    f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy) {
-      const int cr = 2 * py + dy;
-      if (cr < 0 || cr >= OH) continue;
-      const f32x4 u = *reinterpret_cast<const f32x4*>(hrow + ((cr - c_lo) * WP + px) * C + c);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], u[e]);
-    }
+    f32x4 m = *reinterpret_cast<const f32x4*>(hpool + (pyl * WP + px) * C + c);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (gamma[c + e] < 0.f) m[e] = -m[e];
@@ -207,7 +217,7 @@ __global__ __launch_bounds__(256, 2) void stem_fused_kernel(const float* __restr
   s1 += __shfl_xor(s1, 32, 64);
   s2 += __shfl_xor(s2, 32, 64);
   __syncthreads();
-  float* red = hrow;  // [4 waves][2][32]
+  float* red = hpool;  // [4 waves][2][32]
   if (lane < 32) {
     red[wave * 64 + lane] = s1;
     red[wave * 64 + 32 + lane] = s2;
@@ -226,7 +236,7 @@ int g_stem_fused = 1;  // tuning knob "stem_fused": the frozen stem's forward wi
 static int stem_pitch(int OW) { return (int)cdiv(2 * OW + 6, 8) * 8; }
 static size_t stem_lds(int OW) {
   const int WP = (OW - 1) / 2 + 1;
-  return (size_t)(2 * ST_PB + 1) * WP * 32 * sizeof(float) +
+  return (size_t)ST_PB * WP * 32 * sizeof(float) +
          (size_t)3 * (2 * (2 * ST_PB + 1) + 6) * stem_pitch(OW) * sizeof(__bf16);
 }
 
