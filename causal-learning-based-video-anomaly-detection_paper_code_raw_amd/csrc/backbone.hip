@@ -923,6 +923,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_split_s2") g_wgrad_split_s2 = value;
   else if (k == "conv_wgrad_s2_blocks") g_wgrad_s2_blocks = value;
   else if (k == "stem_fused") g_stem_fused = value;
+  else if (k == "stem_dbg") g_stem_dbg = value;
   else if (k == "conv_wgrad_s1_nt") g_wgrad_s1_nt = value;
   else if (k == "conv_wgrad_s1_nt_wide") g_wgrad_s1_nt_wide = value;
   else if (k == "conv_wgrad_s1_nt_blocks") g_wgrad_s1_nt_blocks = value;

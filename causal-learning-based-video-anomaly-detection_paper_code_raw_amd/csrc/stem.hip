@@ -68,20 +68,26 @@ __device__ __forceinline__ void stem_fetch(const float* __restrict__ xi, int H, 
                                            R& r) {
   constexpr int ST_ITEMS = R::items;
   const int half = PWb / 2;
+  // q / half by a float reciprocal: q + 0.5 sits >= 0.5 / half away from a multiple of half, far above the
+  // rounding error of q * (1 / half) for q < 2^12
+  const float inv = 1.f / (float)half;
+  // branch-free: clamped (always in-bounds) addresses, out-of-frame taps zeroed by a select, so all loads issue
+  // back to back
 #pragma unroll
   for (int k = 0; k < ST_ITEMS; ++k) {
     const int q = threadIdx.x + k * 256;
-    const int pr = q / half, m = q - pr * half;
+    const int pr = (int)(((float)q + 0.5f) * inv), m = q - pr * half;
     const int ih = 2 * c0 - 3 + pr, iw = 2 * m - 3;
-    r.v[k][0] = r.v[k][1] = 0.f;
-    if (pr < rows && ih >= 0 && ih < H) {
-      if (iw >= 0 && iw < W) r.v[k][0] = xi[(int64_t)ih * W + iw];
-      if (iw + 1 >= 0 && iw + 1 < W) r.v[k][1] = xi[(int64_t)ih * W + iw + 1];
-    }
+    const bool rok = pr < rows && ih >= 0 && ih < H;
+    const int64_t rowo = (int64_t)min(max(ih, 0), H - 1) * W;
+    const float a0 = xi[rowo + min(max(iw, 0), W - 1)];
+    const float a1 = xi[rowo + min(max(iw + 1, 0), W - 1)];
+    r.v[k][0] = (rok && iw >= 0 && iw < W) ? a0 : 0.f;
+    r.v[k][1] = (rok && iw + 1 >= 0 && iw + 1 < W) ? a1 : 0.f;
   }
 }
 
-template <class R>
+template <int NP, class R>
 __device__ __forceinline__ void stem_store(const R& r, int rows, int PWb, __bf16* xs) {
   constexpr int ST_ITEMS = R::items;
   typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -96,8 +102,10 @@ __device__ __forceinline__ void stem_store(const R& r, int rows, int PWb, __bf16
       split3s(r.v[k][1], h1, m1, l1);
       const bf16x2 hi = {h0, h1}, mid = {m0, m1}, lo = {l0, l1};
       d[q] = hi;  // q = pr * half + m
-      d[q + plane2] = mid;
-      d[q + 2 * plane2] = lo;
+      if constexpr (NP == 3) {
+        d[q + plane2] = mid;
+        d[q + 2 * plane2] = lo;
+      }
     }
   }
 }
@@ -108,12 +116,14 @@ __device__ __forceinline__ void stem_store(const R& r, int rows, int PWb, __bf16
 constexpr int ST_PB = 3;
 constexpr int ST_SLOTS = 12;  // input staging register slots: (2 * (2 * ST_PB + 1) + 6) rows * PWb / 2 <= 12 * 256
 
+// NP = 3: split-bf16 operands (fp32 numerics, the default); NP = 1: bf16 operands (conv_bf16, BASELINE config 4)
+template <int NP>
 __global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restrict__ x, int H, int W,
                                                             const float* __restrict__ w,
                                                             const float* __restrict__ bias,
                                                             const float* __restrict__ gamma, int OH, int OW, int HP,
                                                             int WP, int nbands, int PWb, float* __restrict__ pool,
-                                                            float* __restrict__ partials) {
+                                                            float* __restrict__ partials, int dbg) {
   extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
   constexpr int C = 32;
   const int img = blockIdx.x / nbands, band = blockIdx.x % nbands;
@@ -129,8 +139,10 @@ __global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restr
   stem_weights(w, b);
   {
     StemRegs<ST_SLOTS> sr;
-    stem_fetch(x + (int64_t)img * H * W, H, W, c_lo, rows, PWb, sr);
-    stem_store(sr, rows, PWb, xs);
+    if (!(dbg & 2)) stem_fetch(x + (int64_t)img * H * W, H, W, c_lo, rows, PWb, sr);
+    else
+      for (int k = 0; k < ST_SLOTS; ++k) sr.v[k][0] = sr.v[k][1] = 0.f;
+    stem_store<NP>(sr, rows, PWb, xs);
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
   const float bj = bias[j];
@@ -148,20 +160,22 @@ __global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restr
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     const int plane2 = rows * PWb / 2;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    for (int ks = 0; ks < ((dbg & 1) ? 0 : 4); ++ks) {
       const unsigned* rowp = reinterpret_cast<const unsigned*>(xs + (2 * rl + 2 * ks + h) * PWb) + colc;
-      bf16x8s a[3];
+      bf16x8s a[NP];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < NP; ++q) {
         const unsigned* sp = rowp + q * plane2;
         const u32x4s d = {sp[0], sp[1], sp[2], sp[3]};
         a[q] = __builtin_bit_cast(bf16x8s, d);
       }
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[ks][0], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[ks][1], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][2], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[ks][0], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][1], acc, 0, 0, 0);
+      if constexpr (NP == 3) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[ks][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[ks][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[ks][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][1], acc, 0, 0, 0);
+      }
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][0], acc, 0, 0, 0);
     }
     // D row i (pixel = column c0 - 1 + i) of register r in lane half h: i = (r & 3) + 8 (r >> 2) + 4 h.  Valid
@@ -198,21 +212,26 @@ __global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restr
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float m = fmaxf(fmaxf(loc(2 * k), loc(2 * k + 1)), loc(2 * k + 2));
-      if (k < 8 - h && pxb + k < WP) {
+      if (k < 8 - h && pxb + k < WP && !(dbg & 4)) {
         if (wa) __hip_atomic_fetch_max(ha + k * C, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (wb) __hip_atomic_fetch_max(hb + k * C, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < (py1 - py0) * WP * (C / 4); q += blockDim.x) {
-    const int pyl = q / (WP * (C / 4)), rem = q - pyl * (WP * (C / 4));
-    const int px = rem / (C / 4), c = (rem % (C / 4)) * 4, py = py0 + pyl;
-    f32x4 m = *reinterpret_cast<const f32x4*>(hpool + (pyl * WP + px) * C + c);
+  {
+    // pooled row py is contiguous in both hpool and the output: float4 q of the row is channel group (q & 7),
+    // fixed per thread (256 % 8 == 0)
+    const int c = (threadIdx.x & 7) * 4;
+    f32x4 sg;
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (gamma[c + e] < 0.f) m[e] = -m[e];
-    *reinterpret_cast<f32x4*>(pool + (((int64_t)img * HP + py) * WP + px) * C + c) = m;
+    for (int e = 0; e < 4; ++e) sg[e] = gamma[c + e] < 0.f ? -1.f : 1.f;
+    for (int pyl = 0; pyl < py1 - py0; ++pyl) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(hpool + pyl * WP * C);
+      f32x4* dst = reinterpret_cast<f32x4*>(pool + ((int64_t)img * HP + py0 + pyl) * WP * C);
+      if (!(dbg & 8))
+        for (int q = threadIdx.x; q < WP * (C / 4); q += blockDim.x) dst[q] = src[q] * sg;
+    }
   }
   s1 += __shfl_xor(s1, 32, 64);
   s2 += __shfl_xor(s2, 32, 64);
@@ -232,6 +251,9 @@ __global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restr
 }  // namespace
 
 int g_stem_fused = 1;  // tuning knob "stem_fused": the frozen stem's forward without the conv1 activation
+// knob "stem_dbg" (measurement only, results wrong with any bit): 1 no MFMA, 2 no input loads, 4 no window
+// atomics, 8 no pooled-map stores
+int g_stem_dbg = 0;
 
 static int stem_pitch(int OW) { return (int)cdiv(2 * OW + 6, 8) * 8; }
 static size_t stem_lds(int OW) {
@@ -252,8 +274,12 @@ int stem_fused(const float* x, int NF, int H, int W, const float* w, const float
   const int nbands = (int)cdiv(HP, ST_PB);
   // (the partial rows fit the conv1_fwd layout: ceil(ceil(OH/2)/3) == ceil(OH/6))
   VAD_CHECK(nbands == (int)cdiv(OH, 6) && (int64_t)NF * nbands == conv1_num_parts(NF, OH), "stem_fused: partials");
-  VAD_KLAUNCH(stem_fused_kernel, dim3(NF * nbands), dim3(256), stem_lds(OW), st, x, H, W, w, b, gamma, OH, OW, HP,
-              WP, nbands, stem_pitch(OW), pool, partials);
+  if (g_conv_bf16)
+    VAD_KLAUNCH(stem_fused_kernel<1>, dim3(NF * nbands), dim3(256), stem_lds(OW), st, x, H, W, w, b, gamma, OH, OW,
+                HP, WP, nbands, stem_pitch(OW), pool, partials, g_stem_dbg);
+  else
+    VAD_KLAUNCH(stem_fused_kernel<3>, dim3(NF * nbands), dim3(256), stem_lds(OW), st, x, H, W, w, b, gamma, OH, OW,
+                HP, WP, nbands, stem_pitch(OW), pool, partials, g_stem_dbg);
   VAD_LAUNCH_CHECK();
   *nparts = NF * nbands;
   return 0;

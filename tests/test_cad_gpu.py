@@ -287,7 +287,7 @@ def test_fused_stem_matches_float64_stem(B, T, H, W):
 def test_config4_shape_fp32_and_bf16(B, T, H, W):
     """BASELINE config 4 shape (T=32, 256x256; 2 clips per rank here to bound the oracle's CPU time).
     fp32 mode: scores / loss within the north-star 1e-4 of the CPU oracle.  bf16 mode (conv_bf16: the 3x3 convs
-    on bf16 operands, fp32 accumulation, everything else fp32): the outputs move by bf16 rounding of the conv
+    and the frozen stem's conv1 on bf16 operands, fp32 accumulation, everything else fp32): the outputs move by bf16 rounding of the conv
     operands only -- scores and probabilities (bounded in [0, 1]) within 2e-2 absolute, the total loss within 2e-2
     relative, the global gradient norm within 5 % (tolerance stated for bf16 compute: unit roundoff 2^-8)."""
     case = dict(name="cfg4", B=B, T=T, H=H, W=W, seed=9, step=1, forced=None)
