@@ -34,7 +34,7 @@ def main():
         if "SQ_VALU_MFMA_BUSY_CYCLES" not in c or "GRBM_GUI_ACTIVE" not in c:
             continue
         n = names[d]
-        f = family(n) or ("conv1" if "conv1_kernel" in n else None)
+        f = family(n) or ("conv1" if ("conv1_kernel" in n or "stem_fused_kernel" in n) else None)
         k = kern[n.split("(")[0][:120]]
         k["launches"] += 1
         k["busy"] += c["SQ_VALU_MFMA_BUSY_CYCLES"]
