@@ -12,6 +12,8 @@ int conv1_num_parts(int NF, int OH);
 // frozen-stem forward without the conv1 activation (stem.hip): conv1 + bias, its BN partial sums ([P][64], the
 // conv1_fwd layout and P) and the 3x3/s2 pooling of the RAW output (max where gamma >= 0, min where gamma < 0);
 // the consumer applies bn1+ReLU on load (exact: the affine+ReLU is monotone per channel)
+extern int g_x3_stagger;  // knob "conv_split_stagger"
+extern int g_cad_prep_stream, g_cad_wgrad_stream;  // knobs "cad_prep_stream", "cad_wgrad_stream" (A/B)
 extern int g_stem_fused, g_stem_dbg;  // knobs "stem_fused" (default 1), "stem_dbg" (measurement only)
 bool stem_fused_ok(int OW);  // conv1 output width the fused stem handles
 int stem_fused(const float* x, int NF, int H, int W, const float* w, const float* b, const float* gamma, int OH,

@@ -7,6 +7,9 @@
 
 namespace vad {
 
+int g_cad_prep_stream = 1;   // knob "cad_prep_stream": weight relayouts on the plan's side stream (A/B measurement)
+int g_cad_wgrad_stream = 1;  // knob "cad_wgrad_stream": backbone weight gradients on their own stream
+
 // =====================================================================================================
 // conv1: 1 -> 32 channels, 7x7, stride 2, pad 3, as a K=49 (padded to 56) GEMM on f32 MFMA.
 // One block = one frame x a band of C1_RB output rows.  The zero-padded input band is staged in LDS; each wave
@@ -923,6 +926,9 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_split_s2") g_wgrad_split_s2 = value;
   else if (k == "conv_wgrad_s2_blocks") g_wgrad_s2_blocks = value;
   else if (k == "stem_fused") g_stem_fused = value;
+  else if (k == "conv_split_stagger") g_x3_stagger = value;
+  else if (k == "cad_prep_stream") g_cad_prep_stream = value;
+  else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "stem_dbg") g_stem_dbg = value;
   else if (k == "conv_wgrad_s1_nt") g_wgrad_s1_nt = value;
   else if (k == "conv_wgrad_s1_nt_wide") g_wgrad_s1_nt_wide = value;

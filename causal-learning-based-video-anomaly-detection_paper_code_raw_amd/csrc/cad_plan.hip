@@ -329,7 +329,7 @@ struct CadPlanImpl {
   int *counts, *nmax, *clip_flags, *flags;
   float *d_causal, *d_kl, *d_glog, *d_dlog, *slabs, *d_feat_det, *d_pooled, *dense_scratch, *dense_scratch2;
   float *dg[5], *ddh[5];
-  float *dA, *dY, *wpart, *stem_d;  // stem_d: [NF][H1][W1][32], the stem backward's dA / dY (stem_grad only)
+  float *dA, *dY, *dY2, *wpart, *stem_d;  // stem_d: [NF][H1][W1][32], the stem backward's dA / dY (stem_grad only)
   float *sq_parts, *slot_info, *clip;
   int16_t* chunk_slot;
   int64_t parts_floats, dense_scratch_floats, wpart_floats, slab_len, act_max;
@@ -350,13 +350,31 @@ struct CadPlanImpl {
   // and at the backbone backward (fork / join through events on the caller's stream)
   hipStream_t st2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_det = nullptr;
-  int fork(hipStream_t st) {
+  // weight-gradient stream: in the backbone backward, layer l's weight gradient (+ split-K reduce) runs here
+  // concurrently with its input gradient and the next layer's BN backward on the caller's stream.  dY alternates
+  // between two buffers: ev_dy[b] = "dYb[b] written" (caller's stream), ev_wg[b] = "the weight gradient reading
+  // dYb[b] is done" (st3)
+  hipStream_t st3 = nullptr;
+  hipEvent_t ev_dy[2] = {nullptr, nullptr}, ev_wg[2] = {nullptr, nullptr}, ev_wgj = nullptr, ev_prep = nullptr;
+  int wgrad_stream = 1;  // option "wgrad_stream" (0: weight gradients on the caller's stream)
+  int streams() {
     if (!st2) {
       VAD_HIP(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
       VAD_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
       VAD_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
       VAD_HIP(hipEventCreateWithFlags(&ev_det, hipEventDisableTiming));
+      VAD_HIP(hipStreamCreateWithFlags(&st3, hipStreamNonBlocking));
+      for (int b = 0; b < 2; ++b) {
+        VAD_HIP(hipEventCreateWithFlags(&ev_dy[b], hipEventDisableTiming));
+        VAD_HIP(hipEventCreateWithFlags(&ev_wg[b], hipEventDisableTiming));
+      }
+      VAD_HIP(hipEventCreateWithFlags(&ev_wgj, hipEventDisableTiming));
+      VAD_HIP(hipEventCreateWithFlags(&ev_prep, hipEventDisableTiming));
     }
+    return 0;
+  }
+  int fork(hipStream_t st) {
+    VAD_TRY(streams());
     VAD_HIP(hipEventRecord(ev_fork, st));
     VAD_HIP(hipStreamWaitEvent(st2, ev_fork, 0));
     return 0;
@@ -370,6 +388,13 @@ struct CadPlanImpl {
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     if (ev_det) (void)hipEventDestroy(ev_det);
+    for (int b = 0; b < 2; ++b) {
+      if (ev_dy[b]) (void)hipEventDestroy(ev_dy[b]);
+      if (ev_wg[b]) (void)hipEventDestroy(ev_wg[b]);
+    }
+    if (ev_wgj) (void)hipEventDestroy(ev_wgj);
+    if (ev_prep) (void)hipEventDestroy(ev_prep);
+    if (st3) (void)hipStreamDestroy(st3);
     if (st2) (void)hipStreamDestroy(st2);
   }
   char lbl[64];
@@ -444,6 +469,7 @@ struct CadPlanImpl {
     dense_scratch2 = w.take<float>(dense_scratch_floats);  // the side stream's (detector) split-K scratch
     dA = w.take<float>(act_max);
     dY = w.take<float>(act_max);
+    dY2 = w.take<float>(act_max);
     stem_d = w.take<float>(nf * H1 * W1 * 32);
     wpart_floats = 16ll << 20;
     wpart = w.take<float>(wpart_floats);
@@ -610,13 +636,19 @@ struct CadPlanImpl {
   const float* x_last = nullptr;  // the last forward's input (the stem backward's conv1 weight gradient reads it)
 
   int forward(const float* x, hipStream_t st) {
+    const hipStream_t st0 = st;
     ConvPrecision prec(conv_bf16);
     x_last = x;
     const CadLayout& LY = layout();
+    // weight relayouts (conv images, the detector's transposed layers) on the side stream, beside the stem
+    VAD_TRY(fork(st));
     {
+      hipStream_t st = g_cad_prep_stream ? st2 : st0;
       const float* w8[8];
       for (int l = 0; l < 8; ++l) w8[l] = P(LY.conv_w[l]);
       TIMED("prep", conv3_prep_weights_all(8, w8, L, wf, wd, st));
+      TIMED("prep", mlp_transpose(mlp_transpose_args(), st));
+      VAD_HIP(hipEventRecord(ev_prep, st));
     }
     int np = 0;
     bwd_state = 0;
@@ -635,6 +667,7 @@ struct CadPlanImpl {
       TIMED("maxpool", maxpool3s2_bnrelu(y1, stats[0], NF, H1, W1, 32, pool, HP, WP, st));
       pool_stats = nullptr;
     }
+    VAD_HIP(hipStreamWaitEvent(st, ev_prep, 0));  // layer1.0 reads the prepared weight images
     const float* src = pool;
     const float* sst = pool_stats;
     for (int l = 0; l < 8; ++l) {
@@ -652,7 +685,6 @@ struct CadPlanImpl {
     VAD_TRY(fork(st));
     {  // side stream: detector_net (cad:167-179; layer 0 as a split-K GEMM, layers 1-4 fused per row block)
       hipStream_t st = st2;
-      TIMED("prep", mlp_transpose(mlp_transpose_args(), st));
       TIMED("det_fwd", dense_fwd(feats, NF, 6144, P(LY.det_w[0]), P(LY.det_b[0]), 512, dh[0],
                                  act(true, S_DET_DROP1, 0.3, f0), dense_scratch2, dense_scratch_floats, st));
       TIMED("det_fwd", mlp_tail_fwd(mlp_args(NF, f0, dd, LY.det_w, LY.det_b, dh, dlog, S_DET_DROP2, wt), st));
@@ -771,19 +803,39 @@ struct CadPlanImpl {
     // backbone (BatchNorm backward as streaming passes: the conv kernels are MFMA/LDS-bound and slowed down more by
     // extra loads than the separate 6 TB/s passes cost -- DESIGN.md §6, BN-backward fusion experiment)
     TIMED("avgpool_bwd", avgpool_bwd(d_feat_det, d_pooled, B, T, HF, WF, 256, dA, st));
+    VAD_TRY(streams());
+    const bool wgs = wgrad_stream != 0 && g_cad_wgrad_stream;
     for (int l = 7; l >= 0; --l) {
       const int64_t M = (int64_t)NF * L[l].OH * L[l].OW;
       const int C = L[l].Co;
-      int np = 0, nb = 0, ns = 0;
+      int np = 0, nb = 0;
+      float* dYl = (l & 1) ? dY2 : dY;
       TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st));
       VAD_TRY(bn_bwd_stats(l + 1, np, C, (double)M, P(LY.bn_w[l]), G(LY.bn_w[l]), G(LY.bn_b[l]), G(LY.conv_b[l]), st));
-      TIMED(L_("bn_bwd_apply", l), bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dY, nullptr, &nb, st));
+      // dYl was last read by layer l+2's weight gradient
+      if (wgs && l + 2 <= 7) VAD_HIP(hipStreamWaitEvent(st, ev_wg[l & 1], 0));
+      TIMED(L_("bn_bwd_apply", l), bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dYl, nullptr, &nb, st));
       const float* src = l == 0 ? pool : y[l - 1];
       const float* sst = l == 0 ? pool_stats : stats[l];
-      TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dY, src, sst, wpart, &ns, wpart_floats, st));
-      TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], wpart, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
-      if (l > 0) TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dY, wd[l], dA, st));
+      {
+        hipStream_t wst = st;
+        if (wgs) {
+          VAD_HIP(hipEventRecord(ev_dy[l & 1], st));
+          VAD_HIP(hipStreamWaitEvent(st3, ev_dy[l & 1], 0));
+          wst = st3;
+        }
+        hipStream_t st = wst;
+        int ns = 0;
+        TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dYl, src, sst, wpart, &ns, wpart_floats, st));
+        TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], wpart, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
+        if (wgs) VAD_HIP(hipEventRecord(ev_wg[l & 1], st));
+      }
+      if (l > 0) TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st));
       if (l == debug_stop_layer) break;
+    }
+    if (wgs) {  // every weight gradient is final before the stem backward / optimizer on the caller's stream
+      VAD_HIP(hipEventRecord(ev_wgj, st3));
+      VAD_HIP(hipStreamWaitEvent(st, ev_wgj, 0));
     }
     stem_active = 0;
     if (stem_grad && debug_stop_layer < 0) {
@@ -1052,7 +1104,7 @@ int vad_cad_debug_buffer(vad_cad_plan* plan, const char* name, int idx, void** p
   else if (n == "feats") { *ptr = c.feats; *nfloats = NF * 6144; }
   else if (n == "pooled") { *ptr = c.pooled; *nfloats = (int64_t)c.B * 6144; }
   else if (n == "dA") { *ptr = c.dA; *nfloats = c.act_max; }
-  else if (n == "dY") { *ptr = c.dY; *nfloats = c.act_max; }
+  else if (n == "dY") { *ptr = (c.debug_stop_layer & 1) ? c.dY2 : c.dY; *nfloats = c.act_max; }
   else if (n == "d_pooled") { *ptr = c.d_pooled; *nfloats = (int64_t)c.B * 6144; }
   else if (n == "d_feat_det") { *ptr = c.d_feat_det; *nfloats = NF * 6144; }
   else if (n == "det_logits") { *ptr = c.dlog; *nfloats = NF * 20; }
@@ -1072,6 +1124,7 @@ int vad_cad_set_option(vad_cad_plan* plan, const char* key, int64_t value) {
   VAD_CHECK(plan && key, "vad_cad_set_option: null argument");
   if (std::string(key) == "conv_bf16") plan->impl.conv_bf16 = value ? 1 : 0;
   else if (std::string(key) == "stem_grad") plan->impl.stem_grad = value ? 1 : 0;
+  else if (std::string(key) == "wgrad_stream") plan->impl.wgrad_stream = value ? 1 : 0;
   else { vad::set_error("vad_cad_set_option: unknown key"); return 1; }
   return 0;
 }

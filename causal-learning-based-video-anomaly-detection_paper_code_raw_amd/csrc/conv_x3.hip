@@ -35,6 +35,8 @@ struct X3Args {
   int tiles_h, tiles_w, ntiles, tpb;
   int dbg;  // measurement only (knob "conv_split_dbg"): 1 no weight restaging, 2 no patch split, 4 no MFMA,
             // 8 no patch loads -- results are wrong with any bit set
+  int stagger;  // knob "conv_split_stagger": odd blocks start this many x 1024 cycles late (phase offset of the two
+                // co-resident blocks of a CU)
 };
 
 __device__ __forceinline__ void split3(const float* v, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
@@ -113,6 +115,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
   constexpr int WQ = NC * 9 * G8, WIT = (WQ + 255) / 256;
   const int g8 = tid % G8;
   f32x4 pv[PIT][2], wv[WIT][2];
+  // prefetch loads are unconditional (out-of-range lanes read a valid dummy address) and the zero padding is applied
+  // at stash time from these bits, so no masked-load branch makes the compiler wait for the loads before the MFMAs
+  bool pok[PIT], wok[WIT];
   auto origin = [&](int tile, int& img0, int& oy0, int& ox0) {
     img0 = (tile / tiles_per_img) * NI;
     const int tr = tile % tiles_per_img;
@@ -128,37 +133,40 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
       const int row = q / G8;
       const int im = row / (PH * PW), rr = row % (PH * PW);
       const int iy = oy0 * S - 1 + rr / PW, ix = ox0 * S - 1 + rr % PW, img = img0 + im;
-      pv[it][0] = pv[it][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (!(p.dbg & 8) && q < PQ && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW) {
-        const float* s = p.src + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C + c0 + g8 * 8;
-        pv[it][0] = *reinterpret_cast<const f32x4*>(s);
-        pv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
-      }
+      pok[it] = !(p.dbg & 8) && q < PQ && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
+      const float* s = p.src + c0 + g8 * 8 +
+                       (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
+      pv[it][0] = *reinterpret_cast<const f32x4*>(s);
+      pv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
     }
     if (weights) {
 #pragma unroll
       for (int it = 0; it < WIT; ++it) {
         const int q = tid + it * 256;
         const int n = q / (9 * G8), t = (q / G8) % 9;
-        wv[it][0] = wv[it][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (q < WQ && n0 + n < p.N) {
-          const float* s = p.w + ((int64_t)(n0 + n) * 9 + (FWD ? t : 8 - t)) * p.C + c0 + g8 * 8;
-          wv[it][0] = *reinterpret_cast<const f32x4*>(s);
-          wv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
-        }
+        wok[it] = q < WQ && n0 + n < p.N;
+        const float* s = p.w + c0 + g8 * 8 +
+                         (wok[it] ? ((int64_t)(n0 + n) * 9 + (FWD ? t : 8 - t)) * p.C : (int64_t)0);
+        wv[it][0] = *reinterpret_cast<const f32x4*>(s);
+        wv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
       }
     }
   };
   auto stash = [&](int tile, int c0, bool weights) {
     int img0, oy0, ox0;
     origin(tile, img0, oy0, ox0);
+    // (BN constants loaded and used unconditionally -- from a dummy address when there is no BN -- so no load is
+    // left pending on a branch the waitcnt analysis would have to assume, which made it drain the prefetch loads
+    // before the first MFMA)
     const bool bn = FWD && p.scale;
-    f32x4 sc[2] = {{1.f, 1.f, 1.f, 1.f}, {1.f, 1.f, 1.f, 1.f}}, sh[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    if (bn) {
-      sc[0] = *reinterpret_cast<const f32x4*>(p.scale + c0 + g8 * 8);
-      sc[1] = *reinterpret_cast<const f32x4*>(p.scale + c0 + g8 * 8 + 4);
-      sh[0] = *reinterpret_cast<const f32x4*>(p.shift + c0 + g8 * 8);
-      sh[1] = *reinterpret_cast<const f32x4*>(p.shift + c0 + g8 * 8 + 4);
+    f32x4 sc[2], sh[2];
+    if constexpr (FWD) {
+      const float* scp = bn ? p.scale : p.w;
+      const float* shp = bn ? p.shift : p.w;
+      sc[0] = *reinterpret_cast<const f32x4*>(scp + c0 + g8 * 8);
+      sc[1] = *reinterpret_cast<const f32x4*>(scp + c0 + g8 * 8 + 4);
+      sh[0] = *reinterpret_cast<const f32x4*>(shp + c0 + g8 * 8);
+      sh[1] = *reinterpret_cast<const f32x4*>(shp + c0 + g8 * 8 + 4);
     }
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
@@ -170,18 +178,18 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
         float v[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = pv[it][0][e];
-          v[4 + e] = pv[it][1][e];
+          v[e] = pok[it] ? pv[it][0][e] : 0.f;
+          v[4 + e] = pok[it] ? pv[it][1][e] : 0.f;
         }
-        if (bn) {
+        if constexpr (FWD) {
           // zero padding stays zero: padded taps read 0 in the reference's zero-padded relu(bn(y))
-          const int iy = oy0 * S - 1 + ry, ix = ox0 * S - 1 + rx;
-          if (img0 + im < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW) {
+          const bool app = bn && pok[it];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              v[e] = relu_nan(fmaf(v[e], sc[0][e], sh[0][e]));
-              v[4 + e] = relu_nan(fmaf(v[4 + e], sc[1][e], sh[1][e]));
-            }
+          for (int e = 0; e < 4; ++e) {
+            const float a0 = relu_nan(fmaf(v[e], sc[0][e], sh[0][e]));
+            const float a1 = relu_nan(fmaf(v[4 + e], sc[1][e], sh[1][e]));
+            v[e] = app ? a0 : v[e];
+            v[4 + e] = app ? a1 : v[4 + e];
           }
         }
         const int col = S == 1 ? rx : ((rx & 1) ? PWE + (rx >> 1) : (rx >> 1));
@@ -198,13 +206,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
           float v[8];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            v[e] = wv[it][0][e];
-            v[4 + e] = wv[it][1][e];
+            v[e] = wok[it] ? wv[it][0][e] : 0.f;
+            v[4 + e] = wok[it] ? wv[it][1][e] : 0.f;
           }
           put_planes<NP>(wl + n * WP + (WCH > 1 ? (c0 / PC) * WCS : 0) + t * NP * PC + g8 * 8, PC, v, false);
         }
       }
     }
+    // every load the stash consumed is complete here (vmcnt(0); the next prefetch is issued after the barrier),
+    // so the waitcnt analysis does not carry them, pending on some branch, into the MFMA loop and drain the
+    // prefetch there
+    __builtin_amdgcn_s_waitcnt(0x0F70);
   };
 
   float bj[NT], s1[NT], s2[NT];
@@ -217,6 +229,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
   f32x16 acc[NT];
   const int nitems = (t1 - t0) * nch;
   if (nitems > 0) fetch(t0, 0, true);
+  if (blockIdx.x & 1)
+    for (int k = 0; k < p.stagger; ++k) __builtin_amdgcn_s_sleep(16);
   for (int item = 0; item < nitems; ++item) {
     const int tile = t0 + item / nch, ch = item % nch, c0 = ch * PC;
     const bool wnow = WCH > 1 ? item < nch : ((nch > 1 && !(p.dbg & 1)) || item == 0);
@@ -314,6 +328,7 @@ static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   const int target = std::max(1, std::min(max_blocks, 512 / ny));  // 2 resident blocks per CU over 256 CUs
   a.tpb = (int)cdiv(a.ntiles, target);
   a.dbg = g_x3_dbg;
+  a.stagger = g_x3_stagger;
   const int gx = (int)cdiv(a.ntiles, a.tpb);
   VAD_KLAUNCH((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD, NP, WCH>), dim3(gx, ny), dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
@@ -325,6 +340,7 @@ int g_conv_split = 1;  // tuning knob "conv_split": 1 = split-bf16 patch kernels
 thread_local int g_conv_bf16 = 0;  // bf16-operand convs (one plane, one product; set per plan, see ConvPrecision)
 int g_x3_nt = 0;       // tuning knob "conv_split_nt": 0 = auto, 1 / 2 = force 32 / 64 output channels per block
 int g_x3_dbg = 0;      // knob "conv_split_dbg" (measurement only, see X3Args::dbg)
+int g_x3_stagger = 0;  // knob "conv_split_stagger" (see X3Args::stagger)
 
 int g_x3_wres = 1;  // knob "conv_split_wres": 32-channel stride-1 layers keep all split weights resident in LDS
 

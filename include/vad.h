@@ -275,7 +275,9 @@ int vad_resize_u8(const uint8_t* src, int sh, int sw, uint8_t* dst, int dh, int 
 
 /* Plan options.  "conv_bf16" (0/1): the 3x3 convs of the backbone run on bf16 operands with fp32 accumulation
  * (BASELINE config 4's bf16 compute; BN, pooling, heads, losses and the optimizer stay fp32).  Default 0: fp32
- * numerics (split-bf16 products). */
+ * numerics (split-bf16 products).  "stem_grad" (0/1): backbone.conv1 / bn1 train (the module without
+ * apply_memory_efficient_training, cad:592-598); set before the forward.  "wgrad_stream" (0/1, default 1): the
+ * backbone's weight gradients run on a plan-owned stream beside the input gradients (results identical). */
 int vad_cad_set_option(vad_cad_plan* plan, const char* key, int64_t value);
 /* Kernel family of backbone 3x3 conv `layer` (0..7) for kind 0 forward / 1 input gradient / 2 weight gradient:
  * 6 = split-bf16 (fp32 numerics, six bf16 MFMA products per K step), 1 = bf16 operands, 0 = f32 MFMA; -1 on error.
