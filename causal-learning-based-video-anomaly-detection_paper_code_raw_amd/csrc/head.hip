@@ -292,7 +292,8 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
   __shared__ int s_N, s_any;
   __shared__ float s_red[4];
   const float* Whh = PW(H_GRU_WHH);
-  block_copy4<6>(whh, Whh, G3 * GH / 4, [](int i) { return (i >> 4) * (WHH_LD / 4) + (i & 15); });
+  // the n-gate rows of W_hh in LDS (the r / z rows live in registers, below)
+  block_copy4<6>(whh, Whh + 2 * GH * GH, GH * GH / 4, [](int i) { return (i >> 4) * (WHH_LD / 4) + (i & 15); });
   for (int i = tid; i < NMAX * GH; i += HT) hs[i] = 0.f;
   if (tid == 0) {
     int N = 1, any = 0;
@@ -307,8 +308,9 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
   const int N = s_N;
   const float* bhh = PW(H_GRU_BHH);
   // GRU recurrence, gate order (r, z, n) (cad:284,298): one wave per trajectory slot, lane u owns hidden unit u
-  // and computes exactly its three gate pre-activations (W_hh rows u, GH+u, 2GH+u from LDS), so a time step
-  // needs no block barrier -- only the wave's own LDS copy of h is exchanged between steps.
+  // and computes exactly its three gate pre-activations from W_hh rows u, GH+u (held in its registers: 128 VGPRs,
+  // read once) and 2GH+u (LDS), so a time step needs no block barrier -- only the wave's own LDS copy of h
+  // (broadcast reads) is exchanged between steps.
   static_assert(NMAX * 64 <= HT && GH == 64, "one wave per trajectory, one lane per hidden unit");
   {
     const int nn = tid >> 6, u = tid & 63;
@@ -316,13 +318,17 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
       float h = 0.f;
       const bool live = nn < N;
       const float br = bhh[u], bz = bhh[GH + u], bn = bhh[2 * GH + u];
-      const f32x4* wr = reinterpret_cast<const f32x4*>(whh + u * WHH_LD);
-      const f32x4* wz = reinterpret_cast<const f32x4*>(whh + (GH + u) * WHH_LD);
-      const f32x4* wn = reinterpret_cast<const f32x4*>(whh + (2 * GH + u) * WHH_LD);
+      f32x4 wr[GH / 4], wz[GH / 4];
+#pragma unroll
+      for (int kk = 0; kk < GH / 4; ++kk) {
+        wr[kk] = *reinterpret_cast<const f32x4*>(Whh + u * GH + 4 * kk);
+        wz[kk] = *reinterpret_cast<const f32x4*>(Whh + (GH + u) * GH + 4 * kk);
+      }
+      const f32x4* wn = reinterpret_cast<const f32x4*>(whh + u * WHH_LD);
       const f32x4* hv = reinterpret_cast<const f32x4*>(hs + nn * GH);
       // the input projections are loaded TC steps at a time, one chunk ahead (double-buffered in registers): a
       // per-step prefetch would be waited for together with the previous step's stores (vmcnt counts both)
-      constexpr int TC = 8;
+      constexpr int TC = 4;
       float gc[TC][3], gn[TC][3];
       auto load_gi = [&](int t0, float (&g)[TC][3]) {
 #pragma unroll
@@ -523,7 +529,7 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
   float* g = slabs + (int64_t)b * slab_len;
   __shared__ __attribute__((aligned(16))) float big[HF_BIG];  // MLP weight image, then W_hh [q][j] for BPTT
   __shared__ __attribute__((aligned(16))) float sw[HL_TOTAL];
-  __shared__ float dgh_s[NMAX * G3];
+  __shared__ __attribute__((aligned(16))) float dgh_s[NMAX * G3];
   float* sW = big;
   float* w = sw;
   stage_head_weights(a, sW);
@@ -705,20 +711,20 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
     // published to the wave's LDS row, and dh_prev[u] = dh[u] z[u] + sum_q W_hh[q][u] dgh[q] reads them back --
     // no block barrier inside the time loop
     static_assert(NMAX * 64 <= HT && GH == 64, "one wave per trajectory, one lane per hidden unit");
-    static_assert(G3 * GH <= HF_BIG, "W_hh fits the weight image's LDS");
-    __syncthreads();  // the MLP weight image is dead: load W_hh [q][j] (read by columns, conflict-free)
-    float* whh = big;
+    // column u of W_hh (W_hh[q][u], q < 3 GH) lives in lane u's registers: the recurrence reads only the
+    // wave's 3 GH gate grads from LDS (broadcast b128), not 192 lane-distinct LDS words per step
     const float* Whh = PW(H_GRU_WHH);
-    block_copy4<6>(whh, Whh, G3 * GH / 4, Ident{});
-    __syncthreads();
     const int nn = tid >> 6, u = tid & 63;
     if (nn < NMAX) {
       const bool live = nn < N;
+      float wc[G3];
+#pragma unroll
+      for (int q = 0; q < G3; ++q) wc[q] = Whh[q * GH + u];
       float d = live ? dh[nn * GH + u] : 0.f;
       float* dgv = dgh_s + nn * G3;
       // the saved gates are loaded TC steps at a time, one chunk ahead (double-buffered in registers; see the
       // forward recurrence)
-      constexpr int TC = 8;
+      constexpr int TC = 2;
       float sc_[TC][5], sn_[TC][5];  // r, z, n, h_prev, W_hn h_prev + b_hn of steps t0, t0-1, ...
       auto load_gates = [&](int t0, float (&g)[TC][5]) {
 #pragma unroll
@@ -757,7 +763,15 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             float s = d * z;
-            for (int q = 0; q < G3; ++q) s = fmaf(whh[q * GH + u], dgv[q], s);
+            const f32x4* dg4 = reinterpret_cast<const f32x4*>(dgv);
+#pragma unroll
+            for (int q4 = 0; q4 < G3 / 4; ++q4) {
+              const f32x4 g = dg4[q4];
+              s = fmaf(wc[4 * q4], g[0], s);
+              s = fmaf(wc[4 * q4 + 1], g[1], s);
+              s = fmaf(wc[4 * q4 + 2], g[2], s);
+              s = fmaf(wc[4 * q4 + 3], g[3], s);
+            }
             d = s;
           } else {
             dgi[u] = 0.f; dgi[GH + u] = 0.f; dgi[2 * GH + u] = 0.f;
