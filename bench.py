@@ -133,10 +133,16 @@ def run_gpu(args, rank, world, local_rank):
     torch.cuda.synchronize()
     breakdown = eng.profile_read()
     fam_time = {}
+    # the backbone's weight gradients run on their own stream concurrently with the input gradients (DESIGN.md
+    # §3 Streams, option "wgrad_stream"): their event times include sharing the GPU, and they are off the
+    # critical path, so the dominant family is the largest one on the plan's critical stream
+    wgrad_overlapped = not any(kv.startswith("cad_wgrad_stream=0") for kv in args.tune)
     for lab, (ms, n) in breakdown.items():
         if algorithmic_work(lab, B, T, H, W)[0] is None:
             continue  # only families with a defined algorithmic work can carry a roofline
         fam = lab.split("/L")[0]
+        if fam == "conv_wgrad" and wgrad_overlapped and args.config in (2, 4):
+            continue
         fam_time[fam] = fam_time.get(fam, 0.0) + ms
     dominant = max(fam_time, key=fam_time.get)
 
@@ -199,6 +205,9 @@ def run_gpu(args, rank, world, local_rank):
             ach = tot_work / (tot_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 1), "peak": PEAK_HBM_GBPS,
                     "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 4), "traffic": None}
+        roof["dominant_basis"] = ("largest conv family on the critical stream (conv_wgrad runs concurrently on its "
+                                  "own stream)" if wgrad_overlapped and args.config in (2, 4) else
+                                  "largest conv family in an instrumented step")
         roof["launches_timed"] = launches
         roof["avg_launch_us"] = round(1e3 * tot_ms / max(launches, 1), 2)
         traffic, src = pmc_traffic(dominant)
