@@ -96,6 +96,11 @@ bool conv3_x3_supported(const Conv3Layer& L, bool fwd);
 int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
                  float* y, float* partials, int* nparts, hipStream_t st);
 int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
+// stride-2 input gradient on the split-bf16 (or, with conv_bf16, bf16) MFMA: parity classes of a 16x16 dX tile
+// sharing one dY patch; Wd in the plain [Ci][9][Co] layout (conv3_prep_weights with classes == 0)
+extern int g_dgrad_s2_x3;  // knob "conv_dgrad_s2_x3"
+bool conv3_x3_dgrad_s2_supported(const Conv3Layer& L);
+int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
 extern int g_wgrad_split;     // stride-1 weight gradients on the split-bf16 kernel (knob "conv_wgrad_split")
 extern int g_wgrad_s1_nt, g_wgrad_s1_nt_blocks, g_wgrad_s1_nt_wide;  // knobs "conv_wgrad_s1_nt", "conv_wgrad_s1_nt_blocks"
 extern int g_wgrad_s2_blocks;  // their target grid size (knob "conv_wgrad_s2_blocks")

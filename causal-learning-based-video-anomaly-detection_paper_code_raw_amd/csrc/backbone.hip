@@ -927,6 +927,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_s2_blocks") g_wgrad_s2_blocks = value;
   else if (k == "stem_fused") g_stem_fused = value;
   else if (k == "conv_split_stagger") g_x3_stagger = value;
+  else if (k == "conv_dgrad_s2_x3") g_dgrad_s2_x3 = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "stem_dbg") g_stem_dbg = value;
@@ -1132,6 +1133,9 @@ int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX
   VAD_CHECK(L.Co % 32 == 0, "conv3_dgrad: Co must be a multiple of 32");
   const int N = L.Ci;
   if (g_tune.patch && conv3_x3_supported(L, false)) return conv3_x3_dgrad(L, dY, wd, dX, st);
+  // (the split kernel reads the plain Wd layout, which the prep writes exactly when the f32 patch kernel is usable)
+  if (g_tune.patch && conv3_patch_supported(L, false) && conv3_x3_dgrad_s2_supported(L))
+    return conv3_x3_dgrad_s2(L, dY, wd, dX, st);
   if (g_tune.patch && conv3_patch_supported(L, false)) return conv3_patch_dgrad(L, dY, wd, dX, st);
   if (L.stride == 1) {
     ConvGeom g{L.NF, L.IH, L.IW, 1, 1, L.OH, L.OW, L.Co};

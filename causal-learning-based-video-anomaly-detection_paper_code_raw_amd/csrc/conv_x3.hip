@@ -412,6 +412,187 @@ int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float*
 }
 
 // =====================================================================================================
+// Stride-2 input gradient on the split-bf16 MFMA (the parity-class scheme of conv_patch.hip's f32 kernel): the four
+// parity classes (ph, pw) of a 16x16 dX tile read one 9x9 dY patch -- class (ph, pw) uses the kernel rows kh with
+// ph + 1 - kh even at dY row offset (ph + 1 - kh) / 2, likewise columns -- so one staged patch and one staged
+// 9-tap weight slice serve 1 + 2 + 2 + 4 taps.  Wave w takes the class-tile half w & 1 (32 class pixels) of two
+// classes, (1,1)+(0,0) for waves 0-1 and (0,1)+(1,0) for waves 2-3 (5 / 4 taps), for 32*NT input channels.
+// p.src = dY [NF][IH][IW][C = Co], p.w = Wd [N = Ci][9][C], p.out = dX [NF][OH][OW][N].
+// =====================================================================================================
+template <int NT, int PC, int NP, int CPH, int CPW>
+__device__ __forceinline__ void dgrad_s2x3_class(f32x16 (&acc)[NT], const __bf16* abase, const __bf16* bbase,
+                                                 int WP) {
+#pragma unroll
+  for (int a = 0; a < (CPH ? 2 : 1); ++a) {
+    const int kh = CPH ? (a == 0 ? 0 : 2) : 1, dh = (CPH && a == 0) ? 1 : 0;
+#pragma unroll
+    for (int b = 0; b < (CPW ? 2 : 1); ++b) {
+      const int kw = CPW ? (b == 0 ? 0 : 2) : 1, dw = (CPW && b == 0) ? 1 : 0;
+      const __bf16* ap = abase + (dh * 9 + dw) * (NP * PC + 8);
+      const __bf16* bp = bbase + (kh * 3 + kw) * NP * PC;
+#pragma unroll
+      for (int kk = 0; kk < PC / 16; ++kk) {
+        bf16x8 av[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) av[q] = *reinterpret_cast<const bf16x8*>(ap + q * PC + kk * 16);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          bf16x8 bv[NP];
+#pragma unroll
+          for (int q = 0; q < NP; ++q)
+            bv[q] = *reinterpret_cast<const bf16x8*>(bp + nt * 32 * WP + q * PC + kk * 16);
+          if constexpr (NP == 3) acc[nt] = mfma_x3(av, bv, acc[nt]);
+          else acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[0], acc[nt], 0, 0, 0);
+        }
+      }
+    }
+  }
+}
+
+template <int NT, int PC, int NP>
+__global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args p) {
+  static_assert(PC % 16 == 0, "16-deep K steps");
+  constexpr int NC = 32 * NT, G8 = PC / 8, PROWS = 81;
+  constexpr int RP = NP * PC + 8, WP = 9 * NP * PC + 8;
+  static_assert(((RP * 2 / 16) & 1) && ((WP * 2 / 16) & 1), "odd 16-B row pitch");
+  __shared__ __attribute__((aligned(16))) __bf16 sm[PROWS * RP + NC * WP];
+  __bf16* patch = sm;
+  __bf16* wl = sm + PROWS * RP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, j = lane & 31;
+  const int tiles_per_img = p.tiles_h * p.tiles_w;
+  const int img = blockIdx.x / tiles_per_img, trem = blockIdx.x % tiles_per_img;
+  const int i0 = (trem / p.tiles_w) * 8, j0 = (trem % p.tiles_w) * 8;  // class-grid origin = dY patch origin
+  const int n0 = blockIdx.y * NC;
+  const int g = wave & 1;  // class-tile rows 4g .. 4g+3
+  const __bf16* abase = patch + ((4 * g + j / 8) * 9 + j % 8) * RP + 8 * h;
+  const __bf16* bbase = wl + j * WP + 8 * h;
+  const int nch = p.C / PC;
+
+  constexpr int PQ = PROWS * G8, PIT = (PQ + 255) / 256;
+  constexpr int WQ = NC * 9 * G8, WIT = (WQ + 255) / 256;
+  const int g8 = tid % G8;
+  f32x4 pv[PIT][2], wv[WIT][2];
+  bool pok[PIT], wok[WIT];
+  // unconditional loads from clamped addresses; out-of-range rows are zeroed at stash time (see conv3x3_x3_kernel)
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = tid + it * 256, row = q / G8;
+      const int y = i0 + row / 9, x = j0 + row % 9;
+      pok[it] = q < PQ && y < p.IH && x < p.IW;
+      const float* s = p.src + c0 + g8 * 8 + (pok[it] ? (((int64_t)img * p.IH + y) * p.IW + x) * p.C : (int64_t)0);
+      pv[it][0] = *reinterpret_cast<const f32x4*>(s);
+      pv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
+    }
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int q = tid + it * 256, n = q / (9 * G8), t = (q / G8) % 9;
+      wok[it] = q < WQ && n0 + n < p.N;
+      const float* s = p.w + c0 + g8 * 8 + (wok[it] ? ((int64_t)(n0 + n) * 9 + t) * p.C : (int64_t)0);
+      wv[it][0] = *reinterpret_cast<const f32x4*>(s);
+      wv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = tid + it * 256;
+      if (q < PQ) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = pok[it] ? pv[it][0][e] : 0.f;
+          v[4 + e] = pok[it] ? pv[it][1][e] : 0.f;
+        }
+        put_planes<NP>(patch + (q / G8) * RP + g8 * 8, PC, v, false);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int q = tid + it * 256;
+      if (q < WQ) {
+        const int n = q / (9 * G8), t = (q / G8) % 9;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = wok[it] ? wv[it][0][e] : 0.f;
+          v[4 + e] = wok[it] ? wv[it][1][e] : 0.f;
+        }
+        put_planes<NP>(wl + n * WP + t * NP * PC + g8 * 8, PC, v, false);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // (see conv3x3_x3_kernel's stash)
+  };
+
+  f32x16 acc0[NT], acc1[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc0[nt][r] = acc1[nt][r] = 0.f;
+  fetch(0);
+  for (int ch = 0; ch < nch; ++ch) {
+    __syncthreads();  // the previous chunk's fragment reads are done
+    stash();
+    __syncthreads();
+    if (ch + 1 < nch) fetch((ch + 1) * PC);
+    if (wave < 2) {
+      dgrad_s2x3_class<NT, PC, NP, 1, 1>(acc0, abase, bbase, WP);
+      dgrad_s2x3_class<NT, PC, NP, 0, 0>(acc1, abase, bbase, WP);
+    } else {
+      dgrad_s2x3_class<NT, PC, NP, 0, 1>(acc0, abase, bbase, WP);
+      dgrad_s2x3_class<NT, PC, NP, 1, 0>(acc1, abase, bbase, WP);
+    }
+  }
+  const int ph0 = wave < 2 ? 1 : 0, pw0 = 1;  // acc0 class: (1,1) or (0,1)
+  const int ph1 = wave < 2 ? 0 : 1, pw1 = 0;  // acc1 class: (0,0) or (1,0)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int pm = (r & 3) + 8 * (r >> 2) + 4 * h;
+    const int ca = i0 + 4 * g + pm / 8, cb = j0 + pm % 8;
+    const int y0 = 2 * ca + ph0, x0 = 2 * cb + pw0, y1 = 2 * ca + ph1, x1 = 2 * cb + pw1;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int col = n0 + nt * 32 + j;
+      if (col >= p.N) continue;
+      if (y0 < p.OH && x0 < p.OW) p.out[(((int64_t)img * p.OH + y0) * p.OW + x0) * p.N + col] = acc0[nt][r];
+      if (y1 < p.OH && x1 < p.OW) p.out[(((int64_t)img * p.OH + y1) * p.OW + x1) * p.N + col] = acc1[nt][r];
+    }
+  }
+}
+
+int g_dgrad_s2_x3 = 1;  // tuning knob "conv_dgrad_s2_x3": stride-2 input gradients on the split-bf16 kernel
+
+bool conv3_x3_dgrad_s2_supported(const Conv3Layer& L) {
+  return g_conv_split && g_dgrad_s2_x3 && L.stride == 2 && L.Co % 16 == 0 && L.Ci % 32 == 0 &&
+         L.OH == (L.IH - 1) / 2 + 1 && L.OW == (L.IW - 1) / 2 + 1;
+}
+
+int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st) {
+  VAD_CHECK(conv3_x3_dgrad_s2_supported(L), "conv3_x3_dgrad_s2: unsupported layer");
+  X3Args a{};
+  a.src = dY;
+  a.w = wd;
+  a.out = dX;
+  a.NF = L.NF; a.IH = L.OH; a.IW = L.OW; a.C = L.Co; a.OH = L.IH; a.OW = L.IW; a.N = L.Ci;
+  a.tiles_h = (int)cdiv((L.IH + 1) / 2, 8);
+  a.tiles_w = (int)cdiv((L.IW + 1) / 2, 8);
+  const int tiles = L.NF * a.tiles_h * a.tiles_w;
+  // 64 input channels per block where that still gives >= 2 blocks per CU, else 32
+  const bool nt2 = L.Ci % 64 == 0 && (int64_t)tiles * (L.Ci / 64) >= 512;
+  dim3 grid((unsigned)tiles, (unsigned)(L.Ci / (nt2 ? 64 : 32)));
+  if (g_conv_bf16) {
+    if (nt2) VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<2, 16, 1>), grid, dim3(256), 0, st, a);
+    else VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<1, 16, 1>), grid, dim3(256), 0, st, a);
+  } else {
+    if (nt2) VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<2, 16, 3>), grid, dim3(256), 0, st, a);
+    else VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<1, 16, 3>), grid, dim3(256), 0, st, a);
+  }
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+// =====================================================================================================
 // Stride-1 weight gradient on the split-bf16 MFMA: dW[co][t][ci] = sum_p dY[p][co] * relu(bn(x))[p + off_t][ci].
 // GEMM view per tap: M = 32 co (A = dY^T), N = 32 ci (B = shifted input), K = output pixels.  A K step is 16
 // consecutive tile pixels; lane half h holds 8 of them, which lie in one tile row (TW % 8 == 0).  LDS holds

@@ -61,7 +61,7 @@ def _conv_default(nat):
 @pytest.mark.parametrize("patch", [3, 1, 0, 2])
 @pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", CONV_CASES)
 def test_conv3x3_forward_and_dgrad(NF, Ci, Co, IH, IW, s, patch):
-    """patch 3: split-bf16 patch kernels (conv_x3.hip; stride-2 input gradients stay on the f32 parity kernel),
+    """patch 3: split-bf16 patch kernels (conv_x3.hip; stride-2 input gradients on the split parity-class kernel),
     1: f32 LDS-patch kernels (persistent variant for 32-channel stride-1 layers), 2: f32 patch kernels without the
     persistent variant, 0: implicit-GEMM path."""
     nat = _lib()
@@ -130,6 +130,36 @@ def test_conv3x3_split_accuracy_matches_f32(NF, Ci, Co, IH, IW, s):
     _conv_default(nat)
     assert errs[3] < 1e-6, errs
     assert errs[3] <= 2.0 * errs[1] + 1e-8, errs
+
+
+@pytest.mark.parametrize("NF,Ci,Co,IH,IW", [(2, 32, 64, 57, 57), (3, 64, 128, 29, 29), (4, 128, 256, 15, 15),
+                                            (2, 64, 128, 31, 18)])
+def test_conv3x3_dgrad_s2_split_accuracy_matches_f32(NF, Ci, Co, IH, IW):
+    """Stride-2 input gradient on the split-bf16 parity-class kernel against an fp64 reference: worst error relative
+    to sum |dy||w| within 2x that of the exact-f32 parity kernel (both ~1e-7)."""
+    nat = _lib()
+    g = torch.Generator().manual_seed(17 + Ci + IH)
+    w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
+    OH, OW = (IH - 1) // 2 + 1, (IW - 1) // 2 + 1
+    dy = torch.randn(NF, Co, OH, OW, generator=g)
+    ref = torch.nn.grad.conv2d_input((NF, Ci, IH, IW), w.double(), dy.double(), stride=2, padding=1)
+    mag = torch.nn.grad.conv2d_input((NF, Ci, IH, IW), w.double().abs(), dy.double().abs(), stride=2, padding=1)
+    d = torch.device("cuda")
+    dyh = dy.permute(0, 2, 3, 1).contiguous().to(d)
+    wdev = w.contiguous().to(d)
+    wf = torch.empty(9 * Ci * Co, device=d)
+    wd = torch.empty(9 * Ci * Co, device=d)
+    errs = {}
+    for split in (0, 1):
+        nat.lib().vad_set_tuning(b"conv_dgrad_s2_x3", split)
+        dx = torch.empty(NF, IH, IW, Ci, device=d)
+        nat.check(nat.lib().vad_conv3x3_dgrad(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, 2, dx.data_ptr(),
+                                              wf.data_ptr(), wd.data_ptr(), nat.stream_of(d)))
+        torch.cuda.synchronize()
+        errs[split] = float(((dx.cpu().permute(0, 3, 1, 2).double() - ref).abs() / (mag + 1e-30)).max())
+    nat.lib().vad_set_tuning(b"conv_dgrad_s2_x3", 1)
+    assert errs[1] < 1e-6, errs
+    assert errs[1] <= 2.0 * errs[0] + 1e-8, errs
 
 
 @pytest.mark.parametrize("stream", [rng.S_DET_DROP1, rng.S_EPS, rng.S_INPUT])
@@ -235,7 +265,7 @@ def _bf16(t):
 def test_conv3x3_bf16_mode_matches_rounded_fp64(NF, Ci, Co, IH, IW, s):
     """conv_bf16 (BASELINE config 4): operands rounded to bf16, products exact, fp32 accumulation.  Against an fp64
     conv of the bf16-rounded operands the error stays at fp32 accumulation level (< 1e-5 of sum |a||b|); stride-1
-    input and weight gradients take the same path (stride-2 input gradients stay on the fp32 kernel)."""
+    input and weight gradients take the same path (stride-2 input gradients on the bf16 parity-class kernel)."""
     nat = _lib()
     nat.lib().vad_set_tuning(b"conv_bf16", 1)
     try:
@@ -271,14 +301,12 @@ def test_conv3x3_bf16_mode_matches_rounded_fp64(NF, Ci, Co, IH, IW, s):
         rdw = torch.nn.grad.conv2d_weight(_bf16(x), w.shape, _bf16(dy), stride=s, padding=1)
         mdw = torch.nn.grad.conv2d_weight(_bf16(x).abs(), w.shape, _bf16(dy).abs(), stride=s, padding=1)
         assert float(((dW.cpu().double() - rdw).abs() / (mdw + 1e-30)).max()) < 1e-5
-        if s != 1:
-            return
         dx = torch.empty(NF, IH, IW, Ci, device=d)
         nat.check(nat.lib().vad_conv3x3_dgrad(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, s, dx.data_ptr(),
                                               wf.data_ptr(), wd.data_ptr(), st))
         torch.cuda.synchronize()
-        rdx = torch.nn.grad.conv2d_input(x.shape, _bf16(w), _bf16(dy), stride=1, padding=1)
-        mdx = torch.nn.grad.conv2d_input(x.shape, _bf16(w).abs(), _bf16(dy).abs(), stride=1, padding=1)
+        rdx = torch.nn.grad.conv2d_input(x.shape, _bf16(w), _bf16(dy), stride=s, padding=1)
+        mdx = torch.nn.grad.conv2d_input(x.shape, _bf16(w).abs(), _bf16(dy).abs(), stride=s, padding=1)
         assert float(((dx.cpu().permute(0, 3, 1, 2).double() - rdx).abs() / (mdx + 1e-30)).max()) < 1e-5
     finally:
         nat.lib().vad_set_tuning(b"conv_bf16", 0)
