@@ -904,7 +904,7 @@ struct ConvTuning {
   int wgrad_min_ktiles = 16;             // minimum BK-slices per split
   int patch = 1;                         // stride-1 fwd/dgrad on the LDS-patch kernels
   int wgrad_patch = 1;                   // weight gradients on the LDS-patch kernel: 1 stride-1 layers, 2 all
-  int wgrad_patch_blocks = 512;          // its target grid size
+  int wgrad_patch_blocks = 448;          // its target grid size (below 2 per CU: the weight gradients share the GPU with the input gradients, own stream)
 };
 static ConvTuning g_tune;
 

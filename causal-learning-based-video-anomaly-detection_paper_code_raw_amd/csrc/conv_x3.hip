@@ -1090,10 +1090,10 @@ static int launch_wgrad_x3nt_co(WgX3Args a, int nt, int target_blocks, int64_t p
 
 int g_wgrad_split = 1;     // tuning knob "conv_wgrad_split": stride-1 weight gradients on the split-bf16 kernel
 int g_wgrad_split_s2 = 1;  // tuning knob "conv_wgrad_split_s2": stride-2 weight gradients on the split-bf16 kernel
-int g_wgrad_s2_blocks = 512;  // tuning knob "conv_wgrad_s2_blocks": their target grid size
+int g_wgrad_s2_blocks = 384;  // tuning knob "conv_wgrad_s2_blocks": their target grid size (sweep: profiles/r02_wgrad_grid_sweep.json)
 int g_wgrad_s1_nt = 2;  // tuning knob "conv_wgrad_s1_nt": stride-1 frames <= 16 wide on the multi-co-tile kernel (2|4)
 int g_wgrad_s1_nt_wide = 0;  // knob "conv_wgrad_s1_nt_wide": wider stride-1 frames too (2x32 tiles)
-int g_wgrad_s1_nt_blocks = 512;  // knob "conv_wgrad_s1_nt_blocks"
+int g_wgrad_s1_nt_blocks = 384;  // knob "conv_wgrad_s1_nt_blocks"
 
 bool conv3_wgrad_x3_supported(const Conv3Layer& L) {
   if (!g_conv_split || L.Ci % 32 != 0 || L.Co % 32 != 0) return false;
