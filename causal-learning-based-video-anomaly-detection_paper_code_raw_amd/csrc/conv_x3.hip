@@ -318,6 +318,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
   }
 }
 
+int g_x3_dgrad_blocks = 512;  // knob "conv_dgrad_blocks"
+
 template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1>
 static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   VAD_CHECK(WCH == 1 || a.C == WCH * PC, "conv3x3_x3: resident weights need C == WCH * PC");
@@ -325,7 +327,9 @@ static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   a.tiles_w = (int)cdiv(a.OW, TW);
   a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);
   const int ny = (int)cdiv(a.N, 32 * NT);
-  const int target = std::max(1, std::min(max_blocks, 512 / ny));  // 2 resident blocks per CU over 256 CUs
+  // 2 resident blocks per CU over 256 CUs (input gradients: knob "conv_dgrad_blocks", they share the GPU with the
+  // weight gradients)
+  const int target = std::max(1, std::min(max_blocks, (FWD ? 512 : g_x3_dgrad_blocks) / ny));
   a.tpb = (int)cdiv(a.ntiles, target);
   a.dbg = g_x3_dbg;
   a.stagger = g_x3_stagger;
@@ -341,6 +345,7 @@ thread_local int g_conv_bf16 = 0;  // bf16-operand convs (one plane, one product
 int g_x3_nt = 0;       // tuning knob "conv_split_nt": 0 = auto, 1 / 2 = force 32 / 64 output channels per block
 int g_x3_dbg = 0;      // knob "conv_split_dbg" (measurement only, see X3Args::dbg)
 int g_x3_stagger = 0;  // knob "conv_split_stagger" (see X3Args::stagger)
+
 
 int g_x3_wres = 1;  // knob "conv_split_wres": 32-channel stride-1 layers keep all split weights resident in LDS
 
