@@ -81,10 +81,14 @@ __device__ __forceinline__ void put_planes(__bf16* d, int pitch, const float* v,
 // WCH > 1: the block keeps the split weights of all WCH reduction chunks resident in LDS (staged during its first
 // tile, p.C == WCH * PC) instead of restaging the chunk's slice for every (tile, chunk) item -- the weight split is
 // most of the staging VALU of the 32-channel layers
-template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1>
-__global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
+// NW = 8: 512-thread blocks over 256-pixel tiles (one block per CU): the weight slice staged per item serves twice
+// the pixels (the weight staging per MFMA halves) and the halo share of the patch drops
+template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Args p) {
   static_assert(NP == 3 || NP == 1, "three split planes (fp32 numerics) or one (bf16 operands)");
-  static_assert(NI * TH * TW == 128, "a block owns 128 output pixels");
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(NI * TH * TW == 32 * NW, "a wave owns 32 output pixels");
+  constexpr int NTHR = 64 * NW;
   static_assert(FWD || S == 1, "stride-2 input gradients use conv3x3_dgrad_s2_kernel");
   static_assert(PC % 16 == 0, "16-deep K steps");
   constexpr int NC = 32 * NT, G8 = PC / 8;
@@ -110,9 +114,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
   const int arow0 = (mi * PH + py * S) * PW;
   const __bf16* bbase = wl + j * WP + 8 * h;
 
-  // staging: thread tid always handles the channel group g8 = tid % G8 (256 % G8 == 0)
-  constexpr int PQ = PROWS * G8, PIT = (PQ + 255) / 256;
-  constexpr int WQ = NC * 9 * G8, WIT = (WQ + 255) / 256;
+  // staging: thread tid always handles the channel group g8 = tid % G8 (NTHR % G8 == 0)
+  constexpr int PQ = PROWS * G8, PIT = (PQ + NTHR - 1) / NTHR;
+  constexpr int WQ = NC * 9 * G8, WIT = (WQ + NTHR - 1) / NTHR;
   const int g8 = tid % G8;
   f32x4 pv[PIT][2], wv[WIT][2];
   // prefetch loads are unconditional (out-of-range lanes read a valid dummy address) and the zero padding is applied
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
     origin(tile, img0, oy0, ox0);
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
-      const int q = tid + it * 256;
+      const int q = tid + it * NTHR;
       const int row = q / G8;
       const int im = row / (PH * PW), rr = row % (PH * PW);
       const int iy = oy0 * S - 1 + rr / PW, ix = ox0 * S - 1 + rr % PW, img = img0 + im;
@@ -142,7 +146,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
     if (weights) {
 #pragma unroll
       for (int it = 0; it < WIT; ++it) {
-        const int q = tid + it * 256;
+        const int q = tid + it * NTHR;
         const int n = q / (9 * G8), t = (q / G8) % 9;
         wok[it] = q < WQ && n0 + n < p.N;
         const float* s = p.w + c0 + g8 * 8 +
@@ -170,7 +174,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
     }
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
-      const int q = tid + it * 256;
+      const int q = tid + it * NTHR;
       if (q < PQ) {
         const int row = q / G8;
         const int im = row / (PH * PW), rr = row % (PH * PW);
@@ -200,7 +204,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
     if (weights) {
 #pragma unroll
       for (int it = 0; it < WIT; ++it) {
-        const int q = tid + it * 256;
+        const int q = tid + it * NTHR;
         if (q < WQ) {
           const int n = q / (9 * G8), t = (q / G8) % 9;
           float v[8];
@@ -298,7 +302,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
   }
   if (FWD) {
     __syncthreads();
-    float* red = reinterpret_cast<float*>(sm);  // [4 waves][2][NC]
+    float* red = reinterpret_cast<float*>(sm);  // [NW waves][2][NC]
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const float a1 = s1[nt] + __shfl_xor(s1[nt], 32, 64);
@@ -309,10 +313,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
       }
     }
     __syncthreads();
-    for (int q = tid; q < 2 * NC; q += 256) {
+    for (int q = tid; q < 2 * NC; q += NTHR) {
       const int which = q / NC, c = q % NC;
-      const float v = red[which * NC + c] + red[(2 + which) * NC + c] + red[(4 + which) * NC + c] +
-                      red[(6 + which) * NC + c];
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += red[(2 * w + which) * NC + c];  // fixed order
       if (n0 + c < p.N) p.partials[(int64_t)blockIdx.x * 2 * p.N + which * p.N + n0 + c] = v;
     }
   }
@@ -320,7 +325,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(const X3Args p) {
 
 int g_x3_dgrad_blocks = 512;  // knob "conv_dgrad_blocks"
 
-template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1>
+template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1, int NW = 4>
 static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   VAD_CHECK(WCH == 1 || a.C == WCH * PC, "conv3x3_x3: resident weights need C == WCH * PC");
   a.tiles_h = (int)cdiv(a.OH, TH);
@@ -329,12 +334,12 @@ static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   const int ny = (int)cdiv(a.N, 32 * NT);
   // 2 resident blocks per CU over 256 CUs (input gradients: knob "conv_dgrad_blocks", they share the GPU with the
   // weight gradients)
-  const int target = std::max(1, std::min(max_blocks, (FWD ? 512 : g_x3_dgrad_blocks) / ny));
+  const int target = std::max(1, std::min(max_blocks, (FWD ? 512 : g_x3_dgrad_blocks) * 4 / NW / ny));
   a.tpb = (int)cdiv(a.ntiles, target);
   a.dbg = g_x3_dbg;
   a.stagger = g_x3_stagger;
   const int gx = (int)cdiv(a.ntiles, a.tpb);
-  VAD_KLAUNCH((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD, NP, WCH>), dim3(gx, ny), dim3(256), 0, st, a);
+  VAD_KLAUNCH((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD, NP, WCH, NW>), dim3(gx, ny), dim3(64 * NW), 0, st, a);
   VAD_LAUNCH_CHECK();
   if (nparts) *nparts = gx;
   return 0;
@@ -349,22 +354,31 @@ int g_x3_stagger = 0;  // knob "conv_split_stagger" (see X3Args::stagger)
 
 int g_x3_wres = 1;  // knob "conv_split_wres": 32-channel stride-1 layers keep all split weights resident in LDS
 
-template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD>
+template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NW = 4>
 static int launch_x3(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   if constexpr (S == 1 && NT == 1) {
     if (g_x3_wres && a.C == 2 * PC) {
-      if (g_conv_bf16) return launch_np<S, NI, TH, TW, NT, PC, FWD, 1, 2>(a, max_blocks, st, nparts);
-      return launch_np<S, NI, TH, TW, NT, PC, FWD, 3, 2>(a, max_blocks, st, nparts);
+      if (g_conv_bf16) return launch_np<S, NI, TH, TW, NT, PC, FWD, 1, 2, NW>(a, max_blocks, st, nparts);
+      return launch_np<S, NI, TH, TW, NT, PC, FWD, 3, 2, NW>(a, max_blocks, st, nparts);
     }
   }
-  if (g_conv_bf16) return launch_np<S, NI, TH, TW, NT, PC, FWD, 1>(a, max_blocks, st, nparts);
-  return launch_np<S, NI, TH, TW, NT, PC, FWD, 3>(a, max_blocks, st, nparts);
+  if (g_conv_bf16) return launch_np<S, NI, TH, TW, NT, PC, FWD, 1, 1, NW>(a, max_blocks, st, nparts);
+  return launch_np<S, NI, TH, TW, NT, PC, FWD, 3, 1, NW>(a, max_blocks, st, nparts);
 }
+
+int g_x3_big = 1;  // knob "conv_split_big": stride-1 layers on 256-pixel tiles, 512-thread blocks (NW = 8)
 
 
 template <int S, bool FWD, int NT>
 static int dispatch_x3_nt(const X3Args& a, int max_blocks, hipStream_t st, int* nparts) {
   const int OH = a.OH, OW = a.OW;
+  if constexpr (S == 1) {
+    if (g_x3_big) {
+      if (OH <= 8 && OW <= 8) return launch_x3<S, 4, 8, 8, NT, 16, FWD, 8>(a, max_blocks, st, nparts);
+      if (OW <= 16) return launch_x3<S, 2, 8, 16, NT, 16, FWD, 8>(a, max_blocks, st, nparts);
+      return launch_x3<S, 1, 8, 32, NT, 16, FWD, 8>(a, max_blocks, st, nparts);
+    }
+  }
   if (OH <= 8 && OW <= 8) return launch_x3<S, 2, 8, 8, NT, 16, FWD>(a, max_blocks, st, nparts);
   if (OW <= 16) return launch_x3<S, 1, 8, 16, NT, 16, FWD>(a, max_blocks, st, nparts);
   return launch_x3<S, 1, 4, 32, NT, 16, FWD>(a, max_blocks, st, nparts);
