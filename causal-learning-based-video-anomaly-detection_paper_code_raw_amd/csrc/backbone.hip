@@ -4,11 +4,14 @@
 // nn.MaxPool2d(3,2,1), nn.AdaptiveAvgPool2d((4,6)), nn.Linear / ReLU / Dropout stacks (cad:167-179, 525-538).
 #include "backbone.h"
 #include "gemm.h"
+#include "head.h"
 
 namespace vad {
 
 int g_cad_prep_stream = 1;   // knob "cad_prep_stream": weight relayouts on the plan's side stream (A/B measurement)
 int g_cad_wgrad_stream = 1;  // knob "cad_wgrad_stream": backbone weight gradients on their own stream
+int g_dbg_skip_bnred = 0;    // knob "dbg_skip_bnred" (measurement only, results wrong): bit 1 skips the BN backward
+                             // reduce of layers 0-6, bit 2 the causal head's kernels
 
 // =====================================================================================================
 // conv1: 1 -> 32 channels, 7x7, stride 2, pad 3, as a K=49 (padded to 56) GEMM on f32 MFMA.
@@ -932,6 +935,8 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_split_big") g_x3_big = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
+  else if (k == "dbg_skip_bnred") g_dbg_skip_bnred = value;
+  else if (k == "head_dbg") g_head_dbg = value;
   else if (k == "stem_dbg") g_stem_dbg = value;
   else if (k == "conv_wgrad_s1_nt") g_wgrad_s1_nt = value;
   else if (k == "conv_wgrad_s1_nt_wide") g_wgrad_s1_nt_wide = value;

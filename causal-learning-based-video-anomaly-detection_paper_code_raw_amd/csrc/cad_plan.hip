@@ -507,6 +507,7 @@ struct CadPlanImpl {
     a.iws_stride = head_iws_ints(T);
     a.rows = head_rows;
     a.grad = grads;
+    a.dbg = g_head_dbg;
     return a;
   }
   HeadOut head_out() const { return HeadOut{causal, kl, z, adj, boxes, counts, nmax, clip_flags}; }
@@ -705,7 +706,7 @@ struct CadPlanImpl {
     VAD_HIP(hipMemsetAsync(d_feat_det, 0, sizeof(float) * (size_t)NF * 6144, st));
     {  // side stream: the causal head on the detections
       hipStream_t st = st2;
-      TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
+      if (!(g_dbg_skip_bnred & 2)) TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
     }
     VAD_TRY(join(st));
     TailArgs t = tail_args(nullptr, nullptr, nullptr, nullptr);
@@ -765,7 +766,7 @@ struct CadPlanImpl {
        // grads reach it, cad:221-226)
       hipStream_t st = st2;
       HeadUp up{d_causal, d_kl, dz, dadj, dboxes};
-      TIMED("head_bwd", head_bwd(head_args(), dlog, head_out(), up, slabs, slab_len, d_dlog, st));
+      if (!(g_dbg_skip_bnred & 2)) TIMED("head_bwd", head_bwd(head_args(), dlog, head_out(), up, slabs, slab_len, d_dlog, st));
     }
     // direct classifier chain (B rows): per-layer input-gradient GEMMs spread over many CUs, the layer 1-4 weight
     // grads in one launch, layer 0 GEMMs
@@ -810,7 +811,8 @@ struct CadPlanImpl {
       const int C = L[l].Co;
       int np = 0, nb = 0;
       float* dYl = (l & 1) ? dY2 : dY;
-      TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st));
+      if ((g_dbg_skip_bnred & 1) && l < 7) np = 1;  // measurement only (knob "dbg_skip_bnred": results wrong)
+      else TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st));
       VAD_TRY(bn_bwd_stats(l + 1, np, C, (double)M, P(LY.bn_w[l]), G(LY.bn_w[l]), G(LY.bn_b[l]), G(LY.conv_b[l]), st));
       // dYl was last read by layer l+2's weight gradient
       if (wgs && l + 2 <= 7) VAD_HIP(hipStreamWaitEvent(st, ev_wg[l & 1], 0));

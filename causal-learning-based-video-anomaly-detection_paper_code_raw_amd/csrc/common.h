@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <string>
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -109,6 +110,11 @@ __device__ inline float rng_normal(uint64_t h1, uint64_t row, uint64_t idx) {
 
 // ---------------------------------------------------------------- device math
 __device__ inline float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+// gate nonlinearities of the GRU recurrences: hardware exp2 and reciprocal (v_exp_f32 / v_rcp_f32, ~1 ulp each)
+// instead of the correctly rounded library forms (division: ~10 instructions) -- absolute error < 2e-7, both
+// saturate cleanly (exp -> inf gives 0 / +-1)
+__device__ inline float gate_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ inline float gate_tanh(float x) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x)); }
 
 __device__ inline float wave_sum(float v) {
 #pragma unroll

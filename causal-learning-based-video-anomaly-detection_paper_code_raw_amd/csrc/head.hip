@@ -78,73 +78,146 @@ int64_t head_ws_floats(int T) {
 int64_t head_iws_ints(int T) { return (int64_t)T * (1 + NMAX) + 8; }
 
 // ------------------------------------------------------------------ block-wide small dense layers
-__device__ void lin_fwd(const float* in, int ldi, int R, int I, const float* __restrict__ W,
-                        const float* __restrict__ b, int O, float* out, int ldo, bool relu) {
-  for (int idx = threadIdx.x; idx < R * O; idx += blockDim.x) {
-    const int r = idx / O, o = idx - r * O;
-    float s = b ? b[o] : 0.f;
-    const float* w = W + (int64_t)o * I;
-    const float* v = in + (int64_t)r * ldi;
-    // W lives in LDS: rotating the start column by o spreads the lanes of one row block over the banks
-    int i = o % I;
-    for (int k = 0; k < I; ++k) {
-      s = fmaf(w[i], v[i], s);
-      i = i + 1 == I ? 0 : i + 1;
+// Every layer here is tiny (R <= 5 rows, I, O <= 64) and sits on the head's serial chain, so latency rules: an
+// output's dot product is split over a quad of lanes (k = lane&3, +4, ...) and summed with two DPP quad
+// permutations, so one pass costs ~I/4 dependent LDS-fed FMAs instead of I. The weight chunk a quad starts at
+// is rotated by its output index, spreading the quads of a wave over the LDS banks.
+__device__ inline float quad_sum(float s) {
+  s += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s), 0xB1, 0xF, 0xF, false));
+  s += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s), 0x4E, 0xF, 0xF, false));
+  return s;
+}
+
+// sum_k a[k * sa] b[k * sb] over k < K, split over the quad (lane q = threadIdx.x & 3), chunk start rotated by rot
+__device__ inline float quad_dot(const float* a, int sa, const float* b, int sb, int K, int q, int rot) {
+  const int nch = (K + 3) >> 2;
+  int c = rot % nch;
+  float s = 0.f;
+  for (int j = 0; j < nch; ++j) {
+    const int k = 4 * c + q;
+    if (k < K) s = fmaf(a[k * sa], b[k * sb], s);
+    c = c + 1 == nch ? 0 : c + 1;
+  }
+  return quad_sum(s);
+}
+
+// out[r][o] = act(b[o] + sum_i W[o][i] in[r][i]) for r < R, o < O (W row-major [O][I])
+struct LinF {
+  const float* in; int ldi, R, I;
+  const float* W; const float* b; int O;
+  float* out; int ldo; bool relu;
+};
+
+// NL independent layers in one pass (one barrier): layer l's outputs go to the quads following layer l-1's
+template <int NL>
+__device__ void lin_fwd_n(const LinF (&L)[NL]) {
+  const int q = threadIdx.x & 3, nq = blockDim.x >> 2, me = threadIdx.x >> 2;
+  int off = 0;
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const LinF& f = L[l];
+    const int n = f.R * f.O;
+    int idx = me - off;
+    if (idx < 0) idx += nq;
+    for (; idx < n; idx += nq) {
+      const int r = idx / f.O, o = idx - r * f.O;
+      float s = quad_dot(f.W + o * f.I, 1, f.in + r * f.ldi, 1, f.I, q, o);
+      if (q == 0) {
+        if (f.b) s += f.b[o];
+        f.out[r * f.ldo + o] = f.relu ? fmaxf(s, 0.f) : s;
+      }
     }
-    out[(int64_t)r * ldo + o] = relu ? fmaxf(s, 0.f) : s;
+    off = (off + n) % nq;
   }
   __syncthreads();
 }
 
-// dW[o][i] = sum_r dpre[r][o] in[r][i]; db[o] += sum_r dpre[r][o]; din[r][i] (=|+=) sum_o W[o][i] dpre[r][o]
+__device__ void lin_fwd(const float* in, int ldi, int R, int I, const float* W, const float* b, int O, float* out,
+                        int ldo, bool relu) {
+  const LinF L[1] = {{in, ldi, R, I, W, b, O, out, ldo, relu}};
+  lin_fwd_n(L);
+}
+
+// backward of one LinF-shaped layer given dpre = d(pre-activation) [R][O]:
+//   dW[o][i] = sum_r dpre[r][o] in[r][i];  db[o] = sum_r dpre[r][o];
+//   din[r][i] (= | +=) sum_o W[o][i] dpre[r][o], then optionally gated by the producer's ReLU: din = gate > 0 ?
+//   din * gscale : 0 (fuses the relu_gate pass of the layer below)
+struct LinB {
+  const float* dpre; int ldd;
+  const float* in; int ldi, R, I;
+  const float* W; int O;
+  float* dW; float* db;
+  float* din; int lddin; bool acc;
+  const float* gate; int ldg; float gscale;
+};
+
+template <int NL>
+__device__ void lin_bwd_n(const LinB (&L)[NL]) {
+  const int tid = threadIdx.x, q = tid & 3, nq = blockDim.x >> 2, me = tid >> 2;
+  // weight / bias grads: R <= 5 terms each, one thread per element
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const LinB& f = L[l];
+    for (int idx = tid; idx < f.O * f.I; idx += blockDim.x) {
+      const int o = idx / f.I, i = idx - o * f.I;
+      float s = 0.f;
+      for (int r = 0; r < f.R; ++r) s = fmaf(f.dpre[r * f.ldd + o], f.in[r * f.ldi + i], s);
+      f.dW[idx] = s;  // every head slot is produced by exactly one layer call
+    }
+    if (f.db) {
+      for (int o = tid; o < f.O; o += blockDim.x) {
+        float s = 0.f;
+        for (int r = 0; r < f.R; ++r) s += f.dpre[r * f.ldd + o];
+        f.db[o] = s;
+      }
+    }
+  }
+  // input grads: O-long dots, quad-split
+  int off = 0;
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const LinB& f = L[l];
+    if (!f.din) continue;
+    const int n = f.R * f.I;
+    int idx = me - off;
+    if (idx < 0) idx += nq;
+    for (; idx < n; idx += nq) {
+      const int r = idx / f.I, i = idx - r * f.I;
+      const float s = quad_dot(f.W + i, f.I, f.dpre + r * f.ldd, 1, f.O, q, i);
+      if (q == 0) {
+        float* d = f.din + r * f.lddin + i;
+        const float v = f.acc ? *d + s : s;
+        *d = f.gate ? (f.gate[r * f.ldg + i] > 0.f ? v * f.gscale : 0.f) : v;
+      }
+    }
+    off = (off + n) % nq;
+  }
+  __syncthreads();
+}
+
 __device__ void lin_bwd(const float* dpre, int ldd, const float* in, int ldi, int R, int I,
-                        const float* __restrict__ W, int O, float* dW, float* db, float* din, int lddin, bool acc) {
-  for (int idx = threadIdx.x; idx < O * I; idx += blockDim.x) {
-    const int o = idx / I, i = idx - o * I;
-    float s = 0.f;
-    for (int r = 0; r < R; ++r) s = fmaf(dpre[(int64_t)r * ldd + o], in[(int64_t)r * ldi + i], s);
-    dW[idx] = s;  // every head slot is produced by exactly one layer call
-  }
-  if (db) {
-    for (int o = threadIdx.x; o < O; o += blockDim.x) {
-      float s = 0.f;
-      for (int r = 0; r < R; ++r) s += dpre[(int64_t)r * ldd + o];
-      db[o] = s;
-    }
-  }
-  if (din) {
-    for (int idx = threadIdx.x; idx < R * I; idx += blockDim.x) {
-      const int r = idx / I, i = idx - r * I;
-      float s = 0.f;
-      for (int o = 0; o < O; ++o) s = fmaf(W[(int64_t)o * I + i], dpre[(int64_t)r * ldd + o], s);
-      if (acc) din[(int64_t)r * lddin + i] += s;
-      else din[(int64_t)r * lddin + i] = s;
-    }
-  }
-  __syncthreads();
-}
-
-__device__ void relu_gate(float* d, int ldd, const float* out, int ldo, int R, int O, float scale) {
-  for (int idx = threadIdx.x; idx < R * O; idx += blockDim.x) {
-    const int r = idx / O, o = idx - r * O;
-    d[(int64_t)r * ldd + o] = out[(int64_t)r * ldo + o] > 0.f ? d[(int64_t)r * ldd + o] * scale : 0.f;
-  }
-  __syncthreads();
+                        const float* __restrict__ W, int O, float* dW, float* db, float* din, int lddin, bool acc,
+                        const float* gate = nullptr, int ldg = 0, float gscale = 1.f) {
+  const LinB L[1] = {{dpre, ldd, in, ldi, R, I, W, O, dW, db, din, lddin, acc, gate, ldg, gscale}};
+  lin_bwd_n(L);
 }
 
 #define PW(slot) (a.pbase + a.off[slot])
 #define PL(slot) (sW + (a.off[slot] - a.off[H_ENC_W]))  // LDS weight image
 
 // block-wide copy of n4 float4s (dst index remapped by map): every thread issues U loads before its LDS stores,
-// so a copy costs one memory latency per U*blockDim float4s instead of one per blockDim
+// so a copy costs one memory latency per U*blockDim float4s instead of one per blockDim. The loads are
+// unconditional (clamped index): a predicated load makes the compiler wait for the previous one before issuing
+// the next (its destination registers may still be pending), i.e. U serial round trips.
 template <int U, typename Map>
 __device__ void block_copy4(float* dst, const float* src, int n4, Map map) {
+  if (n4 <= 0) return;
   for (int base = 0; base < n4; base += U * (int)blockDim.x) {
     f32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = base + u * (int)blockDim.x + (int)threadIdx.x;
-      if (i < n4) v[u] = reinterpret_cast<const f32x4*>(src)[i];
+      v[u] = reinterpret_cast<const f32x4*>(src)[min(i, n4 - 1)];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -291,6 +364,8 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
   float* w = sw;
   __shared__ int s_N, s_any;
   __shared__ float s_red[4];
+  long long clk[6];
+  clk[0] = __builtin_readcyclecounter();
   const float* Whh = PW(H_GRU_WHH);
   // the n-gate rows of W_hh in LDS (the r / z rows live in registers, below)
   block_copy4<6>(whh, Whh + 2 * GH * GH, GH * GH / 4, [](int i) { return (i >> 4) * (WHH_LD / 4) + (i & 15); });
@@ -318,16 +393,23 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
       float h = 0.f;
       const bool live = nn < N;
       const float br = bhh[u], bz = bhh[GH + u], bn = bhh[2 * GH + u];
-      f32x4 wr[GH / 4], wz[GH / 4];
+      // (W_hr[u][i], W_hz[u][i]) pairs: the r and z dot products advance together in packed FMAs (v_pk_fma_f32,
+      // two fp32 FMAs per lane per instruction -- the step is VALU-bound, two of the five waves share a SIMD)
+      f32x2 wrz[GH];
 #pragma unroll
       for (int kk = 0; kk < GH / 4; ++kk) {
-        wr[kk] = *reinterpret_cast<const f32x4*>(Whh + u * GH + 4 * kk);
-        wz[kk] = *reinterpret_cast<const f32x4*>(Whh + (GH + u) * GH + 4 * kk);
+        const f32x4 r4 = *reinterpret_cast<const f32x4*>(Whh + u * GH + 4 * kk);
+        const f32x4 z4 = *reinterpret_cast<const f32x4*>(Whh + (GH + u) * GH + 4 * kk);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wrz[4 * kk + j] = f32x2{r4[j], z4[j]};
       }
       const f32x4* wn = reinterpret_cast<const f32x4*>(whh + u * WHH_LD);
       const f32x4* hv = reinterpret_cast<const f32x4*>(hs + nn * GH);
       // the input projections are loaded TC steps at a time, one chunk ahead (double-buffered in registers): a
-      // per-step prefetch would be waited for together with the previous step's stores (vmcnt counts both)
+      // per-step prefetch would be waited for together with the previous step's stores (vmcnt counts both, and
+      // with loads and stores both pending the compiler can only wait for zero). The first chunk is waited for
+      // explicitly before the loop: left pending, its registers would be treated as pending at every step of
+      // every chunk (loop-header merge), i.e. one full store round trip per step.
       constexpr int TC = 4;
       float gc[TC][3], gn[TC][3];
       auto load_gi = [&](int t0, float (&g)[TC][3]) {
@@ -341,6 +423,7 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
         }
       };
       if (live) load_gi(0, gc);
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
       for (int t0 = 0; t0 < T; t0 += TC) {
         if (live && t0 + TC < T) load_gi(t0 + TC, gn);
 #pragma unroll
@@ -349,17 +432,22 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
           if (t >= T) break;
           const int64_t row = ((int64_t)b * T + t) * NMAX + nn;
           if (live) {
-            float ar = br, az = bz, an = bn;
+            f32x2 rz0 = {br, bz}, rz1 = {0.f, 0.f}, n0 = {bn, 0.f}, n1 = {0.f, 0.f};
 #pragma unroll
             for (int kk = 0; kk < GH / 4; ++kk) {
-              const f32x4 x = hv[kk], a0 = wr[kk], a1 = wz[kk], a2 = wn[kk];
-              ar = fmaf(a0[0], x[0], ar); ar = fmaf(a0[1], x[1], ar); ar = fmaf(a0[2], x[2], ar); ar = fmaf(a0[3], x[3], ar);
-              az = fmaf(a1[0], x[0], az); az = fmaf(a1[1], x[1], az); az = fmaf(a1[2], x[2], az); az = fmaf(a1[3], x[3], az);
-              an = fmaf(a2[0], x[0], an); an = fmaf(a2[1], x[1], an); an = fmaf(a2[2], x[2], an); an = fmaf(a2[3], x[3], an);
+              const f32x4 x = hv[kk], a2 = wn[kk];
+              rz0 = __builtin_elementwise_fma(wrz[4 * kk], f32x2{x[0], x[0]}, rz0);
+              rz1 = __builtin_elementwise_fma(wrz[4 * kk + 1], f32x2{x[1], x[1]}, rz1);
+              rz0 = __builtin_elementwise_fma(wrz[4 * kk + 2], f32x2{x[2], x[2]}, rz0);
+              rz1 = __builtin_elementwise_fma(wrz[4 * kk + 3], f32x2{x[3], x[3]}, rz1);
+              n0 = __builtin_elementwise_fma(f32x2{a2[0], a2[1]}, f32x2{x[0], x[1]}, n0);
+              n1 = __builtin_elementwise_fma(f32x2{a2[2], a2[3]}, f32x2{x[2], x[3]}, n1);
             }
-            const float r = sigmoidf_(gc[k][0] + ar);
-            const float z = sigmoidf_(gc[k][1] + az);
-            const float nv = tanhf(gc[k][2] + r * an);
+            const f32x2 rz = rz0 + rz1, nn2 = n0 + n1;
+            const float an = nn2[0] + nn2[1];
+            const float r = gate_sigmoid(gc[k][0] + rz[0]);
+            const float z = gate_sigmoid(gc[k][1] + rz[1]);
+            const float nv = gate_tanh(gc[k][2] + r * an);
             rows[RL.r + row * GH + u] = r;
             rows[RL.z + row * GH + u] = z;
             rows[RL.n + row * GH + u] = nv;
@@ -388,15 +476,20 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
     }
   }
   __syncthreads();  // W_hh is dead: its LDS now takes the MLP weight image
+  clk[1] = __builtin_readcyclecounter();
   stage_head_weights(a, sW);
   for (int i = tid; i < NMAX * GH; i += HT) w[L.hT + i] = hs[i];
   __syncthreads();
+  clk[2] = __builtin_readcyclecounter();
   // encoder + VAE (cad:299, 333-352)
   lin_fwd(w + L.hT, GH, N, GH, PL(H_ENC_W), PL(H_ENC_B), 32, w + L.enc, 32, false);
   lin_fwd(w + L.enc, 32, N, 32, PL(H_CE0_W), PL(H_CE0_B), 32, w + L.ce1, 32, true);
   lin_fwd(w + L.ce1, 32, N, 32, PL(H_CE2_W), PL(H_CE2_B), 32, w + L.ce2, 32, true);
-  lin_fwd(w + L.ce2, 32, N, 32, PL(H_MU_W), PL(H_MU_B), NF_, w + L.mu, NF_, false);
-  lin_fwd(w + L.ce2, 32, N, 32, PL(H_LV_W), PL(H_LV_B), NF_, w + L.lv, NF_, false);
+  {
+    const LinF V[2] = {{w + L.ce2, 32, N, 32, PL(H_MU_W), PL(H_MU_B), NF_, w + L.mu, NF_, false},
+                       {w + L.ce2, 32, N, 32, PL(H_LV_W), PL(H_LV_B), NF_, w + L.lv, NF_, false}};
+    lin_fwd_n(V);
+  }
   if (tid < N * NF_) {
     const int nn = tid / NF_, f = tid - nn * NF_;
     const float eps = rng_normal(a.h1_eps, (uint64_t)(a.clip0 + b), (uint64_t)(nn * NF_ + f));
@@ -416,6 +509,7 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
     s = wave_sum(s);
     if (tid == 0) s_red[0] = s / (float)N;
   }
+  clk[3] = __builtin_readcyclecounter();
   // structure learner (cad:371-398)
   lin_fwd(w + L.zz, NF_, N, NF_, PL(H_NODE_W), PL(H_NODE_B), 32, w + L.node, 32, false);
   const int m = min(N, NF_);
@@ -460,6 +554,7 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
   lin_fwd(w + L.s, NF_, N, NF_, PL(H_DYN0_W), PL(H_DYN0_B), 32, w + L.d1, 32, true);
   lin_fwd(w + L.d1, 32, N, 32, PL(H_DYN2_W), PL(H_DYN2_B), 32, w + L.d2, 32, true);
   lin_fwd(w + L.d2, 32, N, 32, PL(H_DYN4_W), PL(H_DYN4_B), NF_, w + L.pred, NF_, false);
+  clk[4] = __builtin_readcyclecounter();
   // scorer (cad:463-502)
   float* cin = w + L.cin;
   if (tid < NF_) {
@@ -477,20 +572,28 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
     cin[12 + tid] = fabsf(c - p);
   }
   __syncthreads();
-  lin_fwd(cin, 18, 1, 18, PL(H_CS0_W), PL(H_CS0_B), 64, w + L.cs1, 64, true);
+  // the three scorers are independent: one pass (and barrier) per depth
+  {
+    const LinF S0[3] = {{cin, 18, 1, 18, PL(H_CS0_W), PL(H_CS0_B), 64, w + L.cs1, 64, true},
+                        {cin, 18, 1, 12, PL(H_MS0_W), PL(H_MS0_B), 32, w + L.ms1, 32, true},
+                        {cin, 18, 1, 6, PL(H_TS0_W), PL(H_TS0_B), 32, w + L.ts1, 32, true}};
+    lin_fwd_n(S0);
+  }
   if (a.training && tid < 64) {
     const bool keep = rng_u24(a.h1_drop, (uint64_t)(a.clip0 + b), (uint64_t)tid) >= a.thr_drop;
     w[L.cs1 + tid] = keep ? w[L.cs1 + tid] * (1.0f / 0.8f) : 0.f;
   }
   __syncthreads();
-  lin_fwd(w + L.cs1, 64, 1, 64, PL(H_CS3_W), PL(H_CS3_B), 32, w + L.cs2, 32, true);
-  lin_fwd(w + L.cs2, 32, 1, 32, PL(H_CS5_W), PL(H_CS5_B), 1, w + L.cs, 1, false);
-  lin_fwd(cin, 18, 1, 12, PL(H_MS0_W), PL(H_MS0_B), 32, w + L.ms1, 32, true);
-  lin_fwd(w + L.ms1, 32, 1, 32, PL(H_MS2_W), PL(H_MS2_B), 16, w + L.ms2, 16, true);
-  lin_fwd(w + L.ms2, 16, 1, 16, PL(H_MS4_W), PL(H_MS4_B), 1, w + L.ms, 1, false);
-  lin_fwd(cin, 18, 1, 6, PL(H_TS0_W), PL(H_TS0_B), 32, w + L.ts1, 32, true);
-  lin_fwd(w + L.ts1, 32, 1, 32, PL(H_TS2_W), PL(H_TS2_B), 16, w + L.ts2, 16, true);
-  lin_fwd(w + L.ts2, 16, 1, 16, PL(H_TS4_W), PL(H_TS4_B), 1, w + L.ts, 1, false);
+  {
+    const LinF S1[3] = {{w + L.cs1, 64, 1, 64, PL(H_CS3_W), PL(H_CS3_B), 32, w + L.cs2, 32, true},
+                        {w + L.ms1, 32, 1, 32, PL(H_MS2_W), PL(H_MS2_B), 16, w + L.ms2, 16, true},
+                        {w + L.ts1, 32, 1, 32, PL(H_TS2_W), PL(H_TS2_B), 16, w + L.ts2, 16, true}};
+    lin_fwd_n(S1);
+    const LinF S2[3] = {{w + L.cs2, 32, 1, 32, PL(H_CS5_W), PL(H_CS5_B), 1, w + L.cs, 1, false},
+                        {w + L.ms2, 16, 1, 16, PL(H_MS4_W), PL(H_MS4_B), 1, w + L.ms, 1, false},
+                        {w + L.ts2, 16, 1, 16, PL(H_TS4_W), PL(H_TS4_B), 1, w + L.ts, 1, false}};
+    lin_fwd_n(S2);
+  }
   if (tid == 0) {
     const float cs = sigmoidf_(w[L.cs]), ms = sigmoidf_(w[L.ms]), ts = sigmoidf_(w[L.ts]);
     w[L.cs + 1] = cs; w[L.ms + 1] = ms; w[L.ts + 1] = ts;
@@ -505,6 +608,10 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
   __syncthreads();
   // hand the activations to the backward kernel
   block_copy4<3>(wg, sw, HL_HANDOFF / 4, Ident{});
+  clk[5] = __builtin_readcyclecounter();
+  if (a.dbg && b == 0 && tid == 0)
+    printf("head_seq_fwd cycles: gru %lld, stage %lld, enc+vae %lld, struct+dyn %lld, scorer+out %lld\n",
+           clk[1] - clk[0], clk[2] - clk[1], clk[3] - clk[2], clk[4] - clk[3], clk[5] - clk[4]);
 }
 
 int head_fwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, hipStream_t st) {
@@ -515,6 +622,8 @@ int head_fwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, hipSt
   VAD_LAUNCH_CHECK();
   return 0;
 }
+
+int g_head_dbg = 0;
 
 // ================================================================== backward
 #define GW(slot) (g + (a.off[slot] - a.head_begin))
@@ -555,27 +664,33 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
       d1[2] = 0.2f * dscore * ts * (1.f - ts);
     }
     __syncthreads();
+    // the three scorers are independent: one pass per depth, the ReLU gates fused into the input grads; their
+    // d cin parts land in separate rows and are summed in the reference's order (cs, ms, ts) below
     float* dcs2 = d1 + 8;
     float* dcs1 = d1 + 40;
-    lin_bwd(d1 + 0, 1, w + L.cs2, 32, 1, 32, PL(H_CS5_W), 1, GW(H_CS5_W), GW(H_CS5_B), dcs2, 32, false);
-    relu_gate(dcs2, 32, w + L.cs2, 32, 1, 32, 1.f);
-    lin_bwd(dcs2, 32, w + L.cs1, 64, 1, 64, PL(H_CS3_W), 32, GW(H_CS3_W), GW(H_CS3_B), dcs1, 64, false);
-    relu_gate(dcs1, 64, w + L.cs1, 64, 1, 64, a.training ? 1.f / 0.8f : 1.f);
-    lin_bwd(dcs1, 64, cin, 18, 1, 18, PL(H_CS0_W), 64, GW(H_CS0_W), GW(H_CS0_B), dcin, 18, true);
     float* dms2 = d1 + 104;
     float* dms1 = d1 + 120;
-    lin_bwd(d1 + 1, 1, w + L.ms2, 16, 1, 16, PL(H_MS4_W), 1, GW(H_MS4_W), GW(H_MS4_B), dms2, 16, false);
-    relu_gate(dms2, 16, w + L.ms2, 16, 1, 16, 1.f);
-    lin_bwd(dms2, 16, w + L.ms1, 32, 1, 32, PL(H_MS2_W), 16, GW(H_MS2_W), GW(H_MS2_B), dms1, 32, false);
-    relu_gate(dms1, 32, w + L.ms1, 32, 1, 32, 1.f);
-    lin_bwd(dms1, 32, cin, 18, 1, 12, PL(H_MS0_W), 32, GW(H_MS0_W), GW(H_MS0_B), dcin, 18, true);
     float* dts2 = d1 + 152;
     float* dts1 = d1 + 168;
-    lin_bwd(d1 + 2, 1, w + L.ts2, 16, 1, 16, PL(H_TS4_W), 1, GW(H_TS4_W), GW(H_TS4_B), dts2, 16, false);
-    relu_gate(dts2, 16, w + L.ts2, 16, 1, 16, 1.f);
-    lin_bwd(dts2, 16, w + L.ts1, 32, 1, 32, PL(H_TS2_W), 16, GW(H_TS2_W), GW(H_TS2_B), dts1, 32, false);
-    relu_gate(dts1, 32, w + L.ts1, 32, 1, 32, 1.f);
-    lin_bwd(dts1, 32, cin, 18, 1, 6, PL(H_TS0_W), 32, GW(H_TS0_W), GW(H_TS0_B), dcin, 18, true);
+    float* dcin3 = d1 + 200;  // [3][18]: d cin from cs / ms / ts
+    const LinB S2[3] = {
+        {d1 + 0, 1, w + L.cs2, 32, 1, 32, PL(H_CS5_W), 1, GW(H_CS5_W), GW(H_CS5_B), dcs2, 32, false, w + L.cs2, 32, 1.f},
+        {d1 + 1, 1, w + L.ms2, 16, 1, 16, PL(H_MS4_W), 1, GW(H_MS4_W), GW(H_MS4_B), dms2, 16, false, w + L.ms2, 16, 1.f},
+        {d1 + 2, 1, w + L.ts2, 16, 1, 16, PL(H_TS4_W), 1, GW(H_TS4_W), GW(H_TS4_B), dts2, 16, false, w + L.ts2, 16, 1.f}};
+    lin_bwd_n(S2);
+    const float sdrop = a.training ? 1.f / 0.8f : 1.f;
+    const LinB S1[3] = {
+        {dcs2, 32, w + L.cs1, 64, 1, 64, PL(H_CS3_W), 32, GW(H_CS3_W), GW(H_CS3_B), dcs1, 64, false, w + L.cs1, 64, sdrop},
+        {dms2, 16, w + L.ms1, 32, 1, 32, PL(H_MS2_W), 16, GW(H_MS2_W), GW(H_MS2_B), dms1, 32, false, w + L.ms1, 32, 1.f},
+        {dts2, 16, w + L.ts1, 32, 1, 32, PL(H_TS2_W), 16, GW(H_TS2_W), GW(H_TS2_B), dts1, 32, false, w + L.ts1, 32, 1.f}};
+    lin_bwd_n(S1);
+    const LinB S0[3] = {
+        {dcs1, 64, cin, 18, 1, 18, PL(H_CS0_W), 64, GW(H_CS0_W), GW(H_CS0_B), dcin3, 18, false, nullptr, 0, 1.f},
+        {dms1, 32, cin, 18, 1, 12, PL(H_MS0_W), 32, GW(H_MS0_W), GW(H_MS0_B), dcin3 + 18, 18, false, nullptr, 0, 1.f},
+        {dts1, 32, cin, 18, 1, 6, PL(H_TS0_W), 32, GW(H_TS0_W), GW(H_TS0_B), dcin3 + 36, 18, false, nullptr, 0, 1.f}};
+    lin_bwd_n(S0);
+    if (tid < 18) dcin[tid] = (dcin3[tid] + (tid < 12 ? dcin3[18 + tid] : 0.f)) + (tid < 6 ? dcin3[36 + tid] : 0.f);
+    __syncthreads();
   }
   float* dz = w + L.dz;
   float* dpred = w + L.dpred;
@@ -595,10 +710,9 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
   {
     float* dd2 = d1;
     float* dd1 = d1 + NMAX * 32;
-    lin_bwd(dpred, NF_, w + L.d2, 32, N, 32, PL(H_DYN4_W), NF_, GW(H_DYN4_W), GW(H_DYN4_B), dd2, 32, false);
-    relu_gate(dd2, 32, w + L.d2, 32, N, 32, 1.f);
-    lin_bwd(dd2, 32, w + L.d1, 32, N, 32, PL(H_DYN2_W), 32, GW(H_DYN2_W), GW(H_DYN2_B), dd1, 32, false);
-    relu_gate(dd1, 32, w + L.d1, 32, N, 32, 1.f);
+    lin_bwd(dpred, NF_, w + L.d2, 32, N, 32, PL(H_DYN4_W), NF_, GW(H_DYN4_W), GW(H_DYN4_B), dd2, 32, false,
+            w + L.d2, 32);
+    lin_bwd(dd2, 32, w + L.d1, 32, N, 32, PL(H_DYN2_W), 32, GW(H_DYN2_W), GW(H_DYN2_B), dd1, 32, false, w + L.d1, 32);
     lin_bwd(dd1, 32, w + L.s, NF_, N, NF_, PL(H_DYN0_W), 32, GW(H_DYN0_W), GW(H_DYN0_B), ds, NF_, false);
   }
   float* dA = w + L.dA;
@@ -696,10 +810,8 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
     float* dce2 = d1 + 64;
     float* dce1 = d1 + 256;
     lin_bwd(dmu, NF_, w + L.ce2, 32, N, 32, PL(H_MU_W), NF_, GW(H_MU_W), GW(H_MU_B), dce2, 32, false);
-    lin_bwd(dlv, NF_, w + L.ce2, 32, N, 32, PL(H_LV_W), NF_, GW(H_LV_W), GW(H_LV_B), dce2, 32, true);
-    relu_gate(dce2, 32, w + L.ce2, 32, N, 32, 1.f);
-    lin_bwd(dce2, 32, w + L.ce1, 32, N, 32, PL(H_CE2_W), 32, GW(H_CE2_W), GW(H_CE2_B), dce1, 32, false);
-    relu_gate(dce1, 32, w + L.ce1, 32, N, 32, 1.f);
+    lin_bwd(dlv, NF_, w + L.ce2, 32, N, 32, PL(H_LV_W), NF_, GW(H_LV_W), GW(H_LV_B), dce2, 32, true, w + L.ce2, 32);
+    lin_bwd(dce2, 32, w + L.ce1, 32, N, 32, PL(H_CE2_W), 32, GW(H_CE2_W), GW(H_CE2_B), dce1, 32, false, w + L.ce1, 32);
     float* denc = d1 + 448;
     lin_bwd(dce1, 32, w + L.enc, 32, N, 32, PL(H_CE0_W), 32, GW(H_CE0_W), GW(H_CE0_B), denc, 32, false);
     lin_bwd(denc, 32, w + L.hT, GH, N, GH, PL(H_ENC_W), 32, GW(H_ENC_W), GW(H_ENC_B), w + L.dh, GH, false);
@@ -717,9 +829,9 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
     const int nn = tid >> 6, u = tid & 63;
     if (nn < NMAX) {
       const bool live = nn < N;
-      float wc[G3];
+      f32x2 wc[G3 / 2];  // (W_hh[2p][u], W_hh[2p+1][u]): packed FMAs, two partial-sum chains (see the forward)
 #pragma unroll
-      for (int q = 0; q < G3; ++q) wc[q] = Whh[q * GH + u];
+      for (int q = 0; q < G3 / 2; ++q) wc[q] = f32x2{Whh[2 * q * GH + u], Whh[(2 * q + 1) * GH + u]};
       float d = live ? dh[nn * GH + u] : 0.f;
       float* dgv = dgh_s + nn * G3;
       // the saved gates are loaded TC steps at a time, one chunk ahead (double-buffered in registers; see the
@@ -739,6 +851,7 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
         }
       };
       if (live) load_gates(T - 1, sc_);
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see the forward recurrence
       for (int t0 = T - 1; t0 >= 0; t0 -= TC) {
         if (live && t0 - TC >= 0) load_gates(t0 - TC, sn_);
 #pragma unroll
@@ -762,17 +875,16 @@ __global__ __launch_bounds__(HT) void head_seq_bwd_kernel(HeadArgs a, HeadOut o,
             dgv[2 * GH + u] = dan * r;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            float s = d * z;
+            f32x2 s0 = {d * z, 0.f}, s1 = {0.f, 0.f};
             const f32x4* dg4 = reinterpret_cast<const f32x4*>(dgv);
 #pragma unroll
             for (int q4 = 0; q4 < G3 / 4; ++q4) {
               const f32x4 g = dg4[q4];
-              s = fmaf(wc[4 * q4], g[0], s);
-              s = fmaf(wc[4 * q4 + 1], g[1], s);
-              s = fmaf(wc[4 * q4 + 2], g[2], s);
-              s = fmaf(wc[4 * q4 + 3], g[3], s);
+              s0 = __builtin_elementwise_fma(wc[2 * q4], f32x2{g[0], g[1]}, s0);
+              s1 = __builtin_elementwise_fma(wc[2 * q4 + 1], f32x2{g[2], g[3]}, s1);
             }
-            d = s;
+            const f32x2 s2 = s0 + s1;
+            d = s2[0] + s2[1];
           } else {
             dgi[u] = 0.f; dgi[GH + u] = 0.f; dgi[2 * GH + u] = 0.f;
             dgh[u] = 0.f; dgh[GH + u] = 0.f; dgh[2 * GH + u] = 0.f;
