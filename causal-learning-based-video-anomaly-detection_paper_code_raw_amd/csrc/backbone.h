@@ -94,6 +94,16 @@ struct ConvPrecision {
   explicit ConvPrecision(int bf16) : saved(g_conv_bf16) { g_conv_bf16 = bf16; }
   ~ConvPrecision() { g_conv_bf16 = saved; }
 };
+// bf16 activation storage (common.h ActT): the stem's pooled map, the raw conv outputs y, dA and dY hold bf16 (the
+// float* arguments of the launchers below then point at bf16 data). Only with g_conv_bf16 (the split kernels'
+// bf16 instantiations read and write it); BN statistics, partial sums, weights and grads stay fp32. Thread-local,
+// set per plan call by ActStorage.
+extern thread_local int g_act_bf16;
+struct ActStorage {
+  int saved;
+  explicit ActStorage(int bf16) : saved(g_act_bf16) { g_act_bf16 = bf16; }
+  ~ActStorage() { g_act_bf16 = saved; }
+};
 bool conv3_x3_supported(const Conv3Layer& L, bool fwd);
 int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
                  float* y, float* partials, int* nparts, hipStream_t st);
@@ -116,6 +126,9 @@ int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, co
 // which kernel family conv3_fwd (kind 0) / conv3_dgrad (1) / conv3_wgrad (2) dispatches to for this layer under the
 // current knobs: 6 = split-bf16 (six bf16 products per K step), 1 = bf16 operands, 0 = f32 MFMA kernels
 int conv3_path(const Conv3Layer& L, int kind);
+// every pass of this layer (forward, input gradient when dgrad, weight gradient) runs on a split kernel under the
+// current knobs, i.e. can take bf16 activations
+bool conv3_act_bf16_ok(const Conv3Layer& L, bool dgrad);
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
                 int* nsplit, int64_t partial_cap, hipStream_t st);
 int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, const float* bias_partials,

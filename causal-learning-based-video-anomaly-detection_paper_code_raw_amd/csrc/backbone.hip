@@ -251,6 +251,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
 
 int maxpool3s2_bwd(const float* y, const float* stats, const float* dpool, int NF, int H, int W, int C, int OH,
                    int OW, float* dA, hipStream_t st) {
+  VAD_CHECK(!g_act_bf16, "stem: the unfused stem keeps fp32 activations");
   VAD_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && C % 4 == 0, "maxpool_bwd: bad dims");
   const int64_t total = (int64_t)NF * H * W * (C / 4);
   const int grid = (int)std::min<int64_t>(cdiv(total, 256), 16384);
@@ -261,6 +262,7 @@ int maxpool3s2_bwd(const float* y, const float* stats, const float* dpool, int N
 
 int conv1_fwd(const float* x, int NF, int H, int W, const float* w, const float* b, float* y, int OH, int OW,
               float* partials, int* nparts, hipStream_t st) {
+  VAD_CHECK(!g_act_bf16, "stem: the unfused stem keeps fp32 activations");
   VAD_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1, "conv1: bad output dims");
   const int bands = (int)cdiv(OH, C1_RB);
   const size_t lds = (size_t)(2 * C1_RB + 5) * (2 * OW + 6) * sizeof(float);
@@ -413,7 +415,9 @@ __device__ inline void bn_block_reduce_store(float (&v)[2][4], int C, float* out
   }
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ dA, const float* __restrict__ y,
+template <bool AB>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const act_t<AB>* __restrict__ dA,
+                                                            const act_t<AB>* __restrict__ y,
                                                             const float* __restrict__ stats, int M, int C,
                                                             float* __restrict__ partials, int BN_ROWS) {
   const int nq = C / 4, groups = 256 / nq;
@@ -427,8 +431,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
   const int r0 = blockIdx.x * BN_ROWS;
   const int r1 = min(M, r0 + BN_ROWS);
   for (int r = r0 + g; r < r1; r += groups) {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(dA + (int64_t)r * C + c);
-    const f32x4 yy = *reinterpret_cast<const f32x4*>(y + (int64_t)r * C + c);
+    const f32x4 a = act_f4(act_ld4(dA + (int64_t)r * C + c));
+    const f32x4 yy = act_f4(act_ld4(y + (int64_t)r * C + c));
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float z = fmaf(yy[e], sc[e], sh[e]);
@@ -444,7 +448,12 @@ int bn_bwd_reduce(const float* dA, const float* y, const float* stats, int M, in
                   hipStream_t st) {
   VAD_CHECK(C % 4 == 0 && C <= 1024 && 256 % (C / 4) == 0, "bn_bwd_reduce: unsupported C");
   const int P = bn_rows_parts(M, C);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(P), dim3(256), 0, st, dA, y, stats, M, C, partials, bn_rows(M));
+  if (g_act_bf16)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(P), dim3(256), 0, st, reinterpret_cast<const __bf16*>(dA),
+                       reinterpret_cast<const __bf16*>(y), stats, M, C, partials, bn_rows(M));
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(P), dim3(256), 0, st, dA, y, stats, M, C, partials,
+                       bn_rows(M));
   VAD_LAUNCH_CHECK();
   *nparts = P;
   return 0;
@@ -505,9 +514,11 @@ int bn_bwd_finalize_sums(const double* sums, int C, double count, const float* g
   return 0;
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ dA, const float* __restrict__ y,
+template <bool AB>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const act_t<AB>* __restrict__ dA,
+                                                           const act_t<AB>* __restrict__ y,
                                                            const float* __restrict__ stats, int M, int C,
-                                                           float* __restrict__ dY, float* __restrict__ bparts,
+                                                           act_t<AB>* __restrict__ dY, float* __restrict__ bparts,
                                                            int BN_ROWS) {
   const int nq = C / 4, groups = 256 / nq;
   const int q = threadIdx.x % nq, g = threadIdx.x / nq;
@@ -523,8 +534,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
   const int r0 = blockIdx.x * BN_ROWS;
   const int r1 = min(M, r0 + BN_ROWS);
   for (int r = r0 + g; r < r1; r += groups) {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(dA + (int64_t)r * C + c);
-    const f32x4 yy = *reinterpret_cast<const f32x4*>(y + (int64_t)r * C + c);
+    const f32x4 a = act_f4(act_ld4(dA + (int64_t)r * C + c));
+    const f32x4 yy = act_f4(act_ld4(y + (int64_t)r * C + c));
     f32x4 o;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -534,7 +545,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
       o[e] = k[e] * (dz - mdz[e] - xh * mdzx[e]);
       v[0][e] += o[e];
     }
-    *reinterpret_cast<f32x4*>(dY + (int64_t)r * C + c) = o;
+    act_st4(dY + (int64_t)r * C + c, o);
   }
   if (bparts) bn_block_reduce_store(v, C, bparts + (int64_t)blockIdx.x * 2 * C);
 }
@@ -542,8 +553,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
                  int* nparts, hipStream_t st) {
   const int P = bn_rows_parts(M, C);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(P), dim3(256), 0, st, dA, y, stats, M, C, dY, bias_partials,
-                     bn_rows(M));
+  if (g_act_bf16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(P), dim3(256), 0, st, reinterpret_cast<const __bf16*>(dA),
+                       reinterpret_cast<const __bf16*>(y), stats, M, C, reinterpret_cast<__bf16*>(dY), bias_partials,
+                       bn_rows(M));
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(P), dim3(256), 0, st, dA, y, stats, M, C, dY, bias_partials,
+                       bn_rows(M));
   VAD_LAUNCH_CHECK();
   *nparts = P;
   return 0;
@@ -585,6 +601,7 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const float* __restrict__ 
 
 int maxpool3s2_bnrelu(const float* y, const float* stats, int NF, int H, int W, int C, float* out, int OH, int OW,
                       hipStream_t st) {
+  VAD_CHECK(!g_act_bf16, "stem: the unfused stem keeps fp32 activations");
   VAD_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && C % 4 == 0, "maxpool: bad dims");
   const int64_t total = (int64_t)NF * OH * OW * (C / 4);
   const int grid = (int)std::min<int64_t>(cdiv(total, 256), 8192);
@@ -600,13 +617,15 @@ int maxpool3s2_bnrelu(const float* y, const float* stats, int NF, int H, int W, 
 __device__ inline int ap_start(int i, int in, int out) { return (i * in) / out; }
 __device__ inline int ap_end(int i, int in, int out) { return ((i + 1) * in + out - 1) / out; }
 
-__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restrict__ y, const float* __restrict__ stats,
-                                                          int H, int W, int C, float* __restrict__ feats) {
+template <bool AB>
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const act_t<AB>* __restrict__ y,
+                                                          const float* __restrict__ stats, int H, int W, int C,
+                                                          float* __restrict__ feats) {
   const int img = blockIdx.y;
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   const float sc = stats[2 * C + c], sh = stats[3 * C + c];
-  const float* yi = y + (int64_t)img * H * W * C;
+  const act_t<AB>* yi = y + (int64_t)img * H * W * C;
   {  // one output row i per blockIdx.z: 4x the blocks of a per-image grid, a quarter of the serial sums
     const int i = blockIdx.z;
     const int h0 = ap_start(i, H, 4), h1 = ap_end(i, H, 4);
@@ -615,7 +634,7 @@ __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restric
       const int w0 = ap_start(j, W, 6), w1 = ap_end(j, W, 6);
       float s = 0.f;
       for (int hh = h0; hh < h1; ++hh)
-        for (int ww = w0; ww < w1; ++ww) s += fmaxf(fmaf(yi[((int64_t)hh * W + ww) * C + c], sc, sh), 0.f);
+        for (int ww = w0; ww < w1; ++ww) s += fmaxf(fmaf(act_ld(yi + ((int64_t)hh * W + ww) * C + c), sc, sh), 0.f);
       feats[(int64_t)img * C * 24 + c * 24 + i * 6 + j] = s / (float)((h1 - h0) * (w1 - w0));
     }
   }
@@ -635,8 +654,12 @@ __global__ __launch_bounds__(256) void temporal_mean_kernel(const float* __restr
 
 int avgpool_fwd(const float* y, const float* stats, int B, int T, int H, int W, int C, float* feats, float* pooled,
                 hipStream_t st) {
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((unsigned)cdiv(C, 256), B * T, 4), dim3(256), 0, st, y, stats, H, W,
-                     C, feats);
+  if (g_act_bf16)
+    hipLaunchKernelGGL(avgpool_fwd_kernel<true>, dim3((unsigned)cdiv(C, 256), B * T, 4), dim3(256), 0, st,
+                       reinterpret_cast<const __bf16*>(y), stats, H, W, C, feats);
+  else
+    hipLaunchKernelGGL(avgpool_fwd_kernel<false>, dim3((unsigned)cdiv(C, 256), B * T, 4), dim3(256), 0, st, y, stats,
+                       H, W, C, feats);
   VAD_LAUNCH_CHECK();
   const int64_t total = (int64_t)B * C * 24;
   hipLaunchKernelGGL(temporal_mean_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 1024)), dim3(256), 0,
@@ -645,9 +668,10 @@ int avgpool_fwd(const float* y, const float* stats, int B, int T, int H, int W, 
   return 0;
 }
 
+template <bool AB>
 __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restrict__ dfeat,
                                                           const float* __restrict__ dpooled, int B, int T, int H,
-                                                          int W, int C, float* __restrict__ dA) {
+                                                          int W, int C, act_t<AB>* __restrict__ dA) {
   const int img = blockIdx.y;
   const int b = img / T;
   const int c = blockIdx.x * 256 + threadIdx.x;
@@ -674,15 +698,19 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restric
           s += g[i * 6 + j] / (float)((h1 - h0) * (w1 - w0));
         }
       }
-      dA[(((int64_t)img * H + hh) * W + ww) * C + c] = s;
+      act_st(dA + (((int64_t)img * H + hh) * W + ww) * C + c, s);
     }
   }
 }
 
 int avgpool_bwd(const float* dfeat, const float* dpooled, int B, int T, int H, int W, int C, float* dA,
                 hipStream_t st) {
-  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3((unsigned)cdiv(C, 256), B * T), dim3(256), 0, st, dfeat, dpooled, B, T,
-                     H, W, C, dA);
+  if (g_act_bf16)
+    hipLaunchKernelGGL(avgpool_bwd_kernel<true>, dim3((unsigned)cdiv(C, 256), B * T), dim3(256), 0, st, dfeat, dpooled,
+                       B, T, H, W, C, reinterpret_cast<__bf16*>(dA));
+  else
+    hipLaunchKernelGGL(avgpool_bwd_kernel<false>, dim3((unsigned)cdiv(C, 256), B * T), dim3(256), 0, st, dfeat,
+                       dpooled, B, T, H, W, C, dA);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -1106,8 +1134,10 @@ int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, con
   // (the patch grid may exceed ceil(M/64) BN partial blocks on tiny images: those stay on the GEMM path)
   if (g_tune.patch && conv3_patch_blocks(L.NF, L.OH, L.OW) <= cdiv((int64_t)L.NF * L.OH * L.OW, 64)) {
     if (conv3_x3_supported(L, true)) return conv3_x3_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st);
+    VAD_CHECK(!g_act_bf16, "conv3_fwd: bf16 activations need the split kernels");
     if (conv3_patch_supported(L, true)) return conv3_patch_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st);
   }
+  VAD_CHECK(!g_act_bf16, "conv3_fwd: bf16 activations need the split kernels");
   ConvGeom g{L.NF, L.OH, L.OW, L.stride, L.stride, L.IH, L.IW, L.Ci};
   TapTable taps;
   fwd_taps(taps);
@@ -1143,6 +1173,7 @@ int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX
   // (the split kernel reads the plain Wd layout, which the prep writes exactly when the f32 patch kernel is usable)
   if (g_tune.patch && conv3_patch_supported(L, false) && conv3_x3_dgrad_s2_supported(L))
     return conv3_x3_dgrad_s2(L, dY, wd, dX, st);
+  VAD_CHECK(!g_act_bf16, "conv3_dgrad: bf16 activations need the split kernels");
   if (g_tune.patch && conv3_patch_supported(L, false)) return conv3_patch_dgrad(L, dY, wd, dX, st);
   if (L.stride == 1) {
     ConvGeom g{L.NF, L.IH, L.IW, 1, 1, L.OH, L.OW, L.Co};
@@ -1176,6 +1207,15 @@ int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX
   return 0;
 }
 
+bool conv3_act_bf16_ok(const Conv3Layer& L, bool dgrad) {
+  const bool fwd = g_tune.patch && conv3_patch_blocks(L.NF, L.OH, L.OW) <= cdiv((int64_t)L.NF * L.OH * L.OW, 64) &&
+                   conv3_x3_supported(L, true);
+  const bool dg = !dgrad || (g_tune.patch && (conv3_x3_supported(L, false) ||
+                                              (conv3_patch_supported(L, false) && conv3_x3_dgrad_s2_supported(L))));
+  const bool wg = g_tune.wgrad_patch && conv3_wgrad_x3_supported(L);
+  return fwd && dg && wg;
+}
+
 int conv3_path(const Conv3Layer& L, int kind) {
   bool x3 = false;
   if (kind == 0)
@@ -1192,6 +1232,7 @@ int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const fl
                 int* nsplit, int64_t partial_cap, hipStream_t st) {
   if (g_tune.wgrad_patch && conv3_wgrad_x3_supported(L))
     return conv3_wgrad_x3(L, dY, src, src_stats, partial, nsplit, partial_cap, g_tune.wgrad_patch_blocks, st);
+  VAD_CHECK(!g_act_bf16, "conv3_wgrad: bf16 activations need the split kernels");
   if (g_tune.wgrad_patch && conv3_wgrad_patch_supported(L) && (L.stride == 1 || g_tune.wgrad_patch == 2))
     return conv3_wgrad_patch(L, dY, src, src_stats, partial, nsplit, partial_cap, g_tune.wgrad_patch_blocks, st);
   const int M = L.Co, N = 9 * L.Ci, K = L.NF * L.OH * L.OW;

@@ -599,6 +599,10 @@ struct CadPlanImpl {
   }
 
   int conv_bf16 = 0;  // option "conv_bf16": 3x3 convs on bf16 operands (BASELINE config 4)
+  // option "act_bf16" (default on): with conv_bf16, the backbone activations (pooled stem map, conv outputs y, dA,
+  // dY) are stored as bf16 -- half the bytes of every memory-bound pass. act_bf16: the last forward ran so (the
+  // frozen fused stem and split kernels for every pass are required; the backward follows the forward)
+  int act_bf16_opt = 1, act_bf16 = 0;
   // option "stem_grad": backbone.conv1 / bn1 train (the reference's module without apply_memory_efficient_training);
   // stem_active: the last backward wrote their grads (the fused optimizer then steps them too)
   int stem_grad = 0, stem_active = 0;
@@ -654,6 +658,9 @@ struct CadPlanImpl {
     int np = 0;
     bwd_state = 0;
     y1_fresh = !(g_stem_fused && !stem_grad && stem_fused_ok(W1));
+    act_bf16 = conv_bf16 && act_bf16_opt && !y1_fresh;
+    for (int l = 0; l < 8; ++l) act_bf16 = act_bf16 && conv3_act_bf16_ok(L[l], l > 0);
+    ActStorage abf(act_bf16);
     if (!y1_fresh) {
       // frozen stem (the training default): conv1 + BN sums + pooling of the raw output in one pass (stem.hip);
       // `pool` then holds the pooled conv1 output and layer1.0 applies bn1 + ReLU on load
@@ -748,6 +755,7 @@ struct CadPlanImpl {
   int backward(bool use_loss, const float* dfin, const float* dprobs, const float* dcaus, const float* dkl,
                const float* dz, const float* dadj, hipStream_t st, int stage = -1, const float* dboxes = nullptr) {
     ConvPrecision prec(conv_bf16);
+    ActStorage abf(act_bf16);
     const CadLayout& LY = layout();
     VAD_CHECK(grads != nullptr, "backward: grads not bound");
     VAD_CHECK(!use_loss || labels != nullptr, "backward(use_loss): forward ran without labels");
@@ -1107,6 +1115,7 @@ int vad_cad_debug_buffer(vad_cad_plan* plan, const char* name, int idx, void** p
   else if (n == "pooled") { *ptr = c.pooled; *nfloats = (int64_t)c.B * 6144; }
   else if (n == "dA") { *ptr = c.dA; *nfloats = c.act_max; }
   else if (n == "dY") { *ptr = (c.debug_stop_layer & 1) ? c.dY2 : c.dY; *nfloats = c.act_max; }
+  else if (n == "act_bf16") { *ptr = nullptr; *nfloats = c.act_bf16; }  // storage of pool / y / dA / dY
   else if (n == "d_pooled") { *ptr = c.d_pooled; *nfloats = (int64_t)c.B * 6144; }
   else if (n == "d_feat_det") { *ptr = c.d_feat_det; *nfloats = NF * 6144; }
   else if (n == "det_logits") { *ptr = c.dlog; *nfloats = NF * 20; }
@@ -1127,6 +1136,7 @@ int vad_cad_set_option(vad_cad_plan* plan, const char* key, int64_t value) {
   if (std::string(key) == "conv_bf16") plan->impl.conv_bf16 = value ? 1 : 0;
   else if (std::string(key) == "stem_grad") plan->impl.stem_grad = value ? 1 : 0;
   else if (std::string(key) == "wgrad_stream") plan->impl.wgrad_stream = value ? 1 : 0;
+  else if (std::string(key) == "act_bf16") plan->impl.act_bf16_opt = value ? 1 : 0;
   else { vad::set_error("vad_cad_set_option: unknown key"); return 1; }
   return 0;
 }

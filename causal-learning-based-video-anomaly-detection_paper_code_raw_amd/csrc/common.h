@@ -116,6 +116,40 @@ __device__ inline float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ inline float gate_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ inline float gate_tanh(float x) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x)); }
 
+// ---------------------------------------------------------------- activation storage
+// Backbone activations (raw conv outputs, the pooled stem map) and their gradients are fp32, or bf16 in plans that
+// run the convs on bf16 operands (config 4, CadPlan option conv_bf16): AB selects the element type. Loads keep the
+// raw element vector (act_raw4) until the value is needed, so a prefetch is not waited for at the load.
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+template <bool AB>
+struct ActT {
+  using T = float;
+  using R4 = f32x4;
+};
+template <>
+struct ActT<true> {
+  using T = __bf16;
+  using R4 = bf16x4_t;
+};
+template <bool AB>
+using act_t = typename ActT<AB>::T;
+template <bool AB>
+using act_raw4 = typename ActT<AB>::R4;
+__device__ inline f32x4 act_f4(f32x4 v) { return v; }
+__device__ inline f32x4 act_f4(bf16x4_t v) { return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]}; }
+template <typename T>
+__device__ inline typename ActT<sizeof(T) == 2>::R4 act_ld4(const T* p) {
+  return *reinterpret_cast<const typename ActT<sizeof(T) == 2>::R4*>(p);
+}
+__device__ inline void act_st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ inline void act_st4(__bf16* p, f32x4 v) {
+  *reinterpret_cast<bf16x4_t*>(p) = bf16x4_t{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+}
+__device__ inline float act_ld(const float* p) { return *p; }
+__device__ inline float act_ld(const __bf16* p) { return (float)*p; }
+__device__ inline void act_st(float* p, float v) { *p = v; }
+__device__ inline void act_st(__bf16* p, float v) { *p = (__bf16)v; }
+
 __device__ inline float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

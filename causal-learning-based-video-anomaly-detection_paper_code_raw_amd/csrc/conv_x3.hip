@@ -83,9 +83,14 @@ __device__ __forceinline__ void put_planes(__bf16* d, int pitch, const float* v,
 // most of the staging VALU of the 32-channel layers
 // NW = 8: 512-thread blocks over 256-pixel tiles (one block per CU): the weight slice staged per item serves twice
 // the pixels (the weight staging per MFMA halves) and the halo share of the patch drops
-template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1, int NW = 4>
+// AB: bf16 activation storage (p.src / p.out hold bf16; only with NP == 1)
+template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1, int NW = 4, bool AB = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Args p) {
   static_assert(NP == 3 || NP == 1, "three split planes (fp32 numerics) or one (bf16 operands)");
+  static_assert(!AB || NP == 1, "bf16 storage with bf16 operands only");
+  using TA = act_t<AB>;
+  const TA* src = reinterpret_cast<const TA*>(p.src);
+  TA* out = reinterpret_cast<TA*>(p.out);
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(NI * TH * TW == 32 * NW, "a wave owns 32 output pixels");
   constexpr int NTHR = 64 * NW;
@@ -118,7 +123,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
   constexpr int PQ = PROWS * G8, PIT = (PQ + NTHR - 1) / NTHR;
   constexpr int WQ = NC * 9 * G8, WIT = (WQ + NTHR - 1) / NTHR;
   const int g8 = tid % G8;
-  f32x4 pv[PIT][2], wv[WIT][2];
+  act_raw4<AB> pv[PIT][2];
+  f32x4 wv[WIT][2];
   // prefetch loads are unconditional (out-of-range lanes read a valid dummy address) and the zero padding is applied
   // at stash time from these bits, so no masked-load branch makes the compiler wait for the loads before the MFMAs
   bool pok[PIT], wok[WIT];
@@ -138,10 +144,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
       const int im = row / (PH * PW), rr = row % (PH * PW);
       const int iy = oy0 * S - 1 + rr / PW, ix = ox0 * S - 1 + rr % PW, img = img0 + im;
       pok[it] = !(p.dbg & 8) && q < PQ && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
-      const float* s = p.src + c0 + g8 * 8 +
-                       (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
-      pv[it][0] = *reinterpret_cast<const f32x4*>(s);
-      pv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
+      const TA* s = src + c0 + g8 * 8 + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
+      pv[it][0] = act_ld4(s);
+      pv[it][1] = act_ld4(s + 4);
     }
     if (weights) {
 #pragma unroll
@@ -180,10 +185,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
         const int im = row / (PH * PW), rr = row % (PH * PW);
         const int ry = rr / PW, rx = rr % PW;
         float v[8];
+        const f32x4 v0 = act_f4(pv[it][0]), v1 = act_f4(pv[it][1]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = pok[it] ? pv[it][0][e] : 0.f;
-          v[4 + e] = pok[it] ? pv[it][1][e] : 0.f;
+          v[e] = pok[it] ? v0[e] : 0.f;
+          v[4 + e] = pok[it] ? v1[e] : 0.f;
         }
         if constexpr (FWD) {
           // zero padding stays zero: padded taps read 0 in the reference's zero-padded relu(bn(y))
@@ -284,12 +290,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
         const int qi = pm / (TH * TW), qr = pm % (TH * TW);
         const int oy = oy0 + qr / TW, ox = ox0 + qr % TW, img = img0 + qi;
         if (img < p.NF && oy < p.OH && ox < p.OW) {
-          float* o = p.out + (((int64_t)img * p.OH + oy) * p.OW + ox) * p.N + n0 + j;
+          TA* o = out + (((int64_t)img * p.OH + oy) * p.OW + ox) * p.N + n0 + j;
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) {
             if (n0 + nt * 32 + j < p.N) {
               const float v = acc[nt][r] + bj[nt];
-              o[nt * 32] = v;
+              act_st(o + nt * 32, v);
               if (FWD) {
                 s1[nt] += v;
                 s2[nt] = fmaf(v, v, s2[nt]);
@@ -327,6 +333,7 @@ int g_x3_dgrad_blocks = 512;  // knob "conv_dgrad_blocks"
 
 template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1, int NW = 4>
 static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
+  VAD_CHECK(!g_act_bf16 || NP == 1, "conv3x3_x3: bf16 activations need the bf16-operand kernels (conv_bf16)");
   VAD_CHECK(WCH == 1 || a.C == WCH * PC, "conv3x3_x3: resident weights need C == WCH * PC");
   a.tiles_h = (int)cdiv(a.OH, TH);
   a.tiles_w = (int)cdiv(a.OW, TW);
@@ -339,7 +346,15 @@ static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   a.dbg = g_x3_dbg;
   a.stagger = g_x3_stagger;
   const int gx = (int)cdiv(a.ntiles, a.tpb);
-  VAD_KLAUNCH((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD, NP, WCH, NW>), dim3(gx, ny), dim3(64 * NW), 0, st, a);
+  if constexpr (NP == 1) {
+    if (g_act_bf16)
+      VAD_KLAUNCH((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD, NP, WCH, NW, true>), dim3(gx, ny), dim3(64 * NW), 0,
+                  st, a);
+    else
+      VAD_KLAUNCH((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD, NP, WCH, NW>), dim3(gx, ny), dim3(64 * NW), 0, st, a);
+  } else {
+    VAD_KLAUNCH((conv3x3_x3_kernel<S, NI, TH, TW, NT, PC, FWD, NP, WCH, NW>), dim3(gx, ny), dim3(64 * NW), 0, st, a);
+  }
   VAD_LAUNCH_CHECK();
   if (nparts) *nparts = gx;
   return 0;
@@ -347,6 +362,7 @@ static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
 
 int g_conv_split = 1;  // tuning knob "conv_split": 1 = split-bf16 patch kernels where supported, 0 = f32 MFMA
 thread_local int g_conv_bf16 = 0;  // bf16-operand convs (one plane, one product; set per plan, see ConvPrecision)
+thread_local int g_act_bf16 = 0;   // bf16 activation storage (set per plan, see ActStorage)
 int g_x3_nt = 0;       // tuning knob "conv_split_nt": 0 = auto, 1 / 2 = force 32 / 64 output channels per block
 int g_x3_dbg = 0;      // knob "conv_split_dbg" (measurement only, see X3Args::dbg)
 int g_x3_stagger = 0;  // knob "conv_split_stagger" (see X3Args::stagger)
@@ -468,9 +484,13 @@ __device__ __forceinline__ void dgrad_s2x3_class(f32x16 (&acc)[NT], const __bf16
   }
 }
 
-template <int NT, int PC, int NP>
+template <int NT, int PC, int NP, bool AB = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args p) {
   static_assert(PC % 16 == 0, "16-deep K steps");
+  static_assert(!AB || NP == 1, "bf16 storage with bf16 operands only");
+  using TA = act_t<AB>;
+  const TA* src = reinterpret_cast<const TA*>(p.src);
+  TA* out = reinterpret_cast<TA*>(p.out);
   constexpr int NC = 32 * NT, G8 = PC / 8, PROWS = 81;
   constexpr int RP = NP * PC + 8, WP = 9 * NP * PC + 8;
   static_assert(((RP * 2 / 16) & 1) && ((WP * 2 / 16) & 1), "odd 16-B row pitch");
@@ -491,7 +511,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args
   constexpr int PQ = PROWS * G8, PIT = (PQ + 255) / 256;
   constexpr int WQ = NC * 9 * G8, WIT = (WQ + 255) / 256;
   const int g8 = tid % G8;
-  f32x4 pv[PIT][2], wv[WIT][2];
+  act_raw4<AB> pv[PIT][2];
+  f32x4 wv[WIT][2];
   bool pok[PIT], wok[WIT];
   // unconditional loads from clamped addresses; out-of-range rows are zeroed at stash time (see conv3x3_x3_kernel)
   auto fetch = [&](int c0) {
@@ -500,9 +521,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args
       const int q = tid + it * 256, row = q / G8;
       const int y = i0 + row / 9, x = j0 + row % 9;
       pok[it] = q < PQ && y < p.IH && x < p.IW;
-      const float* s = p.src + c0 + g8 * 8 + (pok[it] ? (((int64_t)img * p.IH + y) * p.IW + x) * p.C : (int64_t)0);
-      pv[it][0] = *reinterpret_cast<const f32x4*>(s);
-      pv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
+      const TA* s = src + c0 + g8 * 8 + (pok[it] ? (((int64_t)img * p.IH + y) * p.IW + x) * p.C : (int64_t)0);
+      pv[it][0] = act_ld4(s);
+      pv[it][1] = act_ld4(s + 4);
     }
 #pragma unroll
     for (int it = 0; it < WIT; ++it) {
@@ -519,10 +540,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args
       const int q = tid + it * 256;
       if (q < PQ) {
         float v[8];
+        const f32x4 v0 = act_f4(pv[it][0]), v1 = act_f4(pv[it][1]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = pok[it] ? pv[it][0][e] : 0.f;
-          v[4 + e] = pok[it] ? pv[it][1][e] : 0.f;
+          v[e] = pok[it] ? v0[e] : 0.f;
+          v[4 + e] = pok[it] ? v1[e] : 0.f;
         }
         put_planes<NP>(patch + (q / G8) * RP + g8 * 8, PC, v, false);
       }
@@ -574,8 +596,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args
     for (int nt = 0; nt < NT; ++nt) {
       const int col = n0 + nt * 32 + j;
       if (col >= p.N) continue;
-      if (y0 < p.OH && x0 < p.OW) p.out[(((int64_t)img * p.OH + y0) * p.OW + x0) * p.N + col] = acc0[nt][r];
-      if (y1 < p.OH && x1 < p.OW) p.out[(((int64_t)img * p.OH + y1) * p.OW + x1) * p.N + col] = acc1[nt][r];
+      if (y0 < p.OH && x0 < p.OW) act_st(out + (((int64_t)img * p.OH + y0) * p.OW + x0) * p.N + col, acc0[nt][r]);
+      if (y1 < p.OH && x1 < p.OW) act_st(out + (((int64_t)img * p.OH + y1) * p.OW + x1) * p.N + col, acc1[nt][r]);
     }
   }
 }
@@ -600,7 +622,11 @@ int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, flo
   // 64 input channels per block where that still gives >= 2 blocks per CU, else 32
   const bool nt2 = L.Ci % 64 == 0 && (int64_t)tiles * (L.Ci / 64) >= 512;
   dim3 grid((unsigned)tiles, (unsigned)(L.Ci / (nt2 ? 64 : 32)));
-  if (g_conv_bf16) {
+  VAD_CHECK(!g_act_bf16 || g_conv_bf16, "conv3_x3_dgrad_s2: bf16 activations need conv_bf16");
+  if (g_conv_bf16 && g_act_bf16) {
+    if (nt2) VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<2, 16, 1, true>), grid, dim3(256), 0, st, a);
+    else VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<1, 16, 1, true>), grid, dim3(256), 0, st, a);
+  } else if (g_conv_bf16) {
     if (nt2) VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<2, 16, 1>), grid, dim3(256), 0, st, a);
     else VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<1, 16, 1>), grid, dim3(256), 0, st, a);
   } else {
@@ -643,8 +669,13 @@ constexpr int odd16_pitch(int n) { return ((n / 8) & 1) ? n : n + 8; }
 __device__ __forceinline__ void wgrad_combine_store(f32x16 (&acc)[9], __bf16* sm, float* out, int co0, int ci0,
                                                     int Ci);
 
-template <int NI, int TH, int TW, bool PF, int NP>
+template <int NI, int TH, int TW, bool PF, int NP, bool AB = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args p) {
+  static_assert(!AB || NP == 1, "bf16 storage with bf16 operands only");
+  using TA = act_t<AB>;
+  using R4 = act_raw4<AB>;
+  const TA* dYp = reinterpret_cast<const TA*>(p.dY);
+  const TA* srcp = reinterpret_cast<const TA*>(p.src);
   constexpr int TPX = NI * TH * TW, KS = TPX / 64;
   static_assert(TPX % 64 == 0 && TW % 8 == 0, "whole 16-pixel K steps per wave, 8-pixel row runs");
   constexpr int PH = TH + 2, PW = TW + 2, PWP = TW + 8, NCG = PWP / 4;
@@ -661,7 +692,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
 
   constexpr int XQ = NI * PH * NCG * 8, XIT = (XQ + 255) / 256;
   constexpr int YQ = TPX / 4 * 8, YIT = (YQ + 255) / 256;
-  f32x4 xv[XIT][4], yv[YIT][4];
+  R4 xv[XIT][4], yv[YIT][4];
   auto origin = [&](int tile, int& i0, int& y0, int& x0) {
     i0 = (tile / tiles_per_img) * NI;
     const int tr = tile % tiles_per_img;
@@ -678,10 +709,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
       const int oy = y0 + mr / TW, ox = x0 + mr % TW, img = i0 + mi;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        yv[it][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+        yv[it][e] = R4{};
         if (!(p.dbg & 8) && q < YQ && img < p.NF && oy < p.OH && ox + e < p.OW)
-          yv[it][e] = *reinterpret_cast<const f32x4*>(p.dY + (((int64_t)img * p.OH + oy) * p.OW + ox + e) * p.Co +
-                                                      co0 + c4 * 4);
+          yv[it][e] = act_ld4(dYp + (((int64_t)img * p.OH + oy) * p.OW + ox + e) * p.Co + co0 + c4 * 4);
       }
     }
 #pragma unroll
@@ -692,10 +722,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int px = cg * 4 + e, ix = x0 - 1 + px;
-        xv[it][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+        xv[it][e] = R4{};
         if (!(p.dbg & 8) && q < XQ && px < PW && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
-          xv[it][e] = *reinterpret_cast<const f32x4*>(p.src + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.Ci +
-                                                      ci0 + c4 * 4);
+          xv[it][e] = act_ld4(srcp + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.Ci + ci0 + c4 * 4);
       }
     }
   };
@@ -738,7 +767,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
 #pragma unroll
     for (int it = 0; it < YIT; ++it) {
       const int q = tid + it * 256;
-      if (q < YQ) put4(ys + (q >> 3) * 4, DYP, TPX, yv[it]);
+      if (q < YQ) {
+        const f32x4 v[4] = {act_f4(yv[it][0]), act_f4(yv[it][1]), act_f4(yv[it][2]), act_f4(yv[it][3])};
+        put4(ys + (q >> 3) * 4, DYP, TPX, v);
+      }
     }
 #pragma unroll
     for (int it = 0; it < XIT; ++it) {
@@ -749,7 +781,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
         f32x4 v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = xv[it][e];
+          v[e] = act_f4(xv[it][e]);
           const int ix = x0 - 1 + cg * 4 + e;
           // zero padding stays zero: padded taps read 0 in the reference's zero-padded relu(bn(y))
           if (p.scale && i0 + mi < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW && cg * 4 + e < PW) {
@@ -865,8 +897,13 @@ __device__ __forceinline__ void wgrad_combine_store(f32x16 (&acc)[9], __bf16* sm
 // 2TW+1 columns incl. halo) is stored parity-split as [E: even patch columns, TW+8 slots][O: odd ones, TW slots];
 // the 8 consecutive output pixels of a lane half need E[ox..ox+7] (kw = 0), O[ox..ox+7] (kw = 1) and E[ox+1..ox+8]
 // (kw = 2, the 2-byte shift): every fragment is an aligned b128 read per plane, no strided LDS access.
-template <int S, int TH, int TW, int NT, int NP>
+template <int S, int TH, int TW, int NT, int NP, bool AB = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Args p) {
+  static_assert(!AB || NP == 1, "bf16 storage with bf16 operands only");
+  using TA = act_t<AB>;
+  using R4 = act_raw4<AB>;
+  const TA* dYp = reinterpret_cast<const TA*>(p.dY);
+  const TA* srcp = reinterpret_cast<const TA*>(p.src);
   constexpr int TPX = TH * TW, NC = 32 * NT, KT = TPX / 16, KSW = KT * NT / 4;
   static_assert((TPX == 32 || TPX == 64) && TW % 8 == 0 && (NT == 2 || NT == 4) && (S == 1 || S == 2),
                 "whole K steps per wave, 8-pixel row runs");
@@ -887,7 +924,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Ar
 
   constexpr int XQ = PH * NCG * 8, XIT = (XQ + 255) / 256;
   static_assert(XIT <= 2, "patch staged in one register pass");
-  f32x4 xv[XIT][4], yv[YIT][4];
+  R4 xv[XIT][4], yv[YIT][4];
   // patch column (0 = input column S*x0 - 1) held by LDS column c of a row
   auto pcol = [](int c) { return S == 1 ? c : (c < EW ? 2 * c : 2 * (c - EW) + 1); };
   auto origin = [&](int tile, int& img, int& y0, int& x0) {
@@ -904,10 +941,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Ar
       const int yp = ((tid + it * 256) / YG) * 4, oy = y0 + yp / TW, ox = x0 + yp % TW;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        yv[it][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+        yv[it][e] = R4{};
         if (!(p.dbg & 8) && tid + it * 256 < YQ && oy < p.OH && ox + e < p.OW)
-          yv[it][e] = *reinterpret_cast<const f32x4*>(p.dY + (((int64_t)img * p.OH + oy) * p.OW + ox + e) * p.Co +
-                                                      co0 + yc * 4);
+          yv[it][e] = act_ld4(dYp + (((int64_t)img * p.OH + oy) * p.OW + ox + e) * p.Co + co0 + yc * 4);
       }
     }
 #pragma unroll
@@ -917,10 +953,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Ar
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int pc = pcol(cg * 4 + e), ix = S * x0 - 1 + pc;
-        xv[it][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+        xv[it][e] = R4{};
         if (!(p.dbg & 8) && q < XQ && pc < PW && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
-          xv[it][e] = *reinterpret_cast<const f32x4*>(p.src + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.Ci + ci0 +
-                                                      c4 * 4);
+          xv[it][e] = act_ld4(srcp + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.Ci + ci0 + c4 * 4);
       }
     }
   };
@@ -962,7 +997,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Ar
     origin(tile, img, y0, x0);
 #pragma unroll
     for (int it = 0; it < YIT; ++it)
-      if (tid + it * 256 < YQ) put4(ys + yc * 4 * DYP + ((tid + it * 256) / YG) * 4, DYP, TPX, yv[it]);
+      if (tid + it * 256 < YQ) {
+        const f32x4 v[4] = {act_f4(yv[it][0]), act_f4(yv[it][1]), act_f4(yv[it][2]), act_f4(yv[it][3])};
+        put4(ys + yc * 4 * DYP + ((tid + it * 256) / YG) * 4, DYP, TPX, v);
+      }
 #pragma unroll
     for (int it = 0; it < XIT; ++it) {
       const int q = tid + it * 256, g = q >> 3;
@@ -971,7 +1009,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Ar
         f32x4 v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = xv[it][e];
+          v[e] = act_f4(xv[it][e]);
           const int pc = pcol(cg * 4 + e), ix = S * x0 - 1 + pc;
           // zero padding stays zero (the reference pads relu(bn(y)) with zeros)
           if (p.scale && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW && pc < PW) {
@@ -1077,7 +1115,9 @@ static int launch_wgrad_x3(WgX3Args a, int target_blocks, int64_t partial_cap, h
   int64_t z = std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, pairs), a.ntiles));
   z = std::min<int64_t>(z, std::max<int64_t>(1, partial_cap / ((int64_t)a.Co * 9 * a.Ci)));
   dim3 grid((unsigned)(a.Co / 32), (unsigned)(a.Ci / 32), (unsigned)z);
-  if (g_conv_bf16) VAD_KLAUNCH((conv3x3_wgrad_x3_kernel<NI, TH, TW, PF, 1>), grid, dim3(256), 0, st, a);
+  VAD_CHECK(!g_act_bf16 || g_conv_bf16, "conv3_wgrad_x3: bf16 activations need conv_bf16");
+  if (g_conv_bf16 && g_act_bf16) VAD_KLAUNCH((conv3x3_wgrad_x3_kernel<NI, TH, TW, PF, 1, true>), grid, dim3(256), 0, st, a);
+  else if (g_conv_bf16) VAD_KLAUNCH((conv3x3_wgrad_x3_kernel<NI, TH, TW, PF, 1>), grid, dim3(256), 0, st, a);
   else VAD_KLAUNCH((conv3x3_wgrad_x3_kernel<NI, TH, TW, PF, 3>), grid, dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   *nsplit = (int)z;
@@ -1093,7 +1133,9 @@ static int launch_wgrad_x3nt(WgX3Args a, int target_blocks, int64_t partial_cap,
   int64_t z = std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, pairs), a.ntiles));
   z = std::min<int64_t>(z, std::max<int64_t>(1, partial_cap / ((int64_t)a.Co * 9 * a.Ci)));
   dim3 grid((unsigned)(a.Co / (32 * NT)), (unsigned)(a.Ci / 32), (unsigned)z);
-  if (g_conv_bf16) VAD_KLAUNCH((conv3x3_wgrad_x3nt_kernel<S, TH, TW, NT, 1>), grid, dim3(256), 0, st, a);
+  VAD_CHECK(!g_act_bf16 || g_conv_bf16, "conv3_wgrad_x3: bf16 activations need conv_bf16");
+  if (g_conv_bf16 && g_act_bf16) VAD_KLAUNCH((conv3x3_wgrad_x3nt_kernel<S, TH, TW, NT, 1, true>), grid, dim3(256), 0, st, a);
+  else if (g_conv_bf16) VAD_KLAUNCH((conv3x3_wgrad_x3nt_kernel<S, TH, TW, NT, 1>), grid, dim3(256), 0, st, a);
   else VAD_KLAUNCH((conv3x3_wgrad_x3nt_kernel<S, TH, TW, NT, 3>), grid, dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   *nsplit = (int)z;

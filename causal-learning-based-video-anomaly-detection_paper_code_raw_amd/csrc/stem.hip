@@ -116,8 +116,9 @@ __device__ __forceinline__ void stem_store(const R& r, int rows, int PWb, __bf16
 constexpr int ST_PB = 3;
 constexpr int ST_SLOTS = 12;  // input staging register slots: (2 * (2 * ST_PB + 1) + 6) rows * PWb / 2 <= 12 * 256
 
-// NP = 3: split-bf16 operands (fp32 numerics, the default); NP = 1: bf16 operands (conv_bf16, BASELINE config 4)
-template <int NP>
+// NP = 3: split-bf16 operands (fp32 numerics, the default); NP = 1: bf16 operands (conv_bf16, BASELINE config 4);
+// AB: the pooled map is stored as bf16 (bf16 activation storage)
+template <int NP, bool AB = false>
 __global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restrict__ x, int H, int W,
                                                             const float* __restrict__ w,
                                                             const float* __restrict__ bias,
@@ -228,9 +229,9 @@ __global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restr
     for (int e = 0; e < 4; ++e) sg[e] = gamma[c + e] < 0.f ? -1.f : 1.f;
     for (int pyl = 0; pyl < py1 - py0; ++pyl) {
       const f32x4* src = reinterpret_cast<const f32x4*>(hpool + pyl * WP * C);
-      f32x4* dst = reinterpret_cast<f32x4*>(pool + ((int64_t)img * HP + py0 + pyl) * WP * C);
+      act_t<AB>* dst = reinterpret_cast<act_t<AB>*>(pool) + ((int64_t)img * HP + py0 + pyl) * WP * C;
       if (!(dbg & 8))
-        for (int q = threadIdx.x; q < WP * (C / 4); q += blockDim.x) dst[q] = src[q] * sg;
+        for (int q = threadIdx.x; q < WP * (C / 4); q += blockDim.x) act_st4(dst + 4 * q, src[q] * sg);
     }
   }
   s1 += __shfl_xor(s1, 32, 64);
@@ -274,7 +275,11 @@ int stem_fused(const float* x, int NF, int H, int W, const float* w, const float
   const int nbands = (int)cdiv(HP, ST_PB);
   // (the partial rows fit the conv1_fwd layout: ceil(ceil(OH/2)/3) == ceil(OH/6))
   VAD_CHECK(nbands == (int)cdiv(OH, 6) && (int64_t)NF * nbands == conv1_num_parts(NF, OH), "stem_fused: partials");
-  if (g_conv_bf16)
+  VAD_CHECK(!g_act_bf16 || g_conv_bf16, "stem_fused: bf16 activations need conv_bf16");
+  if (g_conv_bf16 && g_act_bf16)
+    VAD_KLAUNCH((stem_fused_kernel<1, true>), dim3(NF * nbands), dim3(256), stem_lds(OW), st, x, H, W, w, b, gamma, OH,
+                OW, HP, WP, nbands, stem_pitch(OW), pool, partials, g_stem_dbg);
+  else if (g_conv_bf16)
     VAD_KLAUNCH(stem_fused_kernel<1>, dim3(NF * nbands), dim3(256), stem_lds(OW), st, x, H, W, w, b, gamma, OH, OW,
                 HP, WP, nbands, stem_pitch(OW), pool, partials, g_stem_dbg);
   else

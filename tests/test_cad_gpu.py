@@ -287,9 +287,11 @@ def test_fused_stem_matches_float64_stem(B, T, H, W):
 def test_config4_shape_fp32_and_bf16(B, T, H, W):
     """BASELINE config 4 shape (T=32, 256x256; 2 clips per rank here to bound the oracle's CPU time).
     fp32 mode: scores / loss within the north-star 1e-4 of the CPU oracle.  bf16 mode (conv_bf16: the 3x3 convs
-    and the frozen stem's conv1 on bf16 operands, fp32 accumulation, everything else fp32): the outputs move by bf16 rounding of the conv
-    operands only -- scores and probabilities (bounded in [0, 1]) within 2e-2 absolute, the total loss within 2e-2
-    relative, the global gradient norm within 5 % (tolerance stated for bf16 compute: unit roundoff 2^-8)."""
+    and the frozen stem's conv1 on bf16 operands, fp32 accumulation; the backbone activations -- pooled stem map,
+    conv outputs, their gradients -- stored as bf16 (option act_bf16, on by default); BN statistics, weights, grads
+    and the heads fp32): the outputs move by bf16 rounding of the conv operands and stored activations only --
+    scores and probabilities (bounded in [0, 1]) within 2e-2 absolute, the total loss within 2e-2 relative, the
+    global gradient norm within 5 % (tolerance stated for bf16 compute: unit roundoff 2^-8)."""
     case = dict(name="cfg4", B=B, T=T, H=H, W=W, seed=9, step=1, forced=None)
     x = co.synth_clips(9, 1, 0, B, T, H, W)
     y = co.synth_labels(0, B)
@@ -307,6 +309,13 @@ def test_config4_shape_fp32_and_bf16(B, T, H, W):
         torch.cuda.synchronize()
         g = eng.grads[:eng.param_floats].double()
         fp32 = dt == torch.float32
+        if not fp32:  # the bf16 run stored its activations as bf16
+            import ctypes
+            from vad_amd import _native as nat
+            pl = next(iter(eng.plans.values()))
+            p, k = ctypes.c_void_p(), ctypes.c_int64()
+            nat.check(nat.lib().vad_cad_debug_buffer(pl.h, b"act_bf16", 0, ctypes.byref(p), ctypes.byref(k)))
+            assert k.value == 1
         atol = 1e-5 if fp32 else 2e-2
         np.testing.assert_allclose(o["final"].cpu().numpy(), res["out"]["anomaly_scores"].detach().numpy(),
                                    rtol=1e-4 if fp32 else 0, atol=atol)
