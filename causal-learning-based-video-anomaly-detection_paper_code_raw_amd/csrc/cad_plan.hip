@@ -795,12 +795,14 @@ struct CadPlanImpl {
     {  // side stream, continued: the detector chain (it feeds the backbone: event ev_det), then the head's weight
        // grads, which only the optimizer / the grad all-reduce wait for
       hipStream_t st = st2;
+      // (the input-gradient chain first: the backbone backward waits for d_feat_det, the weight grads after it do not
+      // hold it up)
       TIMED("det_bwd", mlp_tail_bwd(mlp_bwd_args(NF, d_dlog, dd, LY.det_w, dh, ddh, flags), st));
+      TIMED("det_bwd", dense_dgrad(ddh[0], NF, 512, P(LY.det_w[0]), 6144, d_feat_det, nullptr, 1.f, flags, st));
+      VAD_HIP(hipEventRecord(ev_det, st));
       TIMED("det_bwd", rows_wgrad(mlp_wgrad_args(NF, d_dlog, dd, LY.det_w, LY.det_b, dh, ddh, flags), st));
       TIMED("det_bwd", dense_wgrad(ddh[0], NF, 512, feats, 6144, G(LY.det_w[0]), G(LY.det_b[0]), dense_scratch2,
                                    dense_scratch_floats, flags, st));
-      TIMED("det_bwd", dense_dgrad(ddh[0], NF, 512, P(LY.det_w[0]), 6144, d_feat_det, nullptr, 1.f, flags, st));
-      VAD_HIP(hipEventRecord(ev_det, st));
       TIMED("head_bwd", head_slab_reduce(slabs, B, slab_len, grads + LY.slots[LY.head0].offset, st));
       TIMED("head_bwd", head_rows_wgrad(head_args(), st));
     }
