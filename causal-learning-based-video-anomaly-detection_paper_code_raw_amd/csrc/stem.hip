@@ -15,9 +15,9 @@
 // and column 7 zero): K step ks covers kernel rows 2ks (lane half 0) and 2ks+1 (half 1), so a lane's 8 A values are
 // input columns 2ox-3 .. 2ox+4 of one input row -- four consecutive dwords of a bf16 LDS row (x is staged once per
 // band as 3 bf16 planes).  The weights live in 48 registers.  A wave's 32 pixels are conv columns c0-1 .. c0+30 of
-// one row (c0 = 30 * tile): after swapping the lane halves every lane holds all 32 values of its channel and takes
-// the 15 horizontal windows (columns 2px-1 .. 2px+1) in registers; the block folds them into its pooled rows in LDS
-// (ds_max_f32) and writes them at the end.
+// one row (c0 = 30 * tile): a wave folds the three conv rows of a pooled row in registers, and after swapping the
+// lane halves every lane holds all 32 values of its channel and takes the 15 horizontal windows (columns 2px-1 ..
+// 2px+1) in registers -- no LDS round trip for the pooling.
 #include <algorithm>
 
 #include "backbone.h"
@@ -118,8 +118,14 @@ constexpr int ST_SLOTS = 12;  // input staging register slots: (2 * (2 * ST_PB +
 
 // NP = 3: split-bf16 operands (fp32 numerics, the default); NP = 1: bf16 operands (conv_bf16, BASELINE config 4);
 // AB: the pooled map is stored as bf16 (bf16 activation storage)
+//
+// A wave item is (pooled row py, tile of 15 pooled columns): the wave computes the tile's 32 conv columns of conv
+// rows 2py-1, 2py, 2py+1 (row 2py-1 is also the previous pooled row's; recomputing it is cheaper than sharing it
+// through LDS atomics), folds them with a running max in registers, takes the 15 horizontal windows after the lane
+// half swap, and writes the pooled values straight to the map (lane = channel: 128 contiguous bytes per column).
+// BN sums: rows 2py and 2py+1 are pooled row py's own.
 template <int NP, bool AB = false>
-__global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restrict__ x, int H, int W,
+__global__ __launch_bounds__(256, 4) void stem_fused_kernel(const float* __restrict__ x, int H, int W,
                                                             const float* __restrict__ w,
                                                             const float* __restrict__ bias,
                                                             const float* __restrict__ gamma, int OH, int OW, int HP,
@@ -131,11 +137,8 @@ __global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restr
   const int py0 = band * ST_PB, py1 = min(HP, py0 + ST_PB);
   const int c_lo = max(2 * py0 - 1, 0), c_hi = min(2 * py1 - 1, OH - 1), n = c_hi - c_lo + 1;
   const int rows = 2 * n + 6;
-  // [ST_PB][WP][32] pooled rows: each conv row's horizontal window maxima are folded in with LDS max atomics
-  // (exact and order-independent), conv row 2py+1 into pooled rows py and py+1
-  float* hpool = reinterpret_cast<float*>(smb);
-  __bf16* xs = smb + 2 * ST_PB * WP * C;
-  for (int q = threadIdx.x; q < ST_PB * WP * C; q += blockDim.x) hpool[q] = -INFINITY;
+  __bf16* xs = smb;
+  __shared__ float red[4 * 64];  // [4 waves][2][32] BN partial sums
   bf16x8s b[4][3];
   stem_weights(w, b);
   {
@@ -147,51 +150,58 @@ __global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restr
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
   const float bj = bias[j];
-  const bool neg = gamma[j] < 0.f;  // this channel pools the minimum (as the maximum of -y)
-  const int ntr = (WP + 14) / 15;   // tiles per conv row
+  const float sgn = gamma[j] < 0.f ? -1.f : 1.f;  // this channel pools the minimum (as the maximum of -y)
+  const int ntr = (WP + 14) / 15;                  // tiles per pooled row
+  act_t<AB>* poolp = reinterpret_cast<act_t<AB>*>(pool);
   __syncthreads();
   float s1 = 0.f, s2 = 0.f;
-  for (int t = wave; t < n * ntr; t += 4) {
-    const int rl = t / ntr, c0 = 30 * (t - rl * ntr);
-    const int crow = c_lo + rl;
-    // lane pixel: conv column c0 - 1 + (lane & 31) of conv row crow (address clamped; out-of-map columns excluded)
+  const int plane2 = rows * PWb / 2;
+  for (int t = wave; t < (py1 - py0) * ntr; t += 4) {
+    const int pyl = t / ntr, c0 = 30 * (t - pyl * ntr), py = py0 + pyl;
+    // lane pixel: conv column c0 - 1 + (lane & 31) (address clamped; out-of-map columns excluded)
     const int col = c0 - 1 + (lane & 31), colc = min(max(col, 0), OW - 1);
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const int plane2 = rows * PWb / 2;
-#pragma unroll
-    for (int ks = 0; ks < ((dbg & 1) ? 0 : 4); ++ks) {
-      const unsigned* rowp = reinterpret_cast<const unsigned*>(xs + (2 * rl + 2 * ks + h) * PWb) + colc;
-      bf16x8s a[NP];
-#pragma unroll
-      for (int q = 0; q < NP; ++q) {
-        const unsigned* sp = rowp + q * plane2;
-        const u32x4s d = {sp[0], sp[1], sp[2], sp[3]};
-        a[q] = __builtin_bit_cast(bf16x8s, d);
-      }
-      if constexpr (NP == 3) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[ks][0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[ks][1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[ks][0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][1], acc, 0, 0, 0);
-      }
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][0], acc, 0, 0, 0);
-    }
     // D row i (pixel = column c0 - 1 + i) of register r in lane half h: i = (r & 3) + 8 (r >> 2) + 4 h.  Valid
     // columns are i <= ihi (and i >= 1 on the first tile); this tile's own columns for the BN sums are i = 1 .. 30
     const int ihi = min(30, OW - c0), ilo = c0 == 0 ? 1 : 0;
-    const float own = crow >= 2 * py0 ? 1.f : 0.f, sgn = neg ? -1.f : 1.f;
     float v[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float y = acc[r] + bj;
-      const float m = (i >= 1 && i <= ihi) ? own : 0.f;
-      s1 = fmaf(y, m, s1);
-      s2 = fmaf(y * y, m, s2);
-      v[r] = (i >= ilo && i <= ihi) ? y * sgn : -INFINITY;  // pooled as a max of y (gamma >= 0) or of -y
+    for (int r = 0; r < 16; ++r) v[r] = -INFINITY;
+    for (int dr = -1; dr <= 1; ++dr) {
+      const int crow = 2 * py + dr;
+      if (crow < 0 || crow >= OH) continue;
+      const int rl = crow - c_lo;
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < ((dbg & 1) ? 0 : 4); ++ks) {
+        const unsigned* rowp = reinterpret_cast<const unsigned*>(xs + (2 * rl + 2 * ks + h) * PWb) + colc;
+        bf16x8s a[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+          const unsigned* sp = rowp + q * plane2;
+          const u32x4s d = {sp[0], sp[1], sp[2], sp[3]};
+          a[q] = __builtin_bit_cast(bf16x8s, d);
+        }
+        if constexpr (NP == 3) {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[ks][0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[ks][1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[ks][0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][1], acc, 0, 0, 0);
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[ks][0], acc, 0, 0, 0);
+      }
+      const float own = dr >= 0 ? 1.f : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float y = acc[r] + bj;
+        const float m = (i >= 1 && i <= ihi) ? own : 0.f;
+        s1 = fmaf(y, m, s1);
+        s2 = fmaf(y * y, m, s2);
+        v[r] = fmaxf(v[r], (i >= ilo && i <= ihi) ? y * sgn : -INFINITY);  // a max of y (gamma >= 0) or of -y
+      }
     }
     // v_permlane32_swap of (v[r], v[r+8]): lane half 0 gets pixels 0..15 in X/Y (its windows 0..7 also need pixel
     // 16 = its own v[8], kept aside), lane half 1 pixels 16..31 -- the same registers for local pixel 16h + l:
@@ -206,38 +216,15 @@ __global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restr
     }
     auto loc = [&](int l) { return l == 16 ? p16 : (((l >> 2) & 1) ? Y : X)[(l & 3) + 4 * (l >> 3)]; };
     const int pxb = 15 * (c0 / 30) + 8 * h;  // window k of this half = pooled column pxb + k
-    const int pa = crow >> 1, pb = (crow + 1) >> 1;  // the pooled rows this conv row belongs to (equal if even)
-    float* ha = hpool + ((pa - py0) * WP + pxb) * C + j;
-    float* hb = hpool + ((pb - py0) * WP + pxb) * C + j;
-    const bool wa = pa >= py0, wb = pb != pa && pb < py1;
+    act_t<AB>* dst = poolp + (((int64_t)img * HP + py) * WP + pxb) * C + j;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float m = fmaxf(fmaxf(loc(2 * k), loc(2 * k + 1)), loc(2 * k + 2));
-      if (k < 8 - h && pxb + k < WP && !(dbg & 4)) {
-        if (wa) __hip_atomic_fetch_max(ha + k * C, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (wb) __hip_atomic_fetch_max(hb + k * C, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-  }
-  __syncthreads();
-  {
-    // pooled row py is contiguous in both hpool and the output: float4 q of the row is channel group (q & 7),
-    // fixed per thread (256 % 8 == 0)
-    const int c = (threadIdx.x & 7) * 4;
-    f32x4 sg;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) sg[e] = gamma[c + e] < 0.f ? -1.f : 1.f;
-    for (int pyl = 0; pyl < py1 - py0; ++pyl) {
-      const f32x4* src = reinterpret_cast<const f32x4*>(hpool + pyl * WP * C);
-      act_t<AB>* dst = reinterpret_cast<act_t<AB>*>(pool) + ((int64_t)img * HP + py0 + pyl) * WP * C;
-      if (!(dbg & 8))
-        for (int q = threadIdx.x; q < WP * (C / 4); q += blockDim.x) act_st4(dst + 4 * q, src[q] * sg);
+      if (k < 8 - h && pxb + k < WP && !(dbg & 8)) act_st(dst + k * C, m * sgn);
     }
   }
   s1 += __shfl_xor(s1, 32, 64);
   s2 += __shfl_xor(s2, 32, 64);
-  __syncthreads();
-  float* red = hpool;  // [4 waves][2][32]
   if (lane < 32) {
     red[wave * 64 + lane] = s1;
     red[wave * 64 + 32 + lane] = s2;
@@ -252,16 +239,12 @@ __global__ __launch_bounds__(256, 3) void stem_fused_kernel(const float* __restr
 }  // namespace
 
 int g_stem_fused = 1;  // tuning knob "stem_fused": the frozen stem's forward without the conv1 activation
-// knob "stem_dbg" (measurement only, results wrong with any bit): 1 no MFMA, 2 no input loads, 4 no window
-// atomics, 8 no pooled-map stores
+// knob "stem_dbg" (measurement only, results wrong with any bit): 1 no MFMA, 2 no input loads, 8 no pooled-map
+// stores
 int g_stem_dbg = 0;
 
 static int stem_pitch(int OW) { return (int)cdiv(2 * OW + 6, 8) * 8; }
-static size_t stem_lds(int OW) {
-  const int WP = (OW - 1) / 2 + 1;
-  return (size_t)ST_PB * WP * 32 * sizeof(float) +
-         (size_t)3 * (2 * (2 * ST_PB + 1) + 6) * stem_pitch(OW) * sizeof(__bf16);
-}
+static size_t stem_lds(int OW) { return (size_t)3 * (2 * (2 * ST_PB + 1) + 6) * stem_pitch(OW) * sizeof(__bf16); }
 
 bool stem_fused_ok(int OW) {
   return OW >= 2 && (2 * (2 * ST_PB + 1) + 6) * stem_pitch(OW) / 2 <= ST_SLOTS * 256 && stem_lds(OW) <= 160 * 1024;
