@@ -327,6 +327,11 @@ struct CadPlanImpl {
   int* head_iws;
   float *probs, *finalv, *causal, *kl, *z, *adj, *boxes;
   int *counts, *nmax, *clip_flags, *flags;
+  // detector gate (device word): the loss tail of the forward writes 1 when no box is in range (the detector then
+  // gets no gradient, cad:221-226, and its input gradient into the backbone is the zero the forward cleared) and 0
+  // otherwise; the side stream writes 1 once the detector's input gradient is final.  The backbone backward waits on
+  // the word (hipStreamWaitValue64) instead of on the whole causal-head backward.
+  uint64_t* det_gate = nullptr;
   float *d_causal, *d_kl, *d_glog, *d_dlog, *slabs, *d_feat_det, *d_pooled, *dense_scratch, *dense_scratch2;
   float *dg[5], *ddh[5];
   float *dA, *dY, *dY2, *wpart, *stem_d;  // stem_d: [NF][H1][W1][32], the stem backward's dA / dY (stem_grad only)
@@ -450,6 +455,7 @@ struct CadPlanImpl {
     nmax = w.take<int>(B);
     clip_flags = w.take<int>(B * 2);
     flags = w.take<int>(4);
+    det_gate = w.take<uint64_t>(1);
     d_causal = w.take<float>(B);
     d_kl = w.take<float>(B);
     d_glog = w.take<float>(B * 2);
@@ -735,6 +741,7 @@ struct CadPlanImpl {
     t.probs = probs;
     t.final_scores = finalv;
     t.flags = flags;
+    t.det_gate = det_gate;
     t.flags_f = grads ? grads + layout().param_floats : nullptr;
     t.labels = labels;
     t.losses = losses_ptr;
@@ -761,6 +768,8 @@ struct CadPlanImpl {
     VAD_CHECK(!use_loss || labels != nullptr, "backward(use_loss): forward ran without labels");
     VAD_CHECK(stage >= -1 && stage <= 1, "backward: stage must be -1, 0 or 1");
     VAD_CHECK(bwd_state != 0 || stage != 1, "backward stage 1: stage 0 has not run for the current forward");
+    // detector gate: knob "cad_det_gate" (0: the backbone waits for the side stream's event as before)
+    const bool gate = g_cad_det_gate != 0 && det_gate != nullptr;
     if (stage != 1) {
     // grads of frozen / never-used slots stay zero
     VAD_HIP(hipMemsetAsync(grads, 0, sizeof(float) * LY.param_floats, st));
@@ -800,6 +809,7 @@ struct CadPlanImpl {
       TIMED("det_bwd", mlp_tail_bwd(mlp_bwd_args(NF, d_dlog, dd, LY.det_w, dh, ddh, flags), st));
       TIMED("det_bwd", dense_dgrad(ddh[0], NF, 512, P(LY.det_w[0]), 6144, d_feat_det, nullptr, 1.f, flags, st));
       VAD_HIP(hipEventRecord(ev_det, st));
+      if (gate) VAD_HIP(hipStreamWriteValue64(st, det_gate, 1, 0));
       TIMED("det_bwd", rows_wgrad(mlp_wgrad_args(NF, d_dlog, dd, LY.det_w, LY.det_b, dh, ddh, flags), st));
       TIMED("det_bwd", dense_wgrad(ddh[0], NF, 512, feats, 6144, G(LY.det_w[0]), G(LY.det_b[0]), dense_scratch2,
                                    dense_scratch_floats, flags, st));
@@ -807,6 +817,7 @@ struct CadPlanImpl {
       TIMED("head_bwd", head_rows_wgrad(head_args(), st));
     }
     if (stage == 0) VAD_TRY(join(st));  // every non-backbone grad is final when stage 0 returns
+    else if (gate) VAD_HIP(hipStreamWaitValue64(st, det_gate, 1, hipStreamWaitValueEq, ~0ull));
     else VAD_HIP(hipStreamWaitEvent(st, ev_det, 0));
     }
     bwd_state = 1;

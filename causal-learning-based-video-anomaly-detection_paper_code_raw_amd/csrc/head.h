@@ -89,6 +89,7 @@ struct TailArgs {
   float* final_scores;          // [B]
   int* flags;                   // [2] (det_in_graph, struct_in_graph) -> also mirrored as floats
   float* flags_f;               // [2] or null
+  uint64_t* det_gate;           // forward: 1 when no box is in range (no detector gradient), else 0; or null
   // loss mode
   const int64_t* labels;        // [B] or null
   float* losses;                // [5]: classification, anomaly, causal, kl, total

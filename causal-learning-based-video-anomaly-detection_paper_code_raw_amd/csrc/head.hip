@@ -1064,6 +1064,7 @@ __global__ void cad_tail_fwd_kernel(TailArgs t) {
   if (threadIdx.x == 0) {
     t.flags[0] = fl[0];
     t.flags[1] = fl[1];
+    if (t.det_gate) *t.det_gate = fl[0] ? 0ull : 1ull;
     if (t.flags_f) {
       t.flags_f[0] = (float)fl[0];
       t.flags_f[1] = (float)fl[1];
