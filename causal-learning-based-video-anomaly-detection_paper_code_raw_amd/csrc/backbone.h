@@ -15,6 +15,7 @@ int conv1_num_parts(int NF, int OH);
 extern int g_x3_stagger;  // knob "conv_split_stagger"
 extern int g_x3_dgrad_blocks;  // knob "conv_dgrad_blocks"
 extern int g_x3_big;  // knob "conv_split_big"
+extern int g_x3_ws;   // knob "conv_split_ws"
 extern int g_cad_prep_stream, g_cad_wgrad_stream, g_cad_det_gate, g_dbg_skip_bnred;  // knobs "cad_prep_stream", "cad_wgrad_stream" (A/B)
 extern int g_stem_fused, g_stem_dbg;  // knobs "stem_fused" (default 1), "stem_dbg" (measurement only)
 bool stem_fused_ok(int OW);  // conv1 output width the fused stem handles

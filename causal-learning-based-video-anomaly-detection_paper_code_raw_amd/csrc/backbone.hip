@@ -962,6 +962,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_dgrad_s2_x3") g_dgrad_s2_x3 = value;
   else if (k == "conv_dgrad_blocks") g_x3_dgrad_blocks = value;
   else if (k == "conv_split_big") g_x3_big = value;
+  else if (k == "conv_split_ws") g_x3_ws = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "cad_det_gate") g_cad_det_gate = value;

@@ -329,6 +329,296 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
   }
 }
 
+// Wave-specialised variant of the stride-1 kernel above for 256-pixel tiles (512 threads, one block per CU): waves
+// 0-3 multiply (each owns 64 output pixels = two 32-row MFMA tiles of one staged patch) while waves 4-7 stage the
+// NEXT item (global prefetch -> BN+ReLU on load -> split planes -> the other half of a double-buffered patch, and of
+// the weight slice when it is restaged per item), so the staging VALU / LDS-write / load latency of item k+1 runs on
+// the SIMDs beside the MFMAs of item k instead of between barriers; one barrier per item.  Same products and the same
+// accumulation order per output as conv3x3_x3_kernel.  WCH = 2: the split weights of both reduction chunks stay
+// resident (staged once by all 512 threads).
+template <int NI, int TH, int TW, int PC, bool FWD, int NP, int WCH, bool AB, int CW>
+__global__ __launch_bounds__(128 * CW, 1) void conv3x3_x3ws_kernel(const X3Args p) {
+  static_assert(CW == 4 || CW == 8, "4 or 8 consumer waves");
+  constexpr int SUB = 8 / CW, NTHR = 128 * CW;  // 32-row MFMA tiles per consumer wave, threads
+  static_assert(NI * TH * TW == 256, "256-pixel tiles");
+  static_assert(NP == 3 || NP == 1, "three split planes or one");
+  static_assert(!AB || NP == 1, "bf16 storage with bf16 operands only");
+  static_assert(PC == 16, "one 16-deep K step per tap");
+  using TA = act_t<AB>;
+  const TA* src = reinterpret_cast<const TA*>(p.src);
+  TA* out = reinterpret_cast<TA*>(p.out);
+  constexpr int NC = 32, G8 = PC / 8, NPR = 64 * CW;  // output channels per block, producer threads
+  constexpr int PH = TH + 2, PW = TW + 2, PROWS = NI * PH * PW;
+  constexpr int RP = NP * PC + 8;
+  constexpr int WCS = 9 * NP * PC;
+  constexpr int WP = WCH * WCS + 8;
+  constexpr int NWB = WCH > 1 ? 1 : 2;  // weight buffers: resident, or double-buffered per item
+  static_assert(((RP * 2 / 16) & 1) && ((WP * 2 / 16) & 1), "odd 16-B row pitch");
+  __shared__ __attribute__((aligned(16))) __bf16 sm[2 * PROWS * RP + NWB * NC * WP];
+  __bf16* const patch0 = sm;
+  __bf16* const wl0 = sm + 2 * PROWS * RP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, j = lane & 31;
+  const bool consumer = wave < CW;
+  const int tiles_per_img = p.tiles_h * p.tiles_w;
+  const int n0 = blockIdx.y * NC;
+  const int t0 = blockIdx.x * p.tpb, t1 = min(p.ntiles, t0 + p.tpb);
+  const int nch = p.C / PC;
+  const int nitems = (t1 - t0) * nch;
+  // weights restaged per item (double-buffered) unless resident or a single chunk
+  const bool wper = WCH == 1 && nch > 1;
+
+  auto origin = [&](int tile, int& img0, int& oy0, int& ox0) {
+    img0 = (tile / tiles_per_img) * NI;
+    const int tr = tile % tiles_per_img;
+    oy0 = (tr / p.tiles_w) * TH;
+    ox0 = (tr % p.tiles_w) * TW;
+  };
+
+  // ---------------- producer state (waves 4-7): thread ptid handles channel group g8 = ptid % G8
+  constexpr int PQ = PROWS * G8, PIT = (PQ + NPR - 1) / NPR;
+  constexpr int WQ = NC * 9 * G8, WIT = (WQ + NPR - 1) / NPR;
+  const int ptid = tid - NPR, g8 = tid % G8;
+  act_raw4<AB> pv[PIT][2];
+  f32x4 wv[WIT][2];
+  bool pok[PIT], wok[WIT];
+  auto fetch = [&](int tile, int c0, bool weights) {
+    int img0, oy0, ox0;
+    origin(tile, img0, oy0, ox0);
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = ptid + it * NPR;
+      const int row = q / G8;
+      const int im = row / (PH * PW), rr = row % (PH * PW);
+      const int iy = oy0 - 1 + rr / PW, ix = ox0 - 1 + rr % PW, img = img0 + im;
+      pok[it] = q < PQ && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
+      const TA* s = src + c0 + g8 * 8 + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
+      pv[it][0] = act_ld4(s);
+      pv[it][1] = act_ld4(s + 4);
+    }
+    if (weights) {
+#pragma unroll
+      for (int it = 0; it < WIT; ++it) {
+        const int q = ptid + it * NPR;
+        const int n = q / (9 * G8), t = (q / G8) % 9;
+        wok[it] = q < WQ && n0 + n < p.N;
+        const float* s = p.w + c0 + g8 * 8 +
+                         (wok[it] ? ((int64_t)(n0 + n) * 9 + (FWD ? t : 8 - t)) * p.C : (int64_t)0);
+        wv[it][0] = *reinterpret_cast<const f32x4*>(s);
+        wv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
+      }
+    }
+  };
+  auto stash = [&](int c0, __bf16* patch, __bf16* wl, bool weights) {
+    const bool bn = FWD && p.scale;
+    f32x4 sc[2], sh[2];
+    if constexpr (FWD) {
+      const float* scp = bn ? p.scale : p.w;
+      const float* shp = bn ? p.shift : p.w;
+      sc[0] = *reinterpret_cast<const f32x4*>(scp + c0 + g8 * 8);
+      sc[1] = *reinterpret_cast<const f32x4*>(scp + c0 + g8 * 8 + 4);
+      sh[0] = *reinterpret_cast<const f32x4*>(shp + c0 + g8 * 8);
+      sh[1] = *reinterpret_cast<const f32x4*>(shp + c0 + g8 * 8 + 4);
+    }
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = ptid + it * NPR;
+      if (q < PQ) {
+        const int row = q / G8;
+        float v[8];
+        const f32x4 v0 = act_f4(pv[it][0]), v1 = act_f4(pv[it][1]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = pok[it] ? v0[e] : 0.f;
+          v[4 + e] = pok[it] ? v1[e] : 0.f;
+        }
+        if constexpr (FWD) {
+          // zero padding stays zero: padded taps read 0 in the reference's zero-padded relu(bn(y))
+          const bool app = bn && pok[it];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float a0 = relu_nan(fmaf(v[e], sc[0][e], sh[0][e]));
+            const float a1 = relu_nan(fmaf(v[4 + e], sc[1][e], sh[1][e]));
+            v[e] = app ? a0 : v[e];
+            v[4 + e] = app ? a1 : v[4 + e];
+          }
+        }
+        put_planes<NP>(patch + row * RP + g8 * 8, PC, v, false);
+      }
+    }
+    if (weights) {
+#pragma unroll
+      for (int it = 0; it < WIT; ++it) {
+        const int q = ptid + it * NPR;
+        if (q < WQ) {
+          const int n = q / (9 * G8), t = (q / G8) % 9;
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = wok[it] ? wv[it][0][e] : 0.f;
+            v[4 + e] = wok[it] ? wv[it][1][e] : 0.f;
+          }
+          put_planes<NP>(wl + n * WP + t * NP * PC + g8 * 8, PC, v, false);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  };
+
+  // ---------------- prologue
+  if constexpr (WCH > 1) {
+    // resident split weights of every chunk, staged once by all 512 threads
+    for (int q = tid; q < NC * 9 * WCH * G8; q += NTHR) {
+      const int n = q / (9 * WCH * G8), t = (q / (WCH * G8)) % 9, cg = q % (WCH * G8);
+      const int ch = cg / G8, g = cg % G8;
+      const bool ok = n0 + n < p.N;
+      float v[8];
+      const float* s = p.w + ((int64_t)(ok ? n0 + n : 0) * 9 + (FWD ? t : 8 - t)) * p.C + ch * PC + g * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = ok ? s[e] : 0.f;
+      put_planes<NP>(wl0 + n * WP + ch * WCS + t * NP * PC + g * 8, PC, v, false);
+    }
+  }
+  if (!consumer && nitems > 0) {
+    fetch(t0, 0, WCH == 1);
+    stash(0, patch0, wl0, WCH == 1);
+    if (nitems > 1) fetch(t0 + 1 / nch, (1 % nch) * PC, wper);
+  }
+  __syncthreads();
+
+  // ---------------- consumer state (waves 0-3): pixels [64 wave, 64 wave + 64) as two 32-row tiles
+  int arow[SUB];
+#pragma unroll
+  for (int s2 = 0; s2 < SUB; ++s2) {
+    const int m = wave * 32 * SUB + s2 * 32 + j;
+    const int mi = m / (TH * TW), mr = m % (TH * TW);
+    arow[s2] = (mi * PH + mr / TW) * PW + mr % TW;
+  }
+  const float bj = (FWD && n0 + j < p.N) ? p.bias[n0 + j] : 0.f;
+  float s1 = 0.f, sq = 0.f;
+  f32x16 acc[SUB];
+
+  for (int item = 0; item < nitems; ++item) {
+    const int tile = t0 + item / nch, ch = item % nch;
+    const int buf = item & 1;
+    if (consumer) {
+      const __bf16* patch = patch0 + buf * PROWS * RP;
+      const __bf16* bbase = wl0 + (wper ? buf * NC * WP : 0) + j * WP + 8 * h + (WCH > 1 ? ch * WCS : 0);
+      if (ch == 0) {
+#pragma unroll
+        for (int s2 = 0; s2 < SUB; ++s2)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[s2][r] = 0.f;
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int kh = t / 3, kw = t % 3;
+        bf16x8 a[SUB][NP], b[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) b[q] = *reinterpret_cast<const bf16x8*>(bbase + (t * NP + q) * PC);
+#pragma unroll
+        for (int s2 = 0; s2 < SUB; ++s2)
+#pragma unroll
+          for (int q = 0; q < NP; ++q)
+            a[s2][q] = *reinterpret_cast<const bf16x8*>(patch + (arow[s2] + kh * PW + kw) * RP + 8 * h + q * PC);
+#pragma unroll
+        for (int s2 = 0; s2 < SUB; ++s2) {
+          if constexpr (NP == 3) acc[s2] = mfma_x3(a[s2], b, acc[s2]);
+          else acc[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s2][0], b[0], acc[s2], 0, 0, 0);
+        }
+      }
+      if (ch == nch - 1) {
+        // row = pixel (r&3) + 8(r>>2) + 4h of the sub-tile's 32, column = channel n0 + j
+        int img0, oy0, ox0;
+        origin(tile, img0, oy0, ox0);
+        const bool colok = n0 + j < p.N;
+#pragma unroll
+        for (int s2 = 0; s2 < SUB; ++s2)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int pm = wave * 32 * SUB + s2 * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int qi = pm / (TH * TW), qr = pm % (TH * TW);
+            const int oy = oy0 + qr / TW, ox = ox0 + qr % TW, img = img0 + qi;
+            if (colok && img < p.NF && oy < p.OH && ox < p.OW) {
+              const float v = acc[s2][r] + bj;
+              act_st(out + (((int64_t)img * p.OH + oy) * p.OW + ox) * p.N + n0 + j, v);
+              if (FWD) {
+                s1 += v;
+                sq = fmaf(v, v, sq);
+              }
+            }
+          }
+      }
+    } else if (item + 1 < nitems) {
+      const int nx = item + 1;
+      stash((nx % nch) * PC, patch0 + (buf ^ 1) * PROWS * RP, wl0 + (wper ? (buf ^ 1) * NC * WP : 0), wper);
+      if (nx + 1 < nitems) fetch(t0 + (nx + 1) / nch, ((nx + 1) % nch) * PC, wper);
+    }
+    __syncthreads();
+  }
+  if (FWD) {
+    float* red = reinterpret_cast<float*>(sm);  // [CW consumer waves][2][32]
+    if (consumer) {
+      const float a1 = s1 + __shfl_xor(s1, 32, 64);
+      const float a2 = sq + __shfl_xor(sq, 32, 64);
+      if (lane < 32) {
+        red[(wave * 2 + 0) * NC + lane] = a1;
+        red[(wave * 2 + 1) * NC + lane] = a2;
+      }
+    }
+    __syncthreads();
+    if (tid < 2 * NC) {
+      const int which = tid / NC, c = tid % NC;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < CW; ++w) v += red[(2 * w + which) * NC + c];  // fixed order
+      if (n0 + c < p.N) p.partials[(int64_t)blockIdx.x * 2 * p.N + which * p.N + n0 + c] = v;
+    }
+  }
+}
+
+extern int g_x3_wres;
+int g_x3_ws = 0;  // knob "conv_split_ws": stride-1 256-pixel layers on the wave-specialised kernel (1: 4 + 4 waves,
+                  // 2: 8 + 8 waves)
+
+template <int NI, int TH, int TW, bool FWD, int NP, int WCH, bool AB>
+static int launch_ws_k(const X3Args& a, int gx, int ny, hipStream_t st) {
+  if (g_x3_ws == 2)
+    VAD_KLAUNCH((conv3x3_x3ws_kernel<NI, TH, TW, 16, FWD, NP, WCH, AB, 8>), dim3(gx, ny), dim3(1024), 0, st, a);
+  else
+    VAD_KLAUNCH((conv3x3_x3ws_kernel<NI, TH, TW, 16, FWD, NP, WCH, AB, 4>), dim3(gx, ny), dim3(512), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+template <int NI, int TH, int TW, bool FWD>
+static int launch_ws(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
+  VAD_CHECK(a.C % 16 == 0, "conv3x3_x3ws: C % 16");
+  a.tiles_h = (int)cdiv(a.OH, TH);
+  a.tiles_w = (int)cdiv(a.OW, TW);
+  a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);
+  const int ny = (int)cdiv(a.N, 32);
+  // one block per CU over 256 CUs (input gradients: knob "conv_dgrad_blocks" / 2)
+  const int target = std::max(1, std::min(max_blocks, (FWD ? 512 : g_x3_dgrad_blocks) / 2 / ny));
+  a.tpb = (int)cdiv(a.ntiles, target);
+  const int gx = (int)cdiv(a.ntiles, a.tpb);
+  const bool wres = g_x3_wres && a.C == 32;
+  int rc;
+  if (g_conv_bf16) {
+    if (g_act_bf16) rc = wres ? launch_ws_k<NI, TH, TW, FWD, 1, 2, true>(a, gx, ny, st)
+                              : launch_ws_k<NI, TH, TW, FWD, 1, 1, true>(a, gx, ny, st);
+    else rc = wres ? launch_ws_k<NI, TH, TW, FWD, 1, 2, false>(a, gx, ny, st)
+                   : launch_ws_k<NI, TH, TW, FWD, 1, 1, false>(a, gx, ny, st);
+  } else {
+    VAD_CHECK(!g_act_bf16, "conv3x3_x3ws: bf16 activations need the bf16-operand kernels (conv_bf16)");
+    rc = wres ? launch_ws_k<NI, TH, TW, FWD, 3, 2, false>(a, gx, ny, st)
+              : launch_ws_k<NI, TH, TW, FWD, 3, 1, false>(a, gx, ny, st);
+  }
+  if (rc) return rc;
+  if (nparts) *nparts = gx;
+  return 0;
+}
+
 int g_x3_dgrad_blocks = 512;  // knob "conv_dgrad_blocks"
 
 template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1, int NW = 4>
@@ -402,6 +692,13 @@ static int dispatch_x3_nt(const X3Args& a, int max_blocks, hipStream_t st, int* 
 
 template <int S, bool FWD>
 static int dispatch_x3(const X3Args& a, int max_blocks, hipStream_t st, int* nparts) {
+  if constexpr (S == 1) {
+    if (g_x3_ws && g_x3_big) {
+      if (a.OH <= 8 && a.OW <= 8) return launch_ws<4, 8, 8, FWD>(a, max_blocks, st, nparts);
+      if (a.OW <= 16) return launch_ws<2, 8, 16, FWD>(a, max_blocks, st, nparts);
+      return launch_ws<1, 8, 32, FWD>(a, max_blocks, st, nparts);
+    }
+  }
   int nt = g_x3_nt;
   if (nt == 0) {
     // 64 channels per block halves the fragment reads per MFMA; keep 32 when that would leave the chip underfull

@@ -16,6 +16,11 @@ def pytest_configure(config):
 def pytest_collection_modifyitems(config, items):
     import torch
     if torch.cuda.is_available():
+        # VAD_TUNE="knob=v,knob=v": run the GPU suite with library tuning knobs set (A/B of kernel variants)
+        for kv in filter(None, os.environ.get("VAD_TUNE", "").split(",")):
+            from vad_amd import _native as nat
+            k, v = kv.split("=")
+            nat.check(nat.lib().vad_set_tuning(k.encode(), int(v)))
         return
     skip = pytest.mark.skip(reason="no HIP device in this container")
     for it in items:

@@ -11,6 +11,8 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ends = [i for i, r in enumerate(rows) if end_k in r["Kernel_Name"]]
 a, b = ends[-2], ends[-1]
 prev = None
+t0 = int(rows[a + 1]["Start_Timestamp"])
+qcol = "Queue_Id" if "Queue_Id" in rows[0] else None
 tot = collections.Counter()
 busy = 0
 for r in rows[a + 1:b + 1]:
@@ -20,6 +22,7 @@ for r in rows[a + 1:b + 1]:
     prev = e
     busy += e - s
     tot[n] += (e - s) / 1e3
-    print(f"{(e - s) / 1e3:7.1f} gap{gap:5.1f} g={r['Grid_Size_X']}x{r['Grid_Size_Y']}x{r['Grid_Size_Z']} {n}")
+    q = r[qcol] if qcol else "?"
+    print(f"t={(s - t0) / 1e3:7.1f} q{q:>2} {(e - s) / 1e3:7.1f} gap{gap:6.1f} g={r['Grid_Size_X']}x{r['Grid_Size_Y']} {n}")
 span = int(rows[b]["End_Timestamp"]) - int(rows[a + 1]["Start_Timestamp"])
 print(f"step span {span / 1e3:.1f} us, kernel busy {busy / 1e3:.1f} us, launches {b - a}")
