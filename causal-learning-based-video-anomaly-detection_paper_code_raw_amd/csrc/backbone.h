@@ -16,6 +16,7 @@ extern int g_x3_stagger;  // knob "conv_split_stagger"
 extern int g_x3_dgrad_blocks;  // knob "conv_dgrad_blocks"
 extern int g_x3_big;  // knob "conv_split_big"
 extern int g_x3_ws;   // knob "conv_split_ws"
+extern int g_bn_fin_fused;  // knob "bn_fin_fused"
 extern int g_cad_prep_stream, g_cad_wgrad_stream, g_cad_det_gate, g_dbg_skip_bnred;  // knobs "cad_prep_stream", "cad_wgrad_stream" (A/B)
 extern int g_stem_fused, g_stem_dbg;  // knobs "stem_fused" (default 1), "stem_dbg" (measurement only)
 bool stem_fused_ok(int OW);  // conv1 output width the fused stem handles
@@ -72,8 +73,22 @@ int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd
 // the same for n <= 8 layers in one launch
 int conv3_prep_weights_all(int n, const float* const* w, const Conv3Layer* L, float* const* wf, float* const* wd,
                            hipStream_t st);
+// In-kernel train-mode BatchNorm finalize for a conv forward (the last block to finish folds every block's partial
+// sums; bn_finalize semantics): counter = a zeroed int (the last block re-zeroes it); `done` is set by the call when
+// the conv kernel took it (otherwise the caller runs bn_finalize on the partials as before).
+struct BnFinArgs {
+  int* counter = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  float* running_mean = nullptr;
+  float* running_var = nullptr;
+  float* stats = nullptr;
+  double count = 0;
+  int done = 0;
+};
 int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats /*nullable: BN+ReLU on load*/,
-              const float* wf, const float* bias, float* y, float* partials, int* nparts, hipStream_t st);
+              const float* wf, const float* bias, float* y, float* partials, int* nparts, hipStream_t st,
+              BnFinArgs* fin = nullptr);
 int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
 // direct LDS-patch kernels (conv_patch.hip) for stride-1 layers; conv3_fwd / conv3_dgrad route there by default
 bool conv3_patch_supported(const Conv3Layer& L, bool fwd);
@@ -107,7 +122,7 @@ struct ActStorage {
 };
 bool conv3_x3_supported(const Conv3Layer& L, bool fwd);
 int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
-                 float* y, float* partials, int* nparts, hipStream_t st);
+                 float* y, float* partials, int* nparts, hipStream_t st, BnFinArgs* fin = nullptr);
 int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
 // stride-2 input gradient on the split-bf16 (or, with conv_bf16, bf16) MFMA: parity classes of a 16x16 dX tile
 // sharing one dY patch; Wd in the plain [Ci][9][Co] layout (conv3_prep_weights with classes == 0)
@@ -130,8 +145,9 @@ int conv3_path(const Conv3Layer& L, int kind);
 // every pass of this layer (forward, input gradient when dgrad, weight gradient) runs on a split kernel under the
 // current knobs, i.e. can take bf16 activations
 bool conv3_act_bf16_ok(const Conv3Layer& L, bool dgrad);
+// alone: nothing else runs beside this weight gradient (the last layer's): the grid fills every CU
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
-                int* nsplit, int64_t partial_cap, hipStream_t st);
+                int* nsplit, int64_t partial_cap, hipStream_t st, bool alone = false);
 int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, const float* bias_partials,
                        int nbias_parts, float* dW, float* db, hipStream_t st);
 

@@ -936,6 +936,8 @@ struct ConvTuning {
   int wgrad_min_ktiles = 16;             // minimum BK-slices per split
   int patch = 1;                         // stride-1 fwd/dgrad on the LDS-patch kernels
   int wgrad_patch = 1;                   // weight gradients on the LDS-patch kernel: 1 stride-1 layers, 2 all
+  int wgrad_alone_blocks = 448;          // the same for a weight gradient nothing else runs beside (the last layer's;
+                                         // 512 / 1024 measured no faster)
   int wgrad_patch_blocks = 448;          // its target grid size (below 2 per CU: the weight gradients share the GPU with the input gradients, own stream)
 };
 static ConvTuning g_tune;
@@ -963,6 +965,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_dgrad_blocks") g_x3_dgrad_blocks = value;
   else if (k == "conv_split_big") g_x3_big = value;
   else if (k == "conv_split_ws") g_x3_ws = value;
+  else if (k == "bn_fin_fused") g_bn_fin_fused = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "cad_det_gate") g_cad_det_gate = value;
@@ -974,6 +977,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_s1_nt_blocks") g_wgrad_s1_nt_blocks = value;
   else if (k == "conv_bf16") g_conv_bf16 = value;  // ops API only (calling thread); plans use their own option
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
+  else if (k == "conv_wgrad_alone_blocks") g_tune.wgrad_alone_blocks = value;
   else {
     set_error("unknown tuning key " + k);
     return 1;
@@ -1132,11 +1136,11 @@ int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd
 }
 
 int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
-              float* y, float* partials, int* nparts, hipStream_t st) {
+              float* y, float* partials, int* nparts, hipStream_t st, BnFinArgs* fin) {
   VAD_CHECK(L.Ci % 32 == 0, "conv3_fwd: Ci must be a multiple of 32");
   // (the patch grid may exceed ceil(M/64) BN partial blocks on tiny images: those stay on the GEMM path)
   if (g_tune.patch && conv3_patch_blocks(L.NF, L.OH, L.OW) <= cdiv((int64_t)L.NF * L.OH * L.OW, 64)) {
-    if (conv3_x3_supported(L, true)) return conv3_x3_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st);
+    if (conv3_x3_supported(L, true)) return conv3_x3_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st, fin);
     VAD_CHECK(!g_act_bf16, "conv3_fwd: bf16 activations need the split kernels");
     if (conv3_patch_supported(L, true)) return conv3_patch_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st);
   }
@@ -1232,9 +1236,10 @@ int conv3_path(const Conv3Layer& L, int kind) {
 }
 
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
-                int* nsplit, int64_t partial_cap, hipStream_t st) {
+                int* nsplit, int64_t partial_cap, hipStream_t st, bool alone) {
   if (g_tune.wgrad_patch && conv3_wgrad_x3_supported(L))
-    return conv3_wgrad_x3(L, dY, src, src_stats, partial, nsplit, partial_cap, g_tune.wgrad_patch_blocks, st);
+    return conv3_wgrad_x3(L, dY, src, src_stats, partial, nsplit, partial_cap,
+                          alone ? g_tune.wgrad_alone_blocks : g_tune.wgrad_patch_blocks, st);
   VAD_CHECK(!g_act_bf16, "conv3_wgrad: bf16 activations need the split kernels");
   if (g_tune.wgrad_patch && conv3_wgrad_patch_supported(L) && (L.stride == 1 || g_tune.wgrad_patch == 2))
     return conv3_wgrad_patch(L, dY, src, src_stats, partial, nsplit, partial_cap, g_tune.wgrad_patch_blocks, st);

@@ -332,6 +332,7 @@ struct CadPlanImpl {
   // otherwise; the side stream writes 1 once the detector's input gradient is final.  The backbone backward waits on
   // the word (hipStreamWaitValue64) instead of on the whole causal-head backward.
   uint64_t* det_gate = nullptr;
+  int* fin_counters = nullptr;  // tickets of the in-kernel BN finalize of the 8 conv layers (zeroed per forward)
   float *d_causal, *d_kl, *d_glog, *d_dlog, *slabs, *d_feat_det, *d_pooled, *dense_scratch, *dense_scratch2;
   float *dg[5], *ddh[5];
   float *dA, *dY, *dY2, *wpart, *stem_d;  // stem_d: [NF][H1][W1][32], the stem backward's dA / dY (stem_grad only)
@@ -456,6 +457,7 @@ struct CadPlanImpl {
     clip_flags = w.take<int>(B * 2);
     flags = w.take<int>(4);
     det_gate = w.take<uint64_t>(1);
+    fin_counters = w.take<int>(8);
     d_causal = w.take<float>(B);
     d_kl = w.take<float>(B);
     d_glog = w.take<float>(B * 2);
@@ -659,6 +661,7 @@ struct CadPlanImpl {
       for (int l = 0; l < 8; ++l) w8[l] = P(LY.conv_w[l]);
       TIMED("prep", conv3_prep_weights_all(8, w8, L, wf, wd, st));
       TIMED("prep", mlp_transpose(mlp_transpose_args(), st));
+      VAD_HIP(hipMemsetAsync(fin_counters, 0, 8 * sizeof(int), st));
       VAD_HIP(hipEventRecord(ev_prep, st));
     }
     int np = 0;
@@ -685,8 +688,23 @@ struct CadPlanImpl {
     const float* src = pool;
     const float* sst = pool_stats;
     for (int l = 0; l < 8; ++l) {
-      TIMED(L_("conv_fwd", l), conv3_fwd(L[l], src, sst, wf[l], P(LY.conv_b[l]), y[l], parts, &np, st));
-      VAD_TRY(bn_fwd_stats(l + 1, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]), st));
+      // train-mode BN statistics folded by the conv kernel's last block where it can (not with SyncBN: the sums
+      // cross the process group first)
+      BnFinArgs fin;
+      const bool fuse = training && sync_fn == nullptr;
+      if (fuse) {
+        fin.counter = fin_counters + l;
+        fin.gamma = P(LY.bn_w[l]);
+        fin.beta = P(LY.bn_b[l]);
+        fin.running_mean = RM(l + 1);
+        fin.running_var = RV(l + 1);
+        fin.stats = stats[l + 1];
+        fin.count = (double)NF * L[l].OH * L[l].OW;
+      }
+      TIMED(L_("conv_fwd", l), conv3_fwd(L[l], src, sst, wf[l], P(LY.conv_b[l]), y[l], parts, &np, st,
+                                         fuse ? &fin : nullptr));
+      if (!fin.done)
+        VAD_TRY(bn_fwd_stats(l + 1, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]), st));
       src = y[l];
       sst = stats[l + 1];
     }
@@ -849,7 +867,8 @@ struct CadPlanImpl {
         }
         hipStream_t st = wst;
         int ns = 0;
-        TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dYl, src, sst, wpart, &ns, wpart_floats, st));
+        // (layer 0 with the frozen stem: nothing runs beside its weight gradient)
+        TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dYl, src, sst, wpart, &ns, wpart_floats, st, l == 0 && !stem_grad));
         TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], wpart, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
         if (wgs) VAD_HIP(hipEventRecord(ev_wg[l & 1], st));
       }

@@ -36,8 +36,86 @@ struct X3Args {
   int dbg;  // measurement only (knob "conv_split_dbg"): 1 no weight restaging, 2 no patch split, 4 no MFMA,
             // 8 no patch loads -- results are wrong with any bit set
   int stagger;  // knob "conv_split_stagger": odd blocks start this many x 1024 cycles late (phase offset of the two
-                // co-resident blocks of a CU)
+                // co-resident blocks of a CU)  // forward: in-kernel BatchNorm finalize (fin_counter != nullptr; see bn_fin_last_block)
+  int* fin_counter;
+  const float* fin_gamma;
+  const float* fin_beta;
+  float* fin_rm;
+  float* fin_rv;
+  float* fin_stats;
+  double fin_count;
 };
+
+// In-kernel BatchNorm finalize (forward, train mode) after every block has written its [2N] partial row: partial
+// sums are stored write-through (sc1) and drained by every storing wave, one lane per block draws a ticket from an
+// agent-scope counter, and the block drawing the last one acquires (agent scope) and reads the partial rows with plain
+// (pipelined) loads -- per-element sc1 loads serialise at memory latency -- folding them in double in a fixed
+// order (bn_finalize_kernel semantics: batch mean / biased var, running stats with momentum 0.1 and the unbiased
+// var, scale = gamma * invstd, shift = beta - mean * scale), then re-zeroes the counter.  Saves the finalize launch
+// after every conv.  `red` is LDS scratch of at least NTHR doubles + 4 bytes.
+template <int NTHR>
+__device__ __forceinline__ void bn_fin_last_block(const X3Args& p, int P, char* red) {
+  const int tid = threadIdx.x;
+  int* flag = reinterpret_cast<int*>(red + NTHR * sizeof(double));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 partial stores are complete
+  __syncthreads();
+  if (tid == 0) {
+    const int total = gridDim.x * gridDim.y;
+    const int prev = __hip_atomic_fetch_add(p.fin_counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == total - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  const int N = p.N, NC2 = 2 * N;
+  double* part = reinterpret_cast<double*>(red);
+  // columns 2N x rows P: G row groups per column when 2N <= NTHR, else each thread walks several columns
+  const int G = NC2 <= NTHR ? NTHR / NC2 : 1;
+  if (G > 1) {
+    if (tid < G * NC2) {
+      const int g = tid / NC2, col = tid % NC2;
+      double acc = 0.0;
+#pragma unroll 8
+      for (int r = g; r < P; r += G) acc += (double)p.partials[(int64_t)r * NC2 + col];
+      part[g * NC2 + col] = acc;
+    }
+  } else {
+    for (int col = tid; col < NC2; col += NTHR) {
+      double acc = 0.0;
+#pragma unroll 8
+      for (int r = 0; r < P; ++r) acc += (double)p.partials[(int64_t)r * NC2 + col];
+      part[col] = acc;
+    }
+  }
+  __syncthreads();
+  if (G > 1) {
+    double tot = 0.0;
+    if (tid < NC2)
+      for (int g = 0; g < G; ++g) tot += part[g * NC2 + tid];  // fixed order
+    __syncthreads();
+    if (tid < NC2) part[tid] = tot;
+    __syncthreads();
+  }
+  const double count = p.fin_count, momentum = 0.1, eps = 1e-5;
+  for (int c = tid; c < N; c += NTHR) {
+    const double mean = part[c] / count;
+    double var = part[N + c] / count - mean * mean;
+    if (var < 0) var = 0;
+    p.fin_rm[c] = (float)((1.0 - momentum) * p.fin_rm[c] + momentum * mean);
+    p.fin_rv[c] = (float)((1.0 - momentum) * p.fin_rv[c] + momentum * var * count / (count - 1.0));
+    const double invstd = 1.0 / sqrt(var + eps);
+    const double scale = (double)p.fin_gamma[c] * invstd;
+    p.fin_stats[c] = (float)mean;
+    p.fin_stats[N + c] = (float)invstd;
+    p.fin_stats[2 * N + c] = (float)scale;
+    p.fin_stats[3 * N + c] = (float)((double)p.fin_beta[c] - mean * scale);
+  }
+  if (tid == 0) __hip_atomic_store(p.fin_counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ void split3(const float* v, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
 #pragma unroll
@@ -324,7 +402,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) v += red[(2 * w + which) * NC + c];  // fixed order
-      if (n0 + c < p.N) p.partials[(int64_t)blockIdx.x * 2 * p.N + which * p.N + n0 + c] = v;
+      float* dst = p.partials + (int64_t)blockIdx.x * 2 * p.N + which * p.N + n0 + c;
+      if (n0 + c < p.N) {
+        if (p.fin_counter) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+        else *dst = v;
+      }
+    }
+    if (p.fin_counter) {
+      __syncthreads();  // (red is reused as the finalize scratch)
+      bn_fin_last_block<NTHR>(p, gridDim.x, reinterpret_cast<char*>(sm));
     }
   }
 }
@@ -579,11 +665,11 @@ __global__ __launch_bounds__(128 * CW, 1) void conv3x3_x3ws_kernel(const X3Args 
 
 extern int g_x3_wres;
 int g_x3_ws = 0;  // knob "conv_split_ws": stride-1 256-pixel layers on the wave-specialised kernel (1: 4 + 4 waves,
-                  // 2: 8 + 8 waves)
+                  // 2: 8 + 8 waves, 3: 8 + 8 waves for the input gradients of frames wider than 8 only)
 
 template <int NI, int TH, int TW, bool FWD, int NP, int WCH, bool AB>
 static int launch_ws_k(const X3Args& a, int gx, int ny, hipStream_t st) {
-  if (g_x3_ws == 2)
+  if (g_x3_ws >= 2)
     VAD_KLAUNCH((conv3x3_x3ws_kernel<NI, TH, TW, 16, FWD, NP, WCH, AB, 8>), dim3(gx, ny), dim3(1024), 0, st, a);
   else
     VAD_KLAUNCH((conv3x3_x3ws_kernel<NI, TH, TW, 16, FWD, NP, WCH, AB, 4>), dim3(gx, ny), dim3(512), 0, st, a);
@@ -620,6 +706,8 @@ static int launch_ws(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
 }
 
 int g_x3_dgrad_blocks = 512;  // knob "conv_dgrad_blocks"
+int g_bn_fin_fused = 0;       // knob "bn_fin_fused": BatchNorm forward finalize inside the split conv kernels (measured
+                              // slower: +20 us/step at config 2, profiles/r02_bnfin_fused_ab.json)
 
 template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1, int NW = 4>
 static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
@@ -693,7 +781,8 @@ static int dispatch_x3_nt(const X3Args& a, int max_blocks, hipStream_t st, int* 
 template <int S, bool FWD>
 static int dispatch_x3(const X3Args& a, int max_blocks, hipStream_t st, int* nparts) {
   if constexpr (S == 1) {
-    if (g_x3_ws && g_x3_big) {
+    // (knob value 3: input gradients of frames wider than 8 only, on the 8 + 8-wave kernel)
+    if (g_x3_ws && g_x3_big && (g_x3_ws != 3 || (!FWD && a.OW > 8))) {
       if (a.OH <= 8 && a.OW <= 8) return launch_ws<4, 8, 8, FWD>(a, max_blocks, st, nparts);
       if (a.OW <= 16) return launch_ws<2, 8, 16, FWD>(a, max_blocks, st, nparts);
       return launch_ws<1, 8, 32, FWD>(a, max_blocks, st, nparts);
@@ -717,7 +806,7 @@ bool conv3_x3_supported(const Conv3Layer& L, bool fwd) {
 }
 
 int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
-                 float* y, float* partials, int* nparts, hipStream_t st) {
+                 float* y, float* partials, int* nparts, hipStream_t st, BnFinArgs* fin) {
   VAD_CHECK(conv3_x3_supported(L, true), "conv3_x3_fwd: unsupported layer");
   X3Args a{};
   a.src = src;
@@ -728,6 +817,17 @@ int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, 
   a.out = y;
   a.partials = partials;
   a.NF = L.NF; a.IH = L.IH; a.IW = L.IW; a.C = L.Ci; a.OH = L.OH; a.OW = L.OW; a.N = L.Co;
+  // in-kernel BN finalize (not on the opt-in wave-specialised stride-1 kernel)
+  if (fin && fin->counter && g_bn_fin_fused && !(L.stride == 1 && g_x3_ws && g_x3_big && g_x3_ws != 3)) {
+    a.fin_counter = fin->counter;
+    a.fin_gamma = fin->gamma;
+    a.fin_beta = fin->beta;
+    a.fin_rm = fin->running_mean;
+    a.fin_rv = fin->running_var;
+    a.fin_stats = fin->stats;
+    a.fin_count = fin->count;
+    fin->done = 1;
+  }
   // BN partial rows are bounded by conv3_patch_blocks (the caller's partial buffer)
   const int max_blocks = (int)std::min<int64_t>(conv3_patch_blocks(L.NF, L.OH, L.OW), 1 << 20);
   return L.stride == 1 ? dispatch_x3<1, true>(a, max_blocks, st, nparts) : dispatch_x3<2, true>(a, max_blocks, st, nparts);
