@@ -385,6 +385,13 @@ struct CadPlanImpl {
     VAD_HIP(hipStreamWaitEvent(st2, ev_fork, 0));
     return 0;
   }
+  // orders `st` after everything queued so far on the side stream (the stage-2 backward's head / detector grads)
+  int wait_side(hipStream_t st) {
+    VAD_TRY(streams());
+    VAD_HIP(hipEventRecord(ev_join, st2));
+    VAD_HIP(hipStreamWaitEvent(st, ev_join, 0));
+    return 0;
+  }
   int join(hipStream_t st) {
     VAD_HIP(hipEventRecord(ev_join, st2));
     VAD_HIP(hipStreamWaitEvent(st, ev_join, 0));
@@ -784,7 +791,7 @@ struct CadPlanImpl {
     const CadLayout& LY = layout();
     VAD_CHECK(grads != nullptr, "backward: grads not bound");
     VAD_CHECK(!use_loss || labels != nullptr, "backward(use_loss): forward ran without labels");
-    VAD_CHECK(stage >= -1 && stage <= 1, "backward: stage must be -1, 0 or 1");
+    VAD_CHECK(stage >= -1 && stage <= 2, "backward: stage must be -1, 0, 1 or 2");
     VAD_CHECK(bwd_state != 0 || stage != 1, "backward stage 1: stage 0 has not run for the current forward");
     // detector gate: knob "cad_det_gate" (0: the backbone waits for the side stream's event as before)
     const bool gate = g_cad_det_gate != 0 && det_gate != nullptr;
@@ -834,12 +841,15 @@ struct CadPlanImpl {
       TIMED("head_bwd", head_slab_reduce(slabs, B, slab_len, grads + LY.slots[LY.head0].offset, st));
       TIMED("head_bwd", head_rows_wgrad(head_args(), st));
     }
-    if (stage == 0) VAD_TRY(join(st));  // every non-backbone grad is final when stage 0 returns
+    // stage 0: every non-backbone grad is final on the caller's stream when it returns.  Stage 2 (= stage 0 for a
+    // caller that orders its own consumer after the side stream with vad_cad_wait_side): the head / detector chain
+    // keeps running on the side stream and the backbone (stage 1) waits only for the detector input gradient
+    if (stage == 0) VAD_TRY(join(st));
     else if (gate) VAD_HIP(hipStreamWaitValue64(st, det_gate, 1, hipStreamWaitValueEq, ~0ull));
     else VAD_HIP(hipStreamWaitEvent(st, ev_det, 0));
     }
-    bwd_state = 1;
-    if (stage == 0) return 0;
+    if (stage != 1) bwd_state = stage == 2 ? 2 : 1;
+    if (stage == 0 || stage == 2) return 0;
     // backbone (BatchNorm backward as streaming passes: the conv kernels are MFMA/LDS-bound and slowed down more by
     // extra loads than the separate 6 TB/s passes cost -- DESIGN.md §6, BN-backward fusion experiment)
     TIMED("avgpool_bwd", avgpool_bwd(d_feat_det, d_pooled, B, T, HF, WF, 256, dA, st));
@@ -894,7 +904,7 @@ struct CadPlanImpl {
       TIMED("stem_bwd", conv1_wgrad(x_last, NF, H, W, stem_d, H1, W1, wpart, wpart_floats, G(LY.conv1_w), st));
       stem_active = 1;
     }
-    if (stage == -1) VAD_TRY(join(st));  // the head's weight grads (side stream)
+    if (stage == -1 || bwd_state == 2) VAD_TRY(join(st));  // the head's weight grads (side stream)
     return 0;
   }
 
@@ -1115,6 +1125,11 @@ int vad_cad_backward_stage(vad_cad_plan* plan, int stage, int use_loss, const fl
   VAD_CHECK(plan != nullptr, "vad_cad_backward_stage: null plan");
   return plan->impl.backward(use_loss != 0, d_final, d_probs, d_causal, d_kl, d_z, d_adj, (hipStream_t)stream,
                              stage);
+}
+
+int vad_cad_wait_side(vad_cad_plan* plan, void* stream) {
+  VAD_CHECK(plan != nullptr, "vad_cad_wait_side: null plan");
+  return plan->impl.wait_side((hipStream_t)stream);
 }
 
 int vad_cad_backward_ext(vad_cad_plan* plan, int stage, int use_loss, const float* d_final, const float* d_probs,

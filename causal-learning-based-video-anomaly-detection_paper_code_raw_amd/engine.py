@@ -232,7 +232,8 @@ class CadEngine:
     def backward(self, use_loss: bool, d_final=None, d_probs=None, d_causal=None, d_kl=None, d_z=None, d_adj=None,
                  stage: int = -1, d_boxes=None):
         """stage -1: whole backward; 0: everything but the backbone (grads outside [0, backbone_floats) final);
-        1: the backbone (after stage 0).  d_boxes: grad of the (B, T, 5, 4) detections output."""
+        1: the backbone (after stage 0 or 2); 2: stage 0 whose causal-head / detector grads finish on the plan's side
+        stream (order a consumer after them with wait_side).  d_boxes: grad of the (B, T, 5, 4) detections output."""
         pl, lab, _ = self._last
         self._set_stem_grad(pl)
         c = [t.contiguous() if t is not None else None for t in (d_final, d_probs, d_causal, d_kl, d_z, d_adj)]
@@ -247,6 +248,12 @@ class CadEngine:
         else:
             nat.check(nat.lib().vad_cad_backward_stage(pl.h, stage, 1 if use_loss else 0, *[nat.ptr(t) for t in c],
                                                        nat.stream_of(self.device)))
+
+    def wait_side(self, stream):
+        """Make `stream` (a torch.cuda.Stream) wait for everything queued so far on the last plan's side stream (the
+        stage-2 backward's head / detector grads)."""
+        pl = self._last[0]
+        nat.check(nat.lib().vad_cad_wait_side(pl.h, ctypes.c_void_p(stream.cuda_stream)))
 
     STEM = ("backbone.conv1.weight", "backbone.conv1.bias", "backbone.bn1.weight", "backbone.bn1.bias")
 

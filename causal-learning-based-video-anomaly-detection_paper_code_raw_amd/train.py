@@ -86,7 +86,8 @@ class CadTrainer:
     def _backward_overlapped(self):
         """Backward in two stages with the gradient all-reduce split at the backbone boundary: the head / classifier
         / detector grads (+ has-grad flags; ~85 % of the bytes) are summed on a side stream while the backbone
-        backward runs on the compute stream, then the backbone grads; the optimizer waits for both.  Each element
+        backward runs on the compute stream (it waits only for the detector's input gradient, not for the whole
+        causal-head backward), then the backbone grads; the optimizer waits for both.  Each element
         is summed over the same ranks as the single all_reduce."""
         eng = self.eng
         main = torch.cuda.current_stream(eng.device)
@@ -94,7 +95,10 @@ class CadTrainer:
             self._comm = torch.cuda.Stream(eng.device)
         side = self._comm
         nb = eng.backbone_floats
-        eng.backward(True, stage=0)
+        # stage 2: the causal-head / detector backward keeps running on the plan's side stream while the backbone
+        # (stage 1) starts; the all-reduce stream waits for both that side stream and the compute stream
+        eng.backward(True, stage=2)
+        eng.wait_side(side)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             dist.all_reduce(eng.grads[nb:], group=self.pg)

@@ -85,6 +85,12 @@ int vad_cad_backward(vad_cad_plan* plan, int use_loss, const float* d_final, con
 int vad_cad_backward_stage(vad_cad_plan* plan, int stage, int use_loss, const float* d_final, const float* d_probs,
                            const float* d_causal, const float* d_kl, const float* d_z, const float* d_adj,
                            void* stream);
+/* stage 2 of vad_cad_backward_stage is stage 0 for a caller that orders its own consumer of the non-backbone grads
+ * itself: it returns as soon as the caller's stream has its part queued, the causal head / detector backward keeps
+ * running on the plan's side stream, and stage 1 (the backbone) then waits only for the detector's input gradient;
+ * vad_cad_wait_side(plan, s) makes stream s wait for everything queued so far on that side stream (a data-parallel
+ * caller's all-reduce stream, before it sums those grads).  Stage 1 after stage 2 re-joins the side stream. */
+int vad_cad_wait_side(vad_cad_plan* plan, void* stream);
 /* vad_cad_backward_stage with one more upstream grad: d_boxes [B,T,5,4] (may be NULL), the grad of a loss on the
  * forward's compacted per-frame detections (boxes output of vad_cad_forward; the reference's detections are slices
  * of the rescaled detector output and carry autograd, cad:201-222).  The constant fallback box takes no grad. */

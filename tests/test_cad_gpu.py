@@ -345,6 +345,33 @@ def test_staged_backward_equals_whole_backward():
     assert torch.equal(eng.grads[:eng.param_floats + 2], grads[:eng.param_floats + 2])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("ci", [0, 1])
+def test_stage2_backward_equals_whole_backward(ci):
+    """Stage 2 (the head / detector backward left running on the plan's side stream, the backbone gated on the
+    detector's input gradient only) + wait_side + stage 1 write the same grads, bit for bit, as one backward: in the
+    fallback regime (no box in range: the backbone does not wait for the causal head) and the forced one (it waits
+    for the detector's input gradient)."""
+    case = CASES[ci]
+    m, eng, o, grads, tn = _hip_step(case, step_opt=False)
+    B, T, H, W = case["B"], case["T"], case["H"], case["W"]
+    x = co.synth_clips(case["seed"], case["step"], 0, B, T, H, W).cuda()
+    y = co.synth_labels(0, B).cuda()
+    eng.forward(x, True, case["seed"], case["step"], 0, y)
+    eng.backward(True, stage=2)
+    side = torch.cuda.Stream()
+    eng.wait_side(side)
+    side.wait_stream(torch.cuda.current_stream())
+    nb = eng.backbone_floats
+    with torch.cuda.stream(side):
+        head = eng.grads[nb:eng.param_floats + 2].clone()
+    eng.backward(True, stage=1)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert torch.equal(head, grads[nb:eng.param_floats + 2])
+    assert torch.equal(eng.grads[:eng.param_floats + 2], grads[:eng.param_floats + 2])
+
+
 def test_module_api_detection_grads():
     """Detections carry autograd as in the reference (cad:201-222: each frame's boxes are slices of the rescaled
     detector output; the fallback box is a constant): a loss on out["detections"] trains the detector and the
