@@ -29,6 +29,10 @@ def family(name):
         return "conv_fwd" if _targs(name)[6:7] == ["true"] else "conv_dgrad"
     if "conv3x3_patch_kernel" in name:
         return "conv_fwd" if "true" in _targs(name) else "conv_dgrad"
+    if "conv3x3_x3ws_kernel" in name:  # <NI, TH, TW, PC, FWD, ...>
+        return "conv_fwd" if _targs(name)[4:5] == ["true"] else "conv_dgrad"
+    if "conv3x3_dgrad_s2x3_kernel" in name:
+        return "conv_dgrad"
     if "conv3x3_dgrad_s2_kernel" in name or ("gemm_kernel" in name and "EpiConvDgrad" in name):
         return "conv_dgrad"
     if "gemm_kernel" in name and "EpiConvFwd" in name:
