@@ -9,6 +9,7 @@
 namespace vad {
 
 int g_cad_prep_stream = 1;   // knob "cad_prep_stream": weight relayouts on the plan's side stream (A/B measurement)
+int g_cad_last_wgrad_main = 1;  // knob "cad_last_wgrad_main": layer 0's weight gradient on the caller's stream
 int g_cad_det_gate = 1;      // knob "cad_det_gate": the backbone backward waits on the device detector gate
 int g_cad_wgrad_stream = 1;  // knob "cad_wgrad_stream": backbone weight gradients on their own stream
 int g_dbg_skip_bnred = 0;    // knob "dbg_skip_bnred" (measurement only, results wrong): bit 1 skips the BN backward
@@ -969,6 +970,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "cad_det_gate") g_cad_det_gate = value;
+  else if (k == "cad_last_wgrad_main") g_cad_last_wgrad_main = value;
   else if (k == "dbg_skip_bnred") g_dbg_skip_bnred = value;
   else if (k == "head_dbg") g_head_dbg = value;
   else if (k == "stem_dbg") g_stem_dbg = value;

@@ -869,18 +869,24 @@ struct CadPlanImpl {
       const float* src = l == 0 ? pool : y[l - 1];
       const float* sst = l == 0 ? pool_stats : stats[l];
       {
+        // layer 0 with the frozen stem: nothing follows its weight gradient on the caller's stream, so it runs there
+        // (after layer 1's weight gradient has released the slab) -- no cross-queue hand-off of dY0 and no join
+        // behind it before the optimizer
+        const bool on_main = wgs && l == 0 && !stem_grad && g_cad_last_wgrad_main;
         hipStream_t wst = st;
-        if (wgs) {
+        if (wgs && !on_main) {
           VAD_HIP(hipEventRecord(ev_dy[l & 1], st));
           VAD_HIP(hipStreamWaitEvent(st3, ev_dy[l & 1], 0));
           wst = st3;
+        } else if (on_main) {
+          VAD_HIP(hipStreamWaitEvent(st, ev_wg[1], 0));  // layer 1's weight gradient + slab reduce are done
         }
         hipStream_t st = wst;
         int ns = 0;
         // (layer 0 with the frozen stem: nothing runs beside its weight gradient)
         TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dYl, src, sst, wpart, &ns, wpart_floats, st, l == 0 && !stem_grad));
         TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], wpart, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
-        if (wgs) VAD_HIP(hipEventRecord(ev_wg[l & 1], st));
+        if (wgs && !on_main) VAD_HIP(hipEventRecord(ev_wg[l & 1], st));
       }
       if (l > 0) TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st));
       if (l == debug_stop_layer) break;
