@@ -3,6 +3,7 @@
 // Reference semantics: ResNetBackbone (causal_anomaly_detection.py:110-158), nn.BatchNorm2d train mode,
 // nn.MaxPool2d(3,2,1), nn.AdaptiveAvgPool2d((4,6)), nn.Linear / ReLU / Dropout stacks (cad:167-179, 525-538).
 #include "backbone.h"
+#include "mlp.h"
 #include "gemm.h"
 #include "head.h"
 
@@ -970,6 +971,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "cad_det_gate") g_cad_det_gate = value;
+  else if (k == "mlp_tail_wide") g_mlp_tail_wide = value;
   else if (k == "cad_last_wgrad_main") g_cad_last_wgrad_main = value;
   else if (k == "dbg_skip_bnred") g_dbg_skip_bnred = value;
   else if (k == "head_dbg") g_head_dbg = value;

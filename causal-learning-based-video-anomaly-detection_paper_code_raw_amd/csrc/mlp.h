@@ -45,6 +45,7 @@ struct MlpTailBwdArgs {
   const int* skip;     // nullable device flag: 0 -> no-op
 };
 
+extern int g_mlp_tail_wide;  // knob "mlp_tail_wide"
 int mlp_tail_fwd(const MlpTailArgs& a, hipStream_t st);
 int mlp_tail_bwd(const MlpTailBwdArgs& a, hipStream_t st);
 

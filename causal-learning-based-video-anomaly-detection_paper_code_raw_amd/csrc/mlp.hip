@@ -22,15 +22,16 @@ __device__ __forceinline__ float mlp_finish(const MlpLayer& L, int64_t grow, int
 // layers 1-4 for RB rows; h0 (layer-0 output, finished by the split-K reduce) is read from global.  Thread t of a
 // layer owns 4 consecutive outputs g = t % (N/4) over the K-slice p = t / (N/4): float4 loads of the transposed
 // weight WT[k][4g..4g+3] (coalesced across g), 8 in flight; the K-slices are combined in a fixed order in LDS.
-template <int RB>
-__global__ __launch_bounds__(256) void mlp_tail_fwd_kernel(const MlpTailArgs a) {
+// NTH = 1024 (knob mlp_tail_wide) gives each layer 4x the K-slices of 256; measured no faster, so 256 is the default.
+template <int RB, int NTH>
+__global__ __launch_bounds__(NTH) void mlp_tail_fwd_kernel(const MlpTailArgs a) {
   __shared__ __attribute__((aligned(16))) float buf[2][RB][MLP_MAXW];
-  __shared__ __attribute__((aligned(16))) float red[256 * 4 * RB];
+  __shared__ __attribute__((aligned(16))) float red[NTH * 4 * RB];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * RB;
   {
     const int N = a.L[0].N;
-    for (int idx = tid; idx < RB * N; idx += 256) {
+    for (int idx = tid; idx < RB * N; idx += NTH) {
       const int r = idx / N, n = idx % N, row = r0 + r;
       buf[0][r][n] = row < a.M ? a.L[0].out[(int64_t)row * N + n] : 0.f;
     }
@@ -42,7 +43,7 @@ __global__ __launch_bounds__(256) void mlp_tail_fwd_kernel(const MlpTailArgs a) 
     const float(*in)[MLP_MAXW] = buf[(i - 1) & 1];
     float(*outb)[MLP_MAXW] = buf[i & 1];
     const int K = L.K, N = L.N, NG = N / 4;
-    const int P = 256 / NG;
+    const int P = NTH / NG;
     const int kper = ((K + P - 1) / P + 7) & ~7;
     const float* WT = a.WT[i];
     if (tid < NG * P) {
@@ -70,7 +71,7 @@ __global__ __launch_bounds__(256) void mlp_tail_fwd_kernel(const MlpTailArgs a) 
       for (int r = 0; r < RB; ++r) *reinterpret_cast<f32x4*>(&red[(p * RB + r) * N + 4 * g]) = acc[r];
     }
     __syncthreads();
-    for (int idx = tid; idx < RB * N; idx += 256) {
+    for (int idx = tid; idx < RB * N; idx += NTH) {
       const int r = idx / N, n = idx % N, row = r0 + r;
       float sum = 0.f;
       for (int p = 0; p < P; ++p) sum += red[(p * RB + r) * N + n];
@@ -228,16 +229,21 @@ int rows_wgrad(const RowsWgradArgs& a, hipStream_t st) {
 
 static int mlp_rb(int M) { return M >= 64 ? 4 : 8; }
 
+int g_mlp_tail_wide = 0;  // knob "mlp_tail_wide": 1024-thread blocks for the detector's layers 1-4 (4-row blocks;
+                          // measured no faster: 30.6 us either way at config 2)
+
 int mlp_tail_fwd(const MlpTailArgs& a, hipStream_t st) {
   for (int i = 1; i < 5; ++i)
     VAD_CHECK(a.L[i].N <= MLP_MAXW && a.L[i].N % 4 == 0 && a.L[i].N / 4 <= 256 && a.L[i].K <= MLP_MAXW &&
                   a.L[i].K % 8 == 0 && a.WT[i],
               "mlp_tail_fwd: layer shape");
   const int rb = mlp_rb(a.M);
-  if (rb == 4)
-    hipLaunchKernelGGL(mlp_tail_fwd_kernel<4>, dim3((unsigned)cdiv(a.M, 4)), dim3(256), 0, st, a);
+  if (rb == 4 && g_mlp_tail_wide)
+    hipLaunchKernelGGL((mlp_tail_fwd_kernel<4, 1024>), dim3((unsigned)cdiv(a.M, 4)), dim3(1024), 0, st, a);
+  else if (rb == 4)
+    hipLaunchKernelGGL((mlp_tail_fwd_kernel<4, 256>), dim3((unsigned)cdiv(a.M, 4)), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(mlp_tail_fwd_kernel<8>, dim3((unsigned)cdiv(a.M, 8)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((mlp_tail_fwd_kernel<8, 256>), dim3((unsigned)cdiv(a.M, 8)), dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   return 0;
 }
