@@ -333,6 +333,7 @@ struct CadPlanImpl {
   // the word (hipStreamWaitValue64) instead of on the whole causal-head backward.
   uint64_t* det_gate = nullptr;
   int* fin_counters = nullptr;  // tickets of the in-kernel BN finalize of the 8 conv layers (zeroed per forward)
+  int grads_zeroed = 0;  // the last forward cleared the grad buffer for the backward that follows it
   float *d_causal, *d_kl, *d_glog, *d_dlog, *slabs, *d_feat_det, *d_pooled, *dense_scratch, *dense_scratch2;
   float *dg[5], *ddh[5];
   float *dA, *dY, *dY2, *wpart, *stem_d;  // stem_d: [NF][H1][W1][32], the stem backward's dA / dY (stem_grad only)
@@ -742,6 +743,13 @@ struct CadPlanImpl {
     // the detector's input gradient buffer is zero unless its backward writes it (the backward skips it on device when
     // no box was in range); cleared here, where the main stream has slack
     VAD_HIP(hipMemsetAsync(d_feat_det, 0, sizeof(float) * (size_t)NF * 6144, st));
+    // (train mode: the backward's grad buffer is cleared here too, off its critical path; the backward clears it
+    // itself when the forward did not)
+    grads_zeroed = 0;
+    if (training && grads) {
+      VAD_HIP(hipMemsetAsync(grads, 0, sizeof(float) * layout().param_floats, st));
+      grads_zeroed = 1;
+    }
     {  // side stream: the causal head on the detections
       hipStream_t st = st2;
       if (!(g_dbg_skip_bnred & 2)) TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
@@ -797,7 +805,8 @@ struct CadPlanImpl {
     const bool gate = g_cad_det_gate != 0 && det_gate != nullptr;
     if (stage != 1) {
     // grads of frozen / never-used slots stay zero
-    VAD_HIP(hipMemsetAsync(grads, 0, sizeof(float) * LY.param_floats, st));
+    if (!grads_zeroed) VAD_HIP(hipMemsetAsync(grads, 0, sizeof(float) * LY.param_floats, st));
+    grads_zeroed = 0;
     TailArgs t = use_loss ? tail_args(nullptr, nullptr, nullptr, nullptr) : tail_args(dfin, dprobs, dcaus, dkl);
     if (!use_loss) t.labels = nullptr;
     TIMED("tail", cad_tail_bwd(t, st));
