@@ -366,17 +366,21 @@ struct CadPlanImpl {
   int wgrad_stream = 1;  // option "wgrad_stream" (0: weight gradients on the caller's stream)
   int streams() {
     if (!st2) {
+      // the plan's events only order its own queues on this device (stream waits, never host inspection): an
+      // agent-scope release suffices, so the system-scope fence at each record is dropped (knob
+      // "cad_event_sysfence" = 1 restores it)
+      const unsigned evf = hipEventDisableTiming | (g_cad_event_sysfence ? 0u : (unsigned)hipEventDisableSystemFence);
       VAD_HIP(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
-      VAD_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-      VAD_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-      VAD_HIP(hipEventCreateWithFlags(&ev_det, hipEventDisableTiming));
+      VAD_HIP(hipEventCreateWithFlags(&ev_fork, evf));
+      VAD_HIP(hipEventCreateWithFlags(&ev_join, evf));
+      VAD_HIP(hipEventCreateWithFlags(&ev_det, evf));
       VAD_HIP(hipStreamCreateWithFlags(&st3, hipStreamNonBlocking));
       for (int b = 0; b < 2; ++b) {
-        VAD_HIP(hipEventCreateWithFlags(&ev_dy[b], hipEventDisableTiming));
-        VAD_HIP(hipEventCreateWithFlags(&ev_wg[b], hipEventDisableTiming));
+        VAD_HIP(hipEventCreateWithFlags(&ev_dy[b], evf));
+        VAD_HIP(hipEventCreateWithFlags(&ev_wg[b], evf));
       }
-      VAD_HIP(hipEventCreateWithFlags(&ev_wgj, hipEventDisableTiming));
-      VAD_HIP(hipEventCreateWithFlags(&ev_prep, hipEventDisableTiming));
+      VAD_HIP(hipEventCreateWithFlags(&ev_wgj, evf));
+      VAD_HIP(hipEventCreateWithFlags(&ev_prep, evf));
     }
     return 0;
   }
