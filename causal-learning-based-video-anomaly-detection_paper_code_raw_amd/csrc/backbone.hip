@@ -12,6 +12,7 @@ namespace vad {
 int g_cad_prep_stream = 1;   // knob "cad_prep_stream": weight relayouts on the plan's side stream (A/B measurement)
 int g_cad_last_wgrad_main = 1;  // knob "cad_last_wgrad_main": layer 0's weight gradient on the caller's stream
 int g_cad_event_sysfence = 0;  // knob "cad_event_sysfence": system-scope fence on the plan's stream-order events
+int g_cad_dy_per_layer = 1;  // knob "cad_dy_per_layer" (A/B of the plan option dy_per_layer)
 int g_cad_det_gate = 1;      // knob "cad_det_gate": the backbone backward waits on the device detector gate
 int g_cad_wgrad_stream = 1;  // knob "cad_wgrad_stream": backbone weight gradients on their own stream
 int g_dbg_skip_bnred = 0;    // knob "dbg_skip_bnred" (measurement only, results wrong): bit 1 skips the BN backward
@@ -972,6 +973,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "cad_det_gate") g_cad_det_gate = value;
+  else if (k == "cad_dy_per_layer") g_cad_dy_per_layer = value;
   else if (k == "cad_event_sysfence") g_cad_event_sysfence = value;
   else if (k == "mlp_tail_wide") g_mlp_tail_wide = value;
   else if (k == "cad_last_wgrad_main") g_cad_last_wgrad_main = value;

@@ -337,6 +337,11 @@ struct CadPlanImpl {
   float *d_causal, *d_kl, *d_glog, *d_dlog, *slabs, *d_feat_det, *d_pooled, *dense_scratch, *dense_scratch2;
   float *dg[5], *ddh[5];
   float *dA, *dY, *dY2, *wpart, *stem_d;  // stem_d: [NF][H1][W1][32], the stem backward's dA / dY (stem_grad only)
+  // per-layer dY buffers (option "dy_per_layer", default on): layer l's BN backward writes dYL[l], which only layer l's
+  // weight and input gradients read, so the compute stream never waits for the weight-gradient stream to release a
+  // shared dY buffer (one cross-queue barrier per layer less); ~2x the dY memory (≈210 MB at config 2)
+  float* dYL[8] = {};
+  int dy_per_layer = 1;
   float *sq_parts, *slot_info, *clip;
   int16_t* chunk_slot;
   int64_t parts_floats, dense_scratch_floats, wpart_floats, slab_len, act_max;
@@ -490,6 +495,7 @@ struct CadPlanImpl {
     dA = w.take<float>(act_max);
     dY = w.take<float>(act_max);
     dY2 = w.take<float>(act_max);
+    for (int l = 0; l < 8; ++l) dYL[l] = w.take<float>(nf * L[l].OH * L[l].OW * L[l].Co);
     stem_d = w.take<float>(nf * H1 * W1 * 32);
     wpart_floats = 16ll << 20;
     wpart = w.take<float>(wpart_floats);
@@ -872,12 +878,13 @@ struct CadPlanImpl {
       const int64_t M = (int64_t)NF * L[l].OH * L[l].OW;
       const int C = L[l].Co;
       int np = 0, nb = 0;
-      float* dYl = (l & 1) ? dY2 : dY;
+      const bool perl = dy_per_layer != 0 && g_cad_dy_per_layer != 0;
+      float* dYl = perl ? dYL[l] : ((l & 1) ? dY2 : dY);
       if ((g_dbg_skip_bnred & 1) && l < 7) np = 1;  // measurement only (knob "dbg_skip_bnred": results wrong)
       else TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st));
       VAD_TRY(bn_bwd_stats(l + 1, np, C, (double)M, P(LY.bn_w[l]), G(LY.bn_w[l]), G(LY.bn_b[l]), G(LY.conv_b[l]), st));
       // dYl was last read by layer l+2's weight gradient
-      if (wgs && l + 2 <= 7) VAD_HIP(hipStreamWaitEvent(st, ev_wg[l & 1], 0));
+      if (wgs && l + 2 <= 7 && !perl) VAD_HIP(hipStreamWaitEvent(st, ev_wg[l & 1], 0));
       TIMED(L_("bn_bwd_apply", l), bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dYl, nullptr, &nb, st));
       const float* src = l == 0 ? pool : y[l - 1];
       const float* sst = l == 0 ? pool_stats : stats[l];
@@ -913,7 +920,7 @@ struct CadPlanImpl {
       VAD_CHECK(y1_fresh, "stem backward: the forward ran with the stem frozen (set option stem_grad before it)");
       // the stem (cad:145-147): input gradient of layer1.0 into the pooled map, MaxPool2d backward, bn1 backward (in
       // place), conv1 weight gradient (its bias gradient comes from the bn1 finalize)
-      TIMED("stem_bwd", conv3_dgrad(L[0], dY, wd[0], dA, st));
+      TIMED("stem_bwd", conv3_dgrad(L[0], (dy_per_layer && g_cad_dy_per_layer) ? dYL[0] : dY, wd[0], dA, st));
       TIMED("stem_bwd", maxpool3s2_bwd(y1, stats[0], dA, NF, H1, W1, 32, HP, WP, stem_d, st));
       const int64_t M1 = (int64_t)NF * H1 * W1;
       int np = 0, nb = 0;
@@ -1180,7 +1187,12 @@ int vad_cad_debug_buffer(vad_cad_plan* plan, const char* name, int idx, void** p
   else if (n == "feats") { *ptr = c.feats; *nfloats = NF * 6144; }
   else if (n == "pooled") { *ptr = c.pooled; *nfloats = (int64_t)c.B * 6144; }
   else if (n == "dA") { *ptr = c.dA; *nfloats = c.act_max; }
-  else if (n == "dY") { *ptr = (c.debug_stop_layer & 1) ? c.dY2 : c.dY; *nfloats = c.act_max; }
+  else if (n == "dY") {
+    const int l = c.debug_stop_layer;
+    const bool perl = c.dy_per_layer && g_cad_dy_per_layer && l >= 0 && l < 8;
+    *ptr = perl ? c.dYL[l] : ((l & 1) ? c.dY2 : c.dY);
+    *nfloats = perl ? (int64_t)c.NF * c.L[l].OH * c.L[l].OW * c.L[l].Co : c.act_max;
+  }
   else if (n == "act_bf16") { *ptr = nullptr; *nfloats = c.act_bf16; }  // storage of pool / y / dA / dY
   else if (n == "d_pooled") { *ptr = c.d_pooled; *nfloats = (int64_t)c.B * 6144; }
   else if (n == "d_feat_det") { *ptr = c.d_feat_det; *nfloats = NF * 6144; }
@@ -1202,6 +1214,7 @@ int vad_cad_set_option(vad_cad_plan* plan, const char* key, int64_t value) {
   if (std::string(key) == "conv_bf16") plan->impl.conv_bf16 = value ? 1 : 0;
   else if (std::string(key) == "stem_grad") plan->impl.stem_grad = value ? 1 : 0;
   else if (std::string(key) == "wgrad_stream") plan->impl.wgrad_stream = value ? 1 : 0;
+  else if (std::string(key) == "dy_per_layer") plan->impl.dy_per_layer = value ? 1 : 0;
   else if (std::string(key) == "act_bf16") plan->impl.act_bf16_opt = value ? 1 : 0;
   else { vad::set_error("vad_cad_set_option: unknown key"); return 1; }
   return 0;
