@@ -34,7 +34,7 @@ int maxpool3s2_bwd(const float* y, const float* stats, const float* dpool, int N
 // partials: [P][2*C] (sum | sumsq).  Writes mean/invstd/scale/shift [C] and updates running stats.
 int bn_finalize(const float* partials, int P, int C, double count, const float* gamma, const float* beta,
                 float* running_mean, float* running_var, float momentum, float eps, int training, float* stats,
-                hipStream_t st);
+                hipStream_t st, int cm = 0);  // cm: partials column-major [2C][P] (the fused stem's)
 // stats layout per layer (BN_STATS_PER_C = 7): [0:C) mean, [C:2C) invstd, [2C:3C) scale, [3C:4C) shift,
 //   [4C:5C) k (bwd), [5C:6C) mean(dZ), [6C:7C) mean(dZ*xhat)
 int bn_bwd_reduce(const float* dA, const float* y, const float* stats, int M, int C, float* partials, int* nparts,
@@ -49,7 +49,8 @@ int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int
 int bn_rows_parts(int M, int C);
 // SyncBatchNorm: [P][2C] partials -> [2C] double sums (+ optional float copies of the two halves); finalize from
 // (all-reduced) sums over `count` elements of the whole process group
-int bn_sum_partials(const float* partials, int P, int C, double* sums, float* a_out, float* b_out, hipStream_t st);
+int bn_sum_partials(const float* partials, int P, int C, double* sums, float* a_out, float* b_out, hipStream_t st,
+                    int cm = 0);
 int bn_finalize_sums(const double* sums, int C, double count, const float* gamma, const float* beta,
                      float* running_mean, float* running_var, float momentum, float eps, float* stats,
                      hipStream_t st);

@@ -287,14 +287,16 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const PT* __restrict__
                                                           double count, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* running_mean,
                                                           float* running_var, float momentum, float eps,
-                                                          int training, float* __restrict__ stats) {
+                                                          int training, float* __restrict__ stats, int cm) {
   const int c = blockIdx.x;
   __shared__ double red[2][256];
   double a = 0.0, b = 0.0;
+  // partials row-major [P][2C], or column-major [2C][P] (cm: the fused stem's layout, coalesced here)
+  const int64_t rs = cm ? 1 : 2 * C, ia = cm ? (int64_t)c * P : c, ib = cm ? (int64_t)(C + c) * P : C + c;
   if (training) {
     for (int p = threadIdx.x; p < P; p += 256) {
-      a += (double)partials[(int64_t)p * 2 * C + c];
-      b += (double)partials[(int64_t)p * 2 * C + C + c];
+      a += (double)partials[p * rs + ia];
+      b += (double)partials[p * rs + ib];
     }
   }
   red[0][threadIdx.x] = a;
@@ -330,9 +332,9 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const PT* __restrict__
 
 int bn_finalize(const float* partials, int P, int C, double count, const float* gamma, const float* beta,
                 float* running_mean, float* running_var, float momentum, float eps, int training, float* stats,
-                hipStream_t st) {
+                hipStream_t st, int cm) {
   hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3(C), dim3(256), 0, st, partials, P, C, count, gamma, beta,
-                     running_mean, running_var, momentum, eps, training, stats);
+                     running_mean, running_var, momentum, eps, training, stats, cm);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -341,7 +343,7 @@ int bn_finalize_sums(const double* sums, int C, double count, const float* gamma
                      float* running_mean, float* running_var, float momentum, float eps, float* stats,
                      hipStream_t st) {
   hipLaunchKernelGGL(bn_finalize_kernel<double>, dim3(C), dim3(256), 0, st, sums, 1, C, count, gamma, beta,
-                     running_mean, running_var, momentum, eps, 1, stats);
+                     running_mean, running_var, momentum, eps, 1, stats, 0);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -350,13 +352,14 @@ int bn_finalize_sums(const double* sums, int C, double count, const float* gamma
 // all-reduces across ranks); optionally also writes them as float to a_out / b_out (the local dbeta / dgamma)
 __global__ __launch_bounds__(256) void bn_sum_partials_kernel(const float* __restrict__ partials, int P, int C,
                                                               double* __restrict__ sums, float* a_out,
-                                                              float* b_out) {
+                                                              float* b_out, int cm) {
   const int c = blockIdx.x;
   __shared__ double red[2][256];
   double a = 0.0, b = 0.0;
+  const int64_t rs = cm ? 1 : 2 * C, ia = cm ? (int64_t)c * P : c, ib = cm ? (int64_t)(C + c) * P : C + c;
   for (int p = threadIdx.x; p < P; p += 256) {
-    a += (double)partials[(int64_t)p * 2 * C + c];
-    b += (double)partials[(int64_t)p * 2 * C + C + c];
+    a += (double)partials[p * rs + ia];
+    b += (double)partials[p * rs + ib];
   }
   red[0][threadIdx.x] = a;
   red[1][threadIdx.x] = b;
@@ -376,8 +379,9 @@ __global__ __launch_bounds__(256) void bn_sum_partials_kernel(const float* __res
   }
 }
 
-int bn_sum_partials(const float* partials, int P, int C, double* sums, float* a_out, float* b_out, hipStream_t st) {
-  hipLaunchKernelGGL(bn_sum_partials_kernel, dim3(C), dim3(256), 0, st, partials, P, C, sums, a_out, b_out);
+int bn_sum_partials(const float* partials, int P, int C, double* sums, float* a_out, float* b_out, hipStream_t st,
+                    int cm) {
+  hipLaunchKernelGGL(bn_sum_partials_kernel, dim3(C), dim3(256), 0, st, partials, P, C, sums, a_out, b_out, cm);
   VAD_LAUNCH_CHECK();
   return 0;
 }

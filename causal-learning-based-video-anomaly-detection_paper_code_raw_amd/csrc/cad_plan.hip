@@ -638,13 +638,14 @@ struct CadPlanImpl {
 
   // batch statistics of BN layer i (0 = bn1) from the `np` partials in `parts`: local (default) or, with a sync
   // callback in training mode, over the whole process group (torch.nn.SyncBatchNorm semantics)
-  int bn_fwd_stats(int i, int np, int C, double count, const float* gamma, const float* beta, hipStream_t st) {
+  int bn_fwd_stats(int i, int np, int C, double count, const float* gamma, const float* beta, hipStream_t st,
+                   int cm = 0) {
     if (sync_fn == nullptr || !training) {
       TIMED("bn_fin", bn_finalize(parts, np, C, count, gamma, beta, RM(i), RV(i), 0.1f, 1e-5f, training, stats[i],
-                                  st));
+                                  st, cm));
       return 0;
     }
-    TIMED("bn_fin", bn_sum_partials(parts, np, C, bnsync, nullptr, nullptr, st));
+    TIMED("bn_fin", bn_sum_partials(parts, np, C, bnsync, nullptr, nullptr, st, cm));
     VAD_CHECK(sync_fn(sync_user, i, 0, 2 * C, st) == 0, "BatchNorm sync callback failed (forward)");
     TIMED("bn_fin", bn_finalize_sums(bnsync, C, count * sync_world, gamma, beta, RM(i), RV(i), 0.1f, 1e-5f, stats[i],
                                      st));
@@ -693,7 +694,7 @@ struct CadPlanImpl {
       // `pool` then holds the pooled conv1 output and layer1.0 applies bn1 + ReLU on load
       TIMED("conv1", stem_fused(x, NF, H, W, P(LY.conv1_w), P(LY.conv1_b), P(LY.bn1_w), H1, W1, pool, HP, WP, parts,
                                 &np, st));
-      VAD_TRY(bn_fwd_stats(0, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), st));
+      VAD_TRY(bn_fwd_stats(0, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), st, 1));  // column-major
       pool_stats = stats[0];
     } else {
       // training stem: the backward's MaxPool / bn1 / conv1 gradients read conv1's output y1
@@ -874,6 +875,7 @@ struct CadPlanImpl {
     TIMED("avgpool_bwd", avgpool_bwd(d_feat_det, d_pooled, B, T, HF, WF, 256, dA, st));
     VAD_TRY(streams());
     const bool wgs = wgrad_stream != 0 && g_cad_wgrad_stream;
+    bool st3_joined = false;
     for (int l = 7; l >= 0; --l) {
       const int64_t M = (int64_t)NF * L[l].OH * L[l].OW;
       const int C = L[l].Co;
@@ -900,6 +902,7 @@ struct CadPlanImpl {
           wst = st3;
         } else if (on_main) {
           VAD_HIP(hipStreamWaitEvent(st, ev_wg[1], 0));  // layer 1's weight gradient + slab reduce are done
+          st3_joined = true;  // (the weight-gradient stream's last work)
         }
         hipStream_t st = wst;
         int ns = 0;
@@ -911,7 +914,7 @@ struct CadPlanImpl {
       if (l > 0) TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st));
       if (l == debug_stop_layer) break;
     }
-    if (wgs) {  // every weight gradient is final before the stem backward / optimizer on the caller's stream
+    if (wgs && !st3_joined) {  // every weight gradient is final before the stem backward / optimizer
       VAD_HIP(hipEventRecord(ev_wgj, st3));
       VAD_HIP(hipStreamWaitEvent(st, ev_wgj, 0));
     }

@@ -232,7 +232,8 @@ __global__ __launch_bounds__(256, 4) void stem_fused_kernel(const float* __restr
   __syncthreads();
   if (threadIdx.x < 64) {
     const int t = threadIdx.x;
-    partials[(int64_t)blockIdx.x * 64 + t] = (red[t] + red[64 + t]) + (red[128 + t] + red[192 + t]);
+    // column-major [64][P] (P = gridDim.x): the finalize then reads each channel's P sums contiguously
+    partials[(int64_t)t * gridDim.x + blockIdx.x] = (red[t] + red[64 + t]) + (red[128 + t] + red[192 + t]);
   }
 }
 
