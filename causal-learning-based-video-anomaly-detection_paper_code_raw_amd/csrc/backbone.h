@@ -38,11 +38,11 @@ int bn_finalize(const float* partials, int P, int C, double count, const float* 
 // stats layout per layer (BN_STATS_PER_C = 7): [0:C) mean, [C:2C) invstd, [2C:3C) scale, [3C:4C) shift,
 //   [4C:5C) k (bwd), [5C:6C) mean(dZ), [6C:7C) mean(dZ*xhat)
 int bn_bwd_reduce(const float* dA, const float* y, const float* stats, int M, int C, float* partials, int* nparts,
-                  hipStream_t st);
+                  hipStream_t st, int cm = 0);  // cm: partials column-major [2C][P] (coalesced finalize reads)
 // when dbias is given, also the gradient of the conv bias in front of the BN: the sum over pixels of dY (zero up to
 // rounding in training mode)
 int bn_bwd_finalize(const float* partials, int P, int C, double count, const float* gamma, float* stats,
-                    float* dgamma, float* dbeta, int training, hipStream_t st, float* dbias = nullptr);
+                    float* dgamma, float* dbeta, int training, hipStream_t st, float* dbias = nullptr, int cm = 0);
 // bias_partials may be null (the conv bias grad then comes from bn_bwd_finalize's dbias)
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
                  int* nparts, hipStream_t st);

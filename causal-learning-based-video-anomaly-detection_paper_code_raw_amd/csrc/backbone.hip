@@ -406,7 +406,8 @@ int bn_rows_parts(int M, int C) {
   return (int)cdiv(M, bn_rows(M));
 }
 
-__device__ inline void bn_block_reduce_store(float (&v)[2][4], int C, float* out) {
+// out: this block's [2C] row (row-major partials), or with cs > 0 element j at out[j * cs] (column-major [2C][P])
+__device__ inline void bn_block_reduce_store(float (&v)[2][4], int C, float* out, int64_t cs = 0) {
   // threads sharing a channel quad: tid % (C/4) equal.  Reduce through LDS.
   __shared__ float red[256 * 8];
   const int t = threadIdx.x;
@@ -420,7 +421,7 @@ __device__ inline void bn_block_reduce_store(float (&v)[2][4], int C, float* out
     const int s = idx / C, c = idx % C, q = c / 4, e = c % 4;
     float acc = 0.f;
     for (int g = 0; g < groups; ++g) acc += red[(s * 4 + e) * 256 + g * nq + q];
-    out[s * C + c] = acc;
+    out[cs ? (int64_t)(s * C + c) * cs : s * C + c] = acc;
   }
 }
 
@@ -428,7 +429,7 @@ template <bool AB>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const act_t<AB>* __restrict__ dA,
                                                             const act_t<AB>* __restrict__ y,
                                                             const float* __restrict__ stats, int M, int C,
-                                                            float* __restrict__ partials, int BN_ROWS) {
+                                                            float* __restrict__ partials, int BN_ROWS, int cm) {
   const int nq = C / 4, groups = 256 / nq;
   const int q = threadIdx.x % nq, g = threadIdx.x / nq;
   const int c = q * 4;
@@ -450,19 +451,20 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const act_t<AB>* __r
       v[1][e] = fmaf(dz, (yy[e] - mean[e]) * inv[e], v[1][e]);
     }
   }
-  bn_block_reduce_store(v, C, partials + (int64_t)blockIdx.x * 2 * C);
+  if (cm) bn_block_reduce_store(v, C, partials + blockIdx.x, gridDim.x);
+  else bn_block_reduce_store(v, C, partials + (int64_t)blockIdx.x * 2 * C);
 }
 
 int bn_bwd_reduce(const float* dA, const float* y, const float* stats, int M, int C, float* partials, int* nparts,
-                  hipStream_t st) {
+                  hipStream_t st, int cm) {
   VAD_CHECK(C % 4 == 0 && C <= 1024 && 256 % (C / 4) == 0, "bn_bwd_reduce: unsupported C");
   const int P = bn_rows_parts(M, C);
   if (g_act_bf16)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(P), dim3(256), 0, st, reinterpret_cast<const __bf16*>(dA),
-                       reinterpret_cast<const __bf16*>(y), stats, M, C, partials, bn_rows(M));
+                       reinterpret_cast<const __bf16*>(y), stats, M, C, partials, bn_rows(M), cm);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(P), dim3(256), 0, st, dA, y, stats, M, C, partials,
-                       bn_rows(M));
+                       bn_rows(M), cm);
   VAD_LAUNCH_CHECK();
   *nparts = P;
   return 0;
@@ -472,13 +474,15 @@ template <typename PT>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const PT* __restrict__ partials, int P, int C,
                                                               double count, const float* __restrict__ gamma,
                                                               float* __restrict__ stats, float* dgamma,
-                                                              float* dbeta, int training, float* dbias) {
+                                                              float* dbeta, int training, float* dbias, int cm) {
   const int c = blockIdx.x;
   __shared__ double red[2][256];
   double a = 0.0, b = 0.0;
+  // partials row-major [P][2C] or column-major [2C][P] (cm)
+  const int64_t rs = cm ? 1 : 2 * C, ia = cm ? (int64_t)c * P : c, ib = cm ? (int64_t)(C + c) * P : C + c;
   for (int p = threadIdx.x; p < P; p += 256) {
-    a += (double)partials[(int64_t)p * 2 * C + c];
-    b += (double)partials[(int64_t)p * 2 * C + C + c];
+    a += (double)partials[p * rs + ia];
+    b += (double)partials[p * rs + ib];
   }
   red[0][threadIdx.x] = a;
   red[1][threadIdx.x] = b;
@@ -508,9 +512,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const PT* __restri
 }
 
 int bn_bwd_finalize(const float* partials, int P, int C, double count, const float* gamma, float* stats,
-                    float* dgamma, float* dbeta, int training, hipStream_t st, float* dbias) {
+                    float* dgamma, float* dbeta, int training, hipStream_t st, float* dbias, int cm) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3(C), dim3(256), 0, st, partials, P, C, count, gamma, stats,
-                     dgamma, dbeta, training, dbias);
+                     dgamma, dbeta, training, dbias, cm);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -518,7 +522,7 @@ int bn_bwd_finalize(const float* partials, int P, int C, double count, const flo
 int bn_bwd_finalize_sums(const double* sums, int C, double count, const float* gamma, float* stats, hipStream_t st,
                          float* dbias) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, sums, 1, C, count, gamma, stats,
-                     nullptr, nullptr, 1, dbias);
+                     nullptr, nullptr, 1, dbias, 0);
   VAD_LAUNCH_CHECK();
   return 0;
 }

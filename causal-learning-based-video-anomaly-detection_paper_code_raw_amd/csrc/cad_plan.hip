@@ -652,14 +652,15 @@ struct CadPlanImpl {
     return 0;
   }
   // backward of BN layer i: dgamma/dbeta from this rank's sums (the grad all-reduce adds the ranks), the mean terms
-  // from the group's sums when synchronised
+  // from the group's sums when synchronised; the partials are column-major [2C][P] (bn_bwd_reduce with cm = 1)
   int bn_bwd_stats(int i, int np, int C, double count, const float* gamma, float* dgamma, float* dbeta,
                    float* dbias, hipStream_t st) {
     if (sync_fn == nullptr || !training) {
-      TIMED("bn_bwd_fin", bn_bwd_finalize(parts, np, C, count, gamma, stats[i], dgamma, dbeta, training, st, dbias));
+      TIMED("bn_bwd_fin", bn_bwd_finalize(parts, np, C, count, gamma, stats[i], dgamma, dbeta, training, st, dbias,
+                                          1));
       return 0;
     }
-    TIMED("bn_bwd_fin", bn_sum_partials(parts, np, C, bnsync, dbeta, dgamma, st));
+    TIMED("bn_bwd_fin", bn_sum_partials(parts, np, C, bnsync, dbeta, dgamma, st, 1));
     VAD_CHECK(sync_fn(sync_user, i, 1, 2 * C, st) == 0, "BatchNorm sync callback failed (backward)");
     TIMED("bn_bwd_fin", bn_bwd_finalize_sums(bnsync, C, count * sync_world, gamma, stats[i], st, dbias));
     return 0;
@@ -883,7 +884,7 @@ struct CadPlanImpl {
       const bool perl = dy_per_layer != 0 && g_cad_dy_per_layer != 0;
       float* dYl = perl ? dYL[l] : ((l & 1) ? dY2 : dY);
       if ((g_dbg_skip_bnred & 1) && l < 7) np = 1;  // measurement only (knob "dbg_skip_bnred": results wrong)
-      else TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st));
+      else TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st, 1));
       VAD_TRY(bn_bwd_stats(l + 1, np, C, (double)M, P(LY.bn_w[l]), G(LY.bn_w[l]), G(LY.bn_b[l]), G(LY.conv_b[l]), st));
       // dYl was last read by layer l+2's weight gradient
       if (wgs && l + 2 <= 7 && !perl) VAD_HIP(hipStreamWaitEvent(st, ev_wg[l & 1], 0));
@@ -927,7 +928,7 @@ struct CadPlanImpl {
       TIMED("stem_bwd", maxpool3s2_bwd(y1, stats[0], dA, NF, H1, W1, 32, HP, WP, stem_d, st));
       const int64_t M1 = (int64_t)NF * H1 * W1;
       int np = 0, nb = 0;
-      TIMED("stem_bwd", bn_bwd_reduce(stem_d, y1, stats[0], (int)M1, 32, parts, &np, st));
+      TIMED("stem_bwd", bn_bwd_reduce(stem_d, y1, stats[0], (int)M1, 32, parts, &np, st, 1));
       VAD_TRY(bn_bwd_stats(0, np, 32, (double)M1, P(LY.bn1_w), G(LY.bn1_w), G(LY.bn1_b), G(LY.conv1_b), st));
       TIMED("stem_bwd", bn_bwd_apply(stem_d, y1, stats[0], (int)M1, 32, stem_d, nullptr, &nb, st));
       TIMED("stem_bwd", conv1_wgrad(x_last, NF, H, W, stem_d, H1, W1, wpart, wpart_floats, G(LY.conv1_w), st));
