@@ -90,7 +90,7 @@ struct BnFinArgs {
 };
 int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats /*nullable: BN+ReLU on load*/,
               const float* wf, const float* bias, float* y, float* partials, int* nparts, hipStream_t st,
-              BnFinArgs* fin = nullptr);
+              BnFinArgs* fin = nullptr, int* parts_cm = nullptr);  // parts_cm: in = accepted, out = 1 if written so
 int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
 // direct LDS-patch kernels (conv_patch.hip) for stride-1 layers; conv3_fwd / conv3_dgrad route there by default
 bool conv3_patch_supported(const Conv3Layer& L, bool fwd);
@@ -124,7 +124,8 @@ struct ActStorage {
 };
 bool conv3_x3_supported(const Conv3Layer& L, bool fwd);
 int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
-                 float* y, float* partials, int* nparts, hipStream_t st, BnFinArgs* fin = nullptr);
+                 float* y, float* partials, int* nparts, hipStream_t st, BnFinArgs* fin = nullptr,
+                 int* parts_cm = nullptr);
 int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
 // stride-2 input gradient on the split-bf16 (or, with conv_bf16, bf16) MFMA: parity classes of a 16x16 dX tile
 // sharing one dY patch; Wd in the plain [Ci][9][Co] layout (conv3_prep_weights with classes == 0)

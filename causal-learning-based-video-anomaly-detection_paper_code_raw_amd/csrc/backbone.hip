@@ -1152,11 +1152,13 @@ int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd
 }
 
 int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
-              float* y, float* partials, int* nparts, hipStream_t st, BnFinArgs* fin) {
+              float* y, float* partials, int* nparts, hipStream_t st, BnFinArgs* fin, int* parts_cm) {
+  if (parts_cm) *parts_cm = 0;
   VAD_CHECK(L.Ci % 32 == 0, "conv3_fwd: Ci must be a multiple of 32");
   // (the patch grid may exceed ceil(M/64) BN partial blocks on tiny images: those stay on the GEMM path)
   if (g_tune.patch && conv3_patch_blocks(L.NF, L.OH, L.OW) <= cdiv((int64_t)L.NF * L.OH * L.OW, 64)) {
-    if (conv3_x3_supported(L, true)) return conv3_x3_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st, fin);
+    if (conv3_x3_supported(L, true))
+      return conv3_x3_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st, fin, parts_cm);
     VAD_CHECK(!g_act_bf16, "conv3_fwd: bf16 activations need the split kernels");
     if (conv3_patch_supported(L, true)) return conv3_patch_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st);
   }

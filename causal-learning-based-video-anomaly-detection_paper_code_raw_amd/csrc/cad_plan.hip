@@ -721,10 +721,12 @@ struct CadPlanImpl {
         fin.stats = stats[l + 1];
         fin.count = (double)NF * L[l].OH * L[l].OW;
       }
+      int cm = 1;  // the split kernels write the partials column-major (coalesced finalize reads)
       TIMED(L_("conv_fwd", l), conv3_fwd(L[l], src, sst, wf[l], P(LY.conv_b[l]), y[l], parts, &np, st,
-                                         fuse ? &fin : nullptr));
+                                         fuse ? &fin : nullptr, &cm));
       if (!fin.done)
-        VAD_TRY(bn_fwd_stats(l + 1, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]), st));
+        VAD_TRY(bn_fwd_stats(l + 1, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]), st,
+                             cm));
       src = y[l];
       sst = stats[l + 1];
     }

@@ -44,6 +44,7 @@ struct X3Args {
   float* fin_rv;
   float* fin_stats;
   double fin_count;
+  int parts_cm;  // forward: BN partial sums column-major [2N][gridDim.x] (coalesced finalize reads)
 };
 
 // In-kernel BatchNorm finalize (forward, train mode) after every block has written its [2N] partial row: partial
@@ -402,7 +403,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) v += red[(2 * w + which) * NC + c];  // fixed order
-      float* dst = p.partials + (int64_t)blockIdx.x * 2 * p.N + which * p.N + n0 + c;
+      float* dst = p.parts_cm ? p.partials + (int64_t)(which * p.N + n0 + c) * gridDim.x + blockIdx.x
+                              : p.partials + (int64_t)blockIdx.x * 2 * p.N + which * p.N + n0 + c;
       if (n0 + c < p.N) {
         if (p.fin_counter) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
         else *dst = v;
@@ -806,7 +808,7 @@ bool conv3_x3_supported(const Conv3Layer& L, bool fwd) {
 }
 
 int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
-                 float* y, float* partials, int* nparts, hipStream_t st, BnFinArgs* fin) {
+                 float* y, float* partials, int* nparts, hipStream_t st, BnFinArgs* fin, int* parts_cm) {
   VAD_CHECK(conv3_x3_supported(L, true), "conv3_x3_fwd: unsupported layer");
   X3Args a{};
   a.src = src;
@@ -828,6 +830,11 @@ int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, 
     a.fin_count = fin->count;
     fin->done = 1;
   }
+  // column-major partials when the caller reads them so (not with the in-kernel finalize, nor on the opt-in
+  // wave-specialised stride-1 kernel, which write rows)
+  const bool ws = L.stride == 1 && g_x3_ws && g_x3_big && g_x3_ws != 3;
+  a.parts_cm = (parts_cm && !a.fin_counter && !ws) ? 1 : 0;
+  if (parts_cm) *parts_cm = a.parts_cm;
   // BN partial rows are bounded by conv3_patch_blocks (the caller's partial buffer)
   const int max_blocks = (int)std::min<int64_t>(conv3_patch_blocks(L.NF, L.OH, L.OW), 1 << 20);
   return L.stride == 1 ? dispatch_x3<1, true>(a, max_blocks, st, nparts) : dispatch_x3<2, true>(a, max_blocks, st, nparts);
