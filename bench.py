@@ -63,37 +63,120 @@ def algorithmic_work(label, B, T, H, W):
     return None, None
 
 
-def pmc_traffic(family):
-    """HBM bytes per launch of a conv family from the latest committed PMC summary (tools/pmc_traffic.py over two
-    rocprofv3 --pmc passes of this bench), or None."""
+CONV_FAMILIES = ("conv_fwd", "conv_dgrad", "conv_wgrad")
+
+
+def conv_io(B, T, H, W):
+    """(NF, Ci, Co, IH, IW, OH, OW) of the eight 3x3 convs (cad:121-139)."""
+    out = []
+    NF = B * T
+    h, w = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    h, w = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    for ci, co, s in [(32, 32, 1), (32, 32, 1), (32, 64, 2), (64, 64, 1), (64, 128, 2), (128, 128, 1),
+                      (128, 256, 2), (256, 256, 1)]:
+        oh, ow = (h - 1) // s + 1, (w - 1) // s + 1
+        out.append((NF, ci, co, h, w, oh, ow))
+        h, w = oh, ow
+    return out
+
+
+def conv_bytes(fam, layer, B, T, H, W, act_bytes):
+    """Algorithmic HBM bytes of one conv launch: each activation operand read or written once (act_bytes per
+    element: 4 fp32, 2 with bf16 activation storage) plus the fp32 weight (or weight-gradient) tensor once."""
+    NF, ci, co, ih, iw, oh, ow = conv_io(B, T, H, W)[layer]
+    x, y, w = NF * ih * iw * ci * act_bytes, NF * oh * ow * co * act_bytes, co * ci * 9 * 4
+    return x + y + w  # fwd: x in, y out, W in; dgrad: dY in, dX out, W in; wgrad: dY, X in, dW out
+
+
+def family_roofline(fam, live, pl, args, act_bytes):
+    """Roofline of one conv family from the live HIP events of the timed region.  fp32 configs: MFMA-bound (SURVEY
+    §8d), achieved = algorithmic FLOPs / time against the 157.3 TF fp32 peak (the kernels' own instruction peak --
+    split-bf16 launches issue six bf16 products per fp32 product -- reported beside it).  bf16 config 4: HBM-bound,
+    achieved = algorithmic bytes (conv_bytes) / time against 8 TB/s."""
+    from vad_amd import _native as nat
+    B, T, H, W = args.batch, args.T, args.H, args.W
+    kind = {"conv_fwd": 0, "conv_dgrad": 1, "conv_wgrad": 2}[fam]
+    flops = byts = ms_tot = ideal_s = 0.0
+    launches = 0
+    paths = {}
+    for lab, (ms, n) in live.items():
+        f, _, lay = lab.partition("/L")
+        if f != fam:
+            continue
+        l = int(lay)
+        work = algorithmic_work(lab, B, T, H, W)[1]
+        flops += work * n
+        byts += conv_bytes(fam, l, B, T, H, W, act_bytes) * n
+        ms_tot += ms
+        launches += n
+        path = nat.lib().vad_cad_conv_path(pl.h, l, kind)
+        paths[lab] = {6: "split-bf16", 1: "bf16", 0: "f32"}.get(path, "?")
+        ideal_s += work * n / (PATH_PEAK.get(path, PEAK_FP32_TFLOPS) * 1e12)
+    sec = ms_tot * 1e-3
+    tf, gbs = flops / sec / 1e12, byts / sec / 1e9
+    if args.dtype == "bf16":
+        r = {"bound": "hbm", "kernel": fam, "achieved": round(gbs, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+             "frac": round(gbs / PEAK_HBM_GBPS, 4), "traffic": None,
+             "algorithmic_bytes_per_launch": round(byts / max(launches, 1)),
+             "mfma_ceiling": {"achieved_tflops": round(tf, 2), "peak": PEAK_BF16_TFLOPS,
+                              "frac": round(tf / PEAK_BF16_TFLOPS, 4)}}
+    else:
+        r = {"bound": "mfma", "kernel": fam, "achieved": round(tf, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+             "frac": round(tf / PEAK_FP32_TFLOPS, 4), "traffic": None,
+             "algorithmic_bytes_per_launch": round(byts / max(launches, 1)),
+             "instruction_peak": {"peak": round(flops / ideal_s / 1e12, 1),
+                                  "frac": round(tf / (flops / ideal_s / 1e12), 4),
+                                  "basis": "fp32-equivalent peak of each launch's kernel (f32 MFMA 157.3; "
+                                           "split-bf16 2500/6), work-weighted harmonic mean over the family"}}
+    r["launches_timed"] = launches
+    r["avg_launch_us"] = round(1e3 * ms_tot / max(launches, 1), 2)
+    r["kernel_paths"] = paths
+    tag = f"cfg{args.config}"
+    traffic, src = pmc_family("pmc_traffic", tag, fam, "hbm_bytes_per_launch")
+    if traffic is not None:
+        r["traffic"] = round(traffic)
+        r["traffic_unit"] = "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE)"
+        r["traffic_source"] = src
+        r["traffic_over_algorithmic"] = round(traffic / (byts / max(launches, 1)), 3)
+    util, usrc = pmc_family("pmc_mfma", tag, fam, "mfma_util")
+    if util is not None:
+        r["mfma_util"] = round(util, 4)
+        r["mfma_util_source"] = usrc
+    return r
+
+
+def pmc_family(kind, tag, family, key):
+    """A conv family's PMC figure from the latest committed summary of THIS configuration
+    (profiles/*_{tag}_{kind}.json, written by tools/pmc_traffic.py / pmc_mfma.py over rocprofv3 --pmc passes of
+    `bench.py --config N`), or (None, None)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{tag}_{kind}.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
-        d = json.load(f)
-    fam = d.get("families", {}).get(family)
-    if not fam:
+        fam = json.load(f).get("families", {}).get(family)
+    if not fam or fam.get(key) is None:
         return None, None
-    return fam["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    return fam[key], os.path.relpath(files[-1], ROOT)
+
+
+def cpu_quota():
+    """CPUs this process may run on: the affinity mask, capped by the cgroup v2 CPU quota (the GPU box grants a
+    16-CPU quota on a 256-CPU host; 256 threads under that quota run the CPU oracle 80x slower than 16)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def host_cpu_info(threads):
     """Threads the CPU leg used, plus the host's logical CPU count and this process's affinity mask size."""
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
-    return {"cores": threads, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff}
-
-
-def pmc_mfma_util(family):
-    """MFMA utilisation of a conv family from the latest committed rocprofv3 counter summary (tools/pmc_mfma.py:
-    SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)), or None."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_mfma.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        fam = json.load(f).get("families", {}).get(family)
-    return (round(fam["mfma_util"], 4), os.path.relpath(files[-1], ROOT)) if fam else (None, None)
+    return {"cores": threads, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "cpu_quota": cpu_quota()}
 
 
 def run_gpu(args, rank, world, local_rank):
@@ -126,29 +209,25 @@ def run_gpu(args, rank, world, local_rank):
         trainer.step(pool[i % 2], labels)
     torch.cuda.synchronize()
 
-    # one instrumented step: per-label kernel times -> the dominant kernel family
+    # one instrumented step: per-label kernel times -> the dominant kernel family (largest summed time over the conv
+    # families, the weight gradients included although they run on their own stream beside the input gradients)
     eng = trainer.eng
     eng.profile(True, "")
     trainer.step(pool[0], labels)
     torch.cuda.synchronize()
     breakdown = eng.profile_read()
     fam_time = {}
-    # the backbone's weight gradients run on their own stream concurrently with the input gradients (DESIGN.md
-    # §3 Streams, option "wgrad_stream"): their event times include sharing the GPU, and they are off the
-    # critical path, so the dominant family is the largest one on the plan's critical stream
-    wgrad_overlapped = not any(kv.startswith("cad_wgrad_stream=0") for kv in args.tune)
     for lab, (ms, n) in breakdown.items():
-        if algorithmic_work(lab, B, T, H, W)[0] is None:
-            continue  # only families with a defined algorithmic work can carry a roofline
-        fam = lab.split("/L")[0]
-        if fam == "conv_wgrad" and wgrad_overlapped and args.config in (2, 4):
-            continue
-        fam_time[fam] = fam_time.get(fam, 0.0) + ms
+        if lab.split("/L")[0] in CONV_FAMILIES:
+            fam = lab.split("/L")[0]
+            fam_time[fam] = fam_time.get(fam, 0.0) + ms
     dominant = max(fam_time, key=fam_time.get)
+    # (the largest family on the critical stream: conv_wgrad is overlapped, DESIGN.md §3 Streams)
+    critical = max((f for f in fam_time if f != "conv_wgrad"), key=fam_time.get)
 
-    # timed region: the dominant family's kernels are dispatched with HIP start/stop events (hipExtLaunchKernel, on
-    # the plan's stream) on every --prof-every'th timed step; the other steps run uninstrumented
-    eng.profile(True, dominant)  # clears the breakdown records
+    # timed region: every conv family's kernels are dispatched with HIP start/stop events (hipExtLaunchKernel, on
+    # the stream each runs on) on every --prof-every'th timed step; the other steps run uninstrumented
+    eng.profile(True, "conv_")  # clears the breakdown records
     eng.profile(False)
     if world > 1:
         dist.barrier()
@@ -157,7 +236,7 @@ def run_gpu(args, rank, world, local_rank):
     for i in range(args.steps):
         instrument = i % args.prof_every == 0
         if instrument:
-            eng.profile(True, dominant, reset=False)
+            eng.profile(True, "conv_", reset=False)
         losses = trainer.step(pool[i % 2], labels)
         if instrument:
             eng.profile(False, reset=False)
@@ -172,58 +251,24 @@ def run_gpu(args, rank, world, local_rank):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(losses[4].item())
-
-    # roofline of the dominant family, from the live events; each launch is priced against the peak of the
-    # instruction mix its kernel runs (PATH_PEAK), the family's peak is the work-weighted harmonic mean of those
     pl = eng.plans[(B, T, H, W)]
-    kind = {"conv_fwd": 0, "conv_dgrad": 1, "conv_wgrad": 2}
-    bound, tot_work, tot_ms, launches, ideal_s = None, 0.0, 0.0, 0, 0.0
-    paths = {}
-    for lab, (ms, n) in live.items():
-        bnd, work = algorithmic_work(lab, B, T, H, W)
-        if bnd is None:
-            continue
-        bound = bnd
-        tot_work += work * n
-        tot_ms += ms
-        launches += n
-        fam, _, lay = lab.partition("/L")
-        path = nat.lib().vad_cad_conv_path(pl.h, int(lay), kind[fam]) if fam in kind else 0
-        paths[lab] = {6: "split-bf16", 1: "bf16", 0: "f32"}.get(path, "?")
-        ideal_s += work * n / (PATH_PEAK.get(path, PEAK_FP32_TFLOPS) * 1e12)
-    roof = None
-    if bound is not None and tot_ms > 0:
-        if bound == "mfma":
-            ach = tot_work / (tot_ms * 1e-3) / 1e12
-            peak = tot_work / ideal_s / 1e12
-            roof = {"bound": "mfma", "kernel": dominant, "achieved": round(ach, 3), "peak": round(peak, 1),
-                    "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
-                    "peak_basis": "fp32-equivalent peak of each launch's kernel (f32 MFMA 157.3; split-bf16 "
-                                  "2500/6; bf16 2500), work-weighted harmonic mean over the family",
-                    "frac_of_fp32_peak": round(ach / PEAK_FP32_TFLOPS, 4), "kernel_paths": paths}
-        else:
-            ach = tot_work / (tot_ms * 1e-3) / 1e9
-            roof = {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 1), "peak": PEAK_HBM_GBPS,
-                    "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 4), "traffic": None}
-        roof["dominant_basis"] = ("largest conv family on the critical stream (conv_wgrad runs concurrently on its "
-                                  "own stream)" if wgrad_overlapped and args.config in (2, 4) else
-                                  "largest conv family in an instrumented step")
-        roof["launches_timed"] = launches
-        roof["avg_launch_us"] = round(1e3 * tot_ms / max(launches, 1), 2)
-        traffic, src = pmc_traffic(dominant)
-        if traffic is not None:
-            roof["traffic"] = round(traffic)
-            roof["traffic_unit"] = "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE)"
-            roof["traffic_source"] = src
-        util, usrc = pmc_mfma_util(dominant)
-        if util is not None:
-            roof["mfma_util"] = util
-            roof["mfma_util_source"] = usrc
+    act_bytes = 2 if args.dtype == "bf16" else 4
+    families = {f: family_roofline(f, live, pl, args, act_bytes) for f in fam_time}
+    roof = dict(families[dominant])
+    roof["dominant_basis"] = ("largest summed kernel time over the conv families in an instrumented step "
+                              "(weight gradients included: they overlap the input gradients on their own stream)")
+    if critical != dominant:
+        roof["critical_stream"] = families[critical]
+    roof["families"] = {f: {k: r[k] for k in ("achieved", "frac", "avg_launch_us", "launches_timed")}
+                        for f, r in families.items()}
     step_ms = 1e3 * elapsed / args.steps
     # parity probe (rank 0): one more forward on the first batch with the trained weights; the CPU leg re-runs it on
     # the oracle (cpu_baseline) and reports the score difference and the frame-AUC of both
     probe = None
+    allreduce_bytes = 4 * trainer.allreduce_floats if trainer.dist else 0
     if rank == 0:
+        if trainer.sync_bn:  # (the probe runs on rank 0 alone: per-rank statistics, as the oracle leg computes them)
+            eng.set_bn_sync(enable=False)
         o = eng.forward(pool[0], True, 777, 0, 0, labels)
         torch.cuda.synchronize()
         probe = dict(state={k: v.detach().cpu().clone() for k, v in model.state_dict().items()},
@@ -260,7 +305,31 @@ def run_gpu(args, rank, world, local_rank):
     c1 = algorithmic_work("conv1", B, T, H, W)[1]
     step_flops = 2 * conv_flops + dgrad_flops + c1
     return dict(elapsed=elapsed, step_ms=step_ms, roof=roof, breakdown=breakdown, dominant=dominant,
-                final_loss=final_loss, step_tflops=step_flops / (step_ms * 1e-3) / 1e12, probe=probe, h2d=h2d)
+                final_loss=final_loss, step_tflops=step_flops / (step_ms * 1e-3) / 1e12, probe=probe, h2d=h2d,
+                allreduce_bytes=allreduce_bytes)
+
+
+# SURVEY §8d fixed per-clip work of the train step: cfg 2 (T=16, 227^2, fp32) 20.25 GFLOP, MFMA-bound; cfg 4
+# (T=32, 256^2, bf16 storage) 681 MB of HBM traffic (3 x 14.19 MB/frame x 32 frames / 2), HBM-bound
+STEP_WORK = {(2, 16, 227, 227): ("mfma", 20.25e9), (4, 32, 256, 256): ("hbm", 681e6)}
+
+
+def step_roofline(args, clips_per_s_per_gpu, step_tflops):
+    """Whole-step fraction of the governing ceiling: clips/s per GPU x the fixed per-clip work."""
+    key = (args.config, args.T, args.H, args.W)
+    if key not in STEP_WORK:
+        return {"bound": "mfma", "achieved": round(step_tflops, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(step_tflops / PEAK_FP32_TFLOPS, 4), "basis": "algorithmic conv FLOPs of the step"}
+    bound, work = STEP_WORK[key]
+    if bound == "mfma":
+        a = clips_per_s_per_gpu * work / 1e12
+        return {"bound": "mfma", "achieved": round(a, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(a / PEAK_FP32_TFLOPS, 4), "ceiling_clips_per_s": round(PEAK_FP32_TFLOPS * 1e12 / work),
+                "basis": "SURVEY §8d F_clip = 20.25 GFLOP x clips/s per GPU"}
+    a = clips_per_s_per_gpu * work / 1e9
+    return {"bound": "hbm", "achieved": round(a, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+            "frac": round(a / PEAK_HBM_GBPS, 4), "ceiling_clips_per_s": round(PEAK_HBM_GBPS * 1e9 / work),
+            "basis": "SURVEY §8d B_clip = 681 MB x clips/s per GPU"}
 
 
 def parity_check(args, probe):
@@ -294,7 +363,8 @@ def cpu_baseline(args):
     import torch
     from oracle import cad_oracle as co
     from vad_amd.cad import CausalAnomalyDetector
-    threads = torch.get_num_threads()
+    threads = cpu_quota()  # every CPU this process may use (os.cpu_count() capped by affinity and cgroup quota)
+    torch.set_num_threads(threads)
     torch.manual_seed(0)
     m = CausalAnomalyDetector()
     sd = {k: v.clone() for k, v in m.state_dict().items()}
@@ -373,7 +443,8 @@ def bbox_cpu(args, r):
     scores of the first two clips of every T bucket."""
     import torch
     from oracle import bbox_oracle as bo
-    threads = torch.get_num_threads()
+    threads = cpu_quota()  # every CPU this process may use (os.cpu_count() capped by affinity and cgroup quota)
+    torch.set_num_threads(threads)
     p = r["state"]
     diff = 0.0
     with torch.no_grad():
@@ -461,7 +532,8 @@ def mc_cpu(args, r):
     oracle's StableTrainer iteration (oracle/mc_oracle.py) over the 4 batches of an epoch, timed."""
     import torch
     from oracle import mc_oracle as mo
-    threads = torch.get_num_threads()
+    threads = cpu_quota()  # every CPU this process may use (os.cpu_count() capped by affinity and cgroup quota)
+    torch.set_num_threads(threads)
     sd = r["state"]
     params = {k: v for k, v in sd.items() if "running" not in k and "num_batches" not in k}
     bufs = {k: v.clone() for k, v in sd.items() if "running" in k}
@@ -542,7 +614,8 @@ def ae_cpu(args, r):
     oracle train step (oracle/ae_oracle.py) timed on a bounded sample."""
     import torch
     from oracle import ae_oracle as ae
-    threads = torch.get_num_threads()
+    threads = cpu_quota()  # every CPU this process may use (os.cpu_count() capped by affinity and cgroup quota)
+    torch.set_num_threads(threads)
     params, bufs, mem = ae.split_state(r["probe"]["state"])
     ev = ae.ae_eval_batch(params, bufs, mem, r["probe"]["x"])
     parity = {"max_abs_recon_error_diff": float((ev["recon_error"] - r["probe"]["recon_error"]).abs().max()),
@@ -563,6 +636,34 @@ def ae_cpu(args, r):
     return ({"value": round(B * n / el, 3), "unit": "clips/s", **host_cpu_info(threads), "kind": "port",
              "sample": f"{n} train steps of B={B} clips x T={T} x 1x64x64 (oracle/ae_oracle.py, torch CPU fp32, "
                        f"{threads} threads), after 1 warm-up step"}, parity)
+
+
+def finish(world):
+    """N > 1: every rank waits until rank 0 has run the CPU legs (after the timed region), then leaves the group."""
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def launch_ranks(n, backend):
+    """Run this command as n ranks (torch.distributed.run, one process per GPU, rendezvous on 127.0.0.1) in a child
+    process; returns its exit status.  Refuses (status 2) when fewer than n GPUs are visible for an RCCL run: the
+    measurement would otherwise time a different configuration than the one named."""
+    import socket
+    import subprocess
+    import torch
+    visible = torch.cuda.device_count()  # (counting devices does not initialise the GPU on this image)
+    if backend == "nccl" and visible < n:
+        print(f"bench.py: --gpus {n} needs {n} GPUs, {visible} visible", file=sys.stderr, flush=True)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -594,6 +695,14 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=V",
                     help="measurement only: set a libvadhip tuning knob (vad_set_tuning) before the run")
     args = ap.parse_args()
+    # --gpus N: one process per GPU.  Launched without torch.distributed.run (no WORLD_SIZE), bench.py starts the N
+    # ranks itself as a child torch.distributed.run before anything touches the GPU and exits with its status;
+    # launched by torch.distributed.run, the world size must be N.
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus, args.dist_backend))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} ranks were launched")
     if args.tune:
         from vad_amd import _native as nat
         for kv in args.tune:
@@ -630,7 +739,7 @@ def main():
     if args.config == 1:
         r = run_mc(args, rank, world, local_rank)
         if rank == 0:
-            cpu, parity = (None, None) if (args.no_cpu_baseline or world > 1) else mc_cpu(args, r)
+            cpu, parity = (None, None) if args.no_cpu_baseline else mc_cpu(args, r)
             clips = world * args.batch * args.steps
             tflops = MC_TRAIN_FLOP_PER_CLIP * clips / r["elapsed"] / 1e12
             print(json.dumps({
@@ -647,11 +756,12 @@ def main():
                              "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_FP32_TFLOPS, 4),
                              "traffic": None, "basis": "566.3 MFLOP per train clip (SURVEY §8d) x clips / time"},
                 "cpu_baseline": cpu, "parity": parity, "final_loss": r["loss"]}), flush=True)
+        finish(world)
         return
     if args.config == "cad1":
         r = run_ae(args, rank, world, local_rank)
         if rank == 0:
-            cpu, parity = (None, None) if (args.no_cpu_baseline or world > 1) else ae_cpu(args, r)
+            cpu, parity = (None, None) if args.no_cpu_baseline else ae_cpu(args, r)
             clips = world * args.batch * args.steps
             tflops = ae_flops_per_clip(args.T) * args.batch / (r["step_ms"] * 1e-3) / 1e12
             print(json.dumps({
@@ -670,14 +780,12 @@ def main():
                              "basis": f"{ae_flops_per_clip(args.T)} algorithmic FLOP per clip x clips / step time"},
                 "cpu_baseline": cpu, "parity": parity, "final_loss": r["loss"], "final_status": r["status"]}),
                 flush=True)
-        if world > 1:
-            import torch.distributed as dist
-            dist.destroy_process_group()
+        finish(world)
         return
     if args.config == 5:
         r = run_bbox(args, rank, world, local_rank)
         if rank == 0:
-            cpu, parity = (None, None) if (args.no_cpu_baseline or world > 1) else bbox_cpu(args, r)
+            cpu, parity = (None, None) if args.no_cpu_baseline else bbox_cpu(args, r)
             clips = world * args.batch * args.steps
             print(json.dumps({
                 "metric": BASELINE_METRIC, "value": round(clips / r["elapsed"], 3), "unit": "clips/s",
@@ -690,14 +798,12 @@ def main():
                            "frames_per_step_per_gpu": r["frames"]},
                 "roofline": bbox_roofline(world * r["frames"] / (r["step_ms"] * 1e-3)),
                 "cpu_baseline": cpu, "parity": parity}), flush=True)
-        if world > 1:
-            import torch.distributed as dist
-            dist.destroy_process_group()
+        finish(world)
         return
     r = run_gpu(args, rank, world, local_rank)
     if rank == 0:
-        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
-        parity = None if (args.no_cpu_baseline or world > 1 or r.get("probe") is None) else parity_check(args, r["probe"])
+        cpu = None if args.no_cpu_baseline else cpu_baseline(args)
+        parity = None if (args.no_cpu_baseline or r.get("probe") is None) else parity_check(args, r["probe"])
         clips = world * args.batch * args.steps
         out = {
             "metric": BASELINE_METRIC,
@@ -721,16 +827,15 @@ def main():
             "parity": parity,
             "h2d_inclusive": r.get("h2d"),
             "bn_stats": "group (SyncBatchNorm)" if (args.sync_bn and world > 1) else "per rank",
-            "step_algorithmic_tflops": round(r["step_tflops"], 3),
+            "step_roofline": step_roofline(args, clips / r["elapsed"] / world, r["step_tflops"]),
+            "allreduce_bytes_per_step": r["allreduce_bytes"],
             "final_loss": r["final_loss"],
         }
         if args.breakdown_out:
             with open(args.breakdown_out, "w") as f:
                 json.dump({"dominant": r["dominant"], "per_label_ms": r["breakdown"]}, f, indent=1)
         print(json.dumps(out), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    finish(world)
 
 
 if __name__ == "__main__":

@@ -46,6 +46,8 @@ int bn_bwd_finalize(const float* partials, int P, int C, double count, const flo
 // bias_partials may be null (the conv bias grad then comes from bn_bwd_finalize's dbias)
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
                  int* nparts, hipStream_t st);
+// the same in place (dA == dY; fp32 activations: the training stem's backward)
+int bn_bwd_apply_inplace(float* dAY, const float* y, const float* stats, int M, int C, hipStream_t st);
 int bn_rows_parts(int M, int C);
 // SyncBatchNorm: [P][2C] partials -> [2C] double sums (+ optional float copies of the two halves); finalize from
 // (all-reduced) sums over `count` elements of the whole process group

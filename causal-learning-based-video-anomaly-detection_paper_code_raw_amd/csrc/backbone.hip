@@ -527,12 +527,12 @@ int bn_bwd_finalize_sums(const double* sums, int C, double count, const float* g
   return 0;
 }
 
+// dY = k (dZ - mean(dZ) - xhat mean(dZ xhat)), dZ = dA where relu(fma(y, scale, shift)) > 0.  The body takes plain
+// pointers: bn_bwd_apply_kernel adds __restrict__ (distinct buffers), bn_bwd_apply_inplace_kernel does not (the
+// training stem's backward applies it in place, dY == dA: every thread reads an element before it writes it)
 template <bool AB>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const act_t<AB>* __restrict__ dA,
-                                                           const act_t<AB>* __restrict__ y,
-                                                           const float* __restrict__ stats, int M, int C,
-                                                           act_t<AB>* __restrict__ dY, float* __restrict__ bparts,
-                                                           int BN_ROWS) {
+__device__ __forceinline__ void bn_bwd_apply_body(const act_t<AB>* dA, const act_t<AB>* y, const float* stats, int M,
+                                                  int C, act_t<AB>* dY, float* bparts, int BN_ROWS) {
   const int nq = C / 4, groups = 256 / nq;
   const int q = threadIdx.x % nq, g = threadIdx.x / nq;
   const int c = q * 4;
@@ -561,6 +561,29 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const act_t<AB>* __re
     act_st4(dY + (int64_t)r * C + c, o);
   }
   if (bparts) bn_block_reduce_store(v, C, bparts + (int64_t)blockIdx.x * 2 * C);
+}
+
+template <bool AB>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const act_t<AB>* __restrict__ dA,
+                                                           const act_t<AB>* __restrict__ y,
+                                                           const float* __restrict__ stats, int M, int C,
+                                                           act_t<AB>* __restrict__ dY, float* __restrict__ bparts,
+                                                           int BN_ROWS) {
+  bn_bwd_apply_body<AB>(dA, y, stats, M, C, dY, bparts, BN_ROWS);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_inplace_kernel(float* dAY, const float* __restrict__ y,
+                                                                   const float* __restrict__ stats, int M, int C,
+                                                                   int BN_ROWS) {
+  bn_bwd_apply_body<false>(dAY, y, stats, M, C, dAY, nullptr, BN_ROWS);
+}
+
+int bn_bwd_apply_inplace(float* dAY, const float* y, const float* stats, int M, int C, hipStream_t st) {
+  VAD_CHECK(!g_act_bf16, "bn_bwd_apply_inplace: fp32 activations only");
+  hipLaunchKernelGGL(bn_bwd_apply_inplace_kernel, dim3(bn_rows_parts(M, C)), dim3(256), 0, st, dAY, y, stats, M, C,
+                     bn_rows(M));
+  VAD_LAUNCH_CHECK();
+  return 0;
 }
 
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,

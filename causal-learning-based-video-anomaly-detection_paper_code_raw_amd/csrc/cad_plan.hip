@@ -670,6 +670,7 @@ struct CadPlanImpl {
 
   int forward(const float* x, hipStream_t st) {
     const hipStream_t st0 = st;
+    VAD_TRY(join_open_stage2(st));
     ConvPrecision prec(conv_bf16);
     x_last = x;
     const CadLayout& LY = layout();
@@ -929,14 +930,26 @@ struct CadPlanImpl {
       TIMED("stem_bwd", conv3_dgrad(L[0], (dy_per_layer && g_cad_dy_per_layer) ? dYL[0] : dY, wd[0], dA, st));
       TIMED("stem_bwd", maxpool3s2_bwd(y1, stats[0], dA, NF, H1, W1, 32, HP, WP, stem_d, st));
       const int64_t M1 = (int64_t)NF * H1 * W1;
-      int np = 0, nb = 0;
+      int np = 0;
       TIMED("stem_bwd", bn_bwd_reduce(stem_d, y1, stats[0], (int)M1, 32, parts, &np, st, 1));
       VAD_TRY(bn_bwd_stats(0, np, 32, (double)M1, P(LY.bn1_w), G(LY.bn1_w), G(LY.bn1_b), G(LY.conv1_b), st));
-      TIMED("stem_bwd", bn_bwd_apply(stem_d, y1, stats[0], (int)M1, 32, stem_d, nullptr, &nb, st));
+      TIMED("stem_bwd", bn_bwd_apply_inplace(stem_d, y1, stats[0], (int)M1, 32, st));
       TIMED("stem_bwd", conv1_wgrad(x_last, NF, H, W, stem_d, H1, W1, wpart, wpart_floats, G(LY.conv1_w), st));
       stem_active = 1;
     }
-    if (stage == -1 || bwd_state == 2) VAD_TRY(join(st));  // the head's weight grads (side stream)
+    if (stage == -1 || bwd_state == 2) {
+      VAD_TRY(join(st));  // the head's weight grads (side stream)
+      bwd_state = 1;      // (joined: a following forward / optimizer step need not join again)
+    }
+    return 0;
+  }
+  // a stage-2 backward leaves the head / detector grads running on the side stream until stage 1 joins them; a forward
+  // or an optimizer step issued without stage 1 must not overwrite what that work still reads or writes
+  int join_open_stage2(hipStream_t st) {
+    if (bwd_state == 2) {
+      VAD_TRY(join(st));
+      bwd_state = 1;
+    }
     return 0;
   }
 
@@ -944,6 +957,7 @@ struct CadPlanImpl {
                 hipStream_t st) {
     const CadLayout& LY = layout();
     VAD_CHECK(m && v && steps, "optimizer: state buffers not bound");
+    VAD_TRY(join_open_stage2(st));
     const bool pw = prof.wants("optimizer");
     hipEvent_t pa = nullptr, pb = nullptr;
     if (pw) {

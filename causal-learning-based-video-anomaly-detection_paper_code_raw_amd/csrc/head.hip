@@ -1091,6 +1091,9 @@ int cad_tail_fwd(const TailArgs& t, hipStream_t st) {
 __global__ void cad_tail_bwd_kernel(TailArgs t) {
   const int B = t.B;
   const float fB = (float)B;
+  // re-arm the detector gate for this backward (a second backward on the same forward must wait for its own detector
+  // input gradient again): 0 = wait, 1 = no detector gradient (no box in range)
+  if (threadIdx.x == 0 && t.det_gate) *t.det_gate = t.flags[0] ? 0ull : 1ull;
   for (int b = threadIdx.x; b < B; b += 256) {
     const float p0 = t.probs[b * 2], p1 = t.probs[b * 2 + 1];
     const float c = t.causal[b], fin = t.final_scores[b];

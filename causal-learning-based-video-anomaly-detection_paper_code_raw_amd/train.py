@@ -40,7 +40,9 @@ class CadTrainer:
     """
 
     def __init__(self, model, lr=3e-4, weight_decay=1e-5, eps=1e-8, betas=(0.9, 0.999), max_norm=1.0, seed=0,
-                 process_group=None, engine=None, compute_dtype=None, sync_bn=False):
+                 process_group=None, engine=None, compute_dtype=None, sync_bn=False, force_dist=False):
+        """force_dist: run the data-parallel protocol (broadcasts, bucketed all-reduces, SyncBN callback) even at
+        world size 1 of an initialised process group -- exercises the collective path on one device (tests)."""
         self.model = model
         if compute_dtype is not None:
             model.set_compute_dtype(compute_dtype)
@@ -49,11 +51,20 @@ class CadTrainer:
         self.seed = seed
         self.step_idx = 0
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
-        self.rank = dist.get_rank(process_group) if self.world > 1 else 0
+        initialised = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(process_group) if initialised else 1
+        self.rank = dist.get_rank(process_group) if initialised else 0
+        self.dist = initialised and (self.world > 1 or force_dist)
         self.eng.init_optimizer_state()
-        self.sync_bn = bool(sync_bn) and self.world > 1
-        if self.world > 1:
+        self.sync_bn = bool(sync_bn) and self.dist
+        # gradient buckets of the flat grad buffer (slot order: backbone | detector | causal head | direct classifier
+        # | has-grad flags): the detector bucket (13.3 MB) is all-reduced only when some rank's detector has a grad
+        names = self.eng.slot_names
+        i0 = next(i for i, n in enumerate(names) if n.startswith("detector."))
+        i1 = next(i for i in range(i0, len(names)) if not names[i].startswith("detector."))
+        self.det_range = (self.eng.slot_offset[i0], self.eng.slot_offset[i1])
+        self.allreduce_floats = 0  # floats all-reduced by the last step (per rank, before the ring's 2(P-1)/P factor)
+        if self.dist:
             dist.broadcast(self.eng.params, 0, group=process_group)
             dist.broadcast(self.eng.bufs, 0, group=process_group)
         if self.sync_bn:
@@ -68,44 +79,66 @@ class CadTrainer:
         forward's output dict, see CadEngine.forward)."""
         eng = self.eng
         B = videos.shape[0]
-        if self.world > 1 and not self.sync_bn:
+        if self.dist and not self.sync_bn:
             dist.broadcast(eng.bufs, 0, group=self.pg)
         o = eng.forward(videos, True, self.seed, self.step_idx, self.rank * B, labels, want_outputs=want_outputs)
-        if self.world > 1 and eng.grads.is_cuda:
+        self.allreduce_floats = 0
+        if self.dist and eng.grads.is_cuda:
             self._backward_overlapped()
         else:
             eng.backward(True)
-            if self.world > 1:
-                dist.all_reduce(eng.grads, group=self.pg)
+            if self.dist:
+                d0, d1 = self.det_range
+                self._reduce(eng.grads[d1:])  # causal head + direct classifier + has-grad flags
+                if float(eng.grads[eng.param_floats]) > 0:
+                    self._reduce(eng.grads[d0:d1])
+                self._reduce(eng.grads[:d0])
         eng.optimizer_step(self.lr if lr is None else lr, self.betas, self.eps, self.wd, self.max_norm,
                            1.0 / self.world)
         self.step_idx += 1
         return o if want_outputs else o["losses"]
 
+    def _reduce(self, t):
+        dist.all_reduce(t, group=self.pg)
+        self.allreduce_floats += t.numel()
 
     def _backward_overlapped(self):
-        """Backward in two stages with the gradient all-reduce split at the backbone boundary: the head / classifier
-        / detector grads (+ has-grad flags; ~85 % of the bytes) are summed on a side stream while the backbone
-        backward runs on the compute stream (it waits only for the detector's input gradient, not for the whole
-        causal-head backward), then the backbone grads; the optimizer waits for both.  Each element
-        is summed over the same ranks as the single all_reduce."""
+        """Backward in two stages with the gradient all-reduce in three buckets (DDP's reduce-during-backward, with
+        the splits chosen for this model's grad order):
+          1. causal head + direct classifier + the has-grad flags, summed on a side stream while the backbone backward
+             runs on the compute stream (which waits only for the detector's input gradient);
+          2. the detector, only when the summed detector flag says some rank's detector has a gradient (it is
+             identically zero on every rank otherwise: every frame took the fallback box, cad:221-226) -- the flag is
+             read on the host after the backbone backward is queued, so the GPU never idles for it;
+          3. the backbone, after the backbone backward.
+        The optimizer waits for all of them.  Each element is summed over the same ranks as one all_reduce of the
+        whole buffer, so results are identical to it."""
         eng = self.eng
         main = torch.cuda.current_stream(eng.device)
         if getattr(self, "_comm", None) is None:
             self._comm = torch.cuda.Stream(eng.device)
+            self._flag_host = torch.zeros(2, dtype=torch.float32, pin_memory=True)
+            self._flag_ev = torch.cuda.Event()
         side = self._comm
-        nb = eng.backbone_floats
+        d0, d1 = self.det_range
+        pf = eng.param_floats
         # stage 2: the causal-head / detector backward keeps running on the plan's side stream while the backbone
         # (stage 1) starts; the all-reduce stream waits for both that side stream and the compute stream
         eng.backward(True, stage=2)
         eng.wait_side(side)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            dist.all_reduce(eng.grads[nb:], group=self.pg)
+            self._reduce(eng.grads[d1:])
+            self._flag_host.copy_(eng.grads[pf:pf + 2], non_blocking=True)
+            self._flag_ev.record(side)
         eng.backward(True, stage=1)
+        self._flag_ev.synchronize()
+        if float(self._flag_host[0]) > 0:
+            with torch.cuda.stream(side):
+                self._reduce(eng.grads[d0:d1])
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            dist.all_reduce(eng.grads[:nb], group=self.pg)
+            self._reduce(eng.grads[:d0])
         main.wait_stream(side)
 
 

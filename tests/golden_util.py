@@ -68,20 +68,89 @@ def read_debug(plan, name, idx=0, n=None, dtype=np.float32):
     return out
 
 
+def read_act(plan, name, idx=0):
+    """A backbone activation buffer as float64, whatever its storage (fp32, or bf16 when the plan ran act_bf16)."""
+    if int(read_debug_len(plan, "act_bf16")) == 1 and name in ("y", "pool"):
+        u = read_debug(plan, name, idx, dtype=np.uint16)
+        return (u.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+    return read_debug(plan, name, idx).astype(np.float64)
+
+
+def read_debug_len(plan, name, idx=0):
+    import ctypes
+    from vad_amd import _native as nat
+    p, k = ctypes.c_void_p(), ctypes.c_int64()
+    nat.check(nat.lib().vad_cad_debug_buffer(plan.h, name.encode(), idx, ctypes.byref(p), ctypes.byref(k)))
+    return k.value
+
+
 def hip_relu_masks(eng, NF):
     """The ReLU decisions the HIP forward took after the eight 3x3-conv BatchNorms: relu(fma(y, scale, shift)) is
     taken iff the exact value y*scale + shift > 0.  y*scale is exact in float64 (24-bit x 24-bit mantissas) and the
-    float64 add keeps the sign, so the comparison reproduces the device's fp32 fma decision bit for bit.
+    float64 add keeps the sign, so the comparison reproduces the device's fp32 fma decision bit for bit (bf16-stored
+    activations are widened exactly first).
     Returns 8 bool tensors (NF, C, OH, OW) for oracle.cad_oracle.backbone_forward(relu_masks=...)."""
     pl = eng._last[0]
     masks = []
     for l in range(8):
         st = read_debug(pl, "stats", l + 1)
         C = st.size // 7  # BN stats layout [7C] (csrc/common.h BN_STATS_PER_C)
-        y = read_debug(pl, "y", l).astype(np.float64).reshape(NF, -1, C)
+        y = read_act(pl, "y", l).reshape(NF, -1, C)
         z = y * st[2 * C:3 * C].astype(np.float64) + st[3 * C:4 * C].astype(np.float64)
         masks.append(torch.from_numpy(z > 0).permute(0, 2, 1))  # (NF, C, OH*OW); pinned_oracle_grads reshapes
     return masks
+
+
+def hip_stem_pins(eng, NF, H, W):
+    """The training stem's decisions in the HIP forward (option stem_grad: conv1's output y1 stored): bn1's ReLU
+    mask (exact sign of y1*scale + shift, as hip_relu_masks) and the MaxPool2d(3, 2, 1) window maxima under torch's
+    first-max rule (strict >, row-major window scan) over z = relu(fma(y1, scale, shift)) rounded to fp32 as the
+    device computes it (backbone.hip maxpool_bwd_kernel).  Returns (mask (NF, 32, H1, W1) bool, idx (NF, 32, HP, WP)
+    int64 flat indices into each H1 x W1 plane) for backbone_forward(stem_pins=...)."""
+    pl = eng._last[0]
+    H1, W1 = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    HP, WP = (H1 - 1) // 2 + 1, (W1 - 1) // 2 + 1
+    st = read_debug(pl, "stats", 0).astype(np.float64)
+    y1 = read_debug(pl, "y1").astype(np.float64).reshape(NF, H1, W1, 32)
+    zz = y1 * st[64:96] + st[96:128]
+    mask = zz > 0
+    idx = first_max_pool_idx(np.maximum(zz.astype(np.float32), np.float32(0)))
+    return (torch.from_numpy(mask).permute(0, 3, 1, 2).contiguous(),
+            torch.from_numpy(idx).permute(0, 3, 1, 2).contiguous())
+
+
+def first_max_pool_idx(z):
+    """MaxPool2d(3, 2, 1) window maxima of an NHWC array as flat indices into each H x W plane, torch's rule: scan
+    the window row-major, take a value when it is strictly greater than the best so far (padding never wins).
+    Returns (N, OH, OW, C) int64."""
+    N, H, W, C = z.shape
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    zp = np.full((N, H + 2, W + 2, C), -np.inf, z.dtype)
+    zp[:, 1:-1, 1:-1] = z
+    best = np.full((N, OH, OW, C), -np.inf, z.dtype)
+    idx = np.zeros((N, OH, OW, C), np.int64)
+    oy = np.arange(OH)[:, None] * 2
+    ox = np.arange(OW)[None, :] * 2
+    for dy in (-1, 0, 1):
+        for dx in (-1, 0, 1):
+            v = zp[:, oy + 1 + dy, ox + 1 + dx]
+            better = v > best
+            best = np.where(better, v, best)
+            idx = np.where(better, ((oy + dy) * W + (ox + dx))[None, :, :, None], idx)
+    return idx
+
+
+def reshape_masks(masks, x):
+    """hip_relu_masks output (NF, C, OH*OW) -> the (NF, C, OH, OW) tensors backbone_forward takes."""
+    from oracle import cad_oracle as co
+    shapes = []
+    NF = x.shape[0] * x.shape[1]
+    h, w = (x.shape[3] - 1) // 2 + 1, (x.shape[4] - 1) // 2 + 1
+    h, w = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    for _, _, s in co.BACKBONE_CONVS:
+        h, w = (h - 1) // s + 1, (w - 1) // s + 1
+        shapes.append((h, w))
+    return [m.reshape(NF, m.shape[1], hh, ww) for m, (hh, ww) in zip(masks, shapes)]
 
 
 def pinned_oracle_grads(state_dict, x, labels, draws, masks, sync_group=None):
@@ -93,14 +162,7 @@ def pinned_oracle_grads(state_dict, x, labels, draws, masks, sync_group=None):
               if "running" not in k and "num_batches" not in k}
     bufs = {k: v.detach().double().clone() for k, v in state_dict.items() if "running" in k}
     xd = x.double()
-    shapes = []
-    NF = xd.shape[0] * xd.shape[1]
-    h, w = (xd.shape[3] - 1) // 2 + 1, (xd.shape[4] - 1) // 2 + 1
-    h, w = (h - 1) // 2 + 1, (w - 1) // 2 + 1
-    for _, _, s in co.BACKBONE_CONVS:
-        h, w = (h - 1) // s + 1, (w - 1) // s + 1
-        shapes.append((h, w))
-    rm = [m.reshape(NF, m.shape[1], hh, ww) for m, (hh, ww) in zip(masks, shapes)]
+    rm = reshape_masks(masks, xd)
     res = co.cad_train_step(params, bufs, {}, xd, labels, draws, relu_masks=rm, sync_group=sync_group)
     res["bufs"] = bufs  # running stats after the step's forward
     return res["grads"], res["losses"], res

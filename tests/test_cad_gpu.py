@@ -283,47 +283,128 @@ def test_fused_stem_matches_float64_stem(B, T, H, W):
         np.testing.assert_allclose(got_v, rv.numpy(), rtol=1e-5, atol=1e-7)
 
 
-@pytest.mark.parametrize("B,T,H,W", [(2, 32, 256, 256)])
-def test_config4_shape_fp32_and_bf16(B, T, H, W):
-    """BASELINE config 4 shape (T=32, 256x256; 2 clips per rank here to bound the oracle's CPU time).
-    fp32 mode: scores / loss within the north-star 1e-4 of the CPU oracle.  bf16 mode (conv_bf16: the 3x3 convs
-    and the frozen stem's conv1 on bf16 operands, fp32 accumulation; the backbone activations -- pooled stem map,
-    conv outputs, their gradients -- stored as bf16 (option act_bf16, on by default); BN statistics, weights, grads
-    and the heads fp32): the outputs move by bf16 rounding of the conv operands and stored activations only --
-    scores and probabilities (bounded in [0, 1]) within 2e-2 absolute, the total loss within 2e-2 relative, the
-    global gradient norm within 5 % (tolerance stated for bf16 compute: unit roundoff 2^-8)."""
+def test_module_api_train_mode_unfrozen_227():
+    """The module API in train mode WITHOUT the trainer's freeze (the reference's CausalAnomalyDetector used as a
+    plain nn.Module: conv1 / bn1 train with batch statistics, cad:115-116,145-147; the freeze is only in train_model,
+    cad:592-598), forced detections (live boxes: detector and detection-box grads), B=2, T=16, 227x227:
+    model.train(); out = model(x); loss.backward() for a user loss over scores, probabilities, KL terms and the
+    detections.  Every parameter gradient vs the mask-pinned float64 oracle (the eight conv ReLUs, bn1's ReLU and
+    the MaxPool2d window maxima taken from the HIP forward) to relative L2 <= 1e-4 per tensor -- this covers bn1's
+    batch-statistics backward, maxpool_bwd, conv1's weight gradient and the detection-box grads in train mode; the
+    scores within 1e-4 and bn1's running statistics too."""
+    from tests.golden.cases import FORCED_A
+    from tests.golden_util import hip_stem_pins, reshape_masks
+    B, T, H, W = 2, 16, 227, 227
+    case = dict(name="api_train", B=B, T=T, H=H, W=W, seed=6, step=0, forced=FORCED_A)
+    m = make_cad_model(case).cuda()
+    m.train()
+    x = co.synth_clips(6, 0, 0, B, T, H, W)
+    coef = torch.tensor([1.0, -0.5, 0.25, 2.0])
+
+    def user_loss(o, cf):
+        det = sum((d * cf).sum() for fr in o["detections"] for d in fr)
+        return (o["anomaly_scores"].sum() + 0.5 * o["direct_predictions"][:, 0].sum()
+                + 0.1 * sum(o["kl_losses"]) + 1e-3 * det)
+
+    out = m(x.cuda(), seed=77, step=3, clip0=0)
+    user_loss(out, coef.cuda()).backward()
+    torch.cuda.synchronize()
+    eng = m.engine()
+    assert eng.stem_grad_on
+    masks = reshape_masks(hip_relu_masks(eng, B * T), x)
+    pins = hip_stem_pins(eng, B * T, H, W)
+    sd = make_cad_model(case).state_dict()
+    params = {k: v.detach().double().clone().requires_grad_(True) for k, v in sd.items()
+              if "running" not in k and "num_batches" not in k}
+    bufs = {k: v.detach().double().clone() for k, v in sd.items() if "running" in k}
+    ref = co.cad_forward(params, bufs, x.double(), co.CadDraws.make(77, 3, 0, B, T), training=True,
+                         relu_masks=masks, stem_pins=pins)
+    assert sum(int(d.shape[0]) for fr in ref["detections"] for d in fr) > B * T  # live boxes
+    user_loss(ref, coef.double()).backward()
+    np.testing.assert_allclose(out["anomaly_scores"].detach().cpu().numpy(), ref["anomaly_scores"].detach().numpy(),
+                               rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(out["direct_predictions"].detach().cpu().numpy(),
+                               ref["direct_predictions"].detach().numpy(), rtol=1e-4, atol=1e-5)
+    worst, det_live, stem_live = 0.0, False, False
+    for n, p in m.named_parameters():
+        pr = params[n]
+        if pr.grad is None or float(pr.grad.abs().max()) == 0.0:
+            assert p.grad is None or float(p.grad.abs().max()) < 1e-9, n
+            continue
+        assert p.grad is not None, n
+        mine = p.grad.detach().cpu().double().numpy()
+        if is_pre_bn_bias(n) or n == "backbone.conv1.bias":  # true gradient 0 (BN removes the mean)
+            assert np.abs(mine).max() < 1e-6 * max(1.0, float(pr.grad.abs().max())) + 1e-6, n
+            continue
+        e = rel_l2(mine, pr.grad.numpy())
+        worst = max(worst, e)
+        det_live |= n.startswith("detector.")
+        stem_live |= n.startswith(("backbone.conv1.", "backbone.bn1."))
+        assert e <= 1e-4, f"{n}: relative L2 error {e:.3g} vs the mask-pinned oracle"
+    assert det_live and stem_live
+    bufs_dev = dict(m.named_buffers())
+    for k in ("backbone.bn1.running_mean", "backbone.bn1.running_var"):
+        np.testing.assert_allclose(bufs_dev[k].cpu().numpy(), bufs[k].numpy(), rtol=1e-5, atol=1e-6, err_msg=k)
+    print(f"worst per-tensor relative L2 vs the mask-pinned oracle: {worst:.3g}")
+
+
+# per-tensor tolerance of the bf16 mode (conv_bf16 + act_bf16) against the exact (float64) gradient of the branch the
+# device took.  bf16 operands and stored activations carry a relative rounding of up to 2^-8 = 3.9e-3 per element, but
+# the gradients of this workload at init are cancellation-dominated: the 8 clips of random frames have nearly identical
+# features and the labels are balanced (i mod 2), so every gradient is a small difference of large per-clip terms and
+# the per-element rounding is amplified.  The fp32 mode shows the same amplification (2.3e-5 per-tensor error = ~380x
+# its unit roundoff 6e-8); bf16 measures 0.02-0.09 (~20x 2^-8) on MI355X for every backbone / classifier tensor.
+BF16_GRAD_REL_L2 = 0.15
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_config4_shape_per_rank(dt):
+    """BASELINE config 4 per-rank workload: B=8 clips x T=32 frames x 256x256 (BN couples all 256 frames).
+    fp32 mode: scores and loss within the north-star 1e-4 of the CPU oracle, every gradient tensor within relative
+    L2 1e-4 of the mask-pinned float64 oracle.  bf16 mode (conv_bf16: the 3x3 convs and the frozen stem's conv1 on
+    bf16 operands, fp32 accumulation; the backbone activations -- pooled stem map, conv outputs, their gradients --
+    stored as bf16 (option act_bf16, on by default); BN statistics, weights, grads and the heads fp32): scores and
+    probabilities (bounded in [0, 1]) within 2e-2 absolute, the total loss within 2e-2 relative, and every
+    gradient tensor within relative L2 BF16_GRAD_REL_L2 of the mask-pinned float64 oracle (tolerance stated for
+    bf16 compute: unit roundoff 2^-8)."""
+    B, T, H, W = 8, 32, 256, 256
     case = dict(name="cfg4", B=B, T=T, H=H, W=W, seed=9, step=1, forced=None)
     x = co.synth_clips(9, 1, 0, B, T, H, W)
     y = co.synth_labels(0, B)
-    mc = make_cad_model(case)
-    sd = {k: v.clone() for k, v in mc.state_dict().items()}
-    params = {k: v for k, v in sd.items() if "running" not in k and "num_batches" not in k}
-    bufs = {k: v for k, v in sd.items() if "running" in k}
-    res = co.cad_train_step(params, bufs, {}, x, y, co.CadDraws.make(9, 1, 0, B, T))
-    ref_norm = float(res["total_norm"])
-    for dt in (torch.float32, torch.bfloat16):
-        m = _frozen(make_cad_model(case)).cuda().set_compute_dtype(dt)
-        eng = m.engine()
-        o = eng.forward(x.cuda(), True, 9, 1, 0, y.cuda())
-        eng.backward(True)
-        torch.cuda.synchronize()
-        g = eng.grads[:eng.param_floats].double()
-        fp32 = dt == torch.float32
-        if not fp32:  # the bf16 run stored its activations as bf16
-            import ctypes
-            from vad_amd import _native as nat
-            pl = next(iter(eng.plans.values()))
-            p, k = ctypes.c_void_p(), ctypes.c_int64()
-            nat.check(nat.lib().vad_cad_debug_buffer(pl.h, b"act_bf16", 0, ctypes.byref(p), ctypes.byref(k)))
-            assert k.value == 1
-        atol = 1e-5 if fp32 else 2e-2
-        np.testing.assert_allclose(o["final"].cpu().numpy(), res["out"]["anomaly_scores"].detach().numpy(),
-                                   rtol=1e-4 if fp32 else 0, atol=atol)
-        np.testing.assert_allclose(o["probs"].cpu().numpy(), res["out"]["direct_predictions"].detach().numpy(),
-                                   rtol=1e-4 if fp32 else 0, atol=atol)
-        assert float(o["losses"][4]) == pytest.approx(float(res["losses"]["total"]), rel=1e-4 if fp32 else 2e-2)
-        # (frozen-stem / no-grad slots are zero in both)
-        assert float(g.norm()) == pytest.approx(ref_norm, rel=5e-3 if fp32 else 5e-2)
+    fp32 = dt == "fp32"
+    m = _frozen(make_cad_model(case)).cuda().set_compute_dtype(torch.float32 if fp32 else torch.bfloat16)
+    eng = m.engine()
+    o = eng.forward(x.cuda(), True, 9, 1, 0, y.cuda())
+    eng.backward(True)
+    torch.cuda.synchronize()
+    gr = eng.grads.cpu().numpy()
+    from tests.golden_util import read_debug_len
+    assert read_debug_len(eng._last[0], "act_bf16") == (0 if fp32 else 1)
+    masks = hip_relu_masks(eng, B * T)
+    ref_grads, ref_losses, res = pinned_oracle_grads(make_cad_model(case).state_dict(), x, y,
+                                                     co.CadDraws.make(9, 1, 0, B, T), masks)
+    atol = 1e-5 if fp32 else 2e-2
+    np.testing.assert_allclose(o["final"].cpu().numpy(), res["out"]["anomaly_scores"].detach().numpy(),
+                               rtol=1e-4 if fp32 else 0, atol=atol)
+    np.testing.assert_allclose(o["probs"].cpu().numpy(), res["out"]["direct_predictions"].detach().numpy(),
+                               rtol=1e-4 if fp32 else 0, atol=atol)
+    assert float(o["losses"][4]) == pytest.approx(float(ref_losses["total"]), rel=1e-4 if fp32 else 2e-2)
+    errs = {}
+    for i, n in enumerate(eng.slot_names):
+        ref = ref_grads.get(n)
+        mine = gr[eng.slot_offset[i]:eng.slot_offset[i] + eng.slot_numel[i]].astype(np.float64)
+        if ref is None:
+            assert np.abs(mine).max() == 0.0, n
+            continue
+        if is_pre_bn_bias(n):
+            assert np.abs(mine).max() < (1e-6 if fp32 else 1e-4), n
+            continue
+        errs[n] = rel_l2(mine, ref.detach().numpy())
+    for n, e in sorted(errs.items(), key=lambda kv: -kv[1])[:12]:
+        print(f"  {dt} {n}: {e:.3g}")
+    bad = {n: e for n, e in errs.items() if e > (1e-4 if fp32 else BF16_GRAD_REL_L2)}
+    assert not bad, f"relative L2 errors above tolerance ({dt}): {bad}"
+    print(f"config 4 per rank, {dt}: worst per-tensor relative L2 vs the mask-pinned oracle {max(errs.values()):.3g}")
 
 
 def test_staged_backward_equals_whole_backward():
@@ -370,6 +451,34 @@ def test_stage2_backward_equals_whole_backward(ci):
     torch.cuda.synchronize()
     assert torch.equal(head, grads[nb:eng.param_floats + 2])
     assert torch.equal(eng.grads[:eng.param_floats + 2], grads[:eng.param_floats + 2])
+
+
+@pytest.mark.parametrize("ci", [0, 1])
+def test_second_backward_on_one_forward(ci):
+    """Two backwards with different upstream grads on one forward (autograd retain_graph=True) give the grads of two
+    fresh forward + backward runs, bit for bit: the second backward re-arms the detector gate (cad_plan.hip) and
+    waits for its own detector input gradient again.  Fallback and forced regimes."""
+    case = CASES[ci]
+    m = make_cad_model(case).cuda()
+    eng = m.engine()
+    B, T, H, W = case["B"], case["T"], case["H"], case["W"]
+    x = co.synth_clips(case["seed"], case["step"], 0, B, T, H, W).cuda()
+    g = torch.Generator().manual_seed(5)
+    ups = [(torch.randn(B, generator=g).cuda(), torch.randn(B, 2, generator=g).cuda()) for _ in range(2)]
+    eng.forward(x, True, case["seed"], case["step"], 0)
+    shared = []
+    for dc, dp in ups:
+        eng.backward(False, d_causal=dc, d_probs=dp)
+        shared.append(eng.grads.clone())
+    fresh = []
+    for dc, dp in ups:
+        eng.forward(x, True, case["seed"], case["step"], 0)
+        eng.backward(False, d_causal=dc, d_probs=dp)
+        fresh.append(eng.grads.clone())
+    torch.cuda.synchronize()
+    assert not torch.equal(fresh[0], fresh[1])
+    for a, b in zip(shared, fresh):
+        assert torch.equal(a, b)
 
 
 def test_module_api_detection_grads():

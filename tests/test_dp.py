@@ -120,6 +120,68 @@ def test_dp_hip_engine_gloo_two_ranks(tmp_path):
     np.testing.assert_array_equal(got["bufs"].numpy(), eng.bufs.cpu().numpy())
 
 
+# ---------------------------------------------------------------- the collective path on RCCL (nccl) at world 1
+def _world1_worker(rank, backend, port, sync_bn, forced, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        out = _world1_run(sync_bn, forced, force_dist=True)
+        torch.save(out, out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def _world1_run(sync_bn, forced, force_dist):
+    from tests.golden.cases import FORCED_A, force_detector
+    from vad_amd.cad import CausalAnomalyDetector
+    from vad_amd.train import CadTrainer
+    torch.manual_seed(0)
+    m = CausalAnomalyDetector()
+    if forced:
+        force_detector(m.state_dict(), FORCED_A)
+    m = m.cuda()
+    tr = CadTrainer(m, lr=3e-4, seed=0, sync_bn=sync_bn, force_dist=force_dist)
+    assert tr.dist == force_dist and tr.sync_bn == (sync_bn and force_dist)
+    x, y = make_batches(1, **SHAPE)[0]
+    floats = []
+    for _ in range(2):
+        tr.step(x.cuda(), y.cuda())
+        floats.append(tr.allreduce_floats)
+        tr.allreduce_floats = 0
+    torch.cuda.synchronize()
+    return {"params": tr.eng.params.cpu(), "bufs": tr.eng.bufs.cpu(), "grads": tr.eng.grads.cpu(),
+            "floats": torch.tensor(floats), "det_range": torch.tensor(tr.det_range)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sync_bn,forced", [(False, False), (False, True), (True, False)],
+                         ids=["ddp-fallback", "ddp-forced", "syncbn-fallback"])
+def test_collective_path_rccl_world1(sync_bn, forced, tmp_path):
+    """CadTrainer's data-parallel protocol forced on at world size 1 (force_dist): the stage-2/stage-1 overlapped
+    backward with its three all-reduce buckets (the detector bucket skipped on device-read flags when no box is in
+    range), the BN-buffer broadcasts and, with sync_bn, the SyncBatchNorm callback (dist.all_reduce from inside the
+    library's ctypes callback).  On RCCL (backend nccl) the result equals the gloo run bit for bit, and in DDP mode
+    also the plain single-process step (a world-1 all-reduce is the identity)."""
+    res = {}
+    for backend in ("nccl", "gloo"):
+        out = str(tmp_path / f"{backend}.pt")
+        mp.spawn(_world1_worker, args=(backend, _free_port(), sync_bn, forced, out), nprocs=1, join=True)
+        res[backend] = torch.load(out, weights_only=True)
+    for k in ("params", "bufs", "grads", "floats"):
+        assert torch.equal(res["nccl"][k], res["gloo"][k]), k
+    d0, d1 = res["nccl"]["det_range"].tolist()
+    total = res["nccl"]["grads"].numel()
+    want = total if forced else total - (d1 - d0)  # the detector bucket only when a box is in range
+    assert res["nccl"]["floats"].tolist() == [want, want]
+    if not sync_bn:
+        plain = _world1_run(False, forced, force_dist=False)
+        for k in ("params", "bufs", "grads"):
+            assert torch.equal(res["nccl"][k], plain[k]), k
+
+
 # ---------------------------------------------------------------- BASELINE config 3 per-rank shape, vs the oracle
 CFG3 = dict(B=8, T=16, H=227, W=227)
 
