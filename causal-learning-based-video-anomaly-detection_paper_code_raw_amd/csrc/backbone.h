@@ -12,13 +12,11 @@ int conv1_num_parts(int NF, int OH);
 // frozen-stem forward without the conv1 activation (stem.hip): conv1 + bias, its BN partial sums ([P][64], the
 // conv1_fwd layout and P) and the 3x3/s2 pooling of the RAW output (max where gamma >= 0, min where gamma < 0);
 // the consumer applies bn1+ReLU on load (exact: the affine+ReLU is monotone per channel)
-extern int g_x3_stagger;  // knob "conv_split_stagger"
 extern int g_x3_dgrad_blocks;  // knob "conv_dgrad_blocks"
 extern int g_x3_big;  // knob "conv_split_big"
-extern int g_x3_ws;   // knob "conv_split_ws"
-extern int g_bn_fin_fused;  // knob "bn_fin_fused"
+extern int g_x3_s2big;  // knob "conv_split_s2big"
 extern int g_cad_prep_stream, g_cad_wgrad_stream, g_cad_det_gate, g_cad_last_wgrad_main, g_cad_event_sysfence,
-    g_cad_dy_per_layer, g_dbg_skip_bnred;  // knobs "cad_prep_stream", "cad_wgrad_stream" (A/B)
+    g_cad_dy_per_layer;  // knobs "cad_prep_stream", "cad_wgrad_stream" (A/B)
 extern int g_stem_fused, g_stem_dbg;  // knobs "stem_fused" (default 1), "stem_dbg" (measurement only)
 bool stem_fused_ok(int OW);  // conv1 output width the fused stem handles
 int stem_fused(const float* x, int NF, int H, int W, const float* w, const float* b, const float* gamma, int OH,
@@ -77,22 +75,9 @@ int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd
 // the same for n <= 8 layers in one launch
 int conv3_prep_weights_all(int n, const float* const* w, const Conv3Layer* L, float* const* wf, float* const* wd,
                            hipStream_t st);
-// In-kernel train-mode BatchNorm finalize for a conv forward (the last block to finish folds every block's partial
-// sums; bn_finalize semantics): counter = a zeroed int (the last block re-zeroes it); `done` is set by the call when
-// the conv kernel took it (otherwise the caller runs bn_finalize on the partials as before).
-struct BnFinArgs {
-  int* counter = nullptr;
-  const float* gamma = nullptr;
-  const float* beta = nullptr;
-  float* running_mean = nullptr;
-  float* running_var = nullptr;
-  float* stats = nullptr;
-  double count = 0;
-  int done = 0;
-};
 int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats /*nullable: BN+ReLU on load*/,
               const float* wf, const float* bias, float* y, float* partials, int* nparts, hipStream_t st,
-              BnFinArgs* fin = nullptr, int* parts_cm = nullptr);  // parts_cm: in = accepted, out = 1 if written so
+              int* parts_cm = nullptr);  // parts_cm: in = accepted, out = 1 if written so
 int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
 // direct LDS-patch kernels (conv_patch.hip) for stride-1 layers; conv3_fwd / conv3_dgrad route there by default
 bool conv3_patch_supported(const Conv3Layer& L, bool fwd);
@@ -104,7 +89,6 @@ int conv3_patch_dgrad(const Conv3Layer& L, const float* dY, const float* wd, flo
 // split-bf16 patch kernels (conv_x3.hip): fp32 operands as three bf16 planes, six bf16 MFMA products per K step
 extern int g_conv_split;  // 0 disables them (f32 MFMA patch kernels)
 extern int g_x3_nt;       // output channels per block: 0 auto, 1 -> 32, 2 -> 64
-extern int g_x3_dbg;      // measurement-only bits (X3Args::dbg)
 extern int g_x3_wres;     // 32-channel stride-1 layers: all split weights resident in LDS (1, default) or restaged
 // bf16-operand mode of the split kernels (one plane, one bf16 product per K step, fp32 accumulation): BASELINE
 // config 4's bf16 compute.  Thread-local, set for the duration of a plan call by ConvPrecision.
@@ -126,8 +110,7 @@ struct ActStorage {
 };
 bool conv3_x3_supported(const Conv3Layer& L, bool fwd);
 int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
-                 float* y, float* partials, int* nparts, hipStream_t st, BnFinArgs* fin = nullptr,
-                 int* parts_cm = nullptr);
+                 float* y, float* partials, int* nparts, hipStream_t st, int* parts_cm = nullptr);
 int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
 // stride-2 input gradient on the split-bf16 (or, with conv_bf16, bf16) MFMA: parity classes of a 16x16 dX tile
 // sharing one dY patch; Wd in the plain [Ci][9][Co] layout (conv3_prep_weights with classes == 0)

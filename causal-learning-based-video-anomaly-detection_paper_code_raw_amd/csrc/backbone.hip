@@ -15,7 +15,6 @@ int g_cad_event_sysfence = 0;  // knob "cad_event_sysfence": system-scope fence 
 int g_cad_dy_per_layer = 1;  // knob "cad_dy_per_layer" (A/B of the plan option dy_per_layer)
 int g_cad_det_gate = 1;      // knob "cad_det_gate": the backbone backward waits on the device detector gate
 int g_cad_wgrad_stream = 1;  // knob "cad_wgrad_stream": backbone weight gradients on their own stream
-int g_dbg_skip_bnred = 0;    // knob "dbg_skip_bnred" (measurement only, results wrong): bit 1 skips the BN backward
                              // reduce of layers 0-6, bit 2 the causal head's kernels
 
 // =====================================================================================================
@@ -988,19 +987,16 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_patch_persist") g_patch_persist = value;
   else if (k == "conv_split") g_conv_split = value;
   else if (k == "conv_split_nt") g_x3_nt = value;
-  else if (k == "conv_split_dbg") g_x3_dbg = value;
   else if (k == "conv_split_wres") g_x3_wres = value;
   else if (k == "conv_wgrad_patch") g_tune.wgrad_patch = value;
   else if (k == "conv_wgrad_split") g_wgrad_split = value;
   else if (k == "conv_wgrad_split_s2") g_wgrad_split_s2 = value;
   else if (k == "conv_wgrad_s2_blocks") g_wgrad_s2_blocks = value;
   else if (k == "stem_fused") g_stem_fused = value;
-  else if (k == "conv_split_stagger") g_x3_stagger = value;
   else if (k == "conv_dgrad_s2_x3") g_dgrad_s2_x3 = value;
   else if (k == "conv_dgrad_blocks") g_x3_dgrad_blocks = value;
   else if (k == "conv_split_big") g_x3_big = value;
-  else if (k == "conv_split_ws") g_x3_ws = value;
-  else if (k == "bn_fin_fused") g_bn_fin_fused = value;
+  else if (k == "conv_split_s2big") g_x3_s2big = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "cad_det_gate") g_cad_det_gate = value;
@@ -1008,7 +1004,6 @@ int set_tuning(const char* key, int value) {
   else if (k == "cad_event_sysfence") g_cad_event_sysfence = value;
   else if (k == "mlp_tail_wide") g_mlp_tail_wide = value;
   else if (k == "cad_last_wgrad_main") g_cad_last_wgrad_main = value;
-  else if (k == "dbg_skip_bnred") g_dbg_skip_bnred = value;
   else if (k == "head_dbg") g_head_dbg = value;
   else if (k == "stem_dbg") g_stem_dbg = value;
   else if (k == "conv_wgrad_s1_nt") g_wgrad_s1_nt = value;
@@ -1175,13 +1170,13 @@ int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd
 }
 
 int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
-              float* y, float* partials, int* nparts, hipStream_t st, BnFinArgs* fin, int* parts_cm) {
+              float* y, float* partials, int* nparts, hipStream_t st, int* parts_cm) {
   if (parts_cm) *parts_cm = 0;
   VAD_CHECK(L.Ci % 32 == 0, "conv3_fwd: Ci must be a multiple of 32");
   // (the patch grid may exceed ceil(M/64) BN partial blocks on tiny images: those stay on the GEMM path)
   if (g_tune.patch && conv3_patch_blocks(L.NF, L.OH, L.OW) <= cdiv((int64_t)L.NF * L.OH * L.OW, 64)) {
     if (conv3_x3_supported(L, true))
-      return conv3_x3_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st, fin, parts_cm);
+      return conv3_x3_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st, parts_cm);
     VAD_CHECK(!g_act_bf16, "conv3_fwd: bf16 activations need the split kernels");
     if (conv3_patch_supported(L, true)) return conv3_patch_fwd(L, src, src_stats, wf, bias, y, partials, nparts, st);
   }

@@ -332,7 +332,6 @@ struct CadPlanImpl {
   // otherwise; the side stream writes 1 once the detector's input gradient is final.  The backbone backward waits on
   // the word (hipStreamWaitValue64) instead of on the whole causal-head backward.
   uint64_t* det_gate = nullptr;
-  int* fin_counters = nullptr;  // tickets of the in-kernel BN finalize of the 8 conv layers (zeroed per forward)
   int grads_zeroed = 0;  // the last forward cleared the grad buffer for the backward that follows it
   float *d_causal, *d_kl, *d_glog, *d_dlog, *slabs, *d_feat_det, *d_pooled, *dense_scratch, *dense_scratch2;
   float *dg[5], *ddh[5];
@@ -444,6 +443,8 @@ struct CadPlanImpl {
     const int cs[9] = {32, 32, 32, 64, 64, 128, 128, 256, 256};
     for (int l = 0; l < 9; ++l) stats[l] = w.take<float>(BN_STATS_PER_C * cs[l]);
     parts_floats = std::max<int64_t>((int64_t)conv1_num_parts(NF, H1) * 64, 1024);
+    // (the training stem's bn1 backward reduces over all NF * H1 * W1 conv1 outputs: bn_rows_parts <= cdiv(M, 64))
+    parts_floats = std::max<int64_t>(parts_floats, cdiv((int64_t)nf * H1 * W1, 64) * 2 * 32);
     for (int l = 0; l < 8; ++l) {
       const int64_t M = nf * L[l].OH * L[l].OW;
       parts_floats = std::max<int64_t>(parts_floats, cdiv(M, 64) * 2 * L[l].Co);
@@ -474,7 +475,6 @@ struct CadPlanImpl {
     clip_flags = w.take<int>(B * 2);
     flags = w.take<int>(4);
     det_gate = w.take<uint64_t>(1);
-    fin_counters = w.take<int>(8);
     d_causal = w.take<float>(B);
     d_kl = w.take<float>(B);
     d_glog = w.take<float>(B * 2);
@@ -682,7 +682,6 @@ struct CadPlanImpl {
       for (int l = 0; l < 8; ++l) w8[l] = P(LY.conv_w[l]);
       TIMED("prep", conv3_prep_weights_all(8, w8, L, wf, wd, st));
       TIMED("prep", mlp_transpose(mlp_transpose_args(), st));
-      VAD_HIP(hipMemsetAsync(fin_counters, 0, 8 * sizeof(int), st));
       VAD_HIP(hipEventRecord(ev_prep, st));
     }
     int np = 0;
@@ -709,25 +708,9 @@ struct CadPlanImpl {
     const float* src = pool;
     const float* sst = pool_stats;
     for (int l = 0; l < 8; ++l) {
-      // train-mode BN statistics folded by the conv kernel's last block where it can (not with SyncBN: the sums
-      // cross the process group first)
-      BnFinArgs fin;
-      const bool fuse = training && sync_fn == nullptr;
-      if (fuse) {
-        fin.counter = fin_counters + l;
-        fin.gamma = P(LY.bn_w[l]);
-        fin.beta = P(LY.bn_b[l]);
-        fin.running_mean = RM(l + 1);
-        fin.running_var = RV(l + 1);
-        fin.stats = stats[l + 1];
-        fin.count = (double)NF * L[l].OH * L[l].OW;
-      }
       int cm = 1;  // the split kernels write the partials column-major (coalesced finalize reads)
-      TIMED(L_("conv_fwd", l), conv3_fwd(L[l], src, sst, wf[l], P(LY.conv_b[l]), y[l], parts, &np, st,
-                                         fuse ? &fin : nullptr, &cm));
-      if (!fin.done)
-        VAD_TRY(bn_fwd_stats(l + 1, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]), st,
-                             cm));
+      TIMED(L_("conv_fwd", l), conv3_fwd(L[l], src, sst, wf[l], P(LY.conv_b[l]), y[l], parts, &np, st, &cm));
+      VAD_TRY(bn_fwd_stats(l + 1, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]), st, cm));
       src = y[l];
       sst = stats[l + 1];
     }
@@ -767,7 +750,7 @@ struct CadPlanImpl {
     }
     {  // side stream: the causal head on the detections
       hipStream_t st = st2;
-      if (!(g_dbg_skip_bnred & 2)) TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
+      TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
     }
     VAD_TRY(join(st));
     TailArgs t = tail_args(nullptr, nullptr, nullptr, nullptr);
@@ -832,7 +815,7 @@ struct CadPlanImpl {
        // grads reach it, cad:221-226)
       hipStream_t st = st2;
       HeadUp up{d_causal, d_kl, dz, dadj, dboxes};
-      if (!(g_dbg_skip_bnred & 2)) TIMED("head_bwd", head_bwd(head_args(), dlog, head_out(), up, slabs, slab_len, d_dlog, st));
+      TIMED("head_bwd", head_bwd(head_args(), dlog, head_out(), up, slabs, slab_len, d_dlog, st));
     }
     // direct classifier chain (B rows): per-layer input-gradient GEMMs spread over many CUs, the layer 1-4 weight
     // grads in one launch, layer 0 GEMMs
@@ -850,21 +833,11 @@ struct CadPlanImpl {
     TIMED("dir_bwd", dense_wgrad(dg[0], B, 512, pooled, 6144, G(LY.dir_w[0]), G(LY.dir_b[0]), dense_scratch,
                                  dense_scratch_floats, nullptr, st));
     TIMED("dir_bwd", dense_dgrad(dg[0], B, 512, P(LY.dir_w[0]), 6144, d_pooled, nullptr, 1.f, nullptr, st));
-    {  // side stream, continued: the detector chain (it feeds the backbone: event ev_det), then the head's weight
-       // grads, which only the optimizer / the grad all-reduce wait for
-      hipStream_t st = st2;
-      // (the input-gradient chain first: the backbone backward waits for d_feat_det, the weight grads after it do not
-      // hold it up)
-      TIMED("det_bwd", mlp_tail_bwd(mlp_bwd_args(NF, d_dlog, dd, LY.det_w, dh, ddh, flags), st));
-      TIMED("det_bwd", dense_dgrad(ddh[0], NF, 512, P(LY.det_w[0]), 6144, d_feat_det, nullptr, 1.f, flags, st));
-      VAD_HIP(hipEventRecord(ev_det, st));
-      if (gate) VAD_HIP(hipStreamWriteValue64(st, det_gate, 1, 0));
-      TIMED("det_bwd", rows_wgrad(mlp_wgrad_args(NF, d_dlog, dd, LY.det_w, LY.det_b, dh, ddh, flags), st));
-      TIMED("det_bwd", dense_wgrad(ddh[0], NF, 512, feats, 6144, G(LY.det_w[0]), G(LY.det_b[0]), dense_scratch2,
-                                   dense_scratch_floats, flags, st));
-      TIMED("head_bwd", head_slab_reduce(slabs, B, slab_len, grads + LY.slots[LY.head0].offset, st));
-      TIMED("head_bwd", head_rows_wgrad(head_args(), st));
-    }
+    // side stream, continued: the detector chain (it feeds the backbone: event ev_det / the gate word), then the
+    // head's weight grads, which only the optimizer / the grad all-reduce wait for.  (It must be queued BEFORE the
+    // compute stream's wait on the gate: streams share a few hardware queues, and a wait queued ahead of the work
+    // that releases it on the same hardware queue never completes -- measured: a hang in the forced regime.)
+    VAD_TRY(side_det_chain(st2));
     // stage 0: every non-backbone grad is final on the caller's stream when it returns.  Stage 2 (= stage 0 for a
     // caller that orders its own consumer after the side stream with vad_cad_wait_side): the head / detector chain
     // keeps running on the side stream and the backbone (stage 1) waits only for the detector input gradient
@@ -886,8 +859,8 @@ struct CadPlanImpl {
       int np = 0, nb = 0;
       const bool perl = dy_per_layer != 0 && g_cad_dy_per_layer != 0;
       float* dYl = perl ? dYL[l] : ((l & 1) ? dY2 : dY);
-      if ((g_dbg_skip_bnred & 1) && l < 7) np = 1;  // measurement only (knob "dbg_skip_bnred": results wrong)
-      else TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st, 1));
+      VAD_CHECK((int64_t)bn_rows_parts((int)M, C) * 2 * C <= parts_floats, "backward: BN partial buffer too small");
+      TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st, 1));
       VAD_TRY(bn_bwd_stats(l + 1, np, C, (double)M, P(LY.bn_w[l]), G(LY.bn_w[l]), G(LY.bn_b[l]), G(LY.conv_b[l]), st));
       // dYl was last read by layer l+2's weight gradient
       if (wgs && l + 2 <= 7 && !perl) VAD_HIP(hipStreamWaitEvent(st, ev_wg[l & 1], 0));
@@ -931,6 +904,7 @@ struct CadPlanImpl {
       TIMED("stem_bwd", maxpool3s2_bwd(y1, stats[0], dA, NF, H1, W1, 32, HP, WP, stem_d, st));
       const int64_t M1 = (int64_t)NF * H1 * W1;
       int np = 0;
+      VAD_CHECK((int64_t)bn_rows_parts((int)M1, 32) * 64 <= parts_floats, "stem backward: BN partial buffer too small");
       TIMED("stem_bwd", bn_bwd_reduce(stem_d, y1, stats[0], (int)M1, 32, parts, &np, st, 1));
       VAD_TRY(bn_bwd_stats(0, np, 32, (double)M1, P(LY.bn1_w), G(LY.bn1_w), G(LY.bn1_b), G(LY.conv1_b), st));
       TIMED("stem_bwd", bn_bwd_apply_inplace(stem_d, y1, stats[0], (int)M1, 32, st));
@@ -950,6 +924,24 @@ struct CadPlanImpl {
       VAD_TRY(join(st));
       bwd_state = 1;
     }
+    return 0;
+  }
+
+  // the detector's backward (input gradient first: the backbone waits for d_feat_det; its weight grads after it)
+  // and the head's weight-grad reductions, on the side stream
+  int side_det_chain(hipStream_t st) {
+    const CadLayout& LY = layout();
+    const int dd[6] = {6144, 512, 256, 128, 64, 20};
+    const bool gate = g_cad_det_gate != 0 && det_gate != nullptr;
+    TIMED("det_bwd", mlp_tail_bwd(mlp_bwd_args(NF, d_dlog, dd, LY.det_w, dh, ddh, flags), st));
+    TIMED("det_bwd", dense_dgrad(ddh[0], NF, 512, P(LY.det_w[0]), 6144, d_feat_det, nullptr, 1.f, flags, st));
+    VAD_HIP(hipEventRecord(ev_det, st));
+    if (gate) VAD_HIP(hipStreamWriteValue64(st, det_gate, 1, 0));
+    TIMED("det_bwd", rows_wgrad(mlp_wgrad_args(NF, d_dlog, dd, LY.det_w, LY.det_b, dh, ddh, flags), st));
+    TIMED("det_bwd", dense_wgrad(ddh[0], NF, 512, feats, 6144, G(LY.det_w[0]), G(LY.det_b[0]), dense_scratch2,
+                                 dense_scratch_floats, flags, st));
+    TIMED("head_bwd", head_slab_reduce(slabs, B, slab_len, grads + LY.slots[LY.head0].offset, st));
+    TIMED("head_bwd", head_rows_wgrad(head_args(), st));
     return 0;
   }
 

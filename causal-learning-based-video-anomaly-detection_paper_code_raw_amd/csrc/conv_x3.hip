@@ -33,90 +33,8 @@ struct X3Args {
   float* partials;     // forward: [gridDim.x][2N] BN partial sums
   int NF, IH, IW, C, OH, OW, N;
   int tiles_h, tiles_w, ntiles, tpb;
-  int dbg;  // measurement only (knob "conv_split_dbg"): 1 no weight restaging, 2 no patch split, 4 no MFMA,
-            // 8 no patch loads -- results are wrong with any bit set
-  int stagger;  // knob "conv_split_stagger": odd blocks start this many x 1024 cycles late (phase offset of the two
-                // co-resident blocks of a CU)  // forward: in-kernel BatchNorm finalize (fin_counter != nullptr; see bn_fin_last_block)
-  int* fin_counter;
-  const float* fin_gamma;
-  const float* fin_beta;
-  float* fin_rm;
-  float* fin_rv;
-  float* fin_stats;
-  double fin_count;
   int parts_cm;  // forward: BN partial sums column-major [2N][gridDim.x] (coalesced finalize reads)
 };
-
-// In-kernel BatchNorm finalize (forward, train mode) after every block has written its [2N] partial row: partial
-// sums are stored write-through (sc1) and drained by every storing wave, one lane per block draws a ticket from an
-// agent-scope counter, and the block drawing the last one acquires (agent scope) and reads the partial rows with plain
-// (pipelined) loads -- per-element sc1 loads serialise at memory latency -- folding them in double in a fixed
-// order (bn_finalize_kernel semantics: batch mean / biased var, running stats with momentum 0.1 and the unbiased
-// var, scale = gamma * invstd, shift = beta - mean * scale), then re-zeroes the counter.  Saves the finalize launch
-// after every conv.  `red` is LDS scratch of at least NTHR doubles + 4 bytes.
-template <int NTHR>
-__device__ __forceinline__ void bn_fin_last_block(const X3Args& p, int P, char* red) {
-  const int tid = threadIdx.x;
-  int* flag = reinterpret_cast<int*>(red + NTHR * sizeof(double));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 partial stores are complete
-  __syncthreads();
-  if (tid == 0) {
-    const int total = gridDim.x * gridDim.y;
-    const int prev = __hip_atomic_fetch_add(p.fin_counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == total - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  const int N = p.N, NC2 = 2 * N;
-  double* part = reinterpret_cast<double*>(red);
-  // columns 2N x rows P: G row groups per column when 2N <= NTHR, else each thread walks several columns
-  const int G = NC2 <= NTHR ? NTHR / NC2 : 1;
-  if (G > 1) {
-    if (tid < G * NC2) {
-      const int g = tid / NC2, col = tid % NC2;
-      double acc = 0.0;
-#pragma unroll 8
-      for (int r = g; r < P; r += G) acc += (double)p.partials[(int64_t)r * NC2 + col];
-      part[g * NC2 + col] = acc;
-    }
-  } else {
-    for (int col = tid; col < NC2; col += NTHR) {
-      double acc = 0.0;
-#pragma unroll 8
-      for (int r = 0; r < P; ++r) acc += (double)p.partials[(int64_t)r * NC2 + col];
-      part[col] = acc;
-    }
-  }
-  __syncthreads();
-  if (G > 1) {
-    double tot = 0.0;
-    if (tid < NC2)
-      for (int g = 0; g < G; ++g) tot += part[g * NC2 + tid];  // fixed order
-    __syncthreads();
-    if (tid < NC2) part[tid] = tot;
-    __syncthreads();
-  }
-  const double count = p.fin_count, momentum = 0.1, eps = 1e-5;
-  for (int c = tid; c < N; c += NTHR) {
-    const double mean = part[c] / count;
-    double var = part[N + c] / count - mean * mean;
-    if (var < 0) var = 0;
-    p.fin_rm[c] = (float)((1.0 - momentum) * p.fin_rm[c] + momentum * mean);
-    p.fin_rv[c] = (float)((1.0 - momentum) * p.fin_rv[c] + momentum * var * count / (count - 1.0));
-    const double invstd = 1.0 / sqrt(var + eps);
-    const double scale = (double)p.fin_gamma[c] * invstd;
-    p.fin_stats[c] = (float)mean;
-    p.fin_stats[N + c] = (float)invstd;
-    p.fin_stats[2 * N + c] = (float)scale;
-    p.fin_stats[3 * N + c] = (float)((double)p.fin_beta[c] - mean * scale);
-  }
-  if (tid == 0) __hip_atomic_store(p.fin_counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 __device__ __forceinline__ void split3(const float* v, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
 #pragma unroll
@@ -222,7 +140,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
       const int row = q / G8;
       const int im = row / (PH * PW), rr = row % (PH * PW);
       const int iy = oy0 * S - 1 + rr / PW, ix = ox0 * S - 1 + rr % PW, img = img0 + im;
-      pok[it] = !(p.dbg & 8) && q < PQ && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
+      pok[it] = q < PQ && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
       const TA* s = src + c0 + g8 * 8 + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
       pv[it][0] = act_ld4(s);
       pv[it][1] = act_ld4(s + 4);
@@ -283,7 +201,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
         }
         const int col = S == 1 ? rx : ((rx & 1) ? PWE + (rx >> 1) : (rx >> 1));
         __bf16* d = patch + ((im * PH + ry) * PW + col) * RP + g8 * 8;
-        put_planes<NP>(d, PC, v, p.dbg & 2);
+        put_planes<NP>(d, PC, v, false);
       }
     }
     if (weights) {
@@ -318,18 +236,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
   f32x16 acc[NT];
   const int nitems = (t1 - t0) * nch;
   if (nitems > 0) fetch(t0, 0, true);
-  if (blockIdx.x & 1)
-    for (int k = 0; k < p.stagger; ++k) __builtin_amdgcn_s_sleep(16);
   for (int item = 0; item < nitems; ++item) {
     const int tile = t0 + item / nch, ch = item % nch, c0 = ch * PC;
-    const bool wnow = WCH > 1 ? item < nch : ((nch > 1 && !(p.dbg & 1)) || item == 0);
+    const bool wnow = WCH > 1 ? item < nch : (nch > 1 || item == 0);
     const int wseg = WCH > 1 ? ch * WCS : 0;
     __syncthreads();  // the previous item's fragment reads are done
     stash(tile, c0, wnow);
     __syncthreads();
     if (item + 1 < nitems) {
       const int nx = item + 1;
-      fetch(t0 + nx / nch, (nx % nch) * PC, WCH > 1 ? nx < nch : (nch > 1 && !(p.dbg & 1)));
+      fetch(t0 + nx / nch, (nx % nch) * PC, WCH > 1 ? nx < nch : nch > 1);
     }
     if (ch == 0) {
 #pragma unroll
@@ -338,7 +254,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
         for (int r = 0; r < 16; ++r) acc[nt][r] = 0.f;
     }
 #pragma unroll
-    for (int t = 0; t < ((p.dbg & 4) ? 0 : 9); ++t) {
+    for (int t = 0; t < 9; ++t) {
       const int kh = t / 3, kw = t % 3;
       const int col = S == 1 ? px + kw : ((kw & 1) ? PWE + px + (kw >> 1) : px + (kw >> 1));
       const __bf16* ap = patch + (arow0 + kh * PW + col) * RP + 8 * h;
@@ -405,311 +321,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
       for (int w = 0; w < NW; ++w) v += red[(2 * w + which) * NC + c];  // fixed order
       float* dst = p.parts_cm ? p.partials + (int64_t)(which * p.N + n0 + c) * gridDim.x + blockIdx.x
                               : p.partials + (int64_t)blockIdx.x * 2 * p.N + which * p.N + n0 + c;
-      if (n0 + c < p.N) {
-        if (p.fin_counter) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
-        else *dst = v;
-      }
-    }
-    if (p.fin_counter) {
-      __syncthreads();  // (red is reused as the finalize scratch)
-      bn_fin_last_block<NTHR>(p, gridDim.x, reinterpret_cast<char*>(sm));
+      if (n0 + c < p.N) *dst = v;
     }
   }
-}
-
-// Wave-specialised variant of the stride-1 kernel above for 256-pixel tiles (512 threads, one block per CU): waves
-// 0-3 multiply (each owns 64 output pixels = two 32-row MFMA tiles of one staged patch) while waves 4-7 stage the
-// NEXT item (global prefetch -> BN+ReLU on load -> split planes -> the other half of a double-buffered patch, and of
-// the weight slice when it is restaged per item), so the staging VALU / LDS-write / load latency of item k+1 runs on
-// the SIMDs beside the MFMAs of item k instead of between barriers; one barrier per item.  Same products and the same
-// accumulation order per output as conv3x3_x3_kernel.  WCH = 2: the split weights of both reduction chunks stay
-// resident (staged once by all 512 threads).
-template <int NI, int TH, int TW, int PC, bool FWD, int NP, int WCH, bool AB, int CW>
-__global__ __launch_bounds__(128 * CW, 1) void conv3x3_x3ws_kernel(const X3Args p) {
-  static_assert(CW == 4 || CW == 8, "4 or 8 consumer waves");
-  constexpr int SUB = 8 / CW, NTHR = 128 * CW;  // 32-row MFMA tiles per consumer wave, threads
-  static_assert(NI * TH * TW == 256, "256-pixel tiles");
-  static_assert(NP == 3 || NP == 1, "three split planes or one");
-  static_assert(!AB || NP == 1, "bf16 storage with bf16 operands only");
-  static_assert(PC == 16, "one 16-deep K step per tap");
-  using TA = act_t<AB>;
-  const TA* src = reinterpret_cast<const TA*>(p.src);
-  TA* out = reinterpret_cast<TA*>(p.out);
-  constexpr int NC = 32, G8 = PC / 8, NPR = 64 * CW;  // output channels per block, producer threads
-  constexpr int PH = TH + 2, PW = TW + 2, PROWS = NI * PH * PW;
-  constexpr int RP = NP * PC + 8;
-  constexpr int WCS = 9 * NP * PC;
-  constexpr int WP = WCH * WCS + 8;
-  constexpr int NWB = WCH > 1 ? 1 : 2;  // weight buffers: resident, or double-buffered per item
-  static_assert(((RP * 2 / 16) & 1) && ((WP * 2 / 16) & 1), "odd 16-B row pitch");
-  __shared__ __attribute__((aligned(16))) __bf16 sm[2 * PROWS * RP + NWB * NC * WP];
-  __bf16* const patch0 = sm;
-  __bf16* const wl0 = sm + 2 * PROWS * RP;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, j = lane & 31;
-  const bool consumer = wave < CW;
-  const int tiles_per_img = p.tiles_h * p.tiles_w;
-  const int n0 = blockIdx.y * NC;
-  const int t0 = blockIdx.x * p.tpb, t1 = min(p.ntiles, t0 + p.tpb);
-  const int nch = p.C / PC;
-  const int nitems = (t1 - t0) * nch;
-  // weights restaged per item (double-buffered) unless resident or a single chunk
-  const bool wper = WCH == 1 && nch > 1;
-
-  auto origin = [&](int tile, int& img0, int& oy0, int& ox0) {
-    img0 = (tile / tiles_per_img) * NI;
-    const int tr = tile % tiles_per_img;
-    oy0 = (tr / p.tiles_w) * TH;
-    ox0 = (tr % p.tiles_w) * TW;
-  };
-
-  // ---------------- producer state (waves 4-7): thread ptid handles channel group g8 = ptid % G8
-  constexpr int PQ = PROWS * G8, PIT = (PQ + NPR - 1) / NPR;
-  constexpr int WQ = NC * 9 * G8, WIT = (WQ + NPR - 1) / NPR;
-  const int ptid = tid - NPR, g8 = tid % G8;
-  act_raw4<AB> pv[PIT][2];
-  f32x4 wv[WIT][2];
-  bool pok[PIT], wok[WIT];
-  auto fetch = [&](int tile, int c0, bool weights) {
-    int img0, oy0, ox0;
-    origin(tile, img0, oy0, ox0);
-#pragma unroll
-    for (int it = 0; it < PIT; ++it) {
-      const int q = ptid + it * NPR;
-      const int row = q / G8;
-      const int im = row / (PH * PW), rr = row % (PH * PW);
-      const int iy = oy0 - 1 + rr / PW, ix = ox0 - 1 + rr % PW, img = img0 + im;
-      pok[it] = q < PQ && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
-      const TA* s = src + c0 + g8 * 8 + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
-      pv[it][0] = act_ld4(s);
-      pv[it][1] = act_ld4(s + 4);
-    }
-    if (weights) {
-#pragma unroll
-      for (int it = 0; it < WIT; ++it) {
-        const int q = ptid + it * NPR;
-        const int n = q / (9 * G8), t = (q / G8) % 9;
-        wok[it] = q < WQ && n0 + n < p.N;
-        const float* s = p.w + c0 + g8 * 8 +
-                         (wok[it] ? ((int64_t)(n0 + n) * 9 + (FWD ? t : 8 - t)) * p.C : (int64_t)0);
-        wv[it][0] = *reinterpret_cast<const f32x4*>(s);
-        wv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
-      }
-    }
-  };
-  auto stash = [&](int c0, __bf16* patch, __bf16* wl, bool weights) {
-    const bool bn = FWD && p.scale;
-    f32x4 sc[2], sh[2];
-    if constexpr (FWD) {
-      const float* scp = bn ? p.scale : p.w;
-      const float* shp = bn ? p.shift : p.w;
-      sc[0] = *reinterpret_cast<const f32x4*>(scp + c0 + g8 * 8);
-      sc[1] = *reinterpret_cast<const f32x4*>(scp + c0 + g8 * 8 + 4);
-      sh[0] = *reinterpret_cast<const f32x4*>(shp + c0 + g8 * 8);
-      sh[1] = *reinterpret_cast<const f32x4*>(shp + c0 + g8 * 8 + 4);
-    }
-#pragma unroll
-    for (int it = 0; it < PIT; ++it) {
-      const int q = ptid + it * NPR;
-      if (q < PQ) {
-        const int row = q / G8;
-        float v[8];
-        const f32x4 v0 = act_f4(pv[it][0]), v1 = act_f4(pv[it][1]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = pok[it] ? v0[e] : 0.f;
-          v[4 + e] = pok[it] ? v1[e] : 0.f;
-        }
-        if constexpr (FWD) {
-          // zero padding stays zero: padded taps read 0 in the reference's zero-padded relu(bn(y))
-          const bool app = bn && pok[it];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float a0 = relu_nan(fmaf(v[e], sc[0][e], sh[0][e]));
-            const float a1 = relu_nan(fmaf(v[4 + e], sc[1][e], sh[1][e]));
-            v[e] = app ? a0 : v[e];
-            v[4 + e] = app ? a1 : v[4 + e];
-          }
-        }
-        put_planes<NP>(patch + row * RP + g8 * 8, PC, v, false);
-      }
-    }
-    if (weights) {
-#pragma unroll
-      for (int it = 0; it < WIT; ++it) {
-        const int q = ptid + it * NPR;
-        if (q < WQ) {
-          const int n = q / (9 * G8), t = (q / G8) % 9;
-          float v[8];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] = wok[it] ? wv[it][0][e] : 0.f;
-            v[4 + e] = wok[it] ? wv[it][1][e] : 0.f;
-          }
-          put_planes<NP>(wl + n * WP + t * NP * PC + g8 * 8, PC, v, false);
-        }
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-  };
-
-  // ---------------- prologue
-  if constexpr (WCH > 1) {
-    // resident split weights of every chunk, staged once by all 512 threads
-    for (int q = tid; q < NC * 9 * WCH * G8; q += NTHR) {
-      const int n = q / (9 * WCH * G8), t = (q / (WCH * G8)) % 9, cg = q % (WCH * G8);
-      const int ch = cg / G8, g = cg % G8;
-      const bool ok = n0 + n < p.N;
-      float v[8];
-      const float* s = p.w + ((int64_t)(ok ? n0 + n : 0) * 9 + (FWD ? t : 8 - t)) * p.C + ch * PC + g * 8;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = ok ? s[e] : 0.f;
-      put_planes<NP>(wl0 + n * WP + ch * WCS + t * NP * PC + g * 8, PC, v, false);
-    }
-  }
-  if (!consumer && nitems > 0) {
-    fetch(t0, 0, WCH == 1);
-    stash(0, patch0, wl0, WCH == 1);
-    if (nitems > 1) fetch(t0 + 1 / nch, (1 % nch) * PC, wper);
-  }
-  __syncthreads();
-
-  // ---------------- consumer state (waves 0-3): pixels [64 wave, 64 wave + 64) as two 32-row tiles
-  int arow[SUB];
-#pragma unroll
-  for (int s2 = 0; s2 < SUB; ++s2) {
-    const int m = wave * 32 * SUB + s2 * 32 + j;
-    const int mi = m / (TH * TW), mr = m % (TH * TW);
-    arow[s2] = (mi * PH + mr / TW) * PW + mr % TW;
-  }
-  const float bj = (FWD && n0 + j < p.N) ? p.bias[n0 + j] : 0.f;
-  float s1 = 0.f, sq = 0.f;
-  f32x16 acc[SUB];
-
-  for (int item = 0; item < nitems; ++item) {
-    const int tile = t0 + item / nch, ch = item % nch;
-    const int buf = item & 1;
-    if (consumer) {
-      const __bf16* patch = patch0 + buf * PROWS * RP;
-      const __bf16* bbase = wl0 + (wper ? buf * NC * WP : 0) + j * WP + 8 * h + (WCH > 1 ? ch * WCS : 0);
-      if (ch == 0) {
-#pragma unroll
-        for (int s2 = 0; s2 < SUB; ++s2)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[s2][r] = 0.f;
-      }
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int kh = t / 3, kw = t % 3;
-        bf16x8 a[SUB][NP], b[NP];
-#pragma unroll
-        for (int q = 0; q < NP; ++q) b[q] = *reinterpret_cast<const bf16x8*>(bbase + (t * NP + q) * PC);
-#pragma unroll
-        for (int s2 = 0; s2 < SUB; ++s2)
-#pragma unroll
-          for (int q = 0; q < NP; ++q)
-            a[s2][q] = *reinterpret_cast<const bf16x8*>(patch + (arow[s2] + kh * PW + kw) * RP + 8 * h + q * PC);
-#pragma unroll
-        for (int s2 = 0; s2 < SUB; ++s2) {
-          if constexpr (NP == 3) acc[s2] = mfma_x3(a[s2], b, acc[s2]);
-          else acc[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s2][0], b[0], acc[s2], 0, 0, 0);
-        }
-      }
-      if (ch == nch - 1) {
-        // row = pixel (r&3) + 8(r>>2) + 4h of the sub-tile's 32, column = channel n0 + j
-        int img0, oy0, ox0;
-        origin(tile, img0, oy0, ox0);
-        const bool colok = n0 + j < p.N;
-#pragma unroll
-        for (int s2 = 0; s2 < SUB; ++s2)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int pm = wave * 32 * SUB + s2 * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int qi = pm / (TH * TW), qr = pm % (TH * TW);
-            const int oy = oy0 + qr / TW, ox = ox0 + qr % TW, img = img0 + qi;
-            if (colok && img < p.NF && oy < p.OH && ox < p.OW) {
-              const float v = acc[s2][r] + bj;
-              act_st(out + (((int64_t)img * p.OH + oy) * p.OW + ox) * p.N + n0 + j, v);
-              if (FWD) {
-                s1 += v;
-                sq = fmaf(v, v, sq);
-              }
-            }
-          }
-      }
-    } else if (item + 1 < nitems) {
-      const int nx = item + 1;
-      stash((nx % nch) * PC, patch0 + (buf ^ 1) * PROWS * RP, wl0 + (wper ? (buf ^ 1) * NC * WP : 0), wper);
-      if (nx + 1 < nitems) fetch(t0 + (nx + 1) / nch, ((nx + 1) % nch) * PC, wper);
-    }
-    __syncthreads();
-  }
-  if (FWD) {
-    float* red = reinterpret_cast<float*>(sm);  // [CW consumer waves][2][32]
-    if (consumer) {
-      const float a1 = s1 + __shfl_xor(s1, 32, 64);
-      const float a2 = sq + __shfl_xor(sq, 32, 64);
-      if (lane < 32) {
-        red[(wave * 2 + 0) * NC + lane] = a1;
-        red[(wave * 2 + 1) * NC + lane] = a2;
-      }
-    }
-    __syncthreads();
-    if (tid < 2 * NC) {
-      const int which = tid / NC, c = tid % NC;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < CW; ++w) v += red[(2 * w + which) * NC + c];  // fixed order
-      if (n0 + c < p.N) p.partials[(int64_t)blockIdx.x * 2 * p.N + which * p.N + n0 + c] = v;
-    }
-  }
-}
-
-extern int g_x3_wres;
-int g_x3_ws = 0;  // knob "conv_split_ws": stride-1 256-pixel layers on the wave-specialised kernel (1: 4 + 4 waves,
-                  // 2: 8 + 8 waves, 3: 8 + 8 waves for the input gradients of frames wider than 8 only)
-
-template <int NI, int TH, int TW, bool FWD, int NP, int WCH, bool AB>
-static int launch_ws_k(const X3Args& a, int gx, int ny, hipStream_t st) {
-  if (g_x3_ws >= 2)
-    VAD_KLAUNCH((conv3x3_x3ws_kernel<NI, TH, TW, 16, FWD, NP, WCH, AB, 8>), dim3(gx, ny), dim3(1024), 0, st, a);
-  else
-    VAD_KLAUNCH((conv3x3_x3ws_kernel<NI, TH, TW, 16, FWD, NP, WCH, AB, 4>), dim3(gx, ny), dim3(512), 0, st, a);
-  VAD_LAUNCH_CHECK();
-  return 0;
-}
-
-template <int NI, int TH, int TW, bool FWD>
-static int launch_ws(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
-  VAD_CHECK(a.C % 16 == 0, "conv3x3_x3ws: C % 16");
-  a.tiles_h = (int)cdiv(a.OH, TH);
-  a.tiles_w = (int)cdiv(a.OW, TW);
-  a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);
-  const int ny = (int)cdiv(a.N, 32);
-  // one block per CU over 256 CUs (input gradients: knob "conv_dgrad_blocks" / 2)
-  const int target = std::max(1, std::min(max_blocks, (FWD ? 512 : g_x3_dgrad_blocks) / 2 / ny));
-  a.tpb = (int)cdiv(a.ntiles, target);
-  const int gx = (int)cdiv(a.ntiles, a.tpb);
-  const bool wres = g_x3_wres && a.C == 32;
-  int rc;
-  if (g_conv_bf16) {
-    if (g_act_bf16) rc = wres ? launch_ws_k<NI, TH, TW, FWD, 1, 2, true>(a, gx, ny, st)
-                              : launch_ws_k<NI, TH, TW, FWD, 1, 1, true>(a, gx, ny, st);
-    else rc = wres ? launch_ws_k<NI, TH, TW, FWD, 1, 2, false>(a, gx, ny, st)
-                   : launch_ws_k<NI, TH, TW, FWD, 1, 1, false>(a, gx, ny, st);
-  } else {
-    VAD_CHECK(!g_act_bf16, "conv3x3_x3ws: bf16 activations need the bf16-operand kernels (conv_bf16)");
-    rc = wres ? launch_ws_k<NI, TH, TW, FWD, 3, 2, false>(a, gx, ny, st)
-              : launch_ws_k<NI, TH, TW, FWD, 3, 1, false>(a, gx, ny, st);
-  }
-  if (rc) return rc;
-  if (nparts) *nparts = gx;
-  return 0;
 }
 
 int g_x3_dgrad_blocks = 512;  // knob "conv_dgrad_blocks"
-int g_bn_fin_fused = 0;       // knob "bn_fin_fused": BatchNorm forward finalize inside the split conv kernels (measured
-                              // slower: +20 us/step at config 2, profiles/r02_bnfin_fused_ab.json)
 
 template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1, int NW = 4>
 static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
@@ -723,8 +340,6 @@ static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   // weight gradients)
   const int target = std::max(1, std::min(max_blocks, (FWD ? 512 : g_x3_dgrad_blocks) * 4 / NW / ny));
   a.tpb = (int)cdiv(a.ntiles, target);
-  a.dbg = g_x3_dbg;
-  a.stagger = g_x3_stagger;
   const int gx = (int)cdiv(a.ntiles, a.tpb);
   if constexpr (NP == 1) {
     if (g_act_bf16)
@@ -744,8 +359,6 @@ int g_conv_split = 1;  // tuning knob "conv_split": 1 = split-bf16 patch kernels
 thread_local int g_conv_bf16 = 0;  // bf16-operand convs (one plane, one product; set per plan, see ConvPrecision)
 thread_local int g_act_bf16 = 0;   // bf16 activation storage (set per plan, see ActStorage)
 int g_x3_nt = 0;       // tuning knob "conv_split_nt": 0 = auto, 1 / 2 = force 32 / 64 output channels per block
-int g_x3_dbg = 0;      // knob "conv_split_dbg" (measurement only, see X3Args::dbg)
-int g_x3_stagger = 0;  // knob "conv_split_stagger" (see X3Args::stagger)
 
 
 int g_x3_wres = 1;  // knob "conv_split_wres": 32-channel stride-1 layers keep all split weights resident in LDS
@@ -763,6 +376,7 @@ static int launch_x3(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
 }
 
 int g_x3_big = 1;  // knob "conv_split_big": stride-1 layers on 256-pixel tiles, 512-thread blocks (NW = 8)
+int g_x3_s2big = 1;  // knob "conv_split_s2big": fp32 stride-2 forwards on 256-pixel tiles, 8 waves, 32 channels
 
 
 template <int S, bool FWD, int NT>
@@ -782,12 +396,14 @@ static int dispatch_x3_nt(const X3Args& a, int max_blocks, hipStream_t st, int* 
 
 template <int S, bool FWD>
 static int dispatch_x3(const X3Args& a, int max_blocks, hipStream_t st, int* nparts) {
-  if constexpr (S == 1) {
-    // (knob value 3: input gradients of frames wider than 8 only, on the 8 + 8-wave kernel)
-    if (g_x3_ws && g_x3_big && (g_x3_ws != 3 || (!FWD && a.OW > 8))) {
-      if (a.OH <= 8 && a.OW <= 8) return launch_ws<4, 8, 8, FWD>(a, max_blocks, st, nparts);
-      if (a.OW <= 16) return launch_ws<2, 8, 16, FWD>(a, max_blocks, st, nparts);
-      return launch_ws<1, 8, 32, FWD>(a, max_blocks, st, nparts);
+  if constexpr (S == 2) {
+    // fp32 numerics (three split planes): a 128-pixel stride-2 tile needs a 4.5x larger patch than its output, so the
+    // 4-wave block's LDS (patch + 64-channel weight slice, 121 KB) allows one block -- one wave per SIMD -- per CU.
+    // 256-pixel tiles of 8 waves over 32 output channels fit 152-158 KB: two waves per SIMD
+    if (g_x3_s2big && !g_conv_bf16) {
+      if (a.OH <= 8 && a.OW <= 8) return launch_x3<2, 4, 8, 8, 1, 16, FWD, 8>(a, max_blocks, st, nparts);
+      if (a.OW <= 16) return launch_x3<2, 2, 8, 16, 1, 16, FWD, 8>(a, max_blocks, st, nparts);
+      return launch_x3<2, 1, 8, 32, 1, 16, FWD, 8>(a, max_blocks, st, nparts);
     }
   }
   int nt = g_x3_nt;
@@ -808,7 +424,7 @@ bool conv3_x3_supported(const Conv3Layer& L, bool fwd) {
 }
 
 int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
-                 float* y, float* partials, int* nparts, hipStream_t st, BnFinArgs* fin, int* parts_cm) {
+                 float* y, float* partials, int* nparts, hipStream_t st, int* parts_cm) {
   VAD_CHECK(conv3_x3_supported(L, true), "conv3_x3_fwd: unsupported layer");
   X3Args a{};
   a.src = src;
@@ -819,21 +435,7 @@ int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, 
   a.out = y;
   a.partials = partials;
   a.NF = L.NF; a.IH = L.IH; a.IW = L.IW; a.C = L.Ci; a.OH = L.OH; a.OW = L.OW; a.N = L.Co;
-  // in-kernel BN finalize (not on the opt-in wave-specialised stride-1 kernel)
-  if (fin && fin->counter && g_bn_fin_fused && !(L.stride == 1 && g_x3_ws && g_x3_big && g_x3_ws != 3)) {
-    a.fin_counter = fin->counter;
-    a.fin_gamma = fin->gamma;
-    a.fin_beta = fin->beta;
-    a.fin_rm = fin->running_mean;
-    a.fin_rv = fin->running_var;
-    a.fin_stats = fin->stats;
-    a.fin_count = fin->count;
-    fin->done = 1;
-  }
-  // column-major partials when the caller reads them so (not with the in-kernel finalize, nor on the opt-in
-  // wave-specialised stride-1 kernel, which write rows)
-  const bool ws = L.stride == 1 && g_x3_ws && g_x3_big && g_x3_ws != 3;
-  a.parts_cm = (parts_cm && !a.fin_counter && !ws) ? 1 : 0;
+  a.parts_cm = parts_cm ? 1 : 0;  // column-major partials when the caller reads them so
   if (parts_cm) *parts_cm = a.parts_cm;
   // BN partial rows are bounded by conv3_patch_blocks (the caller's partial buffer)
   const int max_blocks = (int)std::min<int64_t>(conv3_patch_blocks(L.NF, L.OH, L.OW), 1 << 20);
@@ -1063,7 +665,6 @@ struct WgX3Args {
   float* slab;         // [S][Co][9*Ci]
   int NF, IH, IW, Ci, OH, OW, Co;
   int tiles_h, tiles_w, ntiles;
-  int dbg;  // measurement only (knob "conv_split_dbg"): 2 no split, 4 no MFMA, 8 no global loads
 };
 
 // LDS row pitch (elements, a multiple of 8) with an odd number of 16-B units: the 16 lanes of a b128 read phase
@@ -1114,7 +715,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         yv[it][e] = R4{};
-        if (!(p.dbg & 8) && q < YQ && img < p.NF && oy < p.OH && ox + e < p.OW)
+        if (q < YQ && img < p.NF && oy < p.OH && ox + e < p.OW)
           yv[it][e] = act_ld4(dYp + (((int64_t)img * p.OH + oy) * p.OW + ox + e) * p.Co + co0 + c4 * 4);
       }
     }
@@ -1127,7 +728,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
       for (int e = 0; e < 4; ++e) {
         const int px = cg * 4 + e, ix = x0 - 1 + px;
         xv[it][e] = R4{};
-        if (!(p.dbg & 8) && q < XQ && px < PW && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
+        if (q < XQ && px < PW && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
           xv[it][e] = act_ld4(srcp + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.Ci + ci0 + c4 * 4);
       }
     }
@@ -1147,7 +748,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
       for (int e = 0; e < 4; ++e) {
         const float x = v[e][cc];
         const __bf16 a = (__bf16)x;
-        if (NP == 1 || (p.dbg & 2)) {
+        if (NP == 1) {
           hi[e] = mid[e] = lo[e] = a;
           continue;
         }
@@ -1213,7 +814,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
     __syncthreads();
     if (PF && tile + (int)gridDim.z < p.ntiles) fetch(tile + gridDim.z);
 #pragma unroll
-    for (int ks = 0; ks < ((p.dbg & 4) ? 0 : KS); ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       const int lin = (wave * KS + ks) * 16 + 8 * h;
       const int mi = lin / (TH * TW), mr = lin % (TH * TW);
       const int oy = mr / TW, ox = mr % TW;
@@ -1346,7 +947,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Ar
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         yv[it][e] = R4{};
-        if (!(p.dbg & 8) && tid + it * 256 < YQ && oy < p.OH && ox + e < p.OW)
+        if (tid + it * 256 < YQ && oy < p.OH && ox + e < p.OW)
           yv[it][e] = act_ld4(dYp + (((int64_t)img * p.OH + oy) * p.OW + ox + e) * p.Co + co0 + yc * 4);
       }
     }
@@ -1358,7 +959,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Ar
       for (int e = 0; e < 4; ++e) {
         const int pc = pcol(cg * 4 + e), ix = S * x0 - 1 + pc;
         xv[it][e] = R4{};
-        if (!(p.dbg & 8) && q < XQ && pc < PW && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
+        if (q < XQ && pc < PW && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
           xv[it][e] = act_ld4(srcp + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.Ci + ci0 + c4 * 4);
       }
     }
@@ -1378,7 +979,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Ar
       for (int e = 0; e < 4; ++e) {
         const float x = v[e][cc];
         const __bf16 a = (__bf16)x;
-        if (NP == 1 || (p.dbg & 2)) {
+        if (NP == 1) {
           hi[e] = mid[e] = lo[e] = a;
           continue;
         }
@@ -1438,7 +1039,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Ar
     __syncthreads();  // the previous tile's fragment reads are done
     stash(tile);
     __syncthreads();
-    if (p.dbg & 4) continue;
 #pragma unroll
     for (int k = 0; k < KSW; ++k) {
       const int lin = (ks0 + k) * 16 + 8 * h, oyr = lin / TW, oxr = lin % TW;
@@ -1579,7 +1179,6 @@ int conv3_wgrad_x3(const Conv3Layer& L, const float* dY, const float* src, const
   a.shift = src_stats ? src_stats + 3 * L.Ci : nullptr;
   a.slab = slab;
   a.NF = L.NF; a.IH = L.IH; a.IW = L.IW; a.Ci = L.Ci; a.OH = L.OH; a.OW = L.OW; a.Co = L.Co;
-  a.dbg = g_x3_dbg;
   if (L.stride == 2) {
     VAD_CHECK(L.IH >= 2 * L.OH - 1 && L.IW >= 2 * L.OW - 1, "conv3_wgrad_x3: stride-2 geometry");
     target_blocks = g_wgrad_s2_blocks;

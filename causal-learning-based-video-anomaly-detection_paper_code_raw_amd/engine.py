@@ -125,6 +125,9 @@ class CadEngine:
             for i, k in enumerate(nbt_names):
                 self.nbt[i].copy_(named_bufs[k].reshape(()))
                 _set_buffer(model, k, self.nbt[i])
+        # (the stem's Parameter objects, for the per-call requires_grad check: building the named-parameter dict
+        # costs ~0.3 ms of host time, twice per step, on the step's critical path where the GPU runs short kernels)
+        self._stem_params = [p for k, p in named if k in self.STEM]
         self.exp_avg = self.exp_avg_sq = self.steps = None
         self.bn_sync = None  # (process_group, world) in SyncBatchNorm mode
         self._compute_dtype = torch.float32
@@ -259,8 +262,7 @@ class CadEngine:
 
     def stem_trains(self) -> bool:
         """backbone.conv1 / bn1 take grads unless frozen (apply_memory_efficient_training, cad:592-598)."""
-        named = dict(self.model.named_parameters())
-        return any(named[n].requires_grad for n in self.STEM)
+        return any(p.requires_grad for p in self._stem_params)
 
     def _set_stem_grad(self, pl):
         on = self.stem_trains()
