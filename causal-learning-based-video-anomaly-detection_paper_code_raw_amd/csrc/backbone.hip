@@ -976,6 +976,7 @@ struct ConvTuning {
 };
 static ConvTuning g_tune;
 
+extern int g_bbox_im2col;  // bbox_plan.hip
 int set_tuning(const char* key, int value) {
   const std::string k(key);
   if (k == "conv_fwd_tile") g_tune.fwd = value;
@@ -997,6 +998,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_dgrad_blocks") g_x3_dgrad_blocks = value;
   else if (k == "conv_split_big") g_x3_big = value;
   else if (k == "conv_split_s2big") g_x3_s2big = value;
+  else if (k == "bbox_im2col") g_bbox_im2col = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "cad_det_gate") g_cad_det_gate = value;

@@ -59,6 +59,13 @@ int adaptive_avgpool3d_fwd(const float* x, const float* stats, int relu, const V
 // dx (NDHWC) = backward of the average (act' is NOT applied: callers route through their ReLU/BN backward)
 int adaptive_avgpool3d_bwd(const float* dout, const Vol5& v, int OD, int OH, int OW, float* dx, hipStream_t st);
 
+// Conv3d k3 p1 s1 on NDHWC volumes (B clips x D slices x H x W x C) with split-bf16 MFMA (fp32-class numerics,
+// conv_x3.hip): w3 = weights as [kd][N][kh*3+kw][C] (conv3d_prep_w3), out = conv + bias (no activation), NDHWC
+int conv3d_x3_fwd(int B, int D, int H, int W, int C, int N, const float* src, const float* w3, const float* bias,
+                  float* out, hipStream_t st);
+// torch Conv3d weight [N][C][3][3][3] -> [3][N][9][C]
+int conv3d_prep_w3(const float* w, int N, int C, float* w3, hipStream_t st);
+
 // per-block column sums / sums of squares of Y[M][C] -> partials [P][2C] (bn_finalize layout)
 int bn_fwd_partials(const float* y, int64_t M, int C, float* partials, int* nparts, hipStream_t st);
 int64_t bn_fwd_partials_blocks(int64_t M);

@@ -112,6 +112,28 @@ int col2im3d(const float* dcols, const Conv3dGeom& g, float* dsrc, hipStream_t s
   return 0;
 }
 
+__global__ __launch_bounds__(256) void conv3d_prep_w3_kernel(const float* __restrict__ w, int N, int C,
+                                                             float* __restrict__ w3) {
+  const int64_t total = (int64_t)N * C * 27;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    int64_t r = i / C;
+    const int t = (int)(r % 9);
+    r /= 9;
+    const int n = (int)(r % N);
+    const int kd = (int)(r / N);
+    w3[i] = w[((int64_t)n * C + c) * 27 + kd * 9 + t];
+  }
+}
+
+int conv3d_prep_w3(const float* w, int N, int C, float* w3, hipStream_t st) {
+  const int64_t total = (int64_t)N * C * 27;
+  hipLaunchKernelGGL(conv3d_prep_w3_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 2048)), dim3(256), 0,
+                     st, w, N, C, w3);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
 // ------------------------------------------------------------------ MaxPool3d (kernel == stride)
 __device__ __forceinline__ float pool_act(const float* y, const float* stats, int relu, int C, int c, int64_t idx) {
   float v = y[idx];

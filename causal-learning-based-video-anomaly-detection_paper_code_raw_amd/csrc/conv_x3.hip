@@ -18,6 +18,7 @@
 #include <algorithm>
 
 #include "backbone.h"
+#include "conv3d.h"
 
 namespace vad {
 
@@ -34,6 +35,7 @@ struct X3Args {
   int NF, IH, IW, C, OH, OW, N;
   int tiles_h, tiles_w, ntiles, tpb;
   int parts_cm;  // forward: BN partial sums column-major [2N][gridDim.x] (coalesced finalize reads)
+  int D;         // KD == 3 (Conv3d k3 p1 s1): depth of the NDHWC volumes; image index = n * D + d
 };
 
 __device__ __forceinline__ void split3(const float* v, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
@@ -81,8 +83,13 @@ __device__ __forceinline__ void put_planes(__bf16* d, int pitch, const float* v,
 // NW = 8: 512-thread blocks over 256-pixel tiles (one block per CU): the weight slice staged per item serves twice
 // the pixels (the weight staging per MFMA halves) and the halo share of the patch drops
 // AB: bf16 activation storage (p.src / p.out hold bf16; only with NP == 1)
-template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1, int NW = 4, bool AB = false>
+// KD = 3: Conv3d 3x3x3, stride 1, padding 1 on NDHWC volumes (images = depth slices, p.D per clip): the three depth taps
+// kd are further reduction chunks -- chunk (kd, c0) stages depth slice d + kd - 1 (zero outside the clip) and the
+// weight image kd of p.w [KD][N][9][C]; forward only
+template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int WCH = 1, int NW = 4, bool AB = false,
+          int KD = 1>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Args p) {
+  static_assert(KD == 1 || (KD == 3 && FWD && S == 1 && WCH == 1), "depth taps: stride-1 forwards");
   static_assert(NP == 3 || NP == 1, "three split planes (fp32 numerics) or one (bf16 operands)");
   static_assert(!AB || NP == 1, "bf16 storage with bf16 operands only");
   using TA = act_t<AB>;
@@ -107,7 +114,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
   const int tiles_per_img = p.tiles_h * p.tiles_w;
   const int n0 = blockIdx.y * NC;
   const int t0 = blockIdx.x * p.tpb, t1 = min(p.ntiles, t0 + p.tpb);
-  const int nch = p.C / PC;
+  const int nchc = p.C / PC, nch = KD * nchc;  // reduction chunks: (depth tap, channel chunk)
 
   // this lane's A pixel (MFMA row lane & 31) inside the tile
   const int m = wave * 32 + j;
@@ -131,16 +138,24 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
     oy0 = (tr / p.tiles_w) * TH;
     ox0 = (tr % p.tiles_w) * TW;
   };
-  auto fetch = [&](int tile, int c0, bool weights) {
+  auto fetch = [&](int tile, int ch, bool weights) {
     int img0, oy0, ox0;
     origin(tile, img0, oy0, ox0);
+    const int kd = ch / nchc, c0 = (ch - kd * nchc) * PC;
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
       const int q = tid + it * NTHR;
       const int row = q / G8;
       const int im = row / (PH * PW), rr = row % (PH * PW);
-      const int iy = oy0 * S - 1 + rr / PW, ix = ox0 * S - 1 + rr % PW, img = img0 + im;
-      pok[it] = q < PQ && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
+      const int iy = oy0 * S - 1 + rr / PW, ix = ox0 * S - 1 + rr % PW;
+      int img = img0 + im;
+      bool dok = true;
+      if constexpr (KD == 3) {  // depth slice d + kd - 1 of the same clip
+        const int d = img % p.D + kd - 1;
+        dok = d >= 0 && d < p.D;
+        img += kd - 1;
+      }
+      pok[it] = q < PQ && dok && img0 + im < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
       const TA* s = src + c0 + g8 * 8 + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
       pv[it][0] = act_ld4(s);
       pv[it][1] = act_ld4(s + 4);
@@ -151,16 +166,17 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
         const int q = tid + it * NTHR;
         const int n = q / (9 * G8), t = (q / G8) % 9;
         wok[it] = q < WQ && n0 + n < p.N;
-        const float* s = p.w + c0 + g8 * 8 +
+        const float* s = p.w + (int64_t)kd * p.N * 9 * p.C + c0 + g8 * 8 +
                          (wok[it] ? ((int64_t)(n0 + n) * 9 + (FWD ? t : 8 - t)) * p.C : (int64_t)0);
         wv[it][0] = *reinterpret_cast<const f32x4*>(s);
         wv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
       }
     }
   };
-  auto stash = [&](int tile, int c0, bool weights) {
+  auto stash = [&](int tile, int ch, bool weights) {
     int img0, oy0, ox0;
     origin(tile, img0, oy0, ox0);
+    const int c0 = (ch % nchc) * PC;
     // (BN constants loaded and used unconditionally -- from a dummy address when there is no BN -- so no load is
     // left pending on a branch the waitcnt analysis would have to assume, which made it drain the prefetch loads
     // before the first MFMA)
@@ -237,15 +253,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
   const int nitems = (t1 - t0) * nch;
   if (nitems > 0) fetch(t0, 0, true);
   for (int item = 0; item < nitems; ++item) {
-    const int tile = t0 + item / nch, ch = item % nch, c0 = ch * PC;
+    const int tile = t0 + item / nch, ch = item % nch;
     const bool wnow = WCH > 1 ? item < nch : (nch > 1 || item == 0);
     const int wseg = WCH > 1 ? ch * WCS : 0;
     __syncthreads();  // the previous item's fragment reads are done
-    stash(tile, c0, wnow);
+    stash(tile, ch, wnow);
     __syncthreads();
     if (item + 1 < nitems) {
       const int nx = item + 1;
-      fetch(t0 + nx / nch, (nx % nch) * PC, WCH > 1 ? nx < nch : nch > 1);
+      fetch(t0 + nx / nch, nx % nch, WCH > 1 ? nx < nch : nch > 1);
     }
     if (ch == 0) {
 #pragma unroll
@@ -301,7 +317,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
       }
     }
   }
-  if (FWD) {
+  if (FWD && p.partials) {
     __syncthreads();
     float* red = reinterpret_cast<float*>(sm);  // [NW waves][2][NC]
 #pragma unroll
@@ -440,6 +456,38 @@ int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, 
   // BN partial rows are bounded by conv3_patch_blocks (the caller's partial buffer)
   const int max_blocks = (int)std::min<int64_t>(conv3_patch_blocks(L.NF, L.OH, L.OW), 1 << 20);
   return L.stride == 1 ? dispatch_x3<1, true>(a, max_blocks, st, nparts) : dispatch_x3<2, true>(a, max_blocks, st, nparts);
+}
+
+// Conv3d 3x3x3 / stride 1 / padding 1 forward (+ bias, no BN sums) on NDHWC volumes: the KD = 3 instantiation of
+// conv3x3_x3_kernel on 256-pixel tiles of 8 waves (three split planes: fp32-class numerics)
+template <int NI, int TH, int TW, int NT>
+static int launch_x3_3d(X3Args a, hipStream_t st) {
+  a.tiles_h = (int)cdiv(a.OH, TH);
+  a.tiles_w = (int)cdiv(a.OW, TW);
+  a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);
+  const int ny = (int)cdiv(a.N, 32 * NT);
+  const int target = std::max(1, 512 * 4 / 8 / ny);
+  a.tpb = (int)cdiv(a.ntiles, target);
+  const int gx = (int)cdiv(a.ntiles, a.tpb);
+  VAD_KLAUNCH((conv3x3_x3_kernel<1, NI, TH, TW, NT, 16, true, 3, 1, 8, false, 3>), dim3(gx, ny), dim3(512), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int conv3d_x3_fwd(int B, int D, int H, int W, int C, int N, const float* src, const float* w3, const float* bias,
+                  float* out, hipStream_t st) {
+  VAD_CHECK(C % 16 == 0 && N % 32 == 0 && D >= 1, "conv3d_x3_fwd: C % 16 and N % 32");
+  VAD_CHECK(!g_act_bf16, "conv3d_x3_fwd: fp32 activations");
+  X3Args a{};
+  a.src = src;
+  a.w = w3;
+  a.bias = bias;
+  a.out = out;
+  a.NF = B * D; a.D = D; a.IH = H; a.IW = W; a.C = C; a.OH = H; a.OW = W; a.N = N;
+  const bool nt2 = N % 64 == 0;
+  if (H <= 8 && W <= 8) return nt2 ? launch_x3_3d<4, 8, 8, 2>(a, st) : launch_x3_3d<4, 8, 8, 1>(a, st);
+  if (W <= 16) return nt2 ? launch_x3_3d<2, 8, 16, 2>(a, st) : launch_x3_3d<2, 8, 16, 1>(a, st);
+  return nt2 ? launch_x3_3d<1, 8, 32, 2>(a, st) : launch_x3_3d<1, 8, 32, 1>(a, st);
 }
 
 int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st) {

@@ -110,3 +110,30 @@ def test_bbox_data_parallel_two_ranks(tmp_path):
     np.testing.assert_allclose(got["s"].numpy(), np.array([r[0] for r in ref], dtype=np.float32), rtol=1e-6,
                                atol=1e-7)
     np.testing.assert_allclose(got["f"].numpy(), np.stack([r[2] for r in ref]), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T,H,W", [(3, 7, 33, 50), (2, 2, 16, 18), (1, 32, 64, 64), (5, 9, 20, 70)])
+def test_bbox_encoder_ragged_shapes(B, T, H, W):
+    """The fused conv1 + ReLU + MaxPool3d kernel and the depth-tap split-bf16 Conv3d (implicit GEMM, no im2col) on
+    ragged shapes -- odd T (MaxPool3d floor), pooled planes that are not whole 8 x 8 / 8 x 32 tiles -- against the
+    oracle: features (1e-4 of their scale), scores and graphs within 1e-4; and equal (1e-5) to the im2col path."""
+    from vad_amd import _native as nat
+    m = make_bbox_model(dict(seed=40)).cuda()
+    p = {k: v.detach().cpu().clone() for k, v in make_bbox_model(dict(seed=40)).state_dict().items()}
+    x = bo.synth_clips(41, 0, 0, B, T, H, W)
+    with torch.no_grad():
+        rs, radj, rf = bo.bbox_forward(p, x)
+        outs = []
+        for im2col in (0, 1):
+            nat.check(nat.lib().vad_set_tuning(b"bbox_im2col", im2col))
+            try:
+                outs.append([t.cpu() for t in m(x.cuda())])
+            finally:
+                nat.check(nat.lib().vad_set_tuning(b"bbox_im2col", 0))
+    for s, adj, f in outs:
+        scale = float(rf.abs().max())
+        np.testing.assert_allclose(f.numpy(), rf.numpy(), rtol=1e-4, atol=1e-4 * scale)
+        np.testing.assert_allclose(s.reshape(-1).numpy(), rs.reshape(-1).numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(adj.numpy(), radj.numpy(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(outs[0][2].numpy(), outs[1][2].numpy(), rtol=1e-5, atol=1e-5 * float(rf.abs().max()))
