@@ -470,7 +470,7 @@ BBOX_FLOP_PER_FRAME = 2 * 4096 * 32 * 81 + 2 * 1024 * 64 * 864 // 2  # conv3d 3-
 BBOX_BYTES_PER_FRAME = 4 * (3 * 4096 + 2 * 32 * 4096 + 2 * 32 * 1024 // 2 + 2 * 64 * 1024 // 2)
 
 
-def bbox_roofline(frames_per_s):
+def bbox_roofline(frames_per_s, frames_per_step):
     """Config 5 (inference) against both ceilings SURVEY §8d names: fp32 FLOPs (the two Conv3d layers) and HBM bytes
     (per-layer compulsory fp32 I/O: the clip, conv1's output written and read by the pool, the pool output written
     and read by conv2, conv2's output written and read by the adaptive pool), per frame of a clip."""
@@ -478,14 +478,31 @@ def bbox_roofline(frames_per_s):
     gbs = frames_per_s * BBOX_BYTES_PER_FRAME / 1e9
     f_mfma, f_hbm = tf / PEAK_FP32_TFLOPS, gbs / PEAK_HBM_GBPS
     gov = "mfma" if f_mfma >= f_hbm else "hbm"
-    return {"bound": gov, "kernel": "whole step",
+    r = {"bound": gov, "kernel": "whole step",
             "achieved": round(tf if gov == "mfma" else gbs, 3), "peak": PEAK_FP32_TFLOPS if gov == "mfma" else PEAK_HBM_GBPS,
-            "unit": "TFLOP/s" if gov == "mfma" else "GB/s", "frac": round(max(f_mfma, f_hbm), 4), "traffic": None,
+            "unit": "TFLOP/s" if gov == "mfma" else "GB/s", "frac": round(max(f_mfma, f_hbm), 4),
+            "traffic": None, "algorithmic_bytes_per_step": BBOX_BYTES_PER_FRAME * frames_per_step,
             "other_ceiling": {"unit": "GB/s" if gov == "mfma" else "TFLOP/s",
                               "achieved": round(gbs if gov == "mfma" else tf, 3),
                               "frac": round(f_hbm if gov == "mfma" else f_mfma, 4)},
             "basis": f"{BBOX_FLOP_PER_FRAME} FLOP and {BBOX_BYTES_PER_FRAME} B (per-layer compulsory fp32 I/O) per frame"
                      " x frames scored per second; governing = the ceiling with the larger fraction"}
+    step, src = pmc_step("cfg5")
+    if step is not None:
+        r["traffic"] = round(step)
+        r["traffic_unit"] = "HBM bytes per step (every kernel; PMC FETCH_SIZE x2 + WRITE_SIZE)"
+        r["traffic_source"] = src
+    return r
+
+
+def pmc_step(tag):
+    """Whole-step HBM bytes from the latest committed PMC summary of this configuration, or (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{tag}_pmc_traffic.json")))
+    if not files:
+        return None, None
+    st = json.load(open(files[-1])).get("step")
+    return (st["hbm_bytes_per_step"], os.path.relpath(files[-1], ROOT)) if st else (None, None)
 
 
 MC_TRAIN_FLOP_PER_CLIP = 566.3e6  # SURVEY §8d: minicausal train step, T=16, 64x64
@@ -796,7 +813,7 @@ def main():
                                        "(inference)", "clips_per_gpu": args.batch, "clip_len": "8/16/32 mixed",
                            "frame": "3x64x64", "packing": "one batch per T", "parallelism": f"dp{world}",
                            "frames_per_step_per_gpu": r["frames"]},
-                "roofline": bbox_roofline(world * r["frames"] / (r["step_ms"] * 1e-3)),
+                "roofline": bbox_roofline(r["frames"] / (r["step_ms"] * 1e-3), r["frames"]),
                 "cpu_baseline": cpu, "parity": parity}), flush=True)
         finish(world)
         return

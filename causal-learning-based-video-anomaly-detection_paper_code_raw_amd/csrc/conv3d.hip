@@ -253,12 +253,50 @@ __global__ __launch_bounds__(256) void adaptive_avgpool3d_fwd_kernel(const float
   }
 }
 
+// one block per output bin (n, od, oh, ow): 64 channel lanes x 4 voxel groups, the NDHWC channel rows read
+// coalesced; each thread sums every 4th voxel of the bin in (d, h, w) order, the 4 partial sums combine in a fixed
+// order (large bins: the one-thread-per-output kernel above reads a stride-C column per thread)
+__global__ __launch_bounds__(256) void adaptive_avgpool3d_bin_kernel(const float* __restrict__ x,
+                                                                     const float* __restrict__ stats, int relu,
+                                                                     Vol5 v, int OD, int OH, int OW,
+                                                                     float* __restrict__ out) {
+  const int per = OD * OH * OW, C = v.C;
+  const int n = blockIdx.x / per, o = blockIdx.x % per;
+  const int od = o / (OH * OW), oh = (o / OW) % OH, ow = o % OW;
+  const int d0 = bin_start(od, v.D, OD), d1 = bin_end(od, v.D, OD);
+  const int h0 = bin_start(oh, v.H, OH), h1 = bin_end(oh, v.H, OH);
+  const int w0 = bin_start(ow, v.W, OW), w1 = bin_end(ow, v.W, OW);
+  const int nh = h1 - h0, nw = w1 - w0, nvox = (d1 - d0) * nh * nw;
+  const int lane = threadIdx.x & 63, vg = threadIdx.x >> 6;
+  __shared__ float red[4][64];
+  for (int cb = 0; cb < C; cb += 64) {
+    const int c = cb + lane;
+    float s = 0.f;
+    if (c < C)
+      for (int k = vg; k < nvox; k += 4) {
+        const int d = d0 + k / (nh * nw), h = h0 + (k / nw) % nh, w = w0 + k % nw;
+        s += pool_act(x, stats, relu, C, c, ((((int64_t)n * v.D + d) * v.H + h) * v.W + w) * C + c);
+      }
+    red[vg][lane] = s;
+    __syncthreads();
+    if (vg == 0 && c < C)
+      out[(int64_t)n * C * per + (int64_t)c * per + o] =
+          ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane])) / (float)nvox;
+    __syncthreads();
+  }
+}
+
 int adaptive_avgpool3d_fwd(const float* x, const float* stats, int relu, const Vol5& v, int OD, int OH, int OW,
                            float* out, hipStream_t st) {
   const int64_t total = (int64_t)v.N * v.C * OD * OH * OW;
   if (total == 0) return 0;
-  hipLaunchKernelGGL(adaptive_avgpool3d_fwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 16384)),
-                     dim3(256), 0, st, x, stats, relu, v, OD, OH, OW, out);
+  if ((int64_t)v.D * v.H * v.W >= 64LL * OD * OH * OW) {  // large bins: a block per bin
+    hipLaunchKernelGGL(adaptive_avgpool3d_bin_kernel, dim3((unsigned)((int64_t)v.N * OD * OH * OW)), dim3(256), 0, st,
+                       x, stats, relu, v, OD, OH, OW, out);
+  } else {
+    hipLaunchKernelGGL(adaptive_avgpool3d_fwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 16384)),
+                       dim3(256), 0, st, x, stats, relu, v, OD, OH, OW, out);
+  }
   VAD_LAUNCH_CHECK();
   return 0;
 }

@@ -4,7 +4,10 @@ the conv kernel families that bench.py can name as dominant.
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE / WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports
 half the bytes of 16-B-per-lane streaming reads (all conv kernels stage with 16-B loads), so it is doubled;
 WRITE_SIZE is exact for 16-B stores and taken as is for the 4-B epilogue stores (uncalibrated, noted).
-Usage: python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/<round>_pmc_traffic.json
+Usage: python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write [MARKER PER_STEP]
+            > profiles/<round>_cfg<N>_pmc_traffic.json
+MARKER / PER_STEP: a kernel-name substring launched PER_STEP times per bench step; with them the summary also
+carries the whole step's HBM bytes (every kernel of the run / the number of steps).
 """
 import collections
 import csv
@@ -49,6 +52,8 @@ def per_kernel(path, counter):
 def main():
     fetch, write = per_kernel(sys.argv[1], "FETCH_SIZE"), per_kernel(sys.argv[2], "WRITE_SIZE")
     fam = collections.defaultdict(lambda: {"launches": 0, "fetch": 0.0, "write": 0.0})
+    tot = {"fetch": 0.0, "write": 0.0}
+    kern = collections.defaultdict(lambda: {"launches": 0, "bytes": 0.0})
     # the two passes ran the same program: pair dispatches by kernel name in order
     wq = collections.defaultdict(list)
     for d in sorted(write):
@@ -59,7 +64,14 @@ def main():
         f = family(name)
         k = used[name]
         used[name] += 1
-        if f is None or k >= len(wq[name]):
+        if k >= len(wq[name]):
+            continue
+        tot["fetch"] += 2.0 * fb
+        tot["write"] += wq[name][k]
+        kn = kern[name.split("(")[0][:110]]
+        kn["launches"] += 1
+        kn["bytes"] += 2.0 * fb + wq[name][k]
+        if f is None:
             continue
         a = fam[f]
         a["launches"] += 1
@@ -72,6 +84,16 @@ def main():
         n = a["launches"]
         out["families"][f] = {"launches": n, "hbm_bytes_per_launch": (a["fetch"] + a["write"]) / n,
                               "read_bytes_per_launch": a["fetch"] / n, "write_bytes_per_launch": a["write"] / n}
+    if len(sys.argv) > 4:
+        marker, per_step = sys.argv[3], int(sys.argv[4])
+        n = sum(1 for d in fetch.values() if marker in d[0])
+        steps = n / per_step
+        out["step"] = {"steps": steps, "hbm_bytes_per_step": (tot["fetch"] + tot["write"]) / steps,
+                       "read_bytes_per_step": tot["fetch"] / steps, "write_bytes_per_step": tot["write"] / steps,
+                       "basis": f"all kernels of the run / ({n} launches of '{marker}' / {per_step} per step)"}
+        out["kernels_by_bytes_per_step"] = {k: {"launches_per_step": v["launches"] / steps,
+                                                "bytes_per_step": v["bytes"] / steps}
+                                            for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["bytes"])[:25]}
     json.dump(out, sys.stdout, indent=1)
 
 
