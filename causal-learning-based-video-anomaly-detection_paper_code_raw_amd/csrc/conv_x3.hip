@@ -718,6 +718,23 @@ struct WgX3Args {
 // LDS row pitch (elements, a multiple of 8) with an odd number of 16-B units: the 16 lanes of a b128 read phase
 // hit distinct bank quads
 constexpr int odd16_pitch(int n) { return ((n / 8) & 1) ? n : n + 8; }
+// Staging item t -> (4-channel group, 4-pixel chunk) of the weight-gradient kernels: a 16-lane ds_write_b64 group covers
+// 8 consecutive chunks (64 contiguous bytes) of 2 channel rows 4 rows apart, which the odd 16-B pitch puts 16 banks
+// apart -- all 32 banks, conflict-free (the previous t & 7 -> channel group mapping stored 8 rows at one column: 4-way,
+// SQ_LDS_BANK_CONFLICT 0.6 of the LDS cycles; tools/lds_conflicts.py).  ngroups channel groups; chunks of 8 x ngroups
+// items; the group depends on bits 3.. of t only, so a thread keeps its group across 256-item passes when
+// 16 % (ngroups / 2) == 0.
+// With bf16 activation storage (AB; config 4, HBM-bound) the staging loads are 8 B per lane and this mapping would read
+// each 128-B line in two halves from two wave-instructions (measured +43 us/step at config 4): AB keeps the
+// channel-fastest mapping (group = t % ngroups, chunk = t / ngroups), whose single bf16 plane costs few stores.
+template <bool AB>
+__device__ __forceinline__ int stage_group(int t, int ngroups) {
+  return AB ? t % ngroups : ((t >> 3) & 1) + 2 * ((t >> 4) % (ngroups / 2));
+}
+template <bool AB>
+__device__ __forceinline__ int stage_chunk(int t, int ngroups) {
+  return AB ? t / ngroups : (t & 7) + 8 * (t / (8 * ngroups));
+}
 
 __device__ __forceinline__ void wgrad_combine_store(f32x16 (&acc)[9], __bf16* sm, float* out, int co0, int ci0,
                                                     int Ci);
@@ -741,10 +758,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
   const int h = lane >> 5, j = lane & 31;
   const int co0 = blockIdx.x * 32, ci0 = blockIdx.y * 32;
   const int tiles_per_img = p.tiles_h * p.tiles_w;
-  const int c4 = tid & 7;  // staging: this thread's 4-channel group
+  const int c4 = stage_group<AB>(tid, 8);  // staging: this thread's 4-channel group
 
-  constexpr int XQ = NI * PH * NCG * 8, XIT = (XQ + 255) / 256;
-  constexpr int YQ = TPX / 4 * 8, YIT = (YQ + 255) / 256;
+  constexpr int XCH = NI * PH * NCG, XQ = (XCH + 7) / 8 * 64, XIT = (XQ + 255) / 256;  // patch: row x 4-column chunks
+  constexpr int YCH = TPX / 4, YQ = (YCH + 7) / 8 * 64, YIT = (YQ + 255) / 256;         // dY: 4-pixel chunks
   R4 xv[XIT][4], yv[YIT][4];
   auto origin = [&](int tile, int& i0, int& y0, int& x0) {
     i0 = (tile / tiles_per_img) * NI;
@@ -757,26 +774,26 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
     origin(tile, i0, y0, x0);
 #pragma unroll
     for (int it = 0; it < YIT; ++it) {
-      const int q = tid + it * 256, lin = (q >> 3) * 4;
+      const int yk = stage_chunk<AB>(tid + it * 256, 8), lin = yk * 4;
       const int mi = lin / (TH * TW), mr = lin % (TH * TW);
       const int oy = y0 + mr / TW, ox = x0 + mr % TW, img = i0 + mi;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         yv[it][e] = R4{};
-        if (q < YQ && img < p.NF && oy < p.OH && ox + e < p.OW)
+        if (yk < YCH && img < p.NF && oy < p.OH && ox + e < p.OW)
           yv[it][e] = act_ld4(dYp + (((int64_t)img * p.OH + oy) * p.OW + ox + e) * p.Co + co0 + c4 * 4);
       }
     }
 #pragma unroll
     for (int it = 0; it < XIT; ++it) {
-      const int q = tid + it * 256, g = q >> 3;
+      const int g = stage_chunk<AB>(tid + it * 256, 8);
       const int row = g / NCG, cg = g % NCG;
       const int mi = row / PH, iy = y0 - 1 + row % PH, img = i0 + mi;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int px = cg * 4 + e, ix = x0 - 1 + px;
         xv[it][e] = R4{};
-        if (q < XQ && px < PW && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
+        if (g < XCH && px < PW && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
           xv[it][e] = act_ld4(srcp + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.Ci + ci0 + c4 * 4);
       }
     }
@@ -819,16 +836,16 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3_kernel(const WgX3Args
     origin(tile, i0, y0, x0);
 #pragma unroll
     for (int it = 0; it < YIT; ++it) {
-      const int q = tid + it * 256;
-      if (q < YQ) {
+      const int yk = stage_chunk<AB>(tid + it * 256, 8);
+      if (yk < YCH) {
         const f32x4 v[4] = {act_f4(yv[it][0]), act_f4(yv[it][1]), act_f4(yv[it][2]), act_f4(yv[it][3])};
-        put4(ys + (q >> 3) * 4, DYP, TPX, v);
+        put4(ys + yk * 4, DYP, TPX, v);
       }
     }
 #pragma unroll
     for (int it = 0; it < XIT; ++it) {
-      const int q = tid + it * 256, g = q >> 3;
-      if (q < XQ) {
+      const int g = stage_chunk<AB>(tid + it * 256, 8);
+      if (g < XCH) {
         const int row = g / NCG, cg = g % NCG;
         const int mi = row / PH, iy = y0 - 1 + row % PH;
         f32x4 v[4];
@@ -970,12 +987,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Ar
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, j = lane & 31;
   const int co0 = blockIdx.x * NC, ci0 = blockIdx.y * 32;
-  const int c4 = tid & 7;  // patch staging: this thread's 4-channel group of the 32 ci
-  constexpr int YG = NC / 4, YQ = TPX / 4 * YG, YIT = (YQ + 255) / 256;  // dY staging: 4 pixels x 4 co per item
-  static_assert(256 % YG == 0 && (YQ <= 256 || YQ % 256 == 0), "whole dY staging passes");
-  const int yc = tid % YG;
+  const int c4 = stage_group<AB>(tid, 8);  // patch staging: this thread's 4-channel group of the 32 ci
+  // dY staging: 4 pixels x 4 co per item (stage_group / stage_chunk over YG co groups)
+  constexpr int YG = NC / 4, YCH = TPX / 4, YQ = (YCH + 7) / 8 * 8 * YG, YIT = (YQ + 255) / 256;
+  static_assert(YG % 2 == 0 && 16 % (YG / 2) == 0 && (YQ <= 256 || YQ % 256 == 0), "whole dY staging passes");
+  const int yc = stage_group<AB>(tid, YG);
 
-  constexpr int XQ = PH * NCG * 8, XIT = (XQ + 255) / 256;
+  constexpr int XCH = PH * NCG, XQ = (XCH + 7) / 8 * 64, XIT = (XQ + 255) / 256;
   static_assert(XIT <= 2, "patch staged in one register pass");
   R4 xv[XIT][4], yv[YIT][4];
   // patch column (0 = input column S*x0 - 1) held by LDS column c of a row
@@ -991,23 +1009,23 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Ar
     origin(tile, img, y0, x0);
 #pragma unroll
     for (int it = 0; it < YIT; ++it) {
-      const int yp = ((tid + it * 256) / YG) * 4, oy = y0 + yp / TW, ox = x0 + yp % TW;
+      const int yk = stage_chunk<AB>(tid + it * 256, YG), yp = yk * 4, oy = y0 + yp / TW, ox = x0 + yp % TW;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         yv[it][e] = R4{};
-        if (tid + it * 256 < YQ && oy < p.OH && ox + e < p.OW)
+        if (yk < YCH && tid + it * 256 < YQ && oy < p.OH && ox + e < p.OW)
           yv[it][e] = act_ld4(dYp + (((int64_t)img * p.OH + oy) * p.OW + ox + e) * p.Co + co0 + yc * 4);
       }
     }
 #pragma unroll
     for (int it = 0; it < XIT; ++it) {
-      const int q = tid + it * 256, g = q >> 3;
+      const int g = stage_chunk<AB>(tid + it * 256, 8);
       const int row = g / NCG, cg = g % NCG, iy = S * y0 - 1 + row;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int pc = pcol(cg * 4 + e), ix = S * x0 - 1 + pc;
         xv[it][e] = R4{};
-        if (q < XQ && pc < PW && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
+        if (g < XCH && pc < PW && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)
           xv[it][e] = act_ld4(srcp + (((int64_t)img * p.IH + iy) * p.IW + ix) * p.Ci + ci0 + c4 * 4);
       }
     }
@@ -1050,14 +1068,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_x3nt_kernel(const WgX3Ar
     origin(tile, img, y0, x0);
 #pragma unroll
     for (int it = 0; it < YIT; ++it)
-      if (tid + it * 256 < YQ) {
+      if (stage_chunk<AB>(tid + it * 256, YG) < YCH && tid + it * 256 < YQ) {
         const f32x4 v[4] = {act_f4(yv[it][0]), act_f4(yv[it][1]), act_f4(yv[it][2]), act_f4(yv[it][3])};
-        put4(ys + yc * 4 * DYP + ((tid + it * 256) / YG) * 4, DYP, TPX, v);
+        put4(ys + yc * 4 * DYP + stage_chunk<AB>(tid + it * 256, YG) * 4, DYP, TPX, v);
       }
 #pragma unroll
     for (int it = 0; it < XIT; ++it) {
-      const int q = tid + it * 256, g = q >> 3;
-      if (q < XQ) {
+      const int g = stage_chunk<AB>(tid + it * 256, 8);
+      if (g < XCH) {
         const int row = g / NCG, cg = g % NCG, iy = S * y0 - 1 + row;
         f32x4 v[4];
 #pragma unroll
