@@ -703,36 +703,37 @@ int avgpool_fwd(const float* y, const float* stats, int B, int T, int H, int W, 
   return 0;
 }
 
+// one block per (image, output row hh): thread c spreads the bins covering row hh over the W pixels of the row
+// (1024 blocks at config 2 instead of one 64-pixel loop per channel over 128 blocks)
 template <bool AB>
 __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restrict__ dfeat,
                                                           const float* __restrict__ dpooled, int B, int T, int H,
                                                           int W, int C, act_t<AB>* __restrict__ dA) {
-  const int img = blockIdx.y;
+  const int img = blockIdx.x, hh = blockIdx.y;
   const int b = img / T;
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float g[24];
   const float invT = 1.f / (float)T;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float g[4][6];  // (up to 4 row bins cover hh when H < 4)
+    int ni = 0, iv[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (int k = 0; k < 24; ++k) {
-    float v = dfeat ? dfeat[(int64_t)img * C * 24 + c * 24 + k] : 0.f;
-    if (dpooled) v += dpooled[(int64_t)b * C * 24 + c * 24 + k] * invT;
-    g[k] = v;
-  }
-  for (int hh = 0; hh < H; ++hh) {
+    for (int i = 0; i < 4; ++i)
+      if (hh >= ap_start(i, H, 4) && hh < ap_end(i, H, 4)) iv[ni++] = i;
+    for (int q = 0; q < ni; ++q) {
+      const int i = iv[q];
+      const float hn = (float)(ap_end(i, H, 4) - ap_start(i, H, 4));
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        float v = dfeat ? dfeat[(int64_t)img * C * 24 + c * 24 + i * 6 + j] : 0.f;
+        if (dpooled) v += dpooled[(int64_t)b * C * 24 + c * 24 + i * 6 + j] * invT;
+        g[q][j] = v / (hn * (float)(ap_end(j, W, 6) - ap_start(j, W, 6)));
+      }
+    }
     for (int ww = 0; ww < W; ++ww) {
       float s = 0.f;
+      for (int q = 0; q < ni; ++q)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int h0 = ap_start(i, H, 4), h1 = ap_end(i, H, 4);
-        if (hh < h0 || hh >= h1) continue;
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-          const int w0 = ap_start(j, W, 6), w1 = ap_end(j, W, 6);
-          if (ww < w0 || ww >= w1) continue;
-          s += g[i * 6 + j] / (float)((h1 - h0) * (w1 - w0));
-        }
-      }
+        for (int j = 0; j < 6; ++j)
+          if (ww >= ap_start(j, W, 6) && ww < ap_end(j, W, 6)) s += g[q][j];
       act_st(dA + (((int64_t)img * H + hh) * W + ww) * C + c, s);
     }
   }
@@ -740,12 +741,12 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restric
 
 int avgpool_bwd(const float* dfeat, const float* dpooled, int B, int T, int H, int W, int C, float* dA,
                 hipStream_t st) {
+  const dim3 grid((unsigned)(B * T), (unsigned)H);
   if (g_act_bf16)
-    hipLaunchKernelGGL(avgpool_bwd_kernel<true>, dim3((unsigned)cdiv(C, 256), B * T), dim3(256), 0, st, dfeat, dpooled,
-                       B, T, H, W, C, reinterpret_cast<__bf16*>(dA));
+    hipLaunchKernelGGL(avgpool_bwd_kernel<true>, grid, dim3(256), 0, st, dfeat, dpooled, B, T, H, W, C,
+                       reinterpret_cast<__bf16*>(dA));
   else
-    hipLaunchKernelGGL(avgpool_bwd_kernel<false>, dim3((unsigned)cdiv(C, 256), B * T), dim3(256), 0, st, dfeat,
-                       dpooled, B, T, H, W, C, dA);
+    hipLaunchKernelGGL(avgpool_bwd_kernel<false>, grid, dim3(256), 0, st, dfeat, dpooled, B, T, H, W, C, dA);
   VAD_LAUNCH_CHECK();
   return 0;
 }

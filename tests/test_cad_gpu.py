@@ -515,3 +515,25 @@ def test_module_api_detection_grads():
         np.testing.assert_allclose(p.grad.cpu().numpy(), pr.grad.numpy(), rtol=3e-3,
                                    atol=1e-7 + 2e-4 * ref_norm / np.sqrt(pr.numel()), err_msg=n)
     assert det_grad > 0.0
+
+
+@pytest.mark.parametrize("H,W", [(24, 40), (16, 16)])
+def test_small_frames_grads(H, W):
+    """Frames so small that the final map is 1 x 2 / 1 x 1: every AdaptiveAvgPool2d((4, 6)) bin covers the same rows
+    (up to 4 row bins per row in the backward), stride-2 layers on 2-wide maps.  Loss within 1e-4 and every gradient
+    tensor within relative L2 1e-4 of the mask-pinned float64 oracle."""
+    B, T = 2, 3
+    case = dict(name="small", B=B, T=T, H=H, W=W, seed=12, step=0, forced=None)
+    m = _frozen(make_cad_model(case)).cuda()
+    eng = m.engine()
+    x = co.synth_clips(12, 0, 0, B, T, H, W)
+    y = co.synth_labels(0, B)
+    o = eng.forward(x.cuda(), True, 12, 0, 0, y.cuda())
+    eng.backward(True)
+    torch.cuda.synchronize()
+    gr = eng.grads.cpu().numpy()
+    masks = hip_relu_masks(eng, B * T)
+    ref_grads, ref_losses, _ = pinned_oracle_grads(make_cad_model(case).state_dict(), x, y,
+                                                   co.CadDraws.make(12, 0, 0, B, T), masks)
+    assert float(o["losses"][4]) == pytest.approx(float(ref_losses["total"]), rel=1e-4)
+    check_pinned_grads(eng, gr, ref_grads)
