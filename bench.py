@@ -246,6 +246,21 @@ def run_gpu(args, rank, world, local_rank):
     t1 = time.perf_counter()
     elapsed = t1 - t0
     live = eng.profile_read()
+    # post-backbone chain (after the timed region, 3 more steps): end of the last forward conv to the start of the
+    # first backbone-backward kernel (avgpool_bwd), kernel-dispatch events only on those two launches
+    eng.profile(True, "conv_fwd/L7|avgpool_bwd")
+    for i in range(3):
+        trainer.step(pool[i % 2], labels)
+    torch.cuda.synchronize()
+    marks = eng.profile_marks()
+    eng.profile(False)
+    chain = []
+    for i, (lab, _, t1) in enumerate(marks):
+        if lab == "conv_fwd/L7":
+            nxt = [m for m in marks[i + 1:] if m[0] == "avgpool_bwd"]
+            if nxt:
+                chain.append(1e3 * (nxt[0][1] - t1))
+    post_backbone_us = sorted(chain)[len(chain) // 2] if chain else None
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -306,7 +321,7 @@ def run_gpu(args, rank, world, local_rank):
     step_flops = 2 * conv_flops + dgrad_flops + c1
     return dict(elapsed=elapsed, step_ms=step_ms, roof=roof, breakdown=breakdown, dominant=dominant,
                 final_loss=final_loss, step_tflops=step_flops / (step_ms * 1e-3) / 1e12, probe=probe, h2d=h2d,
-                allreduce_bytes=allreduce_bytes)
+                allreduce_bytes=allreduce_bytes, post_backbone_us=post_backbone_us)
 
 
 # SURVEY §8d fixed per-clip work of the train step: cfg 2 (T=16, 227^2, fp32) 20.25 GFLOP, MFMA-bound; cfg 4
@@ -846,6 +861,7 @@ def main():
             "bn_stats": "group (SyncBatchNorm)" if (args.sync_bn and world > 1) else "per rank",
             "step_roofline": step_roofline(args, clips / r["elapsed"] / world, r["step_tflops"]),
             "allreduce_bytes_per_step": r["allreduce_bytes"],
+            "post_backbone_us": (round(r["post_backbone_us"], 1) if r.get("post_backbone_us") is not None else None),
             "final_loss": r["final_loss"],
         }
         if args.breakdown_out:

@@ -60,6 +60,7 @@ _SIGS = {
     "vad_debug_d2h": (_I, [_P, _P, _I64]),
     "vad_cad_profile": (_I, [_P, _I, ctypes.c_char_p]),
     "vad_cad_profile_read": (_I, [_P, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I), _I]),
+    "vad_cad_profile_marks": (_I, [_P, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _I]),
     "vad_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "vad_conv3x3_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I64, _P]),
     # minicausal (config 1)

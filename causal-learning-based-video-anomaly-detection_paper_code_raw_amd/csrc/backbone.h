@@ -15,6 +15,7 @@ int conv1_num_parts(int NF, int OH);
 extern int g_x3_dgrad_blocks;  // knob "conv_dgrad_blocks"
 extern int g_x3_big;  // knob "conv_split_big"
 extern int g_x3_s2big;  // knob "conv_split_s2big"
+extern int g_cad_dir_affine;  // knob "cad_dir_affine": the direct classifier's loss-mode backward precomputed in the forward
 extern int g_cad_prep_stream, g_cad_wgrad_stream, g_cad_det_gate, g_cad_last_wgrad_main, g_cad_event_sysfence,
     g_cad_dy_per_layer;  // knobs "cad_prep_stream", "cad_wgrad_stream" (A/B)
 extern int g_stem_fused, g_stem_dbg;  // knobs "stem_fused" (default 1), "stem_dbg" (measurement only)
@@ -63,8 +64,10 @@ int maxpool3s2_bnrelu(const float* y, const float* stats, int NF, int H, int W, 
 // AdaptiveAvgPool2d((4,6)) of relu(bn(y)) -> features [NF][C*24] (torch flatten order) and the mean over T.
 int avgpool_fwd(const float* y, const float* stats, int B, int T, int H, int W, int C, float* feats, float* pooled,
                 hipStream_t st);
+// dA of relu(bn(y)) from the feature grads dfeat [NF][C*24] (nullable) and the clip-mean grads dpooled [B][C*24]
+// (nullable); with coef the clip-mean grads are dpooled[b] + coef[b] dpooled_c[b]
 int avgpool_bwd(const float* dfeat, const float* dpooled, int B, int T, int H, int W, int C, float* dA,
-                hipStream_t st);
+                hipStream_t st, const float* dpooled_c = nullptr, const float* coef = nullptr);
 
 // ---------------------------------------------------------------- 3x3 conv as implicit GEMM
 struct Conv3Layer {
@@ -154,9 +157,10 @@ int dense_fwd(const float* X, int M, int K, const float* W, const float* b, int 
 // split-K partials only: scratch[S][M][N] (finished by mlp_tail_fwd)
 int dense_fwd_splitk(const float* X, int M, int K, const float* W, int N, float* scratch, int64_t scratch_floats,
                      int* nsplit, hipStream_t st);
-// dX = (dY W) * gate', where gate' = (gate > 0 ? gscale : 0) when gate != nullptr
+// dX = (dY W) * gate', where gate' = (gate > 0 ? gscale : 0) when gate != nullptr; gate_rows > 0: row m is gated by
+// gate row m % gate_rows
 int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX, const float* gate, float gscale,
-                const int* skip, hipStream_t st);
+                const int* skip, hipStream_t st, int gate_rows = 0);
 // dW = dY^T X, db = colsum(dY) (written, not accumulated)
 int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW, float* db, float* scratch,
                 int64_t scratch_floats, const int* skip, hipStream_t st);

@@ -14,6 +14,7 @@ int g_cad_last_wgrad_main = 1;  // knob "cad_last_wgrad_main": layer 0's weight 
 int g_cad_event_sysfence = 0;  // knob "cad_event_sysfence": system-scope fence on the plan's stream-order events
 int g_cad_dy_per_layer = 1;  // knob "cad_dy_per_layer" (A/B of the plan option dy_per_layer)
 int g_cad_det_gate = 1;      // knob "cad_det_gate": the backbone backward waits on the device detector gate
+int g_cad_dir_affine = 1;  // knob "cad_dir_affine": direct classifier backward as A + c beta, precomputed in the forward
 int g_cad_wgrad_stream = 1;  // knob "cad_wgrad_stream": backbone weight gradients on their own stream
                              // reduce of layers 0-6, bit 2 the causal head's kernels
 
@@ -704,14 +705,18 @@ int avgpool_fwd(const float* y, const float* stats, int B, int T, int H, int W, 
 }
 
 // one block per (image, output row hh): thread c spreads the bins covering row hh over the W pixels of the row
-// (1024 blocks at config 2 instead of one 64-pixel loop per channel over 128 blocks)
+// (1024 blocks at config 2 instead of one 64-pixel loop per channel over 128 blocks).  coef != null: the clip-mean
+// gradient is dpooled[b] + coef[b] dpooled_c[b] (the direct classifier's affine backward, mlp.h DirMidArgs)
 template <bool AB>
 __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restrict__ dfeat,
-                                                          const float* __restrict__ dpooled, int B, int T, int H,
+                                                          const float* __restrict__ dpooled,
+                                                          const float* __restrict__ dpooled_c,
+                                                          const float* __restrict__ coef, int B, int T, int H,
                                                           int W, int C, act_t<AB>* __restrict__ dA) {
   const int img = blockIdx.x, hh = blockIdx.y;
   const int b = img / T;
   const float invT = 1.f / (float)T;
+  const float cb = coef ? coef[b] : 0.f;
   for (int c = threadIdx.x; c < C; c += 256) {
     float g[4][6];  // (up to 4 row bins cover hh when H < 4)
     int ni = 0, iv[4] = {0, 0, 0, 0};
@@ -724,7 +729,10 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restric
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         float v = dfeat ? dfeat[(int64_t)img * C * 24 + c * 24 + i * 6 + j] : 0.f;
-        if (dpooled) v += dpooled[(int64_t)b * C * 24 + c * 24 + i * 6 + j] * invT;
+        if (dpooled) {
+          const int64_t o = (int64_t)b * C * 24 + c * 24 + i * 6 + j;
+          v += (coef ? fmaf(cb, dpooled_c[o], dpooled[o]) : dpooled[o]) * invT;
+        }
         g[q][j] = v / (hn * (float)(ap_end(j, W, 6) - ap_start(j, W, 6)));
       }
     }
@@ -740,13 +748,14 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restric
 }
 
 int avgpool_bwd(const float* dfeat, const float* dpooled, int B, int T, int H, int W, int C, float* dA,
-                hipStream_t st) {
+                hipStream_t st, const float* dpooled_c, const float* coef) {
+  VAD_CHECK(!coef || (dpooled && dpooled_c), "avgpool_bwd: the affine form needs both parts");
   const dim3 grid((unsigned)(B * T), (unsigned)H);
   if (g_act_bf16)
-    hipLaunchKernelGGL(avgpool_bwd_kernel<true>, grid, dim3(256), 0, st, dfeat, dpooled, B, T, H, W, C,
-                       reinterpret_cast<__bf16*>(dA));
+    VAD_KLAUNCH(avgpool_bwd_kernel<true>, grid, dim3(256), 0, st, dfeat, dpooled, dpooled_c, coef, B, T, H, W, C,
+                reinterpret_cast<__bf16*>(dA));
   else
-    hipLaunchKernelGGL(avgpool_bwd_kernel<false>, grid, dim3(256), 0, st, dfeat, dpooled, B, T, H, W, C, dA);
+    VAD_KLAUNCH(avgpool_bwd_kernel<false>, grid, dim3(256), 0, st, dfeat, dpooled, dpooled_c, coef, B, T, H, W, C, dA);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -857,13 +866,14 @@ struct EpiPartial {  // split-K slab: part[z][row][col]
 struct DenseEpiArgs {
   float* out; int64_t ldc; const float* bias; int relu; int drop; uint64_t h1; uint32_t thr; float dscale;
   int64_t row0; const float* gate; float gscale;
+  int gmod;  // gate row = row % gmod when > 0 (the stacked rows of the direct classifier's affine backward)
 };
 
 __device__ inline float dense_finish(const DenseEpiArgs& P, int row, int col, float v) {
   if (P.bias) v += P.bias[col];
   if (P.relu) v = relu_nan(v);
   if (P.drop) v = (rng_u24(P.h1, (uint64_t)(P.row0 + row), (uint64_t)col) >= P.thr) ? v * P.dscale : 0.f;
-  if (P.gate) v = P.gate[(int64_t)row * P.ldc + col] > 0.f ? v * P.gscale : 0.f;
+  if (P.gate) v = P.gate[(int64_t)(P.gmod > 0 ? row % P.gmod : row) * P.ldc + col] > 0.f ? v * P.gscale : 0.f;
   return v;
 }
 
@@ -1002,6 +1012,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "bbox_im2col") g_bbox_im2col = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
+  else if (k == "cad_dir_affine") g_cad_dir_affine = value;
   else if (k == "cad_det_gate") g_cad_det_gate = value;
   else if (k == "cad_dy_per_layer") g_cad_dy_per_layer = value;
   else if (k == "cad_event_sysfence") g_cad_event_sysfence = value;
@@ -1421,14 +1432,15 @@ __global__ __launch_bounds__(512) void skinny_fwd_kernel(const float* __restrict
 }
 
 // dX[m][k] = gate(sum_n dY[m][n] W[n][k]): a block owns 64 consecutive k (one per lane), its 16 waves split N (8 W
-// loads in flight per lane); dY is staged in LDS as [n][MR] (broadcast reads), the waves are combined in a fixed order.
+// loads in flight per lane); dY is staged in LDS as [n][MR] (broadcast reads), the waves are combined in a fixed order
+// (wave q + wave q + 8, then the 8 pair sums in order: an 8-wave combine buffer, so 16 rows fit N <= 512 in 64 KB).
 template <int MR>
 __global__ __launch_bounds__(1024) void skinny_dgrad_kernel(const float* __restrict__ dY, int M, int N,
                                                             const float* __restrict__ W, int K, DenseEpiArgs P,
                                                             const int* skip) {
   if (skip && *skip == 0) return;
   constexpr int NW = 16, U = 8;
-  extern __shared__ __attribute__((aligned(16))) float dsm[];  // [N][MR] then [NW][MR][64]
+  extern __shared__ __attribute__((aligned(16))) float dsm[];  // [N][MR] then [NW / 2][MR][64]
   float* dys = dsm;
   float* red = dsm + (int64_t)N * MR;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1459,14 +1471,21 @@ __global__ __launch_bounds__(1024) void skinny_dgrad_kernel(const float* __restr
       }
     }
   }
+  if (wave >= NW / 2) {
 #pragma unroll
-  for (int m = 0; m < MR; ++m) red[(wave * MR + m) * 64 + lane] = acc[m];
+    for (int m = 0; m < MR; ++m) red[((wave - NW / 2) * MR + m) * 64 + lane] = acc[m];
+  }
+  __syncthreads();
+  if (wave < NW / 2) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m) red[(wave * MR + m) * 64 + lane] += acc[m];
+  }
   __syncthreads();
   if (wave == 0 && k < K) {
     for (int m = 0; m < M; ++m) {
       float v = 0.f;
 #pragma unroll
-      for (int q = 0; q < NW; ++q) v += red[(q * MR + m) * 64 + lane];
+      for (int q = 0; q < NW / 2; ++q) v += red[(q * MR + m) * 64 + lane];
       P.out[(int64_t)m * P.ldc + k] = dense_finish(P, m, k, v);
     }
   }
@@ -1543,17 +1562,17 @@ int dense_fwd_splitk(const float* X, int M, int K, const float* W, int N, float*
 }
 
 int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX, const float* gate, float gscale,
-                const int* skip, hipStream_t st) {
+                const int* skip, hipStream_t st, int gate_rows) {
   // dX[m][k] = sum_n dY[m][n] W[n][k]: A = dY (KC over n), B(row k, red n) = W[n][k] (KM, ld K)
   using C = T64x64;
-  DenseEpiArgs pe{dX, K, nullptr, 0, 0, 0, 0, 1.f, 0, gate, gscale};
-  if (skinny_ok(M, N) && (int64_t)(N + 1024) * (M <= 8 ? 8 : 16) * 4 <= 65536) {  // dY + combine buffer in LDS
+  DenseEpiArgs pe{dX, K, nullptr, 0, 0, 0, 0, 1.f, 0, gate, gscale, gate_rows};
+  if (skinny_ok(M, N) && (int64_t)(N + 512) * (M <= 8 ? 8 : 16) * 4 <= 65536) {  // dY + combine buffer in LDS
     const dim3 grid((unsigned)cdiv(K, 64));
     if (M <= 8)
-      hipLaunchKernelGGL(skinny_dgrad_kernel<8>, grid, dim3(1024), sizeof(float) * (N * 8 + 16 * 8 * 64), st, dY, M, N,
+      hipLaunchKernelGGL(skinny_dgrad_kernel<8>, grid, dim3(1024), sizeof(float) * (N * 8 + 8 * 8 * 64), st, dY, M, N,
                          W, K, pe, skip);
     else
-      hipLaunchKernelGGL(skinny_dgrad_kernel<16>, grid, dim3(1024), sizeof(float) * (N * 16 + 16 * 16 * 64), st, dY, M,
+      hipLaunchKernelGGL(skinny_dgrad_kernel<16>, grid, dim3(1024), sizeof(float) * (N * 16 + 8 * 16 * 64), st, dY, M,
                          N, W, K, pe, skip);
     VAD_LAUNCH_CHECK();
     return 0;

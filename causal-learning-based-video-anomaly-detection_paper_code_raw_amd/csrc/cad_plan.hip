@@ -274,7 +274,19 @@ struct Profiler {
     }
     return pool[used++];
   }
-  bool wants(const char* label) const { return on && std::string(label).rfind(only, 0) == 0; }
+  // only: a label prefix, or several separated by '|'
+  bool wants(const char* label) const {
+    if (!on) return false;
+    const std::string l(label);
+    size_t s = 0;
+    while (true) {
+      const size_t e = only.find('|', s);
+      const std::string pre = only.substr(s, e == std::string::npos ? std::string::npos : e - s);
+      if (l.rfind(pre, 0) == 0) return true;
+      if (e == std::string::npos) return false;
+      s = e + 1;
+    }
+  }
   void reset() { recs.clear(); used = 0; }
   ~Profiler() {
     for (auto e : pool) (void)hipEventDestroy(e);
@@ -335,6 +347,13 @@ struct CadPlanImpl {
   int grads_zeroed = 0;  // the last forward cleared the grad buffer for the backward that follows it
   float *d_causal, *d_kl, *d_glog, *d_dlog, *slabs, *d_feat_det, *d_pooled, *dense_scratch, *dense_scratch2;
   float *dg[5], *ddh[5];
+  // the direct classifier's affine loss-mode backward (knob "cad_dir_affine", B <= 8): the forward with labels leaves
+  // the input-gradient chain of the stacked rows [A; beta] (d_logits = A + c beta) in dl2 / dg2 / dpool2 while the side
+  // stream runs the causal head; a loss-mode backward folds in c (dir_pre).  tail_pre: the forward's loss tail also
+  // wrote the loss-mode upstream grads, so the backward's tail launch is skipped once.  dir_used: stage 0 took the
+  // affine path (stage 1 then reads the stacked clip-mean grads).
+  float *dl2 = nullptr, *dg2[4] = {}, *dpool2 = nullptr;
+  int dir_pre = 0, tail_pre = 0, dir_used = 0;
   float *dA, *dY, *dY2, *wpart, *stem_d;  // stem_d: [NF][H1][W1][32], the stem backward's dA / dY (stem_grad only)
   // per-layer dY buffers (option "dy_per_layer", default on): layer l's BN backward writes dYL[l], which only layer l's
   // weight and input gradients read, so the compute stream never waits for the weight-gradient stream to release a
@@ -487,7 +506,10 @@ struct CadPlanImpl {
     for (int i = 0; i < 4; ++i) {
       ddh[i] = w.take<float>(nf * dd[i]);
       dg[i] = w.take<float>((int64_t)B * gd[i]);
+      dg2[i] = w.take<float>(2ll * B * gd[i]);
     }
+    dl2 = w.take<float>(2ll * B * 2);
+    dpool2 = w.take<float>(2ll * B * 6144);
     dense_scratch_floats = std::max<int64_t>(512ll * 6145, 16ll * nf * 512);
     dense_scratch_floats = std::max<int64_t>(dense_scratch_floats, 16ll * B * 512);
     dense_scratch = w.take<float>(dense_scratch_floats);
@@ -729,14 +751,35 @@ struct CadPlanImpl {
     }
     // direct_classifier on the mean over T (cad:525-538, 568-570)
     // (B rows only: one block per 64 columns, so the chain runs layer by layer on many CUs; layers 1-4 unsplit)
+    // With labels (and B <= 8) layers 2-4 run in dir_mid together with the loss-mode input-gradient chain of the
+    // stacked rows [A; beta], layers 1 and 0 of that chain follow: the backward then only folds in the causal score
+    dir_pre = tail_pre = 0;
+    const bool affine = labels != nullptr && g_cad_dir_affine != 0 && B <= 8;
     const float* in = pooled;
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < (affine ? 2 : 5); ++i) {
       float* out = i < 4 ? gh[i] : glog;
       const int sid = i == 0 ? S_DIRECT_DROP1 : (i == 1 ? S_DIRECT_DROP2 : 0);
       TIMED("dir_fwd", dense_fwd(in, B, gd[i], P(LY.dir_w[i]), P(LY.dir_b[i]), gd[i + 1], out,
                                  act(i < 4, sid, i == 0 ? 0.3 : 0.2, clip0), dense_scratch, dense_scratch_floats, st,
                                  i == 0 ? 0 : 1));
       in = out;
+    }
+    if (affine) {
+      const float gs0 = training ? (float)(1.0 / (1.0 - 0.3)) : 1.f, gs1 = training ? (float)(1.0 / (1.0 - 0.2)) : 1.f;
+      DirMidArgs da{};
+      da.B = B;
+      da.h1 = gh[1];
+      da.W2 = P(LY.dir_w[2]); da.b2 = P(LY.dir_b[2]);
+      da.W3 = P(LY.dir_w[3]); da.b3 = P(LY.dir_b[3]);
+      da.W4 = P(LY.dir_w[4]); da.b4 = P(LY.dir_b[4]);
+      da.h2 = gh[2]; da.h3 = gh[3]; da.logits = glog;
+      da.labels = labels;
+      da.gs1 = gs1;
+      da.dl2 = dl2; da.d3 = dg2[3]; da.d2 = dg2[2]; da.d1 = dg2[1];
+      TIMED("dir_fwd", dir_mid(da, st));
+      TIMED("dir_pre", dense_dgrad(dg2[1], 2 * B, 256, P(LY.dir_w[1]), 512, dg2[0], gh[0], gs0, nullptr, st, B));
+      TIMED("dir_pre", dense_dgrad(dg2[0], 2 * B, 512, P(LY.dir_w[0]), 6144, dpool2, nullptr, 1.f, nullptr, st));
+      dir_pre = tail_pre = 1;
     }
     // the detector's input gradient buffer is zero unless its backward writes it (the backward skips it on device when
     // no box was in range); cleared here, where the main stream has slack
@@ -754,6 +797,7 @@ struct CadPlanImpl {
     }
     VAD_TRY(join(st));
     TailArgs t = tail_args(nullptr, nullptr, nullptr, nullptr);
+    t.fwd_bwd = tail_pre;
     if (training && nbt) {  // num_batches_tracked of the 9 BN layers (bumped by the tail kernel)
       t.nbt = nbt;
       t.nbt_n = 9;
@@ -807,7 +851,11 @@ struct CadPlanImpl {
     grads_zeroed = 0;
     TailArgs t = use_loss ? tail_args(nullptr, nullptr, nullptr, nullptr) : tail_args(dfin, dprobs, dcaus, dkl);
     if (!use_loss) t.labels = nullptr;
-    TIMED("tail", cad_tail_bwd(t, st));
+    // (the forward's loss tail already wrote the loss-mode upstream grads and armed the gate: skipped once)
+    if (!(use_loss && tail_pre)) TIMED("tail", cad_tail_bwd(t, st));
+    tail_pre = 0;
+    const bool aff = use_loss && dir_pre;
+    dir_used = aff ? 1 : 0;
     const int gd[6] = {6144, 512, 256, 128, 64, 2};
     const int dd[6] = {6144, 512, 256, 128, 64, 20};
     VAD_TRY(fork(st));
@@ -818,8 +866,9 @@ struct CadPlanImpl {
       TIMED("head_bwd", head_bwd(head_args(), dlog, head_out(), up, slabs, slab_len, d_dlog, st));
     }
     // direct classifier chain (B rows): per-layer input-gradient GEMMs spread over many CUs, the layer 1-4 weight
-    // grads in one launch, layer 0 GEMMs
-    {
+    // grads in one launch, layer 0 GEMMs.  (Affine path: the forward ran the input-gradient chain; the weight grads
+    // follow the detector chain on the side stream.)
+    if (!aff) {
       const double gp[4] = {0.3, 0.2, 0.0, 0.0};
       const float* dcur = d_glog;
       for (int i = 4; i >= 1; --i) {
@@ -828,16 +877,35 @@ struct CadPlanImpl {
                                      st));
         dcur = dg[i - 1];
       }
+      TIMED("dir_bwd", rows_wgrad(mlp_wgrad_args(B, d_glog, gd, LY.dir_w, LY.dir_b, gh, dg, nullptr), st));
+      TIMED("dir_bwd", dense_wgrad(dg[0], B, 512, pooled, 6144, G(LY.dir_w[0]), G(LY.dir_b[0]), dense_scratch,
+                                   dense_scratch_floats, nullptr, st));
+      TIMED("dir_bwd", dense_dgrad(dg[0], B, 512, P(LY.dir_w[0]), 6144, d_pooled, nullptr, 1.f, nullptr, st));
     }
-    TIMED("dir_bwd", rows_wgrad(mlp_wgrad_args(B, d_glog, gd, LY.dir_w, LY.dir_b, gh, dg, nullptr), st));
-    TIMED("dir_bwd", dense_wgrad(dg[0], B, 512, pooled, 6144, G(LY.dir_w[0]), G(LY.dir_b[0]), dense_scratch,
-                                 dense_scratch_floats, nullptr, st));
-    TIMED("dir_bwd", dense_dgrad(dg[0], B, 512, P(LY.dir_w[0]), 6144, d_pooled, nullptr, 1.f, nullptr, st));
     // side stream, continued: the detector chain (it feeds the backbone: event ev_det / the gate word), then the
     // head's weight grads, which only the optimizer / the grad all-reduce wait for.  (It must be queued BEFORE the
     // compute stream's wait on the gate: streams share a few hardware queues, and a wait queued ahead of the work
     // that releases it on the same hardware queue never completes -- measured: a hang in the forced regime.)
     VAD_TRY(side_det_chain(st2));
+    if (aff) {  // the stacked rows folded with the causal score, then the classifier's weight grads (side stream)
+      hipStream_t st = st2;
+      DirCombineArgs ca{};
+      ca.B = B;
+      ca.c = causal;
+      ca.nseg = 5;
+      for (int i = 0; i < 4; ++i) {
+        ca.src[i] = dg2[i];
+        ca.dst[i] = dg[i];
+        ca.width[i] = gd[i + 1];
+      }
+      ca.src[4] = dpool2;
+      ca.dst[4] = d_pooled;
+      ca.width[4] = 6144;
+      TIMED("dir_bwd", dir_combine(ca, st));
+      TIMED("dir_bwd", rows_wgrad(mlp_wgrad_args(B, d_glog, gd, LY.dir_w, LY.dir_b, gh, dg, nullptr), st));
+      TIMED("dir_bwd", dense_wgrad(dg[0], B, 512, pooled, 6144, G(LY.dir_w[0]), G(LY.dir_b[0]), dense_scratch,
+                                   dense_scratch_floats, nullptr, st));
+    }
     // stage 0: every non-backbone grad is final on the caller's stream when it returns.  Stage 2 (= stage 0 for a
     // caller that orders its own consumer after the side stream with vad_cad_wait_side): the head / detector chain
     // keeps running on the side stream and the backbone (stage 1) waits only for the detector input gradient
@@ -849,7 +917,11 @@ struct CadPlanImpl {
     if (stage == 0 || stage == 2) return 0;
     // backbone (BatchNorm backward as streaming passes: the conv kernels are MFMA/LDS-bound and slowed down more by
     // extra loads than the separate 6 TB/s passes cost -- DESIGN.md §6, BN-backward fusion experiment)
-    TIMED("avgpool_bwd", avgpool_bwd(d_feat_det, d_pooled, B, T, HF, WF, 256, dA, st));
+    if (dir_used)  // clip-mean grads A + c beta, folded while spreading them over the map
+      TIMED("avgpool_bwd", avgpool_bwd(d_feat_det, dpool2, B, T, HF, WF, 256, dA, st, dpool2 + (int64_t)B * 6144,
+                                       causal));
+    else
+      TIMED("avgpool_bwd", avgpool_bwd(d_feat_det, d_pooled, B, T, HF, WF, 256, dA, st));
     VAD_TRY(streams());
     const bool wgs = wgrad_stream != 0 && g_cad_wgrad_stream;
     bool st3_joined = false;
@@ -1289,6 +1361,26 @@ int vad_cad_profile_read(vad_cad_plan* plan, char* labels, double* total_ms, int
     counts[i] = cnt[i];
   }
   return (int)names.size();
+}
+
+/* the recorded launches one by one, in record order: label, start and end in ms after the first record's start (the
+ * post-backbone chain measurement: start of avgpool_bwd minus end of the last forward conv).  Returns the number of
+ * records; fills at most cap. */
+int vad_cad_profile_marks(vad_cad_plan* plan, char* labels, double* t0_ms, double* t1_ms, int cap) {
+  VAD_CHECK(plan != nullptr, "vad_cad_profile_marks: null plan");
+  Profiler& p = plan->impl.prof;
+  for (size_t i = 0; i < p.recs.size() && (int)i < cap; ++i) {
+    const auto& r = p.recs[i];
+    float a = 0.f, b = 0.f;
+    VAD_HIP(hipEventSynchronize(r.b));
+    VAD_HIP(hipEventElapsedTime(&a, p.recs[0].a, r.a));
+    VAD_HIP(hipEventElapsedTime(&b, p.recs[0].a, r.b));
+    strncpy(labels + 64 * i, r.label.c_str(), 63);
+    labels[64 * i + 63] = 0;
+    t0_ms[i] = a;
+    t1_ms[i] = b;
+  }
+  return (int)p.recs.size();
 }
 
 int vad_debug_d2h(void* host, const void* dev, int64_t bytes) {

@@ -103,6 +103,8 @@ struct TailArgs {
   float* d_direct_logits;       // [B][2]
   int64_t* nbt;                 // forward: BN num_batches_tracked counters bumped (train mode) or null
   int nbt_n;
+  int fwd_bwd;                  // forward with labels: also write the loss-mode upstream grads (the backward then
+                                // skips its tail launch)
 };
 int cad_tail_fwd(const TailArgs& t, hipStream_t st);
 int cad_tail_bwd(const TailArgs& t, hipStream_t st);

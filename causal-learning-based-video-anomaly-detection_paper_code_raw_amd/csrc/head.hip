@@ -1016,6 +1016,28 @@ int head_rows_wgrad(const HeadArgs& a, hipStream_t st) {
 }
 
 // ================================================================== tail: softmax, blend, losses
+// loss-mode upstream grads of clip b (cad:655-676 through the blend fin = 0.6 c + 0.4 p1 and the softmax)
+__device__ inline void tail_loss_grads(const TailArgs& t, int b, float p0, float p1, float c, float fin) {
+  const float fB = (float)t.B;
+  const int y = (int)t.labels[b];
+  const float yf = (float)y;
+  float d_final = 0.3f * 2.f * (fin - yf) / fB;
+  float d_c = 0.2f * 2.f * (c - yf) / fB;
+  const float m2 = fmaxf(p0, p1);
+  const float e0 = expf(p0 - m2), e1 = expf(p1 - m2);
+  const float q0 = e0 / (e0 + e1), q1 = e1 / (e0 + e1);
+  float dp0 = 0.4f * (q0 - (y == 0 ? 1.f : 0.f)) / fB;
+  float dp1 = 0.4f * (q1 - (y == 1 ? 1.f : 0.f)) / fB;
+  const float dk = isfinite(t.kl[b]) ? 0.1f / fB : 0.f;
+  d_c += 0.6f * d_final;
+  dp1 += 0.4f * d_final;
+  const float dot = p0 * dp0 + p1 * dp1;  // through softmax: dl = p * (dp - <p, dp>)
+  t.d_direct_logits[b * 2] = p0 * (dp0 - dot);
+  t.d_direct_logits[b * 2 + 1] = p1 * (dp1 - dot);
+  t.d_causal[b] = d_c;
+  t.d_kl[b] = dk;
+}
+
 __global__ void cad_tail_fwd_kernel(TailArgs t) {
   const int B = t.B;
   if (t.nbt && (int)threadIdx.x < t.nbt_n) t.nbt[threadIdx.x] += 1;
@@ -1045,6 +1067,7 @@ __global__ void cad_tail_fwd_kernel(TailArgs t) {
       ca += (c - yf) * (c - yf);
       const float k = t.kl[b];
       if (isfinite(k)) kl += k;
+      if (t.fwd_bwd) tail_loss_grads(t, b, p0, p1, c, fin);
     }
   }
   red[0][threadIdx.x] = cls;
@@ -1090,32 +1113,21 @@ int cad_tail_fwd(const TailArgs& t, hipStream_t st) {
 // upstream grads: from the loss (labels) or from external autograd grads
 __global__ void cad_tail_bwd_kernel(TailArgs t) {
   const int B = t.B;
-  const float fB = (float)B;
   // re-arm the detector gate for this backward (a second backward on the same forward must wait for its own detector
   // input gradient again): 0 = wait, 1 = no detector gradient (no box in range)
   if (threadIdx.x == 0 && t.det_gate) *t.det_gate = t.flags[0] ? 0ull : 1ull;
   for (int b = threadIdx.x; b < B; b += 256) {
     const float p0 = t.probs[b * 2], p1 = t.probs[b * 2 + 1];
     const float c = t.causal[b], fin = t.final_scores[b];
-    float d_final = 0.f, d_c = 0.f, dp0 = 0.f, dp1 = 0.f, dk = 0.f;
     if (t.labels) {
-      const int y = (int)t.labels[b];
-      const float yf = (float)y;
-      d_final = 0.3f * 2.f * (fin - yf) / fB;
-      d_c = 0.2f * 2.f * (c - yf) / fB;
-      const float m2 = fmaxf(p0, p1);
-      const float e0 = expf(p0 - m2), e1 = expf(p1 - m2);
-      const float q0 = e0 / (e0 + e1), q1 = e1 / (e0 + e1);
-      dp0 = 0.4f * (q0 - (y == 0 ? 1.f : 0.f)) / fB;
-      dp1 = 0.4f * (q1 - (y == 1 ? 1.f : 0.f)) / fB;
-      dk = isfinite(t.kl[b]) ? 0.1f / fB : 0.f;
-    } else {
-      d_final = t.ext_d_final ? t.ext_d_final[b] : 0.f;
-      d_c = t.ext_d_causal ? t.ext_d_causal[b] : 0.f;
-      dp0 = t.ext_d_probs ? t.ext_d_probs[b * 2] : 0.f;
-      dp1 = t.ext_d_probs ? t.ext_d_probs[b * 2 + 1] : 0.f;
-      dk = t.ext_d_kl ? t.ext_d_kl[b] : 0.f;
+      tail_loss_grads(t, b, p0, p1, c, fin);
+      continue;
     }
+    float d_final = t.ext_d_final ? t.ext_d_final[b] : 0.f;
+    float d_c = t.ext_d_causal ? t.ext_d_causal[b] : 0.f;
+    float dp0 = t.ext_d_probs ? t.ext_d_probs[b * 2] : 0.f;
+    float dp1 = t.ext_d_probs ? t.ext_d_probs[b * 2 + 1] : 0.f;
+    const float dk = t.ext_d_kl ? t.ext_d_kl[b] : 0.f;
     d_c += 0.6f * d_final;
     dp1 += 0.4f * d_final;
     const float dot = p0 * dp0 + p1 * dp1;  // through softmax: dl = p * (dp - <p, dp>)

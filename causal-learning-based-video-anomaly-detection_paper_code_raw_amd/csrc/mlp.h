@@ -47,6 +47,30 @@ struct MlpTailBwdArgs {
 
 extern int g_mlp_tail_wide;  // knob "mlp_tail_wide"
 int mlp_tail_fwd(const MlpTailArgs& a, hipStream_t st);
+// Direct classifier (cad:525-538) with its loss-mode backward precomputed as an affine function of the causal score
+// c (cad:655-676): with fin = 0.6 c + 0.4 p1 the upstream gradient of the logits is d_l[b] = A[b] + c[b] beta[b], and
+// the classifier's input-gradient chain is linear in d_l, so it runs on the 2B stacked rows [A; beta] while the causal
+// head computes c (B <= 8).  dir_mid runs layers 2-4 forward, the seed rows and the layer 4-2 input gradients in one block.
+struct DirMidArgs {
+  int B;
+  const float* h1;                                   // [B][256] (layer 1 output, after dropout)
+  const float *W2, *b2, *W3, *b3, *W4, *b4;          // [128][256], [64][128], [2][64]
+  float *h2, *h3, *logits;                           // [B][128], [B][64], [B][2]
+  const int64_t* labels;                             // [B]
+  float gs1;                                         // gate scale of layer 1's output (1 / (1 - 0.2) in training)
+  float *dl2, *d3, *d2, *d1;                         // [2B][2], [2B][64], [2B][128], [2B][256]
+};
+int dir_mid(const DirMidArgs& a, hipStream_t st);
+// dst_s[b][k] = src_s[b][k] + c[b] src_s[B + b][k] for up to 6 segments (the stacked rows folded once c is known)
+struct DirCombineArgs {
+  int B, nseg;
+  const float* c;
+  const float* src[6];
+  float* dst[6];
+  int width[6];
+};
+int dir_combine(const DirCombineArgs& a, hipStream_t st);
+
 int mlp_tail_bwd(const MlpTailBwdArgs& a, hipStream_t st);
 
 // dW[o][i] = sum_r A[r][o] X[r][i], db[o] = sum_r A[r][o] for up to ROWS_WGRAD_MAXSEG Linear layers, one launch

@@ -227,6 +227,210 @@ int rows_wgrad(const RowsWgradArgs& a, hipStream_t st) {
   return 0;
 }
 
+// ------------------------------------------------------------------ direct classifier: affine loss-mode backward
+// Sum over the 64 lanes of R per-lane values at once (reduce-scatter over lane bits 0 .. log2 R - 1, then a butterfly
+// over the remaining bits): R - 1 + 6 - log2 R shuffles instead of 6 R.  Every lane returns the total of row
+// rs_row<R>(lane) (the bit reversal of its low log2 R lane bits).
+template <int R>
+__device__ __forceinline__ float rs_sum(float (&v)[R], int lane) {
+  constexpr int LG = R >= 32 ? 5 : R >= 16 ? 4 : R >= 8 ? 3 : R >= 4 ? 2 : R >= 2 ? 1 : 0;
+  static_assert((1 << LG) == R, "power of two rows");
+#pragma unroll
+  for (int s = 0; s < LG; ++s) {
+    const int half = R >> (s + 1);
+    const bool up = (lane >> s) & 1;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const float keep = up ? v[i + half] : v[i];
+      const float send = up ? v[i] : v[i + half];
+      v[i] = keep + __shfl_xor(send, 1 << s, 64);
+    }
+  }
+  float x = v[0];
+#pragma unroll
+  for (int b = LG; b < 6; ++b) x += __shfl_xor(x, 1 << b, 64);
+  return x;
+}
+template <int R>
+__device__ __forceinline__ int rs_row(int lane) {
+  int r = 0;
+#pragma unroll
+  for (int s = 0; (R >> (s + 1)) >= 1; ++s) r |= ((lane >> s) & 1) * (R >> (s + 1));
+  return r;
+}
+
+// out[r][o] = act(b[o] + sum_i W[o][i] in[r][i]) for RB rows (LDS in / out, rows >= B are zero): wave w takes the
+// outputs o = w (mod 16), lane l the inputs 4l .. 4l + 3 (coalesced row loads, all of a wave's rows issued first)
+template <int RB, int I, int O, bool RELU>
+__device__ __forceinline__ void dir_layer_fwd(const float* __restrict__ W, const float* __restrict__ bias,
+                                              const float (*in)[I], float (*out)[O], float* gout, int B) {
+  static_assert(I % 4 == 0 && I <= 256, "one float4 of the row per lane");
+  constexpr int NO = (O + 15) / 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool act = 4 * lane < I;
+  f32x4 w[NO];
+#pragma unroll
+  for (int q = 0; q < NO; ++q) {
+    const int o = wave + 16 * q;
+    w[q] = (act && o < O) ? *reinterpret_cast<const f32x4*>(W + (int64_t)o * I + 4 * lane) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int q = 0; q < NO; ++q) {
+    const int o = wave + 16 * q;
+    if (o >= O) break;  // (wave-uniform)
+    float v[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const f32x4 x = act ? *reinterpret_cast<const f32x4*>(&in[r][4 * lane]) : f32x4{0.f, 0.f, 0.f, 0.f};
+      v[r] = fmaf(w[q][3], x[3], fmaf(w[q][2], x[2], fmaf(w[q][1], x[1], w[q][0] * x[0])));
+    }
+    const float s = rs_sum<RB>(v, lane);
+    if (lane < RB) {
+      const int r = rs_row<RB>(lane);
+      float y = s + bias[o];
+      if (RELU) y = relu_nan(y);
+      if (r >= B) y = 0.f;
+      out[r][o] = y;
+      if (r < B) gout[(int64_t)r * O + o] = y;
+    }
+  }
+}
+
+// din[r][i] = (sum_o W[o][i] dout[r][o]) * (gate[r % B][i] > 0 ? gs : 0) for R2 stacked rows (rows >= 2B zero):
+// thread (i, slice) accumulates its slice of o (coalesced W row reads), the S slices are combined in a fixed order
+template <int R2, int I, int O>
+__device__ __forceinline__ void dir_layer_bwd(const float* __restrict__ W, const float (*dout)[O],
+                                              const float (*gate)[I], float gs, float (*din)[I], float* gdin, int B,
+                                              float* red) {
+  constexpr int S = 1024 / I, OPS = (O + S - 1) / S;
+  const int i = threadIdx.x % I, sl = threadIdx.x / I;
+  const int o0 = sl * OPS, o1 = min(O, o0 + OPS);
+  float acc[R2];
+#pragma unroll
+  for (int r = 0; r < R2; ++r) acc[r] = 0.f;
+  for (int ob = o0; ob < o1; ob += 8) {
+    float w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) w[u] = ob + u < o1 ? W[(int64_t)(ob + u) * I + i] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (ob + u >= o1) break;
+#pragma unroll
+      for (int r = 0; r < R2; ++r) acc[r] = fmaf(w[u], dout[r][ob + u], acc[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R2; ++r) red[(sl * R2 + r) * I + i] = acc[r];
+  __syncthreads();
+  for (int q = threadIdx.x; q < R2 * I; q += 1024) {
+    const int r = q / I, ii = q % I;
+    float v = 0.f;
+    for (int t = 0; t < S; ++t) v += red[(t * R2 + r) * I + ii];
+    v = (r < 2 * B && gate[r % B][ii] > 0.f) ? v * gs : 0.f;
+    if (din) din[r][ii] = v;
+    if (r < 2 * B) gdin[(int64_t)r * I + ii] = v;
+  }
+  __syncthreads();
+}
+
+template <int RB>
+__global__ __launch_bounds__(1024) void dir_mid_kernel(const DirMidArgs a) {
+  constexpr int R2 = 2 * RB;
+  __shared__ __attribute__((aligned(16))) float in1[RB][256];
+  __shared__ __attribute__((aligned(16))) float a2[RB][128];
+  __shared__ __attribute__((aligned(16))) float a3[RB][64];
+  __shared__ __attribute__((aligned(16))) float lg[RB][2];
+  __shared__ __attribute__((aligned(16))) float dl[R2][2];
+  __shared__ __attribute__((aligned(16))) float dd3[R2][64];
+  __shared__ __attribute__((aligned(16))) float dd2[R2][128];
+  __shared__ __attribute__((aligned(16))) float red[4 * R2 * 256];
+  const int B = a.B, tid = threadIdx.x;
+  for (int q = tid; q < RB * 256; q += 1024) in1[q / 256][q % 256] = q / 256 < B ? a.h1[q] : 0.f;
+  __syncthreads();
+  dir_layer_fwd<RB, 256, 128, true>(a.W2, a.b2, in1, a2, a.h2, B);
+  __syncthreads();
+  dir_layer_fwd<RB, 128, 64, true>(a.W3, a.b3, a2, a3, a.h3, B);
+  __syncthreads();
+  dir_layer_fwd<RB, 64, 2, false>(a.W4, a.b4, a3, lg, a.logits, B);
+  __syncthreads();
+  // seed rows: softmax, cross entropy on the probabilities (cad:673) and the c-free / c-linear parts of the anomaly
+  // MSE through fin (cad:674), then the softmax backward -- the per-row arithmetic of cad_tail_bwd_kernel
+  if (tid < R2) {
+    float d0 = 0.f, d1 = 0.f;
+    const int b = tid % RB;
+    if (b < B && (tid < RB || tid - RB < B)) {
+      const bool beta = tid >= RB;
+      const float fB = (float)B;
+      const float l0 = lg[b][0], l1 = lg[b][1];
+      const float mx = fmaxf(l0, l1);
+      const float e0 = expf(l0 - mx), e1 = expf(l1 - mx);
+      const float p0 = e0 / (e0 + e1), p1 = e1 / (e0 + e1);
+      const int y = (int)a.labels[b];
+      const float yf = (float)y;
+      float dp0, dp1;
+      const float k = 0.4f * (0.3f * 2.f / fB);  // d fin / d p1 * d loss / d fin per unit (fin - y)
+      if (!beta) {
+        const float m2 = fmaxf(p0, p1);
+        const float q0e = expf(p0 - m2), q1e = expf(p1 - m2);
+        const float q0 = q0e / (q0e + q1e), q1 = q1e / (q0e + q1e);
+        dp0 = 0.4f * (q0 - (y == 0 ? 1.f : 0.f)) / fB;
+        dp1 = 0.4f * (q1 - (y == 1 ? 1.f : 0.f)) / fB + k * (0.4f * p1 - yf);
+      } else {
+        dp0 = 0.f;
+        dp1 = k * 0.6f;
+      }
+      const float dot = p0 * dp0 + p1 * dp1;
+      d0 = p0 * (dp0 - dot);
+      d1 = p1 * (dp1 - dot);
+    }
+    // stacked row index: A rows 0 .. B-1, beta rows B .. 2B-1 (then zero rows)
+    const int r = tid < RB ? tid : B + (tid - RB);
+    if (tid < RB ? tid < B : tid - RB < B) {
+      dl[r][0] = d0;
+      dl[r][1] = d1;
+      a.dl2[r * 2] = d0;
+      a.dl2[r * 2 + 1] = d1;
+    }
+  }
+  if (tid >= R2 && tid < 2 * R2) {  // zero rows 2B .. R2-1
+    const int r = tid - R2;
+    if (r >= 2 * B) dl[r][0] = dl[r][1] = 0.f;
+  }
+  __syncthreads();
+  dir_layer_bwd<R2, 64, 2>(a.W4, dl, a3, 1.f, dd3, a.d3, B, red);
+  dir_layer_bwd<R2, 128, 64>(a.W3, dd3, a2, 1.f, dd2, a.d2, B, red);
+  dir_layer_bwd<R2, 256, 128>(a.W2, dd2, in1, a.gs1, nullptr, a.d1, B, red);
+}
+
+int dir_mid(const DirMidArgs& a, hipStream_t st) {
+  // (16 stacked rows: the slice-combine buffer of the layer-2 input gradient, 4 x 16 x 256 floats, fills 64 KB of LDS)
+  VAD_CHECK(a.B >= 1 && a.B <= 8, "dir_mid: 1 <= B <= 8");
+  hipLaunchKernelGGL(dir_mid_kernel<8>, dim3(1), dim3(1024), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void dir_combine_kernel(const DirCombineArgs a) {
+  int s = 0, q = blockIdx.x * 256 + threadIdx.x;
+  for (; s < a.nseg; ++s) {
+    const int n = a.B * a.width[s];
+    if (q < n) break;
+    q -= n;
+  }
+  if (s >= a.nseg) return;
+  const int w = a.width[s], b = q / w, k = q % w;
+  a.dst[s][q] = fmaf(a.c[b], a.src[s][(int64_t)(a.B + b) * w + k], a.src[s][q]);
+}
+
+int dir_combine(const DirCombineArgs& a, hipStream_t st) {
+  VAD_CHECK(a.nseg >= 1 && a.nseg <= 6, "dir_combine: segments");
+  int64_t n = 0;
+  for (int s = 0; s < a.nseg; ++s) n += (int64_t)a.B * a.width[s];
+  hipLaunchKernelGGL(dir_combine_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
 static int mlp_rb(int M) { return M >= 64 ? 4 : 8; }
 
 int g_mlp_tail_wide = 0;  // knob "mlp_tail_wide": 1024-thread blocks for the detector's layers 1-4 (4-row blocks;

@@ -299,6 +299,19 @@ class CadEngine:
             out[lab] = (tot[i], cnt[i])
         return out
 
+    def profile_marks(self, shape=None) -> list:
+        """[(label, start_ms, end_ms)] of every recorded launch in record order, relative to the first record's start
+        (synchronises the stream)."""
+        pl = self.plans[shape] if shape is not None else self._last[0]
+        cap = 4096
+        labels = ctypes.create_string_buffer(64 * cap)
+        t0 = (ctypes.c_double * cap)()
+        t1 = (ctypes.c_double * cap)()
+        n = nat.lib().vad_cad_profile_marks(pl.h, labels, t0, t1, cap)
+        if n < 0:
+            nat.check(1)
+        return [(labels.raw[64 * i:64 * (i + 1)].split(b"\0", 1)[0].decode(), t0[i], t1[i]) for i in range(min(n, cap))]
+
     def optimizer_step(self, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, max_norm=1.0, grad_scale=1.0,
                        total_norm=None):
         self.init_optimizer_state()

@@ -303,6 +303,8 @@ int vad_debug_d2h(void* host, const void* dev, int64_t bytes);
  * dispatched with their own start/stop events (hipExtLaunchKernel) instead of event records around the launch. */
 int vad_cad_profile(vad_cad_plan* plan, int enable, const char* only_prefix);
 int vad_cad_profile_read(vad_cad_plan* plan, char* labels, double* total_ms, int* counts, int cap);
+/* per-record label / start / end (ms after the first record), record order (bench.py: the post-backbone chain) */
+int vad_cad_profile_marks(vad_cad_plan* plan, char* labels, double* t0_ms, double* t1_ms, int cap);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,6 @@ for v in "AB":
     runs = []
     for f in sorted(glob.glob(f"gpurun_out/{tag}_{v}_*.log")):
         d = json.loads(open(f).read().strip().split("\n")[-1])
-        runs.append({"value": d["value"], "ms_per_step": d["ms_per_step"]})
+        runs.append({"value": d["value"], "ms_per_step": d["ms_per_step"], "post_backbone_us": d.get("post_backbone_us")})
     out[v] = {"runs": runs, "median_ms": statistics.median(r["ms_per_step"] for r in runs)}
 print(json.dumps(out, indent=1))
