@@ -653,53 +653,62 @@ int maxpool3s2_bnrelu(const float* y, const float* stats, int NF, int H, int W, 
 __device__ inline int ap_start(int i, int in, int out) { return (i * in) / out; }
 __device__ inline int ap_end(int i, int in, int out) { return ((i + 1) * in + out - 1) / out; }
 
+// AdaptiveAvgPool2d((4, 6)) of relu(bn(y)) and its mean over the clip (cad:560-568) in one pass: thread (clip b, bin
+// (i, j), channel c) walks the bin's pixels of the T images in (t, row, column) order -- loads in chunks of 16 from
+// clamped addresses, so a chunk costs one memory round trip -- and writes each image's bin mean and the clip mean
+// (same summation order as a per-image pass followed by a mean over T)
 template <bool AB>
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const act_t<AB>* __restrict__ y,
-                                                          const float* __restrict__ stats, int H, int W, int C,
-                                                          float* __restrict__ feats) {
-  const int img = blockIdx.y;
+                                                          const float* __restrict__ stats, int T, int H, int W, int C,
+                                                          float* __restrict__ feats, float* __restrict__ pooled) {
+  const int b = blockIdx.y, i = blockIdx.z / 6, j = blockIdx.z % 6;
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   const float sc = stats[2 * C + c], sh = stats[3 * C + c];
-  const act_t<AB>* yi = y + (int64_t)img * H * W * C;
-  {  // one output row i per blockIdx.z: 4x the blocks of a per-image grid, a quarter of the serial sums
-    const int i = blockIdx.z;
-    const int h0 = ap_start(i, H, 4), h1 = ap_end(i, H, 4);
+  const int h0 = ap_start(i, H, 4), h1 = ap_end(i, H, 4), w0 = ap_start(j, W, 6), w1 = ap_end(j, W, 6);
+  const int wn = w1 - w0, n = (h1 - h0) * wn, total = T * n;
+  const float fn = (float)n;
+  const act_t<AB>* yb = y + (int64_t)b * T * H * W * C + c;
+  float cur = 0.f, pool = 0.f;
+  int curt = 0;
+  for (int base = 0; base < total; base += 16) {
+    float v[16];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int w0 = ap_start(j, W, 6), w1 = ap_end(j, W, 6);
-      float s = 0.f;
-      for (int hh = h0; hh < h1; ++hh)
-        for (int ww = w0; ww < w1; ++ww) s += fmaxf(fmaf(act_ld(yi + ((int64_t)hh * W + ww) * C + c), sc, sh), 0.f);
-      feats[(int64_t)img * C * 24 + c * 24 + i * 6 + j] = s / (float)((h1 - h0) * (w1 - w0));
+    for (int k = 0; k < 16; ++k) {
+      const int q = min(base + k, total - 1), t = q / n, p = q - t * n;
+      const int hh = h0 + p / wn, ww = w0 + p % wn;
+      v[k] = act_ld(yb + (((int64_t)t * H + hh) * W + ww) * C);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int q = base + k;
+      if (q < total) {
+        const int t = q / n;
+        if (t != curt) {
+          const float f = cur / fn;
+          feats[((int64_t)b * T + curt) * C * 24 + c * 24 + i * 6 + j] = f;
+          pool += f;
+          curt = t;
+          cur = 0.f;
+        }
+        cur += fmaxf(fmaf(v[k], sc, sh), 0.f);
+      }
     }
   }
-}
-
-// features.mean(dim=1) (cad:568)
-__global__ __launch_bounds__(256) void temporal_mean_kernel(const float* __restrict__ feats, int B, int T, int D,
-                                                            float* __restrict__ pooled) {
-  const int64_t total = (int64_t)B * D;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t b = i / D, d = i - b * D;
-    float s = 0.f;
-    for (int t = 0; t < T; ++t) s += feats[(b * T + t) * D + d];
-    pooled[i] = s / (float)T;
-  }
+  const float f = cur / fn;
+  feats[((int64_t)b * T + curt) * C * 24 + c * 24 + i * 6 + j] = f;
+  pool += f;
+  pooled[(int64_t)b * C * 24 + c * 24 + i * 6 + j] = pool / (float)T;
 }
 
 int avgpool_fwd(const float* y, const float* stats, int B, int T, int H, int W, int C, float* feats, float* pooled,
                 hipStream_t st) {
+  const dim3 grid((unsigned)cdiv(C, 256), B, 24);
   if (g_act_bf16)
-    hipLaunchKernelGGL(avgpool_fwd_kernel<true>, dim3((unsigned)cdiv(C, 256), B * T, 4), dim3(256), 0, st,
-                       reinterpret_cast<const __bf16*>(y), stats, H, W, C, feats);
+    VAD_KLAUNCH(avgpool_fwd_kernel<true>, grid, dim3(256), 0, st, reinterpret_cast<const __bf16*>(y), stats, T, H, W,
+                C, feats, pooled);
   else
-    hipLaunchKernelGGL(avgpool_fwd_kernel<false>, dim3((unsigned)cdiv(C, 256), B * T, 4), dim3(256), 0, st, y, stats,
-                       H, W, C, feats);
-  VAD_LAUNCH_CHECK();
-  const int64_t total = (int64_t)B * C * 24;
-  hipLaunchKernelGGL(temporal_mean_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 1024)), dim3(256), 0,
-                     st, feats, B, T, C * 24, pooled);
+    VAD_KLAUNCH(avgpool_fwd_kernel<false>, grid, dim3(256), 0, st, y, stats, T, H, W, C, feats, pooled);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -1392,28 +1401,30 @@ __global__ __launch_bounds__(512) void skinny_fwd_kernel(const float* __restrict
   for (int c = 0; c < 4; ++c)
 #pragma unroll
     for (int m = 0; m < MR; ++m) acc[c][m] = 0.f;
+  // (all loads unconditional from clamped addresses, out-of-range terms zeroed afterwards: a predicated load makes the
+  // compiler wait for the previous one, i.e. one memory round trip per load)
   for (int kb = 0; kb < K4; kb += NT * U) {
     f32x4 w[U][4];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int k4 = kb + u * NT + tid;
+      const int k4 = min(kb + u * NT + tid, K4 - 1);
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        w[u][c] = (k4 < K4 && n0 + c < N) ? *reinterpret_cast<const f32x4*>(W + (int64_t)(n0 + c) * K + 4 * k4)
-                                          : f32x4{0.f, 0.f, 0.f, 0.f};
+        w[u][c] = *reinterpret_cast<const f32x4*>(W + (int64_t)min(n0 + c, N - 1) * K + 4 * k4);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k4 = kb + u * NT + tid;
       if (k4 >= K4) break;
+      f32x4 xv[MR];
+#pragma unroll
+      for (int m = 0; m < MR; ++m) xv[m] = *reinterpret_cast<const f32x4*>(X + (int64_t)min(m, M - 1) * K + 4 * k4);
 #pragma unroll
       for (int m = 0; m < MR; ++m) {
-        if (m < M) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(X + (int64_t)m * K + 4 * k4);
+        const f32x4 x = m < M ? xv[m] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            acc[c][m] = fmaf(x[3], w[u][c][3], fmaf(x[2], w[u][c][2], fmaf(x[1], w[u][c][1], fmaf(x[0], w[u][c][0], acc[c][m]))));
-        }
+        for (int c = 0; c < 4; ++c)
+          acc[c][m] = fmaf(x[3], w[u][c][3], fmaf(x[2], w[u][c][2], fmaf(x[1], w[u][c][1], fmaf(x[0], w[u][c][0], acc[c][m]))));
       }
     }
   }
@@ -1444,9 +1455,18 @@ __global__ __launch_bounds__(1024) void skinny_dgrad_kernel(const float* __restr
   float* dys = dsm;
   float* red = dsm + (int64_t)N * MR;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < N * MR; i += 64 * NW) {
-    const int n = i / MR, m = i % MR;
-    dys[i] = m < M ? dY[(int64_t)m * N + n] : 0.f;
+  for (int i0 = 0; i0 < N * MR; i0 += 4 * 64 * NW) {  // 4 clamped loads in flight per thread, zeroed after
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = min(i0 + u * 64 * NW + tid, N * MR - 1), n = i / MR, m = i % MR;
+      v[u] = dY[(int64_t)min(m, M - 1) * N + n];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * 64 * NW + tid;
+      if (i < N * MR) dys[i] = i % MR < M ? v[u] : 0.f;
+    }
   }
   __syncthreads();
   const int k = blockIdx.x * 64 + lane;
@@ -1458,7 +1478,7 @@ __global__ __launch_bounds__(1024) void skinny_dgrad_kernel(const float* __restr
     for (int n0 = nb; n0 < ne; n0 += U) {
       float w[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) w[u] = n0 + u < ne ? W[(int64_t)(n0 + u) * K + k] : 0.f;
+      for (int u = 0; u < U; ++u) w[u] = W[(int64_t)min(n0 + u, ne - 1) * K + k];  // (clamped: see skinny_fwd)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (n0 + u >= ne) break;

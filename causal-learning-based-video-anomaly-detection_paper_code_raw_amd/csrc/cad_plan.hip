@@ -740,61 +740,63 @@ struct CadPlanImpl {
     const int64_t f0 = clip0 * T;
     const int dd[6] = {6144, 512, 256, 128, 64, 20};
     const int gd[6] = {6144, 512, 256, 128, 64, 2};
-    // (launch order: the side stream's first long kernels are queued before the direct classifier's short chain so
-    // the host's launch latency overlaps GPU work on both streams)
+    // The detector + causal head chain (the longer one, which the loss tail waits for) stays on the caller's stream,
+    // the direct classifier and the buffer clears go to the side stream: a cross-stream hand-off costs ~8 us from the
+    // producer's end to the consumer's start (tools/exp/xstream_probe.hip), a same-stream one ~1 us, so only the
+    // shorter chain pays the fork and the join finds it finished
     VAD_TRY(fork(st));
-    {  // side stream: detector_net (cad:167-179; layer 0 as a split-K GEMM, layers 1-4 fused per row block)
-      hipStream_t st = st2;
-      TIMED("det_fwd", dense_fwd(feats, NF, 6144, P(LY.det_w[0]), P(LY.det_b[0]), 512, dh[0],
-                                 act(true, S_DET_DROP1, 0.3, f0), dense_scratch2, dense_scratch_floats, st));
-      TIMED("det_fwd", mlp_tail_fwd(mlp_args(NF, f0, dd, LY.det_w, LY.det_b, dh, dlog, S_DET_DROP2, wt), st));
-    }
-    // direct_classifier on the mean over T (cad:525-538, 568-570)
-    // (B rows only: one block per 64 columns, so the chain runs layer by layer on many CUs; layers 1-4 unsplit)
-    // With labels (and B <= 8) layers 2-4 run in dir_mid together with the loss-mode input-gradient chain of the
-    // stacked rows [A; beta], layers 1 and 0 of that chain follow: the backward then only folds in the causal score
     dir_pre = tail_pre = 0;
     const bool affine = labels != nullptr && g_cad_dir_affine != 0 && B <= 8;
-    const float* in = pooled;
-    for (int i = 0; i < (affine ? 2 : 5); ++i) {
-      float* out = i < 4 ? gh[i] : glog;
-      const int sid = i == 0 ? S_DIRECT_DROP1 : (i == 1 ? S_DIRECT_DROP2 : 0);
-      TIMED("dir_fwd", dense_fwd(in, B, gd[i], P(LY.dir_w[i]), P(LY.dir_b[i]), gd[i + 1], out,
-                                 act(i < 4, sid, i == 0 ? 0.3 : 0.2, clip0), dense_scratch, dense_scratch_floats, st,
-                                 i == 0 ? 0 : 1));
-      in = out;
-    }
-    if (affine) {
-      const float gs0 = training ? (float)(1.0 / (1.0 - 0.3)) : 1.f, gs1 = training ? (float)(1.0 / (1.0 - 0.2)) : 1.f;
-      DirMidArgs da{};
-      da.B = B;
-      da.h1 = gh[1];
-      da.W2 = P(LY.dir_w[2]); da.b2 = P(LY.dir_b[2]);
-      da.W3 = P(LY.dir_w[3]); da.b3 = P(LY.dir_b[3]);
-      da.W4 = P(LY.dir_w[4]); da.b4 = P(LY.dir_b[4]);
-      da.h2 = gh[2]; da.h3 = gh[3]; da.logits = glog;
-      da.labels = labels;
-      da.gs1 = gs1;
-      da.dl2 = dl2; da.d3 = dg2[3]; da.d2 = dg2[2]; da.d1 = dg2[1];
-      TIMED("dir_fwd", dir_mid(da, st));
-      TIMED("dir_pre", dense_dgrad(dg2[1], 2 * B, 256, P(LY.dir_w[1]), 512, dg2[0], gh[0], gs0, nullptr, st, B));
-      TIMED("dir_pre", dense_dgrad(dg2[0], 2 * B, 512, P(LY.dir_w[0]), 6144, dpool2, nullptr, 1.f, nullptr, st));
-      dir_pre = tail_pre = 1;
-    }
-    // the detector's input gradient buffer is zero unless its backward writes it (the backward skips it on device when
-    // no box was in range); cleared here, where the main stream has slack
-    VAD_HIP(hipMemsetAsync(d_feat_det, 0, sizeof(float) * (size_t)NF * 6144, st));
-    // (train mode: the backward's grad buffer is cleared here too, off its critical path; the backward clears it
-    // itself when the forward did not)
-    grads_zeroed = 0;
-    if (training && grads) {
-      VAD_HIP(hipMemsetAsync(grads, 0, sizeof(float) * layout().param_floats, st));
-      grads_zeroed = 1;
-    }
-    {  // side stream: the causal head on the detections
+    {  // side stream: direct_classifier on the mean over T (cad:525-538, 568-570)
+      // (B rows only: one block per 64 columns, so the chain runs layer by layer on many CUs; layers 1-4 unsplit)
+      // With labels (and B <= 8) layers 2-4 run in dir_mid together with the loss-mode input-gradient chain of the
+      // stacked rows [A; beta], layers 1 and 0 of that chain follow: the backward then only folds in the causal score
       hipStream_t st = st2;
-      TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
+      const float* in = pooled;
+      for (int i = 0; i < (affine ? 2 : 5); ++i) {
+        float* out = i < 4 ? gh[i] : glog;
+        const int sid = i == 0 ? S_DIRECT_DROP1 : (i == 1 ? S_DIRECT_DROP2 : 0);
+        TIMED("dir_fwd", dense_fwd(in, B, gd[i], P(LY.dir_w[i]), P(LY.dir_b[i]), gd[i + 1], out,
+                                   act(i < 4, sid, i == 0 ? 0.3 : 0.2, clip0), dense_scratch, dense_scratch_floats, st,
+                                   i == 0 ? 0 : 1));
+        in = out;
+      }
+      if (affine) {
+        const float gs0 = training ? (float)(1.0 / (1.0 - 0.3)) : 1.f;
+        const float gs1 = training ? (float)(1.0 / (1.0 - 0.2)) : 1.f;
+        DirMidArgs da{};
+        da.B = B;
+        da.h1 = gh[1];
+        da.W2 = P(LY.dir_w[2]); da.b2 = P(LY.dir_b[2]);
+        da.W3 = P(LY.dir_w[3]); da.b3 = P(LY.dir_b[3]);
+        da.W4 = P(LY.dir_w[4]); da.b4 = P(LY.dir_b[4]);
+        da.h2 = gh[2]; da.h3 = gh[3]; da.logits = glog;
+        da.labels = labels;
+        da.gs1 = gs1;
+        da.dl2 = dl2; da.d3 = dg2[3]; da.d2 = dg2[2]; da.d1 = dg2[1];
+        da.dbg = g_head_dbg;
+        TIMED("dir_fwd", dir_mid(da, st));
+        TIMED("dir_pre", dense_dgrad(dg2[1], 2 * B, 256, P(LY.dir_w[1]), 512, dg2[0], gh[0], gs0, nullptr, st, B));
+        TIMED("dir_pre", dense_dgrad(dg2[0], 2 * B, 512, P(LY.dir_w[0]), 6144, dpool2, nullptr, 1.f, nullptr, st));
+        dir_pre = tail_pre = 1;
+      }
+      // the detector's input gradient buffer is zero unless its backward writes it (the backward skips it on device
+      // when no box was in range)
+      VAD_HIP(hipMemsetAsync(d_feat_det, 0, sizeof(float) * (size_t)NF * 6144, st));
+      // (train mode: the backward's grad buffer is cleared here too, off its critical path; the backward clears it
+      // itself when the forward did not)
+      grads_zeroed = 0;
+      if (training && grads) {
+        VAD_HIP(hipMemsetAsync(grads, 0, sizeof(float) * layout().param_floats, st));
+        grads_zeroed = 1;
+      }
     }
+    // caller's stream: detector_net (cad:167-179; layer 0 as a split-K GEMM, layers 1-4 fused per row block), then
+    // the causal head on the detections
+    TIMED("det_fwd", dense_fwd(feats, NF, 6144, P(LY.det_w[0]), P(LY.det_b[0]), 512, dh[0],
+                               act(true, S_DET_DROP1, 0.3, f0), dense_scratch2, dense_scratch_floats, st));
+    TIMED("det_fwd", mlp_tail_fwd(mlp_args(NF, f0, dd, LY.det_w, LY.det_b, dh, dlog, S_DET_DROP2, wt), st));
+    TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
     VAD_TRY(join(st));
     TailArgs t = tail_args(nullptr, nullptr, nullptr, nullptr);
     t.fwd_bwd = tail_pre;

@@ -59,6 +59,7 @@ struct DirMidArgs {
   const int64_t* labels;                             // [B]
   float gs1;                                         // gate scale of layer 1's output (1 / (1 - 0.2) in training)
   float *dl2, *d3, *d2, *d1;                         // [2B][2], [2B][64], [2B][128], [2B][256]
+  int dbg;                                           // knob head_dbg: print the phase cycle counts
 };
 int dir_mid(const DirMidArgs& a, hipStream_t st);
 // dst_s[b][k] = src_s[b][k] + c[b] src_s[B + b][k] for up to 6 segments (the stacked rows folded once c is known)

@@ -31,9 +31,18 @@ __global__ __launch_bounds__(NTH) void mlp_tail_fwd_kernel(const MlpTailArgs a) 
   const int r0 = blockIdx.x * RB;
   {
     const int N = a.L[0].N;
-    for (int idx = tid; idx < RB * N; idx += NTH) {
-      const int r = idx / N, n = idx % N, row = r0 + r;
-      buf[0][r][n] = row < a.M ? a.L[0].out[(int64_t)row * N + n] : 0.f;
+    // (loads from clamped addresses, zeroed after: predicated loads would be issued one round trip apart)
+    constexpr int PER = (RB * MLP_MAXW + NTH - 1) / NTH;
+    float v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = min(tid + u * NTH, RB * N - 1), r = idx / N, n = idx % N;
+      v[u] = a.L[0].out[(int64_t)min(r0 + r, a.M - 1) * N + n];
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = tid + u * NTH, r = idx / N, n = idx % N;
+      if (idx < RB * N) buf[0][r][n] = r0 + r < a.M ? v[u] : 0.f;
     }
   }
   __syncthreads();
@@ -231,18 +240,29 @@ int rows_wgrad(const RowsWgradArgs& a, hipStream_t st) {
 // Sum over the 64 lanes of R per-lane values at once (reduce-scatter over lane bits 0 .. log2 R - 1, then a butterfly
 // over the remaining bits): R - 1 + 6 - log2 R shuffles instead of 6 R.  Every lane returns the total of row
 // rs_row<R>(lane) (the bit reversal of its low log2 R lane bits).
+// dst = lane bit set in mask ? a : b, as one v_cndmask with a constant lane mask (written as inline asm: a plain select
+// between two elements of the unrolled array is rewritten by the compiler into a dynamically indexed vector extract,
+// i.e. a compare/select chain over the whole array)
+__device__ __forceinline__ float lane_sel(float a, float b, unsigned long long mask) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(mask));
+  return r;
+}
 template <int R>
 __device__ __forceinline__ float rs_sum(float (&v)[R], int lane) {
   constexpr int LG = R >= 32 ? 5 : R >= 16 ? 4 : R >= 8 ? 3 : R >= 4 ? 2 : R >= 2 ? 1 : 0;
   static_assert((1 << LG) == R, "power of two rows");
+  constexpr unsigned long long up_mask[6] = {0xAAAAAAAAAAAAAAAAull, 0xCCCCCCCCCCCCCCCCull, 0xF0F0F0F0F0F0F0F0ull,
+                                             0xFF00FF00FF00FF00ull, 0xFFFF0000FFFF0000ull, 0xFFFFFFFF00000000ull};
+  (void)lane;
 #pragma unroll
   for (int s = 0; s < LG; ++s) {
     const int half = R >> (s + 1);
-    const bool up = (lane >> s) & 1;
 #pragma unroll
     for (int i = 0; i < half; ++i) {
-      const float keep = up ? v[i + half] : v[i];
-      const float send = up ? v[i] : v[i + half];
+      // lanes with bit s set keep the upper half of the remaining rows and send the lower half
+      const float keep = lane_sel(v[i + half], v[i], up_mask[s]);
+      const float send = lane_sel(v[i], v[i + half], up_mask[s]);
       v[i] = keep + __shfl_xor(send, 1 << s, 64);
     }
   }
@@ -268,12 +288,11 @@ __device__ __forceinline__ void dir_layer_fwd(const float* __restrict__ W, const
   constexpr int NO = (O + 15) / 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool act = 4 * lane < I;
+  // (unconditional loads from clamped addresses: predicated loads would be issued one round trip apart)
   f32x4 w[NO];
 #pragma unroll
-  for (int q = 0; q < NO; ++q) {
-    const int o = wave + 16 * q;
-    w[q] = (act && o < O) ? *reinterpret_cast<const f32x4*>(W + (int64_t)o * I + 4 * lane) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int q = 0; q < NO; ++q)
+    w[q] = *reinterpret_cast<const f32x4*>(W + (int64_t)min(wave + 16 * q, O - 1) * I + 4 * (act ? lane : 0));
 #pragma unroll
   for (int q = 0; q < NO; ++q) {
     const int o = wave + 16 * q;
@@ -281,8 +300,8 @@ __device__ __forceinline__ void dir_layer_fwd(const float* __restrict__ W, const
     float v[RB];
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-      const f32x4 x = act ? *reinterpret_cast<const f32x4*>(&in[r][4 * lane]) : f32x4{0.f, 0.f, 0.f, 0.f};
-      v[r] = fmaf(w[q][3], x[3], fmaf(w[q][2], x[2], fmaf(w[q][1], x[1], w[q][0] * x[0])));
+      const f32x4 x = *reinterpret_cast<const f32x4*>(&in[r][act ? 4 * lane : 0]);
+      v[r] = act ? fmaf(w[q][3], x[3], fmaf(w[q][2], x[2], fmaf(w[q][1], x[1], w[q][0] * x[0]))) : 0.f;
     }
     const float s = rs_sum<RB>(v, lane);
     if (lane < RB) {
@@ -304,20 +323,19 @@ __device__ __forceinline__ void dir_layer_bwd(const float* __restrict__ W, const
                                               float* red) {
   constexpr int S = 1024 / I, OPS = (O + S - 1) / S;
   const int i = threadIdx.x % I, sl = threadIdx.x / I;
-  const int o0 = sl * OPS, o1 = min(O, o0 + OPS);
+  const int o0 = sl * OPS;
   float acc[R2];
 #pragma unroll
   for (int r = 0; r < R2; ++r) acc[r] = 0.f;
-  for (int ob = o0; ob < o1; ob += 8) {
-    float w[8];
+  // the slice's OPS weights in one batch of loads (clamped rows, see dir_layer_fwd)
+  float w[OPS];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) w[u] = ob + u < o1 ? W[(int64_t)(ob + u) * I + i] : 0.f;
+  for (int u = 0; u < OPS; ++u) w[u] = W[(int64_t)min(o0 + u, O - 1) * I + i];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (ob + u >= o1) break;
+  for (int u = 0; u < OPS; ++u) {
+    if (o0 + u >= O) break;
 #pragma unroll
-      for (int r = 0; r < R2; ++r) acc[r] = fmaf(w[u], dout[r][ob + u], acc[r]);
-    }
+    for (int r = 0; r < R2; ++r) acc[r] = fmaf(w[u], dout[r][o0 + u], acc[r]);
   }
 #pragma unroll
   for (int r = 0; r < R2; ++r) red[(sl * R2 + r) * I + i] = acc[r];
@@ -335,6 +353,7 @@ __device__ __forceinline__ void dir_layer_bwd(const float* __restrict__ W, const
 
 template <int RB>
 __global__ __launch_bounds__(1024) void dir_mid_kernel(const DirMidArgs a) {
+  static_assert(RB * 256 == 2 * 1024, "layer-1 rows staged as two loads per thread");
   constexpr int R2 = 2 * RB;
   __shared__ __attribute__((aligned(16))) float in1[RB][256];
   __shared__ __attribute__((aligned(16))) float a2[RB][128];
@@ -345,14 +364,28 @@ __global__ __launch_bounds__(1024) void dir_mid_kernel(const DirMidArgs a) {
   __shared__ __attribute__((aligned(16))) float dd2[R2][128];
   __shared__ __attribute__((aligned(16))) float red[4 * R2 * 256];
   const int B = a.B, tid = threadIdx.x;
-  for (int q = tid; q < RB * 256; q += 1024) in1[q / 256][q % 256] = q / 256 < B ? a.h1[q] : 0.f;
+  long long clk[8];
+  clk[0] = __builtin_readcyclecounter();
+  {
+    float v[2];  // RB * 256 = 2048 = 2 x 1024 (clamped loads, zeroed after)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) v[u] = a.h1[min(tid + u * 1024, B * 256 - 1)];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = tid + u * 1024;
+      in1[q / 256][q % 256] = q / 256 < B ? v[u] : 0.f;
+    }
+  }
   __syncthreads();
+  clk[1] = __builtin_readcyclecounter();
   dir_layer_fwd<RB, 256, 128, true>(a.W2, a.b2, in1, a2, a.h2, B);
   __syncthreads();
+  clk[2] = __builtin_readcyclecounter();
   dir_layer_fwd<RB, 128, 64, true>(a.W3, a.b3, a2, a3, a.h3, B);
   __syncthreads();
   dir_layer_fwd<RB, 64, 2, false>(a.W4, a.b4, a3, lg, a.logits, B);
   __syncthreads();
+  clk[3] = __builtin_readcyclecounter();
   // seed rows: softmax, cross entropy on the probabilities (cad:673) and the c-free / c-linear parts of the anomaly
   // MSE through fin (cad:674), then the softmax backward -- the per-row arithmetic of cad_tail_bwd_kernel
   if (tid < R2) {
@@ -397,9 +430,17 @@ __global__ __launch_bounds__(1024) void dir_mid_kernel(const DirMidArgs a) {
     if (r >= 2 * B) dl[r][0] = dl[r][1] = 0.f;
   }
   __syncthreads();
+  clk[4] = __builtin_readcyclecounter();
   dir_layer_bwd<R2, 64, 2>(a.W4, dl, a3, 1.f, dd3, a.d3, B, red);
+  clk[5] = __builtin_readcyclecounter();
   dir_layer_bwd<R2, 128, 64>(a.W3, dd3, a2, 1.f, dd2, a.d2, B, red);
+  clk[6] = __builtin_readcyclecounter();
   dir_layer_bwd<R2, 256, 128>(a.W2, dd2, in1, a.gs1, nullptr, a.d1, B, red);
+  clk[7] = __builtin_readcyclecounter();
+  if (a.dbg && tid == 0)
+    printf("dir_mid cycles: stage %lld, fwd2 %lld, fwd3+4 %lld, seed %lld, bwd4 %lld, bwd3 %lld, bwd2 %lld\n",
+           clk[1] - clk[0], clk[2] - clk[1], clk[3] - clk[2], clk[4] - clk[3], clk[5] - clk[4], clk[6] - clk[5],
+           clk[7] - clk[6]);
 }
 
 int dir_mid(const DirMidArgs& a, hipStream_t st) {
