@@ -1026,6 +1026,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "cad_dy_per_layer") g_cad_dy_per_layer = value;
   else if (k == "cad_event_sysfence") g_cad_event_sysfence = value;
   else if (k == "mlp_tail_wide") g_mlp_tail_wide = value;
+  else if (k == "mlp_tail_rb") g_mlp_tail_rb = value;
   else if (k == "cad_last_wgrad_main") g_cad_last_wgrad_main = value;
   else if (k == "head_dbg") g_head_dbg = value;
   else if (k == "stem_dbg") g_stem_dbg = value;
@@ -1442,15 +1443,15 @@ __global__ __launch_bounds__(512) void skinny_fwd_kernel(const float* __restrict
   if (part == 0 && m < M && n0 + c < N) P.out[(int64_t)m * P.ldc + n0 + c] = dense_finish(P, m, n0 + c, v);
 }
 
-// dX[m][k] = gate(sum_n dY[m][n] W[n][k]): a block owns 64 consecutive k (one per lane), its 16 waves split N (8 W
-// loads in flight per lane); dY is staged in LDS as [n][MR] (broadcast reads), the waves are combined in a fixed order
+// dX[m][k] = gate(sum_n dY[m][n] W[n][k]): a block owns 64 consecutive k (one per lane), its 16 waves split N (up to 32
+// W loads in flight per lane); dY is staged in LDS as [n][MR] (broadcast reads), the waves are combined in a fixed order
 // (wave q + wave q + 8, then the 8 pair sums in order: an 8-wave combine buffer, so 16 rows fit N <= 512 in 64 KB).
 template <int MR>
 __global__ __launch_bounds__(1024) void skinny_dgrad_kernel(const float* __restrict__ dY, int M, int N,
                                                             const float* __restrict__ W, int K, DenseEpiArgs P,
                                                             const int* skip) {
   if (skip && *skip == 0) return;
-  constexpr int NW = 16, U = 8;
+  constexpr int NW = 16, U = 32;  // (a wave's whole n range in one batch of loads when N <= 512)
   extern __shared__ __attribute__((aligned(16))) float dsm[];  // [N][MR] then [NW / 2][MR][64]
   float* dys = dsm;
   float* red = dsm + (int64_t)N * MR;

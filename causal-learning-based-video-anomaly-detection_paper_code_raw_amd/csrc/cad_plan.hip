@@ -581,6 +581,7 @@ struct CadPlanImpl {
       L.dscale = a.dscale;
       m.WT[i] = i >= 1 ? wtr[i] : nullptr;
     }
+    m.dbg = g_head_dbg;
     return m;
   }
   MlpTransposeArgs mlp_transpose_args() const {
@@ -766,17 +767,19 @@ struct CadPlanImpl {
         const float gs1 = training ? (float)(1.0 / (1.0 - 0.2)) : 1.f;
         DirMidArgs da{};
         da.B = B;
+        da.h0 = gh[0];
         da.h1 = gh[1];
+        da.W1 = P(LY.dir_w[1]);
         da.W2 = P(LY.dir_w[2]); da.b2 = P(LY.dir_b[2]);
         da.W3 = P(LY.dir_w[3]); da.b3 = P(LY.dir_b[3]);
         da.W4 = P(LY.dir_w[4]); da.b4 = P(LY.dir_b[4]);
         da.h2 = gh[2]; da.h3 = gh[3]; da.logits = glog;
         da.labels = labels;
+        da.gs0 = gs0;
         da.gs1 = gs1;
-        da.dl2 = dl2; da.d3 = dg2[3]; da.d2 = dg2[2]; da.d1 = dg2[1];
+        da.dl2 = dl2; da.d3 = dg2[3]; da.d2 = dg2[2]; da.d1 = dg2[1]; da.d0 = dg2[0];
         da.dbg = g_head_dbg;
         TIMED("dir_fwd", dir_mid(da, st));
-        TIMED("dir_pre", dense_dgrad(dg2[1], 2 * B, 256, P(LY.dir_w[1]), 512, dg2[0], gh[0], gs0, nullptr, st, B));
         TIMED("dir_pre", dense_dgrad(dg2[0], 2 * B, 512, P(LY.dir_w[0]), 6144, dpool2, nullptr, 1.f, nullptr, st));
         dir_pre = tail_pre = 1;
       }
@@ -793,9 +796,22 @@ struct CadPlanImpl {
     }
     // caller's stream: detector_net (cad:167-179; layer 0 as a split-K GEMM, layers 1-4 fused per row block), then
     // the causal head on the detections
-    TIMED("det_fwd", dense_fwd(feats, NF, 6144, P(LY.det_w[0]), P(LY.det_b[0]), 512, dh[0],
-                               act(true, S_DET_DROP1, 0.3, f0), dense_scratch2, dense_scratch_floats, st));
-    TIMED("det_fwd", mlp_tail_fwd(mlp_args(NF, f0, dd, LY.det_w, LY.det_b, dh, dlog, S_DET_DROP2, wt), st));
+    // (layer 0's split-K partials are summed and finished inside the layer 1-4 kernel: one launch less)
+    {
+      int ns = 0;
+      TIMED("det_fwd", dense_fwd_splitk(feats, NF, 6144, P(LY.det_w[0]), 512, dense_scratch2, dense_scratch_floats,
+                                        &ns, st));
+      MlpTailArgs m = mlp_args(NF, f0, dd, LY.det_w, LY.det_b, dh, dlog, S_DET_DROP2, wt);
+      const DenseAct a0 = act(true, S_DET_DROP1, 0.3, f0);
+      m.L[0].relu = a0.relu;
+      m.L[0].drop = a0.drop;
+      m.L[0].h1 = a0.h1;
+      m.L[0].thr = a0.thr;
+      m.L[0].dscale = a0.dscale;
+      m.parts = dense_scratch2;
+      m.nsplit = ns;
+      TIMED("det_fwd", mlp_tail_fwd(m, st));
+    }
     TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
     VAD_TRY(join(st));
     TailArgs t = tail_args(nullptr, nullptr, nullptr, nullptr);

@@ -235,7 +235,12 @@ __device__ void stage_head_weights(const HeadArgs& a, float* sW) {
 }
 
 // ================================================================== forward
+// One block per frame.  Every weight row a thread needs is loaded into its registers at the start, in one batch
+// beside the box decode: threads 0-191 own the GRU input-projection row q = tid (17 float4), threads 192-255 the ReID
+// rows u = tid - 192 (W0 row u < 32, W2 row u, W4 row u).  The dot products keep the reference order (bias first,
+// then the inputs in order), so the rows are bitwise those of a per-output loop.
 __global__ __launch_bounds__(256) void head_rows_fwd_kernel(HeadArgs a, const float* __restrict__ logits, HeadOut o) {
+  static_assert(G3 == 192 && GIN == 68 && NMAX * 4 <= 64, "thread roles: 192 projection rows + 64 ReID rows");
   const int f = blockIdx.x;  // frame b*T + t
   const int b = f / a.T, t = f - b * a.T;
   const int tid = threadIdx.x;
@@ -244,10 +249,27 @@ __global__ __launch_bounds__(256) void head_rows_fwd_kernel(HeadArgs a, const fl
   int* iw = a.iws + (int64_t)b * a.iws_stride;
   __shared__ float sbox[NMAX][4];
   __shared__ int svalid[NMAX];
-  __shared__ float sx[NMAX][GIN];
-  __shared__ float sh1[NMAX][32];
-  __shared__ float sh2[NMAX][64];
+  __shared__ __attribute__((aligned(16))) float sx[NMAX][GIN];
+  __shared__ __attribute__((aligned(16))) float sh1[NMAX][32];
+  __shared__ __attribute__((aligned(16))) float sh2[NMAX][64];
   __shared__ int scnt;
+  const bool proj = tid < G3;
+  const int u = proj ? 0 : tid - G3;  // ReID output of threads 192-255
+  // weight rows (unconditional loads from valid rows: see block_copy4)
+  f32x4 wr[GIN / 4];  // projection row q = tid, or W4 row u (16 float4) + W2 row u (8 float4, in wr[16] / w2)
+  f32x4 w2[8];
+  f32x4 w0 = *reinterpret_cast<const f32x4*>(PW(H_REID0_W) + (u & 31) * 4);
+  if (proj) {
+#pragma unroll
+    for (int k = 0; k < GIN / 4; ++k) wr[k] = *reinterpret_cast<const f32x4*>(PW(H_GRU_WIH) + tid * GIN + 4 * k);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) wr[k] = *reinterpret_cast<const f32x4*>(PW(H_REID4_W) + u * 64 + 4 * k);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w2[k] = *reinterpret_cast<const f32x4*>(PW(H_REID2_W) + u * 32 + 4 * k);
+  }
+  const float bq = proj ? PW(H_GRU_BIH)[tid] : PW(H_REID4_B)[u];
+  const float b2 = PW(H_REID2_B)[u], b0 = PW(H_REID0_B)[u & 31];
   if (tid < NMAX) {
     const float* lg = logits + (int64_t)f * 20 + tid * 4;
     const float X = sigmoidf_(lg[0]) * 360.f, Y = sigmoidf_(lg[1]) * 240.f;
@@ -257,93 +279,106 @@ __global__ __launch_bounds__(256) void head_rows_fwd_kernel(HeadArgs a, const fl
                    Hh <= 150.f) ? 1 : 0;
   }
   __syncthreads();
-  if (tid == 0) {
-    int c = 0;
+  // compaction of the in-range boxes (order kept), fallback box when none (cad:225), zero rows after: box k lands at
+  // the number of valid boxes before it (no per-thread array with a runtime index: that would live in scratch)
+  __shared__ float cbox[NMAX][4];
+  if (tid < NMAX) {
+    int n = 0, pos = 0;
+    for (int k = 0; k < NMAX; ++k) {
+      n += svalid[k];
+      if (k < tid) pos += svalid[k];
+    }
     int* slot = iw + a.T + t * NMAX;
-    float cb[NMAX][4];
-    for (int k = 0; k < NMAX; ++k)
-      if (svalid[k]) {
-        for (int q = 0; q < 4; ++q) cb[c][q] = sbox[k][q];
-        slot[c++] = k;
-      }
-    if (c == 0) {
-      cb[0][0] = 180.f; cb[0][1] = 120.f; cb[0][2] = 30.f; cb[0][3] = 60.f;  // fallback (cad:225)
-      slot[0] = -1;
-      c = 1;
+    if (svalid[tid]) {
+      for (int q = 0; q < 4; ++q) cbox[pos][q] = sbox[tid][q];
+      slot[pos] = tid;
     }
-    for (int j = c; j < NMAX; ++j) {
-      for (int q = 0; q < 4; ++q) cb[j][q] = 0.f;
-      slot[j] = -2;
+    if (tid >= n) {
+      const bool fb = n == 0 && tid == 0;
+      cbox[tid][0] = fb ? 180.f : 0.f;
+      cbox[tid][1] = fb ? 120.f : 0.f;
+      cbox[tid][2] = fb ? 30.f : 0.f;
+      cbox[tid][3] = fb ? 60.f : 0.f;
+      slot[tid] = fb ? -1 : -2;
     }
-    for (int j = 0; j < NMAX; ++j)
-      for (int q = 0; q < 4; ++q) sbox[j][q] = cb[j][q];
-    iw[t] = c;
-    o.counts[f] = c;
-    scnt = c;
+    if (tid == 0) {
+      const int c = n > 0 ? n : 1;
+      iw[t] = c;
+      o.counts[f] = c;
+      scnt = c;
+    }
   }
   __syncthreads();
   const int cnt = scnt;
   const int64_t r0 = (int64_t)f * NMAX;
   if (tid < NMAX * 4) {
     const int j = tid / 4, q = tid % 4;
-    rows[RL.box + (r0 + j) * 4 + q] = sbox[j][q];
-    o.boxes[(int64_t)f * NMAX * 4 + tid] = sbox[j][q];
+    rows[RL.box + (r0 + j) * 4 + q] = cbox[j][q];
+    o.boxes[(int64_t)f * NMAX * 4 + tid] = cbox[j][q];
+    sx[j][q] = j < cnt ? cbox[j][q] : 0.f;
   }
   // ReID MLP 4 -> 32 -> 64 -> 64 on real rows (zeros elsewhere)
-  const float* W0 = PW(H_REID0_W);
-  const float* B0 = PW(H_REID0_B);
-  for (int idx = tid; idx < NMAX * 32; idx += 256) {
-    const int j = idx / 32, u = idx % 32;
-    float v = 0.f;
-    if (j < cnt) {
-      v = B0[u];
-      for (int q = 0; q < 4; ++q) v = fmaf(W0[u * 4 + q], sbox[j][q], v);
-      v = fmaxf(v, 0.f);
-    }
-    sh1[j][u] = v;
-    rows[RL.rh1 + (r0 + j) * 32 + u] = v;
-  }
-  __syncthreads();
-  const float* W2 = PW(H_REID2_W);
-  const float* B2 = PW(H_REID2_B);
-  for (int idx = tid; idx < NMAX * 64; idx += 256) {
-    const int j = idx / 64, u = idx % 64;
-    float v = 0.f;
-    if (j < cnt) {
-      v = B2[u];
-      for (int q = 0; q < 32; ++q) v = fmaf(W2[u * 32 + q], sh1[j][q], v);
-      v = fmaxf(v, 0.f);
-    }
-    sh2[j][u] = v;
-    rows[RL.rh2 + (r0 + j) * 64 + u] = v;
-  }
-  __syncthreads();
-  const float* W4 = PW(H_REID4_W);
-  const float* B4 = PW(H_REID4_B);
-  for (int idx = tid; idx < NMAX * GIN; idx += 256) {
-    const int j = idx / GIN, i = idx % GIN;
-    float v = 0.f;
-    if (j < cnt) {
-      if (i < 4) v = sbox[j][i];
-      else {
-        const int u = i - 4;
-        v = B4[u];
-        for (int q = 0; q < 64; ++q) v = fmaf(W4[u * 64 + q], sh2[j][q], v);
+  if (!proj && u < 32) {
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      float v = 0.f;
+      if (j < cnt) {
+        v = b0;
+        for (int q = 0; q < 4; ++q) v = fmaf(w0[q], cbox[j][q], v);
+        v = fmaxf(v, 0.f);
       }
+      sh1[j][u] = v;
+      rows[RL.rh1 + (r0 + j) * 32 + u] = v;
     }
-    sx[j][i] = v;
-    rows[RL.x + (r0 + j) * GIN + i] = v;
   }
   __syncthreads();
-  // GRU input projection for all 5 rows (padded rows see x = 0)
-  const float* Wih = PW(H_GRU_WIH);
-  const float* bih = PW(H_GRU_BIH);
-  for (int idx = tid; idx < NMAX * G3; idx += 256) {
-    const int j = idx / G3, q = idx % G3;
-    float v = bih[q];
-    const float* wr = Wih + (int64_t)q * GIN;
-    for (int i = 0; i < GIN; ++i) v = fmaf(wr[i], sx[j][i], v);
-    rows[RL.gi + (r0 + j) * G3 + q] = v;
+  if (!proj) {
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      float v = 0.f;
+      if (j < cnt) {
+        v = b2;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(&sh1[j][4 * k]);
+          for (int e = 0; e < 4; ++e) v = fmaf(w2[k][e], x[e], v);
+        }
+        v = fmaxf(v, 0.f);
+      }
+      sh2[j][u] = v;
+      rows[RL.rh2 + (r0 + j) * 64 + u] = v;
+    }
+  }
+  __syncthreads();
+  if (!proj) {
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      float v = 0.f;
+      if (j < cnt) {
+        v = bq;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(&sh2[j][4 * k]);
+          for (int e = 0; e < 4; ++e) v = fmaf(wr[k][e], x[e], v);
+        }
+      }
+      sx[j][4 + u] = v;
+    }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < NMAX * GIN; idx += 256) rows[RL.x + r0 * GIN + idx] = (&sx[0][0])[idx];
+  // GRU input projection W_ih x + b_ih for all 5 rows (padded rows see x = 0)
+  if (proj) {
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      float v = bq;
+#pragma unroll
+      for (int k = 0; k < GIN / 4; ++k) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(&sx[j][4 * k]);
+        for (int e = 0; e < 4; ++e) v = fmaf(wr[k][e], x[e], v);
+      }
+      rows[RL.gi + (r0 + j) * G3 + tid] = v;
+    }
   }
 }
 

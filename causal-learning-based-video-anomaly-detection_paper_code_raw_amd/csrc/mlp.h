@@ -23,6 +23,11 @@ struct MlpTailArgs {
   int64_t row0;        // global row of row 0 (dropout key)
   MlpLayer L[5];
   const float* WT[5];  // transposed weights WT[i][k][n] of layers 1-4
+  int dbg;             // knob head_dbg: block 0 prints its phase cycle counts
+  // optional: layer 0 as split-K partial sums parts[nsplit][M][L[0].N] (dense_fwd_splitk); the kernel then finishes
+  // layer 0 itself (fixed-order sum, bias, ReLU, dropout per L[0]) and writes L[0].out
+  const float* parts;
+  int nsplit;
 };
 
 struct MlpTransposeArgs {
@@ -46,19 +51,20 @@ struct MlpTailBwdArgs {
 };
 
 extern int g_mlp_tail_wide;  // knob "mlp_tail_wide"
+extern int g_mlp_tail_rb;    // knob "mlp_tail_rb"
 int mlp_tail_fwd(const MlpTailArgs& a, hipStream_t st);
 // Direct classifier (cad:525-538) with its loss-mode backward precomputed as an affine function of the causal score
 // c (cad:655-676): with fin = 0.6 c + 0.4 p1 the upstream gradient of the logits is d_l[b] = A[b] + c[b] beta[b], and
 // the classifier's input-gradient chain is linear in d_l, so it runs on the 2B stacked rows [A; beta] while the causal
-// head computes c (B <= 8).  dir_mid runs layers 2-4 forward, the seed rows and the layer 4-2 input gradients in one block.
+// head computes c (B <= 8).  dir_mid runs layers 2-4 forward, the seed rows and the layer 4-1 input gradients in one block.
 struct DirMidArgs {
   int B;
-  const float* h1;                                   // [B][256] (layer 1 output, after dropout)
-  const float *W2, *b2, *W3, *b3, *W4, *b4;          // [128][256], [64][128], [2][64]
+  const float *h0, *h1;                              // [B][512], [B][256] (layer 0 / 1 outputs, after dropout)
+  const float *W1, *W2, *b2, *W3, *b3, *W4, *b4;     // [256][512], [128][256], [64][128], [2][64]
   float *h2, *h3, *logits;                           // [B][128], [B][64], [B][2]
   const int64_t* labels;                             // [B]
-  float gs1;                                         // gate scale of layer 1's output (1 / (1 - 0.2) in training)
-  float *dl2, *d3, *d2, *d1;                         // [2B][2], [2B][64], [2B][128], [2B][256]
+  float gs0, gs1;                                    // gate scales of layer 0 / 1 outputs (1 / (1 - p) in training)
+  float *dl2, *d3, *d2, *d1, *d0;                    // [2B][2], [2B][64], [2B][128], [2B][256], [2B][512]
   int dbg;                                           // knob head_dbg: print the phase cycle counts
 };
 int dir_mid(const DirMidArgs& a, hipStream_t st);

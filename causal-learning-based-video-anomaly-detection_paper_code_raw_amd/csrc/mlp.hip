@@ -14,7 +14,7 @@ namespace vad {
 
 __device__ __forceinline__ float mlp_finish(const MlpLayer& L, int64_t grow, int col, float v) {
   v += L.b[col];
-  if (L.relu) v = fmaxf(v, 0.f);
+  if (L.relu) v = relu_nan(v);  // (NaN kept, as dense_finish)
   if (L.drop) v = (rng_u24(L.h1, (uint64_t)grow, (uint64_t)col) >= L.thr) ? v * L.dscale : 0.f;
   return v;
 }
@@ -29,15 +29,48 @@ __global__ __launch_bounds__(NTH) void mlp_tail_fwd_kernel(const MlpTailArgs a) 
   __shared__ __attribute__((aligned(16))) float red[NTH * 4 * RB];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * RB;
+  long long clk[6];
+  clk[0] = __builtin_readcyclecounter();
   {
     const int N = a.L[0].N;
     // (loads from clamped addresses, zeroed after: predicated loads would be issued one round trip apart)
     constexpr int PER = (RB * MLP_MAXW + NTH - 1) / NTH;
     float v[PER];
+    if (a.parts) {
+      // layer 0's split-K partials summed in split order (as dense_splitk_reduce_kernel), ZC splits per batch of loads
+      // (32 loads in flight per thread)
+      constexpr int ZC = PER >= 8 ? 4 : 32 / PER;
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int idx = min(tid + u * NTH, RB * N - 1), r = idx / N, n = idx % N;
-      v[u] = a.L[0].out[(int64_t)min(r0 + r, a.M - 1) * N + n];
+      for (int u = 0; u < PER; ++u) v[u] = 0.f;
+      for (int z0 = 0; z0 < a.nsplit; z0 += ZC) {
+        float pv[ZC][PER];
+#pragma unroll
+        for (int zz = 0; zz < ZC; ++zz)
+#pragma unroll
+          for (int u = 0; u < PER; ++u) {
+            const int idx = min(tid + u * NTH, RB * N - 1), r = idx / N, n = idx % N;
+            pv[zz][u] = a.parts[((int64_t)min(z0 + zz, a.nsplit - 1) * a.M + min(r0 + r, a.M - 1)) * N + n];
+          }
+#pragma unroll
+        for (int zz = 0; zz < ZC; ++zz)
+#pragma unroll
+          for (int u = 0; u < PER; ++u)
+            if (z0 + zz < a.nsplit) v[u] += pv[zz][u];
+      }
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int idx = tid + u * NTH, r = idx / N, n = idx % N;
+        if (idx < RB * N && r0 + r < a.M) {
+          v[u] = mlp_finish(a.L[0], a.row0 + r0 + r, n, v[u]);
+          a.L[0].out[(int64_t)(r0 + r) * N + n] = v[u];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int idx = min(tid + u * NTH, RB * N - 1), r = idx / N, n = idx % N;
+        v[u] = a.L[0].out[(int64_t)min(r0 + r, a.M - 1) * N + n];
+      }
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -46,13 +79,15 @@ __global__ __launch_bounds__(NTH) void mlp_tail_fwd_kernel(const MlpTailArgs a) 
     }
   }
   __syncthreads();
+  clk[1] = __builtin_readcyclecounter();
 #pragma unroll 1
   for (int i = 1; i < 5; ++i) {
     const MlpLayer& L = a.L[i];
     const float(*in)[MLP_MAXW] = buf[(i - 1) & 1];
     float(*outb)[MLP_MAXW] = buf[i & 1];
     const int K = L.K, N = L.N, NG = N / 4;
-    const int P = NTH / NG;
+    // K-slices of >= 8 inputs only (the combine below reads P partials per output: idle slices would cost reads)
+    const int P = min(NTH / NG, max(1, K / 8));
     const int kper = ((K + P - 1) / P + 7) & ~7;
     const float* WT = a.WT[i];
     if (tid < NG * P) {
@@ -92,7 +127,11 @@ __global__ __launch_bounds__(NTH) void mlp_tail_fwd_kernel(const MlpTailArgs a) 
       outb[r][n] = v;
     }
     __syncthreads();
+    clk[i + 1] = __builtin_readcyclecounter();
   }
+  if (a.dbg && blockIdx.x == 0 && tid == 0)
+    printf("mlp_tail_fwd cycles: stage %lld, L1 %lld, L2 %lld, L3 %lld, L4 %lld\n", clk[1] - clk[0], clk[2] - clk[1],
+           clk[3] - clk[2], clk[4] - clk[3], clk[5] - clk[4]);
 }
 
 // WT[k][n] = W[n][k] for up to 8 matrices (the detector's layer-1..4 weights), once per step: 32x32 tiles through
@@ -237,9 +276,6 @@ int rows_wgrad(const RowsWgradArgs& a, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------ direct classifier: affine loss-mode backward
-// Sum over the 64 lanes of R per-lane values at once (reduce-scatter over lane bits 0 .. log2 R - 1, then a butterfly
-// over the remaining bits): R - 1 + 6 - log2 R shuffles instead of 6 R.  Every lane returns the total of row
-// rs_row<R>(lane) (the bit reversal of its low log2 R lane bits).
 // dst = lane bit set in mask ? a : b, as one v_cndmask with a constant lane mask (written as inline asm: a plain select
 // between two elements of the unrolled array is rewritten by the compiler into a dynamically indexed vector extract,
 // i.e. a compare/select chain over the whole array)
@@ -248,19 +284,22 @@ __device__ __forceinline__ float lane_sel(float a, float b, unsigned long long m
   asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(mask));
   return r;
 }
-template <int R>
-__device__ __forceinline__ float rs_sum(float (&v)[R], int lane) {
-  constexpr int LG = R >= 32 ? 5 : R >= 16 ? 4 : R >= 8 ? 3 : R >= 4 ? 2 : R >= 2 ? 1 : 0;
-  static_assert((1 << LG) == R, "power of two rows");
+constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
+// Sums V per-lane values over each aligned group of 2^LGP lanes at once (V a power of two <= 2^LGP): a reduce-scatter
+// over lane bits 0 .. log2 V - 1 (the lane with bit s set keeps the upper half of the remaining values and sends the
+// lower half), then a butterfly over the remaining group bits -- V - 1 + LGP - log2 V shuffles for V sums.  Lane l
+// returns the group total of value rs_index<V>(l).
+template <int V, int LGP>
+__device__ __forceinline__ float group_rs(float (&v)[V]) {
+  constexpr int LV = ilog2(V);
+  static_assert((1 << LV) == V && LV <= LGP && LGP <= 6, "power-of-two values within the lane group");
   constexpr unsigned long long up_mask[6] = {0xAAAAAAAAAAAAAAAAull, 0xCCCCCCCCCCCCCCCCull, 0xF0F0F0F0F0F0F0F0ull,
                                              0xFF00FF00FF00FF00ull, 0xFFFF0000FFFF0000ull, 0xFFFFFFFF00000000ull};
-  (void)lane;
 #pragma unroll
-  for (int s = 0; s < LG; ++s) {
-    const int half = R >> (s + 1);
+  for (int s = 0; s < LV; ++s) {
+    const int half = V >> (s + 1);
 #pragma unroll
     for (int i = 0; i < half; ++i) {
-      // lanes with bit s set keep the upper half of the remaining rows and send the lower half
       const float keep = lane_sel(v[i + half], v[i], up_mask[s]);
       const float send = lane_sel(v[i], v[i + half], up_mask[s]);
       v[i] = keep + __shfl_xor(send, 1 << s, 64);
@@ -268,74 +307,114 @@ __device__ __forceinline__ float rs_sum(float (&v)[R], int lane) {
   }
   float x = v[0];
 #pragma unroll
-  for (int b = LG; b < 6; ++b) x += __shfl_xor(x, 1 << b, 64);
+  for (int b = LV; b < LGP; ++b) x += __shfl_xor(x, 1 << b, 64);
   return x;
 }
-template <int R>
-__device__ __forceinline__ int rs_row(int lane) {
+template <int V>
+__device__ __forceinline__ int rs_index(int l) {
   int r = 0;
 #pragma unroll
-  for (int s = 0; (R >> (s + 1)) >= 1; ++s) r |= ((lane >> s) & 1) * (R >> (s + 1));
+  for (int s = 0; (V >> (s + 1)) >= 1; ++s) r |= ((l >> s) & 1) * (V >> (s + 1));
   return r;
 }
 
-// out[r][o] = act(b[o] + sum_i W[o][i] in[r][i]) for RB rows (LDS in / out, rows >= B are zero): wave w takes the
-// outputs o = w (mod 16), lane l the inputs 4l .. 4l + 3 (coalesced row loads, all of a wave's rows issued first)
-template <int RB, int I, int O, bool RELU>
+// out[r][o] = act(b[o] + sum_i W[o][i] in[r][i]) for RB rows (LDS in / out, rows >= B zero).  Thread (output group g
+// of OG outputs, K-slice p of I / P inputs; p fastest, so a group's P lanes read consecutive chunks of the W rows):
+// RB x OG partial dots, summed over the group's lanes by group_rs (one value per lane, no LDS combine)
+template <int RB, int I, int O, int OG, int P, bool RELU>
 __device__ __forceinline__ void dir_layer_fwd(const float* __restrict__ W, const float* __restrict__ bias,
                                               const float (*in)[I], float (*out)[O], float* gout, int B) {
-  static_assert(I % 4 == 0 && I <= 256, "one float4 of the row per lane");
-  constexpr int NO = (O + 15) / 16;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool act = 4 * lane < I;
-  // (unconditional loads from clamped addresses: predicated loads would be issued one round trip apart)
-  f32x4 w[NO];
+  constexpr int KPER = I / P, NG = O / OG, V = RB * OG;
+  static_assert(KPER % 4 == 0 && KPER * P == I && NG * OG == O && NG * P <= 1024 && V <= P && 64 % P == 0,
+                "layer tiling");
+  const int p = threadIdx.x % P, g = threadIdx.x / P;
+  if (g >= NG) return;  // (whole lane groups)
+  f32x4 w[OG][KPER / 4];
 #pragma unroll
-  for (int q = 0; q < NO; ++q)
-    w[q] = *reinterpret_cast<const f32x4*>(W + (int64_t)min(wave + 16 * q, O - 1) * I + 4 * (act ? lane : 0));
+  for (int c = 0; c < OG; ++c)
 #pragma unroll
-  for (int q = 0; q < NO; ++q) {
-    const int o = wave + 16 * q;
-    if (o >= O) break;  // (wave-uniform)
-    float v[RB];
+    for (int kk = 0; kk < KPER / 4; ++kk)
+      w[c][kk] = *reinterpret_cast<const f32x4*>(W + (int64_t)(g * OG + c) * I + p * KPER + 4 * kk);
+  float v[V];
 #pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const f32x4 x = *reinterpret_cast<const f32x4*>(&in[r][act ? 4 * lane : 0]);
-      v[r] = act ? fmaf(w[q][3], x[3], fmaf(w[q][2], x[2], fmaf(w[q][1], x[1], w[q][0] * x[0]))) : 0.f;
+  for (int r = 0; r < RB; ++r) {
+#pragma unroll
+    for (int c = 0; c < OG; ++c) v[r * OG + c] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KPER / 4; ++kk) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(&in[r][p * KPER + 4 * kk]);
+#pragma unroll
+      for (int c = 0; c < OG; ++c)
+        v[r * OG + c] = fmaf(w[c][kk][3], x[3], fmaf(w[c][kk][2], x[2], fmaf(w[c][kk][1], x[1],
+                        fmaf(w[c][kk][0], x[0], v[r * OG + c]))));
     }
-    const float s = rs_sum<RB>(v, lane);
-    if (lane < RB) {
-      const int r = rs_row<RB>(lane);
-      float y = s + bias[o];
-      if (RELU) y = relu_nan(y);
-      if (r >= B) y = 0.f;
-      out[r][o] = y;
-      if (r < B) gout[(int64_t)r * O + o] = y;
-    }
+  }
+  const float sum = group_rs<V, ilog2(P)>(v);
+  if (p < V) {
+    const int idx = rs_index<V>(p), r = idx / OG, o = g * OG + idx % OG;
+    float y = sum + bias[o];
+    if (RELU) y = relu_nan(y);
+    if (r >= B) y = 0.f;
+    out[r][o] = y;
+    if (r < B && gout) gout[(int64_t)r * O + o] = y;
   }
 }
 
 // din[r][i] = (sum_o W[o][i] dout[r][o]) * (gate[r % B][i] > 0 ? gs : 0) for R2 stacked rows (rows >= 2B zero):
-// thread (i, slice) accumulates its slice of o (coalesced W row reads), the S slices are combined in a fixed order
-template <int R2, int I, int O>
+// thread (i, slice) accumulates its slice of o (coalesced W row reads, batches of up to 32 loads), the S slices are
+// combined in a fixed order through red
+// (LD > I: the block computes the columns [i0, i0 + I) of rows LD wide; W rows and gate rows are LD wide, din / gdin
+// are written at their full-width positions)
+template <int R2, int I, int O, int LD = I>
 __device__ __forceinline__ void dir_layer_bwd(const float* __restrict__ W, const float (*dout)[O],
-                                              const float (*gate)[I], float gs, float (*din)[I], float* gdin, int B,
-                                              float* red) {
-  constexpr int S = 1024 / I, OPS = (O + S - 1) / S;
+                                              const float (*gate)[LD], float gs, float (*din)[LD], float* gdin, int B,
+                                              float* red, int i0 = 0) {
+  constexpr int S = 1024 / I, OPS = (O + S - 1) / S, UB = OPS < 32 ? OPS : 32;
   const int i = threadIdx.x % I, sl = threadIdx.x / I;
+  W += i0;
   const int o0 = sl * OPS;
   float acc[R2];
+  if constexpr (OPS % 4 == 0 && S * OPS == O) {
+    // packed: even / odd o in the two halves of a v_pk_fma_f32, dout read as float4 (4 o per LDS broadcast)
+    f32x2 acc2[R2];
 #pragma unroll
-  for (int r = 0; r < R2; ++r) acc[r] = 0.f;
-  // the slice's OPS weights in one batch of loads (clamped rows, see dir_layer_fwd)
-  float w[OPS];
+    for (int r = 0; r < R2; ++r) acc2[r] = f32x2{0.f, 0.f};
 #pragma unroll
-  for (int u = 0; u < OPS; ++u) w[u] = W[(int64_t)min(o0 + u, O - 1) * I + i];
+    for (int ob = 0; ob < OPS; ob += UB) {
+      float w[UB];  // (unconditional loads, issued together)
 #pragma unroll
-  for (int u = 0; u < OPS; ++u) {
-    if (o0 + u >= O) break;
+      for (int u = 0; u < UB; ++u) w[u] = W[(int64_t)(o0 + ob + u) * LD + i];
+      // row by row: the row's UB / 4 float4 reads are issued together, then its 2 x UB / 4 packed FMAs (the u-outer
+      // order waited for each read before its two FMAs)
 #pragma unroll
-    for (int r = 0; r < R2; ++r) acc[r] = fmaf(w[u], dout[r][o0 + u], acc[r]);
+      for (int r = 0; r < R2; ++r) {
+        f32x4 d[UB / 4];
+#pragma unroll
+        for (int q = 0; q < UB / 4; ++q) d[q] = *reinterpret_cast<const f32x4*>(&dout[r][o0 + ob + 4 * q]);
+#pragma unroll
+        for (int q = 0; q < UB / 4; ++q) {
+          acc2[r] = __builtin_elementwise_fma(f32x2{w[4 * q], w[4 * q + 1]}, f32x2{d[q][0], d[q][1]}, acc2[r]);
+          acc2[r] = __builtin_elementwise_fma(f32x2{w[4 * q + 2], w[4 * q + 3]}, f32x2{d[q][2], d[q][3]}, acc2[r]);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R2; ++r) acc[r] = acc2[r][0] + acc2[r][1];
+  } else {
+#pragma unroll
+    for (int r = 0; r < R2; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int ob = 0; ob < OPS; ob += UB) {
+      float w[UB];  // (clamped rows: unconditional loads, issued together)
+#pragma unroll
+      for (int u = 0; u < UB; ++u) w[u] = W[(int64_t)min(o0 + ob + u, O - 1) * LD + i];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        if (o0 + ob + u >= O) break;
+#pragma unroll
+        for (int r = 0; r < R2; ++r) acc[r] = fmaf(w[u], dout[r][o0 + ob + u], acc[r]);
+      }
+    }
   }
 #pragma unroll
   for (int r = 0; r < R2; ++r) red[(sl * R2 + r) * I + i] = acc[r];
@@ -344,46 +423,59 @@ __device__ __forceinline__ void dir_layer_bwd(const float* __restrict__ W, const
     const int r = q / I, ii = q % I;
     float v = 0.f;
     for (int t = 0; t < S; ++t) v += red[(t * R2 + r) * I + ii];
-    v = (r < 2 * B && gate[r % B][ii] > 0.f) ? v * gs : 0.f;
-    if (din) din[r][ii] = v;
-    if (r < 2 * B) gdin[(int64_t)r * I + ii] = v;
+    v = (r < 2 * B && gate[r % B][i0 + ii] > 0.f) ? v * gs : 0.f;
+    if (din) din[r][i0 + ii] = v;
+    if (r < 2 * B && gdin) gdin[(int64_t)r * LD + i0 + ii] = v;
   }
   __syncthreads();
 }
 
 template <int RB>
 __global__ __launch_bounds__(1024) void dir_mid_kernel(const DirMidArgs a) {
-  static_assert(RB * 256 == 2 * 1024, "layer-1 rows staged as two loads per thread");
+  static_assert(RB * 256 == 2 * 1024, "layer-1 / layer-0 rows staged as two / four loads per thread");
   constexpr int R2 = 2 * RB;
+  __shared__ __attribute__((aligned(16))) float in0[RB][512];  // layer 0 output: the layer-1 input gradient's gate
   __shared__ __attribute__((aligned(16))) float in1[RB][256];
+  __shared__ __attribute__((aligned(16))) float dd1[R2][256];
   __shared__ __attribute__((aligned(16))) float a2[RB][128];
   __shared__ __attribute__((aligned(16))) float a3[RB][64];
   __shared__ __attribute__((aligned(16))) float lg[RB][2];
   __shared__ __attribute__((aligned(16))) float dl[R2][2];
   __shared__ __attribute__((aligned(16))) float dd3[R2][64];
   __shared__ __attribute__((aligned(16))) float dd2[R2][128];
-  __shared__ __attribute__((aligned(16))) float red[4 * R2 * 256];
+  __shared__ __attribute__((aligned(16))) float red[4 * R2 * 256];  // (= 2 x R2 x 512: the layer-1 combine too)
   const int B = a.B, tid = threadIdx.x;
+  // every block runs layers 2-4, the seed and the layer 4-2 input gradients (cheap, redundant); block k then takes the
+  // layer-1 input-gradient columns [64k, 64k + 64).  Block 0 alone writes the shared outputs.
+  const bool w0 = blockIdx.x == 0;
   long long clk[8];
   clk[0] = __builtin_readcyclecounter();
   {
     float v[2];  // RB * 256 = 2048 = 2 x 1024 (clamped loads, zeroed after)
 #pragma unroll
     for (int u = 0; u < 2; ++u) v[u] = a.h1[min(tid + u * 1024, B * 256 - 1)];
+    float v0[4];  // RB * 512 = 4 x 1024
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v0[u] = a.h0[min(tid + u * 1024, B * 512 - 1)];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int q = tid + u * 1024;
       in1[q / 256][q % 256] = q / 256 < B ? v[u] : 0.f;
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = tid + u * 1024;
+      in0[q / 512][q % 512] = q / 512 < B ? v0[u] : 0.f;
+    }
   }
   __syncthreads();
   clk[1] = __builtin_readcyclecounter();
-  dir_layer_fwd<RB, 256, 128, true>(a.W2, a.b2, in1, a2, a.h2, B);
+  dir_layer_fwd<RB, 256, 128, 4, 32, true>(a.W2, a.b2, in1, a2, w0 ? a.h2 : nullptr, B);
   __syncthreads();
   clk[2] = __builtin_readcyclecounter();
-  dir_layer_fwd<RB, 128, 64, true>(a.W3, a.b3, a2, a3, a.h3, B);
+  dir_layer_fwd<RB, 128, 64, 2, 32, true>(a.W3, a.b3, a2, a3, w0 ? a.h3 : nullptr, B);
   __syncthreads();
-  dir_layer_fwd<RB, 64, 2, false>(a.W4, a.b4, a3, lg, a.logits, B);
+  dir_layer_fwd<RB, 64, 2, 2, 16, false>(a.W4, a.b4, a3, lg, w0 ? a.logits : nullptr, B);
   __syncthreads();
   clk[3] = __builtin_readcyclecounter();
   // seed rows: softmax, cross entropy on the probabilities (cad:673) and the c-free / c-linear parts of the anomaly
@@ -421,8 +513,10 @@ __global__ __launch_bounds__(1024) void dir_mid_kernel(const DirMidArgs a) {
     if (tid < RB ? tid < B : tid - RB < B) {
       dl[r][0] = d0;
       dl[r][1] = d1;
-      a.dl2[r * 2] = d0;
-      a.dl2[r * 2 + 1] = d1;
+      if (w0) {
+        a.dl2[r * 2] = d0;
+        a.dl2[r * 2 + 1] = d1;
+      }
     }
   }
   if (tid >= R2 && tid < 2 * R2) {  // zero rows 2B .. R2-1
@@ -431,22 +525,23 @@ __global__ __launch_bounds__(1024) void dir_mid_kernel(const DirMidArgs a) {
   }
   __syncthreads();
   clk[4] = __builtin_readcyclecounter();
-  dir_layer_bwd<R2, 64, 2>(a.W4, dl, a3, 1.f, dd3, a.d3, B, red);
+  dir_layer_bwd<R2, 64, 2>(a.W4, dl, a3, 1.f, dd3, w0 ? a.d3 : nullptr, B, red);
   clk[5] = __builtin_readcyclecounter();
-  dir_layer_bwd<R2, 128, 64>(a.W3, dd3, a2, 1.f, dd2, a.d2, B, red);
+  dir_layer_bwd<R2, 128, 64>(a.W3, dd3, a2, 1.f, dd2, w0 ? a.d2 : nullptr, B, red);
   clk[6] = __builtin_readcyclecounter();
-  dir_layer_bwd<R2, 256, 128>(a.W2, dd2, in1, a.gs1, nullptr, a.d1, B, red);
+  dir_layer_bwd<R2, 256, 128>(a.W2, dd2, in1, a.gs1, dd1, w0 ? a.d1 : nullptr, B, red);
   clk[7] = __builtin_readcyclecounter();
-  if (a.dbg && tid == 0)
-    printf("dir_mid cycles: stage %lld, fwd2 %lld, fwd3+4 %lld, seed %lld, bwd4 %lld, bwd3 %lld, bwd2 %lld\n",
+  dir_layer_bwd<R2, 64, 256, 512>(a.W1, dd1, in0, a.gs0, nullptr, a.d0, B, red, 64 * (int)blockIdx.x);
+  if (a.dbg && w0 && tid == 0)
+    printf("dir_mid cycles: stage %lld, fwd2 %lld, fwd3+4 %lld, seed %lld, bwd4 %lld, bwd3 %lld, bwd2 %lld, bwd1 %lld\n",
            clk[1] - clk[0], clk[2] - clk[1], clk[3] - clk[2], clk[4] - clk[3], clk[5] - clk[4], clk[6] - clk[5],
-           clk[7] - clk[6]);
+           clk[7] - clk[6], (long long)__builtin_readcyclecounter() - clk[7]);
 }
 
 int dir_mid(const DirMidArgs& a, hipStream_t st) {
   // (16 stacked rows: the slice-combine buffer of the layer-2 input gradient, 4 x 16 x 256 floats, fills 64 KB of LDS)
   VAD_CHECK(a.B >= 1 && a.B <= 8, "dir_mid: 1 <= B <= 8");
-  hipLaunchKernelGGL(dir_mid_kernel<8>, dim3(1), dim3(1024), 0, st, a);
+  hipLaunchKernelGGL(dir_mid_kernel<8>, dim3(512 / 64), dim3(1024), 0, st, a);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -474,16 +569,22 @@ int dir_combine(const DirCombineArgs& a, hipStream_t st) {
 
 static int mlp_rb(int M) { return M >= 64 ? 4 : 8; }
 
-int g_mlp_tail_wide = 0;  // knob "mlp_tail_wide": 1024-thread blocks for the detector's layers 1-4 (4-row blocks;
-                          // measured no faster: 30.6 us either way at config 2)
+int g_mlp_tail_rb = 0;  // knob "mlp_tail_rb": rows per block of the detector's layers 1-4 (0: auto)
+int g_mlp_tail_wide = 1;  // knob "mlp_tail_wide": 1024-thread blocks for the detector's layers 1-4 (4 x the K-slices
+                          // and split-K loads in flight of 256 threads; profiles/r03_mlp_tail_sweep.txt)
 
 int mlp_tail_fwd(const MlpTailArgs& a, hipStream_t st) {
   for (int i = 1; i < 5; ++i)
     VAD_CHECK(a.L[i].N <= MLP_MAXW && a.L[i].N % 4 == 0 && a.L[i].N / 4 <= 256 && a.L[i].K <= MLP_MAXW &&
                   a.L[i].K % 8 == 0 && a.WT[i],
               "mlp_tail_fwd: layer shape");
-  const int rb = mlp_rb(a.M);
-  if (rb == 4 && g_mlp_tail_wide)
+  const int rb = g_mlp_tail_rb ? g_mlp_tail_rb : mlp_rb(a.M);
+  VAD_CHECK(rb == 2 || rb == 4 || rb == 8, "mlp_tail_fwd: rows per block 2, 4 or 8");
+  if (rb == 2 && g_mlp_tail_wide)
+    hipLaunchKernelGGL((mlp_tail_fwd_kernel<2, 1024>), dim3((unsigned)cdiv(a.M, 2)), dim3(1024), 0, st, a);
+  else if (rb == 2)
+    hipLaunchKernelGGL((mlp_tail_fwd_kernel<2, 256>), dim3((unsigned)cdiv(a.M, 2)), dim3(256), 0, st, a);
+  else if (rb == 4 && g_mlp_tail_wide)
     hipLaunchKernelGGL((mlp_tail_fwd_kernel<4, 1024>), dim3((unsigned)cdiv(a.M, 4)), dim3(1024), 0, st, a);
   else if (rb == 4)
     hipLaunchKernelGGL((mlp_tail_fwd_kernel<4, 256>), dim3((unsigned)cdiv(a.M, 4)), dim3(256), 0, st, a);
