@@ -1320,8 +1320,8 @@ int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const fl
 }
 
 // Split-K slab reduction of the conv weight gradient.  Block = 64 consecutive slab elements (16 float4 columns) x 16
-// split-lanes; each lane sums every 16th slab with 2 independent float4 accumulators (a wave reads 4 slabs x 256 B
-// contiguous per load), lanes are combined through LDS in a fixed order.  (16-way split lanes: the 32-channel layers
+// split-lanes; each lane sums every 16th slab in order, 8 loads in flight (a wave reads 4 slabs x 256 B contiguous per
+// load), lanes are combined through LDS in a fixed order.  (16-way split lanes: the 32-channel layers
 // have few elements and up to 512 slabs.)  Slab layout [S][co][t*Ci + ci]; dW is torch
 // [co][ci][kh][kw].
 __global__ __launch_bounds__(256) void conv3_wgrad_reduce_kernel(const float* __restrict__ part, int S, int Co, int Ci,
@@ -1344,16 +1344,23 @@ __global__ __launch_bounds__(256) void conv3_wgrad_reduce_kernel(const float* __
   }
   const int e = threadIdx.x & 15, sl = threadIdx.x >> 4;
   const int64_t i = ((int64_t)blockIdx.x * 16 + e) * 4;  // total % 4 == 0 (Ci % 4 == 0)
-  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f};
   if (i < total) {
-    int z = sl;
-    for (; z + 16 < S; z += 32) {
-      a0 += *reinterpret_cast<const f32x4*>(part + (int64_t)z * total + i);
-      a1 += *reinterpret_cast<const f32x4*>(part + (int64_t)(z + 16) * total + i);
+    // slabs sl, sl + 16, ... summed in order, 8 loads in flight per batch (unconditional from clamped slabs: the
+    // 32-channel layers have up to 512 slabs, i.e. 32 loads per lane, which a one-load-per-iteration loop paid for
+    // with 32 memory round trips)
+    const int n = S > sl ? (S - sl + 15) / 16 : 0;
+    for (int k0 = 0; k0 < n; k0 += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = *reinterpret_cast<const f32x4*>(part + (int64_t)(sl + 16 * min(k0 + u, n - 1)) * total + i);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k0 + u < n) a0 += v[u];
     }
-    if (z < S) a0 += *reinterpret_cast<const f32x4*>(part + (int64_t)z * total + i);
   }
-  red[sl][e] = a0 + a1;
+  red[sl][e] = a0;
   __syncthreads();
   if (threadIdx.x < 16 && i < total) {
     f32x4 q[4];
@@ -1373,7 +1380,7 @@ int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, co
   VAD_CHECK(L.Ci % 4 == 0, "conv3_wgrad_reduce: Ci % 4");
   const int wblocks = (int)cdiv(total, 64);
   const int bblocks = db ? L.Co : 0;
-  hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(256), 0, st, partial, nsplit,
+  VAD_KLAUNCH(conv3_wgrad_reduce_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(256), 0, st, partial, nsplit,
                      L.Co, L.Ci, bias_partials, nbias_parts, dW, db, wblocks);
   VAD_LAUNCH_CHECK();
   return 0;
@@ -1547,8 +1554,8 @@ int dense_fwd(const float* X, int M, int K, const float* W, const float* b, int 
   DenseEpiArgs pe{Y, N, b, act.relu, act.drop, act.h1, act.thr, act.dscale, act.row0, nullptr, 1.f};
   if (skinny_ok(M, K)) {
     const dim3 grid((unsigned)cdiv(N, 4));
-    if (M <= 8) hipLaunchKernelGGL(skinny_fwd_kernel<8>, grid, dim3(512), 0, st, X, M, K, W, N, pe);
-    else hipLaunchKernelGGL(skinny_fwd_kernel<16>, grid, dim3(512), 0, st, X, M, K, W, N, pe);
+    if (M <= 8) VAD_KLAUNCH(skinny_fwd_kernel<8>, grid, dim3(512), 0, st, X, M, K, W, N, pe);
+    else VAD_KLAUNCH(skinny_fwd_kernel<16>, grid, dim3(512), 0, st, X, M, K, W, N, pe);
     VAD_LAUNCH_CHECK();
     return 0;
   }
@@ -1590,10 +1597,10 @@ int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX,
   if (skinny_ok(M, N) && (int64_t)(N + 512) * (M <= 8 ? 8 : 16) * 4 <= 65536) {  // dY + combine buffer in LDS
     const dim3 grid((unsigned)cdiv(K, 64));
     if (M <= 8)
-      hipLaunchKernelGGL(skinny_dgrad_kernel<8>, grid, dim3(1024), sizeof(float) * (N * 8 + 8 * 8 * 64), st, dY, M, N,
+      VAD_KLAUNCH(skinny_dgrad_kernel<8>, grid, dim3(1024), sizeof(float) * (N * 8 + 8 * 8 * 64), st, dY, M, N,
                          W, K, pe, skip);
     else
-      hipLaunchKernelGGL(skinny_dgrad_kernel<16>, grid, dim3(1024), sizeof(float) * (N * 16 + 8 * 16 * 64), st, dY, M,
+      VAD_KLAUNCH(skinny_dgrad_kernel<16>, grid, dim3(1024), sizeof(float) * (N * 16 + 8 * 16 * 64), st, dY, M,
                          N, W, K, pe, skip);
     VAD_LAUNCH_CHECK();
     return 0;

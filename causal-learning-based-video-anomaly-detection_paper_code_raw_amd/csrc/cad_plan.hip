@@ -812,7 +812,8 @@ struct CadPlanImpl {
       m.nsplit = ns;
       TIMED("det_fwd", mlp_tail_fwd(m, st));
     }
-    TIMED("head_fwd", head_fwd(head_args(), dlog, head_out(), st));
+    TIMED("head_rows", head_rows_fwd(head_args(), dlog, head_out(), st));
+    TIMED("head_seq", head_seq_fwd(head_args(), head_out(), st));
     VAD_TRY(join(st));
     TailArgs t = tail_args(nullptr, nullptr, nullptr, nullptr);
     t.fwd_bwd = tail_pre;

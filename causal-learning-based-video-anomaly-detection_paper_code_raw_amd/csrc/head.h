@@ -63,6 +63,9 @@ struct HeadOut {
   int* clip_flags; // [B][2]       (any valid detection, nmax>=2)
 };
 int head_fwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, hipStream_t st);
+// the two launches of head_fwd (row-parallel part, then the per-clip sequence part)
+int head_rows_fwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, hipStream_t st);
+int head_seq_fwd(const HeadArgs& a, const HeadOut& o, hipStream_t st);
 
 // backward: upstream grads -> grad slabs [B][slab] and d(det logits) [B*T][20]
 struct HeadUp {

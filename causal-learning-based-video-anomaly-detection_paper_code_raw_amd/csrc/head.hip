@@ -649,13 +649,20 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
            clk[1] - clk[0], clk[2] - clk[1], clk[3] - clk[2], clk[4] - clk[3], clk[5] - clk[4]);
 }
 
-int head_fwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, hipStream_t st) {
+int head_rows_fwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, hipStream_t st) {
   VAD_CHECK(a.T <= 4096, "head: T too large");
-  hipLaunchKernelGGL(head_rows_fwd_kernel, dim3(a.B * a.T), dim3(256), 0, st, a, det_logits, o);
-  VAD_LAUNCH_CHECK();
-  hipLaunchKernelGGL(head_seq_fwd_kernel, dim3(a.B), dim3(HT), 0, st, a, o);
+  VAD_KLAUNCH(head_rows_fwd_kernel, dim3(a.B * a.T), dim3(256), 0, st, a, det_logits, o);
   VAD_LAUNCH_CHECK();
   return 0;
+}
+int head_seq_fwd(const HeadArgs& a, const HeadOut& o, hipStream_t st) {
+  VAD_KLAUNCH(head_seq_fwd_kernel, dim3(a.B), dim3(HT), 0, st, a, o);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+int head_fwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, hipStream_t st) {
+  VAD_TRY(head_rows_fwd(a, det_logits, o, st));
+  return head_seq_fwd(a, o, st);
 }
 
 int g_head_dbg = 0;
@@ -1140,7 +1147,7 @@ __global__ void cad_tail_fwd_kernel(TailArgs t) {
 }
 
 int cad_tail_fwd(const TailArgs& t, hipStream_t st) {
-  hipLaunchKernelGGL(cad_tail_fwd_kernel, dim3(1), dim3(256), 0, st, t);
+  VAD_KLAUNCH(cad_tail_fwd_kernel, dim3(1), dim3(256), 0, st, t);
   VAD_LAUNCH_CHECK();
   return 0;
 }

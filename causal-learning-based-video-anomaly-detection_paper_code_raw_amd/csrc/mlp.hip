@@ -541,7 +541,7 @@ __global__ __launch_bounds__(1024) void dir_mid_kernel(const DirMidArgs a) {
 int dir_mid(const DirMidArgs& a, hipStream_t st) {
   // (16 stacked rows: the slice-combine buffer of the layer-2 input gradient, 4 x 16 x 256 floats, fills 64 KB of LDS)
   VAD_CHECK(a.B >= 1 && a.B <= 8, "dir_mid: 1 <= B <= 8");
-  hipLaunchKernelGGL(dir_mid_kernel<8>, dim3(512 / 64), dim3(1024), 0, st, a);
+  VAD_KLAUNCH(dir_mid_kernel<8>, dim3(512 / 64), dim3(1024), 0, st, a);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -581,15 +581,15 @@ int mlp_tail_fwd(const MlpTailArgs& a, hipStream_t st) {
   const int rb = g_mlp_tail_rb ? g_mlp_tail_rb : mlp_rb(a.M);
   VAD_CHECK(rb == 2 || rb == 4 || rb == 8, "mlp_tail_fwd: rows per block 2, 4 or 8");
   if (rb == 2 && g_mlp_tail_wide)
-    hipLaunchKernelGGL((mlp_tail_fwd_kernel<2, 1024>), dim3((unsigned)cdiv(a.M, 2)), dim3(1024), 0, st, a);
+    VAD_KLAUNCH((mlp_tail_fwd_kernel<2, 1024>), dim3((unsigned)cdiv(a.M, 2)), dim3(1024), 0, st, a);
   else if (rb == 2)
-    hipLaunchKernelGGL((mlp_tail_fwd_kernel<2, 256>), dim3((unsigned)cdiv(a.M, 2)), dim3(256), 0, st, a);
+    VAD_KLAUNCH((mlp_tail_fwd_kernel<2, 256>), dim3((unsigned)cdiv(a.M, 2)), dim3(256), 0, st, a);
   else if (rb == 4 && g_mlp_tail_wide)
-    hipLaunchKernelGGL((mlp_tail_fwd_kernel<4, 1024>), dim3((unsigned)cdiv(a.M, 4)), dim3(1024), 0, st, a);
+    VAD_KLAUNCH((mlp_tail_fwd_kernel<4, 1024>), dim3((unsigned)cdiv(a.M, 4)), dim3(1024), 0, st, a);
   else if (rb == 4)
-    hipLaunchKernelGGL((mlp_tail_fwd_kernel<4, 256>), dim3((unsigned)cdiv(a.M, 4)), dim3(256), 0, st, a);
+    VAD_KLAUNCH((mlp_tail_fwd_kernel<4, 256>), dim3((unsigned)cdiv(a.M, 4)), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((mlp_tail_fwd_kernel<8, 256>), dim3((unsigned)cdiv(a.M, 8)), dim3(256), 0, st, a);
+    VAD_KLAUNCH((mlp_tail_fwd_kernel<8, 256>), dim3((unsigned)cdiv(a.M, 8)), dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   return 0;
 }

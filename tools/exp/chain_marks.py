@@ -7,7 +7,7 @@ import torch
 from vad_amd import _native as nat
 from vad_amd.cad import CausalAnomalyDetector
 from vad_amd.train import CadTrainer, apply_memory_efficient_training
-for kv in sys.argv[1:]:
+for kv in [a for a in sys.argv[1:] if "=" in a]:
     k, v = kv.split("=")
     nat.check(nat.lib().vad_set_tuning(k.encode(), int(v)))
 dev = torch.device("cuda", 0)
@@ -25,8 +25,12 @@ eng = tr.eng
 for _ in range(5):
     tr.step(x, y)
 torch.cuda.synchronize()
+# kernel mode (--kernel): only the chain's kernels, timed by their own dispatch events (no marker packets between
+# them, so the gaps are the real launch / queue hand-off latencies); default: every labelled op (event records)
+KMODE = "--kernel" in sys.argv
+PREFIX = "conv_fwd/L7|avgpool|det_fwd|head_rows|head_seq|tail|dir_fwd|dir_pre"
 for rep in range(3):
-    eng.profile(True, "")
+    eng.profile(True, PREFIX if KMODE else "")
     tr.step(x, y)
     torch.cuda.synchronize()
     marks = eng.profile_marks()
