@@ -30,8 +30,10 @@ class CadTrainer:
     """One fused train step per call; the building block of train_model and bench.py.
 
     Data parallel: one process per GPU; rank r processes global clips [r*B, (r+1)*B) of each step (RNG keyed by
-    global clip index), grads (+ has-grad flags) are summed with one all_reduce and scaled by 1/world inside the
-    optimizer kernel; BN running stats follow rank 0 (broadcast before each forward, DDP's broadcast_buffers).
+    global clip index), grads (+ has-grad flags) are summed by three bucketed all_reduces -- causal head + direct
+    classifier + flags during the backbone backward, the detector only when some rank's detector has a gradient, the
+    backbone after its backward (_backward_overlapped) -- and scaled by 1/world inside the optimizer kernel; BN
+    running stats follow rank 0 (broadcast before each forward, DDP's broadcast_buffers).
 
     sync_bn=True (world > 1): SyncBatchNorm semantics -- every BN layer normalises over the whole group's batch
     (per-layer sums all-reduced in forward and backward), so the N-rank step equals the reference's single-process
