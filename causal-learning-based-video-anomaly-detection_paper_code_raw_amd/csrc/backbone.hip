@@ -16,6 +16,7 @@ int g_cad_dy_per_layer = 1;  // knob "cad_dy_per_layer" (A/B of the plan option 
 int g_cad_det_gate = 1;      // knob "cad_det_gate": the backbone backward waits on the device detector gate
 int g_cad_dir_affine = 1;  // knob "cad_dir_affine": direct classifier backward as A + c beta, precomputed in the forward
 int g_cad_wgrad_stream = 1;  // knob "cad_wgrad_stream": backbone weight gradients on their own stream
+int g_cad_l0_slab = 1;  // knob "cad_l0_slab": layer 0's weight gradient on a split-K slab of its own (no wait for layer 1's)
                              // reduce of layers 0-6, bit 2 the causal head's kernels
 
 // =====================================================================================================
@@ -289,31 +290,22 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const PT* __restrict__
                                                           float* running_var, float momentum, float eps,
                                                           int training, float* __restrict__ stats, int cm) {
   const int c = blockIdx.x;
-  __shared__ double red[2][256];
   double a = 0.0, b = 0.0;
   // partials row-major [P][2C], or column-major [2C][P] (cm: the fused stem's layout, coalesced here)
   const int64_t rs = cm ? 1 : 2 * C, ia = cm ? (int64_t)c * P : c, ib = cm ? (int64_t)(C + c) * P : C + c;
   if (training) {
+#pragma unroll 4
     for (int p = threadIdx.x; p < P; p += 256) {
       a += (double)partials[p * rs + ia];
       b += (double)partials[p * rs + ib];
     }
   }
-  red[0][threadIdx.x] = a;
-  red[1][threadIdx.x] = b;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + s];
-      red[1][threadIdx.x] += red[1][threadIdx.x + s];
-    }
-    __syncthreads();
-  }
+  block_sum2_256(a, b);
   if (threadIdx.x == 0) {
     double mean, var;
     if (training) {
-      mean = red[0][0] / count;
-      var = red[1][0] / count - mean * mean;
+      mean = a / count;
+      var = b / count - mean * mean;
       if (var < 0) var = 0;
       running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
       running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * var * count / (count - 1.0));
@@ -354,28 +346,19 @@ __global__ __launch_bounds__(256) void bn_sum_partials_kernel(const float* __res
                                                               double* __restrict__ sums, float* a_out,
                                                               float* b_out, int cm) {
   const int c = blockIdx.x;
-  __shared__ double red[2][256];
   double a = 0.0, b = 0.0;
   const int64_t rs = cm ? 1 : 2 * C, ia = cm ? (int64_t)c * P : c, ib = cm ? (int64_t)(C + c) * P : C + c;
+#pragma unroll 4
   for (int p = threadIdx.x; p < P; p += 256) {
     a += (double)partials[p * rs + ia];
     b += (double)partials[p * rs + ib];
   }
-  red[0][threadIdx.x] = a;
-  red[1][threadIdx.x] = b;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + s];
-      red[1][threadIdx.x] += red[1][threadIdx.x + s];
-    }
-    __syncthreads();
-  }
+  block_sum2_256(a, b);
   if (threadIdx.x == 0) {
-    sums[c] = red[0][0];
-    sums[C + c] = red[1][0];
-    if (a_out) a_out[c] = (float)red[0][0];
-    if (b_out) b_out[c] = (float)red[1][0];
+    sums[c] = a;
+    sums[C + c] = b;
+    if (a_out) a_out[c] = (float)a;
+    if (b_out) b_out[c] = (float)b;
   }
 }
 
@@ -476,26 +459,17 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const PT* __restri
                                                               float* __restrict__ stats, float* dgamma,
                                                               float* dbeta, int training, float* dbias, int cm) {
   const int c = blockIdx.x;
-  __shared__ double red[2][256];
   double a = 0.0, b = 0.0;
   // partials row-major [P][2C] or column-major [2C][P] (cm)
   const int64_t rs = cm ? 1 : 2 * C, ia = cm ? (int64_t)c * P : c, ib = cm ? (int64_t)(C + c) * P : C + c;
+#pragma unroll 4
   for (int p = threadIdx.x; p < P; p += 256) {
     a += (double)partials[p * rs + ia];
     b += (double)partials[p * rs + ib];
   }
-  red[0][threadIdx.x] = a;
-  red[1][threadIdx.x] = b;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + s];
-      red[1][threadIdx.x] += red[1][threadIdx.x + s];
-    }
-    __syncthreads();
-  }
+  block_sum2_256(a, b);
   if (threadIdx.x == 0) {
-    const double sdz = red[0][0], sdzx = red[1][0];
+    const double sdz = a, sdzx = b;
     if (dgamma) dgamma[c] = (float)sdzx;
     if (dbeta) dbeta[c] = (float)sdz;
     const double inv = stats[C + c];
@@ -1028,6 +1002,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "mlp_tail_wide") g_mlp_tail_wide = value;
   else if (k == "mlp_tail_rb") g_mlp_tail_rb = value;
   else if (k == "cad_last_wgrad_main") g_cad_last_wgrad_main = value;
+  else if (k == "cad_l0_slab") g_cad_l0_slab = value;
   else if (k == "head_dbg") g_head_dbg = value;
   else if (k == "stem_dbg") g_stem_dbg = value;
   else if (k == "conv_wgrad_s1_nt") g_wgrad_s1_nt = value;
@@ -1319,16 +1294,19 @@ int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const fl
   });
 }
 
-// Split-K slab reduction of the conv weight gradient.  Block = 64 consecutive slab elements (16 float4 columns) x 16
-// split-lanes; each lane sums every 16th slab in order, 8 loads in flight (a wave reads 4 slabs x 256 B contiguous per
-// load), lanes are combined through LDS in a fixed order.  (16-way split lanes: the 32-channel layers
-// have few elements and up to 512 slabs.)  Slab layout [S][co][t*Ci + ci]; dW is torch
-// [co][ci][kh][kw].
+// Split-K slab reduction of the conv weight gradient.  Block = 256/SL float4 columns x SL split lanes; lane sl sums
+// slabs sl, sl + SL, ... in order with 8 loads in flight (unconditional, from clamped slab indices), and the SL lanes
+// of a column are combined through LDS in a fixed order.  SL = the smallest of 1, 2, 4, 8, 16 that leaves each lane
+// <= 16 slabs (the wide layers have 12-48 slabs: one lane per column reads them all; the 32-channel layers up to
+// 512: 16 lanes) -- a fixed function of S, so the summation order is fixed per layer.  Slab layout [S][co][t*Ci + ci];
+// dW is torch [co][ci][kh][kw].  Extra blocks after the first wblocks reduce the conv bias (one block per channel).
+template <int SL>
 __global__ __launch_bounds__(256) void conv3_wgrad_reduce_kernel(const float* __restrict__ part, int S, int Co, int Ci,
                                                                  const float* __restrict__ bparts, int NB,
                                                                  float* __restrict__ dW, float* __restrict__ db,
                                                                  int wblocks) {
-  __shared__ f32x4 red[16][17];
+  constexpr int NCOL = 256 / SL;
+  __shared__ f32x4 red[SL > 1 ? SL : 1][NCOL + 1];
   const int64_t ldp = 9 * Ci;
   const int64_t total = (int64_t)Co * ldp;
   if ((int)blockIdx.x >= wblocks) {  // conv bias: one block per channel, 256-way strided sum + tree
@@ -1336,37 +1314,43 @@ __global__ __launch_bounds__(256) void conv3_wgrad_reduce_kernel(const float* __
     float s = 0.f;
     for (int p = threadIdx.x; p < NB; p += 256) s += bparts[(int64_t)p * 2 * Co + c];
     s = wave_sum(s);
-    float* r0 = reinterpret_cast<float*>(&red[0][0]);
+    __shared__ float r0[4];
     if ((threadIdx.x & 63) == 0) r0[threadIdx.x >> 6] = s;
     __syncthreads();
     if (threadIdx.x == 0) db[c] = (r0[0] + r0[1]) + (r0[2] + r0[3]);
     return;
   }
-  const int e = threadIdx.x & 15, sl = threadIdx.x >> 4;
-  const int64_t i = ((int64_t)blockIdx.x * 16 + e) * 4;  // total % 4 == 0 (Ci % 4 == 0)
+  const int e = threadIdx.x % NCOL, sl = threadIdx.x / NCOL;
+  const int64_t i = ((int64_t)blockIdx.x * NCOL + e) * 4;  // total % 4 == 0 (Ci % 4 == 0)
   f32x4 a0 = {0.f, 0.f, 0.f, 0.f};
   if (i < total) {
-    // slabs sl, sl + 16, ... summed in order, 8 loads in flight per batch (unconditional from clamped slabs: the
-    // 32-channel layers have up to 512 slabs, i.e. 32 loads per lane, which a one-load-per-iteration loop paid for
-    // with 32 memory round trips)
-    const int n = S > sl ? (S - sl + 15) / 16 : 0;
+    const int n = S > sl ? (S - sl + SL - 1) / SL : 0;
     for (int k0 = 0; k0 < n; k0 += 8) {
       f32x4 v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        v[u] = *reinterpret_cast<const f32x4*>(part + (int64_t)(sl + 16 * min(k0 + u, n - 1)) * total + i);
+        v[u] = *reinterpret_cast<const f32x4*>(part + (int64_t)(sl + SL * min(k0 + u, n - 1)) * total + i);
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         if (k0 + u < n) a0 += v[u];
     }
   }
-  red[sl][e] = a0;
-  __syncthreads();
-  if (threadIdx.x < 16 && i < total) {
-    f32x4 q[4];
+  f32x4 s = a0;
+  if constexpr (SL > 1) {
+    red[sl][e] = a0;
+    __syncthreads();
+    if (sl != 0) return;
+    // pairwise tree over the SL lanes, fixed order
+    f32x4 q[SL];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) q[u] = (red[4 * u][e] + red[4 * u + 1][e]) + (red[4 * u + 2][e] + red[4 * u + 3][e]);
-    const f32x4 s = (q[0] + q[1]) + (q[2] + q[3]);
+    for (int u = 0; u < SL; ++u) q[u] = red[u][e];
+#pragma unroll
+    for (int w = 1; w < SL; w <<= 1)
+#pragma unroll
+      for (int u = 0; u < SL; u += 2 * w) q[u] += q[u + w];
+    s = q[0];
+  }
+  if (i < total) {
     const int64_t co = i / ldp, r = i - co * ldp;
     const int t = (int)(r / Ci), ci = (int)(r - (int64_t)t * Ci);
 #pragma unroll
@@ -1378,10 +1362,18 @@ int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, co
                        int nbias_parts, float* dW, float* db, hipStream_t st) {
   const int64_t total = (int64_t)L.Co * L.Ci * 9;
   VAD_CHECK(L.Ci % 4 == 0, "conv3_wgrad_reduce: Ci % 4");
-  const int wblocks = (int)cdiv(total, 64);
+  int sl = 1;
+  while (sl < 16 && cdiv(nsplit, sl) > 16) sl *= 2;
+  const int wblocks = (int)cdiv(total, 4 * (256 / sl));
   const int bblocks = db ? L.Co : 0;
-  VAD_KLAUNCH(conv3_wgrad_reduce_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(256), 0, st, partial, nsplit,
-                     L.Co, L.Ci, bias_partials, nbias_parts, dW, db, wblocks);
+  const dim3 grid((unsigned)(wblocks + bblocks));
+  switch (sl) {
+    case 1: VAD_KLAUNCH(conv3_wgrad_reduce_kernel<1>, grid, dim3(256), 0, st, partial, nsplit, L.Co, L.Ci, bias_partials, nbias_parts, dW, db, wblocks); break;
+    case 2: VAD_KLAUNCH(conv3_wgrad_reduce_kernel<2>, grid, dim3(256), 0, st, partial, nsplit, L.Co, L.Ci, bias_partials, nbias_parts, dW, db, wblocks); break;
+    case 4: VAD_KLAUNCH(conv3_wgrad_reduce_kernel<4>, grid, dim3(256), 0, st, partial, nsplit, L.Co, L.Ci, bias_partials, nbias_parts, dW, db, wblocks); break;
+    case 8: VAD_KLAUNCH(conv3_wgrad_reduce_kernel<8>, grid, dim3(256), 0, st, partial, nsplit, L.Co, L.Ci, bias_partials, nbias_parts, dW, db, wblocks); break;
+    default: VAD_KLAUNCH(conv3_wgrad_reduce_kernel<16>, grid, dim3(256), 0, st, partial, nsplit, L.Co, L.Ci, bias_partials, nbias_parts, dW, db, wblocks); break;
+  }
   VAD_LAUNCH_CHECK();
   return 0;
 }

@@ -354,7 +354,9 @@ struct CadPlanImpl {
   // affine path (stage 1 then reads the stacked clip-mean grads).
   float *dl2 = nullptr, *dg2[4] = {}, *dpool2 = nullptr;
   int dir_pre = 0, tail_pre = 0, dir_used = 0;
-  float *dA, *dY, *dY2, *wpart, *stem_d;  // stem_d: [NF][H1][W1][32], the stem backward's dA / dY (stem_grad only)
+  // wpart0: layer 0's split-K slab (frozen stem: its weight gradient runs on the caller's stream while the weight-gradient
+  // stream may still be reducing layer 1's slab)
+  float *dA, *dY, *dY2, *wpart, *wpart0, *stem_d;  // stem_d: [NF][H1][W1][32], the stem backward's dA / dY (stem_grad only)
   // per-layer dY buffers (option "dy_per_layer", default on): layer l's BN backward writes dYL[l], which only layer l's
   // weight and input gradients read, so the compute stream never waits for the weight-gradient stream to release a
   // shared dY buffer (one cross-queue barrier per layer less); ~2x the dY memory (≈210 MB at config 2)
@@ -362,7 +364,7 @@ struct CadPlanImpl {
   int dy_per_layer = 1;
   float *sq_parts, *slot_info, *clip;
   int16_t* chunk_slot;
-  int64_t parts_floats, dense_scratch_floats, wpart_floats, slab_len, act_max;
+  int64_t parts_floats, dense_scratch_floats, wpart_floats, wpart0_floats, slab_len, act_max;
   int64_t clip0 = 0;
   // SyncBatchNorm (option): per-layer [2C] double sums are handed to the caller's callback (an all-reduce over the
   // process group) between the partial-sum reduction and the finalize, forward and backward
@@ -521,6 +523,8 @@ struct CadPlanImpl {
     stem_d = w.take<float>(nf * H1 * W1 * 32);
     wpart_floats = 16ll << 20;
     wpart = w.take<float>(wpart_floats);
+    wpart0_floats = std::max<int64_t>(8ll << 20, (int64_t)L[0].Co * 9 * L[0].Ci);
+    wpart0 = w.take<float>(wpart0_floats);
     sq_parts = w.take<float>(1024);
     bnsync = w.take<double>(2 * 256);
     slot_info = w.take<float>(4 * 160);
@@ -968,15 +972,22 @@ struct CadPlanImpl {
           VAD_HIP(hipEventRecord(ev_dy[l & 1], st));
           VAD_HIP(hipStreamWaitEvent(st3, ev_dy[l & 1], 0));
           wst = st3;
-        } else if (on_main) {
+        }
+        // layer 0 on the caller's stream: on a slab of its own (knob cad_l0_slab) it starts right after its BN backward,
+        // beside the end of layer 1's weight gradient (the stream join after the loop orders the optimizer after both);
+        // on the shared slab it waits for layer 1's slab reduce
+        const bool own = on_main && g_cad_l0_slab;
+        if (on_main && !own) {
           VAD_HIP(hipStreamWaitEvent(st, ev_wg[1], 0));  // layer 1's weight gradient + slab reduce are done
           st3_joined = true;  // (the weight-gradient stream's last work)
         }
+        float* slab = own ? wpart0 : wpart;
+        const int64_t slab_cap = own ? wpart0_floats : wpart_floats;
         hipStream_t st = wst;
         int ns = 0;
-        // (layer 0 with the frozen stem: nothing runs beside its weight gradient)
-        TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dYl, src, sst, wpart, &ns, wpart_floats, st, l == 0 && !stem_grad));
-        TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], wpart, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
+        // (layer 0 with the frozen stem: little runs beside its weight gradient)
+        TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dYl, src, sst, slab, &ns, slab_cap, st, l == 0 && !stem_grad));
+        TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], slab, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
         if (wgs && !on_main) VAD_HIP(hipEventRecord(ev_wg[l & 1], st));
       }
       if (l > 0) TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st));

@@ -156,6 +156,28 @@ __device__ inline float wave_sum(float v) {
   return v;
 }
 
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// sums of a and b over a 256-thread block (wave butterflies, then the 4 wave sums in a fixed order), returned to every
+// thread; one barrier (the finalize kernels: an 8-level LDS tree with a barrier per level cost ~2 us per launch)
+__device__ inline void block_sum2_256(double& a, double& b) {
+  __shared__ double red2[2][4];
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red2[0][w] = a;
+    red2[1][w] = b;
+  }
+  __syncthreads();
+  a = (red2[0][0] + red2[0][1]) + (red2[0][2] + red2[0][3]);
+  b = (red2[1][0] + red2[1][1]) + (red2[1][2] + red2[1][3]);
+}
+
 // f32-in / f32-acc MFMA 32x32x2: lane l supplies A[l&31][l>>5], B[l>>5][l&31];
 // D row = (r&3) + 8*(r>>2) + 4*(l>>5), col = l&31.
 // torch.relu semantics: NaN propagates (fmaxf(NaN, 0) would return 0 and hide a non-finite batch from the

@@ -77,6 +77,27 @@ __device__ __forceinline__ void put_planes(__bf16* d, int pitch, const float* v,
   }
 }
 
+// Output pixel m (0 .. NI*TH*TW) of a tile -> (image, row, column).  Row-major in general; 8x8 tiles (NI = NW/2
+// images of one 8x8 block each) map the four 8-pixel groups g of a wave's 32 MFMA rows to rows r + {0, 4, 1, 5}
+// (r = 2 (wave & 1)) of image wave / 2, so the 16 lanes of every ds_read_b128 phase (groups 0,1 or 2,3) read patch
+// pixels four patch rows apart: 4 * PW * S pixels, == 8 (mod 16) for PW = 10 (S = 1) and 2 * 17 (S = 2), i.e. the
+// second 8 lanes land on the other half of the 16 bank quads (row-major: PW = 10 put pixels 16, 17 on the quads of
+// pixels 0, 1 -- SQ_LDS_BANK_CONFLICT 0.48 of the LDS cycles on the 8x8 layers)
+template <int S, int NI, int TH, int TW, int NW>
+__device__ __forceinline__ void tile_pixel(int m, int& mi, int& py, int& px) {
+  if constexpr (TH == 8 && TW == 8 && 2 * NI == NW) {
+    const int w = m >> 5, g = (m >> 3) & 3;
+    mi = w >> 1;
+    py = 2 * (w & 1) + 4 * (g & 1) + (g >> 1);
+    px = m & 7;
+  } else {
+    mi = m / (TH * TW);
+    const int mr = m % (TH * TW);
+    py = mr / TW;
+    px = mr % TW;
+  }
+}
+
 // WCH > 1: the block keeps the split weights of all WCH reduction chunks resident in LDS (staged during its first
 // tile, p.C == WCH * PC) instead of restaging the chunk's slice for every (tile, chunk) item -- the weight split is
 // most of the staging VALU of the 32-channel layers
@@ -117,9 +138,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
   const int nchc = p.C / PC, nch = KD * nchc;  // reduction chunks: (depth tap, channel chunk)
 
   // this lane's A pixel (MFMA row lane & 31) inside the tile
-  const int m = wave * 32 + j;
-  const int mi = m / (TH * TW), mr = m % (TH * TW);
-  const int py = mr / TW, px = mr % TW;
+  int mi, py, px;
+  tile_pixel<S, NI, TH, TW, NW>(wave * 32 + j, mi, py, px);
   const int arow0 = (mi * PH + py * S) * PW;
   const __bf16* bbase = wl + j * WP + 8 * h;
 
@@ -297,9 +317,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
       origin(tile, img0, oy0, ox0);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int pm = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int qi = pm / (TH * TW), qr = pm % (TH * TW);
-        const int oy = oy0 + qr / TW, ox = ox0 + qr % TW, img = img0 + qi;
+        int qi, qy, qx;
+        tile_pixel<S, NI, TH, TW, NW>(wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, qi, qy, qx);
+        const int oy = oy0 + qy, ox = ox0 + qx, img = img0 + qi;
         if (img < p.NF && oy < p.OH && ox < p.OW) {
           TA* o = out + (((int64_t)img * p.OH + oy) * p.OW + ox) * p.N + n0 + j;
 #pragma unroll
