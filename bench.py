@@ -232,7 +232,7 @@ def run_gpu(args, rank, world, local_rank):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    t0 = t_loop0 = time.perf_counter()
     for i in range(args.steps):
         instrument = i % args.prof_every == 0
         if instrument:
@@ -240,6 +240,7 @@ def run_gpu(args, rank, world, local_rank):
         losses = trainer.step(pool[i % 2], labels)
         if instrument:
             eng.profile(False, reset=False)
+    t_enq = time.perf_counter()  # host enqueue time of the timed steps (== the step time when the host is the bound)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -306,12 +307,14 @@ def run_gpu(args, rank, world, local_rank):
             x = stager.finish(h)
             h = stager.issue(u8[(i + 1) % 2])
             trainer.step(x, labels)
+        h2d_enq = time.perf_counter() - t0
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         stager.finish(h)
         torch.cuda.synchronize()
         h2d = {"value": round(B * args.h2d_steps / el, 3), "unit": "clips/s", "steps": args.h2d_steps,
                "ms_per_step": round(1e3 * el / args.h2d_steps, 4),
+               "host_enqueue_ms_per_step": round(1e3 * h2d_enq / args.h2d_steps, 4),
                "bytes_h2d_per_step": B * T * H * W,
                "path": "pinned u8 host clips -> ClipStager.issue (H2D, copy stream) -> finish (u8->fp32 on device)"}
     # whole-step algorithmic FLOP rate (all 3x3 convs fwd/dgrad/wgrad + conv1 fwd), for context
@@ -319,7 +322,8 @@ def run_gpu(args, rank, world, local_rank):
     dgrad_flops = conv_flops - 2.0 * B * T * conv_shapes(B, T, H, W)[0][3] * conv_shapes(B, T, H, W)[0][4] * 32 * 32 * 9
     c1 = algorithmic_work("conv1", B, T, H, W)[1]
     step_flops = 2 * conv_flops + dgrad_flops + c1
-    return dict(elapsed=elapsed, step_ms=step_ms, roof=roof, breakdown=breakdown, dominant=dominant,
+    return dict(elapsed=elapsed, step_ms=step_ms, host_enqueue_ms=1e3 * (t_enq - t_loop0) / args.steps, roof=roof,
+                breakdown=breakdown, dominant=dominant,
                 final_loss=final_loss, step_tflops=step_flops / (step_ms * 1e-3) / 1e12, probe=probe, h2d=h2d,
                 allreduce_bytes=allreduce_bytes, post_backbone_us=post_backbone_us)
 
@@ -862,6 +866,7 @@ def main():
             "step_roofline": step_roofline(args, clips / r["elapsed"] / world, r["step_tflops"]),
             "allreduce_bytes_per_step": r["allreduce_bytes"],
             "post_backbone_us": (round(r["post_backbone_us"], 1) if r.get("post_backbone_us") is not None else None),
+            "host_enqueue_ms_per_step": round(r["host_enqueue_ms"], 4),
             "final_loss": r["final_loss"],
         }
         if args.breakdown_out:

@@ -14,6 +14,7 @@ int conv1_num_parts(int NF, int OH);
 // the consumer applies bn1+ReLU on load (exact: the affine+ReLU is monotone per channel)
 extern int g_x3_dgrad_blocks;  // knob "conv_dgrad_blocks"
 extern int g_x3_big;  // knob "conv_split_big"
+extern int g_x3_pipe;  // knob "conv_split_pipe"
 extern int g_x3_s2big;  // knob "conv_split_s2big"
 extern int g_cad_dir_affine;  // knob "cad_dir_affine": the direct classifier's loss-mode backward precomputed in the forward
 extern int g_cad_prep_stream, g_cad_wgrad_stream, g_cad_det_gate, g_cad_last_wgrad_main, g_cad_event_sysfence,
@@ -81,7 +82,18 @@ int conv3_prep_weights_all(int n, const float* const* w, const Conv3Layer* L, fl
 int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats /*nullable: BN+ReLU on load*/,
               const float* wf, const float* bias, float* y, float* partials, int* nparts, hipStream_t st,
               int* parts_cm = nullptr);  // parts_cm: in = accepted, out = 1 if written so
-int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
+// the BN-backward reduce of the layer below fused into an input gradient's epilogue (split kernels only): y = that
+// layer's raw output, stats = its BN state; per-block sums of dZ and dZ*xhat land column-major in parts (cap floats);
+// *nparts = their block count, or 0 when the dispatched kernel does not fuse (the caller then runs bn_bwd_reduce)
+struct BnBwdFuse {
+  const float* y;
+  const float* stats;
+  float* parts;
+  int64_t cap;
+  int* nparts;
+};
+int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,
+                const BnBwdFuse* f = nullptr);
 // direct LDS-patch kernels (conv_patch.hip) for stride-1 layers; conv3_fwd / conv3_dgrad route there by default
 bool conv3_patch_supported(const Conv3Layer& L, bool fwd);
 extern int g_patch_persist;  // single-chunk (C == 32) stride-1 layers on the persistent patch kernel
@@ -114,12 +126,14 @@ struct ActStorage {
 bool conv3_x3_supported(const Conv3Layer& L, bool fwd);
 int conv3_x3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
                  float* y, float* partials, int* nparts, hipStream_t st, int* parts_cm = nullptr);
-int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
+int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,
+                   const BnBwdFuse* f = nullptr);
 // stride-2 input gradient on the split-bf16 (or, with conv_bf16, bf16) MFMA: parity classes of a 16x16 dX tile
 // sharing one dY patch; Wd in the plain [Ci][9][Co] layout (conv3_prep_weights with classes == 0)
 extern int g_dgrad_s2_x3;  // knob "conv_dgrad_s2_x3"
 bool conv3_x3_dgrad_s2_supported(const Conv3Layer& L);
-int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st);
+int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,
+                      const BnBwdFuse* f = nullptr);
 extern int g_wgrad_split;     // stride-1 weight gradients on the split-bf16 kernel (knob "conv_wgrad_split")
 extern int g_wgrad_s1_nt, g_wgrad_s1_nt_blocks, g_wgrad_s1_nt_wide;  // knobs "conv_wgrad_s1_nt", "conv_wgrad_s1_nt_blocks"
 extern int g_wgrad_s2_blocks;  // their target grid size (knob "conv_wgrad_s2_blocks")

@@ -16,6 +16,9 @@ int g_cad_dy_per_layer = 1;  // knob "cad_dy_per_layer" (A/B of the plan option 
 int g_cad_det_gate = 1;      // knob "cad_det_gate": the backbone backward waits on the device detector gate
 int g_cad_dir_affine = 1;  // knob "cad_dir_affine": direct classifier backward as A + c beta, precomputed in the forward
 int g_cad_wgrad_stream = 1;  // knob "cad_wgrad_stream": backbone weight gradients on their own stream
+// knob "bn_bwd_fuse": the BN-backward reduce in the input gradients' epilogues -- bit 0 the stride-1 kernels, bit 1 the
+// stride-2 one (A/B at config 2: both 1.922 -> 1.893 ms, stride-1 only 1.927 -> 1.922, profiles/r03_bnfuse_ab.json)
+int g_bn_bwd_fuse = 3;
 int g_cad_l0_slab = 1;  // knob "cad_l0_slab": layer 0's weight gradient on a split-K slab of its own (no wait for layer 1's)
                              // reduce of layers 0-6, bit 2 the causal head's kernels
 
@@ -1003,6 +1006,8 @@ int set_tuning(const char* key, int value) {
   else if (k == "mlp_tail_rb") g_mlp_tail_rb = value;
   else if (k == "cad_last_wgrad_main") g_cad_last_wgrad_main = value;
   else if (k == "cad_l0_slab") g_cad_l0_slab = value;
+  else if (k == "conv_split_pipe") g_x3_pipe = value;
+  else if (k == "bn_bwd_fuse") g_bn_bwd_fuse = value;
   else if (k == "head_dbg") g_head_dbg = value;
   else if (k == "stem_dbg") g_stem_dbg = value;
   else if (k == "conv_wgrad_s1_nt") g_wgrad_s1_nt = value;
@@ -1208,13 +1213,16 @@ static int dgrad_launch(const ConvGeom& g, const TapTable& taps, const float* dY
   });
 }
 
-int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st) {
+int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,
+                const BnBwdFuse* f) {
   VAD_CHECK(L.Co % 32 == 0, "conv3_dgrad: Co must be a multiple of 32");
   const int N = L.Ci;
-  if (g_tune.patch && conv3_x3_supported(L, false)) return conv3_x3_dgrad(L, dY, wd, dX, st);
+  if (f) *f->nparts = 0;
+  if (g_tune.patch && conv3_x3_supported(L, false))
+    return conv3_x3_dgrad(L, dY, wd, dX, st, (g_bn_bwd_fuse & 1) ? f : nullptr);
   // (the split kernel reads the plain Wd layout, which the prep writes exactly when the f32 patch kernel is usable)
   if (g_tune.patch && conv3_patch_supported(L, false) && conv3_x3_dgrad_s2_supported(L))
-    return conv3_x3_dgrad_s2(L, dY, wd, dX, st);
+    return conv3_x3_dgrad_s2(L, dY, wd, dX, st, (g_bn_bwd_fuse & 2) ? f : nullptr);
   VAD_CHECK(!g_act_bf16, "conv3_dgrad: bf16 activations need the split kernels");
   if (g_tune.patch && conv3_patch_supported(L, false)) return conv3_patch_dgrad(L, dY, wd, dX, st);
   if (L.stride == 1) {

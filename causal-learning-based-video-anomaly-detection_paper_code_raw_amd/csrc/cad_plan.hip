@@ -948,14 +948,15 @@ struct CadPlanImpl {
     VAD_TRY(streams());
     const bool wgs = wgrad_stream != 0 && g_cad_wgrad_stream;
     bool st3_joined = false;
+    int fused_np = 0;  // layer l's BN-backward partial sums, already written by layer l+1's input gradient
     for (int l = 7; l >= 0; --l) {
       const int64_t M = (int64_t)NF * L[l].OH * L[l].OW;
       const int C = L[l].Co;
-      int np = 0, nb = 0;
+      int np = fused_np, nb = 0;
       const bool perl = dy_per_layer != 0 && g_cad_dy_per_layer != 0;
       float* dYl = perl ? dYL[l] : ((l & 1) ? dY2 : dY);
       VAD_CHECK((int64_t)bn_rows_parts((int)M, C) * 2 * C <= parts_floats, "backward: BN partial buffer too small");
-      TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st, 1));
+      if (np == 0) TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st, 1));
       VAD_TRY(bn_bwd_stats(l + 1, np, C, (double)M, P(LY.bn_w[l]), G(LY.bn_w[l]), G(LY.bn_b[l]), G(LY.conv_b[l]), st));
       // dYl was last read by layer l+2's weight gradient
       if (wgs && l + 2 <= 7 && !perl) VAD_HIP(hipStreamWaitEvent(st, ev_wg[l & 1], 0));
@@ -990,7 +991,12 @@ struct CadPlanImpl {
         TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], slab, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
         if (wgs && !on_main) VAD_HIP(hipEventRecord(ev_wg[l & 1], st));
       }
-      if (l > 0) TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st));
+      fused_np = 0;
+      if (l > 0) {
+        // its epilogue also reduces layer l-1's BN backward (dZ = dA masked by layer l-1's ReLU, dZ * xhat)
+        const BnBwdFuse fu{y[l - 1], stats[l], parts, parts_floats, &fused_np};
+        TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st, &fu));
+      }
       if (l == debug_stop_layer) break;
     }
     if (wgs && !st3_joined) {  // every weight gradient is final before the stem backward / optimizer

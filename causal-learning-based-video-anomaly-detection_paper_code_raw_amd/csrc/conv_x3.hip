@@ -36,6 +36,35 @@ struct X3Args {
   int tiles_h, tiles_w, ntiles, tpb;
   int parts_cm;  // forward: BN partial sums column-major [2N][gridDim.x] (coalesced finalize reads)
   int D;         // KD == 3 (Conv3d k3 p1 s1): depth of the NDHWC volumes; image index = n * D + d
+  // input gradients (nullable): the BN-backward reduce of the layer whose activation this dX is, fused into the
+  // epilogue -- bny = that layer's raw output y (same layout as out), bnst = its BN state (mean | invstd | scale |
+  // shift); per-block sums of dZ = dX [scale*y + shift > 0] and dZ * xhat go to partials, column-major [2N][gridDim.x]
+  const void* bny;
+  const float* bnst;
+};
+
+// epilogue half of the fused BN-backward reduce (bn_bwd_reduce_kernel's arithmetic on the value just computed; with
+// bf16 storage on the value as stored)
+struct BnBwdLane {
+  float mean, inv, sc, sh;
+  __device__ __forceinline__ void load(const float* st, int C, int c) {
+    mean = st[c];
+    inv = st[C + c];
+    sc = st[2 * C + c];
+    sh = st[3 * C + c];
+  }
+  template <bool AB>
+  __device__ __forceinline__ static float ld(const void* bny, int64_t idx) {
+    return act_ld(reinterpret_cast<const act_t<AB>*>(bny) + idx);
+  }
+  // (the y values are loaded for the whole epilogue first: one wait instead of a round trip per pixel)
+  template <bool AB>
+  __device__ __forceinline__ void add(float yy, float v, float& s1, float& s2) const {
+    const float a = AB ? (float)(__bf16)v : v;
+    const float dz = fmaf(yy, sc, sh) > 0.f ? a : 0.f;
+    s1 += dz;
+    s2 = fmaf(dz, (yy - mean) * inv, s2);
+  }
 };
 
 __device__ __forceinline__ void split3(const float* v, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
@@ -263,11 +292,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
   };
 
   float bj[NT], s1[NT], s2[NT];
+  BnBwdLane bl[NT];
+  const bool bnb = !FWD && p.bny;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int col = n0 + nt * 32 + j;
     bj[nt] = (FWD && col < p.N) ? p.bias[col] : 0.f;
     s1[nt] = s2[nt] = 0.f;
+    if (bnb) bl[nt].load(p.bnst, p.N, min(col, p.N - 1));
   }
   f32x16 acc[NT];
   const int nitems = (t1 - t0) * nch;
@@ -315,6 +347,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
       // row = pixel (r&3) + 8(r>>2) + 4h of the wave's 32, column = channel n0 + 32 nt + j
       int img0, oy0, ox0;
       origin(tile, img0, oy0, ox0);
+      float yb[16][NT];
+      if (bnb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int qi, qy, qx;
+          tile_pixel<S, NI, TH, TW, NW>(wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, qi, qy, qx);
+          const int oy = oy0 + qy, ox = ox0 + qx, img = img0 + qi;
+          const bool ok = img < p.NF && oy < p.OH && ox < p.OW;
+          const int64_t base = ok ? (((int64_t)img * p.OH + oy) * p.OW + ox) * p.N : 0;
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) yb[r][nt] = BnBwdLane::ld<AB>(p.bny, base + min(n0 + nt * 32 + j, p.N - 1));
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         int qi, qy, qx;
@@ -330,6 +375,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
               if (FWD) {
                 s1[nt] += v;
                 s2[nt] = fmaf(v, v, s2[nt]);
+              } else if (bnb) {
+                bl[nt].template add<AB>(yb[r][nt], v, s1[nt], s2[nt]);
               }
             }
           }
@@ -337,7 +384,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
       }
     }
   }
-  if (FWD && p.partials) {
+  if ((FWD || bnb) && p.partials) {
     __syncthreads();
     float* red = reinterpret_cast<float*>(sm);  // [NW waves][2][NC]
 #pragma unroll
@@ -348,6 +395,268 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
         red[(wave * 2 + 0) * NC + nt * 32 + lane] = a1;
         red[(wave * 2 + 1) * NC + nt * 32 + lane] = a2;
       }
+    }
+    __syncthreads();
+    for (int q = tid; q < 2 * NC; q += NTHR) {
+      const int which = q / NC, c = q % NC;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += red[(2 * w + which) * NC + c];  // fixed order
+      float* dst = p.parts_cm ? p.partials + (int64_t)(which * p.N + n0 + c) * gridDim.x + blockIdx.x
+                              : p.partials + (int64_t)blockIdx.x * 2 * p.N + which * p.N + n0 + c;
+      if (n0 + c < p.N) *dst = v;
+    }
+  }
+}
+
+// Software-pipelined stride-1 variant (knob "conv_split_pipe"): 32 output channels per block, two LDS patch images
+// (and two weight-slice images when the slice is restaged per item), ONE barrier per item.  While the waves multiply
+// item k out of image k & 1, they stage item k+1 -- loaded into registers one item earlier -- into the other image,
+// the staging pieces (BN+ReLU on load, the three-way split, the LDS stores) placed between the taps' MFMAs so the
+// VALU work issues in the matrix cores' shadow instead of in a phase of its own; item k+2's global loads are issued at
+// the top of item k (two register sets, the item loop unrolled by two so both stay in registers).  The BN scale /
+// shift of every input channel sits in LDS (staged once).  WCH > 1: the whole split weight image is resident, staged
+// before the loop.  Same numerics as conv3x3_x3_kernel (the same products per K step in the same fp32 accumulation
+// order per output: identical y; the BN partial sums follow this kernel's own block decomposition).
+template <int NI, int TH, int TW, int PC, bool FWD, int NP, int WCH, int NW, bool AB = false>
+__global__ __launch_bounds__(64 * NW, 1) void conv3x3_x3p_kernel(const X3Args p) {
+  static_assert(NP == 3 || NP == 1, "three split planes (fp32 numerics) or one (bf16 operands)");
+  static_assert(!AB || NP == 1, "bf16 storage with bf16 operands only");
+  using TA = act_t<AB>;
+  const TA* src = reinterpret_cast<const TA*>(p.src);
+  TA* out = reinterpret_cast<TA*>(p.out);
+  static_assert(NI * TH * TW == 32 * NW, "a wave owns 32 output pixels");
+  constexpr int S = 1, NTHR = 64 * NW, NC = 32, G8 = PC / 8;
+  constexpr int PH = TH + 2, PW = TW + 2, PROWS = NI * PH * PW;
+  constexpr int RP = NP * PC + 8, WCS = 9 * NP * PC, WP = WCH * WCS + 8;
+  static_assert(((RP * 2 / 16) & 1) && ((WP * 2 / 16) & 1), "odd 16-B row pitch");
+  constexpr int WB = WCH > 1 ? 1 : 2;  // weight images: resident, or double-buffered per-item slices
+  constexpr int PSZ = PROWS * RP, WSZ = NC * WP, CMAX = 256;
+  __shared__ __attribute__((aligned(16))) __bf16 sm[2 * PSZ + WB * WSZ];
+  __shared__ __attribute__((aligned(16))) float bnl[2 * CMAX];  // [scale | shift] of every input channel
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, j = lane & 31;
+  const int tiles_per_img = p.tiles_h * p.tiles_w;
+  const int n0 = blockIdx.y * NC;
+  const int t0 = blockIdx.x * p.tpb, t1 = min(p.ntiles, t0 + p.tpb);
+  const int nch = p.C / PC;
+  const int nitems = (t1 - t0) * nch;
+  if (nitems <= 0) return;  // (block-uniform)
+  constexpr bool wper = WCH == 1;  // weight slice restaged for every item (the launcher routes nch == 1 elsewhere)
+  const bool bn = FWD && p.scale;
+
+  int mi, py, px;
+  tile_pixel<S, NI, TH, TW, NW>(wave * 32 + j, mi, py, px);
+  const int arow0 = (mi * PH + py) * PW + px;
+
+  constexpr int PQ = PROWS * G8, PIT = (PQ + NTHR - 1) / NTHR;
+  constexpr int WQ = NC * 9 * G8, WIT = (WQ + NTHR - 1) / NTHR;
+  const int g8 = tid % G8;
+  struct Regs {
+    act_raw4<AB> pv[PIT][2];
+    bool pok[PIT];
+    f32x4 wv[WIT][2];
+    bool wok[WIT];
+  };
+  Regs R0, R1;
+  auto origin = [&](int tile, int& img0, int& oy0, int& ox0) {
+    img0 = (tile / tiles_per_img) * NI;
+    const int tr = tile % tiles_per_img;
+    oy0 = (tr / p.tiles_w) * TH;
+    ox0 = (tr % p.tiles_w) * TW;
+  };
+  auto fetch_w = [&](Regs& R, int ch) {
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      // (threads past the slice redo its last item: same loads, same LDS bytes -- no divergent branch in the stash)
+      const int q = min(tid + it * NTHR, WQ - 1);
+      const int n = q / (9 * G8), t = (q / G8) % 9;
+      R.wok[it] = n0 + n < p.N;
+      const float* s = p.w + ch * PC + g8 * 8 + (R.wok[it] ? ((int64_t)(n0 + n) * 9 + (FWD ? t : 8 - t)) * p.C : (int64_t)0);
+      R.wv[it][0] = *reinterpret_cast<const f32x4*>(s);
+      R.wv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
+    }
+  };
+  auto fetch = [&](Regs& R, int item) {
+    const int tile = t0 + item / nch, ch = item % nch;
+    int img0, oy0, ox0;
+    origin(tile, img0, oy0, ox0);
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = min(tid + it * NTHR, PQ - 1);  // (past the patch: the last item again, see fetch_w)
+      const int row = q / G8;
+      const int im = row / (PH * PW), rr = row % (PH * PW);
+      const int iy = oy0 - 1 + rr / PW, ix = ox0 - 1 + rr % PW;
+      R.pok[it] = img0 + im < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
+      const TA* s = src + ch * PC + g8 * 8 + (R.pok[it] ? (((int64_t)(img0 + im) * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
+      R.pv[it][0] = act_ld4(s);
+      R.pv[it][1] = act_ld4(s + 4);
+    }
+    if (wper) fetch_w(R, ch);
+  };
+  // staging pieces: patch piece `it` of item -> image b; weight piece `it` -> weight image b (segment seg)
+  auto stash_p = [&](const Regs& R, int it, int item, __bf16* pimg) {
+    const int q = min(tid + it * NTHR, PQ - 1);
+    {
+      const int row = q / G8;
+      const int c0 = (item % nch) * PC + g8 * 8;
+      float v[8];
+      const f32x4 v0 = act_f4(R.pv[it][0]), v1 = act_f4(R.pv[it][1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = R.pok[it] ? v0[e] : 0.f;
+        v[4 + e] = R.pok[it] ? v1[e] : 0.f;
+      }
+      if constexpr (FWD) {
+        // zero padding stays zero: padded taps read 0 in the reference's zero-padded relu(bn(y))
+        const bool app = bn && R.pok[it];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float a = relu_nan(fmaf(v[e], bnl[c0 + e], bnl[CMAX + c0 + e]));
+          v[e] = app ? a : v[e];
+        }
+      }
+      put_planes<NP>(pimg + row * RP + g8 * 8, PC, v, false);
+    }
+  };
+  auto stash_w = [&](const Regs& R, int it, __bf16* wimg, int seg) {
+    const int q = min(tid + it * NTHR, WQ - 1);
+    {
+      const int n = q / (9 * G8), t = (q / G8) % 9;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = R.wok[it] ? R.wv[it][0][e] : 0.f;
+        v[4 + e] = R.wok[it] ? R.wv[it][1][e] : 0.f;
+      }
+      put_planes<NP>(wimg + n * WP + seg * WCS + t * NP * PC + g8 * 8, PC, v, false);
+    }
+  };
+  __bf16* const pimg0 = sm;
+  __bf16* const pimg1 = sm + PSZ;
+  __bf16* const wimg0 = sm + 2 * PSZ;
+  __bf16* const wimg1 = sm + 2 * PSZ + (WB - 1) * WSZ;
+
+  // prologue: BN constants of every input channel, resident weights, item 0 staged, item 1 in flight
+  if (bn)
+    for (int c = tid; c < p.C; c += NTHR) {
+      bnl[c] = p.scale[c];
+      bnl[CMAX + c] = p.shift[c];
+    }
+  if (!wper) {
+    for (int c = 0; c < (WCH > 1 ? WCH : 1); ++c) {
+      fetch_w(R0, c);
+#pragma unroll
+      for (int it = 0; it < WIT; ++it) stash_w(R0, it, wimg0, WCH > 1 ? c : 0);
+    }
+  }
+  fetch(R0, 0);
+  __syncthreads();  // bnl
+#pragma unroll
+  for (int it = 0; it < PIT; ++it) stash_p(R0, it, 0, pimg0);
+  if (wper) {
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) stash_w(R0, it, wimg0, 0);
+  }
+  fetch(R1, min(1, nitems - 1));
+  __syncthreads();
+
+  float bj = 0.f, s1 = 0.f, s2 = 0.f;
+  if (FWD && n0 + j < p.N) bj = p.bias[n0 + j];
+  BnBwdLane bl;
+  const bool bnb = !FWD && p.bny;
+  if (bnb) bl.load(p.bnst, p.N, min(n0 + j, p.N - 1));
+  f32x16 acc;
+
+  auto step = [&](auto curc, int k) {
+    constexpr int cur = decltype(curc)::value;
+    Regs& Rn = cur ? R0 : R1;  // item k+1, loaded one item ago
+    Regs& Rf = cur ? R1 : R0;  // item k was staged out of it: item k+2's loads go here
+    __bf16* const pc = cur ? pimg1 : pimg0;
+    __bf16* const pn = cur ? pimg0 : pimg1;
+    __bf16* const wc = (WB == 2 && cur) ? wimg1 : wimg0;
+    __bf16* const wn = (WB == 2 && !cur) ? wimg1 : wimg0;
+    // unconditional (item indices clamped): the staging of a nonexistent next item rewrites the idle image with
+    // copies of the last one, so no branch splits the tap loop and the staging can interleave with the MFMAs
+    fetch(Rf, min(k + 2, nitems - 1));
+    const int ch = k % nch;
+    const int wseg = WCH > 1 ? ch * WCS : 0;
+    if (ch == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    }
+    const __bf16* bbase = wc + j * WP + 8 * h + wseg;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int kh = t / 3, kw = t % 3;
+      const __bf16* ap = pc + (arow0 + kh * PW + kw) * RP + 8 * h;
+#pragma unroll
+      for (int kk = 0; kk < PC / 16; ++kk) {
+        bf16x8 a[NP], b[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) a[q] = *reinterpret_cast<const bf16x8*>(ap + q * PC + kk * 16);
+#pragma unroll
+        for (int q = 0; q < NP; ++q) b[q] = *reinterpret_cast<const bf16x8*>(bbase + (t * NP + q) * PC + kk * 16);
+        if constexpr (NP == 3) acc = mfma_x3(a, b, acc);
+        else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+      }
+      // the next item's staging, spread over the taps: patch pieces after taps 0, 4 (, 8), weight pieces after 2, 6
+      if ((t & 3) == 0 && t / 4 < PIT) stash_p(Rn, t / 4, min(k + 1, nitems - 1), pn);
+      if constexpr (wper)
+        if ((t & 3) == 2 && t / 4 < WIT) stash_w(Rn, t / 4, wn, 0);
+    }
+    // pieces beyond the tap slots (PIT > 3 or WIT > 2)
+#pragma unroll
+    for (int it = 3; it < PIT; ++it) stash_p(Rn, it, min(k + 1, nitems - 1), pn);
+    if constexpr (wper) {
+#pragma unroll
+      for (int it = 2; it < WIT; ++it) stash_w(Rn, it, wn, 0);
+    }
+    if (ch == nch - 1) {
+      int img0, oy0, ox0;
+      origin(t0 + k / nch, img0, oy0, ox0);
+      float yb[16];
+      if (bnb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int qi, qy, qx;
+          tile_pixel<S, NI, TH, TW, NW>(wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, qi, qy, qx);
+          const int oy = oy0 + qy, ox = ox0 + qx, img = img0 + qi;
+          const bool ok = img < p.NF && oy < p.OH && ox < p.OW;
+          yb[r] = BnBwdLane::ld<AB>(p.bny, (ok ? (((int64_t)img * p.OH + oy) * p.OW + ox) * p.N : 0) + min(n0 + j, p.N - 1));
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int qi, qy, qx;
+        tile_pixel<S, NI, TH, TW, NW>(wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, qi, qy, qx);
+        const int oy = oy0 + qy, ox = ox0 + qx, img = img0 + qi;
+        if (img < p.NF && oy < p.OH && ox < p.OW && n0 + j < p.N) {
+          const float v = acc[r] + bj;
+          const int64_t oi = (((int64_t)img * p.OH + oy) * p.OW + ox) * p.N + n0 + j;
+          act_st(out + oi, v);
+          if (FWD) {
+            s1 += v;
+            s2 = fmaf(v, v, s2);
+          } else if (bnb) {
+            bl.template add<AB>(yb[r], v, s1, s2);
+          }
+        }
+      }
+    }
+    __syncthreads();  // image cur read, image cur^1 written: the next item multiplies out of it
+  };
+  for (int k = 0; k < nitems; k += 2) {
+    step(std::integral_constant<int, 0>{}, k);
+    if (k + 1 < nitems) step(std::integral_constant<int, 1>{}, k + 1);
+  }
+  if ((FWD || bnb) && p.partials) {
+    float* red = reinterpret_cast<float*>(sm);  // [NW waves][2][32]
+    const float a1 = s1 + __shfl_xor(s1, 32, 64);
+    const float a2 = s2 + __shfl_xor(s2, 32, 64);
+    if (lane < 32) {
+      red[(wave * 2 + 0) * NC + lane] = a1;
+      red[(wave * 2 + 1) * NC + lane] = a2;
     }
     __syncthreads();
     for (int q = tid; q < 2 * NC; q += NTHR) {
@@ -411,6 +720,49 @@ static int launch_x3(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   return launch_np<S, NI, TH, TW, NT, PC, FWD, 3, 1, NW>(a, max_blocks, st, nparts);
 }
 
+// knob "conv_split_pipe": stride-1 layers on the software-pipelined kernel (conv3x3_x3p_kernel); bit 0 forwards, bit 1
+// input gradients (these share the CUs with the weight gradients, which a 132 KB block leaves no LDS for)
+int g_x3_pipe = 1;
+
+template <int NI, int TH, int TW, bool FWD, int NP, int WCH>
+static int launch_pipe(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
+  constexpr int PC = 16, NW = 8;
+  VAD_CHECK(!g_act_bf16 || NP == 1, "conv3x3_x3p: bf16 activations need the bf16-operand kernels (conv_bf16)");
+  VAD_CHECK(a.C % PC == 0 && a.C <= 256 && (WCH == 1 ? a.C > PC : a.C == WCH * PC), "conv3x3_x3p: channel count");
+  a.tiles_h = (int)cdiv(a.OH, TH);
+  a.tiles_w = (int)cdiv(a.OW, TW);
+  a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);
+  const int ny = (int)cdiv(a.N, 32);
+  // one 512-thread block per CU (two patch images + weights: 98-132 KB of LDS)
+  const int target = std::max(1, std::min(max_blocks, (FWD ? 256 : g_x3_dgrad_blocks / 2) / ny));
+  a.tpb = (int)cdiv(a.ntiles, target);
+  const int gx = (int)cdiv(a.ntiles, a.tpb);
+  if (NP == 1 && g_act_bf16)
+    VAD_KLAUNCH((conv3x3_x3p_kernel<NI, TH, TW, PC, FWD, NP, WCH, NW, NP == 1>), dim3(gx, ny), dim3(64 * NW), 0, st, a);
+  else
+    VAD_KLAUNCH((conv3x3_x3p_kernel<NI, TH, TW, PC, FWD, NP, WCH, NW>), dim3(gx, ny), dim3(64 * NW), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  if (nparts) *nparts = gx;
+  return 0;
+}
+
+template <int NI, int TH, int TW, bool FWD>
+static int dispatch_pipe_np(const X3Args& a, int max_blocks, hipStream_t st, int* nparts) {
+  const bool wres = g_x3_wres && a.C == 32;
+  if (g_conv_bf16)
+    return wres ? launch_pipe<NI, TH, TW, FWD, 1, 2>(a, max_blocks, st, nparts)
+                : launch_pipe<NI, TH, TW, FWD, 1, 1>(a, max_blocks, st, nparts);
+  return wres ? launch_pipe<NI, TH, TW, FWD, 3, 2>(a, max_blocks, st, nparts)
+              : launch_pipe<NI, TH, TW, FWD, 3, 1>(a, max_blocks, st, nparts);
+}
+
+template <bool FWD>
+static int dispatch_pipe(const X3Args& a, int max_blocks, hipStream_t st, int* nparts) {
+  if (a.OH <= 8 && a.OW <= 8) return dispatch_pipe_np<4, 8, 8, FWD>(a, max_blocks, st, nparts);
+  if (a.OW <= 16) return dispatch_pipe_np<2, 8, 16, FWD>(a, max_blocks, st, nparts);
+  return dispatch_pipe_np<1, 8, 32, FWD>(a, max_blocks, st, nparts);
+}
+
 int g_x3_big = 1;  // knob "conv_split_big": stride-1 layers on 256-pixel tiles, 512-thread blocks (NW = 8)
 int g_x3_s2big = 1;  // knob "conv_split_s2big": fp32 stride-2 forwards on 256-pixel tiles, 8 waves, 32 channels
 
@@ -448,6 +800,12 @@ static int dispatch_x3(const X3Args& a, int max_blocks, hipStream_t st, int* npa
     const int64_t tiles = conv3_patch_blocks(a.NF, a.OH, a.OW);
     // (stride 2: the 4x larger input patch per tile makes sharing it over 64 channels pay even on a small grid)
     nt = (a.N % 64 == 0 && (S == 2 || tiles * (a.N / 64) >= 512)) ? 2 : 1;
+  }
+  if constexpr (S == 1) {
+    // 32-channel blocks: the pipelined kernel (measured: L0/L1 -1..-3 us, L7 -5 us; on the layers that take 64
+    // channels per block it would lose the patch sharing, +10 us each: profiles/r03_pipe_ab.json)
+    if ((g_x3_pipe & (FWD ? 1 : 2)) && nt == 1 && a.C <= 256 && a.C > 16 && g_x3_big && !g_conv_bf16)
+      return dispatch_pipe<FWD>(a, max_blocks, st, nparts);
   }
   return nt == 2 ? dispatch_x3_nt<S, FWD, 2>(a, max_blocks, st, nparts)
                  : dispatch_x3_nt<S, FWD, 1>(a, max_blocks, st, nparts);
@@ -510,13 +868,25 @@ int conv3d_x3_fwd(int B, int D, int H, int W, int C, int N, const float* src, co
   return nt2 ? launch_x3_3d<1, 8, 32, 2>(a, st) : launch_x3_3d<1, 8, 32, 1>(a, st);
 }
 
-int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st) {
+int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,
+                   const BnBwdFuse* f) {
   VAD_CHECK(conv3_x3_supported(L, false), "conv3_x3_dgrad: unsupported layer");
   X3Args a{};
   a.src = dY;
   a.w = wd;
   a.out = dX;
   a.NF = L.NF; a.IH = L.OH; a.IW = L.OW; a.C = L.Co; a.OH = L.IH; a.OW = L.IW; a.N = L.Ci;
+  if (f) {
+    // (grid bounded by the partial buffer: [2 Ci][blocks])
+    const int mb = (int)std::min<int64_t>(512, f->cap / (2ll * L.Ci));
+    if (mb >= 64) {
+      a.bny = f->y;
+      a.bnst = f->stats;
+      a.partials = f->parts;
+      a.parts_cm = 1;
+      return dispatch_x3<1, false>(a, mb, st, f->nparts);
+    }
+  }
   return dispatch_x3<1, false>(a, 1 << 20, st, nullptr);
 }
 
@@ -661,17 +1031,62 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args
   }
   const int ph0 = wave < 2 ? 1 : 0, pw0 = 1;  // acc0 class: (1,1) or (0,1)
   const int ph1 = wave < 2 ? 0 : 1, pw1 = 0;  // acc1 class: (0,0) or (1,0)
+  float s1[NT], s2[NT];
+  BnBwdLane bl[NT];
+  const bool bnb = p.bny != nullptr;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int pm = (r & 3) + 8 * (r >> 2) + 4 * h;
-    const int ca = i0 + 4 * g + pm / 8, cb = j0 + pm % 8;
-    const int y0 = 2 * ca + ph0, x0 = 2 * cb + pw0, y1 = 2 * ca + ph1, x1 = 2 * cb + pw1;
+  for (int nt = 0; nt < NT; ++nt) {
+    s1[nt] = s2[nt] = 0.f;
+    if (bnb) bl[nt].load(p.bnst, p.N, min(n0 + nt * 32 + j, p.N - 1));
+  }
+  // (two passes, one per parity class: the y values of a pass are loaded first, one wait instead of one per pixel)
+#pragma unroll
+  for (int cls = 0; cls < 2; ++cls) {
+    const int ph = cls ? ph1 : ph0, pw = cls ? pw1 : pw0;
+    float yb[16][NT];
+    if (bnb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int pm = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int yy = 2 * (i0 + 4 * g + pm / 8) + ph, xx = 2 * (j0 + pm % 8) + pw;
+        const bool ok = yy < p.OH && xx < p.OW;
+        const int64_t base = ok ? (((int64_t)img * p.OH + yy) * p.OW + xx) * p.N : 0;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) yb[r][nt] = BnBwdLane::ld<AB>(p.bny, base + min(n0 + nt * 32 + j, p.N - 1));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int pm = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int yy = 2 * (i0 + 4 * g + pm / 8) + ph, xx = 2 * (j0 + pm % 8) + pw;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int col = n0 + nt * 32 + j;
+        if (col >= p.N || yy >= p.OH || xx >= p.OW) continue;
+        const float v = cls ? acc1[nt][r] : acc0[nt][r];
+        act_st(out + (((int64_t)img * p.OH + yy) * p.OW + xx) * p.N + col, v);
+        if (bnb) bl[nt].template add<AB>(yb[r][nt], v, s1[nt], s2[nt]);
+      }
+    }
+  }
+  if (bnb && p.partials) {  // per-block sums, fixed order: lane halves, then the 4 waves
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(sm);  // [4 waves][2][NC]
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const int col = n0 + nt * 32 + j;
-      if (col >= p.N) continue;
-      if (y0 < p.OH && x0 < p.OW) act_st(out + (((int64_t)img * p.OH + y0) * p.OW + x0) * p.N + col, acc0[nt][r]);
-      if (y1 < p.OH && x1 < p.OW) act_st(out + (((int64_t)img * p.OH + y1) * p.OW + x1) * p.N + col, acc1[nt][r]);
+      const float a1 = s1[nt] + __shfl_xor(s1[nt], 32, 64);
+      const float a2 = s2[nt] + __shfl_xor(s2[nt], 32, 64);
+      if (lane < 32) {
+        red[(wave * 2 + 0) * NC + nt * 32 + lane] = a1;
+        red[(wave * 2 + 1) * NC + nt * 32 + lane] = a2;
+      }
+    }
+    __syncthreads();
+    for (int q = tid; q < 2 * NC; q += 256) {
+      const int which = q / NC, c = q % NC;
+      const float v = (red[(0 + which) * NC + c] + red[(2 + which) * NC + c]) +
+                      (red[(4 + which) * NC + c] + red[(6 + which) * NC + c]);
+      if (n0 + c < p.N) p.partials[(int64_t)(which * p.N + n0 + c) * gridDim.x + blockIdx.x] = v;
     }
   }
 }
@@ -683,12 +1098,20 @@ bool conv3_x3_dgrad_s2_supported(const Conv3Layer& L) {
          L.OH == (L.IH - 1) / 2 + 1 && L.OW == (L.IW - 1) / 2 + 1;
 }
 
-int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st) {
+int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,
+                      const BnBwdFuse* f) {
   VAD_CHECK(conv3_x3_dgrad_s2_supported(L), "conv3_x3_dgrad_s2: unsupported layer");
   X3Args a{};
   a.src = dY;
   a.w = wd;
   a.out = dX;
+  const int tiles0 = L.NF * (int)cdiv((L.IH + 1) / 2, 8) * (int)cdiv((L.IW + 1) / 2, 8);
+  if (f && f->cap < 2ll * L.Ci * tiles0) f = nullptr;  // (partial buffer too small: the caller runs the separate pass)
+  if (f) {
+    a.bny = f->y;
+    a.bnst = f->stats;
+    a.partials = f->parts;
+  }
   a.NF = L.NF; a.IH = L.OH; a.IW = L.OW; a.C = L.Co; a.OH = L.IH; a.OW = L.IW; a.N = L.Ci;
   a.tiles_h = (int)cdiv((L.IH + 1) / 2, 8);
   a.tiles_w = (int)cdiv((L.IW + 1) / 2, 8);
@@ -697,6 +1120,7 @@ int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, flo
   const bool nt2 = L.Ci % 64 == 0 && (int64_t)tiles * (L.Ci / 64) >= 512;
   dim3 grid((unsigned)tiles, (unsigned)(L.Ci / (nt2 ? 64 : 32)));
   VAD_CHECK(!g_act_bf16 || g_conv_bf16, "conv3_x3_dgrad_s2: bf16 activations need conv_bf16");
+  if (f) *f->nparts = tiles;
   if (g_conv_bf16 && g_act_bf16) {
     if (nt2) VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<2, 16, 1, true>), grid, dim3(256), 0, st, a);
     else VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<1, 16, 1, true>), grid, dim3(256), 0, st, a);
