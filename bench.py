@@ -193,7 +193,7 @@ def run_gpu(args, rank, world, local_rank):
     with contextlib.redirect_stdout(io.StringIO()):
         apply_memory_efficient_training(model)
     model = model.to(dev)
-    trainer = CadTrainer(model, lr=3e-4, seed=1234,
+    trainer = CadTrainer(model, lr=3e-4, seed=1234, prio_stream=args.prio_stream,
                          compute_dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32,
                          sync_bn=args.sync_bn)
     B, T, H, W = args.batch, args.T, args.H, args.W
@@ -721,6 +721,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--prof-every", type=int, default=4, help="instrument every k-th timed step (roofline events)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--prio-stream", type=int, default=0, help="cad step on a high-priority stream (CadTrainer)")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="nccl (= RCCL over xGMI) for measurement; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--breakdown-out", default=None, help="write the per-kernel breakdown JSON here")

@@ -19,6 +19,7 @@ int g_cad_wgrad_stream = 1;  // knob "cad_wgrad_stream": backbone weight gradien
 // knob "bn_bwd_fuse": the BN-backward reduce in the input gradients' epilogues -- bit 0 the stride-1 kernels, bit 1 the
 // stride-2 one (A/B at config 2: both 1.922 -> 1.893 ms, stride-1 only 1.927 -> 1.922, profiles/r03_bnfuse_ab.json)
 int g_bn_bwd_fuse = 3;
+int g_cad_stream_prio = 0;  // knob "cad_stream_prio" (cad_plan.hip streams())
 int g_cad_l0_slab = 1;  // knob "cad_l0_slab": layer 0's weight gradient on a split-K slab of its own (no wait for layer 1's)
                              // reduce of layers 0-6, bit 2 the causal head's kernels
 
@@ -1006,6 +1007,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "mlp_tail_rb") g_mlp_tail_rb = value;
   else if (k == "cad_last_wgrad_main") g_cad_last_wgrad_main = value;
   else if (k == "cad_l0_slab") g_cad_l0_slab = value;
+  else if (k == "cad_stream_prio") g_cad_stream_prio = value;
   else if (k == "conv_split_pipe") g_x3_pipe = value;
   else if (k == "bn_bwd_fuse") g_bn_bwd_fuse = value;
   else if (k == "head_dbg") g_head_dbg = value;

@@ -395,11 +395,15 @@ struct CadPlanImpl {
       // agent-scope release suffices, so the system-scope fence at each record is dropped (knob
       // "cad_event_sysfence" = 1 restores it)
       const unsigned evf = hipEventDisableTiming | (g_cad_event_sysfence ? 0u : (unsigned)hipEventDisableSystemFence);
-      VAD_HIP(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
+      // knob "cad_stream_prio": the side stream (the detector / causal-head chain, on the forward's critical path) at
+      // the device's greatest priority, the weight-gradient stream (slack beside the input gradients) at its least
+      int lo = 0, hi = 0;
+      if (g_cad_stream_prio) VAD_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      VAD_HIP(hipStreamCreateWithPriority(&st2, hipStreamNonBlocking, g_cad_stream_prio ? hi : 0));
       VAD_HIP(hipEventCreateWithFlags(&ev_fork, evf));
       VAD_HIP(hipEventCreateWithFlags(&ev_join, evf));
       VAD_HIP(hipEventCreateWithFlags(&ev_det, evf));
-      VAD_HIP(hipStreamCreateWithFlags(&st3, hipStreamNonBlocking));
+      VAD_HIP(hipStreamCreateWithPriority(&st3, hipStreamNonBlocking, g_cad_stream_prio ? lo : 0));
       for (int b = 0; b < 2; ++b) {
         VAD_HIP(hipEventCreateWithFlags(&ev_dy[b], evf));
         VAD_HIP(hipEventCreateWithFlags(&ev_wg[b], evf));

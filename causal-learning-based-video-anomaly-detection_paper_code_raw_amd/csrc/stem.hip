@@ -143,9 +143,10 @@ __global__ __launch_bounds__(256, 4) void stem_fused_kernel(const float* __restr
   stem_weights(w, b);
   {
     StemRegs<ST_SLOTS> sr;
-    if (!(dbg & 2)) stem_fetch(x + (int64_t)img * H * W, H, W, c_lo, rows, PWb, sr);
-    else
-      for (int k = 0; k < ST_SLOTS; ++k) sr.v[k][0] = sr.v[k][1] = 0.f;
+    stem_fetch(x + (int64_t)img * H * W, H, W, c_lo, rows, PWb, sr);
+    // every input load is issued before the first is consumed: left to itself the scheduler interleaved the split
+    // and LDS stores of early slots with the loads of later ones, waiting on the memory system a dozen times
+    __builtin_amdgcn_sched_barrier(0);
     stem_store<NP>(sr, rows, PWb, xs);
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
@@ -240,8 +241,7 @@ __global__ __launch_bounds__(256, 4) void stem_fused_kernel(const float* __restr
 }  // namespace
 
 int g_stem_fused = 1;  // tuning knob "stem_fused": the frozen stem's forward without the conv1 activation
-// knob "stem_dbg" (measurement only, results wrong with any bit): 1 no MFMA, 2 no input loads, 8 no pooled-map
-// stores
+// knob "stem_dbg" (measurement only, results wrong with any bit): 1 no MFMA, 8 no pooled-map stores
 int g_stem_dbg = 0;
 
 static int stem_pitch(int OW) { return (int)cdiv(2 * OW + 6, 8) * 8; }

@@ -42,9 +42,13 @@ class CadTrainer:
     """
 
     def __init__(self, model, lr=3e-4, weight_decay=1e-5, eps=1e-8, betas=(0.9, 0.999), max_norm=1.0, seed=0,
-                 process_group=None, engine=None, compute_dtype=None, sync_bn=False, force_dist=False):
+                 process_group=None, engine=None, compute_dtype=None, sync_bn=False, force_dist=False,
+                 prio_stream=False):
         """force_dist: run the data-parallel protocol (broadcasts, bucketed all-reduces, SyncBN callback) even at
-        world size 1 of an initialised process group -- exercises the collective path on one device (tests)."""
+        world size 1 of an initialised process group -- exercises the collective path on one device (tests).
+        prio_stream: run each step on a stream of the device's greatest priority (ordered after and before the
+        caller's stream), so with the plan's low-priority weight-gradient stream (knob cad_stream_prio) the dispatcher
+        prefers the critical path's workgroups."""
         self.model = model
         if compute_dtype is not None:
             model.set_compute_dtype(compute_dtype)
@@ -66,6 +70,9 @@ class CadTrainer:
         i1 = next(i for i in range(i0, len(names)) if not names[i].startswith("detector."))
         self.det_range = (self.eng.slot_offset[i0], self.eng.slot_offset[i1])
         self.allreduce_floats = 0  # floats all-reduced by the last step (per rank, before the ring's 2(P-1)/P factor)
+        self.prio_stream = None
+        if prio_stream and self.eng.grads.is_cuda:
+            self.prio_stream = torch.cuda.Stream(self.eng.device, priority=-1)
         if self.dist:
             dist.broadcast(self.eng.params, 0, group=process_group)
             dist.broadcast(self.eng.bufs, 0, group=process_group)
@@ -79,6 +86,18 @@ class CadTrainer:
     def step(self, videos, labels, lr=None, want_outputs=False):
         """One training step; returns the (device) loss vector [cls, anomaly, causal, kl, total] (want_outputs: the
         forward's output dict, see CadEngine.forward)."""
+        if self.prio_stream is not None and self.eng.grads.is_cuda:
+            # the step's critical path on a stream of the device's greatest priority (the plan's weight-gradient stream
+            # runs at its least with knob cad_stream_prio), ordered after / before the caller's stream
+            caller = torch.cuda.current_stream(self.eng.device)
+            self.prio_stream.wait_stream(caller)
+            with torch.cuda.stream(self.prio_stream):
+                o = self._step(videos, labels, lr, want_outputs)
+            caller.wait_stream(self.prio_stream)
+            return o
+        return self._step(videos, labels, lr, want_outputs)
+
+    def _step(self, videos, labels, lr, want_outputs):
         eng = self.eng
         B = videos.shape[0]
         if self.dist and not self.sync_bn:
