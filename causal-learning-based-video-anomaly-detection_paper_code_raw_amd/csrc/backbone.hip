@@ -19,7 +19,7 @@ int g_cad_wgrad_stream = 1;  // knob "cad_wgrad_stream": backbone weight gradien
 // knob "bn_bwd_fuse": the BN-backward reduce in the input gradients' epilogues -- bit 0 the stride-1 kernels, bit 1 the
 // stride-2 one (A/B at config 2: both 1.922 -> 1.893 ms, stride-1 only 1.927 -> 1.922, profiles/r03_bnfuse_ab.json)
 int g_bn_bwd_fuse = 3;
-int g_cad_stream_prio = 0;  // knob "cad_stream_prio" (cad_plan.hip streams())
+int g_cad_stream_prio = 1;  // knob "cad_stream_prio" (cad_plan.hip streams(); A/B profiles/r03_prio_ab.json)
 int g_cad_l0_slab = 1;  // knob "cad_l0_slab": layer 0's weight gradient on a split-K slab of its own (no wait for layer 1's)
                              // reduce of layers 0-6, bit 2 the causal head's kernels
 
