@@ -196,7 +196,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
       const int q = tid + it * NTHR;
       const int row = q / G8;
       const int im = row / (PH * PW), rr = row % (PH * PW);
-      const int iy = oy0 * S - 1 + rr / PW, ix = ox0 * S - 1 + rr % PW;
+      // (stride 2: staging items run in the stored, parity-split column order, see stash)
+      const int sc = rr % PW, rx = S == 1 ? sc : (sc < PWE ? 2 * sc : 2 * (sc - PWE) + 1);
+      const int iy = oy0 * S - 1 + rr / PW, ix = ox0 * S - 1 + rx;
       int img = img0 + im;
       bool dok = true;
       if constexpr (KD == 3) {  // depth slice d + kd - 1 of the same clip
@@ -245,7 +247,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
       if (q < PQ) {
         const int row = q / G8;
         const int im = row / (PH * PW), rr = row % (PH * PW);
-        const int ry = rr / PW, rx = rr % PW;
+        const int ry = rr / PW;
         float v[8];
         const f32x4 v0 = act_f4(pv[it][0]), v1 = act_f4(pv[it][1]);
 #pragma unroll
@@ -264,7 +266,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
             v[4 + e] = app ? a1 : v[4 + e];
           }
         }
-        const int col = S == 1 ? rx : ((rx & 1) ? PWE + (rx >> 1) : (rx >> 1));
+        // stride 2: item rr % PW is already the stored column ([even input columns | odd ones]), so the 8 rows a
+        // 16-lane ds_write_b128 phase covers are consecutive patch rows -- distinct bank quads at the odd 16-B pitch
+        // (raw column order alternated between the two halves: SQ_LDS_BANK_CONFLICT 0.43-0.52 of the LDS cycles)
+        const int col = rr % PW;
         __bf16* d = patch + ((im * PH + ry) * PW + col) * RP + g8 * 8;
         put_planes<NP>(d, PC, v, false);
       }
