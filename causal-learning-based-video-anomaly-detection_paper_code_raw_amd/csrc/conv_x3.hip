@@ -175,7 +175,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
   // staging: thread tid always handles the channel group g8 = tid % G8 (NTHR % G8 == 0)
   constexpr int PQ = PROWS * G8, PIT = (PQ + NTHR - 1) / NTHR;
   constexpr int WQ = NC * 9 * G8, WIT = (WQ + NTHR - 1) / NTHR;
-  const int g8 = tid % G8;
+  const int g8 = tid % G8;  // weight staging: channel group of item q = q % G8
+  // patch staging: item q -> (row, channel group) with the group above the 16 low bits, so a 16-lane ds_write_b128
+  // phase covers 16 consecutive patch rows of one group -- distinct bank quads at the odd 16-B row pitch (q / G8,
+  // q % G8 put 8 rows x 2 groups in a phase: two lanes on one quad in every phase)
+  const int g8p = G8 == 2 ? (tid >> 4) & 1 : g8;
+  auto prow = [](int q) { return G8 == 2 ? ((q >> 5) << 4) + (q & 15) : q / G8; };
   act_raw4<AB> pv[PIT][2];
   f32x4 wv[WIT][2];
   // prefetch loads are unconditional (out-of-range lanes read a valid dummy address) and the zero padding is applied
@@ -194,7 +199,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
       const int q = tid + it * NTHR;
-      const int row = q / G8;
+      const int row = prow(q);
       const int im = row / (PH * PW), rr = row % (PH * PW);
       // (stride 2: staging items run in the stored, parity-split column order, see stash)
       const int sc = rr % PW, rx = S == 1 ? sc : (sc < PWE ? 2 * sc : 2 * (sc - PWE) + 1);
@@ -206,8 +211,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
         dok = d >= 0 && d < p.D;
         img += kd - 1;
       }
-      pok[it] = q < PQ && dok && img0 + im < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
-      const TA* s = src + c0 + g8 * 8 + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
+      pok[it] = row < PROWS && dok && img0 + im < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
+      const TA* s = src + c0 + g8p * 8 + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
       pv[it][0] = act_ld4(s);
       pv[it][1] = act_ld4(s + 4);
     }
@@ -236,16 +241,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
     if constexpr (FWD) {
       const float* scp = bn ? p.scale : p.w;
       const float* shp = bn ? p.shift : p.w;
-      sc[0] = *reinterpret_cast<const f32x4*>(scp + c0 + g8 * 8);
-      sc[1] = *reinterpret_cast<const f32x4*>(scp + c0 + g8 * 8 + 4);
-      sh[0] = *reinterpret_cast<const f32x4*>(shp + c0 + g8 * 8);
-      sh[1] = *reinterpret_cast<const f32x4*>(shp + c0 + g8 * 8 + 4);
+      sc[0] = *reinterpret_cast<const f32x4*>(scp + c0 + g8p * 8);
+      sc[1] = *reinterpret_cast<const f32x4*>(scp + c0 + g8p * 8 + 4);
+      sh[0] = *reinterpret_cast<const f32x4*>(shp + c0 + g8p * 8);
+      sh[1] = *reinterpret_cast<const f32x4*>(shp + c0 + g8p * 8 + 4);
     }
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
       const int q = tid + it * NTHR;
-      if (q < PQ) {
-        const int row = q / G8;
+      const int row = prow(q);
+      if (row < PROWS) {
         const int im = row / (PH * PW), rr = row % (PH * PW);
         const int ry = rr / PW;
         float v[8];
@@ -270,7 +275,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
         // 16-lane ds_write_b128 phase covers are consecutive patch rows -- distinct bank quads at the odd 16-B pitch
         // (raw column order alternated between the two halves: SQ_LDS_BANK_CONFLICT 0.43-0.52 of the LDS cycles)
         const int col = rr % PW;
-        __bf16* d = patch + ((im * PH + ry) * PW + col) * RP + g8 * 8;
+        __bf16* d = patch + ((im * PH + ry) * PW + col) * RP + g8p * 8;
         put_planes<NP>(d, PC, v, false);
       }
     }
@@ -456,7 +461,10 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_x3p_kernel(const X3Args p)
 
   constexpr int PQ = PROWS * G8, PIT = (PQ + NTHR - 1) / NTHR;
   constexpr int WQ = NC * 9 * G8, WIT = (WQ + NTHR - 1) / NTHR;
-  const int g8 = tid % G8;
+  const int g8 = tid % G8;  // weight staging
+  // patch staging: 16 consecutive rows of one channel group per 16-lane write phase (see conv3x3_x3_kernel)
+  const int g8p = G8 == 2 ? (tid >> 4) & 1 : g8;
+  auto prow = [](int q) { return G8 == 2 ? ((q >> 5) << 4) + (q & 15) : q / G8; };
   struct Regs {
     act_raw4<AB> pv[PIT][2];
     bool pok[PIT];
@@ -488,12 +496,11 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_x3p_kernel(const X3Args p)
     origin(tile, img0, oy0, ox0);
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
-      const int q = min(tid + it * NTHR, PQ - 1);  // (past the patch: the last item again, see fetch_w)
-      const int row = q / G8;
+      const int row = min(prow(tid + it * NTHR), PROWS - 1);  // (past the patch: the last row again, see fetch_w)
       const int im = row / (PH * PW), rr = row % (PH * PW);
       const int iy = oy0 - 1 + rr / PW, ix = ox0 - 1 + rr % PW;
       R.pok[it] = img0 + im < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
-      const TA* s = src + ch * PC + g8 * 8 + (R.pok[it] ? (((int64_t)(img0 + im) * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
+      const TA* s = src + ch * PC + g8p * 8 + (R.pok[it] ? (((int64_t)(img0 + im) * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
       R.pv[it][0] = act_ld4(s);
       R.pv[it][1] = act_ld4(s + 4);
     }
@@ -501,10 +508,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_x3p_kernel(const X3Args p)
   };
   // staging pieces: patch piece `it` of item -> image b; weight piece `it` -> weight image b (segment seg)
   auto stash_p = [&](const Regs& R, int it, int item, __bf16* pimg) {
-    const int q = min(tid + it * NTHR, PQ - 1);
     {
-      const int row = q / G8;
-      const int c0 = (item % nch) * PC + g8 * 8;
+      const int row = min(prow(tid + it * NTHR), PROWS - 1);
+      const int c0 = (item % nch) * PC + g8p * 8;
       float v[8];
       const f32x4 v0 = act_f4(R.pv[it][0]), v1 = act_f4(R.pv[it][1]);
 #pragma unroll
@@ -521,7 +527,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_x3p_kernel(const X3Args p)
           v[e] = app ? a : v[e];
         }
       }
-      put_planes<NP>(pimg + row * RP + g8 * 8, PC, v, false);
+      put_planes<NP>(pimg + row * RP + g8p * 8, PC, v, false);
     }
   };
   auto stash_w = [&](const Regs& R, int it, __bf16* wimg, int seg) {
