@@ -28,7 +28,7 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector == FP32 matrix pea
 PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 # fp32-equivalent peak of a kernel by products per bf16 K step (vad_cad_conv_path): split-bf16 runs six bf16 MFMA
 # products per fp32 product, bf16-operand mode one, the f32 MFMA kernels run at the fp32 peak
-PATH_PEAK = {6: PEAK_BF16_TFLOPS / 6, 1: PEAK_BF16_TFLOPS, 0: PEAK_FP32_TFLOPS}
+PATH_PEAK = {6: PEAK_BF16_TFLOPS / 6, 2: PEAK_BF16_TFLOPS, 1: PEAK_BF16_TFLOPS, 0: PEAK_FP32_TFLOPS}
 PEAK_HBM_GBPS = 8000.0     # MI355X_MICROARCH.md: HBM3E spec peak
 
 
@@ -110,7 +110,7 @@ def family_roofline(fam, live, pl, args, act_bytes):
         ms_tot += ms
         launches += n
         path = nat.lib().vad_cad_conv_path(pl.h, l, kind)
-        paths[lab] = {6: "split-bf16", 1: "bf16", 0: "f32"}.get(path, "?")
+        paths[lab] = {6: "split-bf16", 2: "bf16-native", 1: "bf16-split1", 0: "f32"}.get(path, "?")
         ideal_s += work * n / (PATH_PEAK.get(path, PEAK_FP32_TFLOPS) * 1e12)
     sec = ms_tot * 1e-3
     tf, gbs = flops / sec / 1e12, byts / sec / 1e9

@@ -144,8 +144,26 @@ int conv3_wgrad_x3(const Conv3Layer& L, const float* dY, const float* src, const
 bool conv3_wgrad_patch_supported(const Conv3Layer& L);
 int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
                       int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);
+// native bf16 kernels (conv_bf.hip; bf16 operands AND bf16 activation storage, i.e. config 4): forward and stride-1
+// input gradient.  Their weights are the bf16 copies the prep writes behind the fp32 images (when conv_bf16 and
+// act_bf16 are set), so in that mode a wf / wd buffer holds Co*Ci*9 floats + Co*Ci*9 bf16.
+extern int g_bfc, g_bfc_blocks;  // knobs "conv_bfc", "conv_bfc_blocks"
+bool bfc_supported(const Conv3Layer& L, bool fwd);
+inline const __bf16* conv3_bf16_image(const float* img, const Conv3Layer& L) {
+  return reinterpret_cast<const __bf16*>(img + (int64_t)L.Co * L.Ci * 9);
+}
+int bfc_fwd(const Conv3Layer& L, const __bf16* src, const float* src_stats, const __bf16* wfb, const float* bias,
+            __bf16* y, float* partials, int64_t partial_cap, int* nparts, hipStream_t st);
+int bfc_dgrad(const Conv3Layer& L, const __bf16* dY, const __bf16* wdb, __bf16* dX, hipStream_t st,
+              const BnBwdFuse* f);
+// weight gradient (both strides) into split-K slabs [S][Co][9 Ci] (conv3_wgrad_reduce)
+extern int g_bfw_blocks;  // knob "conv_bfw_blocks"
+bool bfc_wgrad_supported(const Conv3Layer& L);
+int bfc_wgrad(const Conv3Layer& L, const __bf16* dY, const __bf16* src, const float* src_stats, float* slab,
+              int* nsplit, int64_t partial_cap, hipStream_t st);
 // which kernel family conv3_fwd (kind 0) / conv3_dgrad (1) / conv3_wgrad (2) dispatches to for this layer under the
-// current knobs: 6 = split-bf16 (six bf16 products per K step), 1 = bf16 operands, 0 = f32 MFMA kernels
+// current knobs: 6 = split-bf16 (six bf16 products per K step), 2 = native bf16 (conv_bf.hip), 1 = bf16 operands on the
+// split kernels, 0 = f32 MFMA kernels
 int conv3_path(const Conv3Layer& L, int kind);
 // every pass of this layer (forward, input gradient when dgrad, weight gradient) runs on a split kernel under the
 // current knobs, i.e. can take bf16 activations

@@ -1016,6 +1016,10 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_s1_nt_wide") g_wgrad_s1_nt_wide = value;
   else if (k == "conv_wgrad_s1_nt_blocks") g_wgrad_s1_nt_blocks = value;
   else if (k == "conv_bf16") g_conv_bf16 = value;  // ops API only (calling thread); plans use their own option
+  else if (k == "act_bf16") g_act_bf16 = value;    // ops API only: bf16 activation storage for the calling thread
+  else if (k == "conv_bfc") g_bfc = value;
+  else if (k == "conv_bfc_blocks") g_bfc_blocks = value;
+  else if (k == "conv_bfw_blocks") g_bfw_blocks = value;
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else if (k == "conv_wgrad_alone_blocks") g_tune.wgrad_alone_blocks = value;
   else {
@@ -1112,6 +1116,7 @@ struct PrepTab {
   int Ci[8], Co[8], classes[8];
   int64_t end[8];  // inclusive prefix sums of Co*Ci*9
   int n;
+  int bf16;  // also the bf16 copies of the plain images (conv3_bf16_image: behind the fp32 image)
 };
 
 __global__ void conv3_prep_all_kernel(const PrepTab t) {
@@ -1126,6 +1131,11 @@ __global__ void conv3_prep_all_kernel(const PrepTab t) {
     const int co = (int)(i / (9 * Ci));
     const float v = t.w[l][i];
     t.wf[l][((int64_t)co * 9 + tap) * Ci + ci] = v;
+    if (t.bf16) {
+      const int64_t tot = (int64_t)Co * Ci * 9;
+      reinterpret_cast<__bf16*>(t.wf[l] + tot)[((int64_t)co * 9 + tap) * Ci + ci] = (__bf16)v;
+      reinterpret_cast<__bf16*>(t.wd[l] + tot)[((int64_t)ci * 9 + tap) * Co + co] = (__bf16)v;
+    }
     if (!t.classes[l]) {
       t.wd[l][((int64_t)ci * 9 + tap) * Co + co] = v;
     } else {
@@ -1149,6 +1159,7 @@ int conv3_prep_weights_all(int n, const float* const* w, const Conv3Layer* L, fl
   VAD_CHECK(n >= 1 && n <= 8, "conv3_prep_weights_all: 1..8 layers");
   PrepTab t{};
   t.n = n;
+  t.bf16 = g_conv_bf16 && g_act_bf16;
   int64_t acc = 0;
   for (int l = 0; l < n; ++l) {
     t.w[l] = w[l];
@@ -1167,17 +1178,17 @@ int conv3_prep_weights_all(int n, const float* const* w, const Conv3Layer* L, fl
 }
 
 int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd, hipStream_t st) {
-  const int64_t total = (int64_t)L.Co * L.Ci * 9;
-  const int classes = L.stride == 2 && !(g_tune.patch && conv3_patch_supported(L, false));
-  hipLaunchKernelGGL(conv3_prep_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, w, L.Ci, L.Co, classes,
-                     wf, wd);
-  VAD_LAUNCH_CHECK();
-  return 0;
+  return conv3_prep_weights_all(1, &w, &L, &wf, &wd, st);
 }
 
 int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, const float* wf, const float* bias,
               float* y, float* partials, int* nparts, hipStream_t st, int* parts_cm) {
   if (parts_cm) *parts_cm = 0;
+  if (bfc_supported(L, true)) {  // native bf16 kernels (config 4): column-major partials
+    if (parts_cm) *parts_cm = 1;
+    return bfc_fwd(L, reinterpret_cast<const __bf16*>(src), src_stats, conv3_bf16_image(wf, L), bias,
+                   reinterpret_cast<__bf16*>(y), partials, conv3_patch_blocks(L.NF, L.OH, L.OW) * 2 * L.Co, nparts, st);
+  }
   VAD_CHECK(L.Ci % 32 == 0, "conv3_fwd: Ci must be a multiple of 32");
   // (the patch grid may exceed ceil(M/64) BN partial blocks on tiny images: those stay on the GEMM path)
   if (g_tune.patch && conv3_patch_blocks(L.NF, L.OH, L.OW) <= cdiv((int64_t)L.NF * L.OH * L.OW, 64)) {
@@ -1220,6 +1231,9 @@ int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX
   VAD_CHECK(L.Co % 32 == 0, "conv3_dgrad: Co must be a multiple of 32");
   const int N = L.Ci;
   if (f) *f->nparts = 0;
+  if (bfc_supported(L, false))
+    return bfc_dgrad(L, reinterpret_cast<const __bf16*>(dY), conv3_bf16_image(wd, L), reinterpret_cast<__bf16*>(dX), st,
+                     (g_bn_bwd_fuse & 1) ? f : nullptr);
   if (g_tune.patch && conv3_x3_supported(L, false))
     return conv3_x3_dgrad(L, dY, wd, dX, st, (g_bn_bwd_fuse & 1) ? f : nullptr);
   // (the split kernel reads the plain Wd layout, which the prep writes exactly when the f32 patch kernel is usable)
@@ -1260,6 +1274,12 @@ int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX
 }
 
 bool conv3_act_bf16_ok(const Conv3Layer& L, bool dgrad) {
+  {
+    ActStorage abf(1);  // (the native bf16 kernels exist for bf16 storage only)
+    if (bfc_supported(L, true) && (!dgrad || bfc_supported(L, false) || conv3_x3_dgrad_s2_supported(L)) &&
+        (bfc_wgrad_supported(L) || (g_tune.wgrad_patch && conv3_wgrad_x3_supported(L))))
+      return true;
+  }
   const bool fwd = g_tune.patch && conv3_patch_blocks(L.NF, L.OH, L.OW) <= cdiv((int64_t)L.NF * L.OH * L.OW, 64) &&
                    conv3_x3_supported(L, true);
   const bool dg = !dgrad || (g_tune.patch && (conv3_x3_supported(L, false) ||
@@ -1269,8 +1289,11 @@ bool conv3_act_bf16_ok(const Conv3Layer& L, bool dgrad) {
 }
 
 int conv3_path(const Conv3Layer& L, int kind) {
+  if (kind < 2 ? bfc_supported(L, kind == 0) : bfc_wgrad_supported(L)) return 2;
   bool x3 = false;
-  if (kind == 0)
+  if (kind == 1 && L.stride == 2)  // stride-2 input gradients: the parity-class split kernel when supported
+    x3 = g_tune.patch && conv3_patch_supported(L, false) && conv3_x3_dgrad_s2_supported(L);
+  else if (kind == 0)
     x3 = g_tune.patch && conv3_patch_blocks(L.NF, L.OH, L.OW) <= cdiv((int64_t)L.NF * L.OH * L.OW, 64) &&
          conv3_x3_supported(L, true);
   else if (kind == 1)
@@ -1282,6 +1305,9 @@ int conv3_path(const Conv3Layer& L, int kind) {
 
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
                 int* nsplit, int64_t partial_cap, hipStream_t st, bool alone) {
+  if (bfc_wgrad_supported(L))
+    return bfc_wgrad(L, reinterpret_cast<const __bf16*>(dY), reinterpret_cast<const __bf16*>(src), src_stats, partial,
+                     nsplit, partial_cap, st);
   if (g_tune.wgrad_patch && conv3_wgrad_x3_supported(L))
     return conv3_wgrad_x3(L, dY, src, src_stats, partial, nsplit, partial_cap,
                           alone ? g_tune.wgrad_alone_blocks : g_tune.wgrad_patch_blocks, st);

@@ -461,8 +461,9 @@ struct CadPlanImpl {
     act_max = nf * HP * WP * 32;
     for (int l = 0; l < 8; ++l) {
       y[l] = w.take<float>(nf * L[l].OH * L[l].OW * L[l].Co);
-      wf[l] = w.take<float>((int64_t)L[l].Co * L[l].Ci * 9);
-      wd[l] = w.take<float>((int64_t)L[l].Co * L[l].Ci * 9);
+      // (fp32 image + its bf16 copy: conv3_bf16_image)
+      wf[l] = w.take<float>((int64_t)L[l].Co * L[l].Ci * 9 * 3 / 2);
+      wd[l] = w.take<float>((int64_t)L[l].Co * L[l].Ci * 9 * 3 / 2);
       act_max = std::max<int64_t>(act_max, nf * L[l].OH * L[l].OW * L[l].Co);
     }
     const int cs[9] = {32, 32, 32, 64, 64, 128, 128, 256, 256};
@@ -705,7 +706,12 @@ struct CadPlanImpl {
     ConvPrecision prec(conv_bf16);
     x_last = x;
     const CadLayout& LY = layout();
-    // weight relayouts (conv images, the detector's transposed layers) on the side stream, beside the stem
+    y1_fresh = !(g_stem_fused && !stem_grad && stem_fused_ok(W1));
+    act_bf16 = conv_bf16 && act_bf16_opt && !y1_fresh;
+    for (int l = 0; l < 8; ++l) act_bf16 = act_bf16 && conv3_act_bf16_ok(L[l], l > 0);
+    ActStorage abf(act_bf16);
+    // weight relayouts (conv images -- with bf16 storage also their bf16 copies --, the detector's transposed layers)
+    // on the side stream, beside the stem
     VAD_TRY(fork(st));
     {
       hipStream_t st = g_cad_prep_stream ? st2 : st0;
@@ -717,10 +723,6 @@ struct CadPlanImpl {
     }
     int np = 0;
     bwd_state = 0;
-    y1_fresh = !(g_stem_fused && !stem_grad && stem_fused_ok(W1));
-    act_bf16 = conv_bf16 && act_bf16_opt && !y1_fresh;
-    for (int l = 0; l < 8; ++l) act_bf16 = act_bf16 && conv3_act_bf16_ok(L[l], l > 0);
-    ActStorage abf(act_bf16);
     if (!y1_fresh) {
       // frozen stem (the training default): conv1 + BN sums + pooling of the raw output in one pass (stem.hip);
       // `pool` then holds the pooled conv1 output and layer1.0 applies bn1 + ReLU on load

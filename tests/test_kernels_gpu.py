@@ -310,3 +310,72 @@ def test_conv3x3_bf16_mode_matches_rounded_fp64(NF, Ci, Co, IH, IW, s):
         assert float(((dx.cpu().permute(0, 3, 1, 2).double() - rdx).abs() / (mdx + 1e-30)).max()) < 1e-5
     finally:
         nat.lib().vad_set_tuning(b"conv_bf16", 0)
+
+
+# native bf16 kernels (conv_bf.hip: bf16 operands AND bf16 activation storage, BASELINE config 4) -- forward of both
+# strides and the stride-1 input gradient; the stride-2 input gradient and the weight gradient of that mode run the
+# split kernels' bf16 instantiations.  Shapes: the config-4 layer geometries (64/32/16/8-wide maps, every channel
+# pair of the backbone) plus ragged frames smaller than and straddling a tile.
+BF_NATIVE_CASES = [(2, 32, 32, 64, 64, 1), (2, 32, 64, 64, 64, 2), (2, 64, 64, 32, 32, 1), (2, 64, 128, 32, 32, 2),
+                   (2, 128, 128, 16, 16, 1), (3, 128, 256, 16, 16, 2), (5, 256, 256, 8, 8, 1),
+                   (3, 32, 32, 19, 17, 1), (2, 64, 64, 29, 29, 1), (3, 32, 64, 57, 57, 2), (2, 128, 256, 15, 15, 2),
+                   (3, 256, 256, 7, 5, 1), (1, 32, 32, 10, 7, 1), (2, 64, 128, 11, 9, 2)]
+
+
+@pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", BF_NATIVE_CASES)
+def test_conv3x3_bf16_native_matches_rounded_fp64(NF, Ci, Co, IH, IW, s):
+    """Against an fp64 conv of the bf16-rounded operands: the forward and the input gradient are fp32 accumulations
+    rounded once to bf16 on store (|err| <= 2^-8 |ref| + 1e-5 sum|a||b|); the weight gradient (fp32 out) stays at
+    fp32 accumulation level (1e-5 of sum |a||b|)."""
+    nat = _lib()
+    lib = nat.lib()
+    lib.vad_set_tuning(b"conv_bf16", 1)
+    lib.vad_set_tuning(b"act_bf16", 1)
+    try:
+        g = torch.Generator().manual_seed(11 + Ci + IH + s)
+        x = torch.randn(NF, Ci, IH, IW, generator=g).bfloat16()
+        w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
+        bias = torch.randn(Co, generator=g) * 0.1
+        xd, wb = x.double(), _bf16(w)
+        ref = F.conv2d(xd, wb, bias.double(), stride=s, padding=1)
+        mag = F.conv2d(xd.abs(), wb.abs(), None, stride=s, padding=1)
+        OH, OW = ref.shape[2:]
+        d = torch.device("cuda")
+        xh = x.permute(0, 2, 3, 1).contiguous().to(d)
+        wdev, bd = w.contiguous().to(d), bias.to(d)
+        y = torch.full((NF, OH, OW, Co), float("nan"), device=d, dtype=torch.bfloat16)
+        wf = torch.empty(2 * 9 * Ci * Co, device=d)  # fp32 image + its bf16 copy
+        wd = torch.empty(2 * 9 * Ci * Co, device=d)
+        parts = torch.empty((NF * OH * OW // 64 + 2) * 2 * Co, device=d)
+        st = nat.stream_of(d)
+        nat.check(lib.vad_conv3x3_forward(xh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), bd.data_ptr(), Co, s,
+                                          y.data_ptr(), wf.data_ptr(), wd.data_ptr(), parts.data_ptr(), st))
+        torch.cuda.synchronize()
+        yc = y.cpu().permute(0, 3, 1, 2).double()
+        assert torch.isfinite(yc).all()
+        bad = (yc - ref).abs() > 2.0 ** -8 * ref.abs() + 1e-5 * mag
+        assert not bool(bad.any()), f"forward: {int(bad.sum())} elements outside the bf16 bound"
+        dy = torch.randn(NF, Co, OH, OW, generator=g).bfloat16()
+        dyd = dy.double()
+        dyh = dy.permute(0, 2, 3, 1).contiguous().to(d)
+        dx = torch.full((NF, IH, IW, Ci), float("nan"), device=d, dtype=torch.bfloat16)
+        nat.check(lib.vad_conv3x3_dgrad(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, s, dx.data_ptr(),
+                                        wf.data_ptr(), wd.data_ptr(), st))
+        torch.cuda.synchronize()
+        rdx = torch.nn.grad.conv2d_input(x.shape, wb, dyd, stride=s, padding=1)
+        mdx = torch.nn.grad.conv2d_input(x.shape, wb.abs(), dyd.abs(), stride=s, padding=1)
+        dxc = dx.cpu().permute(0, 3, 1, 2).double()
+        assert torch.isfinite(dxc).all()
+        bad = (dxc - rdx).abs() > 2.0 ** -8 * rdx.abs() + 1e-5 * mdx
+        assert not bool(bad.any()), f"input gradient: {int(bad.sum())} elements outside the bf16 bound"
+        dW = torch.empty(Co, Ci, 3, 3, device=d)
+        part = torch.empty(1 << 24, device=d)
+        nat.check(lib.vad_conv3x3_wgrad(xh.data_ptr(), dyh.data_ptr(), NF, Ci, IH, IW, Co, s, dW.data_ptr(),
+                                        part.data_ptr(), part.numel(), st))
+        torch.cuda.synchronize()
+        rdw = torch.nn.grad.conv2d_weight(xd, w.shape, dyd, stride=s, padding=1)
+        mdw = torch.nn.grad.conv2d_weight(xd.abs(), w.shape, dyd.abs(), stride=s, padding=1)
+        assert float(((dW.cpu().double() - rdw).abs() / (mdw + 1e-30)).max()) < 1e-5
+    finally:
+        lib.vad_set_tuning(b"act_bf16", 0)
+        lib.vad_set_tuning(b"conv_bf16", 0)
