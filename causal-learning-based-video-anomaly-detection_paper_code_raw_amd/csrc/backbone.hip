@@ -1010,8 +1010,6 @@ int set_tuning(const char* key, int value) {
   else if (k == "cad_stream_prio") g_cad_stream_prio = value;
   else if (k == "conv_split_pipe") g_x3_pipe = value;
   else if (k == "bn_bwd_fuse") g_bn_bwd_fuse = value;
-  else if (k == "head_dbg") g_head_dbg = value;
-  else if (k == "stem_dbg") g_stem_dbg = value;
   else if (k == "conv_wgrad_s1_nt") g_wgrad_s1_nt = value;
   else if (k == "conv_wgrad_s1_nt_wide") g_wgrad_s1_nt_wide = value;
   else if (k == "conv_wgrad_s1_nt_blocks") g_wgrad_s1_nt_blocks = value;

@@ -454,9 +454,18 @@ struct CadPlanImpl {
   uint64_t seed = 0, step = 0;
   const int64_t* labels = nullptr;
 
+  // workspace carved for the options set before vad_cad_workspace_bytes: the training stem's buffers (y1, stem_d:
+  // 0.2-0.5 GB at configs 2/4) only when the stem trains or the fused frozen stem cannot run, and either the per-layer
+  // dY buffers or the shared pair.  A forward / backward needing a buffer the carve left out fails loudly (the Python
+  // engine builds a new plan when the stem's requires_grad turns on).
+  int ws_stem = 1, ws_dy_shared = 1, bound = 0;
+  void carve_options() {
+    ws_stem = stem_grad || !g_stem_fused || !stem_fused_ok(W1);
+    ws_dy_shared = !(dy_per_layer && g_cad_dy_per_layer);
+  }
   void carve(Ws& w) {
     const int64_t nf = NF;
-    y1 = w.take<float>(nf * H1 * W1 * 32);
+    y1 = ws_stem ? w.take<float>(nf * H1 * W1 * 32) : nullptr;
     pool = w.take<float>(nf * HP * WP * 32);
     act_max = nf * HP * WP * 32;
     for (int l = 0; l < 8; ++l) {
@@ -522,10 +531,10 @@ struct CadPlanImpl {
     dense_scratch = w.take<float>(dense_scratch_floats);
     dense_scratch2 = w.take<float>(dense_scratch_floats);  // the side stream's (detector) split-K scratch
     dA = w.take<float>(act_max);
-    dY = w.take<float>(act_max);
-    dY2 = w.take<float>(act_max);
-    for (int l = 0; l < 8; ++l) dYL[l] = w.take<float>(nf * L[l].OH * L[l].OW * L[l].Co);
-    stem_d = w.take<float>(nf * H1 * W1 * 32);
+    dY = ws_dy_shared ? w.take<float>(act_max) : nullptr;
+    dY2 = ws_dy_shared ? w.take<float>(act_max) : nullptr;
+    for (int l = 0; l < 8; ++l) dYL[l] = ws_dy_shared ? nullptr : w.take<float>(nf * L[l].OH * L[l].OW * L[l].Co);
+    stem_d = ws_stem ? w.take<float>(nf * H1 * W1 * 32) : nullptr;
     wpart_floats = 16ll << 20;
     wpart = w.take<float>(wpart_floats);
     wpart0_floats = std::max<int64_t>(8ll << 20, (int64_t)L[0].Co * 9 * L[0].Ci);
@@ -564,7 +573,6 @@ struct CadPlanImpl {
     a.iws_stride = head_iws_ints(T);
     a.rows = head_rows;
     a.grad = grads;
-    a.dbg = g_head_dbg;
     return a;
   }
   HeadOut head_out() const { return HeadOut{causal, kl, z, adj, boxes, counts, nmax, clip_flags}; }
@@ -590,7 +598,6 @@ struct CadPlanImpl {
       L.dscale = a.dscale;
       m.WT[i] = i >= 1 ? wtr[i] : nullptr;
     }
-    m.dbg = g_head_dbg;
     return m;
   }
   MlpTransposeArgs mlp_transpose_args() const {
@@ -707,6 +714,8 @@ struct CadPlanImpl {
     x_last = x;
     const CadLayout& LY = layout();
     y1_fresh = !(g_stem_fused && !stem_grad && stem_fused_ok(W1));
+    VAD_CHECK(!y1_fresh || y1, "forward: the workspace was carved without the training stem's buffers (option stem_grad "
+                               "or knob stem_fused changed after vad_cad_bind): create a new plan");
     act_bf16 = conv_bf16 && act_bf16_opt && !y1_fresh;
     for (int l = 0; l < 8; ++l) act_bf16 = act_bf16 && conv3_act_bf16_ok(L[l], l > 0);
     ActStorage abf(act_bf16);
@@ -788,7 +797,6 @@ struct CadPlanImpl {
         da.gs0 = gs0;
         da.gs1 = gs1;
         da.dl2 = dl2; da.d3 = dg2[3]; da.d2 = dg2[2]; da.d1 = dg2[1]; da.d0 = dg2[0];
-        da.dbg = g_head_dbg;
         TIMED("dir_fwd", dir_mid(da, st));
         TIMED("dir_pre", dense_dgrad(dg2[0], 2 * B, 512, P(LY.dir_w[0]), 6144, dpool2, nullptr, 1.f, nullptr, st));
         dir_pre = tail_pre = 1;
@@ -961,6 +969,7 @@ struct CadPlanImpl {
       int np = fused_np, nb = 0;
       const bool perl = dy_per_layer != 0 && g_cad_dy_per_layer != 0;
       float* dYl = perl ? dYL[l] : ((l & 1) ? dY2 : dY);
+      VAD_CHECK(dYl != nullptr, "backward: dY buffers carved for the other dy_per_layer setting: create a new plan");
       VAD_CHECK((int64_t)bn_rows_parts((int)M, C) * 2 * C <= parts_floats, "backward: BN partial buffer too small");
       if (np == 0) TIMED(L_("bn_bwd_reduce", l), bn_bwd_reduce(dA, y[l], stats[l + 1], (int)M, C, parts, &np, st, 1));
       VAD_TRY(bn_bwd_stats(l + 1, np, C, (double)M, P(LY.bn_w[l]), G(LY.bn_w[l]), G(LY.bn_b[l]), G(LY.conv_b[l]), st));
@@ -1174,9 +1183,6 @@ int vad_cad_create(int B, int T, int H, int W, vad_cad_plan** out) {
     w = ow;
   }
   c.HF = h; c.WF = w;
-  Ws ws;
-  c.carve(ws);
-  c.ws_bytes = ws.off + 256;
   const CadLayout& LY = layout();
   p->chunk_host.assign(LY.param_floats / 256 + 1, (int16_t)-1);
   for (int i = 0; i < (int)LY.slots.size(); ++i) {
@@ -1189,17 +1195,29 @@ int vad_cad_create(int B, int T, int H, int W, vad_cad_plan** out) {
 
 void vad_cad_destroy(vad_cad_plan* plan) { delete plan; }
 
-int64_t vad_cad_workspace_bytes(const vad_cad_plan* plan) { return plan ? plan->impl.ws_bytes : -1; }
+int64_t vad_cad_workspace_bytes(const vad_cad_plan* plan) {
+  if (!plan) return -1;
+  CadPlanImpl& c = const_cast<vad_cad_plan*>(plan)->impl;
+  if (!c.bound) {  // sized for the options set so far (carve_options); fixed once bound
+    c.carve_options();
+    Ws ws;
+    c.carve(ws);
+    c.ws_bytes = ws.off + 256;
+  }
+  return c.ws_bytes;
+}
 
 int vad_cad_bind(vad_cad_plan* plan, void* workspace, float* params, float* grads, float* bufs, int64_t* nbt,
                  float* exp_avg, float* exp_avg_sq, int32_t* steps) {
   VAD_CHECK(plan && workspace && params && bufs, "vad_cad_bind: null argument");
   VAD_CHECK((reinterpret_cast<uintptr_t>(workspace) & 255) == 0, "vad_cad_bind: workspace must be 256-B aligned");
   CadPlanImpl& c = plan->impl;
+  if (!c.bound) vad_cad_workspace_bytes(plan);  // (fixes the carve options)
   Ws ws;
   ws.base = reinterpret_cast<char*>(workspace);
   ws.dry = false;
   c.carve(ws);
+  c.bound = 1;
   c.params = params; c.grads = grads; c.bufs = bufs; c.nbt = nbt;
   c.m = exp_avg; c.v = exp_avg_sq; c.steps = steps;
   VAD_HIP(hipMemcpy(c.chunk_slot, plan->chunk_host.data(), plan->chunk_host.size() * sizeof(int16_t),
@@ -1325,6 +1343,7 @@ int vad_cad_debug_buffer(vad_cad_plan* plan, const char* name, int idx, void** p
   else if (n == "det_logits") { *ptr = c.dlog; *nfloats = NF * 20; }
   else if (n == "bn_sync") { *ptr = c.bnsync; *nfloats = 2 * 2 * 256; }  // double [2*256]: 1024 float words
   else { vad::set_error("vad_cad_debug_buffer: unknown buffer " + n); return 1; }
+  VAD_CHECK(*ptr != nullptr || n == "act_bf16", "vad_cad_debug_buffer: " + n + " is not carved under this plan's options");
   return 0;
 }
 

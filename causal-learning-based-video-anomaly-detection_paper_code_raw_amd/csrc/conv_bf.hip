@@ -532,13 +532,219 @@ __global__ __launch_bounds__(256, 2) void bfc_wgrad_kernel(const BfwArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------------------------------
+// Stride-2 input gradient: dX[y][x] = sum over the taps with (y + 1 - kh) and (x + 1 - kw) even of
+// dY[(y + 1 - kh) / 2][(x + 1 - kw) / 2] W[kh][kw].  The four parity classes (ph, pw) of dX are small convolutions
+// of dY with 1x1, 1x2, 2x1 and 2x2 taps (ph = 0: kh = 1 at dY row yc; ph = 1: kh = 0 at row yc + 1, kh = 2 at row
+// yc) -- 9 taps in all, like one stride-1 tile.  A block owns an 8 x 16 tile of the class grid and all four classes:
+// the classes share one staged 9 x 17 dY patch and the 9-tap weight slice, wave w takes class-grid rows 2w, 2w + 1
+// (32 class pixels) of every class (four accumulators).  The epilogue writes the four classes' rows to LDS and
+// stores 16-B pieces at dX rows (2 yc + ph, 2 xc + pw), with the fused BN-backward reduce as in bfc_conv_kernel.
+template <int CB>
+__global__ __launch_bounds__(256, 2) void bfc_dgrad_s2_kernel(const BfcArgs p) {
+  constexpr int NTHR = 256, TH = 8, TW = 16, TPX = TH * TW, NC = 32, G8 = CB / 8, NG = NC / 8;
+  constexpr int PH = TH + 1, PW = TW + 1, PROWS = PH * PW;
+  constexpr int RP = CB + 8, WP = 9 * CB + 8, EP = NC + 8;
+  static_assert(((RP / 8) & 1) && ((WP / 8) & 1) && ((EP / 8) & 1), "odd 16-B row pitches");
+  constexpr int PE = PROWS * RP > 4 * TPX * EP ? PROWS * RP : 4 * TPX * EP;
+  __shared__ __attribute__((aligned(16))) __bf16 sm[PE + NC * WP];
+  __bf16* const patch = sm;
+  __bf16* const wl = sm + PE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, j = lane & 31;
+  const int tiles_per_img = p.tiles_h * p.tiles_w;
+  const int n0 = blockIdx.y * NC;
+  const int t0 = blockIdx.x * p.tpb, t1 = min(p.ntiles, t0 + p.tpb);
+  const int nch = p.C / CB;
+  const int nitems = (t1 - t0) * nch;
+  // this lane's class pixel (row j of the wave's 32): patch row of offset (0, 0)
+  const int arow = (2 * wave + j / TW) * PW + j % TW;
+
+  constexpr int PQ = PROWS * G8, PIT = (PQ + NTHR - 1) / NTHR;
+  constexpr int WQ = NC * 9 * G8, WIT = (WQ + NTHR - 1) / NTHR;
+  const int g8 = tid % G8;
+  u32v4 pv[PIT], wv[WIT];
+  bool pok[PIT];
+  auto origin = [&](int tile, int& img, int& yc0, int& xc0) {
+    img = tile / tiles_per_img;
+    const int tr = tile % tiles_per_img;
+    yc0 = (tr / p.tiles_w) * TH;
+    xc0 = (tr % p.tiles_w) * TW;
+  };
+  auto fetch = [&](int tile, int ch, bool wts) {
+    int img, yc0, xc0;
+    origin(tile, img, yc0, xc0);
+    const int c0 = ch * CB + g8 * 8;
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = tid + it * NTHR;
+      const int row = min(q / G8, PROWS - 1);
+      const int iy = yc0 + row / PW, ix = xc0 + row % PW;
+      pok[it] = q < PQ && iy < p.IH && ix < p.IW;
+      pv[it] = *reinterpret_cast<const u32v4*>(p.src + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : 0) + c0);
+    }
+    if (wts) {
+#pragma unroll
+      for (int it = 0; it < WIT; ++it) {
+        const int q = min(tid + it * NTHR, WQ - 1);
+        const int n = q / (9 * G8), t = (q / G8) % 9;
+        wv[it] = *reinterpret_cast<const u32v4*>(p.w + ((int64_t)(n0 + n) * 9 + t) * p.C + c0);
+      }
+    }
+  };
+  auto stash = [&](bool wts) {
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = tid + it * NTHR;
+      if (q < PQ)
+        *reinterpret_cast<u32v4*>(patch + (q / G8) * RP + g8 * 8) = pok[it] ? pv[it] : u32v4{0u, 0u, 0u, 0u};
+    }
+    if (wts) {
+#pragma unroll
+      for (int it = 0; it < WIT; ++it) {
+        const int q = tid + it * NTHR;
+        if (q < WQ) *reinterpret_cast<u32v4*>(wl + (q / (9 * G8)) * WP + ((q / G8) % 9) * CB + g8 * 8) = wv[it];
+      }
+    }
+  };
+
+  const int cg = tid % NG;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+  f32x16 acc[4];
+  if (nitems > 0) fetch(t0, 0, true);
+  for (int item = 0; item < nitems; ++item) {
+    const int tile = t0 + item / nch, ch = item % nch;
+    __syncthreads();
+    stash(nch > 1 || item == 0);
+    __syncthreads();
+    if (item + 1 < nitems) fetch(t0 + (item + 1) / nch, (item + 1) % nch, nch > 1);
+    if (ch == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int ph = c >> 1, pw = c & 1;
+#pragma unroll
+      for (int a = 0; a < (ph ? 2 : 1); ++a) {
+        const int kh = ph ? 2 * a : 1, dr = ph ? 1 - a : 0;
+#pragma unroll
+        for (int b = 0; b < (pw ? 2 : 1); ++b) {
+          const int kw = pw ? 2 * b : 1, dc = pw ? 1 - b : 0;
+#pragma unroll
+          for (int kk = 0; kk < CB / 16; ++kk) {
+            const bfv8 bw = *reinterpret_cast<const bfv8*>(wl + j * WP + (kh * 3 + kw) * CB + kk * 16 + 8 * h);
+            const bfv8 av = *reinterpret_cast<const bfv8*>(patch + (arow + dr * PW + dc) * RP + kk * 16 + 8 * h);
+            acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bw, acc[c], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (ch == nch - 1) {
+      __syncthreads();  // every wave is done reading the patch
+      __bf16* epi = patch;  // [class][pixel][channel]
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          epi[(c * TPX + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * EP + j] = (__bf16)acc[c][r];
+      __syncthreads();
+      int img, yc0, xc0;
+      origin(tile, img, yc0, xc0);
+      float bsc[8], bsh[8], bmean[8], binv[8];
+      if (p.bny) {
+        const int c = min(n0 + cg * 8, p.N - 8);
+#pragma unroll
+        for (int e = 0; e < 8; e += 4) {
+          const f32x4 m4 = *reinterpret_cast<const f32x4*>(p.bnst + c + e);
+          const f32x4 i4 = *reinterpret_cast<const f32x4*>(p.bnst + p.N + c + e);
+          const f32x4 a4 = *reinterpret_cast<const f32x4*>(p.bnst + 2 * p.N + c + e);
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(p.bnst + 3 * p.N + c + e);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            bmean[e + u] = m4[u];
+            binv[e + u] = i4[u];
+            bsc[e + u] = a4[u];
+            bsh[e + u] = b4[u];
+          }
+        }
+      }
+      constexpr int EQ = 4 * TPX * NG, EIT = EQ / NTHR, EB = 2;
+      static_assert(EQ % NTHR == 0 && EIT % EB == 0, "whole epilogue passes");
+#pragma unroll
+      for (int i0 = 0; i0 < EIT; i0 += EB) {
+        u32v4 ev[EB], yv[EB];
+        int64_t oi[EB];
+        bool ok[EB];
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+          const int q = tid + (i0 + u) * NTHR;
+          const int cm = q / NG, c = cm / TPX, m = cm % TPX;
+          const int yy = 2 * (yc0 + m / TW) + (c >> 1), xx = 2 * (xc0 + m % TW) + (c & 1);
+          ok[u] = yy < p.OH && xx < p.OW;
+          oi[u] = ok[u] ? (((int64_t)img * p.OH + yy) * p.OW + xx) * p.N + n0 + cg * 8 : 0;
+          ev[u] = *reinterpret_cast<const u32v4*>(epi + cm * EP + cg * 8);
+          if (p.bny) yv[u] = *reinterpret_cast<const u32v4*>(p.bny + oi[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+          if (!ok[u]) continue;
+          *reinterpret_cast<u32v4*>(p.out + oi[u]) = ev[u];
+          if (p.bny) {
+            float f[8], yy[8];
+            bf8_to_f32(ev[u], f);
+            bf8_to_f32(yv[u], yy);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float dz = fmaf(yy[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
+              s1[e] += dz;
+              s2[e] = fmaf(dz, (yy[e] - bmean[e]) * binv[e], s2[e]);
+            }
+          }
+        }
+      }
+    }
+  }
+  if (p.bny && p.partials) {
+#pragma unroll
+    for (int o = NG; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(sm);  // [4 waves][2][NC]
+    if (lane < NG) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wave * 2 + 0) * NC + lane * 8 + e] = s1[e];
+        red[(wave * 2 + 1) * NC + lane * 8 + e] = s2[e];
+      }
+    }
+    __syncthreads();
+    for (int q = tid; q < 2 * NC; q += NTHR) {
+      const int which = q / NC, c = q % NC;
+      const float v = (red[(0 + which) * NC + c] + red[(2 + which) * NC + c]) +
+                      (red[(4 + which) * NC + c] + red[(6 + which) * NC + c]);
+      p.partials[(int64_t)(which * p.N + n0 + c) * gridDim.x + blockIdx.x] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
 // host side
 int g_bfc = 1;             // knob "conv_bfc": config-4 forwards / stride-1 input gradients on these kernels
 int g_bfc_blocks = 512;    // knob "conv_bfc_blocks": target grid (persistent blocks over the tiles)
 
 bool bfc_supported(const Conv3Layer& L, bool fwd) {
   if (!g_bfc || !g_conv_bf16 || !g_act_bf16) return false;
-  if (L.stride != 1 && !(fwd && L.stride == 2)) return false;
+  if (L.stride != 1 && L.stride != 2) return false;
+  if (!fwd && L.stride == 2)  // the parity-class kernel: dX exactly 2x the dY grid (padding 1)
+    return L.Co % 16 == 0 && L.Ci % 32 == 0 && L.OH == (L.IH - 1) / 2 + 1 && L.OW == (L.IW - 1) / 2 + 1;
   const int C = fwd ? L.Ci : L.Co, N = fwd ? L.Co : L.Ci;
   return C % 16 == 0 && N % 32 == 0;
 }
@@ -623,6 +829,21 @@ int bfc_dgrad(const Conv3Layer& L, const __bf16* dY, const __bf16* wdb, __bf16* 
     a.bnst = f->stats;
     a.partials = f->parts;
     mb = std::max<int64_t>(1, f->cap / (2ll * L.Ci));
+  }
+  if (L.stride == 2) {
+    constexpr int TH = 8, TW = 16;
+    a.tiles_h = (int)cdiv((L.IH + 1) / 2, TH);
+    a.tiles_w = (int)cdiv((L.IW + 1) / 2, TW);
+    a.ntiles = L.NF * a.tiles_h * a.tiles_w;
+    const int ny = L.Ci / 32;
+    const int64_t target = std::max<int64_t>(1, std::min<int64_t>(mb, cdiv(g_bfc_blocks, ny)));
+    a.tpb = (int)cdiv(a.ntiles, target);
+    const int gx = (int)cdiv(a.ntiles, a.tpb);
+    if (L.Co % 32 == 0) VAD_KLAUNCH(bfc_dgrad_s2_kernel<32>, dim3(gx, ny), dim3(256), 0, st, a);
+    else VAD_KLAUNCH(bfc_dgrad_s2_kernel<16>, dim3(gx, ny), dim3(256), 0, st, a);
+    VAD_LAUNCH_CHECK();
+    if (f) *f->nparts = gx;
+    return 0;
   }
   return bfc_dispatch<false>(a, 1, mb, st, f ? f->nparts : nullptr);
 }

@@ -39,9 +39,7 @@ struct HeadArgs {
   int64_t iws_stride;
   float* rows;            // per-trajectory-row arrays, R = B*T*NMAX rows (see RowLayout in head.hip)
   float* grad;            // flat grad buffer (GRU / ReID weight grads are written here directly)
-  int dbg;                // measurement only (knob "head_dbg"): 1 = print per-phase clock counts of block 0
 };
-extern int g_head_dbg;
 
 constexpr int HW_LDS = 20480;  // capacity (floats) of the sequence kernels' LDS weight image
 // sets lw_len from a.off and the last slot's size; nonzero if the image does not fit or a slot is not 16-B aligned

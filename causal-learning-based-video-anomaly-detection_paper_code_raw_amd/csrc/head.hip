@@ -399,8 +399,6 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
   float* w = sw;
   __shared__ int s_N, s_any;
   __shared__ float s_red[4];
-  long long clk[6];
-  clk[0] = __builtin_readcyclecounter();
   const float* Whh = PW(H_GRU_WHH);
   // the n-gate rows of W_hh in LDS (the r / z rows live in registers, below)
   block_copy4<6>(whh, Whh + 2 * GH * GH, GH * GH / 4, [](int i) { return (i >> 4) * (WHH_LD / 4) + (i & 15); });
@@ -511,11 +509,9 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
     }
   }
   __syncthreads();  // W_hh is dead: its LDS now takes the MLP weight image
-  clk[1] = __builtin_readcyclecounter();
   stage_head_weights(a, sW);
   for (int i = tid; i < NMAX * GH; i += HT) w[L.hT + i] = hs[i];
   __syncthreads();
-  clk[2] = __builtin_readcyclecounter();
   // encoder + VAE (cad:299, 333-352)
   lin_fwd(w + L.hT, GH, N, GH, PL(H_ENC_W), PL(H_ENC_B), 32, w + L.enc, 32, false);
   lin_fwd(w + L.enc, 32, N, 32, PL(H_CE0_W), PL(H_CE0_B), 32, w + L.ce1, 32, true);
@@ -544,7 +540,6 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
     s = wave_sum(s);
     if (tid == 0) s_red[0] = s / (float)N;
   }
-  clk[3] = __builtin_readcyclecounter();
   // structure learner (cad:371-398)
   lin_fwd(w + L.zz, NF_, N, NF_, PL(H_NODE_W), PL(H_NODE_B), 32, w + L.node, 32, false);
   const int m = min(N, NF_);
@@ -589,7 +584,6 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
   lin_fwd(w + L.s, NF_, N, NF_, PL(H_DYN0_W), PL(H_DYN0_B), 32, w + L.d1, 32, true);
   lin_fwd(w + L.d1, 32, N, 32, PL(H_DYN2_W), PL(H_DYN2_B), 32, w + L.d2, 32, true);
   lin_fwd(w + L.d2, 32, N, 32, PL(H_DYN4_W), PL(H_DYN4_B), NF_, w + L.pred, NF_, false);
-  clk[4] = __builtin_readcyclecounter();
   // scorer (cad:463-502)
   float* cin = w + L.cin;
   if (tid < NF_) {
@@ -643,10 +637,6 @@ __global__ __launch_bounds__(HT) void head_seq_fwd_kernel(HeadArgs a, HeadOut o)
   __syncthreads();
   // hand the activations to the backward kernel
   block_copy4<3>(wg, sw, HL_HANDOFF / 4, Ident{});
-  clk[5] = __builtin_readcyclecounter();
-  if (a.dbg && b == 0 && tid == 0)
-    printf("head_seq_fwd cycles: gru %lld, stage %lld, enc+vae %lld, struct+dyn %lld, scorer+out %lld\n",
-           clk[1] - clk[0], clk[2] - clk[1], clk[3] - clk[2], clk[4] - clk[3], clk[5] - clk[4]);
 }
 
 int head_rows_fwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, hipStream_t st) {
@@ -665,7 +655,6 @@ int head_fwd(const HeadArgs& a, const float* det_logits, const HeadOut& o, hipSt
   return head_seq_fwd(a, o, st);
 }
 
-int g_head_dbg = 0;
 
 // ================================================================== backward
 #define GW(slot) (g + (a.off[slot] - a.head_begin))

@@ -23,7 +23,6 @@ struct MlpTailArgs {
   int64_t row0;        // global row of row 0 (dropout key)
   MlpLayer L[5];
   const float* WT[5];  // transposed weights WT[i][k][n] of layers 1-4
-  int dbg;             // knob head_dbg: block 0 prints its phase cycle counts
   // optional: layer 0 as split-K partial sums parts[nsplit][M][L[0].N] (dense_fwd_splitk); the kernel then finishes
   // layer 0 itself (fixed-order sum, bias, ReLU, dropout per L[0]) and writes L[0].out
   const float* parts;
@@ -65,7 +64,6 @@ struct DirMidArgs {
   const int64_t* labels;                             // [B]
   float gs0, gs1;                                    // gate scales of layer 0 / 1 outputs (1 / (1 - p) in training)
   float *dl2, *d3, *d2, *d1, *d0;                    // [2B][2], [2B][64], [2B][128], [2B][256], [2B][512]
-  int dbg;                                           // knob head_dbg: print the phase cycle counts
 };
 int dir_mid(const DirMidArgs& a, hipStream_t st);
 // dst_s[b][k] = src_s[b][k] + c[b] src_s[B + b][k] for up to 6 segments (the stacked rows folded once c is known)

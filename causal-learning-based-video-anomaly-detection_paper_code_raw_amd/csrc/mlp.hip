@@ -29,8 +29,6 @@ __global__ __launch_bounds__(NTH) void mlp_tail_fwd_kernel(const MlpTailArgs a) 
   __shared__ __attribute__((aligned(16))) float red[NTH * 4 * RB];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * RB;
-  long long clk[6];
-  clk[0] = __builtin_readcyclecounter();
   {
     const int N = a.L[0].N;
     // (loads from clamped addresses, zeroed after: predicated loads would be issued one round trip apart)
@@ -79,7 +77,6 @@ __global__ __launch_bounds__(NTH) void mlp_tail_fwd_kernel(const MlpTailArgs a) 
     }
   }
   __syncthreads();
-  clk[1] = __builtin_readcyclecounter();
 #pragma unroll 1
   for (int i = 1; i < 5; ++i) {
     const MlpLayer& L = a.L[i];
@@ -127,11 +124,7 @@ __global__ __launch_bounds__(NTH) void mlp_tail_fwd_kernel(const MlpTailArgs a) 
       outb[r][n] = v;
     }
     __syncthreads();
-    clk[i + 1] = __builtin_readcyclecounter();
   }
-  if (a.dbg && blockIdx.x == 0 && tid == 0)
-    printf("mlp_tail_fwd cycles: stage %lld, L1 %lld, L2 %lld, L3 %lld, L4 %lld\n", clk[1] - clk[0], clk[2] - clk[1],
-           clk[3] - clk[2], clk[4] - clk[3], clk[5] - clk[4]);
 }
 
 // WT[k][n] = W[n][k] for up to 8 matrices (the detector's layer-1..4 weights), once per step: 32x32 tiles through
@@ -448,8 +441,6 @@ __global__ __launch_bounds__(1024) void dir_mid_kernel(const DirMidArgs a) {
   // every block runs layers 2-4, the seed and the layer 4-2 input gradients (cheap, redundant); block k then takes the
   // layer-1 input-gradient columns [64k, 64k + 64).  Block 0 alone writes the shared outputs.
   const bool w0 = blockIdx.x == 0;
-  long long clk[8];
-  clk[0] = __builtin_readcyclecounter();
   {
     float v[2];  // RB * 256 = 2048 = 2 x 1024 (clamped loads, zeroed after)
 #pragma unroll
@@ -469,15 +460,12 @@ __global__ __launch_bounds__(1024) void dir_mid_kernel(const DirMidArgs a) {
     }
   }
   __syncthreads();
-  clk[1] = __builtin_readcyclecounter();
   dir_layer_fwd<RB, 256, 128, 4, 32, true>(a.W2, a.b2, in1, a2, w0 ? a.h2 : nullptr, B);
   __syncthreads();
-  clk[2] = __builtin_readcyclecounter();
   dir_layer_fwd<RB, 128, 64, 2, 32, true>(a.W3, a.b3, a2, a3, w0 ? a.h3 : nullptr, B);
   __syncthreads();
   dir_layer_fwd<RB, 64, 2, 2, 16, false>(a.W4, a.b4, a3, lg, w0 ? a.logits : nullptr, B);
   __syncthreads();
-  clk[3] = __builtin_readcyclecounter();
   // seed rows: softmax, cross entropy on the probabilities (cad:673) and the c-free / c-linear parts of the anomaly
   // MSE through fin (cad:674), then the softmax backward -- the per-row arithmetic of cad_tail_bwd_kernel
   if (tid < R2) {
@@ -524,18 +512,10 @@ __global__ __launch_bounds__(1024) void dir_mid_kernel(const DirMidArgs a) {
     if (r >= 2 * B) dl[r][0] = dl[r][1] = 0.f;
   }
   __syncthreads();
-  clk[4] = __builtin_readcyclecounter();
   dir_layer_bwd<R2, 64, 2>(a.W4, dl, a3, 1.f, dd3, w0 ? a.d3 : nullptr, B, red);
-  clk[5] = __builtin_readcyclecounter();
   dir_layer_bwd<R2, 128, 64>(a.W3, dd3, a2, 1.f, dd2, w0 ? a.d2 : nullptr, B, red);
-  clk[6] = __builtin_readcyclecounter();
   dir_layer_bwd<R2, 256, 128>(a.W2, dd2, in1, a.gs1, dd1, w0 ? a.d1 : nullptr, B, red);
-  clk[7] = __builtin_readcyclecounter();
   dir_layer_bwd<R2, 64, 256, 512>(a.W1, dd1, in0, a.gs0, nullptr, a.d0, B, red, 64 * (int)blockIdx.x);
-  if (a.dbg && w0 && tid == 0)
-    printf("dir_mid cycles: stage %lld, fwd2 %lld, fwd3+4 %lld, seed %lld, bwd4 %lld, bwd3 %lld, bwd2 %lld, bwd1 %lld\n",
-           clk[1] - clk[0], clk[2] - clk[1], clk[3] - clk[2], clk[4] - clk[3], clk[5] - clk[4], clk[6] - clk[5],
-           clk[7] - clk[6], (long long)__builtin_readcyclecounter() - clk[7]);
 }
 
 int dir_mid(const DirMidArgs& a, hipStream_t st) {

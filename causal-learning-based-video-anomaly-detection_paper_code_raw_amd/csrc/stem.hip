@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256, 4) void stem_fused_kernel(const float* __restr
                                                             const float* __restrict__ bias,
                                                             const float* __restrict__ gamma, int OH, int OW, int HP,
                                                             int WP, int nbands, int PWb, float* __restrict__ pool,
-                                                            float* __restrict__ partials, int dbg) {
+                                                            float* __restrict__ partials) {
   extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
   constexpr int C = 32;
   const int img = blockIdx.x / nbands, band = blockIdx.x % nbands;
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256, 4) void stem_fused_kernel(const float* __restr
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < ((dbg & 1) ? 0 : 4); ++ks) {
+      for (int ks = 0; ks < 4; ++ks) {
         const unsigned* rowp = reinterpret_cast<const unsigned*>(xs + (2 * rl + 2 * ks + h) * PWb) + colc;
         bf16x8s a[NP];
 #pragma unroll
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256, 4) void stem_fused_kernel(const float* __restr
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float m = fmaxf(fmaxf(loc(2 * k), loc(2 * k + 1)), loc(2 * k + 2));
-      if (k < 8 - h && pxb + k < WP && !(dbg & 8)) act_st(dst + k * C, m * sgn);
+      if (k < 8 - h && pxb + k < WP) act_st(dst + k * C, m * sgn);
     }
   }
   s1 += __shfl_xor(s1, 32, 64);
@@ -241,8 +241,6 @@ __global__ __launch_bounds__(256, 4) void stem_fused_kernel(const float* __restr
 }  // namespace
 
 int g_stem_fused = 1;  // tuning knob "stem_fused": the frozen stem's forward without the conv1 activation
-// knob "stem_dbg" (measurement only, results wrong with any bit): 1 no MFMA, 8 no pooled-map stores
-int g_stem_dbg = 0;
 
 static int stem_pitch(int OW) { return (int)cdiv(2 * OW + 6, 8) * 8; }
 static size_t stem_lds(int OW) { return (size_t)3 * (2 * (2 * ST_PB + 1) + 6) * stem_pitch(OW) * sizeof(__bf16); }
@@ -262,13 +260,13 @@ int stem_fused(const float* x, int NF, int H, int W, const float* w, const float
   VAD_CHECK(!g_act_bf16 || g_conv_bf16, "stem_fused: bf16 activations need conv_bf16");
   if (g_conv_bf16 && g_act_bf16)
     VAD_KLAUNCH((stem_fused_kernel<1, true>), dim3(NF * nbands), dim3(256), stem_lds(OW), st, x, H, W, w, b, gamma, OH,
-                OW, HP, WP, nbands, stem_pitch(OW), pool, partials, g_stem_dbg);
+                OW, HP, WP, nbands, stem_pitch(OW), pool, partials);
   else if (g_conv_bf16)
     VAD_KLAUNCH(stem_fused_kernel<1>, dim3(NF * nbands), dim3(256), stem_lds(OW), st, x, H, W, w, b, gamma, OH, OW,
-                HP, WP, nbands, stem_pitch(OW), pool, partials, g_stem_dbg);
+                HP, WP, nbands, stem_pitch(OW), pool, partials);
   else
     VAD_KLAUNCH(stem_fused_kernel<3>, dim3(NF * nbands), dim3(256), stem_lds(OW), st, x, H, W, w, b, gamma, OH, OW,
-                HP, WP, nbands, stem_pitch(OW), pool, partials, g_stem_dbg);
+                HP, WP, nbands, stem_pitch(OW), pool, partials);
   VAD_LAUNCH_CHECK();
   *nparts = NF * nbands;
   return 0;

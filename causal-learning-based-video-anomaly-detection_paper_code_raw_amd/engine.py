@@ -28,6 +28,11 @@ class _Plan:
         nat.check(L.vad_cad_create(B, T, H, W, ctypes.byref(h)))
         self.h = h
         nat.check(L.vad_cad_set_option(h, b"conv_bf16", 1 if engine.compute_dtype == torch.bfloat16 else 0))
+        # (the workspace is carved for the options set before the size query: the training stem's buffers only when
+        # the stem trains -- CadEngine.plan builds a new plan when that changes)
+        self.stem_grad = engine.stem_trains()
+        self.ws_stem = self.stem_grad
+        nat.check(L.vad_cad_set_option(h, b"stem_grad", 1 if self.stem_grad else 0))
         self.shape = (B, T, H, W)
         nbytes = L.vad_cad_workspace_bytes(h)
         self.ws = torch.empty(int(nbytes) + 256, dtype=torch.uint8, device=engine.device)
@@ -179,9 +184,11 @@ class CadEngine:
 
     def plan(self, B, T, H, W) -> _Plan:
         key = (B, T, H, W)
-        if key not in self.plans:
-            self.plans[key] = _Plan(self, B, T, H, W)
-        return self.plans[key]
+        pl = self.plans.get(key)
+        if pl is None or (self.stem_trains() and not pl.ws_stem):
+            # (a plan carved for the frozen stem has no room for conv1's activation: a training stem needs a new one)
+            pl = self.plans[key] = _Plan(self, B, T, H, W)
+        return pl
 
     def grad_view(self, i):
         off = self.slot_offset[i]
