@@ -388,6 +388,10 @@ struct CadPlanImpl {
   // dYb[b] is done" (st3)
   hipStream_t st3 = nullptr;
   hipEvent_t ev_dy[2] = {nullptr, nullptr}, ev_wg[2] = {nullptr, nullptr}, ev_wgj = nullptr, ev_prep = nullptr;
+  // ev_layer[l]: every grad of backbone layer l (conv weight + bias, BN gamma / beta) is final -- recorded after the
+  // layer's split-K reduce on the queue that ran it (layer 0: also after the stem backward), for per-layer
+  // data-parallel gradient buckets (vad_cad_wait_layer_grads)
+  hipEvent_t ev_layer[8] = {};
   int wgrad_stream = 1;  // option "wgrad_stream" (0: weight gradients on the caller's stream)
   int streams() {
     if (!st2) {
@@ -410,6 +414,7 @@ struct CadPlanImpl {
       }
       VAD_HIP(hipEventCreateWithFlags(&ev_wgj, evf));
       VAD_HIP(hipEventCreateWithFlags(&ev_prep, evf));
+      for (int l = 0; l < 8; ++l) VAD_HIP(hipEventCreateWithFlags(&ev_layer[l], evf));
     }
     return 0;
   }
@@ -441,6 +446,8 @@ struct CadPlanImpl {
     }
     if (ev_wgj) (void)hipEventDestroy(ev_wgj);
     if (ev_prep) (void)hipEventDestroy(ev_prep);
+    for (int l = 0; l < 8; ++l)
+      if (ev_layer[l]) (void)hipEventDestroy(ev_layer[l]);
     if (st3) (void)hipStreamDestroy(st3);
     if (st2) (void)hipStreamDestroy(st2);
   }
@@ -1005,6 +1012,7 @@ struct CadPlanImpl {
         TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dYl, src, sst, slab, &ns, slab_cap, st, l == 0 && !stem_grad));
         TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], slab, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
         if (wgs && !on_main) VAD_HIP(hipEventRecord(ev_wg[l & 1], st));
+        if (l > 0 || !stem_grad) VAD_HIP(hipEventRecord(ev_layer[l], st));
       }
       fused_np = 0;
       if (l > 0) {
@@ -1033,6 +1041,7 @@ struct CadPlanImpl {
       TIMED("stem_bwd", bn_bwd_apply_inplace(stem_d, y1, stats[0], (int)M1, 32, st));
       TIMED("stem_bwd", conv1_wgrad(x_last, NF, H, W, stem_d, H1, W1, wpart, wpart_floats, G(LY.conv1_w), st));
       stem_active = 1;
+      VAD_HIP(hipEventRecord(ev_layer[0], st));  // (layer 0's bucket holds the stem's grads too)
     }
     if (stage == -1 || bwd_state == 2) {
       VAD_TRY(join(st));  // the head's weight grads (side stream)
@@ -1300,6 +1309,14 @@ int vad_cad_backward_stage(vad_cad_plan* plan, int stage, int use_loss, const fl
 int vad_cad_wait_side(vad_cad_plan* plan, void* stream) {
   VAD_CHECK(plan != nullptr, "vad_cad_wait_side: null plan");
   return plan->impl.wait_side((hipStream_t)stream);
+}
+
+int vad_cad_wait_layer_grads(vad_cad_plan* plan, int layer, void* stream) {
+  VAD_CHECK(plan != nullptr && layer >= 0 && layer < 8, "vad_cad_wait_layer_grads: null plan or layer outside 0..7");
+  CadPlanImpl& c = plan->impl;
+  VAD_CHECK(c.ev_layer[layer] != nullptr, "vad_cad_wait_layer_grads: no backbone backward has been queued");
+  VAD_HIP(hipStreamWaitEvent((hipStream_t)stream, c.ev_layer[layer], 0));
+  return 0;
 }
 
 int vad_cad_backward_ext(vad_cad_plan* plan, int stage, int use_loss, const float* d_final, const float* d_probs,

@@ -259,6 +259,12 @@ class CadEngine:
             nat.check(nat.lib().vad_cad_backward_stage(pl.h, stage, 1 if use_loss else 0, *[nat.ptr(t) for t in c],
                                                        nat.stream_of(self.device)))
 
+    def wait_layer_grads(self, layer: int, stream):
+        """Make `stream` wait until every grad of backbone layer `layer` (0..7; layer 0 with the stem's) of the last
+        queued backbone backward is final (per-layer data-parallel buckets)."""
+        pl = self._last[0]
+        nat.check(nat.lib().vad_cad_wait_layer_grads(pl.h, layer, ctypes.c_void_p(stream.cuda_stream)))
+
     def wait_side(self, stream):
         """Make `stream` (a torch.cuda.Stream) wait for everything queued so far on the last plan's side stream (the
         stage-2 backward's head / detector grads)."""

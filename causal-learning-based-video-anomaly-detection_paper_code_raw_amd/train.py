@@ -5,6 +5,7 @@ with an optional data-parallel gradient all-reduce (RCCL) between backward and t
 from __future__ import annotations
 
 import math
+import re
 
 import torch
 import torch.distributed as dist
@@ -69,6 +70,18 @@ class CadTrainer:
         i0 = next(i for i, n in enumerate(names) if n.startswith("detector."))
         i1 = next(i for i in range(i0, len(names)) if not names[i].startswith("detector."))
         self.det_range = (self.eng.slot_offset[i0], self.eng.slot_offset[i1])
+        # backbone buckets [lo, hi) of the flat grad buffer, in the backward's order, each with the backbone layer
+        # whose grads finish last in it: layer 7, layer 6, layers 5-4, layers 3-0 + the stem (the small layers are
+        # merged: a collective costs ~10-30 us of latency at 8 ranks whatever its size)
+        first = {}
+        for i, n in enumerate(names):
+            m = re.match(r"backbone\.layer(\d)\.(\d)\.", n)
+            if m:
+                l = 2 * (int(m.group(1)) - 1) + (0 if int(m.group(2)) < 3 else 1)
+                first.setdefault(l, self.eng.slot_offset[i])
+        first[8] = self.det_range[0]
+        first[0] = 0
+        self.bb_buckets = [(first[lo], first[hi], lo) for lo, hi in ((7, 8), (6, 7), (4, 6), (0, 4))]
         self.allreduce_floats = 0  # floats all-reduced by the last step (per rank, before the ring's 2(P-1)/P factor)
         self.prio_stream = None
         if prio_stream and self.eng.grads.is_cuda:
@@ -124,14 +137,17 @@ class CadTrainer:
         self.allreduce_floats += t.numel()
 
     def _backward_overlapped(self):
-        """Backward in two stages with the gradient all-reduce in three buckets (DDP's reduce-during-backward, with
-        the splits chosen for this model's grad order):
+        """Backward in two stages with the gradient all-reduce in buckets (DDP's reduce-during-backward, with the
+        splits chosen for this model's grad order):
           1. causal head + direct classifier + the has-grad flags, summed on a side stream while the backbone backward
              runs on the compute stream (which waits only for the detector's input gradient);
-          2. the detector, only when the summed detector flag says some rank's detector has a gradient (it is
-             identically zero on every rank otherwise: every frame took the fallback box, cad:221-226) -- the flag is
-             read on the host after the backbone backward is queued, so the GPU never idles for it;
-          3. the backbone, after the backbone backward.
+          2. the backbone in four buckets (self.bb_buckets), each issued behind the plan's event for the last of its
+             layers to finish (vad_cad_wait_layer_grads), so layer 7's all-reduce runs beside layers 6-0's backward;
+          3. the detector, only when the summed detector flag says some rank's detector has a gradient (it is
+             identically zero on every rank otherwise: every frame took the fallback box, cad:221-226).  The decision
+             must be the same on every rank (collectives are matched by issue order), so the host reads the summed
+             flag -- after every other bucket is queued: by then the flag's all-reduce (bucket 1, issued first) has
+             long completed on the GPU, and the wait holds back only the optimizer's enqueue, never GPU work.
         The optimizer waits for all of them.  Each element is summed over the same ranks as one all_reduce of the
         whole buffer, so results are identical to it."""
         eng = self.eng
@@ -153,13 +169,14 @@ class CadTrainer:
             self._flag_host.copy_(eng.grads[pf:pf + 2], non_blocking=True)
             self._flag_ev.record(side)
         eng.backward(True, stage=1)
+        for lo, hi, layer in self.bb_buckets:
+            eng.wait_layer_grads(layer, side)
+            with torch.cuda.stream(side):
+                self._reduce(eng.grads[lo:hi])
         self._flag_ev.synchronize()
         if float(self._flag_host[0]) > 0:
             with torch.cuda.stream(side):
                 self._reduce(eng.grads[d0:d1])
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            self._reduce(eng.grads[:d0])
         main.wait_stream(side)
 
 

@@ -91,6 +91,11 @@ int vad_cad_backward_stage(vad_cad_plan* plan, int stage, int use_loss, const fl
  * vad_cad_wait_side(plan, s) makes stream s wait for everything queued so far on that side stream (a data-parallel
  * caller's all-reduce stream, before it sums those grads).  Stage 1 after stage 2 re-joins the side stream. */
 int vad_cad_wait_side(vad_cad_plan* plan, void* stream);
+/* vad_cad_wait_layer_grads(plan, l, s): stream s waits until every grad of backbone layer l (0..7: the conv weight and
+ * bias and the BatchNorm gamma / beta of causal_anomaly_detection.py:128-139's l-th conv; layer 0 also the stem's) of
+ * the backbone backward queued last is final -- the per-layer buckets of a data-parallel gradient all-reduce, issued
+ * while the layers below are still in their backward (DDP's reduce-during-backward, cad:688-690). */
+int vad_cad_wait_layer_grads(vad_cad_plan* plan, int layer, void* stream);
 /* vad_cad_backward_stage with one more upstream grad: d_boxes [B,T,5,4] (may be NULL), the grad of a loss on the
  * forward's compacted per-frame detections (boxes output of vad_cad_forward; the reference's detections are slices
  * of the rescaled detector output and carry autograd, cad:201-222).  The constant fallback box takes no grad. */
