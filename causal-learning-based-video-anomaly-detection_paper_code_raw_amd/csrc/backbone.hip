@@ -2,6 +2,8 @@
 // train-mode BatchNorm forward/backward, max/adaptive-avg pooling, and the dense-layer GEMMs.
 // Reference semantics: ResNetBackbone (causal_anomaly_detection.py:110-158), nn.BatchNorm2d train mode,
 // nn.MaxPool2d(3,2,1), nn.AdaptiveAvgPool2d((4,6)), nn.Linear / ReLU / Dropout stacks (cad:167-179, 525-538).
+#include <type_traits>
+
 #include "backbone.h"
 #include "mlp.h"
 #include "gemm.h"
@@ -556,6 +558,45 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_inplace_kernel(float* dAY, c
   bn_bwd_apply_body<false>(dAY, y, stats, M, C, dAY, nullptr, BN_ROWS);
 }
 
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+struct f32x8v {
+  f32x4 lo, hi;
+};
+__device__ inline void vload8(u32x4v r, float (&v)[8]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = __uint_as_float(r[e] << 16);
+    v[2 * e + 1] = __uint_as_float(r[e] & 0xffff0000u);
+  }
+}
+__device__ inline void vload8(const f32x8v& r, float (&v)[8]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = r.lo[e];
+    v[4 + e] = r.hi[e];
+  }
+}
+template <typename V>
+__device__ inline V vstore8(const float (&v)[8]);
+template <>
+__device__ inline u32x4v vstore8<u32x4v>(const float (&v)[8]) {
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  b8 b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) b[e] = (__bf16)v[e];
+  return __builtin_bit_cast(u32x4v, b);
+}
+template <>
+__device__ inline f32x8v vstore8<f32x8v>(const float (&v)[8]) {
+  f32x8v o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    o.lo[e] = v[e];
+    o.hi[e] = v[4 + e];
+  }
+  return o;
+}
+
 int bn_bwd_apply_inplace(float* dAY, const float* y, const float* stats, int M, int C, hipStream_t st) {
   VAD_CHECK(!g_act_bf16, "bn_bwd_apply_inplace: fp32 activations only");
   hipLaunchKernelGGL(bn_bwd_apply_inplace_kernel, dim3(bn_rows_parts(M, C)), dim3(256), 0, st, dAY, y, stats, M, C,
@@ -564,9 +605,74 @@ int bn_bwd_apply_inplace(float* dAY, const float* y, const float* stats, int M, 
   return 0;
 }
 
+// Streaming form (no conv-bias partial sums): thread = 8 consecutive channels of a row (16 B per operand in bf16, 32 B in
+// fp32), U rows per iteration with every load issued before the arithmetic (the 4-channel row loop above keeps one 8-B
+// load per operand in flight per thread and reaches ~3.5 TB/s), grid-stride over the row groups.
+template <bool AB, int U>
+__global__ __launch_bounds__(256) void bn_bwd_apply_v_kernel(const act_t<AB>* __restrict__ dA,
+                                                           const act_t<AB>* __restrict__ y,
+                                                           const float* __restrict__ stats, int M, int C,
+                                                           act_t<AB>* __restrict__ dY) {
+  using V = typename std::conditional<AB, u32x4v, f32x8v>::type;  // 8 channels
+  const int tpr = C / 8, rpp = 256 / tpr;                         // threads per row, rows per pass
+  const int q = threadIdx.x % tpr, c = q * 8;
+  float mean[8], inv[8], sc[8], sh[8], k[8], mdz[8], mdzx[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mean[e] = stats[c + e];
+    inv[e] = stats[C + c + e];
+    sc[e] = stats[2 * C + c + e];
+    sh[e] = stats[3 * C + c + e];
+    k[e] = stats[4 * C + c + e];
+    mdz[e] = stats[5 * C + c + e];
+    mdzx[e] = stats[6 * C + c + e];
+  }
+  const int64_t step = (int64_t)gridDim.x * rpp * U;
+  for (int64_t r0 = ((int64_t)blockIdx.x * U) * rpp + threadIdx.x / tpr; r0 < M; r0 += step) {
+    V a[U], yy[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = min(r0 + (int64_t)u * rpp, (int64_t)M - 1);
+      a[u] = *reinterpret_cast<const V*>(dA + r * C + c);
+      yy[u] = *reinterpret_cast<const V*>(y + r * C + c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = r0 + (int64_t)u * rpp;
+      if (r >= M) break;
+      float af[8], yf[8], o[8];
+      vload8(a[u], af);
+      vload8(yy[u], yf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dz = fmaf(yf[e], sc[e], sh[e]) > 0.f ? af[e] : 0.f;
+        const float xh = (yf[e] - mean[e]) * inv[e];
+        o[e] = k[e] * (dz - mdz[e] - xh * mdzx[e]);
+      }
+      *reinterpret_cast<V*>(dY + r * C + c) = vstore8<V>(o);
+    }
+  }
+}
+
+int g_bn_apply_v = 1;  // knob "bn_apply_v": the streaming apply kernel (0: the 4-channel row loop)
+
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
                  int* nparts, hipStream_t st) {
   const int P = bn_rows_parts(M, C);
+  if (g_bn_apply_v && !bias_partials && C % 8 == 0 && C >= 8 && C <= 2048 && 256 % (C / 8) == 0) {
+    constexpr int U = 4;
+    const int rpp = 256 / (C / 8);
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(M, (int64_t)rpp * U), 2048));
+    if (g_act_bf16)
+      hipLaunchKernelGGL((bn_bwd_apply_v_kernel<true, U>), dim3(blocks), dim3(256), 0, st,
+                         reinterpret_cast<const __bf16*>(dA), reinterpret_cast<const __bf16*>(y), stats, M, C,
+                         reinterpret_cast<__bf16*>(dY));
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_v_kernel<false, U>), dim3(blocks), dim3(256), 0, st, dA, y, stats, M, C, dY);
+    VAD_LAUNCH_CHECK();
+    *nparts = 0;
+    return 0;
+  }
   if (g_act_bf16)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(P), dim3(256), 0, st, reinterpret_cast<const __bf16*>(dA),
                        reinterpret_cast<const __bf16*>(y), stats, M, C, reinterpret_cast<__bf16*>(dY), bias_partials,
@@ -1010,6 +1116,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "cad_stream_prio") g_cad_stream_prio = value;
   else if (k == "conv_split_pipe") g_x3_pipe = value;
   else if (k == "bn_bwd_fuse") g_bn_bwd_fuse = value;
+  else if (k == "bn_apply_v") g_bn_apply_v = value;
   else if (k == "conv_wgrad_s1_nt") g_wgrad_s1_nt = value;
   else if (k == "conv_wgrad_s1_nt_wide") g_wgrad_s1_nt_wide = value;
   else if (k == "conv_wgrad_s1_nt_blocks") g_wgrad_s1_nt_blocks = value;

@@ -42,6 +42,11 @@ struct BfcArgs {
   int tiles_h, tiles_w, ntiles, tpb;
 };
 
+// workgroup barrier for LDS hand-offs only: __syncthreads() also waits for every outstanding global load
+// (s_waitcnt vmcnt(0)), which would drain the next item's prefetch at each barrier; the register uses of those loads get
+// their own counted waits from the compiler.  (asm with a memory clobber: no LDS access moves across it.)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ void bf8_to_f32(u32v4 r, float (&v)[8]) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -57,22 +62,29 @@ __device__ __forceinline__ u32v4 f32_to_bf8(const float (&v)[8]) {
   return __builtin_bit_cast(u32v4, b);
 }
 
-template <int S, int NI, int TH, int TW, int CB, int NCT, bool FWD>
+// Per-block constants live in LDS (staged once): global loads issued inside the item loop would be younger than the
+// prefetch and their waits (s_waitcnt vmcnt counts in issue order) would drain it.  The MFMA loop keeps the next K
+// step's fragments in flight (one step of register double-buffering), so no MFMA waits on its own LDS reads.
+template <int S, int NI, int TH, int TW, int CB, int NCT, bool FWD, bool WRES>
 __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
   constexpr int NW = 4, NTHR = 256;
   constexpr int TPX = NI * TH * TW, MF = TPX / (32 * NW);
   static_assert(MF >= 1 && MF * 32 * NW == TPX, "a wave owns 32 MF output pixels");
   static_assert(FWD || S == 1, "stride-2 input gradients: bfc_dgrad_s2_kernel");
   static_assert(CB % 16 == 0 && CB <= 64, "16-deep K steps");
-  constexpr int NC = 32 * NCT, G8 = CB / 8, NG = NC / 8;
+  constexpr int NC = 32 * NCT, G8 = CB / 8, NG = NC / 8, KK = CB / 16, NSTEP = 9 * KK;
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3, PWE = (PW + 1) / 2, PROWS = NI * PH * PW;
   constexpr int RP = CB + 8, WP = 9 * CB + 8, EP = NC + 8;
   static_assert(((RP / 8) & 1) && ((WP / 8) & 1) && ((EP / 8) & 1), "odd 16-B row pitches");
   constexpr int PE = PROWS * RP > TPX * EP ? PROWS * RP : TPX * EP;
+  constexpr int CMAX = 256, CST = FWD ? 2 * CMAX + NC : 4 * NC;  // constants (floats)
   static_assert(NTHR % G8 == 0 && NTHR % NG == 0, "a thread keeps its channel group");
-  __shared__ __attribute__((aligned(16))) __bf16 sm[PE + NC * WP];
+  __shared__ __attribute__((aligned(16))) __bf16 sm[PE + NC * WP + 2 * CST];
   __bf16* const patch = sm;
   __bf16* const wl = sm + PE;
+  float* const cst = reinterpret_cast<float*>(sm + PE + NC * WP);
+  // forward: [scale | shift] of every input channel, then the bias of the block's NC outputs;
+  // input gradient: [mean | invstd | scale | shift] of the block's NC outputs (the layer below's BN)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, j = lane & 31;
   const int tiles_per_img = p.tiles_h * p.tiles_w;
@@ -80,6 +92,19 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
   const int t0 = blockIdx.x * p.tpb, t1 = min(p.ntiles, t0 + p.tpb);
   const int nch = p.C / CB;
   const int nitems = (t1 - t0) * nch;
+  const bool bn = FWD && p.scale != nullptr;
+  const bool bnb = !FWD && p.bny != nullptr;
+  if constexpr (FWD) {
+    for (int c = tid; c < p.C; c += NTHR) {
+      cst[c] = bn ? p.scale[c] : 1.f;
+      cst[CMAX + c] = bn ? p.shift[c] : 0.f;
+    }
+    for (int c = tid; c < NC; c += NTHR) cst[2 * CMAX + c] = p.bias ? p.bias[min(n0 + c, p.N - 1)] : 0.f;
+  } else {
+    if (bnb)
+      for (int q = tid; q < 4 * NC; q += NTHR) cst[q] = p.bnst[(q / NC) * p.N + min(n0 + q % NC, p.N - 1)];
+  }
+  __syncthreads();
 
   // this lane's A rows (MFMA row j of each of its MF pixel groups): patch row of tap (0, 0)
   int arow[MF];
@@ -94,15 +119,27 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
   constexpr int WQ = NC * 9 * G8, WIT = (WQ + NTHR - 1) / NTHR;
   const int g8 = tid % G8;
   u32v4 pv[PIT], wv[WIT];
-  bool pok[PIT], wok[WIT];
+  bool pok[PIT];
+  static_assert(PIT >= 1 && WIT >= 1, "staging passes");
   auto origin = [&](int tile, int& img0, int& oy0, int& ox0) {
     img0 = (tile / tiles_per_img) * NI;
     const int tr = tile % tiles_per_img;
     oy0 = (tr / p.tiles_w) * TH;
     ox0 = (tr % p.tiles_w) * TW;
   };
-  // loads from clamped addresses (no masked-load branches): out-of-range pieces are zeroed when stashed
-  auto fetch = [&](int tile, int ch, bool wts) {
+  // loads from clamped addresses (no masked-load branches): out-of-range pieces are zeroed when stashed.  Every item
+  // issues the same loads (WRES: the resident weight slice is loaded once, before the loop), so the compiler's counted
+  // waits (vmcnt) stay exact and never drain the prefetch
+  auto fetch_w = [&](int ch) {
+    const int c0 = ch * CB + g8 * 8;
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int q = min(tid + it * NTHR, WQ - 1);
+      const int n = q / (9 * G8), t = (q / G8) % 9;
+      wv[it] = *reinterpret_cast<const u32v4*>(p.w + ((int64_t)(n0 + n) * 9 + (FWD ? t : 8 - t)) * p.C + c0);
+    }
+  };
+  auto fetch = [&](int tile, int ch) {
     int img0, oy0, ox0;
     origin(tile, img0, oy0, ox0);
     const int c0 = ch * CB + g8 * 8;
@@ -115,31 +152,28 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
       pok[it] = q < PQ && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
       pv[it] = *reinterpret_cast<const u32v4*>(p.src + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : 0) + c0);
     }
-    if (wts) {
+    if constexpr (!WRES) fetch_w(ch);
+  };
+  auto stash_w = [&]() {
 #pragma unroll
-      for (int it = 0; it < WIT; ++it) {
-        const int q = min(tid + it * NTHR, WQ - 1);
-        const int n = q / (9 * G8), t = (q / G8) % 9;
-        wok[it] = n0 + n < p.N;
-        wv[it] = *reinterpret_cast<const u32v4*>(
-            p.w + (wok[it] ? ((int64_t)(n0 + n) * 9 + (FWD ? t : 8 - t)) * p.C : 0) + c0);
-      }
+    for (int it = 0; it < WIT; ++it) {
+      const int q = tid + it * NTHR;
+      if (q < WQ) *reinterpret_cast<u32v4*>(wl + (q / (9 * G8)) * WP + ((q / G8) % 9) * CB + g8 * 8) = wv[it];
     }
   };
-  auto stash = [&](int ch, bool wts) {
-    // BN scale / shift of this thread's 8 input channels
-    float sc[8] = {}, sh[8] = {};
-    const bool bn = FWD && p.scale != nullptr;
-    if (bn) {
+  auto stash = [&](int ch) {
+    float sc[8], sh[8];
+    if (bn) {  // BN scale / shift of this thread's 8 input channels
       const int c = ch * CB + g8 * 8;
-      const f32x4 a0 = *reinterpret_cast<const f32x4*>(p.scale + c), a1 = *reinterpret_cast<const f32x4*>(p.scale + c + 4);
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.shift + c), b1 = *reinterpret_cast<const f32x4*>(p.shift + c + 4);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        sc[e] = a0[e];
-        sc[4 + e] = a1[e];
-        sh[e] = b0[e];
-        sh[4 + e] = b1[e];
+      for (int e = 0; e < 8; e += 4) {
+        const f32x4 a4 = *reinterpret_cast<const f32x4*>(cst + c + e);
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(cst + CMAX + c + e);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          sc[e + u] = a4[u];
+          sh[e + u] = b4[u];
+        }
       }
     }
 #pragma unroll
@@ -150,7 +184,7 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
         const int im = row / (PH * PW), rr = row % (PH * PW);
         const int rx = rr % PW, col = S == 1 ? rx : ((rx & 1) ? PWE + (rx >> 1) : (rx >> 1));
         u32v4 v = pok[it] ? pv[it] : u32v4{0u, 0u, 0u, 0u};
-        if (FWD && bn && pok[it]) {  // zero padding stays zero: the reference pads relu(bn(y)) with zeros
+        if (bn && pok[it]) {  // zero padding stays zero: the reference pads relu(bn(y)) with zeros
           float f[8];
           bf8_to_f32(v, f);
 #pragma unroll
@@ -160,34 +194,66 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
         *reinterpret_cast<u32v4*>(patch + ((im * PH + rr / PW) * PW + col) * RP + g8 * 8) = v;
       }
     }
-    if (wts) {
+    if constexpr (!WRES) stash_w();
+  };
+  // fragments of K step s (tap s / KK, 16-channel slice s % KK)
+  auto frags = [&](int s, bfv8 (&a)[MF], bfv8 (&b)[NCT]) {
+    const int t = s / KK, kk = s % KK, kh = t / 3, kw = t % 3;
+    const int co = S == 1 ? kw : ((kw & 1) ? PWE + (kw >> 1) : (kw >> 1));
 #pragma unroll
-      for (int it = 0; it < WIT; ++it) {
-        const int q = tid + it * NTHR;
-        if (q < WQ) {
-          const int n = q / (9 * G8), t = (q / G8) % 9;
-          *reinterpret_cast<u32v4*>(wl + n * WP + t * CB + g8 * 8) = wok[it] ? wv[it] : u32v4{0u, 0u, 0u, 0u};
+    for (int nt = 0; nt < NCT; ++nt)
+      b[nt] = *reinterpret_cast<const bfv8*>(wl + (nt * 32 + j) * WP + t * CB + kk * 16 + 8 * h);
+#pragma unroll
+    for (int mf = 0; mf < MF; ++mf)
+      a[mf] = *reinterpret_cast<const bfv8*>(patch + (arow[mf] + kh * PW + co) * RP + kk * 16 + 8 * h);
+  };
+
+  // epilogue: this thread's 8 output channels (group cg) and their block sums
+  const int cg = tid % NG;
+  constexpr int EQ = TPX * NG, EIT = (EQ + NTHR - 1) / NTHR;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+  u32v4 yv[FWD ? 1 : EIT];  // (input gradient: the layer below's y at the written pixels, loaded before the prefetch)
+  (void)yv;
+
+  f32x16 acc[MF][NCT];
+  if (nitems <= 0) return;  // (block-uniform, before any barrier of the loop)
+  if constexpr (WRES) {  // one reduction chunk: the weight slice is staged once and stays resident
+    fetch_w(0);
+    stash_w();
+  }
+  fetch(t0, 0);
+  for (int item = 0; item < nitems; ++item) {
+    const int tile = t0 + item / nch, ch = item % nch;
+    lds_barrier();  // the previous item's fragment reads and epilogue reads are done
+    stash(ch);
+    lds_barrier();
+    int img0, oy0, ox0;
+    origin(tile, img0, oy0, ox0);
+    auto piece = [&](int i, int& m, int64_t& oi) {  // epilogue piece i of this thread: pixel m, NHWC offset (or -1)
+      const int q = tid + i * NTHR;
+      m = min(q / NG, TPX - 1);
+      const int mi = m / (TH * TW), mr = m % (TH * TW);
+      const int img = img0 + mi, oy = oy0 + mr / TW, ox = ox0 + mr % TW;
+      const bool ok = q < EQ && img < p.NF && oy < p.OH && ox < p.OW;
+      oi = ok ? (((int64_t)img * p.OH + oy) * p.OW + ox) * p.N + n0 + cg * 8 : -1;
+    };
+    if constexpr (!FWD) {
+      if (bnb && ch == nch - 1) {
+#pragma unroll
+        for (int i = 0; i < EIT; ++i) {
+          int m;
+          int64_t oi;
+          piece(i, m, oi);
+          yv[i] = *reinterpret_cast<const u32v4*>(p.bny + (oi < 0 ? 0 : oi));
         }
       }
     }
-  };
-
-  // epilogue state: this thread's 8 output channels (group cg) and their block sums
-  const int cg = tid % NG;
-  float s1[8], s2[8], bj[NCT];
-#pragma unroll
-  for (int nt = 0; nt < NCT; ++nt) bj[nt] = (FWD && p.bias) ? p.bias[min(n0 + nt * 32 + j, p.N - 1)] : 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
-
-  f32x16 acc[MF][NCT];
-  if (nitems > 0) fetch(t0, 0, true);
-  for (int item = 0; item < nitems; ++item) {
-    const int tile = t0 + item / nch, ch = item % nch;
-    __syncthreads();  // the previous item's fragment reads and epilogue reads are done
-    stash(ch, nch > 1 || item == 0);  // (one chunk: the weight slice stays resident)
-    __syncthreads();
-    if (item + 1 < nitems) fetch(t0 + (item + 1) / nch, (item + 1) % nch, nch > 1);
+    {  // (unconditional: the last item re-loads its own data)
+      const int nx = min(item + 1, nitems - 1);
+      fetch(t0 + nx / nch, nx % nch);
+    }
     if (ch == 0) {
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf)
@@ -196,52 +262,47 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc[mf][nt][r] = 0.f;
     }
-#pragma unroll 1
-    for (int t = 0; t < 9; ++t) {
-      const int kh = t / 3, kw = t % 3;
-      const int co = S == 1 ? kw : ((kw & 1) ? PWE + (kw >> 1) : (kw >> 1));
+    {
+      bfv8 a0[MF], b0[NCT], a1[MF], b1[NCT];
+      frags(0, a0, b0);
 #pragma unroll
-      for (int kk = 0; kk < CB / 16; ++kk) {
-        bfv8 b[NCT];
+      for (int s = 0; s < NSTEP; ++s) {
+        bfv8(&ac)[MF] = (s & 1) ? a1 : a0;
+        bfv8(&bc)[NCT] = (s & 1) ? b1 : b0;
+        if (s + 1 < NSTEP) frags(s + 1, (s & 1) ? a0 : a1, (s & 1) ? b0 : b1);
 #pragma unroll
-        for (int nt = 0; nt < NCT; ++nt)
-          b[nt] = *reinterpret_cast<const bfv8*>(wl + (nt * 32 + j) * WP + t * CB + kk * 16 + 8 * h);
-#pragma unroll
-        for (int mf = 0; mf < MF; ++mf) {
-          const bfv8 a = *reinterpret_cast<const bfv8*>(patch + (arow[mf] + kh * PW + co) * RP + kk * 16 + 8 * h);
+        for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
           for (int nt = 0; nt < NCT; ++nt)
-            acc[mf][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[nt], acc[mf][nt], 0, 0, 0);
-        }
+            acc[mf][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ac[mf], bc[nt], acc[mf][nt], 0, 0, 0);
       }
     }
     if (ch == nch - 1) {
       // accumulators -> bf16 [pixel][channel] rows in the patch region, then 16-B pieces to global
-      __syncthreads();  // every wave is done reading the patch
+      lds_barrier();  // every wave is done reading the patch
       __bf16* epi = patch;
 #pragma unroll
-      for (int mf = 0; mf < MF; ++mf)
+      for (int nt = 0; nt < NCT; ++nt) {
+        const float bj = FWD ? cst[2 * CMAX + nt * 32 + j] : 0.f;
 #pragma unroll
-        for (int nt = 0; nt < NCT; ++nt)
+        for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int m = (wave * MF + mf) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            epi[m * EP + nt * 32 + j] = (__bf16)(acc[mf][nt][r] + bj[nt]);
+            epi[m * EP + nt * 32 + j] = (__bf16)(acc[mf][nt][r] + bj);
           }
-      __syncthreads();
-      int img0, oy0, ox0;
-      origin(tile, img0, oy0, ox0);
-      // BN state of the layer below for this thread's 8 channels (input gradient with the fused reduce): the dZ mask
+      }
+      lds_barrier();
+      // the layer below's BN state for this thread's 8 channels (input gradient with the fused reduce): the dZ mask
       // test fma(y, scale, shift) > 0 and xhat = (y - mean) * invstd
-      float bsc[8], bsh[8], bmean[8], binv[8];
-      if (!FWD && p.bny) {
-        const int c = min(n0 + cg * 8, p.N - 8);
+      float bmean[8], binv[8], bsc[8], bsh[8];
+      if (bnb) {
 #pragma unroll
         for (int e = 0; e < 8; e += 4) {
-          const f32x4 m4 = *reinterpret_cast<const f32x4*>(p.bnst + c + e);
-          const f32x4 i4 = *reinterpret_cast<const f32x4*>(p.bnst + p.N + c + e);
-          const f32x4 a4 = *reinterpret_cast<const f32x4*>(p.bnst + 2 * p.N + c + e);
-          const f32x4 b4 = *reinterpret_cast<const f32x4*>(p.bnst + 3 * p.N + c + e);
+          const f32x4 m4 = *reinterpret_cast<const f32x4*>(cst + cg * 8 + e);
+          const f32x4 i4 = *reinterpret_cast<const f32x4*>(cst + NC + cg * 8 + e);
+          const f32x4 a4 = *reinterpret_cast<const f32x4*>(cst + 2 * NC + cg * 8 + e);
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(cst + 3 * NC + cg * 8 + e);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             bmean[e + u] = m4[u];
@@ -251,51 +312,36 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
           }
         }
       }
-      // pieces in batches of 2 (the loads of a batch issued together)
-      constexpr int EQ = TPX * NG, EIT = (EQ + NTHR - 1) / NTHR, EB = EIT < 2 ? EIT : 2;
 #pragma unroll
-      for (int i0 = 0; i0 < EIT; i0 += EB) {
-        u32v4 ev[EB], yv[EB];
-        int64_t oi[EB];
-        bool ok[EB];
+      for (int i = 0; i < EIT; ++i) {
+        int m;
+        int64_t oi;
+        piece(i, m, oi);
+        const u32v4 ev = *reinterpret_cast<const u32v4*>(epi + m * EP + cg * 8);
+        if (oi < 0) continue;
+        *reinterpret_cast<u32v4*>(p.out + oi) = ev;
+        float f[8];
+        bf8_to_f32(ev, f);
+        if constexpr (FWD) {
 #pragma unroll
-        for (int u = 0; u < EB; ++u) {
-          const int q = tid + (i0 + u) * NTHR;
-          const int m = min(q / NG, TPX - 1);
-          const int mi = m / (TH * TW), mr = m % (TH * TW);
-          const int img = img0 + mi, oy = oy0 + mr / TW, ox = ox0 + mr % TW;
-          ok[u] = i0 + u < EIT && q < EQ && img < p.NF && oy < p.OH && ox < p.OW;
-          oi[u] = ok[u] ? (((int64_t)img * p.OH + oy) * p.OW + ox) * p.N + n0 + cg * 8 : 0;
-          ev[u] = *reinterpret_cast<const u32v4*>(epi + m * EP + cg * 8);
-          if (!FWD && p.bny) yv[u] = *reinterpret_cast<const u32v4*>(p.bny + oi[u]);
-        }
+          for (int e = 0; e < 8; ++e) {
+            s1[e] += f[e];
+            s2[e] = fmaf(f[e], f[e], s2[e]);
+          }
+        } else if (bnb) {
+          float yy[8];
+          bf8_to_f32(yv[i], yy);
 #pragma unroll
-        for (int u = 0; u < EB; ++u) {
-          if (!ok[u]) continue;
-          *reinterpret_cast<u32v4*>(p.out + oi[u]) = ev[u];
-          float f[8];
-          bf8_to_f32(ev[u], f);
-          if (FWD) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              s1[e] += f[e];
-              s2[e] = fmaf(f[e], f[e], s2[e]);
-            }
-          } else if (p.bny) {
-            float yy[8];
-            bf8_to_f32(yv[u], yy);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float dz = fmaf(yy[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
-              s1[e] += dz;
-              s2[e] = fmaf(dz, (yy[e] - bmean[e]) * binv[e], s2[e]);
-            }
+          for (int e = 0; e < 8; ++e) {
+            const float dz = fmaf(yy[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
+            s1[e] += dz;
+            s2[e] = fmaf(dz, (yy[e] - bmean[e]) * binv[e], s2[e]);
           }
         }
       }
     }
   }
-  if ((FWD || p.bny) && p.partials) {
+  if ((FWD || bnb) && p.partials) {
     // lanes of one channel group: butterfly over the lane bits above the group bits, then the 4 waves in order
 #pragma unroll
     for (int o = NG; o < 64; o <<= 1)
@@ -402,7 +448,7 @@ __global__ __launch_bounds__(256, 2) void bfc_wgrad_kernel(const BfwArgs p) {
     const int img0 = (tile / tiles_per_img) * NI, tr = tile % tiles_per_img;
     const int y0 = (tr / p.tiles_w) * TH, x0 = (tr % p.tiles_w) * TW;
     const bool ragged = img0 + NI > p.NF || y0 + TH > p.OH || x0 + TW > p.OW;
-    __syncthreads();  // the previous tile's fragment reads are done
+    lds_barrier();  // the previous tile's fragment reads are done
 #pragma unroll
     for (int u = 0; u < YI / 4; ++u) {
       const int i = wave + 4 * u, f = i / (TPX / 16), pb = i % (TPX / 16);
@@ -450,7 +496,7 @@ __global__ __launch_bounds__(256, 2) void bfc_wgrad_kernel(const BfwArgs p) {
           *reinterpret_cast<u32v4*>(ys + (pc >> 2) * YIMG + m * 32 + (pc & 3) * 8) = u32v4{0u, 0u, 0u, 0u};
       }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll 1
     for (int k = 0; k < KSW; ++k) {
       // rows of this lane's transposed reads: tile pixels 16 (ks0 + k) + 8h + 4u + q4, u = 0, 1
@@ -539,16 +585,26 @@ __global__ __launch_bounds__(256, 2) void bfc_wgrad_kernel(const BfwArgs p) {
 // the classes share one staged 9 x 17 dY patch and the 9-tap weight slice, wave w takes class-grid rows 2w, 2w + 1
 // (32 class pixels) of every class (four accumulators).  The epilogue writes the four classes' rows to LDS and
 // stores 16-B pieces at dX rows (2 yc + ph, 2 xc + pw), with the fused BN-backward reduce as in bfc_conv_kernel.
-template <int CB>
+// the 9 (class, tap) pairs in class order: class c = 2 ph + pw, kh = ph ? {0, 2} : {1}, kw = pw ? {0, 2} : {1}
+__device__ __forceinline__ void s2_pair(int i, int& c, int& kh, int& kw) {
+  c = i == 0 ? 0 : (i <= 2 ? 1 : (i <= 4 ? 2 : 3));
+  const int q = i == 0 ? 0 : (i <= 2 ? i - 1 : (i <= 4 ? i - 3 : i - 5));
+  const int ph = c >> 1, pw = c & 1;
+  kh = ph ? 2 * (pw ? q >> 1 : q) : 1;
+  kw = pw ? 2 * (ph ? q & 1 : q) : 1;
+}
+
+template <int CB, bool WRES>
 __global__ __launch_bounds__(256, 2) void bfc_dgrad_s2_kernel(const BfcArgs p) {
-  constexpr int NTHR = 256, TH = 8, TW = 16, TPX = TH * TW, NC = 32, G8 = CB / 8, NG = NC / 8;
+  constexpr int NTHR = 256, TH = 8, TW = 16, TPX = TH * TW, NC = 32, G8 = CB / 8, NG = NC / 8, KK = CB / 16;
   constexpr int PH = TH + 1, PW = TW + 1, PROWS = PH * PW;
   constexpr int RP = CB + 8, WP = 9 * CB + 8, EP = NC + 8;
   static_assert(((RP / 8) & 1) && ((WP / 8) & 1) && ((EP / 8) & 1), "odd 16-B row pitches");
   constexpr int PE = PROWS * RP > 4 * TPX * EP ? PROWS * RP : 4 * TPX * EP;
-  __shared__ __attribute__((aligned(16))) __bf16 sm[PE + NC * WP];
+  __shared__ __attribute__((aligned(16))) __bf16 sm[PE + NC * WP + 2 * 4 * NC];
   __bf16* const patch = sm;
   __bf16* const wl = sm + PE;
+  float* const cst = reinterpret_cast<float*>(sm + PE + NC * WP);  // [mean | invstd | scale | shift] of the block's NC
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, j = lane & 31;
   const int tiles_per_img = p.tiles_h * p.tiles_w;
@@ -556,6 +612,11 @@ __global__ __launch_bounds__(256, 2) void bfc_dgrad_s2_kernel(const BfcArgs p) {
   const int t0 = blockIdx.x * p.tpb, t1 = min(p.ntiles, t0 + p.tpb);
   const int nch = p.C / CB;
   const int nitems = (t1 - t0) * nch;
+  const bool bnb = p.bny != nullptr;
+  if (bnb)
+    for (int q = tid; q < 4 * NC; q += NTHR) cst[q] = p.bnst[(q / NC) * p.N + min(n0 + q % NC, p.N - 1)];
+  __syncthreads();
+  if (nitems <= 0) return;
   // this lane's class pixel (row j of the wave's 32): patch row of offset (0, 0)
   const int arow = (2 * wave + j / TW) * PW + j % TW;
 
@@ -570,7 +631,23 @@ __global__ __launch_bounds__(256, 2) void bfc_dgrad_s2_kernel(const BfcArgs p) {
     yc0 = (tr / p.tiles_w) * TH;
     xc0 = (tr % p.tiles_w) * TW;
   };
-  auto fetch = [&](int tile, int ch, bool wts) {
+  auto fetch_w = [&](int ch) {
+    const int c0 = ch * CB + g8 * 8;
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int q = min(tid + it * NTHR, WQ - 1);
+      const int n = q / (9 * G8), t = (q / G8) % 9;
+      wv[it] = *reinterpret_cast<const u32v4*>(p.w + ((int64_t)(n0 + n) * 9 + t) * p.C + c0);
+    }
+  };
+  auto stash_w = [&]() {
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int q = tid + it * NTHR;
+      if (q < WQ) *reinterpret_cast<u32v4*>(wl + (q / (9 * G8)) * WP + ((q / G8) % 9) * CB + g8 * 8) = wv[it];
+    }
+  };
+  auto fetch = [&](int tile, int ch) {
     int img, yc0, xc0;
     origin(tile, img, yc0, xc0);
     const int c0 = ch * CB + g8 * 8;
@@ -582,87 +659,101 @@ __global__ __launch_bounds__(256, 2) void bfc_dgrad_s2_kernel(const BfcArgs p) {
       pok[it] = q < PQ && iy < p.IH && ix < p.IW;
       pv[it] = *reinterpret_cast<const u32v4*>(p.src + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : 0) + c0);
     }
-    if (wts) {
-#pragma unroll
-      for (int it = 0; it < WIT; ++it) {
-        const int q = min(tid + it * NTHR, WQ - 1);
-        const int n = q / (9 * G8), t = (q / G8) % 9;
-        wv[it] = *reinterpret_cast<const u32v4*>(p.w + ((int64_t)(n0 + n) * 9 + t) * p.C + c0);
-      }
-    }
+    if constexpr (!WRES) fetch_w(ch);
   };
-  auto stash = [&](bool wts) {
+  auto stash = [&]() {
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
       const int q = tid + it * NTHR;
       if (q < PQ)
         *reinterpret_cast<u32v4*>(patch + (q / G8) * RP + g8 * 8) = pok[it] ? pv[it] : u32v4{0u, 0u, 0u, 0u};
     }
-    if (wts) {
-#pragma unroll
-      for (int it = 0; it < WIT; ++it) {
-        const int q = tid + it * NTHR;
-        if (q < WQ) *reinterpret_cast<u32v4*>(wl + (q / (9 * G8)) * WP + ((q / G8) % 9) * CB + g8 * 8) = wv[it];
-      }
-    }
+    if constexpr (!WRES) stash_w();
+  };
+  // fragments of K step s: (class, tap) pair s / KK, 16-channel slice s % KK
+  auto frags = [&](int s, bfv8& a, bfv8& b) {
+    int c, kh, kw;
+    s2_pair(s / KK, c, kh, kw);
+    const int kk = s % KK;
+    const int dr = (c >> 1) ? (kh == 0 ? 1 : 0) : 0, dc = (c & 1) ? (kw == 0 ? 1 : 0) : 0;
+    b = *reinterpret_cast<const bfv8*>(wl + j * WP + (kh * 3 + kw) * CB + kk * 16 + 8 * h);
+    a = *reinterpret_cast<const bfv8*>(patch + (arow + dr * PW + dc) * RP + kk * 16 + 8 * h);
   };
 
   const int cg = tid % NG;
+  constexpr int EQ = 4 * TPX * NG, EIT = EQ / NTHR;
+  static_assert(EQ % NTHR == 0, "whole epilogue passes");
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+  u32v4 yv[EIT];
   f32x16 acc[4];
-  if (nitems > 0) fetch(t0, 0, true);
+  if constexpr (WRES) {
+    fetch_w(0);
+    stash_w();
+  }
+  fetch(t0, 0);
   for (int item = 0; item < nitems; ++item) {
     const int tile = t0 + item / nch, ch = item % nch;
-    __syncthreads();
-    stash(nch > 1 || item == 0);
-    __syncthreads();
-    if (item + 1 < nitems) fetch(t0 + (item + 1) / nch, (item + 1) % nch, nch > 1);
+    lds_barrier();
+    stash();
+    lds_barrier();
+    int img, yc0, xc0;
+    origin(tile, img, yc0, xc0);
+    auto piece = [&](int i, int& cm, int64_t& oi) {  // epilogue piece i: class pixel row cm, NHWC offset (or -1)
+      const int q = tid + i * NTHR;
+      cm = q / NG;
+      const int c = cm / TPX, m = cm % TPX;
+      const int yy = 2 * (yc0 + m / TW) + (c >> 1), xx = 2 * (xc0 + m % TW) + (c & 1);
+      oi = (yy < p.OH && xx < p.OW) ? (((int64_t)img * p.OH + yy) * p.OW + xx) * p.N + n0 + cg * 8 : -1;
+    };
+    if (bnb && ch == nch - 1) {  // the layer below's y at the pixels this item writes (issued before the prefetch)
+#pragma unroll
+      for (int i = 0; i < EIT; ++i) {
+        int cm;
+        int64_t oi;
+        piece(i, cm, oi);
+        yv[i] = *reinterpret_cast<const u32v4*>(p.bny + (oi < 0 ? 0 : oi));
+      }
+    }
+    {
+      const int nx = min(item + 1, nitems - 1);
+      fetch(t0 + nx / nch, nx % nch);
+    }
     if (ch == 0) {
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
     }
+    {
+      bfv8 a0, b0, a1, b1;
+      frags(0, a0, b0);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int ph = c >> 1, pw = c & 1;
-#pragma unroll
-      for (int a = 0; a < (ph ? 2 : 1); ++a) {
-        const int kh = ph ? 2 * a : 1, dr = ph ? 1 - a : 0;
-#pragma unroll
-        for (int b = 0; b < (pw ? 2 : 1); ++b) {
-          const int kw = pw ? 2 * b : 1, dc = pw ? 1 - b : 0;
-#pragma unroll
-          for (int kk = 0; kk < CB / 16; ++kk) {
-            const bfv8 bw = *reinterpret_cast<const bfv8*>(wl + j * WP + (kh * 3 + kw) * CB + kk * 16 + 8 * h);
-            const bfv8 av = *reinterpret_cast<const bfv8*>(patch + (arow + dr * PW + dc) * RP + kk * 16 + 8 * h);
-            acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bw, acc[c], 0, 0, 0);
-          }
-        }
+      for (int s = 0; s < 9 * KK; ++s) {
+        if (s + 1 < 9 * KK) frags(s + 1, (s & 1) ? a0 : a1, (s & 1) ? b0 : b1);
+        int c, kh, kw;
+        s2_pair(s / KK, c, kh, kw);
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16((s & 1) ? a1 : a0, (s & 1) ? b1 : b0, acc[c], 0, 0, 0);
       }
     }
     if (ch == nch - 1) {
-      __syncthreads();  // every wave is done reading the patch
+      lds_barrier();  // every wave is done reading the patch
       __bf16* epi = patch;  // [class][pixel][channel]
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           epi[(c * TPX + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * EP + j] = (__bf16)acc[c][r];
-      __syncthreads();
-      int img, yc0, xc0;
-      origin(tile, img, yc0, xc0);
-      float bsc[8], bsh[8], bmean[8], binv[8];
-      if (p.bny) {
-        const int c = min(n0 + cg * 8, p.N - 8);
+      lds_barrier();
+      float bmean[8], binv[8], bsc[8], bsh[8];
+      if (bnb) {
 #pragma unroll
         for (int e = 0; e < 8; e += 4) {
-          const f32x4 m4 = *reinterpret_cast<const f32x4*>(p.bnst + c + e);
-          const f32x4 i4 = *reinterpret_cast<const f32x4*>(p.bnst + p.N + c + e);
-          const f32x4 a4 = *reinterpret_cast<const f32x4*>(p.bnst + 2 * p.N + c + e);
-          const f32x4 b4 = *reinterpret_cast<const f32x4*>(p.bnst + 3 * p.N + c + e);
+          const f32x4 m4 = *reinterpret_cast<const f32x4*>(cst + cg * 8 + e);
+          const f32x4 i4 = *reinterpret_cast<const f32x4*>(cst + NC + cg * 8 + e);
+          const f32x4 a4 = *reinterpret_cast<const f32x4*>(cst + 2 * NC + cg * 8 + e);
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(cst + 3 * NC + cg * 8 + e);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             bmean[e + u] = m4[u];
@@ -672,43 +763,29 @@ __global__ __launch_bounds__(256, 2) void bfc_dgrad_s2_kernel(const BfcArgs p) {
           }
         }
       }
-      constexpr int EQ = 4 * TPX * NG, EIT = EQ / NTHR, EB = 2;
-      static_assert(EQ % NTHR == 0 && EIT % EB == 0, "whole epilogue passes");
 #pragma unroll
-      for (int i0 = 0; i0 < EIT; i0 += EB) {
-        u32v4 ev[EB], yv[EB];
-        int64_t oi[EB];
-        bool ok[EB];
+      for (int i = 0; i < EIT; ++i) {
+        int cm;
+        int64_t oi;
+        piece(i, cm, oi);
+        const u32v4 ev = *reinterpret_cast<const u32v4*>(epi + cm * EP + cg * 8);
+        if (oi < 0) continue;
+        *reinterpret_cast<u32v4*>(p.out + oi) = ev;
+        if (bnb) {
+          float f[8], yy[8];
+          bf8_to_f32(ev, f);
+          bf8_to_f32(yv[i], yy);
 #pragma unroll
-        for (int u = 0; u < EB; ++u) {
-          const int q = tid + (i0 + u) * NTHR;
-          const int cm = q / NG, c = cm / TPX, m = cm % TPX;
-          const int yy = 2 * (yc0 + m / TW) + (c >> 1), xx = 2 * (xc0 + m % TW) + (c & 1);
-          ok[u] = yy < p.OH && xx < p.OW;
-          oi[u] = ok[u] ? (((int64_t)img * p.OH + yy) * p.OW + xx) * p.N + n0 + cg * 8 : 0;
-          ev[u] = *reinterpret_cast<const u32v4*>(epi + cm * EP + cg * 8);
-          if (p.bny) yv[u] = *reinterpret_cast<const u32v4*>(p.bny + oi[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < EB; ++u) {
-          if (!ok[u]) continue;
-          *reinterpret_cast<u32v4*>(p.out + oi[u]) = ev[u];
-          if (p.bny) {
-            float f[8], yy[8];
-            bf8_to_f32(ev[u], f);
-            bf8_to_f32(yv[u], yy);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float dz = fmaf(yy[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
-              s1[e] += dz;
-              s2[e] = fmaf(dz, (yy[e] - bmean[e]) * binv[e], s2[e]);
-            }
+          for (int e = 0; e < 8; ++e) {
+            const float dz = fmaf(yy[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
+            s1[e] += dz;
+            s2[e] = fmaf(dz, (yy[e] - bmean[e]) * binv[e], s2[e]);
           }
         }
       }
     }
   }
-  if (p.bny && p.partials) {
+  if (bnb && p.partials) {
 #pragma unroll
     for (int o = NG; o < 64; o <<= 1)
 #pragma unroll
@@ -759,7 +836,8 @@ static int bfc_launch(BfcArgs a, int64_t max_blocks, hipStream_t st, int* nparts
   const int64_t target = std::max<int64_t>(1, std::min<int64_t>(max_blocks, cdiv(g_bfc_blocks, ny)));
   a.tpb = (int)cdiv(a.ntiles, target);
   const int gx = (int)cdiv(a.ntiles, a.tpb);
-  VAD_KLAUNCH((bfc_conv_kernel<S, NI, TH, TW, CB, NCT, FWD>), dim3(gx, ny), dim3(256), 0, st, a);
+  if (a.C == CB) VAD_KLAUNCH((bfc_conv_kernel<S, NI, TH, TW, CB, NCT, FWD, true>), dim3(gx, ny), dim3(256), 0, st, a);
+  else VAD_KLAUNCH((bfc_conv_kernel<S, NI, TH, TW, CB, NCT, FWD, false>), dim3(gx, ny), dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   if (nparts) *nparts = gx;
   return 0;
@@ -839,8 +917,9 @@ int bfc_dgrad(const Conv3Layer& L, const __bf16* dY, const __bf16* wdb, __bf16* 
     const int64_t target = std::max<int64_t>(1, std::min<int64_t>(mb, cdiv(g_bfc_blocks, ny)));
     a.tpb = (int)cdiv(a.ntiles, target);
     const int gx = (int)cdiv(a.ntiles, a.tpb);
-    if (L.Co % 32 == 0) VAD_KLAUNCH(bfc_dgrad_s2_kernel<32>, dim3(gx, ny), dim3(256), 0, st, a);
-    else VAD_KLAUNCH(bfc_dgrad_s2_kernel<16>, dim3(gx, ny), dim3(256), 0, st, a);
+    if (L.Co == 32) VAD_KLAUNCH((bfc_dgrad_s2_kernel<32, true>), dim3(gx, ny), dim3(256), 0, st, a);
+    else if (L.Co % 32 == 0) VAD_KLAUNCH((bfc_dgrad_s2_kernel<32, false>), dim3(gx, ny), dim3(256), 0, st, a);
+    else VAD_KLAUNCH((bfc_dgrad_s2_kernel<16, false>), dim3(gx, ny), dim3(256), 0, st, a);
     VAD_LAUNCH_CHECK();
     if (f) *f->nparts = gx;
     return 0;
