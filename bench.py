@@ -289,6 +289,15 @@ def run_gpu(args, rank, world, local_rank):
         torch.cuda.synchronize()
         probe = dict(state={k: v.detach().cpu().clone() for k, v in model.state_dict().items()},
                      final=o["final"].cpu(), probs=o["probs"].cpu(), loss=float(o["losses"][4]))
+        # held-out set for the frame-AUC parity: HELDOUT_BATCHES x B synthetic clips never trained on (seed 8), eval mode
+        # (running statistics), labels i mod 2
+        from oracle import cad_oracle as co
+        held = []
+        for k in range(HELDOUT_BATCHES):
+            xh = co.synth_clips(8, k, 0, B, T, H, W).to(dev)
+            held.append(eng.forward(xh, False, 0, 0, 0, None)["final"].cpu())
+        torch.cuda.synchronize()
+        probe["heldout"] = torch.cat(held)
     # input-inclusive leg (rank 0, N=1): the same step fed from pinned host u8 clips through ClipStager (H2D on a
     # copy stream, batch k+1's copy overlapping step k, u8 -> fp32 on the device); never the headline value
     h2d = None
@@ -351,6 +360,9 @@ def step_roofline(args, clips_per_s_per_gpu, step_tflops):
             "basis": "SURVEY §8d B_clip = 681 MB x clips/s per GPU"}
 
 
+HELDOUT_BATCHES = 8  # held-out clips for the frame-AUC parity: 8 x B (64 at the default B = 8)
+
+
 def parity_check(args, probe):
     """CPU leg of the parity probe: the oracle forward (fp32, CPU) on the same clips, weights, BN state and draws
     as the GPU probe; max |score difference| (north star: 1e-4) and frame-AUC of both score sets (clip labels
@@ -368,13 +380,26 @@ def parity_check(args, probe):
         ref = co.cad_forward(params, bufs, x, co.CadDraws.make(777, 0, 0, B, T), training=True)
         rl = co.cad_losses(ref, y)
     gpu_s, cpu_s = probe["final"].double(), ref["anomaly_scores"].double()
+    # held-out frame-AUC: the same eval-mode scoring of the HELDOUT_BATCHES x B unseen clips on the oracle
+    held_cpu = []
+    with torch.no_grad():
+        for k in range(HELDOUT_BATCHES):
+            b2 = {kk: v.clone() for kk, v in sd.items() if "running" in kk}  # (the train-mode probe above moved bufs)
+            r = co.cad_forward(params, b2, co.synth_clips(8, k, 0, B, T, H, W), co.CadDraws.make(0, 0, 0, B, T),
+                               training=False)
+            held_cpu.append(r["anomaly_scores"].double())
+    hc, hg = torch.cat(held_cpu), probe["heldout"].double()
+    yh = torch.arange(hc.numel()) % 2
     return {"max_abs_score_diff": float((gpu_s - cpu_s).abs().max()),
             "max_abs_prob_diff": float((probe["probs"].double() - ref["direct_predictions"].double()).abs().max()),
             "loss_rel_diff": abs(probe["loss"] - float(rl["total"])) / max(abs(float(rl["total"])), 1e-12),
-            "frame_auc_gpu": frame_auc(gpu_s.numpy(), y.numpy(), T),
-            "frame_auc_cpu": frame_auc(cpu_s.numpy(), y.numpy(), T),
+            "frame_auc_gpu": frame_auc(hg.numpy(), yh.numpy(), T),
+            "frame_auc_cpu": frame_auc(hc.numpy(), yh.numpy(), T),
+            "heldout_max_abs_score_diff": float((hg - hc).abs().max()),
             "tolerance": 1e-4 if args.dtype == "fp32" else 2e-2,
-            "sample": f"one train-mode forward of B={B} clips x T={T} x 1x{H}x{W} after the timed steps"}
+            "sample": f"one train-mode forward of B={B} clips x T={T} x 1x{H}x{W} after the timed steps (scores, "
+                      f"loss); frame-AUC and heldout_max_abs_score_diff: eval-mode scores of {hc.numel()} held-out "
+                      f"synthetic clips (seed 8, never trained on), labels i mod 2 broadcast to the T frames"}
 
 
 def cpu_baseline(args):

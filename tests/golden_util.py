@@ -156,16 +156,45 @@ def reshape_masks(masks, x):
 def pinned_oracle_grads(state_dict, x, labels, draws, masks, sync_group=None):
     """float64 oracle forward/backward of one train step with the ReLU decisions of another forward (masks from
     hip_relu_masks): the exact gradient of that forward's piecewise-linear branch, free of kink flips.  Returns
-    (grads {name: float64 tensor or None}, losses {name: float64}, the oracle's result dict incl. "bufs")."""
+    (grads {name: float64 tensor or None}, losses {name: float64}, the oracle's result dict incl. "bufs" and
+    "record" -- the float64 BatchNorm outputs "z{l}" in front of each pinned ReLU, for check_mask_flips)."""
     from oracle import cad_oracle as co
     params = {k: v.detach().double().clone() for k, v in state_dict.items()
               if "running" not in k and "num_batches" not in k}
     bufs = {k: v.detach().double().clone() for k, v in state_dict.items() if "running" in k}
     xd = x.double()
     rm = reshape_masks(masks, xd)
-    res = co.cad_train_step(params, bufs, {}, xd, labels, draws, relu_masks=rm, sync_group=sync_group)
+    record = {}
+    res = co.cad_train_step(params, bufs, {}, xd, labels, draws, relu_masks=rm, sync_group=sync_group,
+                            record=record)
     res["bufs"] = bufs  # running stats after the step's forward
+    res["record"] = record
     return res["grads"], res["losses"], res
+
+
+def check_mask_flips(masks, record, x, ulps=64, unit=2.0 ** -24, accum=True):
+    """The mask-pinned method takes the device's ReLU decisions; this bounds them: a decision may differ from the sign
+    of the float64 oracle's own BatchNorm output z (the pinned oracle forward, record["z{l}"], i.e. the same branch
+    taken in the layers below) only where |z| <= ulps units of the accumulation magnitude of that layer's conv,
+    unit * sqrt(K) * RMS_c(z) per channel (K = 9 Ci: a K-term fp32 sum carries ~sqrt(K) roundings of the terms'
+    scale; accum=False: unit * RMS_c(z), for bf16 storage whose one rounding of y dominates).  Returns per layer
+    (flips, largest |z| at a flip / its bound); raises if a flip lies outside the bound."""
+    from oracle import cad_oracle as co
+    rm = reshape_masks(masks, x.double())
+    out = []
+    cin = [32, 32, 32, 64, 64, 128, 128, 256]
+    for l, m in enumerate(rm):
+        z = record[f"z{l}"]
+        rms = z.pow(2).mean(dim=(0, 2, 3)).sqrt()[None, :, None, None]
+        bound = ulps * unit * ((9 * cin[l]) ** 0.5 if accum else 1.0) * rms
+        flips = (z > 0) != m.to(torch.bool)
+        n = int(flips.sum())
+        worst = float((z.abs() / bound)[flips].max()) if n else 0.0
+        bad = flips & (z.abs() > bound)
+        assert not bool(bad.any()), (f"layer {l}: {int(bad.sum())} of {n} ReLU decisions differ from the float64 "
+                                     f"forward beyond {ulps} ulp of the accumulation scale (worst |z|/bound {worst:.3g})")
+        out.append((n, worst))
+    return out
 
 
 def rel_l2(a, b):

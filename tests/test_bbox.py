@@ -70,6 +70,33 @@ def test_bbox_mixed_t_packing_matches_oracle():
         np.testing.assert_allclose(f, rf[0].numpy(), rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.gpu
+def test_bbox_config5_packed_64_clips_matches_oracle():
+    """BASELINE config 5's per-rank workload: 64 clips with T drawn from {8, 16, 32} (seeded, mixed order), scored in
+    one call (one packed batch per T bucket) -- every clip's score, graph and features equal the oracle's (run per T
+    bucket on CPU, float32) within 1e-4."""
+    from vad_amd.bbox import AnomalyVisualizer
+    case = dict(seed=55)
+    vis = AnomalyVisualizer(None, device="cuda")
+    vis.model = make_bbox_model(case).cuda()
+    p = {k: v.detach().cpu().clone() for k, v in make_bbox_model(case).state_dict().items()}
+    g = np.random.default_rng(55)
+    Ts = [int(t) for t in g.choice([8, 16, 32], size=64)]
+    assert len(set(Ts)) == 3
+    clips = [bo.synth_clips(55, 0, i, 1, T, 64, 64)[0].numpy() for i, T in enumerate(Ts)]
+    res = vis.predict_clips(clips)
+    assert len(res) == 64
+    for T in (8, 16, 32):
+        idx = [i for i, t in enumerate(Ts) if t == T]
+        with torch.no_grad():
+            rs, radj, rf = bo.bbox_forward(p, torch.from_numpy(np.stack([clips[i] for i in idx])))
+        for k, i in enumerate(idx):
+            s, adj, f = res[i]
+            assert s == pytest.approx(float(rs.reshape(-1)[k]), rel=1e-4, abs=1e-6), (i, T)
+            np.testing.assert_allclose(adj, radj[k].numpy(), rtol=1e-4, atol=1e-6)
+            np.testing.assert_allclose(f, rf[k].numpy(), rtol=1e-4, atol=1e-5)
+
+
 def _bbox_dp_worker(rank, world, port, out_path):
     import os
     import torch.distributed as dist

@@ -15,7 +15,8 @@ import pytest
 import torch
 
 from oracle import cad_oracle as co
-from tests.golden_util import cad_cases, hip_relu_masks, load, make_cad_model, pinned_oracle_grads, rel_l2
+from tests.golden_util import (cad_cases, check_mask_flips, hip_relu_masks, load, make_cad_model,
+                               pinned_oracle_grads, rel_l2)
 from tests.test_oracle_golden import is_pre_bn_bias
 
 pytestmark = pytest.mark.gpu
@@ -28,6 +29,48 @@ def _frozen(m):
     with contextlib.redirect_stdout(io.StringIO()):
         apply_memory_efficient_training(m)
     return m
+
+
+def _module_pinned_check(m, case, x, user_loss, training, seed=0, step=0, coef=None):
+    """model(x) + user_loss(out).backward() on the device against the mask-pinned float64 oracle (the eight conv ReLUs,
+    bn1's ReLU and the MaxPool2d window maxima taken from the HIP forward): scores / probabilities within 1e-4 and
+    every parameter gradient within relative L2 1e-4 per tensor (pre-BN conv biases, true gradient 0: rounding noise).
+    Returns (worst relative L2, names of the tensors with a live gradient, the oracle's output)."""
+    from tests.golden_util import hip_stem_pins, reshape_masks
+    B, T, H, W = x.shape[0], x.shape[1], x.shape[3], x.shape[4]
+    out = m(x.cuda(), seed=seed, step=step, clip0=0) if training else m(x.cuda())
+    user_loss(out, coef.cuda() if coef is not None else None).backward()
+    torch.cuda.synchronize()
+    eng = m.engine()
+    masks = reshape_masks(hip_relu_masks(eng, B * T), x)
+    pins = hip_stem_pins(eng, B * T, H, W) if eng.stem_grad_on else None
+    sd = make_cad_model(case).state_dict()
+    params = {k: v.detach().double().clone().requires_grad_(True) for k, v in sd.items()
+              if "running" not in k and "num_batches" not in k}
+    bufs = {k: v.detach().double().clone() for k, v in sd.items() if "running" in k}
+    ref = co.cad_forward(params, bufs, x.double(), co.CadDraws.make(seed, step, 0, B, T), training=training,
+                         relu_masks=masks, stem_pins=pins)
+    user_loss(ref, coef.double() if coef is not None else None).backward()
+    np.testing.assert_allclose(out["anomaly_scores"].detach().cpu().numpy(), ref["anomaly_scores"].detach().numpy(),
+                               rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(out["direct_predictions"].detach().cpu().numpy(),
+                               ref["direct_predictions"].detach().numpy(), rtol=1e-4, atol=1e-5)
+    worst, live = 0.0, set()
+    for n, p in m.named_parameters():
+        pr = params[n]
+        if pr.grad is None or float(pr.grad.abs().max()) == 0.0:
+            assert p.grad is None or float(p.grad.abs().max()) < 1e-9, n
+            continue
+        assert p.grad is not None, n
+        mine = p.grad.detach().cpu().double().numpy()
+        if is_pre_bn_bias(n) or n == "backbone.conv1.bias":  # true gradient 0 (BN removes the mean)
+            assert np.abs(mine).max() < 1e-6 * max(1.0, float(pr.grad.abs().max())) + 1e-6, n
+            continue
+        e = rel_l2(mine, pr.grad.numpy())
+        worst = max(worst, e)
+        live.add(n)
+        assert e <= 1e-4, f"{n}: relative L2 error {e:.3g} vs the mask-pinned oracle"
+    return worst, live, ref
 
 
 def _hip_step(case, step_opt=True, keep_pre=False):
@@ -152,7 +195,9 @@ def test_hip_step_matches_reference(case):
 
 
 def test_module_api_forward_backward():
-    """model(videos) through torch autograd: output structure and grads of a user-defined loss vs the oracle."""
+    """model(videos) through torch autograd in eval mode (running statistics; the stem trains: no freeze): output
+    structure, and the scores plus every gradient of a user-defined loss vs the mask-pinned float64 oracle (relative
+    L2 <= 1e-4 per tensor)."""
     case = dict(name="api", B=2, T=4, H=64, W=64, seed=11, step=0, forced=None)
     m = make_cad_model(case).cuda()
     m.eval()
@@ -161,28 +206,14 @@ def test_module_api_forward_backward():
     assert set(out) == {"anomaly_scores", "causal_factors", "adjacency_matrices", "kl_losses", "detections",
                         "direct_predictions", "causal_anomaly_scores"}
     assert len(out["detections"]) == 2 and len(out["detections"][0]) == 4
-    loss = out["anomaly_scores"].sum() + 0.5 * out["direct_predictions"][:, 0].sum() + sum(out["kl_losses"])
-    loss.backward()
-    # oracle, eval mode
-    mc = make_cad_model(case)
-    sd = {k: v.clone() for k, v in mc.state_dict().items()}
-    params = {k: v.requires_grad_(True) for k, v in sd.items() if "running" not in k and "num_batches" not in k}
-    bufs = {k: v for k, v in sd.items() if "running" in k}
-    draws = co.CadDraws.make(0, 0, 0, 2, 4)
-    ref = co.cad_forward(params, bufs, x, draws, training=False)
-    np.testing.assert_allclose(out["anomaly_scores"].detach().cpu().numpy(), ref["anomaly_scores"].detach().numpy(),
-                               rtol=1e-4, atol=1e-5)
-    lref = ref["anomaly_scores"].sum() + 0.5 * ref["direct_predictions"][:, 0].sum() + sum(ref["kl_losses"])
-    lref.backward()
-    for n, p in m.named_parameters():
-        pr = params[n]
-        # (the stem trains here: no apply_memory_efficient_training, so conv1 / bn1 get grads as in the reference)
-        if pr.grad is None or float(pr.grad.abs().max()) == 0.0:
-            assert p.grad is None or float(p.grad.abs().max()) < 1e-9, n
-            continue
-        ref_norm = float(pr.grad.norm())
-        np.testing.assert_allclose(p.grad.cpu().numpy(), pr.grad.numpy(), rtol=3e-3,
-                                   atol=1e-7 + 2e-4 * ref_norm / np.sqrt(pr.numel()), err_msg=n)
+
+    def user_loss(o, _):
+        return o["anomaly_scores"].sum() + 0.5 * o["direct_predictions"][:, 0].sum() + sum(o["kl_losses"])
+
+    m.zero_grad(set_to_none=True)
+    worst, live, _ = _module_pinned_check(m, case, x, user_loss, training=False)
+    assert any(n.startswith("backbone.conv1.") for n in live)  # (the stem trains: the reference module unfrozen)
+    print(f"worst per-tensor relative L2 vs the mask-pinned oracle: {worst:.3g}")
 
 
 @pytest.mark.parametrize("B,T,H,W", [(8, 16, 227, 227)])
@@ -223,11 +254,13 @@ def test_hip_backward_matches_oracle_full_size():
     torch.cuda.synchronize()
     gr = eng.grads.cpu().numpy()
     masks = hip_relu_masks(eng, B * T)
-    ref_grads, ref_losses, _ = pinned_oracle_grads(make_cad_model(case).state_dict(), x, y,
-                                                   co.CadDraws.make(6, 0, 0, B, T), masks)
+    ref_grads, ref_losses, res = pinned_oracle_grads(make_cad_model(case).state_dict(), x, y,
+                                                     co.CadDraws.make(6, 0, 0, B, T), masks)
     assert float(o["losses"][4]) == pytest.approx(float(ref_losses["total"]), rel=1e-4)
     worst = check_pinned_grads(eng, gr, ref_grads)
-    print(f"worst per-tensor relative L2 vs the mask-pinned oracle: {worst:.3g}")
+    flips = check_mask_flips(masks, res["record"], x)
+    print(f"worst per-tensor relative L2 vs the mask-pinned oracle: {worst:.3g}; ReLU decisions that differ from "
+          f"the float64 forward per layer (count, worst |z| / bound): {flips}")
 
 
 @pytest.mark.parametrize("B,T,H,W", [(2, 8, 227, 227), (1, 4, 256, 256), (1, 3, 64, 80)])
@@ -383,6 +416,11 @@ def test_config4_shape_per_rank(dt):
     masks = hip_relu_masks(eng, B * T)
     ref_grads, ref_losses, res = pinned_oracle_grads(make_cad_model(case).state_dict(), x, y,
                                                      co.CadDraws.make(9, 1, 0, B, T), masks)
+    # (bf16: y is stored rounded to 8 bits: 32 units of 2^-8 of the channel's RMS)
+    flips = (check_mask_flips(masks, res["record"], x) if fp32 else
+             check_mask_flips(masks, res["record"], x, ulps=32, unit=2.0 ** -8, accum=False))
+    print(f"config 4 per rank, {dt}: ReLU decisions that differ from the float64 forward (count, worst |z|/bound) "
+          f"{flips}")
     atol = 1e-5 if fp32 else 2e-2
     np.testing.assert_allclose(o["final"].cpu().numpy(), res["out"]["anomaly_scores"].detach().numpy(),
                                rtol=1e-4 if fp32 else 0, atol=atol)
@@ -484,7 +522,8 @@ def test_second_backward_on_one_forward(ci):
 def test_module_api_detection_grads():
     """Detections carry autograd as in the reference (cad:201-222: each frame's boxes are slices of the rescaled
     detector output; the fallback box is a constant): a loss on out["detections"] trains the detector and the
-    backbone under it.  Forced-detection weights (valid boxes), eval mode; every grad vs the oracle."""
+    backbone under it.  Forced-detection weights (valid boxes), eval mode; every grad vs the mask-pinned float64
+    oracle (relative L2 <= 1e-4 per tensor)."""
     from tests.golden.cases import CAD_CASES
     case = dict(next(c for c in CAD_CASES if c["name"] == "forced_b2t4_64"))
     m = make_cad_model(case).cuda()
@@ -492,29 +531,14 @@ def test_module_api_detection_grads():
     B, T = case["B"], case["T"]
     x = co.synth_clips(case["seed"], 0, 0, B, T, case["H"], case["W"])
     coef = torch.tensor([1.0, -0.5, 0.25, 2.0])
-    out = m(x.cuda())
-    loss = sum((d * coef.cuda()).sum() for fr in out["detections"] for d in fr) + out["anomaly_scores"].sum()
-    loss.backward()
-    mc = make_cad_model(case)
-    sd = {k: v.clone() for k, v in mc.state_dict().items()}
-    params = {k: v.requires_grad_(True) for k, v in sd.items() if "running" not in k and "num_batches" not in k}
-    bufs = {k: v for k, v in sd.items() if "running" in k}
-    ref = co.cad_forward(params, bufs, x, co.CadDraws.make(0, 0, 0, B, T), training=False)
+
+    def user_loss(o, cf):
+        return sum((d * cf).sum() for fr in o["detections"] for d in fr) + o["anomaly_scores"].sum()
+
+    worst, live, ref = _module_pinned_check(m, case, x, user_loss, training=False, coef=coef)
     assert sum(int(d.shape[0]) for fr in ref["detections"] for d in fr) > B * T  # live boxes (forced regime)
-    lref = sum((d * coef).sum() for fr in ref["detections"] for d in fr) + ref["anomaly_scores"].sum()
-    lref.backward()
-    det_grad = 0.0
-    for n, p in m.named_parameters():
-        pr = params[n]
-        if pr.grad is None or float(pr.grad.abs().max()) == 0.0:
-            assert p.grad is None or float(p.grad.abs().max()) < 1e-9, n
-            continue
-        if n.startswith("detector."):
-            det_grad = max(det_grad, float(pr.grad.abs().max()))
-        ref_norm = float(pr.grad.norm())
-        np.testing.assert_allclose(p.grad.cpu().numpy(), pr.grad.numpy(), rtol=3e-3,
-                                   atol=1e-7 + 2e-4 * ref_norm / np.sqrt(pr.numel()), err_msg=n)
-    assert det_grad > 0.0
+    assert any(n.startswith("detector.") for n in live)
+    print(f"worst per-tensor relative L2 vs the mask-pinned oracle: {worst:.3g}")
 
 
 @pytest.mark.parametrize("H,W", [(24, 40), (16, 16)])
