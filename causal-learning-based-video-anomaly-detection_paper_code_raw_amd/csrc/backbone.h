@@ -141,6 +141,11 @@ extern int g_wgrad_split_s2;  // stride-2 weight gradients on the split-bf16 ker
 bool conv3_wgrad_x3_supported(const Conv3Layer& L);
 int conv3_wgrad_x3(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
                    int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);
+// fp32 weight gradients (both strides) on the split-bf16 MFMA with transposed LDS fragment reads (conv_x3w.hip)
+extern int g_wgrad_tr, g_wgrad_tr_blocks;  // knobs "conv_wgrad_tr", "conv_wgrad_tr_blocks"
+bool x3_wgrad_tr_supported(const Conv3Layer& L);
+int x3_wgrad_tr(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
+                int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);
 bool conv3_wgrad_patch_supported(const Conv3Layer& L);
 int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
                       int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);

@@ -1096,6 +1096,8 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_patch") g_tune.wgrad_patch = value;
   else if (k == "conv_wgrad_split") g_wgrad_split = value;
   else if (k == "conv_wgrad_split_s2") g_wgrad_split_s2 = value;
+  else if (k == "conv_wgrad_tr") g_wgrad_tr = value;
+  else if (k == "conv_wgrad_tr_blocks") g_wgrad_tr_blocks = value;
   else if (k == "conv_wgrad_s2_blocks") g_wgrad_s2_blocks = value;
   else if (k == "stem_fused") g_stem_fused = value;
   else if (k == "conv_dgrad_s2_x3") g_dgrad_s2_x3 = value;
@@ -1404,7 +1406,7 @@ int conv3_path(const Conv3Layer& L, int kind) {
   else if (kind == 1)
     x3 = g_tune.patch && conv3_x3_supported(L, false);
   else
-    x3 = g_tune.wgrad_patch && conv3_wgrad_x3_supported(L);
+    x3 = g_tune.wgrad_patch && (x3_wgrad_tr_supported(L) || conv3_wgrad_x3_supported(L));
   return x3 ? (g_conv_bf16 ? 1 : 6) : 0;
 }
 
@@ -1413,6 +1415,8 @@ int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const fl
   if (bfc_wgrad_supported(L))
     return bfc_wgrad(L, reinterpret_cast<const __bf16*>(dY), reinterpret_cast<const __bf16*>(src), src_stats, partial,
                      nsplit, partial_cap, st);
+  if (g_tune.wgrad_patch && x3_wgrad_tr_supported(L))
+    return x3_wgrad_tr(L, dY, src, src_stats, partial, nsplit, partial_cap, alone ? g_tune.wgrad_alone_blocks : 0, st);
   if (g_tune.wgrad_patch && conv3_wgrad_x3_supported(L))
     return conv3_wgrad_x3(L, dY, src, src_stats, partial, nsplit, partial_cap,
                           alone ? g_tune.wgrad_alone_blocks : g_tune.wgrad_patch_blocks, st);

@@ -773,7 +773,8 @@ struct CadPlanImpl {
     // shorter chain pays the fork and the join finds it finished
     VAD_TRY(fork(st));
     dir_pre = tail_pre = 0;
-    const bool affine = labels != nullptr && g_cad_dir_affine != 0 && B <= 8;
+    // (train-mode forwards with grads bound only: an eval / probe forward with labels is followed by no loss backward)
+    const bool affine = labels != nullptr && training && grads != nullptr && g_cad_dir_affine != 0 && B <= 8;
     {  // side stream: direct_classifier on the mean over T (cad:525-538, 568-570)
       // (B rows only: one block per 64 columns, so the chain runs layer by layer on many CUs; layers 1-4 unsplit)
       // With labels (and B <= 8) layers 2-4 run in dir_mid together with the loss-mode input-gradient chain of the
@@ -936,15 +937,14 @@ struct CadPlanImpl {
       DirCombineArgs ca{};
       ca.B = B;
       ca.c = causal;
-      ca.nseg = 5;
+      // (four segments: the clip-mean grads are not folded here -- stage 1's avgpool_bwd reads dpool2 + c dpool2[B:]
+      // itself, so d_pooled is not written on this path; debug_buffer "d_pooled" is the non-affine path's)
+      ca.nseg = 4;
       for (int i = 0; i < 4; ++i) {
         ca.src[i] = dg2[i];
         ca.dst[i] = dg[i];
         ca.width[i] = gd[i + 1];
       }
-      ca.src[4] = dpool2;
-      ca.dst[4] = d_pooled;
-      ca.width[4] = 6144;
       TIMED("dir_bwd", dir_combine(ca, st));
       TIMED("dir_bwd", rows_wgrad(mlp_wgrad_args(B, d_glog, gd, LY.dir_w, LY.dir_b, gh, dg, nullptr), st));
       TIMED("dir_bwd", dense_wgrad(dg[0], B, 512, pooled, 6144, G(LY.dir_w[0]), G(LY.dir_b[0]), dense_scratch,

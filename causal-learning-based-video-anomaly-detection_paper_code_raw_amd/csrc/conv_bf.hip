@@ -121,6 +121,26 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
   u32v4 pv[PIT], wv[WIT];
   bool pok[PIT];
   static_assert(PIT >= 1 && WIT >= 1, "staging passes");
+  // piece geometry, loop-invariant (32-bit offsets: the host checks every tensor < 2^31 elements): patch piece it =
+  // (frame im, patch row ry, patch column rx) packed, its NHWC offset from the tile's patch origin, its LDS offset
+  int pgeo[PIT], pgo[PIT], plo[PIT];
+#pragma unroll
+  for (int it = 0; it < PIT; ++it) {
+    const int q = tid + it * NTHR, row = min(q / G8, PROWS - 1);
+    const int im = row / (PH * PW), rr = row % (PH * PW), ry = rr / PW, rx = rr % PW;
+    const int col = S == 1 ? rx : ((rx & 1) ? PWE + (rx >> 1) : (rx >> 1));
+    pgeo[it] = q < PQ ? (im << 16) | (ry << 8) | rx : -1;
+    pgo[it] = ((im * p.IH + ry) * p.IW + rx) * p.C + g8 * 8;
+    plo[it] = ((im * PH + ry) * PW + col) * RP + g8 * 8;
+  }
+  int wgo[WIT], wlo[WIT];  // weight pieces: offset in the image (from row n0, chunk 0) and in LDS
+#pragma unroll
+  for (int it = 0; it < WIT; ++it) {
+    const int q = min(tid + it * NTHR, WQ - 1);
+    const int n = q / (9 * G8), t = (q / G8) % 9;
+    wgo[it] = (n * 9 + (FWD ? t : 8 - t)) * p.C + g8 * 8;
+    wlo[it] = tid + it * NTHR < WQ ? n * WP + t * CB + g8 * 8 : -1;
+  }
   auto origin = [&](int tile, int& img0, int& oy0, int& ox0) {
     img0 = (tile / tiles_per_img) * NI;
     const int tr = tile % tiles_per_img;
@@ -130,36 +150,31 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
   // loads from clamped addresses (no masked-load branches): out-of-range pieces are zeroed when stashed.  Every item
   // issues the same loads (WRES: the resident weight slice is loaded once, before the loop), so the compiler's counted
   // waits (vmcnt) stay exact and never drain the prefetch
+  const __bf16* const wsrc = p.w + (int64_t)n0 * 9 * p.C;
   auto fetch_w = [&](int ch) {
-    const int c0 = ch * CB + g8 * 8;
 #pragma unroll
-    for (int it = 0; it < WIT; ++it) {
-      const int q = min(tid + it * NTHR, WQ - 1);
-      const int n = q / (9 * G8), t = (q / G8) % 9;
-      wv[it] = *reinterpret_cast<const u32v4*>(p.w + ((int64_t)(n0 + n) * 9 + (FWD ? t : 8 - t)) * p.C + c0);
-    }
+    for (int it = 0; it < WIT; ++it) wv[it] = *reinterpret_cast<const u32v4*>(wsrc + wgo[it] + ch * CB);
   };
   auto fetch = [&](int tile, int ch) {
     int img0, oy0, ox0;
     origin(tile, img0, oy0, ox0);
-    const int c0 = ch * CB + g8 * 8;
+    const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+    // (block-uniform) the whole patch inside the frames: only the padding pieces past PQ are masked
+    const bool inner = iy0 >= 0 && ix0 >= 0 && iy0 + PH <= p.IH && ix0 + PW <= p.IW && img0 + NI <= p.NF;
+    const int base = ((img0 * p.IH + iy0) * p.IW + ix0) * p.C + ch * CB;
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
-      const int q = tid + it * NTHR;
-      const int row = min(q / G8, PROWS - 1);
-      const int im = row / (PH * PW), rr = row % (PH * PW);
-      const int iy = oy0 * S - 1 + rr / PW, ix = ox0 * S - 1 + rr % PW, img = img0 + im;
-      pok[it] = q < PQ && img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
-      pv[it] = *reinterpret_cast<const u32v4*>(p.src + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : 0) + c0);
+      const int g = pgeo[it], im = g >> 16, ry = (g >> 8) & 255, rx = g & 255;
+      pok[it] = g >= 0 && (inner || (img0 + im < p.NF && (unsigned)(iy0 + ry) < (unsigned)p.IH &&
+                                     (unsigned)(ix0 + rx) < (unsigned)p.IW));
+      pv[it] = *reinterpret_cast<const u32v4*>(p.src + (pok[it] ? base + pgo[it] : 0));
     }
     if constexpr (!WRES) fetch_w(ch);
   };
   auto stash_w = [&]() {
 #pragma unroll
-    for (int it = 0; it < WIT; ++it) {
-      const int q = tid + it * NTHR;
-      if (q < WQ) *reinterpret_cast<u32v4*>(wl + (q / (9 * G8)) * WP + ((q / G8) % 9) * CB + g8 * 8) = wv[it];
-    }
+    for (int it = 0; it < WIT; ++it)
+      if (wlo[it] >= 0) *reinterpret_cast<u32v4*>(wl + wlo[it]) = wv[it];
   };
   auto stash = [&](int ch) {
     float sc[8], sh[8];
@@ -178,11 +193,7 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
     }
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
-      const int q = tid + it * NTHR;
-      if (q < PQ) {
-        const int row = q / G8;
-        const int im = row / (PH * PW), rr = row % (PH * PW);
-        const int rx = rr % PW, col = S == 1 ? rx : ((rx & 1) ? PWE + (rx >> 1) : (rx >> 1));
+      if (pgeo[it] >= 0) {
         u32v4 v = pok[it] ? pv[it] : u32v4{0u, 0u, 0u, 0u};
         if (bn && pok[it]) {  // zero padding stays zero: the reference pads relu(bn(y)) with zeros
           float f[8];
@@ -191,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
           for (int e = 0; e < 8; ++e) f[e] = relu_nan(fmaf(f[e], sc[e], sh[e]));
           v = f32_to_bf8(f);
         }
-        *reinterpret_cast<u32v4*>(patch + ((im * PH + rr / PW) * PW + col) * RP + g8 * 8) = v;
+        *reinterpret_cast<u32v4*>(patch + plo[it]) = v;
       }
     }
     if constexpr (!WRES) stash_w();
@@ -208,9 +219,18 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
       a[mf] = *reinterpret_cast<const bfv8*>(patch + (arow[mf] + kh * PW + co) * RP + kk * 16 + 8 * h);
   };
 
-  // epilogue: this thread's 8 output channels (group cg) and their block sums
+  // epilogue: this thread's 8 output channels (group cg) and their block sums; piece i = pixel m of the tile, packed
+  // (frame, row, column) and its NHWC offset from the tile's output origin
   const int cg = tid % NG;
   constexpr int EQ = TPX * NG, EIT = (EQ + NTHR - 1) / NTHR;
+  int egeo[EIT], ego[EIT];
+#pragma unroll
+  for (int i = 0; i < EIT; ++i) {
+    const int q = tid + i * NTHR, m = min(q / NG, TPX - 1);
+    const int mi = m / (TH * TW), mr = m % (TH * TW), py = mr / TW, px = mr % TW;
+    egeo[i] = q < EQ ? (mi << 16) | (py << 8) | px : -1;
+    ego[i] = ((mi * p.OH + py) * p.OW + px) * p.N + cg * 8;
+  }
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
@@ -231,20 +251,19 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
     lds_barrier();
     int img0, oy0, ox0;
     origin(tile, img0, oy0, ox0);
-    auto piece = [&](int i, int& m, int64_t& oi) {  // epilogue piece i of this thread: pixel m, NHWC offset (or -1)
-      const int q = tid + i * NTHR;
-      m = min(q / NG, TPX - 1);
-      const int mi = m / (TH * TW), mr = m % (TH * TW);
-      const int img = img0 + mi, oy = oy0 + mr / TW, ox = ox0 + mr % TW;
-      const bool ok = q < EQ && img < p.NF && oy < p.OH && ox < p.OW;
-      oi = ok ? (((int64_t)img * p.OH + oy) * p.OW + ox) * p.N + n0 + cg * 8 : -1;
+    const bool oinner = oy0 + TH <= p.OH && ox0 + TW <= p.OW && img0 + NI <= p.NF;
+    const int obase = ((img0 * p.OH + oy0) * p.OW + ox0) * p.N + n0;
+    auto piece = [&](int i, int& m, int& oi) {  // epilogue piece i of this thread: pixel m, NHWC offset (or -1)
+      const int g = egeo[i], mi = g >> 16, py = (g >> 8) & 255, px = g & 255;
+      m = (mi * TH + py) * TW + px;
+      const bool ok = g >= 0 && (oinner || (img0 + mi < p.NF && oy0 + py < p.OH && ox0 + px < p.OW));
+      oi = ok ? obase + ego[i] : -1;
     };
     if constexpr (!FWD) {
       if (bnb && ch == nch - 1) {
 #pragma unroll
         for (int i = 0; i < EIT; ++i) {
-          int m;
-          int64_t oi;
+          int m, oi;
           piece(i, m, oi);
           yv[i] = *reinterpret_cast<const u32v4*>(p.bny + (oi < 0 ? 0 : oi));
         }
@@ -314,8 +333,7 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
       }
 #pragma unroll
       for (int i = 0; i < EIT; ++i) {
-        int m;
-        int64_t oi;
+        int m, oi;
         piece(i, m, oi);
         const u32v4 ev = *reinterpret_cast<const u32v4*>(epi + m * EP + cg * 8);
         if (oi < 0) continue;
@@ -829,6 +847,8 @@ bool bfc_supported(const Conv3Layer& L, bool fwd) {
 template <int S, int NI, int TH, int TW, int CB, int NCT, bool FWD>
 static int bfc_launch(BfcArgs a, int64_t max_blocks, hipStream_t st, int* nparts) {
   VAD_CHECK(a.C % CB == 0 && a.N % (32 * NCT) == 0, "bfc_conv: channel counts");
+  VAD_CHECK((int64_t)a.NF * a.IH * a.IW * a.C < (1ll << 31) && (int64_t)a.NF * a.OH * a.OW * a.N < (1ll << 31),
+            "bfc_conv: tensors of 2^31 elements or more (32-bit offsets)");
   a.tiles_h = (int)cdiv(a.OH, TH);
   a.tiles_w = (int)cdiv(a.OW, TW);
   a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);

@@ -1,0 +1,322 @@
+// Weight gradient of the backbone's 3x3 convs (causal_anomaly_detection.py:128-139) for the fp32 configs on the
+// split-bf16 MFMA, built on transposed LDS reads:
+//   dW[co][tap][ci] = sum_p dY[p][co] * relu(bn(x))[p + off(tap)][ci]   (zero padding, stride 1 or 2).
+// GEMM view per tap: M = output channels (A = dY^T), N = input channels (B = the shifted input), K = output pixels;
+// fp32 operands are split three ways (hi + mid + lo bf16 planes, the six products whose magnitude reaches fp32
+// resolution, smallest first: conv_x3.hip's numerics).  Both operands need 8 consecutive pixels of one channel per
+// lane -- the transpose of the NHWC rows the loads deliver -- so the LDS images keep NHWC order, [pixel][32 channels]
+// per plane (64-B rows), and the fragments are read with ds_read_b64_tr_b16 (per 16-lane group 4 rows x 16 columns
+// delivered column-major), two reads per plane fragment: the staging is one 16-B load + BN/ReLU + split + three 8-B
+// LDS stores per 4 channels, no register transposition (conv_x3.hip's weight-gradient kernels spend ~10 VALU per MFMA
+// on the transposition and the unaligned column shifts).
+// MFMA shape 16x16x32 (K = 32 pixels = 4 blocks of 8 consecutive pixels of one tile row, one per 16-lane group): a wave
+// owns 32 co x 16 ci x 9 taps = 72 accumulator registers (a 32x32 tile over 9 taps would take 144 and leave no room
+// for the register prefetch of the next tile at 2 waves per SIMD).  The two 16-lane groups of a 32-lane half read the
+// same 32-B column half of rows 8 apart; with 64-B rows those share banks, so a row's two 32-B halves are swapped when
+// bit 3 of its LDS row index is set (each lane supplies its own row address, so the swizzle is per lane) -- both
+// halves of every 32-lane read then hit distinct banks.  Stride 2: patch columns stored parity-split ([even | odd]),
+// so 4 consecutive output pixels read 4 consecutive LDS rows for every tap.
+// A block owns NCO co tiles of 32 x 32 input channels and a strided set of pixel tiles (2 blocks per CU); wave w takes
+// ci half w & 1 and either co tile w >> 1 (NCO = 2) or K half w >> 1 (NCO = 1, summed in a fixed order).  The block's
+// sum lands in split-K slab blockIdx.z ([S][Co][9 Ci], conv3_wgrad_reduce).
+#include <algorithm>
+
+#include "backbone.h"
+
+namespace vad {
+
+namespace {
+
+typedef float f32x4w __attribute__((ext_vector_type(4)));
+typedef __bf16 bfv8w __attribute__((ext_vector_type(8)));
+typedef __bf16 bfv4w __attribute__((ext_vector_type(4)));
+typedef short s16x4w __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bfv8w trf(const __bf16* a0, const __bf16* a1) {
+  typedef __attribute__((address_space(3))) s16x4w lds_s16x4;
+  const s16x4w u = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  const s16x4w v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  const bfv4w x = __builtin_bit_cast(bfv4w, u), y = __builtin_bit_cast(bfv4w, v);
+  return bfv8w{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+}
+
+// 4 fp32 values -> hi / mid / lo bf16 planes (8 B each)
+__device__ __forceinline__ void split4(const f32x4 v, bfv4w& hi, bfv4w& mid, bfv4w& lo) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const __bf16 h = (__bf16)v[e];
+    const float r = v[e] - (float)h;
+    const __bf16 m = (__bf16)r;
+    hi[e] = h;
+    mid[e] = m;
+    lo[e] = (__bf16)(r - (float)m);
+  }
+}
+
+__device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+}  // namespace
+
+struct TrwArgs {
+  const float* dY;     // [NF][OH][OW][Co]
+  const float* src;    // [NF][IH][IW][Ci]
+  const float* scale;  // BN + ReLU on load (nullable)
+  const float* shift;
+  float* slab;         // [S][Co][9 Ci]
+  int NF, IH, IW, Ci, OH, OW, Co;
+  int tiles_h, tiles_w, ntiles;
+  int dy_bytes, x_bytes;  // buffer extents (< 2^31)
+};
+
+template <int S, int NI, int TH, int TW, int NCO>
+__global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
+  constexpr int TPX = NI * TH * TW, KS = TPX / 32, KSW = NCO == 2 ? KS : KS / 2;
+  static_assert(TW % 8 == 0 && TPX % 32 == 0 && KS % (3 - NCO) == 0 && (NCO == 1 || NCO == 2), "whole K steps");
+  constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3, PWE = (PW + 1) / 2, PROWS = NI * PH * PW;
+  constexpr int YPL = TPX * 32, XPL = (PROWS + 1) * 32;  // one plane's image (bf16 elements; + a junk row)
+  __shared__ __attribute__((aligned(16))) __bf16 sm[3 * (NCO * YPL + XPL)];
+  __bf16* const ys = sm;                  // [co tile][plane][TPX][32]
+  __bf16* const xs = sm + 3 * NCO * YPL;  // [plane][PROWS][32]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;  // transposed-read roles
+  const int co0 = blockIdx.x * 32 * NCO, ci0 = blockIdx.y * 32;
+  const int tiles_per_img = p.tiles_h * p.tiles_w;
+  const int chalf = wave & 1, ct = NCO == 2 ? wave >> 1 : 0, ks0 = NCO == 2 ? 0 : (wave >> 1) * KSW;
+  const bool bn = p.scale != nullptr;
+
+  // staging pieces: 4 channels (16 B fp32) of one pixel; thread-constant channel group c4 (256 % 8 == 0)
+  constexpr int YQ = TPX * 8 * NCO, YIT = YQ / 256;
+  constexpr int XQ = PROWS * 8, XIT = (XQ + 255) / 256;
+  static_assert(YQ % 256 == 0, "whole dY staging passes");
+  const int c4 = tid & 7;
+  f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+  if (bn) {
+    sc = *reinterpret_cast<const f32x4*>(p.scale + ci0 + c4 * 4);
+    sh = *reinterpret_cast<const f32x4*>(p.shift + ci0 + c4 * 4);
+  }
+  // loop-invariant piece geometry: dY piece it -> (co tile, frame, row, column) of the tile, packed (the co tile is the
+  // slowest index: a 32-lane store covers 4 whole rows of one image); input piece -> (frame, patch row, patch column)
+  int ygeo[YIT], xgeo[XIT];
+#pragma unroll
+  for (int it = 0; it < YIT; ++it) {
+    const int q = tid + it * 256, cg = q / (TPX * 8), m = (q % (TPX * 8)) >> 3;
+    const int mi = m / (TH * TW), mr = m % (TH * TW);
+    ygeo[it] = (cg << 24) | (mi << 16) | ((mr / TW) << 8) | (mr % TW);
+  }
+#pragma unroll
+  for (int it = 0; it < XIT; ++it) {
+    const int q = tid + it * 256, row = q >> 3;
+    const int mi = row / (PH * PW), rr = row % (PH * PW), ry = rr / PW, rx = rr % PW;
+    xgeo[it] = q < XQ ? (mi << 16) | (ry << 8) | rx : -1;
+  }
+  // element offset of (LDS row, channel col) in a [rows][32] image: 32-B halves swapped on rows with bit 3 set
+  auto soff = [](int row, int col) { return row * 32 + (col ^ (((row >> 3) & 1) << 4)); };
+
+  f32x4w acc[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[t][u] = f32x4w{0.f, 0.f, 0.f, 0.f};
+
+  // the next tile's pieces are loaded into registers while this tile's MFMAs run.  Buffer loads with 32-bit offsets
+  // (the host keeps every tensor below 2^31 bytes): a piece outside the frames takes an offset past the buffer's end
+  // and loads zeros, so every tile issues the same loads with no branches and the counted waits never drain the
+  // prefetch; xmask keeps which input pieces are real (BN + ReLU apply to those only)
+  constexpr int OOB = 0x7ffffff0;
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void*)p.dY, (short)0, p.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.src, (short)0, p.x_bytes, 0x00020000);
+  f32x4 yv[YIT], xv[XIT];
+  int xmask = 0;
+  auto fetch = [&](int tile) {
+    const int img0 = (tile / tiles_per_img) * NI, tr = tile % tiles_per_img;
+    const int y0 = (tr / p.tiles_w) * TH, x0 = (tr % p.tiles_w) * TW;
+    const int iy0 = S * y0 - 1, ix0 = S * x0 - 1;
+    const int ybase = (((img0 * p.OH + y0) * p.OW + x0) * p.Co + co0 + c4 * 4) * 4;
+    const int xbase = (((img0 * p.IH + iy0) * p.IW + ix0) * p.Ci + ci0 + c4 * 4) * 4;
+#pragma unroll
+    for (int it = 0; it < YIT; ++it) {
+      const int g = ygeo[it], cg = g >> 24, mi = (g >> 16) & 255, py = (g >> 8) & 255, px = g & 255;
+      const int ok = (img0 + mi < p.NF) & (y0 + py < p.OH) & (x0 + px < p.OW);
+      const int off = ybase + ((((mi * p.OH + py) * p.OW + px) * p.Co + cg * 32) << 2);
+      yv[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, ok ? off : OOB, 0, 0));
+    }
+    xmask = 0;
+#pragma unroll
+    for (int it = 0; it < XIT; ++it) {
+      const int g = xgeo[it], mi = (g >> 16) & 255, ry_ = (g >> 8) & 255, rx_ = g & 255;
+      const int ok = (g >= 0) & (img0 + mi < p.NF) & ((unsigned)(iy0 + ry_) < (unsigned)p.IH) &
+                     ((unsigned)(ix0 + rx_) < (unsigned)p.IW);
+      const int off = xbase + ((((mi * p.IH + ry_) * p.IW + rx_) * p.Ci) << 2);
+      xv[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : OOB, 0, 0));
+      xmask |= ok << it;
+    }
+  };
+  fetch(blockIdx.z);  // (the launch keeps gridDim.z <= ntiles)
+  for (int tile = blockIdx.z; tile < p.ntiles; tile += gridDim.z) {
+    int ltid = tid;  // (laundered: the stash addresses are recomputed per tile rather than held in registers)
+    asm volatile("" : "+v"(ltid));
+    lds_bar();  // the previous tile's fragment reads are done
+#pragma unroll
+    for (int it = 0; it < YIT; ++it) {
+      const int q = ltid + it * 256, cg = q / (TPX * 8), m = (q % (TPX * 8)) >> 3;
+      bfv4w a, b, c;
+      split4(yv[it], a, b, c);
+      __bf16* d = ys + cg * 3 * YPL + soff(m, c4 * 4);
+      *reinterpret_cast<bfv4w*>(d) = a;
+      *reinterpret_cast<bfv4w*>(d + YPL) = b;
+      *reinterpret_cast<bfv4w*>(d + 2 * YPL) = c;
+    }
+#pragma unroll
+    for (int it = 0; it < XIT; ++it) {
+      const int g = xgeo[it];
+      const int mi = (g >> 16) & 255, ry_ = (g >> 8) & 255, rx_ = g & 255;
+      const int col = S == 1 ? rx_ : ((rx_ & 1) ? PWE + (rx_ >> 1) : (rx_ >> 1));  // stride 2: [even | odd] columns
+      f32x4 v = xv[it];
+      if (bn) {  // zero padding stays zero (the reference pads relu(bn(y)) with zeros)
+        const bool ok = (xmask >> it) & 1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // (selects, no branches; NaN propagates like torch's relu)
+          const float r = fmaf(v[e], sc[e], sh[e]);
+          const float z = r != r ? r : fmaxf(r, 0.f);
+          v[e] = ok ? z : 0.f;
+        }
+      }
+      bfv4w a, b, c;
+      split4(v, a, b, c);
+      // (the pieces past the patch, last pass only, land in the junk row behind the image)
+      const int row = (it + 1) * 256 <= XQ || g >= 0 ? (mi * PH + ry_) * PW + col : PROWS;
+      __bf16* d = xs + soff(row, c4 * 4);
+      *reinterpret_cast<bfv4w*>(d) = a;
+      *reinterpret_cast<bfv4w*>(d + XPL) = b;
+      *reinterpret_cast<bfv4w*>(d + 2 * XPL) = c;
+    }
+    lds_bar();
+    fetch(min(tile + (int)gridDim.z, p.ntiles - 1));
+    // (laundered per tile: the swizzled fragment addresses are recomputed in the loop, not hoisted into ~60 registers)
+    int lm = 8 * grp + q4;
+    asm volatile("" : "+v"(lm));
+#pragma unroll
+    for (int k = 0; k < KSW; ++k) {
+      // this lane's pixel rows: m (read 0) and m + 4 (read 1) of K step ks0 + k, group grp's 8-pixel block
+      const int m = (ks0 + k) * 32 + lm;
+      const int mi = m / (TH * TW), mr = m % (TH * TW), oy = mr / TW, ox = mr % TW;
+      const int xrow = (mi * PH + S * oy) * PW + ox;  // patch LDS row of tap (0, 0)
+      bfv8w a[2][3];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const __bf16* base = ys + ct * 3 * YPL + q * YPL;
+          a[u][q] = trf(base + soff(m, 16 * u + 4 * p4), base + soff(m + 4, 16 * u + 4 * p4));
+        }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int kh = t / 3, kw = t % 3;
+        const int cs = S == 1 ? kw : ((kw & 1) ? PWE + (kw >> 1) : (kw >> 1));
+        const int r0 = xrow + kh * PW + cs;
+        const int o0 = soff(r0, 16 * chalf + 4 * p4), o1 = soff(r0 + 4, 16 * chalf + 4 * p4);
+        bfv8w b[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) b[q] = trf(xs + q * XPL + o0, xs + q * XPL + o1);
+        // the six products that reach fp32 resolution, smallest first (a: dY planes hi/mid/lo, b: input planes)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          f32x4w c = acc[t][u];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][2], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][1], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][0], b[2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][1], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][0], b[1], c, 0, 0, 0);
+          acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][0], b[0], c, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+
+  // C of a 16x16 tile: lane l, register r -> row (co) 4 (l >> 4) + r, column (ci) l & 15
+  float* out = p.slab + (int64_t)blockIdx.z * p.Co * 9 * p.Ci;
+  const int cob = co0 + ct * 32 + 4 * grp, cic = ci0 + 16 * chalf + (lane & 15);
+  if constexpr (NCO == 1) {  // K halves: waves 2, 3 hand theirs to waves 0, 1 (fixed order)
+    float* red = reinterpret_cast<float*>(sm);  // [2 waves][72][64]
+    __syncthreads();
+    if (wave >= 2) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[((chalf * 9 + t) * 8 + u * 4 + r) * 64 + lane] = acc[t][u][r];
+    }
+    __syncthreads();
+    if (wave >= 2) return;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[t][u][r] += red[((chalf * 9 + t) * 8 + u * 4 + r) * 64 + lane];
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(int64_t)(cob + 16 * u + r) * 9 * p.Ci + t * p.Ci + cic] = acc[t][u][r];
+}
+
+int g_wgrad_tr = 1;           // knob "conv_wgrad_tr": fp32 weight gradients on x3_wgrad_tr_kernel
+int g_wgrad_tr_blocks = 512;  // knob "conv_wgrad_tr_blocks": its target grid
+
+bool x3_wgrad_tr_supported(const Conv3Layer& L) {
+  const int64_t lim = (int64_t)1 << 31;
+  return g_wgrad_tr && g_conv_split && !g_conv_bf16 && !g_act_bf16 && (L.stride == 1 || L.stride == 2) &&
+         L.Ci % 32 == 0 && L.Co % 32 == 0 && (L.stride == 1 || (L.IH >= 2 * L.OH - 1 && L.IW >= 2 * L.OW - 1)) &&
+         (int64_t)L.NF * L.OH * L.OW * L.Co * 4 < lim - 64 && (int64_t)L.NF * L.IH * L.IW * L.Ci * 4 < lim - 64 &&
+         L.OH < 256 && L.OW < 256;
+}
+
+template <int S, int NI, int TH, int TW, int NCO>
+static int trw_launch(TrwArgs a, int target_blocks, int64_t partial_cap, hipStream_t st, int* nsplit) {
+  a.tiles_h = (int)cdiv(a.OH, TH);
+  a.tiles_w = (int)cdiv(a.OW, TW);
+  a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);
+  const int pairs = (a.Co / (32 * NCO)) * (a.Ci / 32);
+  int64_t z = std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, pairs), a.ntiles));
+  z = std::min<int64_t>(z, std::max<int64_t>(1, partial_cap / ((int64_t)a.Co * 9 * a.Ci)));
+  VAD_KLAUNCH((x3_wgrad_tr_kernel<S, NI, TH, TW, NCO>), dim3(a.Co / (32 * NCO), a.Ci / 32, (unsigned)z), dim3(256),
+              0, st, a);
+  VAD_LAUNCH_CHECK();
+  *nsplit = (int)z;
+  return 0;
+}
+
+int x3_wgrad_tr(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
+                int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st) {
+  VAD_CHECK(x3_wgrad_tr_supported(L), "x3_wgrad_tr: unsupported layer");
+  VAD_CHECK(partial_cap >= (int64_t)L.Co * 9 * L.Ci, "x3_wgrad_tr: slab capacity below one split");
+  TrwArgs a{};
+  a.dY = dY;
+  a.src = src;
+  a.scale = src_stats ? src_stats + 2 * L.Ci : nullptr;
+  a.shift = src_stats ? src_stats + 3 * L.Ci : nullptr;
+  a.slab = slab;
+  a.NF = L.NF; a.IH = L.IH; a.IW = L.IW; a.Ci = L.Ci; a.OH = L.OH; a.OW = L.OW; a.Co = L.Co;
+  a.dy_bytes = (int)((int64_t)L.NF * L.OH * L.OW * L.Co * 4);
+  a.x_bytes = (int)((int64_t)L.NF * L.IH * L.IW * L.Ci * 4);
+  const int tb = target_blocks > 0 ? target_blocks : g_wgrad_tr_blocks;
+  // tiles of 64 pixels (both co tiles of a 64-channel slice share the staged patch) or, for 32-channel layers, 128
+  // pixels; at most ~80 KB of LDS so that 2 blocks fit a CU
+  const bool c64 = L.Co % 64 == 0;
+  if (L.stride == 2) {
+    if (L.OW <= 8) return c64 ? trw_launch<2, 1, 8, 8, 2>(a, tb, partial_cap, st, nsplit)
+                              : trw_launch<2, 1, 8, 8, 1>(a, tb, partial_cap, st, nsplit);
+    return c64 ? trw_launch<2, 1, 4, 16, 2>(a, tb, partial_cap, st, nsplit)
+               : trw_launch<2, 1, 4, 16, 1>(a, tb, partial_cap, st, nsplit);
+  }
+  if (!c64) return trw_launch<1, 1, 8, 16, 1>(a, tb, partial_cap, st, nsplit);
+  if (L.OW <= 8 && L.OH <= 8) return trw_launch<1, 1, 8, 8, 2>(a, tb, partial_cap, st, nsplit);
+  return trw_launch<1, 1, 4, 16, 2>(a, tb, partial_cap, st, nsplit);
+}
+
+}  // namespace vad
