@@ -99,11 +99,13 @@ def family_roofline(fam, live, pl, args, act_bytes):
     flops = byts = ms_tot = ideal_s = 0.0
     launches = 0
     paths = {}
+    per_layer = {}
     for lab, (ms, n) in live.items():
         f, _, lay = lab.partition("/L")
         if f != fam:
             continue
         l = int(lay)
+        per_layer[lab] = round(1e3 * ms / max(n, 1), 2)
         work = algorithmic_work(lab, B, T, H, W)[1]
         flops += work * n
         byts += conv_bytes(fam, l, B, T, H, W, act_bytes) * n
@@ -131,6 +133,7 @@ def family_roofline(fam, live, pl, args, act_bytes):
     r["launches_timed"] = launches
     r["avg_launch_us"] = round(1e3 * ms_tot / max(launches, 1), 2)
     r["kernel_paths"] = paths
+    r["per_layer_us"] = dict(sorted(per_layer.items()))
     tag = f"cfg{args.config}"
     traffic, src = pmc_family("pmc_traffic", tag, fam, "hbm_bytes_per_launch")
     if traffic is not None:
@@ -280,7 +283,7 @@ def run_gpu(args, rank, world, local_rank):
                               "(weight gradients included: they overlap the input gradients on their own stream)")
     if critical != dominant:
         roof["critical_stream"] = families[critical]
-    roof["families"] = {f: {k: r[k] for k in ("achieved", "frac", "avg_launch_us", "launches_timed")}
+    roof["families"] = {f: {k: r[k] for k in ("achieved", "frac", "avg_launch_us", "launches_timed", "per_layer_us")}
                         for f, r in families.items()}
     step_ms = 1e3 * elapsed / args.steps
     # parity probe (rank 0): one more forward on the first batch with the trained weights; the CPU leg re-runs it on

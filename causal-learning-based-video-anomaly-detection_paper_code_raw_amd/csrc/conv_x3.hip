@@ -186,6 +186,28 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
   // prefetch loads are unconditional (out-of-range lanes read a valid dummy address) and the zero padding is applied
   // at stash time from these bits, so no masked-load branch makes the compiler wait for the loads before the MFMAs
   bool pok[PIT], wok[WIT];
+  // loop-invariant piece geometry, 32-bit offsets (the host keeps every tensor below 2^31 elements): patch piece it =
+  // (image, patch row, input column) packed (-1: past the patch), its NHWC offset from the tile's patch origin and its
+  // LDS offset; weight piece it = its offset from row n0 of chunk 0 (-1: past the slice or the last channel)
+  int pgeo[PIT], pgo[PIT], plo[PIT], wgo[WIT], wlo[WIT];
+#pragma unroll
+  for (int it = 0; it < PIT; ++it) {
+    const int q = tid + it * NTHR;
+    const int row = prow(q), r = min(row, PROWS - 1);
+    const int im = r / (PH * PW), rr = r % (PH * PW), ry = rr / PW, scol = rr % PW;
+    // (stride 2: staging items run in the stored, parity-split column order, see stash)
+    const int rx = S == 1 ? scol : (scol < PWE ? 2 * scol : 2 * (scol - PWE) + 1);
+    pgeo[it] = row < PROWS ? (im << 16) | (ry << 8) | rx : -1;
+    pgo[it] = ((im * p.IH + ry) * p.IW + rx) * p.C + g8p * 8;
+    plo[it] = ((im * PH + ry) * PW + scol) * RP + g8p * 8;
+  }
+#pragma unroll
+  for (int it = 0; it < WIT; ++it) {
+    const int q = min(tid + it * NTHR, WQ - 1);
+    const int n = q / (9 * G8), t = (q / G8) % 9;
+    wgo[it] = (tid + it * NTHR < WQ && n0 + n < p.N) ? (n * 9 + (FWD ? t : 8 - t)) * p.C + g8 * 8 : -1;
+    wlo[it] = tid + it * NTHR < WQ ? n * WP + t * NP * PC + g8 * 8 : -1;
+  }
   auto origin = [&](int tile, int& img0, int& oy0, int& ox0) {
     img0 = (tile / tiles_per_img) * NI;
     const int tr = tile % tiles_per_img;
@@ -196,42 +218,45 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
     int img0, oy0, ox0;
     origin(tile, img0, oy0, ox0);
     const int kd = ch / nchc, c0 = (ch - kd * nchc) * PC;
+    const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+    if constexpr (KD == 1) {
+      // (block-uniform) the whole patch inside the frames: only the pieces past the patch are masked
+      const bool inner = iy0 >= 0 && ix0 >= 0 && iy0 + PH <= p.IH && ix0 + PW <= p.IW && img0 + NI <= p.NF;
+      const int base = ((img0 * p.IH + iy0) * p.IW + ix0) * p.C + c0;
 #pragma unroll
-    for (int it = 0; it < PIT; ++it) {
-      const int q = tid + it * NTHR;
-      const int row = prow(q);
-      const int im = row / (PH * PW), rr = row % (PH * PW);
-      // (stride 2: staging items run in the stored, parity-split column order, see stash)
-      const int sc = rr % PW, rx = S == 1 ? sc : (sc < PWE ? 2 * sc : 2 * (sc - PWE) + 1);
-      const int iy = oy0 * S - 1 + rr / PW, ix = ox0 * S - 1 + rx;
-      int img = img0 + im;
-      bool dok = true;
-      if constexpr (KD == 3) {  // depth slice d + kd - 1 of the same clip
-        const int d = img % p.D + kd - 1;
-        dok = d >= 0 && d < p.D;
-        img += kd - 1;
+      for (int it = 0; it < PIT; ++it) {
+        const int g = pgeo[it], im = (g >> 16) & 255, ry = (g >> 8) & 255, rx = g & 255;
+        pok[it] = g >= 0 && (inner || (img0 + im < p.NF && (unsigned)(iy0 + ry) < (unsigned)p.IH &&
+                                       (unsigned)(ix0 + rx) < (unsigned)p.IW));
+        const TA* s = src + (pok[it] ? base + pgo[it] : 0);
+        pv[it][0] = act_ld4(s);
+        pv[it][1] = act_ld4(s + 4);
       }
-      pok[it] = row < PROWS && dok && img0 + im < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
-      const TA* s = src + c0 + g8p * 8 + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
-      pv[it][0] = act_ld4(s);
-      pv[it][1] = act_ld4(s + 4);
+    } else {
+#pragma unroll
+      for (int it = 0; it < PIT; ++it) {
+        const int g = pgeo[it], im = (g >> 16) & 255, ry = (g >> 8) & 255, rx = g & 255;
+        const int iy = iy0 + ry, ix = ix0 + rx;
+        // depth slice d + kd - 1 of the same clip
+        const int img = img0 + im + kd - 1, d = (img0 + im) % p.D + kd - 1;
+        pok[it] = g >= 0 && d >= 0 && d < p.D && img0 + im < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
+        const TA* s = src + c0 + g8p * 8 + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
+        pv[it][0] = act_ld4(s);
+        pv[it][1] = act_ld4(s + 4);
+      }
     }
     if (weights) {
+      const float* wsrc = p.w + ((int64_t)kd * p.N + n0) * 9 * p.C + c0;
 #pragma unroll
       for (int it = 0; it < WIT; ++it) {
-        const int q = tid + it * NTHR;
-        const int n = q / (9 * G8), t = (q / G8) % 9;
-        wok[it] = q < WQ && n0 + n < p.N;
-        const float* s = p.w + (int64_t)kd * p.N * 9 * p.C + c0 + g8 * 8 +
-                         (wok[it] ? ((int64_t)(n0 + n) * 9 + (FWD ? t : 8 - t)) * p.C : (int64_t)0);
+        wok[it] = wgo[it] >= 0;
+        const float* s = wok[it] ? wsrc + wgo[it] : p.w;
         wv[it][0] = *reinterpret_cast<const f32x4*>(s);
         wv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
       }
     }
   };
   auto stash = [&](int tile, int ch, bool weights) {
-    int img0, oy0, ox0;
-    origin(tile, img0, oy0, ox0);
     const int c0 = (ch % nchc) * PC;
     // (BN constants loaded and used unconditionally -- from a dummy address when there is no BN -- so no load is
     // left pending on a branch the waitcnt analysis would have to assume, which made it drain the prefetch loads
@@ -248,50 +273,43 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
     }
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
-      const int q = tid + it * NTHR;
-      const int row = prow(q);
-      if (row < PROWS) {
-        const int im = row / (PH * PW), rr = row % (PH * PW);
-        const int ry = rr / PW;
+      if (pgeo[it] >= 0) {
         float v[8];
         const f32x4 v0 = act_f4(pv[it][0]), v1 = act_f4(pv[it][1]);
+        const bool ok = pok[it];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = pok[it] ? v0[e] : 0.f;
-          v[4 + e] = pok[it] ? v1[e] : 0.f;
+          v[e] = ok ? v0[e] : 0.f;
+          v[4 + e] = ok ? v1[e] : 0.f;
         }
         if constexpr (FWD) {
-          // zero padding stays zero: padded taps read 0 in the reference's zero-padded relu(bn(y))
-          const bool app = bn && pok[it];
+          if (bn) {  // zero padding stays zero (padded taps read 0 in the reference's zero-padded relu(bn(y)));
+                     // selects, no branches; NaN propagates like torch's relu
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float a0 = relu_nan(fmaf(v[e], sc[0][e], sh[0][e]));
-            const float a1 = relu_nan(fmaf(v[4 + e], sc[1][e], sh[1][e]));
-            v[e] = app ? a0 : v[e];
-            v[4 + e] = app ? a1 : v[4 + e];
+            for (int e = 0; e < 4; ++e) {
+              const float a0 = fmaf(v0[e], sc[0][e], sh[0][e]), a1 = fmaf(v1[e], sc[1][e], sh[1][e]);
+              v[e] = (a0 <= 0.f || !ok) ? 0.f : a0;
+              v[4 + e] = (a1 <= 0.f || !ok) ? 0.f : a1;
+            }
           }
         }
         // stride 2: item rr % PW is already the stored column ([even input columns | odd ones]), so the 8 rows a
         // 16-lane ds_write_b128 phase covers are consecutive patch rows -- distinct bank quads at the odd 16-B pitch
         // (raw column order alternated between the two halves: SQ_LDS_BANK_CONFLICT 0.43-0.52 of the LDS cycles)
-        const int col = rr % PW;
-        __bf16* d = patch + ((im * PH + ry) * PW + col) * RP + g8p * 8;
-        put_planes<NP>(d, PC, v, false);
+        put_planes<NP>(patch + plo[it], PC, v, false);
       }
     }
     if (weights) {
 #pragma unroll
       for (int it = 0; it < WIT; ++it) {
-        const int q = tid + it * NTHR;
-        if (q < WQ) {
-          const int n = q / (9 * G8), t = (q / G8) % 9;
+        if (wlo[it] >= 0) {
           float v[8];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             v[e] = wok[it] ? wv[it][0][e] : 0.f;
             v[4 + e] = wok[it] ? wv[it][1][e] : 0.f;
           }
-          put_planes<NP>(wl + n * WP + (WCH > 1 ? (c0 / PC) * WCS : 0) + t * NP * PC + g8 * 8, PC, v, false);
+          put_planes<NP>(wl + wlo[it] + (WCH > 1 ? (c0 / PC) * WCS : 0), PC, v, false);
         }
       }
     }
@@ -688,6 +706,8 @@ template <int S, int NI, int TH, int TW, int NT, int PC, bool FWD, int NP, int W
 static int launch_np(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   VAD_CHECK(!g_act_bf16 || NP == 1, "conv3x3_x3: bf16 activations need the bf16-operand kernels (conv_bf16)");
   VAD_CHECK(WCH == 1 || a.C == WCH * PC, "conv3x3_x3: resident weights need C == WCH * PC");
+  VAD_CHECK((int64_t)a.NF * a.IH * a.IW * a.C < ((int64_t)1 << 31) && (int64_t)a.N * 9 * a.C < ((int64_t)1 << 31),
+            "conv3x3_x3: 32-bit staging offsets (input and weight images below 2^31 elements)");
   a.tiles_h = (int)cdiv(a.OH, TH);
   a.tiles_w = (int)cdiv(a.OW, TW);
   a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);

@@ -194,8 +194,8 @@ WGRAD_CASES = [(2, 32, 32, 19, 17, 1), (32, 256, 256, 8, 8, 1), (32, 128, 256, 1
 
 
 def _wgrad_path(nat, patch):
-    """3: split-bf16 transposed-read kernel for both strides (default, conv_x3w.hip), 4: the older split-bf16 kernels
-    (conv_x3.hip), 1: f32 LDS-patch kernel for stride-1 layers, 2: f32 LDS-patch kernel for all strides, 0:
+    """3: split-bf16 transposed-read kernel for both strides (default, conv_x3w.hip), 4: the
+    older split-bf16 kernels (conv_x3.hip), 1: f32 LDS-patch kernel for stride-1 layers, 2: f32 LDS-patch kernel for all strides, 0:
     implicit-GEMM path."""
     split = patch in (3, 4)
     nat.lib().vad_set_tuning(b"conv_wgrad_patch", 1 if split else patch)

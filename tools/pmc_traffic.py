@@ -26,8 +26,13 @@ def _targs(name):
 def family(name):
     if "conv3x3_wgrad_patch_kernel" in name or ("gemm_kernel" in name and "ConvPatchKM" in name):
         return "conv_wgrad"
-    if "conv3x3_wgrad_x3_kernel" in name or "conv3x3_wgrad_x3nt_kernel" in name:
+    if ("conv3x3_wgrad_x3_kernel" in name or "conv3x3_wgrad_x3nt_kernel" in name or "x3_wgrad_tr_kernel" in name
+            or "bfc_wgrad_kernel" in name):
         return "conv_wgrad"
+    if "bfc_conv_kernel" in name:  # <S, NI, TH, TW, CB, NCT, FWD, WRES>
+        return "conv_fwd" if _targs(name)[6:7] == ["true"] else "conv_dgrad"
+    if "bfc_dgrad_s2_kernel" in name:
+        return "conv_dgrad"
     if "conv3x3_x3_kernel" in name:  # <S, NI, TH, TW, NT, PC, FWD, NP>
         return "conv_fwd" if _targs(name)[6:7] == ["true"] else "conv_dgrad"
     if "conv3x3_patch_kernel" in name:
