@@ -46,6 +46,7 @@ _SIGS = {
     "vad_cad_backward_stage": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "vad_cad_wait_side": (_I, [_P, _P]),
     "vad_cad_wait_layer_grads": (_I, [_P, _I, _P]),
+    "vad_cad_input_ready": (_I, [_P, _P]),
     "vad_cad_backward_ext": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vad_cad_optimizer_step": (_I, [_P, _F, _F, _F, _F, _F, _F, _F, _P, _P]),
     "vad_dense_forward": (_I, [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I64, _P]),

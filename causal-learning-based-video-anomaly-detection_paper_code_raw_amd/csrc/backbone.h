@@ -17,6 +17,7 @@ extern int g_x3_big;  // knob "conv_split_big"
 extern int g_x3_pipe;  // knob "conv_split_pipe"
 extern int g_x3_s2big;  // knob "conv_split_s2big"
 extern int g_cad_dir_affine;  // knob "cad_dir_affine": the direct classifier's loss-mode backward precomputed in the forward
+extern int g_cad_stem_early;
 extern int g_cad_prep_stream, g_cad_wgrad_stream, g_cad_det_gate, g_cad_last_wgrad_main, g_cad_event_sysfence,
     g_cad_dy_per_layer, g_cad_l0_slab, g_cad_stream_prio;  // knobs "cad_prep_stream", "cad_wgrad_stream" (A/B)
 extern int g_stem_fused;  // knob "stem_fused" (default 1)

@@ -15,6 +15,7 @@ int g_cad_prep_stream = 1;   // knob "cad_prep_stream": weight relayouts on the 
 int g_cad_last_wgrad_main = 1;  // knob "cad_last_wgrad_main": layer 0's weight gradient on the caller's stream
 int g_cad_event_sysfence = 0;  // knob "cad_event_sysfence": system-scope fence on the plan's stream-order events
 int g_cad_dy_per_layer = 1;  // knob "cad_dy_per_layer" (A/B of the plan option dy_per_layer)
+int g_cad_stem_early = 1;  // knob "cad_stem_early": an armed forward (vad_cad_input_ready) runs its stem early (0: off)
 int g_cad_det_gate = 1;      // knob "cad_det_gate": the backbone backward waits on the device detector gate
 int g_cad_dir_affine = 1;  // knob "cad_dir_affine": direct classifier backward as A + c beta, precomputed in the forward
 int g_cad_wgrad_stream = 1;  // knob "cad_wgrad_stream": backbone weight gradients on their own stream
@@ -1109,6 +1110,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "cad_dir_affine") g_cad_dir_affine = value;
   else if (k == "cad_det_gate") g_cad_det_gate = value;
+  else if (k == "cad_stem_early") g_cad_stem_early = value;
   else if (k == "cad_dy_per_layer") g_cad_dy_per_layer = value;
   else if (k == "cad_event_sysfence") g_cad_event_sysfence = value;
   else if (k == "mlp_tail_wide") g_mlp_tail_wide = value;

@@ -333,6 +333,7 @@ struct CadPlanImpl {
   int32_t* steps = nullptr;
   // workspace carve
   float *y1, *pool, *y[8], *stats[9], *parts, *wf[8], *wd[8], *feats, *pooled;
+  float *poolb[2] = {nullptr, nullptr}, *stats0b[2] = {nullptr, nullptr}, *parts_stem = nullptr;
   float *dh[5], *dlog, *gh[5], *glog;
   float* wt[5] = {};  // transposed detector_net weights of layers 1-4 (mlp_tail_fwd)
   float *head_ws, *head_rows;
@@ -392,6 +393,14 @@ struct CadPlanImpl {
   // layer's split-K reduce on the queue that ran it (layer 0: also after the stem backward), for per-layer
   // data-parallel gradient buckets (vad_cad_wait_layer_grads)
   hipEvent_t ev_layer[8] = {};
+  // early stem (vad_cad_input_ready): the frozen stem of the armed forward runs on the weight-gradient stream (behind
+  // the previous step's weight gradients of layers 7..1) once the inputs are ready (ev_input), beside what the
+  // caller's stream still has queued (layer 0's weight gradient, the optimizer); its outputs (pool, bn1's state
+  // stats[0]) alternate between two sets, set p free again once the backward of the forward that used it has read
+  // layer 0's input (ev_stem_free[p]).  (A stream of its own measured 2x slower steps at config 2 -- 3.46 vs 1.72 ms
+  // -- whatever GPU_MAX_HW_QUEUES; the side stream 1.77 ms, behind the prep's wait for the previous step)
+  hipEvent_t ev_input = nullptr, ev_stem = nullptr, ev_stem_free[2] = {nullptr, nullptr};
+  int input_armed = 0, spar = 0;
   int wgrad_stream = 1;  // option "wgrad_stream" (0: weight gradients on the caller's stream)
   int streams() {
     if (!st2) {
@@ -415,6 +424,9 @@ struct CadPlanImpl {
       VAD_HIP(hipEventCreateWithFlags(&ev_wgj, evf));
       VAD_HIP(hipEventCreateWithFlags(&ev_prep, evf));
       for (int l = 0; l < 8; ++l) VAD_HIP(hipEventCreateWithFlags(&ev_layer[l], evf));
+      VAD_HIP(hipEventCreateWithFlags(&ev_input, evf));
+      VAD_HIP(hipEventCreateWithFlags(&ev_stem, evf));
+      for (int b = 0; b < 2; ++b) VAD_HIP(hipEventCreateWithFlags(&ev_stem_free[b], evf));
     }
     return 0;
   }
@@ -448,6 +460,10 @@ struct CadPlanImpl {
     if (ev_prep) (void)hipEventDestroy(ev_prep);
     for (int l = 0; l < 8; ++l)
       if (ev_layer[l]) (void)hipEventDestroy(ev_layer[l]);
+    if (ev_input) (void)hipEventDestroy(ev_input);
+    if (ev_stem) (void)hipEventDestroy(ev_stem);
+    for (int b = 0; b < 2; ++b)
+      if (ev_stem_free[b]) (void)hipEventDestroy(ev_stem_free[b]);
     if (st3) (void)hipStreamDestroy(st3);
     if (st2) (void)hipStreamDestroy(st2);
   }
@@ -473,7 +489,9 @@ struct CadPlanImpl {
   void carve(Ws& w) {
     const int64_t nf = NF;
     y1 = ws_stem ? w.take<float>(nf * H1 * W1 * 32) : nullptr;
-    pool = w.take<float>(nf * HP * WP * 32);
+    poolb[0] = pool = w.take<float>(nf * HP * WP * 32);
+    // (the early stem's second set: only for the fused frozen stem)
+    poolb[1] = ws_stem ? nullptr : w.take<float>(nf * HP * WP * 32);
     act_max = nf * HP * WP * 32;
     for (int l = 0; l < 8; ++l) {
       y[l] = w.take<float>(nf * L[l].OH * L[l].OW * L[l].Co);
@@ -484,6 +502,9 @@ struct CadPlanImpl {
     }
     const int cs[9] = {32, 32, 32, 64, 64, 128, 128, 256, 256};
     for (int l = 0; l < 9; ++l) stats[l] = w.take<float>(BN_STATS_PER_C * cs[l]);
+    stats0b[0] = stats[0];
+    stats0b[1] = w.take<float>(BN_STATS_PER_C * 32);
+    spar = 0;
     parts_floats = std::max<int64_t>((int64_t)conv1_num_parts(NF, H1) * 64, 1024);
     // (the training stem's bn1 backward reduces over all NF * H1 * W1 conv1 outputs: bn_rows_parts <= cdiv(M, 64))
     parts_floats = std::max<int64_t>(parts_floats, cdiv((int64_t)nf * H1 * W1, 64) * 2 * 32);
@@ -493,6 +514,7 @@ struct CadPlanImpl {
       parts_floats = std::max<int64_t>(parts_floats, conv3_patch_blocks(nf, L[l].OH, L[l].OW) * 2 * L[l].Co);
     }
     parts = w.take<float>(parts_floats);
+    parts_stem = ws_stem ? nullptr : w.take<float>(std::max<int64_t>((int64_t)conv1_num_parts(NF, H1) * 64, 1024));
     feats = w.take<float>(nf * 6144);
     pooled = w.take<float>((int64_t)B * 6144);
     const int dd[5] = {512, 256, 128, 64, 20};
@@ -685,9 +707,9 @@ struct CadPlanImpl {
   // batch statistics of BN layer i (0 = bn1) from the `np` partials in `parts`: local (default) or, with a sync
   // callback in training mode, over the whole process group (torch.nn.SyncBatchNorm semantics)
   int bn_fwd_stats(int i, int np, int C, double count, const float* gamma, const float* beta, hipStream_t st,
-                   int cm = 0) {
+                   int cm = 0, const float* pparts = nullptr) {
     if (sync_fn == nullptr || !training) {
-      TIMED("bn_fin", bn_finalize(parts, np, C, count, gamma, beta, RM(i), RV(i), 0.1f, 1e-5f, training, stats[i],
+      TIMED("bn_fin", bn_finalize(pparts ? pparts : parts, np, C, count, gamma, beta, RM(i), RV(i), 0.1f, 1e-5f, training, stats[i],
                                   st, cm));
       return 0;
     }
@@ -739,12 +761,30 @@ struct CadPlanImpl {
     }
     int np = 0;
     bwd_state = 0;
+    // early stem: armed by vad_cad_input_ready, frozen fused stem, per-rank BN statistics
+    const bool early = g_cad_stem_early && input_armed && !y1_fresh && poolb[1] && (sync_fn == nullptr || !training);
+    input_armed = 0;
+    if (early) {
+      spar ^= 1;
+      pool = poolb[spar];
+      stats[0] = stats0b[spar];
+    }
     if (!y1_fresh) {
       // frozen stem (the training default): conv1 + BN sums + pooling of the raw output in one pass (stem.hip);
       // `pool` then holds the pooled conv1 output and layer1.0 applies bn1 + ReLU on load
-      TIMED("conv1", stem_fused(x, NF, H, W, P(LY.conv1_w), P(LY.conv1_b), P(LY.bn1_w), H1, W1, pool, HP, WP, parts,
+      hipStream_t st = early ? st3 : st0;
+      float* sp = early ? parts_stem : parts;
+      if (early) {
+        VAD_HIP(hipStreamWaitEvent(st, ev_input, 0));
+        VAD_HIP(hipStreamWaitEvent(st, ev_stem_free[spar], 0));
+      }
+      TIMED("conv1", stem_fused(x, NF, H, W, P(LY.conv1_w), P(LY.conv1_b), P(LY.bn1_w), H1, W1, pool, HP, WP, sp,
                                 &np, st));
-      VAD_TRY(bn_fwd_stats(0, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), st, 1));  // column-major
+      VAD_TRY(bn_fwd_stats(0, np, 32, (double)NF * H1 * W1, P(LY.bn1_w), P(LY.bn1_b), st, 1, sp));  // column-major
+      if (early) {
+        VAD_HIP(hipEventRecord(ev_stem, st));
+        VAD_HIP(hipStreamWaitEvent(st0, ev_stem, 0));
+      }
       pool_stats = stats[0];
     } else {
       // training stem: the backward's MaxPool / bn1 / conv1 gradients read conv1's output y1
@@ -1013,6 +1053,7 @@ struct CadPlanImpl {
         TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], slab, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
         if (wgs && !on_main) VAD_HIP(hipEventRecord(ev_wg[l & 1], st));
         if (l > 0 || !stem_grad) VAD_HIP(hipEventRecord(ev_layer[l], st));
+        if (l == 0) VAD_HIP(hipEventRecord(ev_stem_free[spar], st));  // (layer 0's input read: set spar free)
       }
       fused_np = 0;
       if (l > 0) {
@@ -1311,6 +1352,15 @@ int vad_cad_wait_side(vad_cad_plan* plan, void* stream) {
   return plan->impl.wait_side((hipStream_t)stream);
 }
 
+int vad_cad_input_ready(vad_cad_plan* plan, void* stream) {
+  VAD_CHECK(plan != nullptr, "vad_cad_input_ready: null plan");
+  CadPlanImpl& c = plan->impl;
+  VAD_TRY(c.streams());
+  VAD_HIP(hipEventRecord(c.ev_input, (hipStream_t)stream));
+  c.input_armed = 1;
+  return 0;
+}
+
 int vad_cad_wait_layer_grads(vad_cad_plan* plan, int layer, void* stream) {
   VAD_CHECK(plan != nullptr && layer >= 0 && layer < 8, "vad_cad_wait_layer_grads: null plan or layer outside 0..7");
   CadPlanImpl& c = plan->impl;
@@ -1378,6 +1428,7 @@ int vad_cad_set_option(vad_cad_plan* plan, const char* key, int64_t value) {
   else if (std::string(key) == "wgrad_stream") plan->impl.wgrad_stream = value ? 1 : 0;
   else if (std::string(key) == "dy_per_layer") plan->impl.dy_per_layer = value ? 1 : 0;
   else if (std::string(key) == "act_bf16") plan->impl.act_bf16_opt = value ? 1 : 0;
+  else if (std::string(key) == "input_armed" && value == 0) plan->impl.input_armed = 0;  // (arming: vad_cad_input_ready)
   else { vad::set_error("vad_cad_set_option: unknown key"); return 1; }
   return 0;
 }

@@ -204,10 +204,17 @@ class CadEngine:
         B, T, C, H, W = x.shape
         if C != 1:
             raise ValueError("ResNetBackbone here takes single-channel frames (input_channels=1, cad:515)")
+        x0 = x
         x = x.contiguous().float()
         pl = self.plan(B, T, H, W)
         # (before the forward: a training stem needs conv1's activation stored, a frozen one is recomputed in place)
         self._set_stem_grad(pl)
+        armed, self._armed = getattr(self, "_armed", None), None
+        if armed is not None and armed is not pl:  # (armed for another plan: that arm must not outlive this call)
+            nat.check(nat.lib().vad_cad_set_option(armed.h, b"input_armed", 0))
+        elif armed is pl and x.data_ptr() != x0.data_ptr():  # the input was converted here, on the current stream
+            nat.check(nat.lib().vad_cad_input_ready(pl.h, ctypes.c_void_p(
+                torch.cuda.current_stream(self.device).cuda_stream)))
         dev = self.device
         if not want_outputs:
             if self._loss_buf is None:
@@ -264,6 +271,15 @@ class CadEngine:
         queued backbone backward is final (per-layer data-parallel buckets)."""
         pl = self._last[0]
         nat.check(nat.lib().vad_cad_wait_layer_grads(pl.h, layer, ctypes.c_void_p(stream.cuda_stream)))
+
+    def input_ready(self, B: int, T: int, H: int, W: int, stream=None):
+        """Arm the next forward of the (B, T, H, W) plan: its input clips are complete once the work queued on `stream`
+        (a torch.cuda.Stream; default: the current stream) at this call is, so its frozen stem may run beside what
+        the current stream still has queued (the previous step's tail).  One-shot (vad_cad_input_ready)."""
+        pl = self.plan(B, T, H, W)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        nat.check(nat.lib().vad_cad_input_ready(pl.h, ctypes.c_void_p(s.cuda_stream)))
+        self._armed = pl
 
     def wait_side(self, stream):
         """Make `stream` (a torch.cuda.Stream) wait for everything queued so far on the last plan's side stream (the

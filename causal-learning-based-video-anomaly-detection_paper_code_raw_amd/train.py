@@ -84,6 +84,7 @@ class CadTrainer:
         self.bb_buckets = [(first[lo], first[hi], lo) for lo, hi in ((7, 8), (6, 7), (4, 6), (0, 4))]
         self.allreduce_floats = 0  # floats all-reduced by the last step (per rank, before the ring's 2(P-1)/P factor)
         self.prio_stream = None
+        self._bufs_init, self._bufs_ev, self._arm_stream = False, None, None
         if prio_stream and self.eng.grads.is_cuda:
             self.prio_stream = torch.cuda.Stream(self.eng.device, priority=-1)
         if self.dist:
@@ -96,26 +97,53 @@ class CadTrainer:
             self._bn_pg = dist.new_group(ranks=ranks)
             self.eng.set_bn_sync(self._bn_pg)
 
-    def step(self, videos, labels, lr=None, want_outputs=False):
+    def step(self, videos, labels, lr=None, want_outputs=False, inputs_ready=None):
         """One training step; returns the (device) loss vector [cls, anomaly, causal, kl, total] (want_outputs: the
-        forward's output dict, see CadEngine.forward)."""
+        forward's output dict, see CadEngine.forward).  inputs_ready: None -- the clips are produced on the current
+        stream, the step is ordered after it; True -- they are complete on the device already (staged and
+        synchronised before); a torch.cuda.Stream -- its queued work completes them.  Given, the frozen stem may start
+        beside the previous step's queued tail (CadEngine.input_ready)."""
         if self.prio_stream is not None and self.eng.grads.is_cuda:
             # the step's critical path on a stream of the device's greatest priority (the plan's weight-gradient stream
             # runs at its least with knob cad_stream_prio), ordered after / before the caller's stream
             caller = torch.cuda.current_stream(self.eng.device)
             self.prio_stream.wait_stream(caller)
             with torch.cuda.stream(self.prio_stream):
-                o = self._step(videos, labels, lr, want_outputs)
+                o = self._step(videos, labels, lr, want_outputs, inputs_ready)
             caller.wait_stream(self.prio_stream)
             return o
-        return self._step(videos, labels, lr, want_outputs)
+        return self._step(videos, labels, lr, want_outputs, inputs_ready)
 
-    def _step(self, videos, labels, lr, want_outputs):
+    def _step(self, videos, labels, lr, want_outputs, inputs_ready=None):
         eng = self.eng
         B = videos.shape[0]
-        if self.dist and not self.sync_bn:
+        cur = torch.cuda.current_stream(eng.device) if eng.grads.is_cuda else None
+        bcast = self.dist and not self.sync_bn
+        if bcast and not self._bufs_init:
+            # (the buffers of rank 0, before the first forward; later steps take them right after each forward)
             dist.broadcast(eng.bufs, 0, group=self.pg)
+            self._bufs_init = True
+            if cur is not None:
+                self._bufs_ev = torch.cuda.Event()
+                self._bufs_ev.record(cur)
+        if inputs_ready is not None and cur is not None:
+            # the early stem waits for the inputs and for the last buffer broadcast (it updates bn1's running stats),
+            # not for the previous step's tail on the current stream
+            if self._arm_stream is None:
+                self._arm_stream = torch.cuda.Stream(eng.device)
+            if inputs_ready is not True:
+                self._arm_stream.wait_stream(inputs_ready)
+            if self._bufs_ev is not None:
+                self._arm_stream.wait_event(self._bufs_ev)
+            T, H, W = videos.shape[1], videos.shape[3], videos.shape[4]
+            eng.input_ready(B, T, H, W, stream=self._arm_stream)
         o = eng.forward(videos, True, self.seed, self.step_idx, self.rank * B, labels, want_outputs=want_outputs)
+        if bcast:
+            # the running statistics are final once the forward has run (the backward does not touch them): every
+            # rank takes rank 0's here -- the values the reference's replicas start the next step from
+            dist.broadcast(eng.bufs, 0, group=self.pg)
+            if cur is not None:
+                self._bufs_ev.record(cur)
         self.allreduce_floats = 0
         if self.dist and eng.grads.is_cuda:
             self._backward_overlapped()

@@ -96,6 +96,13 @@ int vad_cad_wait_side(vad_cad_plan* plan, void* stream);
  * the backbone backward queued last is final -- the per-layer buckets of a data-parallel gradient all-reduce, issued
  * while the layers below are still in their backward (DDP's reduce-during-backward, cad:688-690). */
 int vad_cad_wait_layer_grads(vad_cad_plan* plan, int layer, void* stream);
+/* vad_cad_input_ready(plan, s) arms the NEXT vad_cad_forward of this plan (one-shot): its input clips are complete
+ * once the work queued on stream s at this call is.  With the frozen fused stem (and per-rank BatchNorm statistics)
+ * that forward then runs conv1 + bn1 + the max pool on a plan stream ordered after that point only -- not after
+ * what the caller's stream still has queued, e.g. the previous step's last weight gradient and optimizer step --
+ * and layer1.0 waits for it.  Without the call a forward orders its stem after the caller's stream, as before.
+ * (No reference counterpart: the reference's forward is synchronous, cad:669-690.) */
+int vad_cad_input_ready(vad_cad_plan* plan, void* stream);
 /* vad_cad_backward_stage with one more upstream grad: d_boxes [B,T,5,4] (may be NULL), the grad of a loss on the
  * forward's compacted per-frame detections (boxes output of vad_cad_forward; the reference's detections are slices
  * of the rescaled detector output and carry autograd, cad:201-222).  The constant fallback box takes no grad. */

@@ -134,7 +134,7 @@ def _world1_worker(rank, backend, port, sync_bn, forced, out_path):
         dist.destroy_process_group()
 
 
-def _world1_run(sync_bn, forced, force_dist):
+def _world1_run(sync_bn, forced, force_dist, early=False, steps=2):
     from tests.golden.cases import FORCED_A, force_detector
     from vad_amd.cad import CausalAnomalyDetector
     from vad_amd.train import CadTrainer
@@ -146,14 +146,47 @@ def _world1_run(sync_bn, forced, force_dist):
     tr = CadTrainer(m, lr=3e-4, seed=0, sync_bn=sync_bn, force_dist=force_dist)
     assert tr.dist == force_dist and tr.sync_bn == (sync_bn and force_dist)
     x, y = make_batches(1, **SHAPE)[0]
-    floats = []
-    for _ in range(2):
-        tr.step(x.cuda(), y.cuda())
+    x, y = x.cuda(), y.cuda()
+    torch.cuda.synchronize()  # (early: the clips are complete before every step)
+    floats, losses = [], []
+    for _ in range(steps):
+        losses.append(tr.step(x, y, inputs_ready=True if early else None).clone())
         floats.append(tr.allreduce_floats)
         tr.allreduce_floats = 0
     torch.cuda.synchronize()
     return {"params": tr.eng.params.cpu(), "bufs": tr.eng.bufs.cpu(), "grads": tr.eng.grads.cpu(),
-            "floats": torch.tensor(floats), "det_range": torch.tensor(tr.det_range)}
+            "floats": torch.tensor(floats), "det_range": torch.tensor(tr.det_range),
+            "losses": torch.stack(losses).cpu()}
+
+
+def _early_worker(rank, port, early, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        torch.save(_world1_run(False, False, force_dist=True, early=early, steps=3), out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_early_stem_equals_serial_steps(tmp_path):
+    """CadTrainer.step(inputs_ready=True): each step's frozen stem runs on the plan's stem stream beside the previous
+    step's queued tail (vad_cad_input_ready; pool and bn1's state alternate between two sets).  Three steps equal
+    three serial steps bit for bit -- params, BN buffers (bn1's running statistics are updated on the stem stream),
+    grads, losses -- both single-process and with the data-parallel protocol forced on over RCCL at world 1 (the
+    BN-buffer broadcast right after each forward, which the next early stem waits for)."""
+    plain = _world1_run(False, False, force_dist=False, early=False, steps=3)
+    early = _world1_run(False, False, force_dist=False, early=True, steps=3)
+    for k in ("params", "bufs", "grads", "losses"):
+        assert torch.equal(early[k], plain[k]), k
+    res = {}
+    for e in (False, True):
+        out = str(tmp_path / f"early{int(e)}.pt")
+        mp.spawn(_early_worker, args=(_free_port(), e, out), nprocs=1, join=True)
+        res[e] = torch.load(out, weights_only=True)
+    for k in ("params", "bufs", "grads", "losses"):
+        assert torch.equal(res[True][k], res[False][k]), k
+        assert torch.equal(res[True][k], plain[k]), k
 
 
 @pytest.mark.gpu
