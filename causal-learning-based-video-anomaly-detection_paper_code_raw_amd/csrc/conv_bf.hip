@@ -194,12 +194,17 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
       if (pgeo[it] >= 0) {
-        u32v4 v = pok[it] ? pv[it] : u32v4{0u, 0u, 0u, 0u};
-        if (bn && pok[it]) {  // zero padding stays zero: the reference pads relu(bn(y)) with zeros
+        const bool ok = pok[it];
+        u32v4 v = ok ? pv[it] : u32v4{0u, 0u, 0u, 0u};
+        if (bn) {  // zero padding stays zero: the reference pads relu(bn(y)) with zeros (selects, no branch; NaN
+                   // propagates like torch's relu)
           float f[8];
-          bf8_to_f32(v, f);
+          bf8_to_f32(pv[it], f);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = relu_nan(fmaf(f[e], sc[e], sh[e]));
+          for (int e = 0; e < 8; ++e) {
+            const float r = fmaf(f[e], sc[e], sh[e]);
+            f[e] = (r <= 0.f || !ok) ? 0.f : r;
+          }
           v = f32_to_bf8(f);
         }
         *reinterpret_cast<u32v4*>(patch + plo[it]) = v;
@@ -462,47 +467,87 @@ __global__ __launch_bounds__(256, 2) void bfc_wgrad_kernel(const BfwArgs p) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
+  // loop-invariant piece geometry, 32-bit offsets from the tile's origin (the host keeps every tensor below 2^31
+  // elements): dY DMA piece u (pixel packed (frame, row, column)), patch DMA piece k (stored row -> (frame, patch row,
+  // input column)), fix-up piece it
+  constexpr int XIW = (XI + 3) / 4, FQ = (PROWS * 4 + 255) / 256;
+  int ygeo[YI / 4], xgeo[XIW], fgeo[FQ];
+#pragma unroll
+  for (int u = 0; u < YI / 4; ++u) {
+    const int i = wave + 4 * u, f = i / (TPX / 16), pb = i % (TPX / 16);
+    const int m = pb * 16 + (lane >> 2);
+    const int mi = m / (TH * TW), mr = m % (TH * TW), py = mr / TW, px = mr % TW;
+    ygeo[u] = (f << 24) | (mi << 16) | (py << 8) | px;
+  }
+  auto patch_geo = [&](int row) {
+    const int mi = row / (PH * PW), rr = row % (PH * PW), col = rr % PW;
+    const int rx = S == 1 ? col : (col < PWE ? 2 * col : 2 * (col - PWE) + 1);
+    return (mi << 16) | ((rr / PW) << 8) | rx;
+  };
+#pragma unroll
+  for (int k = 0; k < XIW; ++k) {
+    const int g = patch_geo(min((wave + 4 * k) * 16 + (lane >> 2), PROWS - 1));  // stored row
+    xgeo[k] = g;
+  }
+#pragma unroll
+  for (int it = 0; it < FQ; ++it) {
+    const int q = tid + it * 256;
+    fgeo[it] = q < PROWS * 4 ? patch_geo(q >> 2) : -1;
+  }
+
   for (int tile = blockIdx.z; tile < p.ntiles; tile += gridDim.z) {
     const int img0 = (tile / tiles_per_img) * NI, tr = tile % tiles_per_img;
     const int y0 = (tr / p.tiles_w) * TH, x0 = (tr % p.tiles_w) * TW;
     const bool ragged = img0 + NI > p.NF || y0 + TH > p.OH || x0 + TW > p.OW;
+    const int iy0 = S * y0 - 1, ix0 = S * x0 - 1;
+    // (block-uniform) the whole patch inside the frames
+    const bool xin = iy0 >= 0 && ix0 >= 0 && iy0 + PH <= p.IH && ix0 + PW <= p.IW && img0 + NI <= p.NF;
+    const int ybase = ((img0 * p.OH + y0) * p.OW + x0) * p.Co + co0;
+    const int xbase = ((img0 * p.IH + iy0) * p.IW + ix0) * p.Ci + ci0;
+    auto xok = [&](int g) {
+      return xin || (img0 + (g >> 16) < p.NF && (unsigned)(iy0 + ((g >> 8) & 255)) < (unsigned)p.IH &&
+                     (unsigned)(ix0 + (g & 255)) < (unsigned)p.IW);
+    };
     lds_barrier();  // the previous tile's fragment reads are done
 #pragma unroll
     for (int u = 0; u < YI / 4; ++u) {
       const int i = wave + 4 * u, f = i / (TPX / 16), pb = i % (TPX / 16);
-      const int m = pb * 16 + (lane >> 2);
-      const int mi = m / (TH * TW), mr = m % (TH * TW);
-      const int img = img0 + mi, oy = y0 + mr / TW, ox = x0 + mr % TW;
-      const bool ok = img < p.NF && oy < p.OH && ox < p.OW;
-      const __bf16* g = p.dY + (ok ? (((int64_t)img * p.OH + oy) * p.OW + ox) * p.Co : 0) + co0 + f * 32 + (lane & 3) * 8;
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
+      const int g = ygeo[u], mi = (g >> 16) & 255, py = (g >> 8) & 255, px = g & 255;
+      // (pixels outside the map: any in-range row, zeroed by the ragged pass below)
+      const bool ok = !ragged || (img0 + mi < p.NF && y0 + py < p.OH && x0 + px < p.OW);
+      const int off = ((mi * p.OH + py) * p.OW + px) * p.Co + (g >> 24) * 32 + (lane & 3) * 8;
+      const __bf16* gp = p.dY + (ok ? ybase + off : 0);
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)gp,
                                        (__attribute__((address_space(3))) void*)(ys + f * YIMG + pb * 16 * 32), 16, 0, 0);
     }
-    for (int i = wave; i < XI; i += 4) {
-      const int row = min(i * 16 + (lane >> 2), PROWS - 1);  // stored row
-      const int mi = row / (PH * PW), rr = row % (PH * PW), col = rr % PW;
-      const int rx = S == 1 ? col : (col < PWE ? 2 * col : 2 * (col - PWE) + 1);
-      const int img = img0 + mi, iy = S * y0 - 1 + rr / PW, ix = S * x0 - 1 + rx;
-      const bool ok = img < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
-      const __bf16* g = p.src + (ok ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.Ci : 0) + ci0 + (lane & 3) * 8;
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
-                                       (__attribute__((address_space(3))) void*)(xs + i * 16 * 32), 16, 0, 0);
+#pragma unroll
+    for (int k = 0; k < XIW; ++k) {
+      const int i = wave + 4 * k;
+      if (i < XI) {  // (wave-uniform)
+        const int g = xgeo[k];
+        const int off = (((g >> 16) * p.IH + ((g >> 8) & 255)) * p.IW + (g & 255)) * p.Ci + (lane & 3) * 8;
+        const __bf16* gp = p.src + (xok(g) ? xbase + off : 0);
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)gp,
+                                         (__attribute__((address_space(3))) void*)(xs + i * 16 * 32), 16, 0, 0);
+      }
     }
     __syncthreads();  // (vmcnt(0) first: every wave's DMA has landed)
-    for (int q = tid; q < PROWS * 4; q += 256) {
-      const int row = q >> 2;
-      const int mi = row / (PH * PW), rr = row % (PH * PW), col = rr % PW;
-      const int rx = S == 1 ? col : (col < PWE ? 2 * col : 2 * (col - PWE) + 1);
-      const int iy = S * y0 - 1 + rr / PW, ix = S * x0 - 1 + rx;
-      const bool ok = img0 + mi < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
+#pragma unroll
+    for (int it = 0; it < FQ; ++it) {
+      const int g = fgeo[it];
+      if (g < 0) continue;
+      const int row = (tid + it * 256) >> 2;
       u32v4* d = reinterpret_cast<u32v4*>(xs + row * 32 + g4 * 8);
-      if (!ok) {
+      if (!xok(g)) {
         *d = u32v4{0u, 0u, 0u, 0u};  // zero padding stays zero (the reference pads relu(bn(y)) with zeros)
       } else if (bn) {
         float f[8];
         bf8_to_f32(*d, f);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = relu_nan(fmaf(f[e], sc[e], sh[e]));
+        for (int e = 0; e < 8; ++e) {  // (NaN propagates like torch's relu)
+          const float r = fmaf(f[e], sc[e], sh[e]);
+          f[e] = r <= 0.f ? 0.f : r;
+        }
         *d = f32_to_bf8(f);
       }
     }
@@ -966,12 +1011,14 @@ static int bfw_launch(BfwArgs a, int target_blocks, int64_t partial_cap, hipStre
   return 0;
 }
 
-int g_bfw_blocks = 512;  // knob "conv_bfw_blocks": target grid of the bf16 weight gradients
+int g_bfw_blocks = 384;  // knob "conv_bfw_blocks": target grid of the bf16 weight gradients (sweep: 384 best)
 
 int bfc_wgrad(const Conv3Layer& L, const __bf16* dY, const __bf16* src, const float* src_stats, float* slab,
               int* nsplit, int64_t partial_cap, hipStream_t st) {
   VAD_CHECK(bfc_wgrad_supported(L), "bfc_wgrad: unsupported layer");
   VAD_CHECK(partial_cap >= (int64_t)L.Co * 9 * L.Ci, "bfc_wgrad: slab capacity below one split");
+  VAD_CHECK((int64_t)L.NF * L.IH * L.IW * L.Ci < ((int64_t)1 << 31) && (int64_t)L.NF * L.OH * L.OW * L.Co < ((int64_t)1 << 31),
+            "bfc_wgrad: 32-bit staging offsets");
   BfwArgs a{};
   a.dY = dY;
   a.src = src;

@@ -508,17 +508,30 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_x3p_kernel(const X3Args p)
       R.wv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
     }
   };
+  // loop-invariant piece geometry, 32-bit offsets from the tile's patch origin (the host keeps the input below 2^31
+  // elements): patch piece it = (image, patch row, patch column) packed
+  int pgeo[PIT], pgo[PIT];
+#pragma unroll
+  for (int it = 0; it < PIT; ++it) {
+    const int row = min(prow(tid + it * NTHR), PROWS - 1);  // (past the patch: the last row again, see fetch_w)
+    const int im = row / (PH * PW), rr = row % (PH * PW), ry = rr / PW, rx = rr % PW;
+    pgeo[it] = (im << 16) | (ry << 8) | rx;
+    pgo[it] = ((im * p.IH + ry) * p.IW + rx) * p.C + g8p * 8;
+  }
   auto fetch = [&](Regs& R, int item) {
     const int tile = t0 + item / nch, ch = item % nch;
     int img0, oy0, ox0;
     origin(tile, img0, oy0, ox0);
+    const int iy0 = oy0 - 1, ix0 = ox0 - 1;
+    // (block-uniform) the whole patch inside the frames
+    const bool inner = iy0 >= 0 && ix0 >= 0 && iy0 + PH <= p.IH && ix0 + PW <= p.IW && img0 + NI <= p.NF;
+    const int base = ((img0 * p.IH + iy0) * p.IW + ix0) * p.C + ch * PC;
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
-      const int row = min(prow(tid + it * NTHR), PROWS - 1);  // (past the patch: the last row again, see fetch_w)
-      const int im = row / (PH * PW), rr = row % (PH * PW);
-      const int iy = oy0 - 1 + rr / PW, ix = ox0 - 1 + rr % PW;
-      R.pok[it] = img0 + im < p.NF && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
-      const TA* s = src + ch * PC + g8p * 8 + (R.pok[it] ? (((int64_t)(img0 + im) * p.IH + iy) * p.IW + ix) * p.C : (int64_t)0);
+      const int g = pgeo[it], im = g >> 16, ry = (g >> 8) & 255, rx = g & 255;
+      R.pok[it] = inner || (img0 + im < p.NF && (unsigned)(iy0 + ry) < (unsigned)p.IH &&
+                            (unsigned)(ix0 + rx) < (unsigned)p.IW);
+      const TA* s = src + (R.pok[it] ? base + pgo[it] : 0);
       R.pv[it][0] = act_ld4(s);
       R.pv[it][1] = act_ld4(s + 4);
     }
@@ -537,12 +550,15 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_x3p_kernel(const X3Args p)
         v[4 + e] = R.pok[it] ? v1[e] : 0.f;
       }
       if constexpr (FWD) {
-        // zero padding stays zero: padded taps read 0 in the reference's zero-padded relu(bn(y))
-        const bool app = bn && R.pok[it];
+        // zero padding stays zero: padded taps read 0 in the reference's zero-padded relu(bn(y)) (selects, no branch;
+        // NaN propagates like torch's relu)
+        if (bn) {
+          const bool ok = R.pok[it];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float a = relu_nan(fmaf(v[e], bnl[c0 + e], bnl[CMAX + c0 + e]));
-          v[e] = app ? a : v[e];
+          for (int e = 0; e < 8; ++e) {
+            const float a = fmaf(e < 4 ? v0[e] : v1[e - 4], bnl[c0 + e], bnl[CMAX + c0 + e]);
+            v[e] = (a <= 0.f || !ok) ? 0.f : a;
+          }
         }
       }
       put_planes<NP>(pimg + row * RP + g8p * 8, PC, v, false);
@@ -760,6 +776,7 @@ static int launch_pipe(X3Args a, int max_blocks, hipStream_t st, int* nparts) {
   constexpr int PC = 16, NW = 8;
   VAD_CHECK(!g_act_bf16 || NP == 1, "conv3x3_x3p: bf16 activations need the bf16-operand kernels (conv_bf16)");
   VAD_CHECK(a.C % PC == 0 && a.C <= 256 && (WCH == 1 ? a.C > PC : a.C == WCH * PC), "conv3x3_x3p: channel count");
+  VAD_CHECK((int64_t)a.NF * a.IH * a.IW * a.C < ((int64_t)1 << 31), "conv3x3_x3p: 32-bit staging offsets");
   a.tiles_h = (int)cdiv(a.OH, TH);
   a.tiles_w = (int)cdiv(a.OW, TW);
   a.ntiles = (int)(cdiv(a.NF, NI) * a.tiles_h * a.tiles_w);

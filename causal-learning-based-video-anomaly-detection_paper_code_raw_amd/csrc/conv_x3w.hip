@@ -266,7 +266,7 @@ __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
 }
 
 int g_wgrad_tr = 1;           // knob "conv_wgrad_tr": fp32 weight gradients on x3_wgrad_tr_kernel
-int g_wgrad_tr_blocks = 512;  // knob "conv_wgrad_tr_blocks": its target grid
+int g_wgrad_tr_blocks = 384;  // knob "conv_wgrad_tr_blocks": its target grid (1.5 blocks per CU: they share the CUs with the input gradients)
 
 bool x3_wgrad_tr_supported(const Conv3Layer& L) {
   const int64_t lim = (int64_t)1 << 31;
