@@ -9,13 +9,13 @@
 // delivered column-major), two reads per plane fragment: the staging is one 16-B load + BN/ReLU + split + three 8-B
 // LDS stores per 4 channels, no register transposition (conv_x3.hip's weight-gradient kernels spend ~10 VALU per MFMA
 // on the transposition and the unaligned column shifts).
-// MFMA shape 16x16x32 (K = 32 pixels = 4 blocks of 8 consecutive pixels of one tile row, one per 16-lane group): a wave
-// owns 32 co x 16 ci x 9 taps = 72 accumulator registers (a 32x32 tile over 9 taps would take 144 and leave no room
-// for the register prefetch of the next tile at 2 waves per SIMD).  The two 16-lane groups of a 32-lane half read the
-// same 32-B column half of rows 8 apart; with 64-B rows those share banks, so a row's two 32-B halves are swapped when
-// bit 3 of its LDS row index is set (each lane supplies its own row address, so the swizzle is per lane) -- both
-// halves of every 32-lane read then hit distinct banks.  Stride 2: patch columns stored parity-split ([even | odd]),
-// so 4 consecutive output pixels read 4 consecutive LDS rows for every tap.
+// MFMA shape 16x16x32 (K = 32 pixels, 8 per 16-lane group): a wave owns 32 co x 16 ci x 9 taps = 72 accumulator
+// registers (a 32x32 tile over 9 taps would take 144 and leave no room for the register prefetch of the next tile at
+// 2 waves per SIMD).  Each 16-channel half of a plane is an image of its own with 32-B rows, and group g of a K step
+// takes pixels 16 (g >> 1) + 4 (g & 1) + {0..3} (first read) and + 8 (second read): the two groups of a 32-lane half
+// then read 8 consecutive rows of one image, 256 contiguous bytes -- conflict-free with no swizzle, so every tap's
+// fragment is a constant offset (the ds_read immediate) from one base per K step.  Stride 2: patch columns stored
+// parity-split ([even | odd]), so 4 consecutive output pixels read 4 consecutive LDS rows for every tap.
 // A block owns NCO co tiles of 32 x 32 input channels and a strided set of pixel tiles (2 blocks per CU); wave w takes
 // ci half w & 1 and either co tile w >> 1 (NCO = 2) or K half w >> 1 (NCO = 1, summed in a fixed order).  The block's
 // sum lands in split-K slab blockIdx.z ([S][Co][9 Ci], conv3_wgrad_reduce).
@@ -73,10 +73,14 @@ __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
   constexpr int TPX = NI * TH * TW, KS = TPX / 32, KSW = NCO == 2 ? KS : KS / 2;
   static_assert(TW % 8 == 0 && TPX % 32 == 0 && KS % (3 - NCO) == 0 && (NCO == 1 || NCO == 2), "whole K steps");
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3, PWE = (PW + 1) / 2, PROWS = NI * PH * PW;
-  constexpr int YPL = TPX * 32, XPL = (PROWS + 1) * 32;  // one plane's image (bf16 elements; + a junk row)
-  __shared__ __attribute__((aligned(16))) __bf16 sm[3 * (NCO * YPL + XPL)];
-  __bf16* const ys = sm;                  // [co tile][plane][TPX][32]
-  __bf16* const xs = sm + 3 * NCO * YPL;  // [plane][PROWS][32]
+  // one (16-channel half, plane) image; + 128 B so that the two halves of a store phase land on different banks when
+  // that still leaves two blocks per CU (input images: + a junk row for the staging pieces past the patch)
+  constexpr int PAD = 12 * (NCO * (TPX * 16 + 64) + (PROWS + 1) * 16 + 64) <= 81920 ? 64 : 0;
+  constexpr int YH = TPX * 16 + PAD, XH = (PROWS + 1) * 16 + PAD;
+  static_assert(12 * (NCO * YH + XH) <= 81920, "two blocks per CU");
+  __shared__ __attribute__((aligned(16))) __bf16 sm[6 * (NCO * YH + XH)];
+  __bf16* const ys = sm;                  // [co tile][half][plane][TPX][16]
+  __bf16* const xs = sm + 6 * NCO * YH;   // [half][plane][PROWS + 1][16]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;  // transposed-read roles
   const int co0 = blockIdx.x * 32 * NCO, ci0 = blockIdx.y * 32;
@@ -84,18 +88,19 @@ __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
   const int chalf = wave & 1, ct = NCO == 2 ? wave >> 1 : 0, ks0 = NCO == 2 ? 0 : (wave >> 1) * KSW;
   const bool bn = p.scale != nullptr;
 
-  // staging pieces: 4 channels (16 B fp32) of one pixel; thread-constant channel group c4 (256 % 8 == 0)
+  // staging pieces: 4 channels (16 B fp32) of one pixel; thread-constant channel group c4 (256 % 8 == 0): half c4 >> 2,
+  // columns 4 (c4 & 3) .. + 3
   constexpr int YQ = TPX * 8 * NCO, YIT = YQ / 256;
   constexpr int XQ = PROWS * 8, XIT = (XQ + 255) / 256;
   static_assert(YQ % 256 == 0, "whole dY staging passes");
-  const int c4 = tid & 7;
+  const int c4 = tid & 7, chal = c4 >> 2, ccol = (c4 & 3) * 4;
   f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
   if (bn) {
     sc = *reinterpret_cast<const f32x4*>(p.scale + ci0 + c4 * 4);
     sh = *reinterpret_cast<const f32x4*>(p.shift + ci0 + c4 * 4);
   }
   // loop-invariant piece geometry: dY piece it -> (co tile, frame, row, column) of the tile, packed (the co tile is the
-  // slowest index: a 32-lane store covers 4 whole rows of one image); input piece -> (frame, patch row, patch column)
+  // slowest index); input piece -> (frame, patch row, patch column)
   int ygeo[YIT], xgeo[XIT];
 #pragma unroll
   for (int it = 0; it < YIT; ++it) {
@@ -109,8 +114,6 @@ __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
     const int mi = row / (PH * PW), rr = row % (PH * PW), ry = rr / PW, rx = rr % PW;
     xgeo[it] = q < XQ ? (mi << 16) | (ry << 8) | rx : -1;
   }
-  // element offset of (LDS row, channel col) in a [rows][32] image: 32-B halves swapped on rows with bit 3 set
-  auto soff = [](int row, int col) { return row * 32 + (col ^ (((row >> 3) & 1) << 4)); };
 
   f32x4w acc[9][2];
 #pragma unroll
@@ -161,10 +164,10 @@ __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
       const int q = ltid + it * 256, cg = q / (TPX * 8), m = (q % (TPX * 8)) >> 3;
       bfv4w a, b, c;
       split4(yv[it], a, b, c);
-      __bf16* d = ys + cg * 3 * YPL + soff(m, c4 * 4);
+      __bf16* d = ys + (cg * 2 + chal) * 3 * YH + m * 16 + ccol;
       *reinterpret_cast<bfv4w*>(d) = a;
-      *reinterpret_cast<bfv4w*>(d + YPL) = b;
-      *reinterpret_cast<bfv4w*>(d + 2 * YPL) = c;
+      *reinterpret_cast<bfv4w*>(d + YH) = b;
+      *reinterpret_cast<bfv4w*>(d + 2 * YH) = c;
     }
 #pragma unroll
     for (int it = 0; it < XIT; ++it) {
@@ -177,47 +180,50 @@ __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {  // (selects, no branches; NaN propagates like torch's relu)
           const float r = fmaf(v[e], sc[e], sh[e]);
-          const float z = r != r ? r : fmaxf(r, 0.f);
-          v[e] = ok ? z : 0.f;
+          v[e] = (r <= 0.f || !ok) ? 0.f : r;
         }
       }
       bfv4w a, b, c;
       split4(v, a, b, c);
       // (the pieces past the patch, last pass only, land in the junk row behind the image)
       const int row = (it + 1) * 256 <= XQ || g >= 0 ? (mi * PH + ry_) * PW + col : PROWS;
-      __bf16* d = xs + soff(row, c4 * 4);
+      __bf16* d = xs + chal * 3 * XH + row * 16 + ccol;
       *reinterpret_cast<bfv4w*>(d) = a;
-      *reinterpret_cast<bfv4w*>(d + XPL) = b;
-      *reinterpret_cast<bfv4w*>(d + 2 * XPL) = c;
+      *reinterpret_cast<bfv4w*>(d + XH) = b;
+      *reinterpret_cast<bfv4w*>(d + 2 * XH) = c;
     }
     lds_bar();
     fetch(min(tile + (int)gridDim.z, p.ntiles - 1));
-    // (laundered per tile: the swizzled fragment addresses are recomputed in the loop, not hoisted into ~60 registers)
-    int lm = 8 * grp + q4;
+    // this lane's first pixel of a K step: group grp's block 16 (grp >> 1) + 4 (grp & 1), row q4 of the read
+    // (laundered per tile: the fragment bases are recomputed in the loop, not hoisted into registers)
+    int lm = 16 * (grp >> 1) + 4 * (grp & 1) + q4;
     asm volatile("" : "+v"(lm));
 #pragma unroll
     for (int k = 0; k < KSW; ++k) {
-      // this lane's pixel rows: m (read 0) and m + 4 (read 1) of K step ks0 + k, group grp's 8-pixel block
-      const int m = (ks0 + k) * 32 + lm;
-      const int mi = m / (TH * TW), mr = m % (TH * TW), oy = mr / TW, ox = mr % TW;
-      const int xrow = (mi * PH + S * oy) * PW + ox;  // patch LDS row of tap (0, 0)
+      const int m = (ks0 + k) * 32 + lm;  // read 0; read 1: m + 8
+      auto prow = [&](int mm) {            // patch LDS row of tap (0, 0) for tile pixel mm
+        const int mi = mm / (TH * TW), mr = mm % (TH * TW);
+        return (mi * PH + S * (mr / TW)) * PW + mr % TW;
+      };
+      const __bf16* ab = ys + ct * 6 * YH + m * 16 + 4 * p4;
+      const __bf16* xb0 = xs + chalf * 3 * XH + prow(m) * 16 + 4 * p4;
+      const __bf16* xb1 = xs + chalf * 3 * XH + prow(m + 8) * 16 + 4 * p4;
       bfv8w a[2][3];
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          const __bf16* base = ys + ct * 3 * YPL + q * YPL;
-          a[u][q] = trf(base + soff(m, 16 * u + 4 * p4), base + soff(m + 4, 16 * u + 4 * p4));
+          const __bf16* base = ab + (u * 3 + q) * YH;
+          a[u][q] = trf(base, base + 8 * 16);
         }
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int kh = t / 3, kw = t % 3;
         const int cs = S == 1 ? kw : ((kw & 1) ? PWE + (kw >> 1) : (kw >> 1));
-        const int r0 = xrow + kh * PW + cs;
-        const int o0 = soff(r0, 16 * chalf + 4 * p4), o1 = soff(r0 + 4, 16 * chalf + 4 * p4);
+        const int to = (kh * PW + cs) * 16;
         bfv8w b[3];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) b[q] = trf(xs + q * XPL + o0, xs + q * XPL + o1);
+        for (int q = 0; q < 3; ++q) b[q] = trf(xb0 + q * XH + to, xb1 + q * XH + to);
         // the six products that reach fp32 resolution, smallest first (a: dY planes hi/mid/lo, b: input planes)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
