@@ -58,6 +58,7 @@ _SIGS = {
     "vad_cad_conv_path": (_I, [_P, _I, _I]),
     "vad_cad_set_bn_sync": (_I, [_P, BN_SYNC_FN, _P, _I]),
     "vad_u8_to_clip": (_I, [_P, _I64, _I, _P, _P]),
+    "vad_host_device_ptr": (_I, [_P, _P]),
     "vad_resize_u8": (_I, [_P, _I, _I, _P, _I, _I]),
     "vad_debug_d2h": (_I, [_P, _P, _I64]),
     "vad_cad_profile": (_I, [_P, _I, ctypes.c_char_p]),

@@ -763,6 +763,8 @@ struct CadPlanImpl {
     bwd_state = 0;
     // early stem: armed by vad_cad_input_ready, frozen fused stem, per-rank BN statistics
     const bool early = g_cad_stem_early && input_armed && !y1_fresh && poolb[1] && (sync_fn == nullptr || !training);
+    // (armed but not early: the inputs may still be in flight on the arming stream, so the stem waits for them)
+    if (input_armed && !early) VAD_HIP(hipStreamWaitEvent(st0, ev_input, 0));
     input_armed = 0;
     if (early) {
       spar ^= 1;

@@ -4,6 +4,8 @@
 //                                                causal_anomaly_detection.py:92-96, 1177-1179)
 //                     dst = u8 / 255           (mode 1: ToTensor range, minicausal:120, bbox:409-411)
 //                     -- the same float expressions as the synthetic-clip generator (bit-identical results)
+//   vad_host_device_ptr: the device address of pinned (page-locked, mapped) host memory, so vad_u8_to_clip can read a
+//                     staged batch straight over PCIe (ClipStager's direct mode: no copy engine, no u8 device slot)
 //   vad_resize_u8   : bilinear resize with half-pixel centres, border clamping and 11-bit fixed-point weights
 //                     (the scheme of cv2.resize INTER_LINEAR on u8 images that UCSDped2Dataset.__getitem__ calls,
 //                     cad:88-89; restated from its published algorithm, cv2 itself is absent here: parity unpinned
@@ -18,23 +20,30 @@
 
 namespace vad {
 
+typedef unsigned u32x4d __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float u8_pixel(uint32_t u, int mode) {
+  const float f = (float)u;
+  return mode == 0 ? (f - 0.5f) / 0.5f : f / 255.f;
+}
+
+// 16 pixels per lane and iteration (one 16-B load, four 16-B stores): the source may be pinned host memory read over
+// PCIe (vad_host_device_ptr), where wide requests matter; n16 = n / 16 full groups, the tail pixel by pixel
 __global__ __launch_bounds__(256) void u8_to_clip_kernel(const uint8_t* __restrict__ src, int64_t n, int mode,
                                                          float* __restrict__ dst) {
-  const int64_t n4 = n / 4;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const uint32_t w = reinterpret_cast<const uint32_t*>(src)[i];
-    f32x4 o;
+  const int64_t n16 = n / 16;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+    const u32x4d w = reinterpret_cast<const u32x4d*>(src)[i];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float u = (float)((w >> (8 * e)) & 0xffu);
-      o[e] = mode == 0 ? (u - 0.5f) / 0.5f : u / 255.f;
+    for (int q = 0; q < 4; ++q) {
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = u8_pixel((w[q] >> (8 * e)) & 0xffu, mode);
+      reinterpret_cast<f32x4*>(dst)[4 * i + q] = o;
     }
-    reinterpret_cast<f32x4*>(dst)[i] = o;
   }
-  for (int64_t i = n4 * 4 + blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float u = (float)src[i];
-    dst[i] = mode == 0 ? (u - 0.5f) / 0.5f : u / 255.f;
-  }
+  for (int64_t i = n16 * 16 + blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    dst[i] = u8_pixel(src[i], mode);
 }
 
 }  // namespace vad
@@ -45,12 +54,19 @@ extern "C" {
 
 int vad_u8_to_clip(const uint8_t* src, int64_t n, int mode, float* dst, void* stream) {
   VAD_CHECK(mode == 0 || mode == 1, "vad_u8_to_clip: mode 0 (Normalize 0.5/0.5) or 1 (u8/255)");
-  VAD_CHECK((reinterpret_cast<uintptr_t>(src) & 3) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0,
-            "vad_u8_to_clip: src must be 4-byte and dst 16-byte aligned");
+  VAD_CHECK((reinterpret_cast<uintptr_t>(src) & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0,
+            "vad_u8_to_clip: src and dst must be 16-byte aligned");
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(u8_to_clip_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n / 4 + 1, 256), 8192)), dim3(256), 0,
+  // (1024 blocks keep ~4 MB of 16-B requests in flight: enough for HBM, and for PCIe when src is mapped host memory)
+  hipLaunchKernelGGL(u8_to_clip_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n / 16 + 1, 256), 1024)), dim3(256), 0,
                      (hipStream_t)stream, src, n, mode, dst);
   VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int vad_host_device_ptr(const void* host, void** dev) {
+  VAD_CHECK(host != nullptr && dev != nullptr, "vad_host_device_ptr: null argument");
+  VAD_HIP(hipHostGetDevicePointer(dev, const_cast<void*>(host), 0));
   return 0;
 }
 

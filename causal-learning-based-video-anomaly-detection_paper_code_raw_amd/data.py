@@ -7,14 +7,14 @@ clips to the device inside the step (cad:639, mc:266).  Here the loader keeps cl
 * ``FrameFolderClips`` / ``FrameFolderClipsMC`` enumerate the same overlapping clips with the same (synthesised)
   labels as the reference datasets (cad:39-80, mc:104-190) and return ``(T, 1, H, W)`` / ``(1, T, H, W)`` uint8
   frames; decoding is PIL, resizing the native ``vad_resize_u8`` (cv2 INTER_LINEAR scheme, cad:88-89).
-* ``ClipStager`` copies a u8 batch into a ring of pinned host buffers, issues the host-to-device copy on its own
-  HIP stream and converts u8 -> fp32 on the device (``vad_u8_to_clip``: the reference's Normalize(0.5, 0.5) over
-  raw 0..255 pixels, or ToTensor's /255) -- a quarter of the PCIe bytes of fp32 clips, and the copy of batch k+1
-  overlaps step k.
+* ``ClipStager`` keeps u8 batches in pinned host memory, copies them to the device as u8 and converts them to fp32
+  there (``vad_u8_to_clip``: the reference's Normalize(0.5, 0.5) over raw 0..255 pixels, or ToTensor's /255), both
+  on a stream of its own -- a quarter of the PCIe bytes of fp32 clips, and batch k+1's staging overlaps step k.
 * ``prefetch(loader, stager)`` yields device clips one batch ahead.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import random
 
@@ -138,63 +138,106 @@ class FrameFolderClipsMC(torch.utils.data.Dataset):
         return torch.from_numpy(frames).unsqueeze(0), torch.tensor(float(self.labels[idx]), dtype=torch.float32)
 
 
+class _Staged:
+    """An issued batch: its fp32 device clip (being written on the stager's stream) and the event that completes it."""
+    __slots__ = ("out", "ready", "slot")
+
+    def __init__(self, out, ready, slot):
+        self.out, self.ready, self.slot = out, ready, slot
+
+
 class ClipStager:
-    """Pinned u8 staging ring + H2D copies on a dedicated stream + on-device u8 -> fp32 conversion.
+    """Pinned u8 staging + on-device u8 -> fp32 conversion on a stream of its own, one batch ahead of the step.
 
-    Two halves, so the copy of batch k+1 overlaps step k: ``issue(batch_u8)`` puts the batch into a pinned ring slot
-    (skipped when the batch is already pinned) and enqueues its H2D copy on the copy stream, ordered only after the
-    previous conversion out of the same device slot (not after the compute stream's other work); ``finish(handle)``
-    makes the current stream wait for that copy and converts it to the fp32 device clip.  ``stage(batch)`` =
-    ``finish(issue(batch))``.  mode 0: (u8 - 0.5) / 0.5 (cad), 1: u8 / 255 (mc/bbox)."""
+    ``issue(batch_u8)`` enqueues batch k+1's conversion while step k computes and returns a handle; ``finish(handle)``
+    returns its fp32 device clip, ordered on the current stream (``wait=True``) or left to the consumer
+    (``wait=False``: hand ``handle.ready`` to ``CadTrainer.step(inputs_ready=...)``, whose early stem waits for it on
+    the plan's stem stream and the step's critical stream never does).  ``stage(batch)`` = ``finish(issue(batch))``.
+    mode 0: (u8 - 0.5) / 0.5 (cad), 1: u8 / 255 (mc/bbox).
 
-    def __init__(self, device, mode=0, depth=2):
+    direct=False (default): an H2D copy of the u8 batch into a device buffer (the copy engine), then the conversion,
+    both on the stager's stream.  Nothing queued there waits for the step's streams: the u8 and fp32 device buffers
+    are stream-ordered by the caching allocator (the fp32 clip recorded on its consumer's stream), which matters --
+    HIP spreads streams over GPU_MAX_HW_QUEUES (4) hardware queues, and the previous design (a fixed device slot whose
+    copy waited for an event of the step's stream) stalled whichever step stream shared the copy's queue: config 2 at
+    3.0 ms/step on two of the four queues, 1.80 on the others; this one 1.75-1.83 ms on all four against 1.74 ms with
+    clips already in HBM (profiles/r04_h2d_queues.json).  direct=True: the conversion kernel reads the pinned host
+    batch itself over PCIe (``vad_host_device_ptr``), no copy engine and no u8 device buffer (1.86-1.93 ms: the
+    PCIe-bound kernel holds CUs beside the step).
+
+    A batch that is not pinned and contiguous goes through a ring of ``depth`` pinned buffers (a slot is refilled
+    once its previous conversion has finished); a pinned batch is read in place and must not be overwritten until
+    ``handle.ready`` has completed.  Each returned clip is a fresh tensor (recorded on the consuming stream)."""
+
+    def __init__(self, device, mode=0, depth=2, direct=False):
         self.device = torch.device(device)
         nat.require_hip(torch.empty(0, device=self.device))
         self.mode = mode
         self.depth = depth
-        self.copy_stream = torch.cuda.Stream(self.device)
-        self._ring = []  # [pinned u8, device u8, copy-done event, read-done event]
+        self.direct = direct
+        self.stream = torch.cuda.Stream(self.device)
+        self.copy_stream = self.stream  # (the name of earlier releases)
+        self._ring = []  # [pinned u8, device u8 (direct=False), conversion-done event]
         self._k = 0
+        self._dptr = {}  # pinned host pointer -> its device address
 
     def _slot(self, shape):
         if len(self._ring) <= self._k or tuple(self._ring[self._k][0].shape) != tuple(shape):
-            slot = [torch.empty(shape, dtype=torch.uint8, pin_memory=True),
-                    torch.empty(shape, dtype=torch.uint8, device=self.device), torch.cuda.Event(), torch.cuda.Event()]
+            slot = [torch.empty(shape, dtype=torch.uint8, pin_memory=True), None, torch.cuda.Event()]
             if len(self._ring) <= self._k:
                 self._ring.append(slot)
             else:
                 self._ring[self._k] = slot
         return self._ring[self._k]
 
-    def issue(self, batch_u8: torch.Tensor):
-        """Start the H2D copy of one u8 batch; returns the handle for finish()."""
+    def _device_address(self, host: torch.Tensor) -> int:
+        p = host.data_ptr()
+        d = self._dptr.get(p)
+        if d is None:
+            out = ctypes.c_void_p()
+            nat.check(nat.lib().vad_host_device_ptr(p, ctypes.addressof(out)))
+            d = self._dptr[p] = out.value
+            if len(self._dptr) > 64:  # (caller-owned pinned batches come and go)
+                self._dptr.pop(next(iter(self._dptr)))
+        return d
+
+    def issue(self, batch_u8: torch.Tensor) -> _Staged:
+        """Enqueue one u8 batch's conversion (and, direct=False, its H2D copy) on the stager's stream."""
         if batch_u8.dtype != torch.uint8:
             raise TypeError("ClipStager.issue expects a uint8 batch")
-        slot = self._slot(batch_u8.shape)
-        pinned, dev, copied, read = slot
-        if batch_u8.is_pinned():
-            src = batch_u8
+        if batch_u8.numel() == 0:
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+            return _Staged(torch.empty(batch_u8.shape, dtype=torch.float32, device=self.device), ev, None)
+        if batch_u8.is_pinned() and batch_u8.is_contiguous() and batch_u8.data_ptr() % 16 == 0:
+            src, slot, done = batch_u8, None, torch.cuda.Event()
         else:
-            copied.synchronize()  # the previous H2D out of this pinned buffer has finished
-            pinned.copy_(batch_u8)
-            src = pinned
-        self.copy_stream.wait_event(read)  # the previous u8 -> fp32 conversion out of this device slot is done
-        with torch.cuda.stream(self.copy_stream):
-            dev.copy_(src, non_blocking=True)
-            copied.record(self.copy_stream)
-        self._k = (self._k + 1) % self.depth
-        return slot
+            slot = self._slot(batch_u8.shape)
+            self._k = (self._k + 1) % self.depth
+            src, done = slot[0], slot[2]
+            done.synchronize()  # the slot's previous conversion (or copy) has read the pinned buffer
+            src.copy_(batch_u8)
+        with torch.cuda.stream(self.stream):
+            out = torch.empty(batch_u8.shape, dtype=torch.float32, device=self.device)
+            if self.direct:
+                sp = self._device_address(src)
+            else:
+                dev = torch.empty(batch_u8.shape, dtype=torch.uint8, device=self.device)
+                dev.copy_(src, non_blocking=True)
+                sp = dev.data_ptr()
+            nat.check(nat.lib().vad_u8_to_clip(sp, src.numel(), self.mode, out.data_ptr(),
+                                               ctypes.c_void_p(self.stream.cuda_stream)))
+            done.record(self.stream)
+        return _Staged(out, done, slot)
 
-    def finish(self, handle) -> torch.Tensor:
-        """The fp32 device clip of an issued batch, ready on the current stream."""
-        _, dev, copied, read = handle
+    def finish(self, handle: _Staged, wait: bool = True) -> torch.Tensor:
+        """The fp32 device clip of an issued batch.  wait=True: ready on the current stream; wait=False: the consumer
+        orders itself after ``handle.ready`` (e.g. CadTrainer.step(x, y, inputs_ready=handle.ready))."""
         cur = torch.cuda.current_stream(self.device)
-        cur.wait_event(copied)
-        out = torch.empty(dev.shape, dtype=torch.float32, device=self.device)
-        nat.check(nat.lib().vad_u8_to_clip(dev.data_ptr(), dev.numel(), self.mode, out.data_ptr(),
-                                           nat.stream_of(self.device)))
-        read.record(cur)
-        return out
+        if wait:
+            cur.wait_event(handle.ready)
+        handle.out.record_stream(cur)  # (its memory is not reused before the current stream's queued work is done)
+        return handle.out
 
     def stage(self, batch_u8: torch.Tensor) -> torch.Tensor:
         return self.finish(self.issue(batch_u8))

@@ -101,7 +101,8 @@ class CadTrainer:
         """One training step; returns the (device) loss vector [cls, anomaly, causal, kl, total] (want_outputs: the
         forward's output dict, see CadEngine.forward).  inputs_ready: None -- the clips are produced on the current
         stream, the step is ordered after it; True -- they are complete on the device already (staged and
-        synchronised before); a torch.cuda.Stream -- its queued work completes them.  Given, the frozen stem may start
+        synchronised before); a torch.cuda.Stream -- its queued work completes them; a torch.cuda.Event -- its
+        completion does (ClipStager.finish(h, wait=False) with h.ready).  Given, the frozen stem may start
         beside the previous step's queued tail (CadEngine.input_ready)."""
         if self.prio_stream is not None and self.eng.grads.is_cuda:
             # the step's critical path on a stream of the device's greatest priority (the plan's weight-gradient stream
@@ -131,7 +132,9 @@ class CadTrainer:
             # not for the previous step's tail on the current stream
             if self._arm_stream is None:
                 self._arm_stream = torch.cuda.Stream(eng.device)
-            if inputs_ready is not True:
+            if isinstance(inputs_ready, torch.cuda.Event):
+                self._arm_stream.wait_event(inputs_ready)
+            elif inputs_ready is not True:
                 self._arm_stream.wait_stream(inputs_ready)
             if self._bufs_ev is not None:
                 self._arm_stream.wait_event(self._bufs_ev)

@@ -284,11 +284,14 @@ int vad_ae_memory_score(const float* memory, const int64_t* memory_ptr, const fl
                         void* stream);
 
 /* Host data path.
- * vad_u8_to_clip: n u8 pixels (already in HBM) -> fp32; mode 0: (u8 - 0.5) / 0.5 (UCSDped2Dataset + Normalize,
- *   cad:85-104, 1177-1179), mode 1: u8 / 255 (ToTensor, mc:120 / bbox:411).  src 4-byte, dst 16-byte aligned.
+ * vad_u8_to_clip: n u8 pixels -> fp32; mode 0: (u8 - 0.5) / 0.5 (UCSDped2Dataset + Normalize, cad:85-104,
+ *   1177-1179), mode 1: u8 / 255 (ToTensor, mc:120 / bbox:411).  src (in HBM, or pinned host memory at the address
+ *   vad_host_device_ptr gives) and dst 16-byte aligned.
+ * vad_host_device_ptr: the device address of pinned host memory (the ClipStager's direct mode reads batches there).
  * vad_resize_u8 (host): bilinear u8 resize, half-pixel centres, clamped borders, 11-bit fixed-point weights (the
  *   cv2.resize INTER_LINEAR scheme of cad:88-89). */
 int vad_u8_to_clip(const uint8_t* src, int64_t n, int mode, float* dst, void* stream);
+int vad_host_device_ptr(const void* host, void** dev);
 int vad_resize_u8(const uint8_t* src, int sh, int sw, uint8_t* dst, int dh, int dw);
 
 /* Plan options.  "conv_bf16" (0/1): the 3x3 convs of the backbone run on bf16 operands with fp32 accumulation

@@ -102,13 +102,21 @@ def test_native_resize_constant_and_ramp():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("direct", [True, False])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_stager_u8_to_clip_bitexact_and_ordered(mode):
+@pytest.mark.parametrize("pinned", [False, True])
+def test_stager_u8_to_clip_bitexact_and_ordered(mode, direct, pinned):
+    """prefetch through the stager: every clip bit-equal to the host normalisation, in order; pageable batches through
+    the pinned ring, pinned ones read in place; direct (PCIe reads in the conversion kernel) and copy-engine modes;
+    odd pixel counts exercise the kernel's per-pixel tail"""
     from vad_amd.data import ClipStager, prefetch
     g = torch.Generator().manual_seed(mode)
-    batches = [(torch.randint(0, 256, (2, 16, 1, 24, 37), generator=g, dtype=torch.uint8), torch.tensor([i, i]))
-               for i in range(5)]
-    st = ClipStager("cuda", mode=mode, depth=2)
+    shapes = [(2, 16, 1, 24, 37), (1, 3, 1, 7, 5), (2, 16, 1, 24, 37), (3, 2, 1, 11, 13), (2, 16, 1, 24, 37)]
+    batches = [(torch.randint(0, 256, sh, generator=g, dtype=torch.uint8), torch.tensor([i, i]))
+               for i, sh in enumerate(shapes)]
+    if pinned:
+        batches = [(x.pin_memory(), y) for x, y in batches]
+    st = ClipStager("cuda", mode=mode, depth=2, direct=direct)
     seen = []
     for (x, y), (xs, ys) in zip(prefetch(batches, st), batches):
         f = xs.float()
@@ -116,6 +124,51 @@ def test_stager_u8_to_clip_bitexact_and_ordered(mode):
         np.testing.assert_array_equal(x.cpu().numpy(), want.numpy())
         seen.append(int(y[0]))
     assert seen == list(range(5))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("early", [1, 0])
+def test_stager_unwaited_inputs_train_like_staged(early):
+    """CadTrainer.step(x, y, inputs_ready=handle.ready) on clips from ClipStager.finish(h, wait=False) -- the step's
+    stream never waits for the conversion, the stem does (early stem on; with it off, the armed forward's stem on the
+    critical stream) -- gives bit-identical losses and weights to synchronously staged clips"""
+    import contextlib
+    import io
+    from vad_amd import _native as nat
+    from vad_amd.cad import CausalAnomalyDetector
+    from vad_amd.data import ClipStager
+    from vad_amd.train import CadTrainer, apply_memory_efficient_training
+    g = torch.Generator().manual_seed(5)
+    u8 = [torch.randint(0, 256, (2, 4, 1, 64, 64), generator=g, dtype=torch.uint8).pin_memory() for _ in range(4)]
+    labels = torch.tensor([0, 1], device="cuda")
+    res = []
+    nat.check(nat.lib().vad_set_tuning(b"cad_stem_early", early))
+    try:
+        for unwaited in (False, True):
+            torch.manual_seed(0)
+            m = CausalAnomalyDetector()
+            with contextlib.redirect_stdout(io.StringIO()):
+                apply_memory_efficient_training(m)
+            tr = CadTrainer(m.cuda(), lr=3e-4, seed=11)
+            st = ClipStager("cuda", mode=0)
+            h = st.issue(u8[0])
+            losses = []
+            for i in range(4):
+                x = st.finish(h, wait=not unwaited)
+                ready = h.ready
+                if i + 1 < 4:
+                    h = st.issue(u8[i + 1])
+                if unwaited:
+                    losses.append(tr.step(x, labels, inputs_ready=ready).clone())
+                else:
+                    losses.append(tr.step(x, labels).clone())
+            torch.cuda.synchronize()
+            res.append((torch.stack(losses).cpu(), {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}))
+    finally:
+        nat.check(nat.lib().vad_set_tuning(b"cad_stem_early", 1))
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=0, atol=0)
+    for k in res[0][1]:
+        torch.testing.assert_close(res[0][1][k], res[1][1][k], rtol=0, atol=0, msg=k)
 
 
 @pytest.mark.gpu
