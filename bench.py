@@ -291,7 +291,7 @@ def run_gpu(args, rank, world, local_rank):
     # the oracle (cpu_baseline) and reports the score difference and the frame-AUC of both
     probe = None
     allreduce_bytes = 4 * trainer.allreduce_floats if trainer.dist else 0
-    if rank == 0:
+    if rank == 0 and not args.no_cpu_baseline:  # (only the CPU leg reads it; PMC passes run without both)
         if trainer.sync_bn:  # (the probe runs on rank 0 alone: per-rank statistics, as the oracle leg computes them)
             eng.set_bn_sync(enable=False)
         o = eng.forward(pool[0], True, 777, 0, 0, labels)
