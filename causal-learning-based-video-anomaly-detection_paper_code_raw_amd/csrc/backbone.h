@@ -154,6 +154,7 @@ int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, co
 // input gradient.  Their weights are the bf16 copies the prep writes behind the fp32 images (when conv_bf16 and
 // act_bf16 are set), so in that mode a wf / wd buffer holds Co*Ci*9 floats + Co*Ci*9 bf16.
 extern int g_bfc, g_bfc_blocks;  // knobs "conv_bfc", "conv_bfc_blocks"
+extern int g_bfc_s2_ni2;         // knob "conv_bfc_s2_ni2"
 bool bfc_supported(const Conv3Layer& L, bool fwd);
 inline const __bf16* conv3_bf16_image(const float* img, const Conv3Layer& L) {
   return reinterpret_cast<const __bf16*>(img + (int64_t)L.Co * L.Ci * 9);

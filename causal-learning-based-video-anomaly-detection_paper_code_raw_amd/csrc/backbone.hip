@@ -1128,6 +1128,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "act_bf16") g_act_bf16 = value;    // ops API only: bf16 activation storage for the calling thread
   else if (k == "conv_bfc") g_bfc = value;
   else if (k == "conv_bfc_blocks") g_bfc_blocks = value;
+  else if (k == "conv_bfc_s2_ni2") g_bfc_s2_ni2 = value;
   else if (k == "conv_bfw_blocks") g_bfw_blocks = value;
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else if (k == "conv_wgrad_alone_blocks") g_tune.wgrad_alone_blocks = value;

@@ -657,10 +657,11 @@ __device__ __forceinline__ void s2_pair(int i, int& c, int& kh, int& kw) {
   kw = pw ? 2 * (ph ? q & 1 : q) : 1;
 }
 
-template <int CB, bool WRES>
+template <int CB, bool WRES, int NI>
 __global__ __launch_bounds__(256, 2) void bfc_dgrad_s2_kernel(const BfcArgs p) {
-  constexpr int NTHR = 256, TH = 8, TW = 16, TPX = TH * TW, NC = 32, G8 = CB / 8, NG = NC / 8, KK = CB / 16;
-  constexpr int PH = TH + 1, PW = TW + 1, PROWS = PH * PW;
+  // NI = 1: one frame's 8 x 16 class tile; NI = 2: 8 x 8 class tiles of two frames (class grids 8 wide or less)
+  constexpr int NTHR = 256, TH = 8, TW = 16 / NI, TPX = NI * TH * TW, NC = 32, G8 = CB / 8, NG = NC / 8, KK = CB / 16;
+  constexpr int PH = TH + 1, PW = TW + 1, PFR = PH * PW, PROWS = NI * PFR;
   constexpr int RP = CB + 8, WP = 9 * CB + 8, EP = NC + 8;
   static_assert(((RP / 8) & 1) && ((WP / 8) & 1) && ((EP / 8) & 1), "odd 16-B row pitches");
   constexpr int PE = PROWS * RP > 4 * TPX * EP ? PROWS * RP : 4 * TPX * EP;
@@ -681,15 +682,16 @@ __global__ __launch_bounds__(256, 2) void bfc_dgrad_s2_kernel(const BfcArgs p) {
   __syncthreads();
   if (nitems <= 0) return;
   // this lane's class pixel (row j of the wave's 32): patch row of offset (0, 0)
-  const int arow = (2 * wave + j / TW) * PW + j % TW;
+  const int am = wave * 32 + j;
+  const int arow = (am / (TH * TW)) * PFR + ((am % (TH * TW)) / TW) * PW + am % TW;
 
   constexpr int PQ = PROWS * G8, PIT = (PQ + NTHR - 1) / NTHR;
   constexpr int WQ = NC * 9 * G8, WIT = (WQ + NTHR - 1) / NTHR;
   const int g8 = tid % G8;
   u32v4 pv[PIT], wv[WIT];
   bool pok[PIT];
-  auto origin = [&](int tile, int& img, int& yc0, int& xc0) {
-    img = tile / tiles_per_img;
+  auto origin = [&](int tile, int& img, int& yc0, int& xc0) {  // (img: the tile's first frame)
+    img = (tile / tiles_per_img) * NI;
     const int tr = tile % tiles_per_img;
     yc0 = (tr / p.tiles_w) * TH;
     xc0 = (tr % p.tiles_w) * TW;
@@ -717,10 +719,11 @@ __global__ __launch_bounds__(256, 2) void bfc_dgrad_s2_kernel(const BfcArgs p) {
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
       const int q = tid + it * NTHR;
-      const int row = min(q / G8, PROWS - 1);
-      const int iy = yc0 + row / PW, ix = xc0 + row % PW;
-      pok[it] = q < PQ && iy < p.IH && ix < p.IW;
-      pv[it] = *reinterpret_cast<const u32v4*>(p.src + (pok[it] ? (((int64_t)img * p.IH + iy) * p.IW + ix) * p.C : 0) + c0);
+      const int row = min(q / G8, PROWS - 1), fr = row / PFR, rr = row % PFR;
+      const int iy = yc0 + rr / PW, ix = xc0 + rr % PW;
+      pok[it] = q < PQ && iy < p.IH && ix < p.IW && img + fr < p.NF;
+      pv[it] = *reinterpret_cast<const u32v4*>(
+          p.src + (pok[it] ? (((int64_t)(img + fr) * p.IH + iy) * p.IW + ix) * p.C : 0) + c0);
     }
     if constexpr (!WRES) fetch_w(ch);
   };
@@ -766,9 +769,10 @@ __global__ __launch_bounds__(256, 2) void bfc_dgrad_s2_kernel(const BfcArgs p) {
     auto piece = [&](int i, int& cm, int64_t& oi) {  // epilogue piece i: class pixel row cm, NHWC offset (or -1)
       const int q = tid + i * NTHR;
       cm = q / NG;
-      const int c = cm / TPX, m = cm % TPX;
-      const int yy = 2 * (yc0 + m / TW) + (c >> 1), xx = 2 * (xc0 + m % TW) + (c & 1);
-      oi = (yy < p.OH && xx < p.OW) ? (((int64_t)img * p.OH + yy) * p.OW + xx) * p.N + n0 + cg * 8 : -1;
+      const int c = cm / TPX, m = cm % TPX, fr = m / (TH * TW), mm = m % (TH * TW);
+      const int yy = 2 * (yc0 + mm / TW) + (c >> 1), xx = 2 * (xc0 + mm % TW) + (c & 1);
+      oi = (yy < p.OH && xx < p.OW && img + fr < p.NF)
+               ? (((int64_t)(img + fr) * p.OH + yy) * p.OW + xx) * p.N + n0 + cg * 8 : -1;
     };
     if (bnb && ch == nch - 1) {  // the layer below's y at the pixels this item writes (issued before the prefetch)
 #pragma unroll
@@ -879,6 +883,7 @@ __global__ __launch_bounds__(256, 2) void bfc_dgrad_s2_kernel(const BfcArgs p) {
 // host side
 int g_bfc = 1;             // knob "conv_bfc": config-4 forwards / stride-1 input gradients on these kernels
 int g_bfc_blocks = 512;    // knob "conv_bfc_blocks": target grid (persistent blocks over the tiles)
+int g_bfc_s2_ni2 = 1;      // knob "conv_bfc_s2_ni2": stride-2 input gradients of class grids <= 8 wide on 2-frame tiles
 
 bool bfc_supported(const Conv3Layer& L, bool fwd) {
   if (!g_bfc || !g_conv_bf16 || !g_act_bf16) return false;
@@ -974,17 +979,24 @@ int bfc_dgrad(const Conv3Layer& L, const __bf16* dY, const __bf16* wdb, __bf16* 
     mb = std::max<int64_t>(1, f->cap / (2ll * L.Ci));
   }
   if (L.stride == 2) {
-    constexpr int TH = 8, TW = 16;
+    // class grids 8 wide or less (the 8 x 8 dY maps of config 4's last stride-2 layer): two frames' 8 x 8 tiles per
+    // block tile instead of a half-empty 8 x 16 one
+    const int ni = (L.IW + 1) / 2 <= 8 && g_bfc_s2_ni2 ? 2 : 1;
+    const int TH = 8, TW = 16 / ni;
     a.tiles_h = (int)cdiv((L.IH + 1) / 2, TH);
     a.tiles_w = (int)cdiv((L.IW + 1) / 2, TW);
-    a.ntiles = L.NF * a.tiles_h * a.tiles_w;
+    a.ntiles = (int)cdiv(L.NF, ni) * a.tiles_h * a.tiles_w;
     const int ny = L.Ci / 32;
     const int64_t target = std::max<int64_t>(1, std::min<int64_t>(mb, cdiv(g_bfc_blocks, ny)));
     a.tpb = (int)cdiv(a.ntiles, target);
     const int gx = (int)cdiv(a.ntiles, a.tpb);
-    if (L.Co == 32) VAD_KLAUNCH((bfc_dgrad_s2_kernel<32, true>), dim3(gx, ny), dim3(256), 0, st, a);
-    else if (L.Co % 32 == 0) VAD_KLAUNCH((bfc_dgrad_s2_kernel<32, false>), dim3(gx, ny), dim3(256), 0, st, a);
-    else VAD_KLAUNCH((bfc_dgrad_s2_kernel<16, false>), dim3(gx, ny), dim3(256), 0, st, a);
+    if (ni == 2) {
+      if (L.Co == 32) VAD_KLAUNCH((bfc_dgrad_s2_kernel<32, true, 2>), dim3(gx, ny), dim3(256), 0, st, a);
+      else if (L.Co % 32 == 0) VAD_KLAUNCH((bfc_dgrad_s2_kernel<32, false, 2>), dim3(gx, ny), dim3(256), 0, st, a);
+      else VAD_KLAUNCH((bfc_dgrad_s2_kernel<16, false, 2>), dim3(gx, ny), dim3(256), 0, st, a);
+    } else if (L.Co == 32) VAD_KLAUNCH((bfc_dgrad_s2_kernel<32, true, 1>), dim3(gx, ny), dim3(256), 0, st, a);
+    else if (L.Co % 32 == 0) VAD_KLAUNCH((bfc_dgrad_s2_kernel<32, false, 1>), dim3(gx, ny), dim3(256), 0, st, a);
+    else VAD_KLAUNCH((bfc_dgrad_s2_kernel<16, false, 1>), dim3(gx, ny), dim3(256), 0, st, a);
     VAD_LAUNCH_CHECK();
     if (f) *f->nparts = gx;
     return 0;
