@@ -398,13 +398,28 @@ __global__ void ae_bias_reduce_kernel(const float* __restrict__ parts, int nblk,
 }
 
 // out[0] = sum of x[0, n) (one block, fixed order): the bias grad of the single-channel last ConvTranspose2d
-__global__ __launch_bounds__(256) void ae_sum_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+// sum of n floats in two fixed-order passes: AE_SUM_BLOCKS block partials (double), then one block adds them
+constexpr int AE_SUM_BLOCKS = 256;
+
+__global__ __launch_bounds__(256) void ae_sum_parts_kernel(const float* __restrict__ x, int64_t n,
+                                                           double* __restrict__ parts) {
   __shared__ double red[256];
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += 256) s += (double)x[i];
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)AE_SUM_BLOCKS * 256) s += (double)x[i];
   red[threadIdx.x] = s;
   __syncthreads();
   for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) parts[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void ae_sum_kernel(const double* __restrict__ parts, float* __restrict__ out) {
+  __shared__ double red[AE_SUM_BLOCKS];
+  red[threadIdx.x] = parts[threadIdx.x];
+  __syncthreads();
+  for (int k = AE_SUM_BLOCKS / 2; k > 0; k >>= 1) {
     if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
     __syncthreads();
   }
@@ -735,6 +750,7 @@ struct AePlanImpl {
   float *u, *dx[4], *dy[4], *dst[3], *dylast, *parts, *bparts, *lpart, *losses, *bufA, *bufB, *bcols;
   float *dG, *dlat, *dz, *da3, *dseq, *dU, *scratch;
   int* bad;
+  double* sum_parts;
   AdamWs aws{};
   int64_t scratch_floats = 0;
   // per-call state
@@ -801,8 +817,9 @@ struct AePlanImpl {
     scratch_floats = 8ll << 20;
     scratch = w.take<float>(scratch_floats);
     bad = w.take<int>(4);
-    aws.sq = w.take<double>(ADAM_MAX_SLOTS);
-    aws.bad = w.take<int>(ADAM_MAX_SLOTS);
+    aws.sq = w.take<double>(ADAM_MAX_SLOTS * ADAM_SQ_CHUNKS);
+    aws.bad = w.take<int>(ADAM_MAX_SLOTS * ADAM_SQ_CHUNKS);
+    sum_parts = w.take<double>(AE_SUM_BLOCKS);
     aws.ctrl = w.take<float>(4);
   }
 
@@ -921,7 +938,10 @@ struct AePlanImpl {
                          dylast);
       VAD_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(ae_sum_kernel, dim3(1), dim3(256), 0, st, dylast, (int64_t)B * AE_PIX, G(L.dec_b[3]));
+    hipLaunchKernelGGL(ae_sum_parts_kernel, dim3(AE_SUM_BLOCKS), dim3(256), 0, st, dylast, (int64_t)B * AE_PIX,
+                       sum_parts);
+    VAD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ae_sum_kernel, dim3(1), dim3(AE_SUM_BLOCKS), 0, st, sum_parts, G(L.dec_b[3]));
     VAD_LAUNCH_CHECK();
     // decoder, last ConvTranspose2d first: dX_j = im2col(dY_j) Wt^T, dWt = X_j^T im2col(dY_j)
     const float* dcur = dylast;

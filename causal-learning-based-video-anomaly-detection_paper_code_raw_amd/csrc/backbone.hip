@@ -5,6 +5,7 @@
 #include <type_traits>
 
 #include "backbone.h"
+#include "conv3d.h"
 #include "mlp.h"
 #include "gemm.h"
 #include "head.h"
@@ -1129,6 +1130,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_bfc") g_bfc = value;
   else if (k == "conv_bfc_blocks") g_bfc_blocks = value;
   else if (k == "conv_bfc_s2_ni2") g_bfc_s2_ni2 = value;
+  else if (k == "conv3d_direct") g_conv3d_direct = value;
   else if (k == "conv_bfw_blocks") g_bfw_blocks = value;
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else if (k == "conv_wgrad_alone_blocks") g_tune.wgrad_alone_blocks = value;

@@ -66,6 +66,20 @@ int conv3d_x3_fwd(int B, int D, int H, int W, int C, int N, const float* src, co
 // torch Conv3d weight [N][C][3][3][3] -> [3][N][9][C]
 int conv3d_prep_w3(const float* w, int N, int C, float* w3, hipStream_t st);
 
+// Direct Conv3d k3 s1 p1 for small channel counts (conv3d_direct.hip; fp32 FMA, no im2col).  Supported: Ci <= 16,
+// Co in {8, 16, 32} (knob "conv3d_direct" off: false).  prep: torch weight [Co][Ci][27] -> wf [Ci][27][Co] (forward)
+// and wd [Co][27][Ci] (flipped taps: the input gradient is conv3d_direct_fwd over dY with wd, CO = Ci).
+extern int g_conv3d_direct;
+bool conv3d_direct_supported(int Ci, int Co);
+int conv3d_direct_prep(const float* w, int Co, int Ci, float* wf, float* wd, hipStream_t st);
+// out (NDHWC, in's spatial dims, CO channels) = conv(src) + bias (nullable)
+int conv3d_direct_fwd(const float* src, const Strides5& s, const Vol5& in, const float* w, int CO, const float* bias,
+                      float* out, hipStream_t st);
+// dW [Co][Ci][27] and db [Co] (nullable) written (not accumulated) from dY (NDHWC, CO channels) and the forward input
+int conv3d_direct_wgrad(const float* dy, int CO, const float* src, const Strides5& s, const Vol5& in, float* dW,
+                        float* db, float* slab, int64_t slab_floats, hipStream_t st);
+int64_t conv3d_direct_wgrad_slab_floats(const Vol5& in, int CO);
+
 // per-block column sums / sums of squares of Y[M][C] -> partials [P][2C] (bn_finalize layout)
 int bn_fwd_partials(const float* y, int64_t M, int C, float* partials, int* nparts, hipStream_t st);
 int64_t bn_fwd_partials_blocks(int64_t M);

@@ -320,7 +320,7 @@ struct McPlanImpl {
   int64_t* nbt = nullptr;
   int32_t* steps = nullptr;
   // workspace
-  float *cols[3], *y[3], *pooled[3], *stats[3];
+  float *cols[3], *y[3], *pooled[3], *stats[3], *wf[3], *wd[3], *xin;
   float *parts, *bparts, *feats, *fd, *h1, *h1d, *h2, *o, *dz1, *dz2, *dz3, *dfeat, *dpool, *dA, *dY, *dcols;
   float *scratch, *labels_copy, *losses, *ctrl;
   double* sq;
@@ -328,7 +328,7 @@ struct McPlanImpl {
   int32_t* flags = nullptr;
   int64_t parts_floats = 0, scratch_floats = 0;
   // per-call state
-  int training = 1;
+  int training = 1, direct_fwd = 0;
   uint64_t seed = 0, step = 0;
   int64_t clip0 = 0;
   bool have_labels = false;
@@ -362,6 +362,12 @@ struct McPlanImpl {
       if (s > 0) max_dcols = std::max(max_dcols, g[s].rows() * g[s].K());
       parts_floats = std::max<int64_t>(parts_floats, std::max<int64_t>(bn_fwd_partials_blocks(V), cdiv(V, 64)) * 2 * Co);
     }
+    for (int s = 0; s < 3; ++s) {
+      const int64_t n = (int64_t)MC_CO[s] * g[s].in.C * 27;
+      wf[s] = w.take<float>(n);
+      wd[s] = w.take<float>(n);
+    }
+    xin = w.take<float>(g[0].in.numel());  // (the forward input, kept for the direct weight gradient)
     max_pool = std::max(max_pool, g[1].in.numel());
     max_pool = std::max(max_pool, g[2].in.numel());
     parts = w.take<float>(parts_floats);
@@ -411,15 +417,26 @@ struct McPlanImpl {
     return a;
   }
 
+  bool direct(int s) const { return conv3d_direct_supported(g[s].in.C, MC_CO[s]); }
+
   int forward(const float* x, float* scores, hipStream_t st) {
+    // direct convs (conv3d_direct.hip) keep the input for the weight gradient instead of the im2col columns
+    direct_fwd = direct(0) && direct(1) && direct(2);
+    if (direct_fwd)
+      VAD_HIP(hipMemcpyAsync(xin, x, g[0].in.numel() * sizeof(float), hipMemcpyDeviceToDevice, st));
     for (int s = 0; s < 3; ++s) {
       const int Co = MC_CO[s];
       const int64_t V = conv_out[s].voxels();
       const float* src = s == 0 ? x : pooled[s - 1];
       const Strides5 str = s == 0 ? ncdhw_strides(g[0].in) : ndhwc_strides(g[s].in);
-      VAD_TRY(im2col3d(src, str, g[s], nullptr, nullptr, 0, cols[s], st));
-      VAD_TRY(dense_fwd(cols[s], (int)g[s].rows(), g[s].K(), P(LY.conv_w[s]), P(LY.conv_b[s]), Co, y[s], DenseAct{},
-                        scratch, scratch_floats, st));
+      if (direct_fwd) {
+        VAD_TRY(conv3d_direct_prep(P(LY.conv_w[s]), Co, g[s].in.C, wf[s], wd[s], st));
+        VAD_TRY(conv3d_direct_fwd(src, str, g[s].in, wf[s], Co, P(LY.conv_b[s]), y[s], st));
+      } else {
+        VAD_TRY(im2col3d(src, str, g[s], nullptr, nullptr, 0, cols[s], st));
+        VAD_TRY(dense_fwd(cols[s], (int)g[s].rows(), g[s].K(), P(LY.conv_w[s]), P(LY.conv_b[s]), Co, y[s],
+                          DenseAct{}, scratch, scratch_floats, st));
+      }
       int np = 0;
       if (training) VAD_TRY(bn_fwd_partials(y[s], V, Co, parts, &np, st));
       VAD_TRY(bn_finalize(parts, np, Co, (double)V, P(LY.bn_w[s]), P(LY.bn_b[s]), RM(s), RV(s), 0.1f, 1e-5f,
@@ -461,11 +478,22 @@ struct McPlanImpl {
       VAD_TRY(bn_bwd_finalize(parts, np, Co, (double)V, P(LY.bn_w[s]), stats[s], G(LY.bn_w[s]), G(LY.bn_b[s]),
                               training, st));
       VAD_TRY(bn_bwd_apply(dA, y[s], stats[s], (int)V, Co, dY, bparts, &nb, st));
-      VAD_TRY(dense_wgrad(dY, (int)V, Co, cols[s], g[s].K(), G(LY.conv_w[s]), G(LY.conv_b[s]), scratch,
-                          scratch_floats, nullptr, st));
-      if (s > 0) {
-        VAD_TRY(dense_dgrad(dY, (int)V, Co, P(LY.conv_w[s]), g[s].K(), dcols, nullptr, 1.f, nullptr, st));
-        VAD_TRY(col2im3d(dcols, g[s], dpool, st));
+      if (direct_fwd) {
+        const float* src = s == 0 ? xin : pooled[s - 1];
+        const Strides5 str = s == 0 ? ncdhw_strides(g[0].in) : ndhwc_strides(g[s].in);
+        VAD_TRY(conv3d_direct_wgrad(dY, Co, src, str, g[s].in, G(LY.conv_w[s]), G(LY.conv_b[s]), scratch,
+                                    scratch_floats, st));
+        if (s > 0) {  // dX = conv(dY, flipped W^T): NDHWC over the layer's input grid
+          const Vol5 vy{g[s].in.N, Co, g[s].in.D, g[s].in.H, g[s].in.W};
+          VAD_TRY(conv3d_direct_fwd(dY, ndhwc_strides(vy), vy, wd[s], g[s].in.C, nullptr, dpool, st));
+        }
+      } else {
+        VAD_TRY(dense_wgrad(dY, (int)V, Co, cols[s], g[s].K(), G(LY.conv_w[s]), G(LY.conv_b[s]), scratch,
+                            scratch_floats, nullptr, st));
+        if (s > 0) {
+          VAD_TRY(dense_dgrad(dY, (int)V, Co, P(LY.conv_w[s]), g[s].K(), dcols, nullptr, 1.f, nullptr, st));
+          VAD_TRY(col2im3d(dcols, g[s], dpool, st));
+        }
       }
     }
     return 0;

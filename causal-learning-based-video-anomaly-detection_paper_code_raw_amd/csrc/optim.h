@@ -11,6 +11,7 @@
 namespace vad {
 
 constexpr int ADAM_MAX_SLOTS = 64;
+constexpr int ADAM_SQ_CHUNKS = 64;  // blocks per slot of the squared-norm pass (fixed-order partials)
 
 struct AdamSlots {
   int n;
@@ -18,8 +19,8 @@ struct AdamSlots {
 };
 
 struct AdamWs {
-  double* sq;   // [ADAM_MAX_SLOTS]
-  int* bad;     // [ADAM_MAX_SLOTS]
+  double* sq;   // [ADAM_MAX_SLOTS][ADAM_SQ_CHUNKS]
+  int* bad;     // [ADAM_MAX_SLOTS][ADAM_SQ_CHUNKS]
   float* ctrl;  // [4]
 };
 

@@ -6,15 +6,19 @@
 
 namespace vad {
 
-// one block per slot: squared L2 norm (double accumulation) and finiteness of the slot's grad
+// block (slot s, chunk c): squared L2 norm (double accumulation) and finiteness of one contiguous chunk of the slot's
+// grad -> partial [s][c]; adam_prepare_kernel sums a slot's chunks in order (one block per slot took 0.4 ms on the
+// autoencoder's largest weight)
 __global__ __launch_bounds__(256) void adam_sqsum_kernel(const float* __restrict__ g, AdamSlots t, double* sq,
                                                          int* bad) {
-  const int s = blockIdx.x;
+  const int s = blockIdx.x, c = blockIdx.y;
+  const int64_t len = (t.numel[s] + ADAM_SQ_CHUNKS - 1) / ADAM_SQ_CHUNKS;
+  const int64_t i0 = c * len, i1 = min(t.numel[s], i0 + len);
   __shared__ double red[256];
   __shared__ int rb[256];
   double acc = 0.0;
   int nf = 0;
-  for (int64_t i = threadIdx.x; i < t.numel[s]; i += 256) {
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
     const float v = g[t.off[s] + i];
     if (!isfinite(v)) nf = 1;
     acc += (double)v * (double)v;
@@ -30,8 +34,8 @@ __global__ __launch_bounds__(256) void adam_sqsum_kernel(const float* __restrict
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    sq[s] = red[0];
-    bad[s] = rb[0];
+    sq[s * ADAM_SQ_CHUNKS + c] = red[0];
+    bad[s * ADAM_SQ_CHUNKS + c] = rb[0];
   }
 }
 
@@ -48,9 +52,13 @@ __global__ void adam_prepare_kernel(const double* sq, const int* bad, int n, flo
   double tot = 0.0;
   int nonfin = 0;
   for (int s = 0; s < n; ++s) {
-    const double ns = (double)(float)(sqrt(sq[s]) * (double)grad_scale);  // per-param norm (float), squared
+    double ss = 0.0;
+    for (int c = 0; c < ADAM_SQ_CHUNKS; ++c) {
+      ss += sq[s * ADAM_SQ_CHUNKS + c];
+      nonfin |= bad[s * ADAM_SQ_CHUNKS + c];
+    }
+    const double ns = (double)(float)(sqrt(ss) * (double)grad_scale);  // per-param norm (float), squared
     tot += ns * ns;
-    nonfin |= bad[s];
   }
   if (nonfin) {
     status[3] = 1.f;
@@ -95,7 +103,7 @@ int adam_clip_step(const AdamSlots& t, float* params, const float* grads, float*
                    float eps, float wd, float clip_above, float max_norm, float grad_scale, hipStream_t st) {
   VAD_CHECK(t.n >= 1 && t.n <= ADAM_MAX_SLOTS, "adam_clip_step: slot table size");
   VAD_CHECK(exp_avg && exp_avg_sq && steps, "adam_clip_step: optimizer state not bound");
-  hipLaunchKernelGGL(adam_sqsum_kernel, dim3(t.n), dim3(256), 0, st, grads, t, w.sq, w.bad);
+  hipLaunchKernelGGL(adam_sqsum_kernel, dim3(t.n, ADAM_SQ_CHUNKS), dim3(256), 0, st, grads, t, w.sq, w.bad);
   VAD_LAUNCH_CHECK();
   hipLaunchKernelGGL(adam_prepare_kernel, dim3(1), dim3(64), 0, st, w.sq, w.bad, t.n, status, steps, lr, b1, b2,
                      clip_above, max_norm, grad_scale, w.ctrl);

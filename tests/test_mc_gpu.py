@@ -22,8 +22,19 @@ def _trainer(case, model):
     return tr
 
 
+@pytest.mark.parametrize("direct", [1, 0], ids=["direct", "im2col"])
 @pytest.mark.parametrize("case", MC_CASES, ids=[c["name"] for c in MC_CASES])
-def test_mc_step_matches_reference(case):
+def test_mc_step_matches_reference(case, direct):
+    """direct: the convs on conv3d_direct.hip (the default); im2col: knob conv3d_direct=0 (im2col + GEMM)"""
+    from vad_amd import _native as nat
+    nat.check(nat.lib().vad_set_tuning(b"conv3d_direct", direct))
+    try:
+        _mc_step_case(case)
+    finally:
+        nat.check(nat.lib().vad_set_tuning(b"conv3d_direct", 1))
+
+
+def _mc_step_case(case):
     g = load(f"mc_{case['name']}.npz")
     model = make_mc_model(case)
     init = {n: p.detach().clone().numpy().reshape(-1) for n, p in model.named_parameters()}
