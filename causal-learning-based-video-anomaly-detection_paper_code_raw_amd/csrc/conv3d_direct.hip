@@ -27,9 +27,10 @@ struct DirectArgs {
   const float* src;
   Strides5 s;
   Vol5 in;            // in.C = input channels
-  const float* w;     // [Ci][27][CO]
-  const float* bias;  // [CO] (nullable)
-  float* out;         // NDHWC [N][D][H][W][CO]
+  const float* w;     // [Ci][27][CoT]
+  const float* bias;  // [CoT] (nullable)
+  float* out;         // NDHWC [N][D][H][W][CoT]
+  int CoT;            // output channels in all; block row blockIdx.y computes [CO * y, CO * y + CO)
   int tiles_d, tiles_h, tiles_w, ntiles;
 };
 
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(256) void conv3d_direct_kernel(const DirectArgs p) 
   __shared__ __attribute__((aligned(16))) float ws[CIB * 27 * CO];
   const int tid = threadIdx.x;
   const int tw = tid % DT_W, th = (tid / DT_W) % DT_H, td = tid / (DT_W * DT_H);
-  const int Ci = p.in.C;
+  const int Ci = p.in.C, co0 = blockIdx.y * CO;
   for (int tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
     int n, d0, h0, w0;
     tile_origin(tile, p.tiles_d, p.tiles_h, p.tiles_w, n, d0, h0, w0);
@@ -78,7 +79,8 @@ __global__ __launch_bounds__(256) void conv3d_direct_kernel(const DirectArgs p) 
       const int cn = min(CIB, Ci - c0);
       __syncthreads();  // the previous chunk's (or tile's) LDS reads are done
       stage_halo(xs, p.src, p.s, p.in, n, d0, h0, w0, c0, cn, tid);
-      for (int q = tid; q < cn * 27 * CO; q += 256) ws[q] = p.w[(int64_t)c0 * 27 * CO + q];
+      for (int q = tid; q < cn * 27 * CO; q += 256)
+        ws[q] = p.w[(int64_t)(c0 * 27 + q / CO) * p.CoT + co0 + q % CO];  // ([ci][tap] rows of CO)
       __syncthreads();
       for (int ci = 0; ci < cn; ++ci) {
         const float* xb = xs + ci * HALO + (td * HH + th) * HW + tw;
@@ -97,13 +99,13 @@ __global__ __launch_bounds__(256) void conv3d_direct_kernel(const DirectArgs p) 
     }
     const int d = d0 + td, h = h0 + th, w = w0 + tw;
     if (d < p.in.D && h < p.in.H && w < p.in.W) {
-      float* o = p.out + ((((int64_t)n * p.in.D + d) * p.in.H + h) * p.in.W + w) * CO;
+      float* o = p.out + ((((int64_t)n * p.in.D + d) * p.in.H + h) * p.in.W + w) * p.CoT + co0;
 #pragma unroll
       for (int c4 = 0; c4 < CO; c4 += 4) {
         f32x4 v = {acc[c4], acc[c4 + 1], acc[c4 + 2], acc[c4 + 3]};
         if (p.bias) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += p.bias[c4 + e];
+          for (int e = 0; e < 4; ++e) v[e] += p.bias[co0 + c4 + e];
         }
         *reinterpret_cast<f32x4*>(o + c4) = v;
       }
@@ -133,9 +135,10 @@ struct DirectWgradArgs {
   int tiles_d, tiles_h, tiles_w, ntiles;
 };
 
-// MP: (ci, tap) pairs per thread (pairs = Ci*27 + 1 bias pair; > 256 pairs: 2 per thread)
-template <int CO, int MP>
+// pairs = Ci*27 + 1 bias pair; more than 256: block row blockIdx.y owns pairs [256 y, 256 y + 256)
+template <int CO>
 __global__ __launch_bounds__(256) void conv3d_direct_wgrad_kernel(const DirectWgradArgs p) {
+  constexpr int MP = 1;
   __shared__ float xs[WG_CI * HALO];
   __shared__ __attribute__((aligned(16))) float dys[256 * CO];
   const int tid = threadIdx.x;
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(256) void conv3d_direct_wgrad_kernel(const DirectWg
   int xoff[MP];                              // per owned pair: ci*HALO + tap offset, -1 = bias pair, -2 = none
 #pragma unroll
   for (int m = 0; m < MP; ++m) {
-    const int pair = P <= 256 ? tid % P : tid + 256 * m;
+    const int pair = P <= 256 ? tid % P : tid + 256 * (int)blockIdx.y;
     if (slice >= S || pair >= P) xoff[m] = -2;
     else if (pair == P - 1) xoff[m] = -1;
     else {
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(256) void conv3d_direct_wgrad_kernel(const DirectWg
   if (S == 1) {
 #pragma unroll
     for (int m = 0; m < MP; ++m) {
-      const int pair = tid + 256 * m;
+      const int pair = P <= 256 ? tid : tid + 256 * (int)blockIdx.y;
       if (xoff[m] != -2)
 #pragma unroll
         for (int c = 0; c < CO; ++c) slab[pair * CO + c] = acc[m][c];
@@ -215,14 +218,22 @@ __global__ __launch_bounds__(256) void conv3d_direct_wgrad_kernel(const DirectWg
   }
 }
 
-// dW[co][ci][t] = sum over blocks (in order) of slab[b][(ci*27 + t)*CO + co]; db[co] likewise from the bias pair
+// dW[co][ci][t] = sum over blocks of slab[b][(ci*27 + t)*CO + co]; db[co] likewise from the bias pair.  Block =
+// 64 outputs x 4 block groups (group g sums blocks g, g + 4, ...), the 4 group sums added in order (deterministic)
 __global__ __launch_bounds__(256) void conv3d_direct_wgrad_reduce_kernel(const float* __restrict__ slab, int nblk,
                                                                          int Ci, int CO, float* __restrict__ dW,
                                                                          float* __restrict__ db) {
+  __shared__ float red[4][64];
   const int P = Ci * 27 + 1, total = P * CO;
-  for (int q = blockIdx.x * 256 + threadIdx.x; q < total; q += gridDim.x * 256) {
-    float v = 0.f;
-    for (int b = 0; b < nblk; ++b) v += slab[(int64_t)b * total + q];
+  const int q = blockIdx.x * 64 + threadIdx.x % 64, grp = threadIdx.x / 64;
+  float v = 0.f;
+  if (q < total)
+    for (int b = grp; b < nblk; b += 4) v += slab[(int64_t)b * total + q];
+  red[grp][threadIdx.x % 64] = v;
+  __syncthreads();
+  if (grp == 0 && q < total) {
+    const int l = threadIdx.x;
+    v = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
     const int pair = q / CO, co = q % CO;
     if (pair == P - 1) {
       if (db) db[co] = v;
@@ -263,11 +274,14 @@ int conv3d_direct_fwd(const float* src, const Strides5& s, const Vol5& in, const
   a.w = w;
   a.bias = bias;
   a.out = out;
+  a.CoT = CO;
   direct_tiles(in, a.tiles_d, a.tiles_h, a.tiles_w, a.ntiles);
   if (a.ntiles == 0) return 0;
-  const dim3 grid((unsigned)std::min(a.ntiles, 2048));
-  if (CO == 8) hipLaunchKernelGGL(conv3d_direct_kernel<8>, grid, dim3(256), 0, st, a);
-  else if (CO == 16) hipLaunchKernelGGL(conv3d_direct_kernel<16>, grid, dim3(256), 0, st, a);
+  // few tiles (small volumes): the output channels split over block rows so the grid still covers the CUs
+  const int split = (a.ntiles < 256 && CO >= 16) ? 2 : 1, cb = CO / split;
+  const dim3 grid((unsigned)std::min(a.ntiles, 2048), (unsigned)split);
+  if (cb == 8) hipLaunchKernelGGL(conv3d_direct_kernel<8>, grid, dim3(256), 0, st, a);
+  else if (cb == 16) hipLaunchKernelGGL(conv3d_direct_kernel<16>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(conv3d_direct_kernel<32>, grid, dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   return 0;
@@ -295,22 +309,13 @@ int conv3d_direct_wgrad(const float* dy, int CO, const float* src, const Strides
   const int P = in.C * 27 + 1;
   VAD_CHECK((int64_t)nblk * P * CO <= slab_floats, "conv3d_direct_wgrad: slab too small");
   if (nblk == 0) return 0;
-  const bool two = P > 256;
-  VAD_CHECK(P <= 512, "conv3d_direct_wgrad: more than 512 (ci, tap) pairs");
-#define VAD_DW(C, M) hipLaunchKernelGGL((conv3d_direct_wgrad_kernel<C, M>), dim3(nblk), dim3(256), 0, st, a)
-  if (CO == 8) {
-    if (two) VAD_DW(8, 2);
-    else VAD_DW(8, 1);
-  } else if (CO == 16) {
-    if (two) VAD_DW(16, 2);
-    else VAD_DW(16, 1);
-  } else {
-    if (two) VAD_DW(32, 2);
-    else VAD_DW(32, 1);
-  }
-#undef VAD_DW
+  VAD_CHECK(P <= 1024, "conv3d_direct_wgrad: more than 1024 (ci, tap) pairs");
+  const dim3 grid((unsigned)nblk, (unsigned)(P > 256 ? cdiv(P, 256) : 1));
+  if (CO == 8) hipLaunchKernelGGL(conv3d_direct_wgrad_kernel<8>, grid, dim3(256), 0, st, a);
+  else if (CO == 16) hipLaunchKernelGGL(conv3d_direct_wgrad_kernel<16>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(conv3d_direct_wgrad_kernel<32>, grid, dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
-  hipLaunchKernelGGL(conv3d_direct_wgrad_reduce_kernel, dim3((unsigned)cdiv(P * CO, 256)), dim3(256), 0, st, slab, nblk,
+  hipLaunchKernelGGL(conv3d_direct_wgrad_reduce_kernel, dim3((unsigned)cdiv(P * CO, 64)), dim3(256), 0, st, slab, nblk,
                      in.C, CO, dW, db);
   VAD_LAUNCH_CHECK();
   return 0;

@@ -44,6 +44,20 @@ __global__ __launch_bounds__(256) void adam_sqsum_kernel(const float* __restrict
 __global__ void adam_prepare_kernel(const double* sq, const int* bad, int n, float* status, int32_t* steps, float lr,
                                     float b1, float b2, float clip_above, float max_norm, float grad_scale,
                                     float* ctrl) {
+  // thread s adds slot s's chunk partials in order; thread 0 then goes on alone
+  __shared__ double slot_sq[ADAM_MAX_SLOTS];
+  __shared__ int slot_bad[ADAM_MAX_SLOTS];
+  for (int s = threadIdx.x; s < n; s += blockDim.x) {
+    double ss = 0.0;
+    int nf = 0;
+    for (int c = 0; c < ADAM_SQ_CHUNKS; ++c) {
+      ss += sq[s * ADAM_SQ_CHUNKS + c];
+      nf |= bad[s * ADAM_SQ_CHUNKS + c];
+    }
+    slot_sq[s] = ss;
+    slot_bad[s] = nf;
+  }
+  __syncthreads();
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   ctrl[0] = 0.f;
   ctrl[1] = grad_scale;
@@ -52,13 +66,9 @@ __global__ void adam_prepare_kernel(const double* sq, const int* bad, int n, flo
   double tot = 0.0;
   int nonfin = 0;
   for (int s = 0; s < n; ++s) {
-    double ss = 0.0;
-    for (int c = 0; c < ADAM_SQ_CHUNKS; ++c) {
-      ss += sq[s * ADAM_SQ_CHUNKS + c];
-      nonfin |= bad[s * ADAM_SQ_CHUNKS + c];
-    }
-    const double ns = (double)(float)(sqrt(ss) * (double)grad_scale);  // per-param norm (float), squared
+    const double ns = (double)(float)(sqrt(slot_sq[s]) * (double)grad_scale);  // per-param norm (float), squared
     tot += ns * ns;
+    nonfin |= slot_bad[s];
   }
   if (nonfin) {
     status[3] = 1.f;
