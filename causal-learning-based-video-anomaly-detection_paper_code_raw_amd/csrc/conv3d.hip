@@ -27,19 +27,21 @@ __device__ __forceinline__ float act_of(float v, const float* scale, const float
   return (relu || scale) ? relu_nan(v) : v;
 }
 
-// one thread per column element; k fastest so the cols writes are coalesced
+// one thread per column element; k fastest so the cols writes are coalesced.  I = int when every index fits 31 bits
+// (the index arithmetic is most of this kernel's work: 64-bit divisions cost several times the 32-bit ones)
+template <typename I>
 __global__ __launch_bounds__(256) void im2col3d_kernel(const float* __restrict__ src, Strides5 s, Conv3dGeom g,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int relu,
                                                        float* __restrict__ cols) {
-  const int K = g.K(), taps = g.kd * g.kh * g.kw;
-  const int64_t total = g.rows() * K;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t row = i / K;
+  const int K = g.K(), taps = g.kd * g.kh * g.kw, khw = g.kh * g.kw;
+  const I total = (I)(g.rows() * K);
+  for (I i = blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
+    const I row = i / K;
     const int k = (int)(i - row * K);
-    const int ci = k / taps, t = k % taps;
-    const int kd = t / (g.kh * g.kw), kh = (t / g.kw) % g.kh, kw = t % g.kw;
-    int64_t r = row;
+    const int ci = k / taps, t = k - ci * taps;
+    const int kd = t / khw, kh = (t - kd * khw) / g.kw, kw = t % g.kw;
+    I r = row;
     const int ow = (int)(r % g.OW);
     r /= g.OW;
     const int oh = (int)(r % g.OH);
@@ -58,20 +60,24 @@ int im2col3d(const float* src, const Strides5& s, const Conv3dGeom& g, const flo
              int relu, float* cols, hipStream_t st) {
   const int64_t total = g.rows() * g.K();
   if (total == 0) return 0;
-  hipLaunchKernelGGL(im2col3d_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 16384)), dim3(256), 0, st,
-                     src, s, g, scale, shift, relu, cols);
+  const dim3 grid((unsigned)std::min<int64_t>(cdiv(total, 256), 16384));
+  if (total + (int64_t)grid.x * 256 < (1ll << 31))
+    hipLaunchKernelGGL(im2col3d_kernel<int>, grid, dim3(256), 0, st, src, s, g, scale, shift, relu, cols);
+  else
+    hipLaunchKernelGGL(im2col3d_kernel<int64_t>, grid, dim3(256), 0, st, src, s, g, scale, shift, relu, cols);
   VAD_LAUNCH_CHECK();
   return 0;
 }
 
 // one thread per source element (NDHWC): gather the taps that read it
+template <typename I>
 __global__ __launch_bounds__(256) void col2im3d_kernel(const float* __restrict__ dcols, Conv3dGeom g,
                                                        const float* __restrict__ bias, float* __restrict__ dsrc) {
   const int K = g.K(), taps = g.kd * g.kh * g.kw, C = g.in.C;
-  const int64_t total = g.in.numel();
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+  const I total = (I)g.in.numel();
+  for (I i = blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
     const int c = (int)(i % C);
-    int64_t r = i / C;
+    I r = i / C;
     const int w = (int)(r % g.in.W);
     r /= g.in.W;
     const int h = (int)(r % g.in.H);
@@ -94,7 +100,7 @@ __global__ __launch_bounds__(256) void col2im3d_kernel(const float* __restrict__
           if (tw < 0 || tw % g.sw) continue;
           const int ow = tw / g.sw;
           if (ow >= g.OW) continue;
-          const int64_t row = (((int64_t)n * g.OD + od) * g.OH + oh) * g.OW + ow;
+          const I row = (((I)n * g.OD + od) * g.OH + oh) * g.OW + ow;
           acc += dcols[row * K + c * taps + (kd * g.kh + kh) * g.kw + kw];
         }
       }
@@ -106,8 +112,11 @@ __global__ __launch_bounds__(256) void col2im3d_kernel(const float* __restrict__
 int col2im3d(const float* dcols, const Conv3dGeom& g, float* dsrc, hipStream_t st, const float* bias) {
   const int64_t total = g.in.numel();
   if (total == 0) return 0;
-  hipLaunchKernelGGL(col2im3d_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 16384)), dim3(256), 0, st,
-                     dcols, g, bias, dsrc);
+  const dim3 grid((unsigned)std::min<int64_t>(cdiv(total, 256), 16384));
+  if (g.rows() * g.K() < (1ll << 31) && total + (int64_t)grid.x * 256 < (1ll << 31))
+    hipLaunchKernelGGL(col2im3d_kernel<int>, grid, dim3(256), 0, st, dcols, g, bias, dsrc);
+  else
+    hipLaunchKernelGGL(col2im3d_kernel<int64_t>, grid, dim3(256), 0, st, dcols, g, bias, dsrc);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -177,15 +186,16 @@ int maxpool3d_fwd(const float* y, const float* stats, int relu, const Vol5& v, i
   return 0;
 }
 
+template <typename I>
 __global__ __launch_bounds__(256) void maxpool3d_bwd_kernel(const float* __restrict__ y,
                                                             const float* __restrict__ stats, int relu, Vol5 v, int kd,
                                                             int kh, int kw, const float* __restrict__ dout,
                                                             float* __restrict__ dA) {
   const int OD = v.D / kd, OH = v.H / kh, OW = v.W / kw, C = v.C;
-  const int64_t total = v.numel();
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+  const I total = (I)v.numel();
+  for (I i = blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
     const int c = (int)(i % C);
-    int64_t r = i / C;
+    I r = i / C;
     const int w = (int)(r % v.W);
     r /= v.W;
     const int h = (int)(r % v.H);
@@ -197,18 +207,18 @@ __global__ __launch_bounds__(256) void maxpool3d_bwd_kernel(const float* __restr
     if (od < OD && oh < OH && ow < OW) {
       // first max of the window in (d, h, w) scan order (torch max_pool3d CPU: val > max || isnan(val))
       float m = -INFINITY;
-      int64_t arg = -1;
+      I arg = -1;
       for (int a = 0; a < kd; ++a)
         for (int b = 0; b < kh; ++b)
           for (int e = 0; e < kw; ++e) {
-            const int64_t idx = ((((int64_t)n * v.D + od * kd + a) * v.H + oh * kh + b) * v.W + ow * kw + e) * C + c;
+            const I idx = ((((I)n * v.D + od * kd + a) * v.H + oh * kh + b) * v.W + ow * kw + e) * C + c;
             const float val = pool_act(y, stats, relu, C, c, idx);
             if (arg < 0 || val > m || isnan(val)) {
               m = val;
               arg = idx;
             }
           }
-      if (arg == i) g = dout[((((int64_t)n * OD + od) * OH + oh) * OW + ow) * C + c];
+      if (arg == i) g = dout[((((I)n * OD + od) * OH + oh) * OW + ow) * C + c];
     }
     dA[i] = g;
   }
@@ -218,8 +228,11 @@ int maxpool3d_bwd(const float* y, const float* stats, int relu, const Vol5& v, i
                   const float* dout, float* dA, hipStream_t st) {
   const int64_t total = v.numel();
   if (total == 0) return 0;
-  hipLaunchKernelGGL(maxpool3d_bwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 16384)), dim3(256), 0,
-                     st, y, stats, relu, v, kd, kh, kw, dout, dA);
+  const dim3 grid((unsigned)std::min<int64_t>(cdiv(total, 256), 16384));
+  if (total + (int64_t)grid.x * 256 < (1ll << 31))
+    hipLaunchKernelGGL(maxpool3d_bwd_kernel<int>, grid, dim3(256), 0, st, y, stats, relu, v, kd, kh, kw, dout, dA);
+  else
+    hipLaunchKernelGGL(maxpool3d_bwd_kernel<int64_t>, grid, dim3(256), 0, st, y, stats, relu, v, kd, kh, kw, dout, dA);
   VAD_LAUNCH_CHECK();
   return 0;
 }
