@@ -1131,6 +1131,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_bfc_blocks") g_bfc_blocks = value;
   else if (k == "conv_bfc_s2_ni2") g_bfc_s2_ni2 = value;
   else if (k == "conv3d_direct") g_conv3d_direct = value;
+  else if (k == "conv_wgrad_bn_fused") g_wgrad_bn_fused = value;
   else if (k == "conv_bfw_blocks") g_bfw_blocks = value;
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else if (k == "conv_wgrad_alone_blocks") g_tune.wgrad_alone_blocks = value;
@@ -1415,8 +1416,17 @@ int conv3_path(const Conv3Layer& L, int kind) {
   return x3 ? (g_conv_bf16 ? 1 : 6) : 0;
 }
 
+bool conv3_wgrad_bn_fusable(const Conv3Layer& L) {
+  return !g_act_bf16 && g_tune.wgrad_patch && !bfc_wgrad_supported(L) && x3_wgrad_tr_bn_supported(L);
+}
+
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
-                int* nsplit, int64_t partial_cap, hipStream_t st, bool alone) {
+                int* nsplit, int64_t partial_cap, hipStream_t st, bool alone, const float* bny, const float* bnst) {
+  if (bny) {  // dY = dA: the BN backward apply happens in the weight gradient's staging
+    VAD_CHECK(conv3_wgrad_bn_fusable(L), "conv3_wgrad: fused BN apply unsupported");
+    return x3_wgrad_tr(L, dY, src, src_stats, partial, nsplit, partial_cap, alone ? g_tune.wgrad_alone_blocks : 0, st,
+                       bny, bnst);
+  }
   if (bfc_wgrad_supported(L))
     return bfc_wgrad(L, reinterpret_cast<const __bf16*>(dY), reinterpret_cast<const __bf16*>(src), src_stats, partial,
                      nsplit, partial_cap, st);

@@ -606,3 +606,31 @@ def test_dir_affine_matches_plain_backward(B):
         assert e <= tol, f"{n}: relative L2 {e:.3g} between cad_dir_affine on and off"
     assert live >= 10  # the five layers' weights and biases carry a gradient
     print(f"B={B}: worst per-tensor relative L2 (affine vs plain) {worst:.3g}")
+
+
+def test_l0_bn_apply_fused_in_wgrad_is_bit_identical():
+    """Knob conv_wgrad_bn_fused (off by default): layer 0's BatchNorm backward apply folded into its weight gradient's dY staging
+    (x3_wgrad_tr_kernel<..., BNA = true>) computes bn_bwd_apply's expression on the loaded dA / y, so every gradient
+    is bit-identical to the separate apply pass (frozen stem, fp32)."""
+    from vad_amd import _native as nat
+    case = dict(name="bnf", B=2, T=3, H=64, W=80, seed=23, step=1, forced=None)
+    x = co.synth_clips(23, 1, 0, 2, 3, 64, 80).cuda()
+    y = co.synth_labels(0, 2).cuda()
+    runs = []
+    for fused in (1, 0):
+        nat.check(nat.lib().vad_set_tuning(b"conv_wgrad_bn_fused", fused))
+        try:
+            eng = _frozen(make_cad_model(case)).cuda().engine()
+            eng.forward(x, True, 23, 1, 0, y)
+            eng.backward(True)
+            torch.cuda.synchronize()
+            runs.append(eng.grads[:eng.param_floats].cpu().clone())
+        finally:
+            nat.check(nat.lib().vad_set_tuning(b"conv_wgrad_bn_fused", 0))
+    i = eng.slot_names.index("backbone.layer1.0.conv1.weight") if "backbone.layer1.0.conv1.weight" in eng.slot_names \
+        else None
+    assert runs[0].abs().sum() > 0
+    assert torch.equal(runs[0], runs[1]), float((runs[0] - runs[1]).abs().max())
+    if i is not None:
+        o, k = eng.slot_offset[i], eng.slot_numel[i]
+        assert runs[0][o:o + k].abs().sum() > 0
