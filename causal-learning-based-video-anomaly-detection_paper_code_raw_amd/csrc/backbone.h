@@ -78,8 +78,9 @@ struct Conv3Layer {
 // weight relayout: W[co][ci][3][3] -> Wf[co][9][ci] and per-parity-class dgrad images Wd[ci][taps][co]
 int conv3_prep_weights(const float* w, const Conv3Layer& L, float* wf, float* wd, hipStream_t st);
 // the same for n <= 8 layers in one launch
+// w3 (nullable, per layer nullable): also the pre-split bf16-plane Wd image of conv3_x3_dgrad_s2
 int conv3_prep_weights_all(int n, const float* const* w, const Conv3Layer* L, float* const* wf, float* const* wd,
-                           hipStream_t st);
+                           hipStream_t st, __bf16* const* w3 = nullptr);
 int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats /*nullable: BN+ReLU on load*/,
               const float* wf, const float* bias, float* y, float* partials, int* nparts, hipStream_t st,
               int* parts_cm = nullptr);  // parts_cm: in = accepted, out = 1 if written so
@@ -94,7 +95,7 @@ struct BnBwdFuse {
   int* nparts;
 };
 int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,
-                const BnBwdFuse* f = nullptr);
+                const BnBwdFuse* f = nullptr, const __bf16* w3 = nullptr);
 // direct LDS-patch kernels (conv_patch.hip) for stride-1 layers; conv3_fwd / conv3_dgrad route there by default
 bool conv3_patch_supported(const Conv3Layer& L, bool fwd);
 extern int g_patch_persist;  // single-chunk (C == 32) stride-1 layers on the persistent patch kernel
@@ -133,8 +134,12 @@ int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float*
 // sharing one dY patch; Wd in the plain [Ci][9][Co] layout (conv3_prep_weights with classes == 0)
 extern int g_dgrad_s2_x3;  // knob "conv_dgrad_s2_x3"
 bool conv3_x3_dgrad_s2_supported(const Conv3Layer& L);
+// w3 (nullable): the Wd image pre-split into bf16 planes [Ci][9][Co/16][3][16] (conv3_prep_weights_all's w3 image):
+// the weight staging copies it instead of splitting fp32 weights in every block
 int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,
-                      const BnBwdFuse* f = nullptr);
+                      const BnBwdFuse* f = nullptr, const __bf16* w3 = nullptr);
+extern int g_dgrad_s2_w3;  // knob "conv_dgrad_s2_w3": the plan pre-splits the stride-2 Wd images (1, default)
+bool conv3_dgrad_w3_wanted(const Conv3Layer& L);
 extern int g_wgrad_split;     // stride-1 weight gradients on the split-bf16 kernel (knob "conv_wgrad_split")
 extern int g_wgrad_s1_nt, g_wgrad_s1_nt_blocks, g_wgrad_s1_nt_wide;  // knobs "conv_wgrad_s1_nt", "conv_wgrad_s1_nt_blocks"
 extern int g_wgrad_s2_blocks;  // their target grid size (knob "conv_wgrad_s2_blocks")

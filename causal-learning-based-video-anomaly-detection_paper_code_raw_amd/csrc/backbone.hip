@@ -1132,6 +1132,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_bfc_s2_ni2") g_bfc_s2_ni2 = value;
   else if (k == "conv3d_direct") g_conv3d_direct = value;
   else if (k == "conv_wgrad_bn_fused") g_wgrad_bn_fused = value;
+  else if (k == "conv_dgrad_s2_w3") g_dgrad_s2_w3 = value;
   else if (k == "conv_bfw_blocks") g_bfw_blocks = value;
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else if (k == "conv_wgrad_alone_blocks") g_tune.wgrad_alone_blocks = value;
@@ -1226,6 +1227,7 @@ struct PrepTab {
   const float* w[8];
   float* wf[8];
   float* wd[8];
+  __bf16* w3[8];  // nullable: pre-split bf16 planes of Wd, [ci][tap][co / 16][3][16]
   int Ci[8], Co[8], classes[8];
   int64_t end[8];  // inclusive prefix sums of Co*Ci*9
   int n;
@@ -1249,6 +1251,15 @@ __global__ void conv3_prep_all_kernel(const PrepTab t) {
       reinterpret_cast<__bf16*>(t.wf[l] + tot)[((int64_t)co * 9 + tap) * Ci + ci] = (__bf16)v;
       reinterpret_cast<__bf16*>(t.wd[l] + tot)[((int64_t)ci * 9 + tap) * Co + co] = (__bf16)v;
     }
+    if (t.w3[l]) {  // (the split of put_planes / split3: hi, mid, lo)
+      const __bf16 h = (__bf16)v;
+      const float r = v - (float)h;
+      const __bf16 m = (__bf16)r;
+      __bf16* d = t.w3[l] + ((((int64_t)ci * 9 + tap) * (Co / 16) + co / 16) * 3) * 16 + co % 16;
+      d[0] = h;
+      d[16] = m;
+      d[32] = (__bf16)(r - (float)m);
+    }
     if (!t.classes[l]) {
       t.wd[l][((int64_t)ci * 9 + tap) * Co + co] = v;
     } else {
@@ -1268,7 +1279,7 @@ __global__ void conv3_prep_all_kernel(const PrepTab t) {
 }
 
 int conv3_prep_weights_all(int n, const float* const* w, const Conv3Layer* L, float* const* wf, float* const* wd,
-                           hipStream_t st) {
+                           hipStream_t st, __bf16* const* w3) {
   VAD_CHECK(n >= 1 && n <= 8, "conv3_prep_weights_all: 1..8 layers");
   PrepTab t{};
   t.n = n;
@@ -1278,6 +1289,8 @@ int conv3_prep_weights_all(int n, const float* const* w, const Conv3Layer* L, fl
     t.w[l] = w[l];
     t.wf[l] = wf[l];
     t.wd[l] = wd[l];
+    t.w3[l] = w3 ? w3[l] : nullptr;
+    VAD_CHECK(!t.w3[l] || L[l].Co % 16 == 0, "conv3_prep_weights_all: pre-split Wd needs Co % 16 == 0");
     t.Ci[l] = L[l].Ci;
     t.Co[l] = L[l].Co;
     t.classes[l] = L[l].stride == 2 && !(g_tune.patch && conv3_patch_supported(L[l], false));
@@ -1340,7 +1353,7 @@ static int dgrad_launch(const ConvGeom& g, const TapTable& taps, const float* dY
 }
 
 int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,
-                const BnBwdFuse* f) {
+                const BnBwdFuse* f, const __bf16* w3) {
   VAD_CHECK(L.Co % 32 == 0, "conv3_dgrad: Co must be a multiple of 32");
   const int N = L.Ci;
   if (f) *f->nparts = 0;
@@ -1351,7 +1364,7 @@ int conv3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float* dX
     return conv3_x3_dgrad(L, dY, wd, dX, st, (g_bn_bwd_fuse & 1) ? f : nullptr);
   // (the split kernel reads the plain Wd layout, which the prep writes exactly when the f32 patch kernel is usable)
   if (g_tune.patch && conv3_patch_supported(L, false) && conv3_x3_dgrad_s2_supported(L))
-    return conv3_x3_dgrad_s2(L, dY, wd, dX, st, (g_bn_bwd_fuse & 2) ? f : nullptr);
+    return conv3_x3_dgrad_s2(L, dY, wd, dX, st, (g_bn_bwd_fuse & 2) ? f : nullptr, w3);
   VAD_CHECK(!g_act_bf16, "conv3_dgrad: bf16 activations need the split kernels");
   if (g_tune.patch && conv3_patch_supported(L, false)) return conv3_patch_dgrad(L, dY, wd, dX, st);
   if (L.stride == 1) {

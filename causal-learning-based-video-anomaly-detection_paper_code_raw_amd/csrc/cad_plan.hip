@@ -333,6 +333,7 @@ struct CadPlanImpl {
   int32_t* steps = nullptr;
   // workspace carve
   float *y1, *pool, *y[8], *stats[9], *parts, *wf[8], *wd[8], *feats, *pooled;
+  __bf16* w3[8] = {};  // the pre-split Wd planes the last prep wrote (stride-2 input gradients), per layer or null
   float *poolb[2] = {nullptr, nullptr}, *stats0b[2] = {nullptr, nullptr}, *parts_stem = nullptr;
   float *dh[5], *dlog, *gh[5], *glog;
   float* wt[5] = {};  // transposed detector_net weights of layers 1-4 (mlp_tail_fwd)
@@ -497,7 +498,7 @@ struct CadPlanImpl {
       y[l] = w.take<float>(nf * L[l].OH * L[l].OW * L[l].Co);
       // (fp32 image + its bf16 copy: conv3_bf16_image)
       wf[l] = w.take<float>((int64_t)L[l].Co * L[l].Ci * 9 * 3 / 2);
-      wd[l] = w.take<float>((int64_t)L[l].Co * L[l].Ci * 9 * 3 / 2);
+      wd[l] = w.take<float>((int64_t)L[l].Co * L[l].Ci * 9 * 5 / 2);  // fp32 | bf16 copy or 3 bf16 planes
       act_max = std::max<int64_t>(act_max, nf * L[l].OH * L[l].OW * L[l].Co);
     }
     const int cs[9] = {32, 32, 32, 64, 64, 128, 128, 256, 256};
@@ -755,7 +756,9 @@ struct CadPlanImpl {
       hipStream_t st = g_cad_prep_stream ? st2 : st0;
       const float* w8[8];
       for (int l = 0; l < 8; ++l) w8[l] = P(LY.conv_w[l]);
-      TIMED("prep", conv3_prep_weights_all(8, w8, L, wf, wd, st));
+      for (int l = 0; l < 8; ++l)
+        w3[l] = conv3_dgrad_w3_wanted(L[l]) ? reinterpret_cast<__bf16*>(wd[l] + (int64_t)L[l].Co * L[l].Ci * 9) : nullptr;
+      TIMED("prep", conv3_prep_weights_all(8, w8, L, wf, wd, st, w3));
       TIMED("prep", mlp_transpose(mlp_transpose_args(), st));
       VAD_HIP(hipEventRecord(ev_prep, st));
     }
@@ -1064,7 +1067,7 @@ struct CadPlanImpl {
       if (l > 0) {
         // its epilogue also reduces layer l-1's BN backward (dZ = dA masked by layer l-1's ReLU, dZ * xhat)
         const BnBwdFuse fu{y[l - 1], stats[l], parts, parts_floats, &fused_np};
-        TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st, &fu));
+        TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st, &fu, w3[l]));
       }
       if (l == debug_stop_layer) break;
     }

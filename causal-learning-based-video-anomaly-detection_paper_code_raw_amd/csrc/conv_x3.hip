@@ -41,6 +41,7 @@ struct X3Args {
   // shift); per-block sums of dZ = dX [scale*y + shift > 0] and dZ * xhat go to partials, column-major [2N][gridDim.x]
   const void* bny;
   const float* bnst;
+  const __bf16* w3;  // stride-2 input gradient: pre-split Wd planes [N][9][C / 16][3][16] (nullable)
 };
 
 // epilogue half of the fused BN-backward reduce (bn_bwd_reduce_kernel's arithmetic on the value just computed; with
@@ -976,8 +977,10 @@ __device__ __forceinline__ void dgrad_s2x3_class(f32x16 (&acc)[NT], const __bf16
   }
 }
 
-template <int NT, int PC, int NP, bool AB = false>
+// W3: the weight slices come pre-split (p.w3, PC == 16, NP == 3): plain 16-B copies instead of the fp32 load + split
+template <int NT, int PC, int NP, bool AB = false, bool W3 = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args p) {
+  static_assert(!W3 || (NP == 3 && PC == 16), "pre-split weights: 3 planes of 16-channel slices");
   static_assert(PC % 16 == 0, "16-deep K steps");
   static_assert(!AB || NP == 1, "bf16 storage with bf16 operands only");
   using TA = act_t<AB>;
@@ -1002,10 +1005,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args
 
   constexpr int PQ = PROWS * G8, PIT = (PQ + 255) / 256;
   constexpr int WQ = NC * 9 * G8, WIT = (WQ + 255) / 256;
+  constexpr int W3Q = NC * 9 * 6, W3IT = (W3Q + 255) / 256;  // W3: 16-B pieces, 6 per (n, tap) row
   const int g8 = tid % G8;
   act_raw4<AB> pv[PIT][2];
-  f32x4 wv[WIT][2];
-  bool pok[PIT], wok[WIT];
+  f32x4 wv[W3 ? 1 : WIT][2];
+  bf16x8 w3v[W3 ? W3IT : 1];
+  bool pok[PIT], wok[W3 ? W3IT : WIT];
   // unconditional loads from clamped addresses; out-of-range rows are zeroed at stash time (see conv3x3_x3_kernel)
   auto fetch = [&](int c0) {
 #pragma unroll
@@ -1017,13 +1022,23 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args
       pv[it][0] = act_ld4(s);
       pv[it][1] = act_ld4(s + 4);
     }
+    if constexpr (W3) {
 #pragma unroll
-    for (int it = 0; it < WIT; ++it) {
-      const int q = tid + it * 256, n = q / (9 * G8), t = (q / G8) % 9;
-      wok[it] = q < WQ && n0 + n < p.N;
-      const float* s = p.w + c0 + g8 * 8 + (wok[it] ? ((int64_t)(n0 + n) * 9 + t) * p.C : (int64_t)0);
-      wv[it][0] = *reinterpret_cast<const f32x4*>(s);
-      wv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
+      for (int it = 0; it < W3IT; ++it) {
+        const int q = tid + it * 256, n = q / 54, t = (q / 6) % 9, j = q % 6;
+        wok[it] = q < W3Q && n0 + n < p.N;
+        const __bf16* s = p.w3 + (wok[it] ? (((int64_t)(n0 + n) * 9 + t) * (p.C / 16) + c0 / 16) * 48 + j * 8 : 0);
+        w3v[it] = *reinterpret_cast<const bf16x8*>(s);
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < WIT; ++it) {
+        const int q = tid + it * 256, n = q / (9 * G8), t = (q / G8) % 9;
+        wok[it] = q < WQ && n0 + n < p.N;
+        const float* s = p.w + c0 + g8 * 8 + (wok[it] ? ((int64_t)(n0 + n) * 9 + t) * p.C : (int64_t)0);
+        wv[it][0] = *reinterpret_cast<const f32x4*>(s);
+        wv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
+      }
     }
   };
   auto stash = [&]() {
@@ -1041,18 +1056,31 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args
         put_planes<NP>(patch + (q / G8) * RP + g8 * 8, PC, v, false);
       }
     }
+    if constexpr (W3) {
 #pragma unroll
-    for (int it = 0; it < WIT; ++it) {
-      const int q = tid + it * 256;
-      if (q < WQ) {
-        const int n = q / (9 * G8), t = (q / G8) % 9;
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = wok[it] ? wv[it][0][e] : 0.f;
-          v[4 + e] = wok[it] ? wv[it][1][e] : 0.f;
+      for (int it = 0; it < W3IT; ++it) {
+        const int q = tid + it * 256;
+        if (q < W3Q) {
+          const int n = q / 54, t = (q / 6) % 9, j = q % 6;
+          bf16x8 v = w3v[it];
+          if (!wok[it]) v = bf16x8{};
+          *reinterpret_cast<bf16x8*>(wl + n * WP + t * NP * PC + j * 8) = v;
         }
-        put_planes<NP>(wl + n * WP + t * NP * PC + g8 * 8, PC, v, false);
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < WIT; ++it) {
+        const int q = tid + it * 256;
+        if (q < WQ) {
+          const int n = q / (9 * G8), t = (q / G8) % 9;
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = wok[it] ? wv[it][0][e] : 0.f;
+            v[4 + e] = wok[it] ? wv[it][1][e] : 0.f;
+          }
+          put_planes<NP>(wl + n * WP + t * NP * PC + g8 * 8, PC, v, false);
+        }
       }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // (see conv3x3_x3_kernel's stash)
@@ -1146,8 +1174,14 @@ bool conv3_x3_dgrad_s2_supported(const Conv3Layer& L) {
          L.OH == (L.IH - 1) / 2 + 1 && L.OW == (L.IW - 1) / 2 + 1;
 }
 
+int g_dgrad_s2_w3 = 1;
+
+bool conv3_dgrad_w3_wanted(const Conv3Layer& L) {
+  return g_dgrad_s2_w3 && !g_conv_bf16 && conv3_x3_dgrad_s2_supported(L);
+}
+
 int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,
-                      const BnBwdFuse* f) {
+                      const BnBwdFuse* f, const __bf16* w3) {
   VAD_CHECK(conv3_x3_dgrad_s2_supported(L), "conv3_x3_dgrad_s2: unsupported layer");
   X3Args a{};
   a.src = dY;
@@ -1175,6 +1209,10 @@ int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, flo
   } else if (g_conv_bf16) {
     if (nt2) VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<2, 16, 1>), grid, dim3(256), 0, st, a);
     else VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<1, 16, 1>), grid, dim3(256), 0, st, a);
+  } else if (w3) {
+    a.w3 = w3;
+    if (nt2) VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<2, 16, 3, false, true>), grid, dim3(256), 0, st, a);
+    else VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<1, 16, 3, false, true>), grid, dim3(256), 0, st, a);
   } else {
     if (nt2) VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<2, 16, 3>), grid, dim3(256), 0, st, a);
     else VAD_KLAUNCH((conv3x3_dgrad_s2x3_kernel<1, 16, 3>), grid, dim3(256), 0, st, a);

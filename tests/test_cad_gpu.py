@@ -634,3 +634,26 @@ def test_l0_bn_apply_fused_in_wgrad_is_bit_identical():
     if i is not None:
         o, k = eng.slot_offset[i], eng.slot_numel[i]
         assert runs[0][o:o + k].abs().sum() > 0
+
+
+def test_s2_dgrad_presplit_weights_bit_identical():
+    """Knob conv_dgrad_s2_w3: the stride-2 input gradients stage the weight image the prep pre-split into bf16 planes
+    (hi, mid, lo of each fp32 weight, split3's arithmetic) instead of splitting it in every block: every gradient
+    bit-identical."""
+    from vad_amd import _native as nat
+    case = dict(name="w3", B=2, T=3, H=96, W=80, seed=29, step=1, forced=None)
+    x = co.synth_clips(29, 1, 0, 2, 3, 96, 80).cuda()
+    y = co.synth_labels(0, 2).cuda()
+    runs = []
+    for on in (1, 0):
+        nat.check(nat.lib().vad_set_tuning(b"conv_dgrad_s2_w3", on))
+        try:
+            eng = _frozen(make_cad_model(case)).cuda().engine()
+            eng.forward(x, True, 29, 1, 0, y)
+            eng.backward(True)
+            torch.cuda.synchronize()
+            runs.append(eng.grads[:eng.param_floats].cpu().clone())
+        finally:
+            nat.check(nat.lib().vad_set_tuning(b"conv_dgrad_s2_w3", 1))
+    assert runs[0].abs().sum() > 0
+    assert torch.equal(runs[0], runs[1]), float((runs[0] - runs[1]).abs().max())
