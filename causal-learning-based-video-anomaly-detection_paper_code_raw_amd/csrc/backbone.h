@@ -138,7 +138,7 @@ bool conv3_x3_dgrad_s2_supported(const Conv3Layer& L);
 // the weight staging copies it instead of splitting fp32 weights in every block
 int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,
                       const BnBwdFuse* f = nullptr, const __bf16* w3 = nullptr);
-extern int g_dgrad_s2_w3;  // knob "conv_dgrad_s2_w3": the plan pre-splits the stride-2 Wd images (1, default)
+extern int g_dgrad_s2_w3, g_dgrad_s2_nt;  // knob "conv_dgrad_s2_w3": the plan pre-splits the stride-2 Wd images (1, default)
 bool conv3_dgrad_w3_wanted(const Conv3Layer& L);
 extern int g_wgrad_split;     // stride-1 weight gradients on the split-bf16 kernel (knob "conv_wgrad_split")
 extern int g_wgrad_s1_nt, g_wgrad_s1_nt_blocks, g_wgrad_s1_nt_wide;  // knobs "conv_wgrad_s1_nt", "conv_wgrad_s1_nt_blocks"

@@ -1133,6 +1133,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv3d_direct") g_conv3d_direct = value;
   else if (k == "conv_wgrad_bn_fused") g_wgrad_bn_fused = value;
   else if (k == "conv_dgrad_s2_w3") g_dgrad_s2_w3 = value;
+  else if (k == "conv_dgrad_s2_nt") g_dgrad_s2_nt = value;
   else if (k == "conv_bfw_blocks") g_bfw_blocks = value;
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else if (k == "conv_wgrad_alone_blocks") g_tune.wgrad_alone_blocks = value;

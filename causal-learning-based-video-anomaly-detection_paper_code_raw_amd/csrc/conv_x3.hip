@@ -1175,6 +1175,7 @@ bool conv3_x3_dgrad_s2_supported(const Conv3Layer& L) {
 }
 
 int g_dgrad_s2_w3 = 1;
+int g_dgrad_s2_nt = 1;  // knob "conv_dgrad_s2_nt": 1 = 32 input channels per block (default: config-2 layer 4 92 -> 75 us, profiles/r04_s2_nt_ab.json), 0 = 64 where the grid allows
 
 bool conv3_dgrad_w3_wanted(const Conv3Layer& L) {
   return g_dgrad_s2_w3 && !g_conv_bf16 && conv3_x3_dgrad_s2_supported(L);
@@ -1199,7 +1200,7 @@ int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, flo
   a.tiles_w = (int)cdiv((L.IW + 1) / 2, 8);
   const int tiles = L.NF * a.tiles_h * a.tiles_w;
   // 64 input channels per block where that still gives >= 2 blocks per CU, else 32
-  const bool nt2 = L.Ci % 64 == 0 && (int64_t)tiles * (L.Ci / 64) >= 512;
+  const bool nt2 = g_dgrad_s2_nt != 1 && L.Ci % 64 == 0 && (int64_t)tiles * (L.Ci / 64) >= 512;
   dim3 grid((unsigned)tiles, (unsigned)(L.Ci / (nt2 ? 64 : 32)));
   VAD_CHECK(!g_act_bf16 || g_conv_bf16, "conv3_x3_dgrad_s2: bf16 activations need conv_bf16");
   if (f) *f->nparts = tiles;
