@@ -657,20 +657,29 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_v_kernel(const act_t<AB>* __
 }
 
 int g_bn_apply_v = 1;  // knob "bn_apply_v": the streaming apply kernel (0: the 4-channel row loop)
+int g_bn_apply_u = 4;          // knob "bn_apply_u": rows in flight per thread (2, 4, 8)
+int g_bn_apply_blocks = 2048;  // knob "bn_apply_blocks": grid cap (grid-stride beyond it)
 
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
                  int* nparts, hipStream_t st) {
   const int P = bn_rows_parts(M, C);
   if (g_bn_apply_v && !bias_partials && C % 8 == 0 && C >= 8 && C <= 2048 && 256 % (C / 8) == 0) {
-    constexpr int U = 4;
+    const int U = g_bn_apply_u == 8 ? 8 : (g_bn_apply_u == 2 ? 2 : 4);
     const int rpp = 256 / (C / 8);
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(M, (int64_t)rpp * U), 2048));
-    if (g_act_bf16)
-      hipLaunchKernelGGL((bn_bwd_apply_v_kernel<true, U>), dim3(blocks), dim3(256), 0, st,
-                         reinterpret_cast<const __bf16*>(dA), reinterpret_cast<const __bf16*>(y), stats, M, C,
-                         reinterpret_cast<__bf16*>(dY));
-    else
-      hipLaunchKernelGGL((bn_bwd_apply_v_kernel<false, U>), dim3(blocks), dim3(256), 0, st, dA, y, stats, M, C, dY);
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(M, (int64_t)rpp * U), g_bn_apply_blocks));
+#define VAD_BNA(AB, UU, T)                                                                                            \
+  hipLaunchKernelGGL((bn_bwd_apply_v_kernel<AB, UU>), dim3(blocks), dim3(256), 0, st, reinterpret_cast<const T*>(dA), \
+                     reinterpret_cast<const T*>(y), stats, M, C, reinterpret_cast<T*>(dY))
+    if (g_act_bf16) {
+      if (U == 8) VAD_BNA(true, 8, __bf16);
+      else if (U == 2) VAD_BNA(true, 2, __bf16);
+      else VAD_BNA(true, 4, __bf16);
+    } else {
+      if (U == 8) VAD_BNA(false, 8, float);
+      else if (U == 2) VAD_BNA(false, 2, float);
+      else VAD_BNA(false, 4, float);
+    }
+#undef VAD_BNA
     VAD_LAUNCH_CHECK();
     *nparts = 0;
     return 0;
@@ -1134,6 +1143,8 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_bn_fused") g_wgrad_bn_fused = value;
   else if (k == "conv_dgrad_s2_w3") g_dgrad_s2_w3 = value;
   else if (k == "conv_dgrad_s2_nt") g_dgrad_s2_nt = value;
+  else if (k == "bn_apply_u") g_bn_apply_u = value;
+  else if (k == "bn_apply_blocks") g_bn_apply_blocks = value;
   else if (k == "conv_bfw_blocks") g_bfw_blocks = value;
   else if (k == "conv_wgrad_patch_blocks") g_tune.wgrad_patch_blocks = value;
   else if (k == "conv_wgrad_alone_blocks") g_tune.wgrad_alone_blocks = value;
