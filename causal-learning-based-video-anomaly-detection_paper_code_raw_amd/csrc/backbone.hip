@@ -1140,6 +1140,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_bfc_blocks") g_bfc_blocks = value;
   else if (k == "conv_bfc_s2_ni2") g_bfc_s2_ni2 = value;
   else if (k == "conv3d_direct") g_conv3d_direct = value;
+  else if (k == "conv3d_wgrad_blocks") g_conv3d_wg_blocks = value;
   else if (k == "conv_wgrad_bn_fused") g_wgrad_bn_fused = value;
   else if (k == "conv_dgrad_s2_w3") g_dgrad_s2_w3 = value;
   else if (k == "conv_dgrad_s2_nt") g_dgrad_s2_nt = value;

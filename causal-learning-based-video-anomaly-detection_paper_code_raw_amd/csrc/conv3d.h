@@ -69,7 +69,7 @@ int conv3d_prep_w3(const float* w, int N, int C, float* w3, hipStream_t st);
 // Direct Conv3d k3 s1 p1 for small channel counts (conv3d_direct.hip; fp32 FMA, no im2col).  Supported: Ci <= 16,
 // Co in {8, 16, 32} (knob "conv3d_direct" off: false).  prep: torch weight [Co][Ci][27] -> wf [Ci][27][Co] (forward)
 // and wd [Co][27][Ci] (flipped taps: the input gradient is conv3d_direct_fwd over dY with wd, CO = Ci).
-extern int g_conv3d_direct;
+extern int g_conv3d_direct, g_conv3d_wg_blocks;
 bool conv3d_direct_supported(int Ci, int Co);
 int conv3d_direct_prep(const float* w, int Co, int Ci, float* wf, float* wd, hipStream_t st);
 // out (NDHWC, in's spatial dims, CO channels) = conv(src) + bias (nullable)

@@ -17,6 +17,7 @@
 namespace vad {
 
 int g_conv3d_direct = 1;  // knob "conv3d_direct": the minicausal convs on these kernels (0: im2col + GEMM)
+int g_conv3d_wg_blocks = 512;  // knob "conv3d_wgrad_blocks": weight-gradient blocks (512: config 1 3.06 -> 3.01 ms over 256, profiles/r04_conv3d_wgrad_blocks_ab.json)
 
 constexpr int DT_D = 2, DT_H = 8, DT_W = 16;                                   // output tile: 256 voxels
 constexpr int HD = DT_D + 2, HH = DT_H + 2, HW = DT_W + 2, HALO = HD * HH * HW;  // 4 x 10 x 18 = 720
@@ -290,7 +291,7 @@ int conv3d_direct_fwd(const float* src, const Strides5& s, const Vol5& in, const
 int64_t conv3d_direct_wgrad_slab_floats(const Vol5& in, int CO) {
   int td, th, tw, nt;
   direct_tiles(in, td, th, tw, nt);
-  return (int64_t)std::min(nt, 256) * (in.C * 27 + 1) * CO;
+  return (int64_t)std::min(nt, std::max(1, g_conv3d_wg_blocks)) * (in.C * 27 + 1) * CO;
 }
 
 int conv3d_direct_wgrad(const float* dy, int CO, const float* src, const Strides5& s, const Vol5& in, float* dW,
@@ -305,7 +306,7 @@ int conv3d_direct_wgrad(const float* dy, int CO, const float* src, const Strides
   a.in = in;
   a.slab = slab;
   direct_tiles(in, a.tiles_d, a.tiles_h, a.tiles_w, a.ntiles);
-  const int nblk = std::min(a.ntiles, 256);
+  const int nblk = std::min(a.ntiles, std::max(1, g_conv3d_wg_blocks));
   const int P = in.C * 27 + 1;
   VAD_CHECK((int64_t)nblk * P * CO <= slab_floats, "conv3d_direct_wgrad: slab too small");
   if (nblk == 0) return 0;
