@@ -1060,7 +1060,9 @@ struct CadPlanImpl {
                                                l == 0 && !stem_grad, bnf ? y[0] : nullptr, bnf ? stats[1] : nullptr));
         TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], slab, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
         if (wgs && !on_main) VAD_HIP(hipEventRecord(ev_wg[l & 1], st));
-        if (l > 0 || !stem_grad) VAD_HIP(hipEventRecord(ev_layer[l], st));
+        // (layer 0: recorded after the join below -- its data-parallel bucket also holds layers 1-3, whose weight
+        // gradients may still run on the weight-gradient stream when layer 0's runs on the caller's)
+        if (l > 0) VAD_HIP(hipEventRecord(ev_layer[l], st));
         if (l == 0) VAD_HIP(hipEventRecord(ev_stem_free[spar], st));  // (layer 0's input read: set spar free)
       }
       fused_np = 0;
@@ -1075,6 +1077,8 @@ struct CadPlanImpl {
       VAD_HIP(hipEventRecord(ev_wgj, st3));
       VAD_HIP(hipStreamWaitEvent(st, ev_wgj, 0));
     }
+    // frozen stem: every backbone grad is final on the caller's stream here (the stem's own are recorded below)
+    if (!stem_grad) VAD_HIP(hipEventRecord(ev_layer[0], st));
     stem_active = 0;
     if (stem_grad && debug_stop_layer < 0) {
       VAD_CHECK(y1_fresh, "stem backward: the forward ran with the stem frozen (set option stem_grad before it)");

@@ -180,6 +180,10 @@ class ClipStager:
         self._ring = []  # [pinned u8, device u8 (direct=False), conversion-done event]
         self._k = 0
         self._dptr = {}  # pinned host pointer -> its device address
+        # direct mode: caller-owned pinned batches read in place over PCIe, kept alive until their conversion is done
+        # (the caching host allocator records no event for a kernel's reads, so a dropped batch could be reused, e.g.
+        # by a DataLoader pin thread, while the conversion still reads it)
+        self._inflight = []
 
     def _slot(self, shape):
         if len(self._ring) <= self._k or tuple(self._ring[self._k][0].shape) != tuple(shape):
@@ -187,6 +191,9 @@ class ClipStager:
             if len(self._ring) <= self._k:
                 self._ring.append(slot)
             else:
+                # (a shape change, e.g. the last partial batch: the old pinned buffer may still be read by its
+                # conversion -- direct mode reads it over PCIe, with no host-allocator event -- before it is freed)
+                self._ring[self._k][2].synchronize()
                 self._ring[self._k] = slot
         return self._ring[self._k]
 
@@ -228,6 +235,9 @@ class ClipStager:
             nat.check(nat.lib().vad_u8_to_clip(sp, src.numel(), self.mode, out.data_ptr(),
                                                ctypes.c_void_p(self.stream.cuda_stream)))
             done.record(self.stream)
+        if self.direct and slot is None:
+            self._inflight = [(b, e) for b, e in self._inflight if not e.query()]
+            self._inflight.append((src, done))
         return _Staged(out, done, slot)
 
     def finish(self, handle: _Staged, wait: bool = True) -> torch.Tensor:

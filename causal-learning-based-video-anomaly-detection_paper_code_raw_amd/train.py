@@ -31,10 +31,10 @@ class CadTrainer:
     """One fused train step per call; the building block of train_model and bench.py.
 
     Data parallel: one process per GPU; rank r processes global clips [r*B, (r+1)*B) of each step (RNG keyed by
-    global clip index), grads (+ has-grad flags) are summed by three bucketed all_reduces -- causal head + direct
-    classifier + flags during the backbone backward, the detector only when some rank's detector has a gradient, the
-    backbone after its backward (_backward_overlapped) -- and scaled by 1/world inside the optimizer kernel; BN
-    running stats follow rank 0 (broadcast before each forward, DDP's broadcast_buffers).
+    global clip index), grads (+ has-grad flags) are summed by bucketed all_reduces -- detector + causal head + direct
+    classifier + flags during the backbone backward, the backbone in per-layer buckets as its layers finish
+    (_backward_overlapped) -- and scaled by 1/world inside the optimizer kernel; BN running stats follow rank 0
+    (broadcast right after each forward, DDP's broadcast_buffers).  No step blocks the host on the device.
 
     sync_bn=True (world > 1): SyncBatchNorm semantics -- every BN layer normalises over the whole group's batch
     (per-layer sums all-reduced in forward and backward), so the N-rank step equals the reference's single-process
@@ -65,7 +65,7 @@ class CadTrainer:
         self.eng.init_optimizer_state()
         self.sync_bn = bool(sync_bn) and self.dist
         # gradient buckets of the flat grad buffer (slot order: backbone | detector | causal head | direct classifier
-        # | has-grad flags): the detector bucket (13.3 MB) is all-reduced only when some rank's detector has a grad
+        # | has-grad flags): everything from the detector on is one bucket, summed beside the backbone backward
         names = self.eng.slot_names
         i0 = next(i for i, n in enumerate(names) if n.startswith("detector."))
         i1 = next(i for i in range(i0, len(names)) if not names[i].startswith("detector."))
@@ -127,6 +127,14 @@ class CadTrainer:
             if cur is not None:
                 self._bufs_ev = torch.cuda.Event()
                 self._bufs_ev.record(cur)
+        if (inputs_ready is not None and inputs_ready is not True and cur is not None
+                and (videos.dtype != torch.float32 or not videos.is_contiguous())):
+            # the forward converts these clips on the current stream: it must see them complete first (only fp32
+            # contiguous clips, e.g. ClipStager's, are read in place by the early stem alone)
+            if isinstance(inputs_ready, torch.cuda.Event):
+                cur.wait_event(inputs_ready)
+            else:
+                cur.wait_stream(inputs_ready)
         if inputs_ready is not None and cur is not None:
             # the early stem waits for the inputs and for the last buffer broadcast (it updates bn1's running stats),
             # not for the previous step's tail on the current stream
@@ -153,10 +161,8 @@ class CadTrainer:
         else:
             eng.backward(True)
             if self.dist:
-                d0, d1 = self.det_range
-                self._reduce(eng.grads[d1:])  # causal head + direct classifier + has-grad flags
-                if float(eng.grads[eng.param_floats]) > 0:
-                    self._reduce(eng.grads[d0:d1])
+                d0 = self.det_range[0]
+                self._reduce(eng.grads[d0:])  # detector + causal head + direct classifier + has-grad flags
                 self._reduce(eng.grads[:d0])
         eng.optimizer_step(self.lr if lr is None else lr, self.betas, self.eps, self.wd, self.max_norm,
                            1.0 / self.world)
@@ -170,44 +176,33 @@ class CadTrainer:
     def _backward_overlapped(self):
         """Backward in two stages with the gradient all-reduce in buckets (DDP's reduce-during-backward, with the
         splits chosen for this model's grad order):
-          1. causal head + direct classifier + the has-grad flags, summed on a side stream while the backbone backward
-             runs on the compute stream (which waits only for the detector's input gradient);
+          1. detector + causal head + direct classifier + the has-grad flags, summed on a side stream while the
+             backbone backward runs on the compute stream (which waits only for the detector's input gradient).  The
+             detector part (13.3 MB) is identically zero on every rank when no box is in range (every frame took the
+             fallback box, cad:221-226) -- it is summed anyway: skipping it would need the flag on the host, i.e. a
+             host wait on the device every step, while its all-reduce runs beside the ~1 ms backbone backward;
           2. the backbone in four buckets (self.bb_buckets), each issued behind the plan's event for the last of its
-             layers to finish (vad_cad_wait_layer_grads), so layer 7's all-reduce runs beside layers 6-0's backward;
-          3. the detector, only when the summed detector flag says some rank's detector has a gradient (it is
-             identically zero on every rank otherwise: every frame took the fallback box, cad:221-226).  The decision
-             must be the same on every rank (collectives are matched by issue order), so the host reads the summed
-             flag -- after every other bucket is queued: by then the flag's all-reduce (bucket 1, issued first) has
-             long completed on the GPU, and the wait holds back only the optimizer's enqueue, never GPU work.
-        The optimizer waits for all of them.  Each element is summed over the same ranks as one all_reduce of the
-        whole buffer, so results are identical to it."""
+             layers to finish (vad_cad_wait_layer_grads), so layer 7's all-reduce runs beside layers 6-0's backward.
+        The optimizer waits for all of them; the host never waits for the device.  Each element is summed over the
+        same ranks as one all_reduce of the whole buffer, so results are identical to it."""
         eng = self.eng
         main = torch.cuda.current_stream(eng.device)
         if getattr(self, "_comm", None) is None:
             self._comm = torch.cuda.Stream(eng.device)
-            self._flag_host = torch.zeros(2, dtype=torch.float32, pin_memory=True)
-            self._flag_ev = torch.cuda.Event()
         side = self._comm
-        d0, d1 = self.det_range
-        pf = eng.param_floats
+        d0 = self.det_range[0]
         # stage 2: the causal-head / detector backward keeps running on the plan's side stream while the backbone
         # (stage 1) starts; the all-reduce stream waits for both that side stream and the compute stream
         eng.backward(True, stage=2)
         eng.wait_side(side)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            self._reduce(eng.grads[d1:])
-            self._flag_host.copy_(eng.grads[pf:pf + 2], non_blocking=True)
-            self._flag_ev.record(side)
+            self._reduce(eng.grads[d0:])
         eng.backward(True, stage=1)
         for lo, hi, layer in self.bb_buckets:
             eng.wait_layer_grads(layer, side)
             with torch.cuda.stream(side):
                 self._reduce(eng.grads[lo:hi])
-        self._flag_ev.synchronize()
-        if float(self._flag_host[0]) > 0:
-            with torch.cuda.stream(side):
-                self._reduce(eng.grads[d0:d1])
         main.wait_stream(side)
 
 

@@ -24,14 +24,19 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, use_gpu, out_path):
+def _worker(rank, world, port, use_gpu, out_path, frozen=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        import contextlib
+        import io
         from vad_amd.cad import CausalAnomalyDetector
-        from vad_amd.train import CadTrainer
+        from vad_amd.train import CadTrainer, apply_memory_efficient_training
         torch.manual_seed(0)
         m = CausalAnomalyDetector()
+        if frozen:
+            with contextlib.redirect_stdout(io.StringIO()):
+                apply_memory_efficient_training(m)
         batches = make_batches(world, **SHAPE)
         x, y = batches[rank]
         if use_gpu:
@@ -43,7 +48,8 @@ def _worker(rank, world, port, use_gpu, out_path):
         for _ in range(2):
             tr.step(x, y)
         if rank == 0:
-            torch.save({"params": tr.eng.params.cpu(), "bufs": tr.eng.bufs.cpu()}, out_path)
+            torch.save({"params": tr.eng.params.cpu(), "bufs": tr.eng.bufs.cpu(), "grads": tr.eng.grads.cpu()},
+                       out_path)
     finally:
         dist.destroy_process_group()
 
@@ -89,9 +95,9 @@ def test_dp_syncbn_protocol_cpu_gloo(tmp_path):
         np.testing.assert_allclose(got[r]["bufs"].numpy(), eng.bufs.numpy(), rtol=1e-5, atol=1e-6)
 
 
-def _run(use_gpu, tmp_path):
+def _run(use_gpu, tmp_path, frozen=False):
     out = str(tmp_path / "rank0.pt")
-    mp.spawn(_worker, args=(2, _free_port(), use_gpu, out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), use_gpu, out, frozen), nprocs=2, join=True)
     return torch.load(out, weights_only=True)
 
 
@@ -107,17 +113,31 @@ def test_dp_protocol_cpu_gloo(tmp_path):
 
 
 @pytest.mark.gpu
-def test_dp_hip_engine_gloo_two_ranks(tmp_path):
-    got = _run(True, tmp_path)
+@pytest.mark.parametrize("frozen", [False, True], ids=["stem-trains", "stem-frozen"])
+def test_dp_hip_engine_gloo_two_ranks(frozen, tmp_path):
+    """Two gloo ranks on cuda:0 with the bucketed, overlapped all-reduce: params, BN buffers and the summed grads of
+    the last step equal the single-process emulation (each rank's backward, then ONE sum of the whole grad buffer)
+    bit for bit.  stem-frozen is the trainer default (apply_memory_efficient_training): layer 0's weight gradient
+    runs on the caller's stream while layers 1-3's may still run on the weight-gradient stream, and the layers 0-3
+    bucket must wait for both."""
+    import contextlib
+    import io
+    got = _run(True, tmp_path, frozen)
     from vad_amd.cad import CausalAnomalyDetector
+    from vad_amd.train import apply_memory_efficient_training
     torch.manual_seed(0)
-    m = CausalAnomalyDetector().cuda()
+    m = CausalAnomalyDetector()
+    if frozen:
+        with contextlib.redirect_stdout(io.StringIO()):
+            apply_memory_efficient_training(m)
+    m = m.cuda()
     eng = m.engine()
     batches = [(x.cuda(), y.cuda()) for x, y in make_batches(2, **SHAPE)]
     emulate_dp_steps(eng, batches, 2, 2)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(got["params"].numpy(), eng.params.cpu().numpy())
     np.testing.assert_array_equal(got["bufs"].numpy(), eng.bufs.cpu().numpy())
+    np.testing.assert_array_equal(got["grads"].numpy(), eng.grads.cpu().numpy())
 
 
 # ---------------------------------------------------------------- the collective path on RCCL (nccl) at world 1
@@ -194,10 +214,10 @@ def test_early_stem_equals_serial_steps(tmp_path):
                          ids=["ddp-fallback", "ddp-forced", "syncbn-fallback"])
 def test_collective_path_rccl_world1(sync_bn, forced, tmp_path):
     """CadTrainer's data-parallel protocol forced on at world size 1 (force_dist): the stage-2/stage-1 overlapped
-    backward with its three all-reduce buckets (the detector bucket skipped on device-read flags when no box is in
-    range), the BN-buffer broadcasts and, with sync_bn, the SyncBatchNorm callback (dist.all_reduce from inside the
+    backward with its all-reduce buckets, the BN-buffer broadcasts and, with sync_bn, the SyncBatchNorm callback (dist.all_reduce from inside the
     library's ctypes callback).  On RCCL (backend nccl) the result equals the gloo run bit for bit, and in DDP mode
-    also the plain single-process step (a world-1 all-reduce is the identity)."""
+    also the plain single-process step (a world-1 all-reduce is the identity).  Every bucket is issued every step
+    (the detector bucket too: no host read of the has-grad flag)."""
     res = {}
     for backend in ("nccl", "gloo"):
         out = str(tmp_path / f"{backend}.pt")
@@ -205,10 +225,8 @@ def test_collective_path_rccl_world1(sync_bn, forced, tmp_path):
         res[backend] = torch.load(out, weights_only=True)
     for k in ("params", "bufs", "grads", "floats"):
         assert torch.equal(res["nccl"][k], res["gloo"][k]), k
-    d0, d1 = res["nccl"]["det_range"].tolist()
     total = res["nccl"]["grads"].numel()
-    want = total if forced else total - (d1 - d0)  # the detector bucket only when a box is in range
-    assert res["nccl"]["floats"].tolist() == [want, want]
+    assert res["nccl"]["floats"].tolist() == [total, total]  # every bucket every step (no host-side skip)
     if not sync_bn:
         plain = _world1_run(False, forced, force_dist=False)
         for k in ("params", "bufs", "grads"):
