@@ -156,6 +156,14 @@ int x3_wgrad_tr(const Conv3Layer& L, const float* dY, const float* src, const fl
                 const float* bnst = nullptr);
 extern int g_wgrad_bn_fused;  // knob "conv_wgrad_bn_fused"
 bool x3_wgrad_tr_bn_supported(const Conv3Layer& L);
+// fp32 weight gradients on pre-split bf16 operand planes staged by LDS-DMA (conv_x3d.hip): dy_planes [3][NF OH OW][Co]
+// (split dY), x_planes [3][NF IH IW][Ci] (split relu(bn(x))) -- planes_split writes both
+extern int g_wgrad_dma, g_wgrad_dma_blocks, g_wgrad_dma_nb;  // knobs "conv_wgrad_dma", "conv_wgrad_dma_blocks", "conv_wgrad_dma_nb"
+bool x3_wgrad_dma_supported(const Conv3Layer& L);
+int x3_wgrad_dma(const Conv3Layer& L, const __bf16* dy_planes, const __bf16* x_planes, float* slab, int* nsplit,
+                 int64_t partial_cap, int target_blocks, hipStream_t st);
+// fp32 [M][C] -> bf16 planes [3][M][C] (hi, mid, lo), with BN + ReLU (stats = the producer's BN state) when given
+int planes_split(const float* src, const float* stats, int64_t M, int C, __bf16* dst, hipStream_t st);
 bool conv3_wgrad_patch_supported(const Conv3Layer& L);
 int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
                       int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);

@@ -1142,6 +1142,9 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv3d_direct") g_conv3d_direct = value;
   else if (k == "conv3d_wgrad_blocks") g_conv3d_wg_blocks = value;
   else if (k == "conv_wgrad_bn_fused") g_wgrad_bn_fused = value;
+  else if (k == "conv_wgrad_dma") g_wgrad_dma = value;
+  else if (k == "conv_wgrad_dma_blocks") g_wgrad_dma_blocks = value;
+  else if (k == "conv_wgrad_dma_nb") g_wgrad_dma_nb = value;
   else if (k == "conv_dgrad_s2_w3") g_dgrad_s2_w3 = value;
   else if (k == "conv_dgrad_s2_nt") g_dgrad_s2_nt = value;
   else if (k == "bn_apply_u") g_bn_apply_u = value;

@@ -364,6 +364,10 @@ struct CadPlanImpl {
   // shared dY buffer (one cross-queue barrier per layer less); ~2x the dY memory (≈210 MB at config 2)
   float* dYL[8] = {};
   int dy_per_layer = 1;
+  // pre-split operand planes of the weight gradients on x3_wgrad_dma_kernel (knob conv_wgrad_dma): dY and the layer
+  // input relu(bn(x)) as bf16 [3][pixels][channels], one pair per queue that runs weight gradients ([0]: the
+  // weight-gradient stream, [1]: the caller's stream, layer 0 with the frozen stem); fp32 plans only
+  __bf16 *pl_dy[2] = {}, *pl_x[2] = {};
   float *sq_parts, *slot_info, *clip;
   int16_t* chunk_slot;
   int64_t parts_floats, dense_scratch_floats, wpart_floats, wpart0_floats, slab_len, act_max;
@@ -569,6 +573,10 @@ struct CadPlanImpl {
     wpart = w.take<float>(wpart_floats);
     wpart0_floats = std::max<int64_t>(8ll << 20, (int64_t)L[0].Co * 9 * L[0].Ci);
     wpart0 = w.take<float>(wpart0_floats);
+    for (int q = 0; q < 2; ++q) {
+      pl_dy[q] = conv_bf16 ? nullptr : w.take<__bf16>(3 * act_max);
+      pl_x[q] = conv_bf16 ? nullptr : w.take<__bf16>(3 * act_max);
+    }
     sq_parts = w.take<float>(1024);
     bnsync = w.take<double>(2 * 256);
     slot_info = w.take<float>(4 * 160);
@@ -1056,8 +1064,17 @@ struct CadPlanImpl {
         hipStream_t st = wst;
         int ns = 0;
         // (layer 0 with the frozen stem: little runs beside its weight gradient)
-        TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], bnf ? dA : dYl, src, sst, slab, &ns, slab_cap, st,
-                                               l == 0 && !stem_grad, bnf ? y[0] : nullptr, bnf ? stats[1] : nullptr));
+        if (!bnf && pl_dy[0] && x3_wgrad_dma_supported(L[l])) {
+          // split dY and the layer input into bf16 planes (on this queue), then the LDS-DMA weight gradient
+          const int q = on_main ? 1 : 0;
+          const int64_t Mi = (int64_t)NF * L[l].IH * L[l].IW;
+          TIMED(L_("wgrad_planes", l), planes_split(dYl, nullptr, M, C, pl_dy[q], st));
+          TIMED(L_("wgrad_planes", l), planes_split(src, sst, Mi, L[l].Ci, pl_x[q], st));
+          TIMED(L_("conv_wgrad", l), x3_wgrad_dma(L[l], pl_dy[q], pl_x[q], slab, &ns, slab_cap, 0, st));
+        } else {
+          TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], bnf ? dA : dYl, src, sst, slab, &ns, slab_cap, st,
+                                                 l == 0 && !stem_grad, bnf ? y[0] : nullptr, bnf ? stats[1] : nullptr));
+        }
         TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], slab, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
         if (wgs && !on_main) VAD_HIP(hipEventRecord(ev_wg[l & 1], st));
         // (layer 0: recorded after the join below -- its data-parallel bucket also holds layers 1-3, whose weight

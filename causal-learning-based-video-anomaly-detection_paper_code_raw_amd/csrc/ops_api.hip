@@ -35,6 +35,17 @@ extern "C" int vad_conv3x3_wgrad(const float* x_nhwc, const float* dy_nhwc, int 
                                  int stride, float* dW, float* partial, int64_t partial_floats, void* stream) {
   Conv3Layer L{NF, Ci, Co, IH, IW, (IH - 1) / stride + 1, (IW - 1) / stride + 1, stride};
   int ns = 0;
+  if (x3_wgrad_dma_supported(L)) {  // (knob conv_wgrad_dma) the operand planes live at the end of the scratch
+    const int64_t mo = (int64_t)L.NF * L.OH * L.OW * L.Co, mi = (int64_t)L.NF * L.IH * L.IW * L.Ci;
+    const int64_t pf = (3 * (mo + mi) + 1) / 2 + 64;
+    VAD_CHECK(partial_floats > pf, "vad_conv3x3_wgrad: scratch too small for the operand planes");
+    __bf16* pdy = reinterpret_cast<__bf16*>(partial + (partial_floats - pf) / 64 * 64);
+    __bf16* px = pdy + 3 * mo;
+    VAD_TRY(planes_split(dy_nhwc, nullptr, mo / L.Co, L.Co, pdy, (hipStream_t)stream));
+    VAD_TRY(planes_split(x_nhwc, nullptr, mi / L.Ci, L.Ci, px, (hipStream_t)stream));
+    VAD_TRY(x3_wgrad_dma(L, pdy, px, partial, &ns, (partial_floats - pf) / 64 * 64, 0, (hipStream_t)stream));
+    return conv3_wgrad_reduce(L, partial, ns, nullptr, 0, dW, nullptr, (hipStream_t)stream);
+  }
   VAD_TRY(conv3_wgrad(L, dy_nhwc, x_nhwc, nullptr, partial, &ns, partial_floats, (hipStream_t)stream));
   return conv3_wgrad_reduce(L, partial, ns, nullptr, 0, dW, nullptr, (hipStream_t)stream);
 }

@@ -153,20 +153,23 @@ def reshape_masks(masks, x):
     return [m.reshape(NF, m.shape[1], hh, ww) for m, (hh, ww) in zip(masks, shapes)]
 
 
-def pinned_oracle_grads(state_dict, x, labels, draws, masks, sync_group=None):
+def pinned_oracle_grads(state_dict, x, labels, draws, masks, sync_group=None, bf16=False, dtype=torch.float64):
     """float64 oracle forward/backward of one train step with the ReLU decisions of another forward (masks from
     hip_relu_masks): the exact gradient of that forward's piecewise-linear branch, free of kink flips.  Returns
     (grads {name: float64 tensor or None}, losses {name: float64}, the oracle's result dict incl. "bufs" and
-    "record" -- the float64 BatchNorm outputs "z{l}" in front of each pinned ReLU, for check_mask_flips)."""
+    "record" -- the float64 BatchNorm outputs "z{l}" in front of each pinned ReLU, for check_mask_flips).
+    bf16: the backbone as the device computes it in bf16 mode (cad_oracle.backbone_forward_bf16).  dtype: the
+    oracle's arithmetic (float64; float32 gives a second, independent restatement at fp32 accumulation)."""
     from oracle import cad_oracle as co
-    params = {k: v.detach().double().clone() for k, v in state_dict.items()
+    params = {k: v.detach().to(dtype).clone() for k, v in state_dict.items()
               if "running" not in k and "num_batches" not in k}
-    bufs = {k: v.detach().double().clone() for k, v in state_dict.items() if "running" in k}
-    xd = x.double()
+    bufs = {k: v.detach().to(dtype).clone() for k, v in state_dict.items() if "running" in k}
+    xd = x.to(dtype)
     rm = reshape_masks(masks, xd)
     record = {}
+    kw = dict(bf16=True) if bf16 else {}
     res = co.cad_train_step(params, bufs, {}, xd, labels, draws, relu_masks=rm, sync_group=sync_group,
-                            record=record)
+                            record=record, **kw)
     res["bufs"] = bufs  # running stats after the step's forward
     res["record"] = record
     return res["grads"], res["losses"], res

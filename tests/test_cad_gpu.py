@@ -382,13 +382,74 @@ def test_module_api_train_mode_unfrozen_227():
     print(f"worst per-tensor relative L2 vs the mask-pinned oracle: {worst:.3g}")
 
 
-# per-tensor tolerance of the bf16 mode (conv_bf16 + act_bf16) against the exact (float64) gradient of the branch the
-# device took.  bf16 operands and stored activations carry a relative rounding of up to 2^-8 = 3.9e-3 per element, but
-# the gradients of this workload at init are cancellation-dominated: the 8 clips of random frames have nearly identical
-# features and the labels are balanced (i mod 2), so every gradient is a small difference of large per-clip terms and
-# the per-element rounding is amplified.  The fp32 mode shows the same amplification (2.3e-5 per-tensor error = ~380x
-# its unit roundoff 6e-8); bf16 measures 0.02-0.09 (~20x 2^-8) on MI355X for every backbone / classifier tensor.
-BF16_GRAD_REL_L2 = 0.15
+# bf16 mode (conv_bf16 + act_bf16) is compared with the float64 oracle restating the device's bf16 rounding points
+# (oracle.cad_oracle.backbone_forward_bf16: bf16 operands, bf16-stored conv outputs y, dA and dY), pinned to the
+# device's ReLU decisions.  What a correct bf16 implementation may differ from that restatement by is not a constant:
+# a stored bf16 value flips by one ulp (2^-8 relative) wherever a tiny difference upstream moves it across a rounding
+# boundary, i.e. with probability ~ delta / ulp, so a pre-rounding difference delta becomes sqrt(delta * 2^-8) after
+# the next storage point and the 16 storage points of the step (8 forward, 8 backward) cascade: at 128^2, B=2, T=8 a
+# float32 run of the same restatement drifts from the float64 one from 1e-4 of the layer-0 outputs to 3 % of every
+# backbone gradient.  The tolerance is therefore derived in the test from an independent second
+# implementation of the same semantics -- the restatement run in float32 (the device's accumulation precision) on the
+# same pinned branch: the device must lie within BF16_SPREAD x that implementation's own distance to the float64
+# restatement (+ a floor at the float32 level).  The same for the scores, the loss and the ReLU decisions (flip count
+# and worst |z| at a flip, against the float32 restatement's own decisions).
+BF16_SPREAD = 2.0
+
+
+def _bf16_vs_restatement(o, eng, masks, gr, x, y, sd, draws):
+    """config-4 bf16 parity: the device (o, eng, gr) vs the float64 bf16 restatement, with the float32 restatement as
+    the yardstick (see BF16_SPREAD)."""
+    ref_g, ref_l, ref = pinned_oracle_grads(sd, x, y, draws, masks, bf16=True)
+    alt_g, alt_l, alt = pinned_oracle_grads(sd, x, y, draws, masks, bf16=True, dtype=torch.float32)
+    ex_g, _, _ = pinned_oracle_grads(sd, x, y, draws, masks)  # the exact step, for the record only
+
+    def within(dev, yard, floor, what):
+        assert dev <= BF16_SPREAD * yard + floor, (f"{what}: device {dev:.3g} vs float32 restatement {yard:.3g} "
+                                                   f"(bound {BF16_SPREAD} x + {floor:g})")
+
+    for key, out_key, floor in (("final", "anomaly_scores", 1e-6), ("probs", "direct_predictions", 1e-6)):
+        r64 = ref["out"][out_key].detach().double().numpy()
+        dev = float(np.abs(o[key].cpu().numpy() - r64).max())
+        yard = float(np.abs(alt["out"][out_key].detach().double().numpy() - r64).max())
+        print(f"  bf16 {key}: device {dev:.3g}, float32 restatement {yard:.3g}")
+        within(dev, yard, floor, key)
+    dev = abs(float(o["losses"][4]) - float(ref_l["total"]))
+    yard = abs(float(alt_l["total"]) - float(ref_l["total"]))
+    within(dev, yard, 1e-6 * abs(float(ref_l["total"])), "total loss")
+    # ReLU decisions: the device's (pinned everywhere) against the float64 restatement's own signs, per layer, beside
+    # the float32 restatement's own signs
+    for l in range(8):
+        z64, z32 = ref["record"][f"z{l}"], alt["record"][f"z{l}"].double()
+        m = masks[l].reshape(z64.shape).to(torch.bool)
+        fd, fa = (z64 > 0) != m, (z64 > 0) != (z32 > 0)
+        wd = float(z64.abs()[fd].max()) if bool(fd.any()) else 0.0
+        wa = float(z64.abs()[fa].max()) if bool(fa.any()) else 0.0
+        rms = float(z64.pow(2).mean().sqrt())
+        print(f"  bf16 layer {l} ReLU flips: device {int(fd.sum())} (worst |z| {wd / rms:.3g} rms), float32 "
+              f"restatement {int(fa.sum())} ({wa / rms:.3g} rms)")
+        # (floors: a decision within one bf16 ulp of the layer's scale from zero may flip on a single rounding flip)
+        near = int((z64.abs() <= 2.0 ** -8 * rms).sum())
+        assert int(fd.sum()) <= BF16_SPREAD * int(fa.sum()) + near, l
+        assert wd <= BF16_SPREAD * wa + 2.0 ** -8 * rms, l
+    worst = 0.0
+    for i, n in enumerate(eng.slot_names):
+        r = ref_g.get(n)
+        mine = gr[eng.slot_offset[i]:eng.slot_offset[i] + eng.slot_numel[i]].astype(np.float64)
+        if r is None:
+            assert np.abs(mine).max() == 0.0, n
+            continue
+        if is_pre_bn_bias(n):
+            assert np.abs(mine).max() < 1e-4, n
+            continue
+        r = r.detach().double().numpy()
+        dev, yard = rel_l2(mine, r), rel_l2(alt_g[n].detach().double().numpy(), r)
+        exact = rel_l2(mine, ex_g[n].detach().double().numpy())
+        worst = max(worst, dev / max(yard, 1e-12))
+        if n.startswith("backbone.layer"):
+            print(f"  bf16 {n}: device {dev:.3g}, float32 restatement {yard:.3g} (device vs the exact step {exact:.3g})")
+        within(dev, yard, 1e-5, n)
+    print(f"config 4 per rank, bf16: worst device / float32-restatement distance ratio {worst:.3g}")
 
 
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
@@ -397,10 +458,9 @@ def test_config4_shape_per_rank(dt):
     fp32 mode: scores and loss within the north-star 1e-4 of the CPU oracle, every gradient tensor within relative
     L2 1e-4 of the mask-pinned float64 oracle.  bf16 mode (conv_bf16: the 3x3 convs and the frozen stem's conv1 on
     bf16 operands, fp32 accumulation; the backbone activations -- pooled stem map, conv outputs, their gradients --
-    stored as bf16 (option act_bf16, on by default); BN statistics, weights, grads and the heads fp32): scores and
-    probabilities (bounded in [0, 1]) within 2e-2 absolute, the total loss within 2e-2 relative, and every
-    gradient tensor within relative L2 BF16_GRAD_REL_L2 of the mask-pinned float64 oracle (tolerance stated for
-    bf16 compute: unit roundoff 2^-8)."""
+    stored as bf16 (option act_bf16, on by default); BN statistics, weights, grads and the heads fp32): against the
+    float64 restatement of those bf16 rounding points, within BF16_SPREAD x the distance of an independent float32
+    restatement (scores, loss, every gradient tensor, ReLU decisions)."""
     B, T, H, W = 8, 32, 256, 256
     case = dict(name="cfg4", B=B, T=T, H=H, W=W, seed=9, step=1, forced=None)
     x = co.synth_clips(9, 1, 0, B, T, H, W)
@@ -415,20 +475,21 @@ def test_config4_shape_per_rank(dt):
     from tests.golden_util import read_debug_len
     assert read_debug_len(eng._last[0], "act_bf16") == (0 if fp32 else 1)
     masks = hip_relu_masks(eng, B * T)
-    ref_grads, ref_losses, res = pinned_oracle_grads(make_cad_model(case).state_dict(), x, y,
-                                                     co.CadDraws.make(9, 1, 0, B, T), masks)
-    # (bf16: y is stored rounded to 8 bits and the rounding compounds over the layers: 64 units of 2^-8 of the
-    # channel's RMS; measured worst |z| at a flip 1.03 x the 32-unit bound on MI355X)
-    flips = (check_mask_flips(masks, res["record"], x) if fp32 else
-             check_mask_flips(masks, res["record"], x, ulps=64, unit=2.0 ** -8, accum=False))
-    print(f"config 4 per rank, {dt}: ReLU decisions that differ from the float64 forward (count, worst |z|/bound) "
+    draws = co.CadDraws.make(9, 1, 0, B, T)
+    sd = make_cad_model(case).state_dict()
+    if not fp32:
+        from tests.golden_util import reshape_masks
+        _bf16_vs_restatement(o, eng, reshape_masks(masks, x.double()), gr, x, y, sd, draws)
+        return
+    ref_grads, ref_losses, res = pinned_oracle_grads(sd, x, y, draws, masks)
+    flips = check_mask_flips(masks, res["record"], x)
+    print(f"config 4 per rank, fp32: ReLU decisions that differ from the float64 forward (count, worst |z|/bound) "
           f"{flips}")
-    atol = 1e-5 if fp32 else 2e-2
     np.testing.assert_allclose(o["final"].cpu().numpy(), res["out"]["anomaly_scores"].detach().numpy(),
-                               rtol=1e-4 if fp32 else 0, atol=atol)
+                               rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(o["probs"].cpu().numpy(), res["out"]["direct_predictions"].detach().numpy(),
-                               rtol=1e-4 if fp32 else 0, atol=atol)
-    assert float(o["losses"][4]) == pytest.approx(float(ref_losses["total"]), rel=1e-4 if fp32 else 2e-2)
+                               rtol=1e-4, atol=1e-5)
+    assert float(o["losses"][4]) == pytest.approx(float(ref_losses["total"]), rel=1e-4)
     errs = {}
     for i, n in enumerate(eng.slot_names):
         ref = ref_grads.get(n)
@@ -437,12 +498,12 @@ def test_config4_shape_per_rank(dt):
             assert np.abs(mine).max() == 0.0, n
             continue
         if is_pre_bn_bias(n):
-            assert np.abs(mine).max() < (1e-6 if fp32 else 1e-4), n
+            assert np.abs(mine).max() < 1e-6, n
             continue
         errs[n] = rel_l2(mine, ref.detach().numpy())
     for n, e in sorted(errs.items(), key=lambda kv: -kv[1])[:12]:
         print(f"  {dt} {n}: {e:.3g}")
-    bad = {n: e for n, e in errs.items() if e > (1e-4 if fp32 else BF16_GRAD_REL_L2)}
+    bad = {n: e for n, e in errs.items() if e > 1e-4}
     assert not bad, f"relative L2 errors above tolerance ({dt}): {bad}"
     print(f"config 4 per rank, {dt}: worst per-tensor relative L2 vs the mask-pinned oracle {max(errs.values()):.3g}")
 

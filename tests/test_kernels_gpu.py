@@ -194,9 +194,13 @@ WGRAD_CASES = [(2, 32, 32, 19, 17, 1), (32, 256, 256, 8, 8, 1), (32, 128, 256, 1
 
 
 def _wgrad_path(nat, patch):
-    """3: split-bf16 transposed-read kernel for both strides (default, conv_x3w.hip), 4: the
-    older split-bf16 kernels (conv_x3.hip), 1: f32 LDS-patch kernel for stride-1 layers, 2: f32 LDS-patch kernel for all strides, 0:
+    """3: split-bf16 transposed-read kernel for both strides (default, conv_x3w.hip), 5: split-bf16 on pre-split
+    operand planes staged by LDS-DMA (conv_x3d.hip; its supported layers), 4: the older split-bf16 kernels
+    (conv_x3.hip), 1: f32 LDS-patch kernel for stride-1 layers, 2: f32 LDS-patch kernel for all strides, 0:
     implicit-GEMM path."""
+    nat.lib().vad_set_tuning(b"conv_wgrad_dma", 1 if patch == 5 else 0)
+    if patch == 5:
+        patch = 3
     split = patch in (3, 4)
     nat.lib().vad_set_tuning(b"conv_wgrad_patch", 1 if split else patch)
     nat.lib().vad_set_tuning(b"conv_wgrad_split", 1 if split else 0)
@@ -204,7 +208,7 @@ def _wgrad_path(nat, patch):
     nat.lib().vad_set_tuning(b"conv_wgrad_tr", 1 if patch == 3 else 0)
 
 
-@pytest.mark.parametrize("patch", [3, 4, 1, 0, 2])
+@pytest.mark.parametrize("patch", [3, 5, 4, 1, 0, 2])
 @pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", WGRAD_CASES)
 def test_conv3x3_wgrad(NF, Ci, Co, IH, IW, s, patch):
     nat = _lib()
@@ -235,7 +239,8 @@ def test_conv3x3_wgrad(NF, Ci, Co, IH, IW, s, patch):
                                               (8, 32, 64, 57, 57, 2), (6, 64, 128, 29, 29, 2),
                                               (8, 128, 256, 15, 15, 2)])
 def test_conv3x3_wgrad_split_accuracy_matches_f32(NF, Ci, Co, IH, IW, s):
-    """Split-bf16 weight gradients (transposed-read kernel 3, older kernels 4) against an fp64 reference: worst error
+    """Split-bf16 weight gradients (transposed-read kernel 3, LDS-DMA planes kernel 5, older kernels 4) against an fp64
+    reference: worst error
     relative to sum_p |dy||x| of each weight within 2x that of the exact-f32 MFMA kernel (a plain bf16 product would
     sit near 4e-3)."""
     nat = _lib()
@@ -250,7 +255,7 @@ def test_conv3x3_wgrad_split_accuracy_matches_f32(NF, Ci, Co, IH, IW, s):
     dyh = dy.permute(0, 2, 3, 1).contiguous().to(d)
     part = torch.empty(1 << 24, device=d)
     errs = {}
-    for patch in ((1, 3, 4) if s == 1 else (2, 3, 4)):
+    for patch in ((1, 3, 4, 5) if s == 1 else (2, 3, 4, 5)):
         _wgrad_path(nat, patch)
         dW = torch.empty(Co, Ci, 3, 3, device=d)
         nat.check(nat.lib().vad_conv3x3_wgrad(xh.data_ptr(), dyh.data_ptr(), NF, Ci, IH, IW, Co, s, dW.data_ptr(),
@@ -258,7 +263,7 @@ def test_conv3x3_wgrad_split_accuracy_matches_f32(NF, Ci, Co, IH, IW, s):
         torch.cuda.synchronize()
         errs[patch] = float(((dW.cpu().double() - ref).abs() / mag).max())
     _wgrad_path(nat, 3)
-    for k in (3, 4):
+    for k in (3, 4, 5):
         assert errs[k] < 1e-6, errs
         assert errs[k] <= 2.0 * errs[1 if s == 1 else 2] + 1e-8, errs
 
