@@ -18,6 +18,7 @@ extern int g_x3_pipe;  // knob "conv_split_pipe"
 extern int g_x3_s2big;  // knob "conv_split_s2big"
 extern int g_cad_dir_affine;  // knob "cad_dir_affine": the direct classifier's loss-mode backward precomputed in the forward
 extern int g_cad_stem_early;
+extern int g_cad_dy_planes, g_cad_x_planes;  // knobs "cad_dy_planes", "cad_x_planes" (operand planes of x3_wgrad_dma)
 extern int g_cad_prep_stream, g_cad_wgrad_stream, g_cad_det_gate, g_cad_last_wgrad_main, g_cad_event_sysfence,
     g_cad_dy_per_layer, g_cad_l0_slab, g_cad_stream_prio;  // knobs "cad_prep_stream", "cad_wgrad_stream" (A/B)
 extern int g_stem_fused;  // knob "stem_fused" (default 1)
@@ -47,6 +48,9 @@ int bn_bwd_finalize(const float* partials, int P, int C, double count, const flo
 // bias_partials may be null (the conv bias grad then comes from bn_bwd_finalize's dbias)
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
                  int* nparts, hipStream_t st);
+// the same writing dY (nullable) and its pre-split bf16 planes [3][M][C] (x3_wgrad_dma's operand; fp32 activations)
+int bn_bwd_apply_planes(const float* dA, const float* y, const float* stats, int M, int C, float* dY, __bf16* planes,
+                        hipStream_t st);
 // the same in place (dA == dY; fp32 activations: the training stem's backward)
 int bn_bwd_apply_inplace(float* dAY, const float* y, const float* stats, int M, int C, hipStream_t st);
 int bn_rows_parts(int M, int C);
