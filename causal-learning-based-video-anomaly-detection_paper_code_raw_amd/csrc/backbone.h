@@ -166,6 +166,12 @@ extern int g_wgrad_dma, g_wgrad_dma_blocks, g_wgrad_dma_nb;  // knobs "conv_wgra
 bool x3_wgrad_dma_supported(const Conv3Layer& L);
 int x3_wgrad_dma(const Conv3Layer& L, const __bf16* dy_planes, const __bf16* x_planes, float* slab, int* nsplit,
                  int64_t partial_cap, int target_blocks, hipStream_t st);
+// stride-2 input gradient on dY planes + the pre-split Wd image by LDS-DMA (conv_x3d.hip; conv3x3_dgrad_s2x3_kernel's
+// arithmetic, bit for bit); f: the fused BN-backward reduce of the layer below (as conv3_dgrad)
+extern int g_dgrad_s2_dma, g_dgrad_s2_dma_nb, g_dgrad_s2_dma_blocks;  // knobs "conv_dgrad_s2_dma", "..._nb", "..._blocks"
+bool dgrad_s2_dma_supported(const Conv3Layer& L);
+int dgrad_s2_dma(const Conv3Layer& L, const __bf16* dy_planes, const __bf16* w3, float* dX, hipStream_t st,
+                 const BnBwdFuse* f);
 // fp32 [M][C] -> bf16 planes [3][M][C] (hi, mid, lo), with BN + ReLU (stats = the producer's BN state) when given
 int planes_split(const float* src, const float* stats, int64_t M, int C, __bf16* dst, hipStream_t st);
 bool conv3_wgrad_patch_supported(const Conv3Layer& L);

@@ -1177,6 +1177,9 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_bn_fused") g_wgrad_bn_fused = value;
   else if (k == "conv_wgrad_dma") g_wgrad_dma = value;
   else if (k == "cad_dy_planes") g_cad_dy_planes = value;
+  else if (k == "conv_dgrad_s2_dma") g_dgrad_s2_dma = value;
+  else if (k == "conv_dgrad_s2_dma_nb") g_dgrad_s2_dma_nb = value;
+  else if (k == "conv_dgrad_s2_dma_blocks") g_dgrad_s2_dma_blocks = value;
   else if (k == "cad_x_planes") g_cad_x_planes = value;
   else if (k == "conv_wgrad_dma_blocks") g_wgrad_dma_blocks = value;
   else if (k == "conv_wgrad_dma_nb") g_wgrad_dma_nb = value;

@@ -1116,7 +1116,10 @@ struct CadPlanImpl {
       if (l > 0) {
         // its epilogue also reduces layer l-1's BN backward (dZ = dA masked by layer l-1's ReLU, dZ * xhat)
         const BnBwdFuse fu{y[l - 1], stats[l], parts, parts_floats, &fused_np};
-        TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st, &fu, w3[l]));
+        if (dypl && w3[l] && dgrad_s2_dma_supported(L[l]))  // (stride 2: dY's planes by LDS-DMA, knob conv_dgrad_s2_dma)
+          TIMED(L_("conv_dgrad", l), dgrad_s2_dma(L[l], pl_dy[l], w3[l], dA, st, &fu));
+        else
+          TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st, &fu, w3[l]));
       }
       if (l == debug_stop_layer) break;
     }

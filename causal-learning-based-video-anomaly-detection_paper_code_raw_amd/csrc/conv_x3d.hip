@@ -27,6 +27,7 @@ namespace vad {
 namespace {
 
 typedef __bf16 bfv8d __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8d __attribute__((ext_vector_type(8)));
 typedef __bf16 bfv4d __attribute__((ext_vector_type(4)));
 typedef short s16x4d __attribute__((ext_vector_type(4)));
 
@@ -289,6 +290,254 @@ __global__ __launch_bounds__(512, 2) void x3_wgrad_dma_kernel(const DwArgs p) {
       for (int r = 0; r < 4; ++r)
         out[(int64_t)(cob + 16 * v + r) * 9 * p.Ci + (T0 + i) * p.Ci + cic] = acc[i][v][r];
   }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Stride-2 input gradient (the transpose of cad:128-136's stride-2 nn.Conv2d) on pre-split dY planes and the pre-split
+// Wd image, staged by LDS-DMA.  The arithmetic is conv3x3_dgrad_s2x3_kernel's (conv_x3.hip): the four parity classes
+// (ph, pw) of a 16x16 dX tile read one 9x9 dY patch, class (ph, pw) taking the kernel rows kh with ph + 1 - kh even at
+// dY row offset (ph + 1 - kh) / 2 (likewise columns), six products per K step in the same order over the same 16-channel
+// chunks -- so the result is that kernel's, bit for bit.  What changes is the staging: a 512-thread block owns TWO
+// class tiles (waves 0-3 and 4-7) that share the staged weight slice, the copies are DMA'd into NB LDS buffers (no
+// VGPR staging, no split), and a block walks a contiguous run of tile pairs x channel chunks as one pipelined stage
+// sequence (the copies of stage s + NB - 1 issued right after the barrier of stage s).
+struct DgS2Args {
+  const __bf16* dy;  // planes [3][NF DH DW][C] (dY of the conv: C = its Co)
+  const __bf16* w3;  // pre-split Wd [N][9][C / 16][3][16] (N = the conv's Ci)
+  float* out;        // dX [NF][OH][OW][N]
+  float* partials;   // fused BN-backward reduce of the layer below: column-major [2N][gridDim.x] (nullable)
+  const float* bny;  //   its raw output y [NF][OH][OW][N]
+  const float* bnst; //   its BN state (mean | invstd | scale | shift)
+  int dy_ps;
+  int NF, DH, DW, C, OH, OW, N;
+  int tiles_h, tiles_w, ntiles, npairs, ppb;
+};
+
+template <int NB>
+__global__ __launch_bounds__(512, 2) void dgrad_s2_dma_kernel(const DgS2Args p) {
+  constexpr int PC = 16, NC = 32, RP = 3 * PC + 8, WP = 9 * 3 * PC + 8;  // odd 16-B row pitches (7 and 55 chunks)
+  constexpr int PCH = 81 * RP / 8, WCH = NC * WP / 8;                     // 16-B chunks: one patch, the weight slice
+  constexpr int NCHK = 2 * PCH + WCH, NI = (NCHK + 63) / 64, DW = (NI + 7) / 8, BUF = NI * 64 * 8;
+  static_assert(NB * BUF * 2 <= 163840 && DW >= 2, "LDS budget");
+  __shared__ __attribute__((aligned(1024))) __bf16 sm[NB * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, j = lane & 31;
+  const int n0 = blockIdx.y * NC;
+  const int nch = p.C / PC;
+  const int pb = blockIdx.x * p.ppb, pe = min(p.npairs, pb + p.ppb);
+  const int stages = (pe - pb) * nch;
+  const int tiles_per_img = p.tiles_h * p.tiles_w;
+  const __bf16* const zp = g_zero_page;
+
+  // copy u of this wave = DMA instruction i = wave + 8u (past the last: its own previous one again); this lane's
+  // chunk c = 64 i + lane: kind 0 / 1 patch of tile A / B (geo = dY row, column in the patch), 2 weights, 3 padding
+  int kind[DW], geo[DW], so[DW];
+#pragma unroll
+  for (int u = 0; u < DW; ++u) {
+    int i = wave + 8 * u;
+    if (i >= NI) i -= 8;
+    const int c = 64 * i + lane;
+    if (c < 2 * PCH) {
+      const int cc = c % PCH, row = cc / 7, k = cc % 7;
+      kind[u] = k < 6 ? c / PCH : 3;
+      geo[u] = ((row / 9) << 8) | (row % 9);
+      so[u] = (k >> 1) * p.dy_ps + (k & 1) * 8;
+    } else if (c < NCHK) {
+      const int cc = c - 2 * PCH, n = cc / 55, k = cc % 55;
+      kind[u] = (k < 54 && n0 + n < p.N) ? 2 : 3;
+      geo[u] = 0;
+      so[u] = ((n0 + n) * 9 + k / 6) * (p.C / 16) * 48 + ((k % 6) >> 1) * 16 + (k & 1) * 8;
+    } else {
+      kind[u] = 3;
+      geo[u] = 0;
+      so[u] = 0;
+    }
+  }
+  auto tile_at = [&](int t, int& img, int& i0, int& j0) {  // class-grid origin = dY patch origin
+    img = t / tiles_per_img;
+    const int tr = t % tiles_per_img;
+    i0 = (tr / p.tiles_w) * 8;
+    j0 = (tr % p.tiles_w) * 8;
+  };
+  auto issue = [&](int s, int buf) {
+    const int pair = pb + s / nch, c0 = (s % nch) * PC;
+    int imgA, i0A, j0A, imgB, i0B, j0B;
+    tile_at(2 * pair, imgA, i0A, j0A);
+    tile_at(2 * pair + 1, imgB, i0B, j0B);
+    const bool okB = 2 * pair + 1 < p.ntiles;
+#pragma unroll
+    for (int u = 0; u < DW; ++u) {
+      const int k = kind[u], gy = geo[u] >> 8, gx = geo[u] & 255;
+      const __bf16* gp = zp;
+      if (k == 2) {
+        gp = p.w3 + so[u] + (c0 / 16) * 48;
+      } else if (k < 2) {
+        const int img = k ? imgB : imgA, y = (k ? i0B : i0A) + gy, x = (k ? j0B : j0A) + gx;
+        if ((k == 0 || okB) && y < p.DH && x < p.DW) gp = p.dy + so[u] + ((img * p.DH + y) * p.DW + x) * p.C + c0;
+      }
+      dma16(gp, sm + buf * BUF + (wave + 8 * u - (wave + 8 * u >= NI ? 8 : 0)) * 512);
+    }
+  };
+
+  // this wave: tile (wave >> 2), class-tile rows 4 g .. 4 g + 3, classes (1,1)+(0,0) or (0,1)+(1,0)
+  const int tsel = wave >> 2, g = wave & 1, csel = (wave >> 1) & 1;
+  const int arow = (4 * g + j / 8) * 9 + j % 8;
+  f32x16 acc0, acc1;
+  float s1 = 0.f, s2 = 0.f;
+  const bool bnb = p.bny != nullptr;
+  float bmean = 0.f, binv = 0.f, bsc = 0.f, bsh = 0.f;
+  if (bnb) {
+    const int col = min(n0 + j, p.N - 1);
+    bmean = p.bnst[col];
+    binv = p.bnst[p.N + col];
+    bsc = p.bnst[2 * p.N + col];
+    bsh = p.bnst[3 * p.N + col];
+  }
+  auto cls = [&](f32x16& acc, const __bf16* abase, const __bf16* bbase, int cph, int cpw) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      if (a == 1 && !cph) break;
+      const int kh = cph ? (a == 0 ? 0 : 2) : 1, dh = (cph && a == 0) ? 1 : 0;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        if (b == 1 && !cpw) break;
+        const int kw = cpw ? (b == 0 ? 0 : 2) : 1, dw = (cpw && b == 0) ? 1 : 0;
+        const __bf16* ap = abase + (dh * 9 + dw) * RP;
+        const __bf16* bp = bbase + (kh * 3 + kw) * 3 * PC;
+        bf16x8d av[3], bv[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          av[q] = *reinterpret_cast<const bf16x8d*>(ap + q * PC);
+          bv[q] = *reinterpret_cast<const bf16x8d*>(bp + q * PC);
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[0], acc, 0, 0, 0);
+      }
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < NB - 1; ++s)
+    if (s < stages) issue(s, s);
+  for (int s = 0; s < stages; ++s) {
+    if (NB == 3 && s + 1 < stages) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (s + NB - 1 < stages) issue(s + NB - 1, (s + NB - 1) % NB);
+    const int c = s % nch, pair = pb + s / nch;
+    if (c == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+    }
+    const __bf16* const bb = sm + (s % NB) * BUF;
+    const __bf16* abase = bb + tsel * 81 * RP + arow * RP + 8 * h;
+    const __bf16* bbase = bb + 2 * 81 * RP + j * WP + 8 * h;
+    if (csel == 0) {
+      cls(acc0, abase, bbase, 1, 1);
+      cls(acc1, abase, bbase, 0, 0);
+    } else {
+      cls(acc0, abase, bbase, 0, 1);
+      cls(acc1, abase, bbase, 1, 0);
+    }
+    if (c == nch - 1) {  // this tile's dX (two parity classes) and the fused BN-backward sums
+      const int t = 2 * pair + tsel;
+      if (t < p.ntiles) {
+        int img, i0, j0;
+        tile_at(t, img, i0, j0);
+        const int col = n0 + j;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int ph = q ? (csel ? 1 : 0) : (csel ? 0 : 1), pw = q ? 0 : 1;
+          float yb[16];
+          if (bnb) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int pm = (r & 3) + 8 * (r >> 2) + 4 * h;
+              const int yy = 2 * (i0 + 4 * g + pm / 8) + ph, xx = 2 * (j0 + pm % 8) + pw;
+              const bool ok = yy < p.OH && xx < p.OW;
+              yb[r] = p.bny[(ok ? ((int64_t)(img * p.OH + yy) * p.OW + xx) * p.N : 0) + min(col, p.N - 1)];
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int pm = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int yy = 2 * (i0 + 4 * g + pm / 8) + ph, xx = 2 * (j0 + pm % 8) + pw;
+            if (col >= p.N || yy >= p.OH || xx >= p.OW) continue;
+            const float v = q ? acc1[r] : acc0[r];
+            p.out[((int64_t)(img * p.OH + yy) * p.OW + xx) * p.N + col] = v;
+            if (bnb) {
+              const float dz = fmaf(yb[r], bsc, bsh) > 0.f ? v : 0.f;
+              s1 += dz;
+              s2 = fmaf(dz, (yb[r] - bmean) * binv, s2);
+            }
+          }
+        }
+      }
+    }
+  }
+  if (bnb && p.partials) {  // per-block sums, fixed order: lane halves, then the 8 waves
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float* red = reinterpret_cast<float*>(sm);  // [8 waves][2][NC]
+    const float a1 = s1 + __shfl_xor(s1, 32, 64), a2 = s2 + __shfl_xor(s2, 32, 64);
+    if (lane < 32) {
+      red[(wave * 2 + 0) * NC + lane] = a1;
+      red[(wave * 2 + 1) * NC + lane] = a2;
+    }
+    __syncthreads();
+    if (tid < 2 * NC) {
+      const int which = tid / NC, c = tid % NC;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += red[(2 * w + which) * NC + c];
+      if (n0 + c < p.N) p.partials[(int64_t)(which * p.N + n0 + c) * gridDim.x + blockIdx.x] = v;
+    }
+  }
+}
+
+int g_dgrad_s2_dma = 0;  // knob "conv_dgrad_s2_dma": stride-2 input gradients on dY planes + the Wd planes by LDS-DMA
+int g_dgrad_s2_dma_nb = 3;       // knob "conv_dgrad_s2_dma_nb": LDS buffers (2 | 3)
+int g_dgrad_s2_dma_blocks = 256;  // knob "conv_dgrad_s2_dma_blocks": target grid
+
+bool dgrad_s2_dma_supported(const Conv3Layer& L) {
+  const int64_t lim = ((int64_t)1 << 31) / 3 - 64;
+  return g_dgrad_s2_dma && !g_conv_bf16 && !g_act_bf16 && L.stride == 2 && L.Co % 16 == 0 && L.Ci % 32 == 0 &&
+         L.OH == (L.IH - 1) / 2 + 1 && L.OW == (L.IW - 1) / 2 + 1 && (int64_t)L.NF * L.OH * L.OW * L.Co < lim &&
+         (int64_t)L.NF * L.IH * L.IW * L.Ci < lim;
+}
+
+int dgrad_s2_dma(const Conv3Layer& L, const __bf16* dy_planes, const __bf16* w3, float* dX, hipStream_t st,
+                 const BnBwdFuse* f) {
+  VAD_CHECK(dgrad_s2_dma_supported(L) && w3 != nullptr, "dgrad_s2_dma: unsupported layer or no pre-split Wd image");
+  DgS2Args a{};
+  a.dy = dy_planes;
+  a.w3 = w3;
+  a.out = dX;
+  a.dy_ps = (int)((int64_t)L.NF * L.OH * L.OW * L.Co);
+  a.NF = L.NF; a.DH = L.OH; a.DW = L.OW; a.C = L.Co; a.OH = L.IH; a.OW = L.IW; a.N = L.Ci;
+  a.tiles_h = (int)cdiv((L.IH + 1) / 2, 8);
+  a.tiles_w = (int)cdiv((L.IW + 1) / 2, 8);
+  a.ntiles = L.NF * a.tiles_h * a.tiles_w;
+  a.npairs = (int)cdiv(a.ntiles, 2);
+  const int nct = L.Ci / 32;
+  a.ppb = (int)std::max<int64_t>(1, cdiv((int64_t)a.npairs * nct, g_dgrad_s2_dma_blocks));
+  const int gx = (int)cdiv(a.npairs, a.ppb);
+  if (f && f->cap < 2ll * L.Ci * gx) f = nullptr;  // (partial buffer too small: the caller runs the separate pass)
+  if (f) {
+    a.bny = f->y;
+    a.bnst = f->stats;
+    a.partials = f->parts;
+    *f->nparts = gx;
+  }
+  const dim3 grid((unsigned)gx, (unsigned)nct);
+  if (g_dgrad_s2_dma_nb == 2) VAD_KLAUNCH((dgrad_s2_dma_kernel<2>), grid, dim3(512), 0, st, a);
+  else VAD_KLAUNCH((dgrad_s2_dma_kernel<3>), grid, dim3(512), 0, st, a);
+  VAD_LAUNCH_CHECK();
+  return 0;
 }
 
 int g_wgrad_dma = 0;           // knob "conv_wgrad_dma": fp32 weight gradients on pre-split planes (x3_wgrad_dma_kernel)

@@ -391,3 +391,38 @@ def test_conv3x3_bf16_native_matches_rounded_fp64(NF, Ci, Co, IH, IW, s):
     finally:
         lib.vad_set_tuning(b"act_bf16", 0)
         lib.vad_set_tuning(b"conv_bf16", 0)
+
+
+@pytest.mark.parametrize("NF,Ci,Co,IH,IW", [(2, 32, 64, 57, 57), (3, 64, 128, 29, 29), (4, 128, 256, 15, 15),
+                                            (2, 64, 128, 31, 18), (3, 32, 64, 20, 9)])
+def test_conv3x3_dgrad_s2_dma_bit_identical(NF, Ci, Co, IH, IW):
+    """Stride-2 input gradient on pre-split dY planes + the pre-split Wd image staged by LDS-DMA (knob
+    conv_dgrad_s2_dma, two class tiles per block, ragged tile pairs included) equals the split-bf16 parity-class kernel
+    bit for bit (same products in the same order), and both match the fp64 reference."""
+    nat = _lib()
+    g = torch.Generator().manual_seed(29 + Ci + IH)
+    w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
+    OH, OW = (IH - 1) // 2 + 1, (IW - 1) // 2 + 1
+    dy = torch.randn(NF, Co, OH, OW, generator=g)
+    ref = torch.nn.grad.conv2d_input((NF, Ci, IH, IW), w.double(), dy.double(), stride=2, padding=1)
+    d = torch.device("cuda")
+    dyh = dy.permute(0, 2, 3, 1).contiguous().to(d)
+    wdev = w.contiguous().to(d)
+    wf = torch.empty(9 * Ci * Co, device=d)
+    wd = torch.empty(9 * Ci * Co, device=d)
+    st = nat.stream_of(d)
+    nat.lib().vad_set_tuning(b"conv_dgrad_s2_x3", 1)
+    dx0 = torch.empty(NF, IH, IW, Ci, device=d)
+    nat.check(nat.lib().vad_conv3x3_dgrad(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, 2, dx0.data_ptr(),
+                                          wf.data_ptr(), wd.data_ptr(), st))
+    scratch = torch.empty(4 * 9 * Ci * Co + 3 * NF * OH * OW * Co // 2 + 4096, device=d)
+    dx1 = torch.full((NF, IH, IW, Ci), float("nan"), device=d)
+    nat.lib().vad_set_tuning(b"conv_dgrad_s2_dma", 1)
+    try:
+        nat.check(nat.lib().vad_conv3x3_dgrad_s2_planes(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co,
+                                                        dx1.data_ptr(), scratch.data_ptr(), scratch.numel(), st))
+        torch.cuda.synchronize()
+    finally:
+        nat.lib().vad_set_tuning(b"conv_dgrad_s2_dma", 0)
+    np.testing.assert_array_equal(dx1.cpu().numpy(), dx0.cpu().numpy())
+    np.testing.assert_allclose(dx1.cpu().permute(0, 3, 1, 2).double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
