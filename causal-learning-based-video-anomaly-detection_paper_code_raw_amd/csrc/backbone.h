@@ -152,7 +152,7 @@ bool conv3_wgrad_x3_supported(const Conv3Layer& L);
 int conv3_wgrad_x3(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
                    int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);
 // fp32 weight gradients (both strides) on the split-bf16 MFMA with transposed LDS fragment reads (conv_x3w.hip)
-extern int g_wgrad_tr, g_wgrad_tr_blocks;  // knobs "conv_wgrad_tr", "conv_wgrad_tr_blocks"
+extern int g_wgrad_tr, g_wgrad_tr_blocks, g_wgrad_tr_pft;  // knobs "conv_wgrad_tr", "conv_wgrad_tr_blocks", "conv_wgrad_tr_pft"
 bool x3_wgrad_tr_supported(const Conv3Layer& L);
 // bny != nullptr: dY holds dA and the layer's BN backward apply (y = bny, BN state bnst) runs in the staging
 int x3_wgrad_tr(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
@@ -171,6 +171,11 @@ int x3_wgrad_dma(const Conv3Layer& L, const __bf16* dy_planes, const __bf16* x_p
 extern int g_dgrad_s2_dma, g_dgrad_s2_dma_nb, g_dgrad_s2_dma_blocks;  // knobs "conv_dgrad_s2_dma", "..._nb", "..._blocks"
 bool dgrad_s2_dma_supported(const Conv3Layer& L);
 int dgrad_s2_dma(const Conv3Layer& L, const __bf16* dy_planes, const __bf16* w3, float* dX, hipStream_t st,
+                 const BnBwdFuse* f);
+// the same for stride 1 (conv3x3_x3_kernel<FWD = false>'s arithmetic, bit for bit; w3 flipped taps as stored)
+extern int g_dgrad_s1_dma, g_dgrad_s1_dma_blocks;  // knobs "conv_dgrad_s1_dma", "conv_dgrad_s1_dma_blocks"
+bool dgrad_s1_dma_supported(const Conv3Layer& L);
+int dgrad_s1_dma(const Conv3Layer& L, const __bf16* dy_planes, const __bf16* w3, float* dX, hipStream_t st,
                  const BnBwdFuse* f);
 // fp32 [M][C] -> bf16 planes [3][M][C] (hi, mid, lo), with BN + ReLU (stats = the producer's BN state) when given
 int planes_split(const float* src, const float* stats, int64_t M, int C, __bf16* dst, hipStream_t st);

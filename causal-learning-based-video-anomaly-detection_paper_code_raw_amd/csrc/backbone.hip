@@ -1142,6 +1142,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_split_s2") g_wgrad_split_s2 = value;
   else if (k == "conv_wgrad_tr") g_wgrad_tr = value;
   else if (k == "conv_wgrad_tr_blocks") g_wgrad_tr_blocks = value;
+  else if (k == "conv_wgrad_tr_pft") g_wgrad_tr_pft = value;
   else if (k == "conv_wgrad_s2_blocks") g_wgrad_s2_blocks = value;
   else if (k == "stem_fused") g_stem_fused = value;
   else if (k == "conv_dgrad_s2_x3") g_dgrad_s2_x3 = value;
@@ -1178,6 +1179,8 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_wgrad_dma") g_wgrad_dma = value;
   else if (k == "cad_dy_planes") g_cad_dy_planes = value;
   else if (k == "conv_dgrad_s2_dma") g_dgrad_s2_dma = value;
+  else if (k == "conv_dgrad_s1_dma") g_dgrad_s1_dma = value;
+  else if (k == "conv_dgrad_s1_dma_blocks") g_dgrad_s1_dma_blocks = value;
   else if (k == "conv_dgrad_s2_dma_nb") g_dgrad_s2_dma_nb = value;
   else if (k == "conv_dgrad_s2_dma_blocks") g_dgrad_s2_dma_blocks = value;
   else if (k == "cad_x_planes") g_cad_x_planes = value;

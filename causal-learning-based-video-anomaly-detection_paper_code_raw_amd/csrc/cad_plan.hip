@@ -1116,8 +1116,11 @@ struct CadPlanImpl {
       if (l > 0) {
         // its epilogue also reduces layer l-1's BN backward (dZ = dA masked by layer l-1's ReLU, dZ * xhat)
         const BnBwdFuse fu{y[l - 1], stats[l], parts, parts_floats, &fused_np};
-        if (dypl && w3[l] && dgrad_s2_dma_supported(L[l]))  // (stride 2: dY's planes by LDS-DMA, knob conv_dgrad_s2_dma)
+        // dY's planes by LDS-DMA (knobs conv_dgrad_s2_dma, conv_dgrad_s1_dma)
+        if (dypl && w3[l] && dgrad_s2_dma_supported(L[l]))
           TIMED(L_("conv_dgrad", l), dgrad_s2_dma(L[l], pl_dy[l], w3[l], dA, st, &fu));
+        else if (dypl && w3[l] && dgrad_s1_dma_supported(L[l]))
+          TIMED(L_("conv_dgrad", l), dgrad_s1_dma(L[l], pl_dy[l], w3[l], dA, st, &fu));
         else
           TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st, &fu, w3[l]));
       }

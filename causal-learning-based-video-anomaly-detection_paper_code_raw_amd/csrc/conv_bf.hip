@@ -568,13 +568,24 @@ __global__ __launch_bounds__(256, 2) void bfc_wgrad_kernel(const BfwArgs p) {
       const __bf16* ya = ys + ct * YIMG + m0 * 32 + 16 * g16 + 4 * p4;
       const bfv8 a = tr_frag(ya, ya + 4 * 32);
       const int prow = (mi * PH + S * oy) * PW;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
+      auto bfrag = [&](int t) {
         const int kh = t / 3, kw = t % 3;
         const int col = S == 1 ? ox + kw : ((kw & 1) ? PWE + ox + (kw >> 1) : ox + (kw >> 1));
         const __bf16* xb = xs + (prow + kh * PW + col) * 32 + 16 * g16 + 4 * p4;
-        const bfv8 b = tr_frag(xb, xb + 4 * 32);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[t], 0, 0, 0);
+        return tr_frag(xb, xb + 4 * 32);
+      };
+      // tap t + 1's fragment is read before tap t's MFMA (left to itself the compiler waits on each tap's own two
+      // transposed reads right before its MFMA: MFMA busy 0.12)
+      // (two taps ahead where the registers allow: the 144 accumulators leave 8-16 VGPRs)
+      constexpr int PD = (S == 1 && NCO == 1) ? 2 : 1;
+      bfv8 bq[PD + 1];
+#pragma unroll
+      for (int t = 0; t < PD; ++t) bq[t] = bfrag(t);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t + PD < 9) bq[(t + PD) % (PD + 1)] = bfrag(t + PD);
+        __builtin_amdgcn_sched_barrier(0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[t % (PD + 1)], acc[t], 0, 0, 0);
       }
     }
   }

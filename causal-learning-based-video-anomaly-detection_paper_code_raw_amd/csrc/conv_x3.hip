@@ -350,26 +350,40 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv3x3_x3_kernel(const X3Arg
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[nt][r] = 0.f;
     }
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
+    // K steps s = (tap t, 16-channel slice kk); the fragments of step s + 1 are read before step s's MFMAs (one step
+    // of register double-buffering: left to itself the compiler reads each fragment right before its MFMA and the
+    // single accumulation chain waits on every LDS read)
+    auto frag = [&](int sidx, bf16x8 (&a)[NP], bf16x8 (&b)[NT][NP]) {
+      const int t = sidx / (PC / 16), kk = sidx % (PC / 16);
       const int kh = t / 3, kw = t % 3;
       const int col = S == 1 ? px + kw : ((kw & 1) ? PWE + px + (kw >> 1) : px + (kw >> 1));
       const __bf16* ap = patch + (arow0 + kh * PW + col) * RP + 8 * h;
 #pragma unroll
-      for (int kk = 0; kk < PC / 16; ++kk) {
-        bf16x8 a[NP], b[NT][NP];
+      for (int q = 0; q < NP; ++q) a[q] = *reinterpret_cast<const bf16x8*>(ap + q * PC + kk * 16);
 #pragma unroll
-        for (int q = 0; q < NP; ++q) a[q] = *reinterpret_cast<const bf16x8*>(ap + q * PC + kk * 16);
+      for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
+        for (int q = 0; q < NP; ++q)
+          b[nt][q] = *reinterpret_cast<const bf16x8*>(bbase + nt * 32 * WP + wseg + (t * NP + q) * PC + kk * 16);
+    };
+    // (not for 4-wave blocks with two channel tiles: the second fragment set would cost them their second block per CU)
+    constexpr int NSTEP = 9 * (PC / 16);
+    constexpr bool PF = NT == 1 || NW == 8;
+    bf16x8 fa[2][NP], fb[2][NT][NP];
+    if constexpr (PF) frag(0, fa[0], fb[0]);
 #pragma unroll
-          for (int q = 0; q < NP; ++q)
-            b[nt][q] = *reinterpret_cast<const bf16x8*>(bbase + nt * 32 * WP + wseg + (t * NP + q) * PC + kk * 16);
+    for (int sidx = 0; sidx < NSTEP; ++sidx) {
+      const int cur = PF ? sidx & 1 : 0;
+      if constexpr (PF) {
+        if (sidx + 1 < NSTEP) frag(sidx + 1, fa[cur ^ 1], fb[cur ^ 1]);
+        __builtin_amdgcn_sched_barrier(0);  // (keeps those reads ahead of this step's MFMAs)
+      } else {
+        frag(sidx, fa[0], fb[0]);
+      }
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          if constexpr (NP == 3) acc[nt] = mfma_x3(a, b[nt], acc[nt]);
-          else acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[nt][0], acc[nt], 0, 0, 0);
-        }
+      for (int nt = 0; nt < NT; ++nt) {
+        if constexpr (NP == 3) acc[nt] = mfma_x3(fa[cur], fb[cur][nt], acc[nt]);
+        else acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][0], fb[cur][nt][0], acc[nt], 0, 0, 0);
       }
     }
     if (ch == nch - 1) {
@@ -632,19 +646,26 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_x3p_kernel(const X3Args p)
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     }
     const __bf16* bbase = wc + j * WP + 8 * h + wseg;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int kh = t / 3, kw = t % 3;
+    // K steps s = (tap, 16-channel slice); step s + 1's fragments are read before step s's MFMAs (as conv3x3_x3_kernel)
+    auto frag = [&](int sidx, bf16x8 (&a)[NP], bf16x8 (&b)[NP]) {
+      const int t = sidx / (PC / 16), kk = sidx % (PC / 16), kh = t / 3, kw = t % 3;
       const __bf16* ap = pc + (arow0 + kh * PW + kw) * RP + 8 * h;
 #pragma unroll
+      for (int q = 0; q < NP; ++q) a[q] = *reinterpret_cast<const bf16x8*>(ap + q * PC + kk * 16);
+#pragma unroll
+      for (int q = 0; q < NP; ++q) b[q] = *reinterpret_cast<const bf16x8*>(bbase + (t * NP + q) * PC + kk * 16);
+    };
+    bf16x8 fa[2][NP], fb[2][NP];
+    frag(0, fa[0], fb[0]);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+#pragma unroll
       for (int kk = 0; kk < PC / 16; ++kk) {
-        bf16x8 a[NP], b[NP];
-#pragma unroll
-        for (int q = 0; q < NP; ++q) a[q] = *reinterpret_cast<const bf16x8*>(ap + q * PC + kk * 16);
-#pragma unroll
-        for (int q = 0; q < NP; ++q) b[q] = *reinterpret_cast<const bf16x8*>(bbase + (t * NP + q) * PC + kk * 16);
-        if constexpr (NP == 3) acc = mfma_x3(a, b, acc);
-        else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+        const int sidx = t * (PC / 16) + kk, cur = sidx & 1;
+        if (sidx + 1 < 9 * (PC / 16)) frag(sidx + 1, fa[cur ^ 1], fb[cur ^ 1]);
+        __builtin_amdgcn_sched_barrier(0);  // (keeps those reads ahead of this step's MFMAs)
+        if constexpr (NP == 3) acc = mfma_x3(fa[cur], fb[cur], acc);
+        else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][0], fb[cur][0], acc, 0, 0, 0);
       }
       // the next item's staging, spread over the taps: patch pieces after taps 0, 4 (, 8), weight pieces after 2, 6
       if ((t & 3) == 0 && t / 4 < PIT) stash_p(Rn, t / 4, min(k + 1, nitems - 1), pn);
@@ -950,29 +971,33 @@ int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float*
 template <int NT, int PC, int NP, int CPH, int CPW>
 __device__ __forceinline__ void dgrad_s2x3_class(f32x16 (&acc)[NT], const __bf16* abase, const __bf16* bbase,
                                                  int WP) {
+  // the class's taps (kh, kw) with their dY offsets (dh, dw), as K steps s = (tap, 16-channel slice); the fragments of
+  // step s + 1 are read before step s's MFMAs (one step of register double-buffering, as conv3x3_x3_kernel)
+  constexpr int NTAP = (CPH ? 2 : 1) * (CPW ? 2 : 1), KK = PC / 16, NSTEP = NTAP * KK;
+  auto frag = [&](int sidx, bf16x8 (&av)[NP], bf16x8 (&bv)[NT][NP]) {
+    const int tp = sidx / KK, kk = sidx % KK, ai = CPW ? tp / 2 : tp, bi = CPW ? tp % 2 : 0;
+    const int kh = CPH ? (ai == 0 ? 0 : 2) : 1, dh = (CPH && ai == 0) ? 1 : 0;
+    const int kw = CPW ? (bi == 0 ? 0 : 2) : 1, dw = (CPW && bi == 0) ? 1 : 0;
+    const __bf16* ap = abase + (dh * 9 + dw) * (NP * PC + 8);
+    const __bf16* bp = bbase + (kh * 3 + kw) * NP * PC;
 #pragma unroll
-  for (int a = 0; a < (CPH ? 2 : 1); ++a) {
-    const int kh = CPH ? (a == 0 ? 0 : 2) : 1, dh = (CPH && a == 0) ? 1 : 0;
+    for (int q = 0; q < NP; ++q) av[q] = *reinterpret_cast<const bf16x8*>(ap + q * PC + kk * 16);
 #pragma unroll
-    for (int b = 0; b < (CPW ? 2 : 1); ++b) {
-      const int kw = CPW ? (b == 0 ? 0 : 2) : 1, dw = (CPW && b == 0) ? 1 : 0;
-      const __bf16* ap = abase + (dh * 9 + dw) * (NP * PC + 8);
-      const __bf16* bp = bbase + (kh * 3 + kw) * NP * PC;
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int kk = 0; kk < PC / 16; ++kk) {
-        bf16x8 av[NP];
+      for (int q = 0; q < NP; ++q) bv[nt][q] = *reinterpret_cast<const bf16x8*>(bp + nt * 32 * WP + q * PC + kk * 16);
+  };
+  bf16x8 fa[2][NP], fb[2][NT][NP];
+  frag(0, fa[0], fb[0]);
 #pragma unroll
-        for (int q = 0; q < NP; ++q) av[q] = *reinterpret_cast<const bf16x8*>(ap + q * PC + kk * 16);
+  for (int sidx = 0; sidx < NSTEP; ++sidx) {
+    const int cur = sidx & 1;
+    if (sidx + 1 < NSTEP) frag(sidx + 1, fa[cur ^ 1], fb[cur ^ 1]);
+    __builtin_amdgcn_sched_barrier(0);  // (keeps those reads ahead of this step's MFMAs)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          bf16x8 bv[NP];
-#pragma unroll
-          for (int q = 0; q < NP; ++q)
-            bv[q] = *reinterpret_cast<const bf16x8*>(bp + nt * 32 * WP + q * PC + kk * 16);
-          if constexpr (NP == 3) acc[nt] = mfma_x3(av, bv, acc[nt]);
-          else acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[0], acc[nt], 0, 0, 0);
-        }
-      }
+    for (int nt = 0; nt < NT; ++nt) {
+      if constexpr (NP == 3) acc[nt] = mfma_x3(fa[cur], fb[cur][nt], acc[nt]);
+      else acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][0], fb[cur][nt][0], acc[nt], 0, 0, 0);
     }
   }
 }
@@ -1178,7 +1203,7 @@ int g_dgrad_s2_w3 = 1;
 int g_dgrad_s2_nt = 1;  // knob "conv_dgrad_s2_nt": 1 = 32 input channels per block (default: config-2 layer 4 92 -> 75 us, profiles/r04_s2_nt_ab.json), 0 = 64 where the grid allows
 
 bool conv3_dgrad_w3_wanted(const Conv3Layer& L) {
-  return g_dgrad_s2_w3 && !g_conv_bf16 && conv3_x3_dgrad_s2_supported(L);
+  return (g_dgrad_s2_w3 && !g_conv_bf16 && conv3_x3_dgrad_s2_supported(L)) || dgrad_s1_dma_supported(L);
 }
 
 int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,

@@ -540,6 +540,251 @@ int dgrad_s2_dma(const Conv3Layer& L, const __bf16* dy_planes, const __bf16* w3,
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Stride-1 input gradient (the transpose of cad:128-139's stride-1 nn.Conv2d): dX[p][n] = sum_{tap, c} dY[p + off(tap)]
+// [c] Wd[n][8 - tap][c], on pre-split dY planes and the pre-split Wd image staged by LDS-DMA, with the BN-backward
+// reduce of the layer below fused into the epilogue (conv3x3_x3_kernel<FWD = false>'s arithmetic: 32 x 32 x 16 bf16
+// MFMA, the six products per K step in the same order over the same 16-channel chunks, so its result bit for bit).
+// A 512-thread block owns a run of 256-pixel tiles (NI images of TH x TW) x 32 output channels; each (tile, chunk)
+// item's patch (TH + 2) x (TW + 2) x 16 channels x 3 planes and weight slice 32 x 9 taps x 16 x 3 planes are DMA'd
+// into one of NB LDS buffers (rows padded to an odd number of 16-B units: conflict-free b128 fragment reads), the
+// copies of item k + NB - 1 issued after the barrier of item k.
+struct DgS1Args {
+  const __bf16* dy;  // planes [3][NF H W][C]
+  const __bf16* w3;  // pre-split Wd [N][9][C / 16][3][16]
+  float* out;        // dX [NF][H][W][N]
+  float* partials;   // fused BN-backward reduce: column-major [2N][gridDim.x] (nullable)
+  const float* bny;  //   y of the layer below [NF][H][W][N]
+  const float* bnst;
+  int dy_ps;
+  int NF, H, W, C, N;
+  int tiles_h, tiles_w, ntiles, tpb;
+};
+
+template <int NI, int TH, int TW>
+__device__ __forceinline__ void s1_tile_pixel(int m, int& mi, int& py, int& px) {
+  if constexpr (TH == 8 && TW == 8 && NI == 4) {  // (conv3x3_x3_kernel's 8x8 map: 16-lane read phases 4 rows apart)
+    const int w = m >> 5, g = (m >> 3) & 3;
+    mi = w >> 1;
+    py = 2 * (w & 1) + 4 * (g & 1) + (g >> 1);
+    px = m & 7;
+  } else {
+    mi = m / (TH * TW);
+    const int mr = m % (TH * TW);
+    py = mr / TW;
+    px = mr % TW;
+  }
+}
+
+template <int NI, int TH, int TW, int NB>
+__global__ __launch_bounds__(512, 2) void dgrad_s1_dma_kernel(const DgS1Args p) {
+  static_assert(NI * TH * TW == 256, "a wave owns 32 pixels");
+  constexpr int PC = 16, NC = 32, RP = 3 * PC + 8, WP = 9 * 3 * PC + 8;  // 7 and 55 chunks per row
+  constexpr int PH = TH + 2, PW = TW + 2, PROWS = NI * PH * PW;
+  constexpr int PCH = PROWS * RP / 8, WCH = NC * WP / 8, NCHK = PCH + WCH;
+  constexpr int NI_ = (NCHK + 63) / 64, DW = (NI_ + 7) / 8, BUF = NI_ * 64 * 8;
+  static_assert(NB * BUF * 2 <= 163840 && DW >= 2, "LDS budget");
+  __shared__ __attribute__((aligned(1024))) __bf16 sm[NB * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, j = lane & 31;
+  const int n0 = blockIdx.y * NC;
+  const int nch = p.C / PC;
+  const int t0 = blockIdx.x * p.tpb, t1 = min(p.ntiles, t0 + p.tpb);
+  const int items = (t1 - t0) * nch;
+  const int tiles_per_img = p.tiles_h * p.tiles_w;
+  const __bf16* const zp = g_zero_page;
+
+  int kind[DW], geo[DW], so[DW];  // kind 0 patch, 1 weights, 2 padding
+#pragma unroll
+  for (int u = 0; u < DW; ++u) {
+    int i = wave + 8 * u;
+    if (i >= NI_) i -= 8;
+    const int c = 64 * i + lane;
+    if (c < PCH) {
+      const int row = c / 7, k = c % 7;
+      const int im = row / (PH * PW), rr = row % (PH * PW);
+      kind[u] = k < 6 ? 0 : 2;
+      geo[u] = (im << 16) | ((rr / PW) << 8) | (rr % PW);
+      so[u] = (k >> 1) * p.dy_ps + (k & 1) * 8;
+    } else if (c < NCHK) {
+      const int cc = c - PCH, n = cc / 55, k = cc % 55;
+      kind[u] = (k < 54 && n0 + n < p.N) ? 1 : 2;
+      geo[u] = 0;
+      so[u] = ((n0 + n) * 9 + 8 - k / 6) * (p.C / 16) * 48 + ((k % 6) >> 1) * 16 + (k & 1) * 8;
+    } else {
+      kind[u] = 2;
+      geo[u] = 0;
+      so[u] = 0;
+    }
+  }
+  auto origin = [&](int tile, int& img0, int& oy0, int& ox0) {
+    img0 = (tile / tiles_per_img) * NI;
+    const int tr = tile % tiles_per_img;
+    oy0 = (tr / p.tiles_w) * TH;
+    ox0 = (tr % p.tiles_w) * TW;
+  };
+  auto issue = [&](int it, int buf) {
+    const int tile = t0 + it / nch, c0 = (it % nch) * PC;
+    int img0, oy0, ox0;
+    origin(tile, img0, oy0, ox0);
+#pragma unroll
+    for (int u = 0; u < DW; ++u) {
+      const int k = kind[u], g = geo[u];
+      const __bf16* gp = zp;
+      if (k == 1) {
+        gp = p.w3 + so[u] + (c0 / 16) * 48;
+      } else if (k == 0) {
+        const int img = img0 + (g >> 16), y = oy0 - 1 + ((g >> 8) & 255), x = ox0 - 1 + (g & 255);
+        if (img < p.NF && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W)
+          gp = p.dy + so[u] + ((img * p.H + y) * p.W + x) * p.C + c0;
+      }
+      dma16(gp, sm + buf * BUF + (wave + 8 * u - (wave + 8 * u >= NI_ ? 8 : 0)) * 512);
+    }
+  };
+
+  int mi, py, px;
+  s1_tile_pixel<NI, TH, TW>(wave * 32 + j, mi, py, px);
+  const int arow0 = (mi * PH + py) * PW + px;
+  f32x16 acc;
+  float s1 = 0.f, s2 = 0.f;
+  const bool bnb = p.bny != nullptr;
+  const int col = n0 + j;
+  float bmean = 0.f, binv = 0.f, bsc = 0.f, bsh = 0.f;
+  if (bnb) {
+    const int cc = min(col, p.N - 1);
+    bmean = p.bnst[cc];
+    binv = p.bnst[p.N + cc];
+    bsc = p.bnst[2 * p.N + cc];
+    bsh = p.bnst[3 * p.N + cc];
+  }
+#pragma unroll
+  for (int s = 0; s < NB - 1; ++s)
+    if (s < items) issue(s, s);
+  for (int it = 0; it < items; ++it) {
+    if (NB == 3 && it + 1 < items) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (it + NB - 1 < items) issue(it + NB - 1, (it + NB - 1) % NB);
+    const int ch = it % nch;
+    if (ch == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    }
+    const __bf16* const bb = sm + (it % NB) * BUF;
+    const __bf16* const wl = bb + PROWS * RP;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int kh = t / 3, kw = t % 3;
+      const __bf16* ap = bb + (arow0 + kh * PW + kw) * RP + 8 * h;
+      const __bf16* bp = wl + j * WP + t * 3 * PC + 8 * h;
+      bf16x8d a[3], b[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        a[q] = *reinterpret_cast<const bf16x8d*>(ap + q * PC);
+        b[q] = *reinterpret_cast<const bf16x8d*>(bp + q * PC);
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+    }
+    if (ch == nch - 1) {
+      int img0, oy0, ox0;
+      origin(t0 + it / nch, img0, oy0, ox0);
+      float yb[16];
+      if (bnb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int qi, qy, qx;
+          s1_tile_pixel<NI, TH, TW>(wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, qi, qy, qx);
+          const int oy = oy0 + qy, ox = ox0 + qx, img = img0 + qi;
+          const bool ok = img < p.NF && oy < p.H && ox < p.W;
+          yb[r] = p.bny[(ok ? ((int64_t)(img * p.H + oy) * p.W + ox) * p.N : 0) + min(col, p.N - 1)];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int qi, qy, qx;
+        s1_tile_pixel<NI, TH, TW>(wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, qi, qy, qx);
+        const int oy = oy0 + qy, ox = ox0 + qx, img = img0 + qi;
+        if (img >= p.NF || oy >= p.H || ox >= p.W || col >= p.N) continue;
+        const float v = acc[r];
+        p.out[((int64_t)(img * p.H + oy) * p.W + ox) * p.N + col] = v;
+        if (bnb) {
+          const float dz = fmaf(yb[r], bsc, bsh) > 0.f ? v : 0.f;
+          s1 += dz;
+          s2 = fmaf(dz, (yb[r] - bmean) * binv, s2);
+        }
+      }
+    }
+  }
+  if (bnb && p.partials) {  // per-block sums, fixed order: lane halves, then the 8 waves
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float* red = reinterpret_cast<float*>(sm);  // [8 waves][2][NC]
+    const float a1 = s1 + __shfl_xor(s1, 32, 64), a2 = s2 + __shfl_xor(s2, 32, 64);
+    if (lane < 32) {
+      red[(wave * 2 + 0) * NC + lane] = a1;
+      red[(wave * 2 + 1) * NC + lane] = a2;
+    }
+    __syncthreads();
+    if (tid < 2 * NC) {
+      const int which = tid / NC, c = tid % NC;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += red[(2 * w + which) * NC + c];
+      if (n0 + c < p.N) p.partials[(int64_t)(which * p.N + n0 + c) * gridDim.x + blockIdx.x] = v;
+    }
+  }
+}
+
+int g_dgrad_s1_dma = 0;           // knob "conv_dgrad_s1_dma": stride-1 input gradients on dY planes by LDS-DMA
+int g_dgrad_s1_dma_blocks = 256;  // knob "conv_dgrad_s1_dma_blocks": target grid
+
+bool dgrad_s1_dma_supported(const Conv3Layer& L) {
+  const int64_t lim = ((int64_t)1 << 31) / 3 - 64;
+  return g_dgrad_s1_dma && !g_conv_bf16 && !g_act_bf16 && L.stride == 1 && L.Co % 16 == 0 && L.Ci % 32 == 0 &&
+         L.OH == L.IH && L.OW == L.IW && (int64_t)L.NF * L.OH * L.OW * L.Co < lim &&
+         (int64_t)L.NF * L.IH * L.IW * L.Ci < lim;
+}
+
+template <int NI, int TH, int TW>
+static int ds1_launch(DgS1Args a, const BnBwdFuse* f, hipStream_t st) {
+  a.tiles_h = (int)cdiv(a.H, TH);
+  a.tiles_w = (int)cdiv(a.W, TW);
+  a.ntiles = (int)cdiv(a.NF, NI) * a.tiles_h * a.tiles_w;
+  const int nct = a.N / 32;
+  a.tpb = (int)std::max<int64_t>(1, cdiv((int64_t)a.ntiles * nct, g_dgrad_s1_dma_blocks));
+  const int gx = (int)cdiv(a.ntiles, a.tpb);
+  if (f && f->cap < 2ll * a.N * gx) f = nullptr;
+  if (f) {
+    a.bny = f->y;
+    a.bnst = f->stats;
+    a.partials = f->parts;
+    *f->nparts = gx;
+  }
+  const dim3 grid((unsigned)gx, (unsigned)nct);
+  VAD_KLAUNCH((dgrad_s1_dma_kernel<NI, TH, TW, 2>), grid, dim3(512), 0, st, a);  // (3 buffers exceed the LDS)
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int dgrad_s1_dma(const Conv3Layer& L, const __bf16* dy_planes, const __bf16* w3, float* dX, hipStream_t st,
+                 const BnBwdFuse* f) {
+  VAD_CHECK(dgrad_s1_dma_supported(L) && w3 != nullptr, "dgrad_s1_dma: unsupported layer or no pre-split Wd image");
+  DgS1Args a{};
+  a.dy = dy_planes;
+  a.w3 = w3;
+  a.out = dX;
+  a.dy_ps = (int)((int64_t)L.NF * L.OH * L.OW * L.Co);
+  a.NF = L.NF; a.H = L.IH; a.W = L.IW; a.C = L.Co; a.N = L.Ci;
+  if (L.IW <= 8 && L.IH <= 8) return ds1_launch<4, 8, 8>(a, f, st);
+  if (L.IW <= 16) return ds1_launch<1, 16, 16>(a, f, st);
+  return ds1_launch<1, 8, 32>(a, f, st);
+}
+
 int g_wgrad_dma = 0;           // knob "conv_wgrad_dma": fp32 weight gradients on pre-split planes (x3_wgrad_dma_kernel)
 int g_wgrad_dma_blocks = 256;  // knob "conv_wgrad_dma_blocks": target grid (one 512-thread block per CU)
 int g_wgrad_dma_nb = 3;        // knob "conv_wgrad_dma_nb": LDS buffers (2 | 3)

@@ -71,7 +71,7 @@ struct TrwArgs {
 };
 
 // BNA: the BatchNorm backward apply of the layer (bn_bwd_apply's expression, bit-identical) folded into the dY staging
-template <int S, int NI, int TH, int TW, int NCO, bool BNA = false>
+template <int S, int NI, int TH, int TW, int NCO, bool BNA = false, bool PFT = false>
 __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
   constexpr int TPX = NI * TH * TW, KS = TPX / 32, KSW = NCO == 2 ? KS : KS / 2;
   static_assert(TW % 8 == 0 && TPX % 32 == 0 && KS % (3 - NCO) == 0 && (NCO == 1 || NCO == 2), "whole K steps");
@@ -250,14 +250,34 @@ __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
           const __bf16* base = ab + (u * 3 + q) * YH;
           a[u][q] = trf(base, base + 8 * 16);
         }
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
+      auto tap_off = [&](int t) {
         const int kh = t / 3, kw = t % 3;
         const int cs = S == 1 ? kw : ((kw & 1) ? PWE + (kw >> 1) : (kw >> 1));
-        const int to = (kh * PW + cs) * 16;
-        bfv8w b[3];
+        return (kh * PW + cs) * 16;
+      };
+      // PFT: tap t + 1's input fragments are read before tap t's MFMAs (one tap of register double-buffering), so a
+      // tap's 12 MFMAs do not wait for its own LDS reads
+      bfv8w bn[3];
+      if constexpr (PFT) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) b[q] = trf(xb0 + q * XH + to, xb1 + q * XH + to);
+        for (int q = 0; q < 3; ++q) bn[q] = trf(xb0 + q * XH, xb1 + q * XH);
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int to = tap_off(t);
+        bfv8w b[3];
+        if constexpr (PFT) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) b[q] = bn[q];
+          if (t + 1 < 9) {
+            const int tn = tap_off(t + 1);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) bn[q] = trf(xb0 + q * XH + tn, xb1 + q * XH + tn);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) b[q] = trf(xb0 + q * XH + to, xb1 + q * XH + to);
+        }
         // the six products that reach fp32 resolution, smallest first (a: dY planes hi/mid/lo, b: input planes)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -316,6 +336,8 @@ bool x3_wgrad_tr_supported(const Conv3Layer& L) {
          L.OH < 256 && L.OW < 256;
 }
 
+int g_wgrad_tr_pft = 1;  // knob "conv_wgrad_tr_pft": the next tap's input fragments read before this tap's MFMAs
+
 template <int S, int NI, int TH, int TW, int NCO, bool BNA = false>
 static int trw_launch(TrwArgs a, int target_blocks, int64_t partial_cap, hipStream_t st, int* nsplit) {
   a.tiles_h = (int)cdiv(a.OH, TH);
@@ -324,8 +346,18 @@ static int trw_launch(TrwArgs a, int target_blocks, int64_t partial_cap, hipStre
   const int pairs = (a.Co / (32 * NCO)) * (a.Ci / 32);
   int64_t z = std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, pairs), a.ntiles));
   z = std::min<int64_t>(z, std::max<int64_t>(1, partial_cap / ((int64_t)a.Co * 9 * a.Ci)));
-  VAD_KLAUNCH((x3_wgrad_tr_kernel<S, NI, TH, TW, NCO, BNA>), dim3(a.Co / (32 * NCO), a.Ci / 32, (unsigned)z),
-              dim3(256), 0, st, a);
+  // (stride 2: the second fragment set does not fit beside the parity-split images' registers -- it spills)
+  bool launched = false;
+  if constexpr (S == 1) {
+    if (g_wgrad_tr_pft) {
+      VAD_KLAUNCH((x3_wgrad_tr_kernel<S, NI, TH, TW, NCO, BNA, true>), dim3(a.Co / (32 * NCO), a.Ci / 32, (unsigned)z),
+                  dim3(256), 0, st, a);
+      launched = true;
+    }
+  }
+  if (!launched)
+    VAD_KLAUNCH((x3_wgrad_tr_kernel<S, NI, TH, TW, NCO, BNA, false>), dim3(a.Co / (32 * NCO), a.Ci / 32, (unsigned)z),
+                dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   *nsplit = (int)z;
   return 0;

@@ -52,12 +52,14 @@ extern "C" int vad_conv3x3_wgrad(const float* x_nhwc, const float* dy_nhwc, int 
 
 extern "C" int vad_set_tuning(const char* key, int value) { return vad::set_tuning(key, value); }
 
-extern "C" int vad_conv3x3_dgrad_s2_planes(const float* dy_nhwc, int NF, int Ci, int IH, int IW, const float* w, int Co,
-                                           float* dx_nhwc, float* scratch, int64_t scratch_floats, void* stream) {
-  Conv3Layer L{NF, Ci, Co, IH, IW, (IH - 1) / 2 + 1, (IW - 1) / 2 + 1, 2};
-  VAD_CHECK(dgrad_s2_dma_supported(L), "vad_conv3x3_dgrad_s2_planes: unsupported shape (or knob conv_dgrad_s2_dma off)");
+extern "C" int vad_conv3x3_dgrad_planes(const float* dy_nhwc, int NF, int Ci, int IH, int IW, const float* w, int Co,
+                                        int stride, float* dx_nhwc, float* scratch, int64_t scratch_floats,
+                                        void* stream) {
+  Conv3Layer L{NF, Ci, Co, IH, IW, (IH - 1) / stride + 1, (IW - 1) / stride + 1, stride};
+  VAD_CHECK((stride == 2 && dgrad_s2_dma_supported(L)) || (stride == 1 && dgrad_s1_dma_supported(L)),
+            "vad_conv3x3_dgrad_planes: unsupported shape (or knob conv_dgrad_s1_dma / conv_dgrad_s2_dma off)");
   const int64_t nw = (int64_t)9 * Ci * Co, mo = (int64_t)NF * L.OH * L.OW * Co;
-  VAD_CHECK(scratch_floats >= 4 * nw + (3 * mo + 1) / 2 + 1024, "vad_conv3x3_dgrad_s2_planes: scratch too small");
+  VAD_CHECK(scratch_floats >= 4 * nw + (3 * mo + 1) / 2 + 1024, "vad_conv3x3_dgrad_planes: scratch too small");
   float* wf = scratch;
   float* wd = scratch + nw;  // fp32 Wd, then its bf16 planes (1.5 nw floats)
   __bf16* w3 = reinterpret_cast<__bf16*>(wd + nw);
@@ -69,5 +71,5 @@ extern "C" int vad_conv3x3_dgrad_s2_planes(const float* dy_nhwc, int NF, int Ci,
   __bf16* w31[1] = {w3};
   VAD_TRY(conv3_prep_weights_all(1, w1, &L, wf1, wd1, st, w31));
   VAD_TRY(planes_split(dy_nhwc, nullptr, mo / Co, Co, pdy, st));
-  return dgrad_s2_dma(L, pdy, w3, dx_nhwc, st, nullptr);
+  return stride == 2 ? dgrad_s2_dma(L, pdy, w3, dx_nhwc, st, nullptr) : dgrad_s1_dma(L, pdy, w3, dx_nhwc, st, nullptr);
 }

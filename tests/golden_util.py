@@ -158,8 +158,9 @@ def pinned_oracle_grads(state_dict, x, labels, draws, masks, sync_group=None, bf
     hip_relu_masks): the exact gradient of that forward's piecewise-linear branch, free of kink flips.  Returns
     (grads {name: float64 tensor or None}, losses {name: float64}, the oracle's result dict incl. "bufs" and
     "record" -- the float64 BatchNorm outputs "z{l}" in front of each pinned ReLU, for check_mask_flips).
-    bf16: the backbone as the device computes it in bf16 mode (cad_oracle.backbone_forward_bf16).  dtype: the
-    oracle's arithmetic (float64; float32 gives a second, independent restatement at fp32 accumulation)."""
+    bf16: the backbone as the device computes it in bf16 mode (cad_oracle.backbone_forward_bf16; "reversed": its convs
+    sum the input channels in reverse order).  dtype: the oracle's arithmetic (float64; float32 gives further,
+    independent restatements at fp32 accumulation)."""
     from oracle import cad_oracle as co
     params = {k: v.detach().to(dtype).clone() for k, v in state_dict.items()
               if "running" not in k and "num_batches" not in k}
@@ -167,7 +168,7 @@ def pinned_oracle_grads(state_dict, x, labels, draws, masks, sync_group=None, bf
     xd = x.to(dtype)
     rm = reshape_masks(masks, xd)
     record = {}
-    kw = dict(bf16=True) if bf16 else {}
+    kw = dict(bf16=bf16) if bf16 else {}
     res = co.cad_train_step(params, bufs, {}, xd, labels, draws, relu_masks=rm, sync_group=sync_group,
                             record=record, **kw)
     res["bufs"] = bufs  # running stats after the step's forward

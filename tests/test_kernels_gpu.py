@@ -419,10 +419,45 @@ def test_conv3x3_dgrad_s2_dma_bit_identical(NF, Ci, Co, IH, IW):
     dx1 = torch.full((NF, IH, IW, Ci), float("nan"), device=d)
     nat.lib().vad_set_tuning(b"conv_dgrad_s2_dma", 1)
     try:
-        nat.check(nat.lib().vad_conv3x3_dgrad_s2_planes(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co,
-                                                        dx1.data_ptr(), scratch.data_ptr(), scratch.numel(), st))
+        nat.check(nat.lib().vad_conv3x3_dgrad_planes(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, 2,
+                                                     dx1.data_ptr(), scratch.data_ptr(), scratch.numel(), st))
         torch.cuda.synchronize()
     finally:
         nat.lib().vad_set_tuning(b"conv_dgrad_s2_dma", 0)
     np.testing.assert_array_equal(dx1.cpu().numpy(), dx0.cpu().numpy())
     np.testing.assert_allclose(dx1.cpu().permute(0, 3, 1, 2).double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("NF,Ci,Co,IH,IW", [(2, 32, 32, 57, 57), (3, 64, 64, 29, 29), (4, 128, 128, 15, 15),
+                                            (5, 256, 256, 8, 8), (2, 32, 64, 13, 40)])
+def test_conv3x3_dgrad_s1_dma_bit_identical(NF, Ci, Co, IH, IW):
+    """Stride-1 input gradient on pre-split dY planes + the pre-split (tap-flipped) Wd image staged by LDS-DMA (knob
+    conv_dgrad_s1_dma; 8x32, 16x16 and 4-frame 8x8 tiles, ragged edges) equals the split-bf16 patch kernel bit for
+    bit and matches the fp64 reference."""
+    nat = _lib()
+    g = torch.Generator().manual_seed(31 + Ci + IH)
+    w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
+    dy = torch.randn(NF, Co, IH, IW, generator=g)
+    ref = torch.nn.grad.conv2d_input((NF, Ci, IH, IW), w.double(), dy.double(), stride=1, padding=1)
+    d = torch.device("cuda")
+    dyh = dy.permute(0, 2, 3, 1).contiguous().to(d)
+    wdev = w.contiguous().to(d)
+    wf = torch.empty(9 * Ci * Co, device=d)
+    wd = torch.empty(9 * Ci * Co, device=d)
+    st = nat.stream_of(d)
+    _conv_path(nat, 3)
+    dx0 = torch.empty(NF, IH, IW, Ci, device=d)
+    nat.check(nat.lib().vad_conv3x3_dgrad(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, 1, dx0.data_ptr(),
+                                          wf.data_ptr(), wd.data_ptr(), st))
+    scratch = torch.empty(4 * 9 * Ci * Co + 3 * NF * IH * IW * Co // 2 + 4096, device=d)
+    dx1 = torch.full((NF, IH, IW, Ci), float("nan"), device=d)
+    nat.lib().vad_set_tuning(b"conv_dgrad_s1_dma", 1)
+    try:
+        nat.check(nat.lib().vad_conv3x3_dgrad_planes(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, 1,
+                                                     dx1.data_ptr(), scratch.data_ptr(), scratch.numel(), st))
+        torch.cuda.synchronize()
+    finally:
+        nat.lib().vad_set_tuning(b"conv_dgrad_s1_dma", 0)
+        _conv_default(nat)
+    np.testing.assert_allclose(dx1.cpu().permute(0, 3, 1, 2).double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(dx1.cpu().numpy(), dx0.cpu().numpy())
