@@ -294,6 +294,8 @@ __global__ __launch_bounds__(256, 2) void bfc_conv_kernel(const BfcArgs p) {
         bfv8(&ac)[MF] = (s & 1) ? a1 : a0;
         bfv8(&bc)[NCT] = (s & 1) ? b1 : b0;
         if (s + 1 < NSTEP) frags(s + 1, (s & 1) ? a0 : a1, (s & 1) ? b0 : b1);
+        // (the compiler otherwise sinks those reads to their MFMAs; not where the pinned fragments would spill)
+        if constexpr (!(NCT == 2 && CB == 32 && !WRES)) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
