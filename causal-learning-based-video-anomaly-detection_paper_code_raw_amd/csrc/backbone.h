@@ -18,7 +18,6 @@ extern int g_x3_pipe;  // knob "conv_split_pipe"
 extern int g_x3_s2big;  // knob "conv_split_s2big"
 extern int g_cad_dir_affine;  // knob "cad_dir_affine": the direct classifier's loss-mode backward precomputed in the forward
 extern int g_cad_stem_early;
-extern int g_cad_dy_planes, g_cad_x_planes;  // knobs "cad_dy_planes", "cad_x_planes" (operand planes of x3_wgrad_dma)
 extern int g_cad_prep_stream, g_cad_wgrad_stream, g_cad_det_gate, g_cad_last_wgrad_main, g_cad_event_sysfence,
     g_cad_dy_per_layer, g_cad_l0_slab, g_cad_stream_prio;  // knobs "cad_prep_stream", "cad_wgrad_stream" (A/B)
 extern int g_stem_fused;  // knob "stem_fused" (default 1)
@@ -48,9 +47,6 @@ int bn_bwd_finalize(const float* partials, int P, int C, double count, const flo
 // bias_partials may be null (the conv bias grad then comes from bn_bwd_finalize's dbias)
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
                  int* nparts, hipStream_t st);
-// the same writing dY (nullable) and its pre-split bf16 planes [3][M][C] (x3_wgrad_dma's operand; fp32 activations)
-int bn_bwd_apply_planes(const float* dA, const float* y, const float* stats, int M, int C, float* dY, __bf16* planes,
-                        hipStream_t st);
 // the same in place (dA == dY; fp32 activations: the training stem's backward)
 int bn_bwd_apply_inplace(float* dAY, const float* y, const float* stats, int M, int C, hipStream_t st);
 int bn_rows_parts(int M, int C);
@@ -160,25 +156,6 @@ int x3_wgrad_tr(const Conv3Layer& L, const float* dY, const float* src, const fl
                 const float* bnst = nullptr);
 extern int g_wgrad_bn_fused;  // knob "conv_wgrad_bn_fused"
 bool x3_wgrad_tr_bn_supported(const Conv3Layer& L);
-// fp32 weight gradients on pre-split bf16 operand planes staged by LDS-DMA (conv_x3d.hip): dy_planes [3][NF OH OW][Co]
-// (split dY), x_planes [3][NF IH IW][Ci] (split relu(bn(x))) -- planes_split writes both
-extern int g_wgrad_dma, g_wgrad_dma_blocks, g_wgrad_dma_nb;  // knobs "conv_wgrad_dma", "conv_wgrad_dma_blocks", "conv_wgrad_dma_nb"
-bool x3_wgrad_dma_supported(const Conv3Layer& L);
-int x3_wgrad_dma(const Conv3Layer& L, const __bf16* dy_planes, const __bf16* x_planes, float* slab, int* nsplit,
-                 int64_t partial_cap, int target_blocks, hipStream_t st);
-// stride-2 input gradient on dY planes + the pre-split Wd image by LDS-DMA (conv_x3d.hip; conv3x3_dgrad_s2x3_kernel's
-// arithmetic, bit for bit); f: the fused BN-backward reduce of the layer below (as conv3_dgrad)
-extern int g_dgrad_s2_dma, g_dgrad_s2_dma_nb, g_dgrad_s2_dma_blocks;  // knobs "conv_dgrad_s2_dma", "..._nb", "..._blocks"
-bool dgrad_s2_dma_supported(const Conv3Layer& L);
-int dgrad_s2_dma(const Conv3Layer& L, const __bf16* dy_planes, const __bf16* w3, float* dX, hipStream_t st,
-                 const BnBwdFuse* f);
-// the same for stride 1 (conv3x3_x3_kernel<FWD = false>'s arithmetic, bit for bit; w3 flipped taps as stored)
-extern int g_dgrad_s1_dma, g_dgrad_s1_dma_blocks;  // knobs "conv_dgrad_s1_dma", "conv_dgrad_s1_dma_blocks"
-bool dgrad_s1_dma_supported(const Conv3Layer& L);
-int dgrad_s1_dma(const Conv3Layer& L, const __bf16* dy_planes, const __bf16* w3, float* dX, hipStream_t st,
-                 const BnBwdFuse* f);
-// fp32 [M][C] -> bf16 planes [3][M][C] (hi, mid, lo), with BN + ReLU (stats = the producer's BN state) when given
-int planes_split(const float* src, const float* stats, int64_t M, int C, __bf16* dst, hipStream_t st);
 bool conv3_wgrad_patch_supported(const Conv3Layer& L);
 int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
                       int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);

@@ -25,8 +25,6 @@ int g_cad_wgrad_stream = 1;  // knob "cad_wgrad_stream": backbone weight gradien
 int g_bn_bwd_fuse = 3;
 int g_cad_stream_prio = 1;  // knob "cad_stream_prio" (cad_plan.hip streams(); A/B profiles/r03_prio_ab.json)
 int g_cad_l0_slab = 1;  // knob "cad_l0_slab": layer 0's weight gradient on a split-K slab of its own (no wait for layer 1's)
-int g_cad_dy_planes = 1;  // knob "cad_dy_planes": with x3_wgrad_dma, the BN backward writes dY's bf16 planes itself
-int g_cad_x_planes = 1;   // knob "cad_x_planes": with x3_wgrad_dma, the training forward splits each layer input on the weight-gradient stream
 
 // =====================================================================================================
 // conv1: 1 -> 32 channels, 7x7, stride 2, pad 3, as a K=49 (padded to 56) GEMM on f32 MFMA.
@@ -611,14 +609,11 @@ int bn_bwd_apply_inplace(float* dAY, const float* y, const float* stats, int M, 
 // Streaming form (no conv-bias partial sums): thread = 8 consecutive channels of a row (16 B per operand in bf16, 32 B in
 // fp32), U rows per iteration with every load issued before the arithmetic (the 4-channel row loop above keeps one 8-B
 // load per operand in flight per thread and reaches ~3.5 TB/s), grid-stride over the row groups.
-// PL: dY also (dY nullable: only) as pre-split bf16 planes [3][M][C] (hi, mid, lo: the weight gradient on
-// x3_wgrad_dma_kernel stages them by LDS-DMA; the split is conv_x3.hip's, bit for bit)
-template <bool AB, int U, bool PL = false>
+template <bool AB, int U>
 __global__ __launch_bounds__(256) void bn_bwd_apply_v_kernel(const act_t<AB>* __restrict__ dA,
                                                            const act_t<AB>* __restrict__ y,
                                                            const float* __restrict__ stats, int M, int C,
-                                                           act_t<AB>* __restrict__ dY,
-                                                           __bf16* __restrict__ planes = nullptr) {
+                                                           act_t<AB>* __restrict__ dY) {
   using V = typename std::conditional<AB, u32x4v, f32x8v>::type;  // 8 channels
   const int tpr = C / 8, rpp = 256 / tpr;                         // threads per row, rows per pass
   const int q = threadIdx.x % tpr, c = q * 8;
@@ -655,24 +650,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_v_kernel(const act_t<AB>* __
         const float xh = (yf[e] - mean[e]) * inv[e];
         o[e] = k[e] * (dz - mdz[e] - xh * mdzx[e]);
       }
-      if (!PL || dY) *reinterpret_cast<V*>(dY + r * C + c) = vstore8<V>(o);
-      if constexpr (PL) {
-        typedef __bf16 b8 __attribute__((ext_vector_type(8)));
-        b8 hi, mid, lo;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const __bf16 h = (__bf16)o[e];
-          const float rr = o[e] - (float)h;
-          const __bf16 mm = (__bf16)rr;
-          hi[e] = h;
-          mid[e] = mm;
-          lo[e] = (__bf16)(rr - (float)mm);
-        }
-        const int64_t ps = (int64_t)M * C;
-        *reinterpret_cast<b8*>(planes + r * C + c) = hi;
-        *reinterpret_cast<b8*>(planes + ps + r * C + c) = mid;
-        *reinterpret_cast<b8*>(planes + 2 * ps + r * C + c) = lo;
-      }
+      *reinterpret_cast<V*>(dY + r * C + c) = vstore8<V>(o);
     }
   }
 }
@@ -680,18 +658,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_v_kernel(const act_t<AB>* __
 int g_bn_apply_v = 1;  // knob "bn_apply_v": the streaming apply kernel (0: the 4-channel row loop)
 int g_bn_apply_u = 4;          // knob "bn_apply_u": rows in flight per thread (2, 4, 8)
 int g_bn_apply_blocks = 2048;  // knob "bn_apply_blocks": grid cap (grid-stride beyond it)
-
-int bn_bwd_apply_planes(const float* dA, const float* y, const float* stats, int M, int C, float* dY, __bf16* planes,
-                        hipStream_t st) {
-  VAD_CHECK(!g_act_bf16 && C % 8 == 0 && C >= 8 && C <= 2048 && 256 % (C / 8) == 0,
-            "bn_bwd_apply_planes: fp32 activations, C = 8 * a power of two");
-  const int rpp = 256 / (C / 8);
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(M, (int64_t)rpp * 4), g_bn_apply_blocks));
-  hipLaunchKernelGGL((bn_bwd_apply_v_kernel<false, 4, true>), dim3(blocks), dim3(256), 0, st, dA, y, stats, M, C, dY,
-                     planes);
-  VAD_LAUNCH_CHECK();
-  return 0;
-}
 
 int bn_bwd_apply(const float* dA, const float* y, const float* stats, int M, int C, float* dY, float* bias_partials,
                  int* nparts, hipStream_t st) {
@@ -1176,16 +1142,6 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv3d_direct") g_conv3d_direct = value;
   else if (k == "conv3d_wgrad_blocks") g_conv3d_wg_blocks = value;
   else if (k == "conv_wgrad_bn_fused") g_wgrad_bn_fused = value;
-  else if (k == "conv_wgrad_dma") g_wgrad_dma = value;
-  else if (k == "cad_dy_planes") g_cad_dy_planes = value;
-  else if (k == "conv_dgrad_s2_dma") g_dgrad_s2_dma = value;
-  else if (k == "conv_dgrad_s1_dma") g_dgrad_s1_dma = value;
-  else if (k == "conv_dgrad_s1_dma_blocks") g_dgrad_s1_dma_blocks = value;
-  else if (k == "conv_dgrad_s2_dma_nb") g_dgrad_s2_dma_nb = value;
-  else if (k == "conv_dgrad_s2_dma_blocks") g_dgrad_s2_dma_blocks = value;
-  else if (k == "cad_x_planes") g_cad_x_planes = value;
-  else if (k == "conv_wgrad_dma_blocks") g_wgrad_dma_blocks = value;
-  else if (k == "conv_wgrad_dma_nb") g_wgrad_dma_nb = value;
   else if (k == "conv_dgrad_s2_w3") g_dgrad_s2_w3 = value;
   else if (k == "conv_dgrad_s2_nt") g_dgrad_s2_nt = value;
   else if (k == "bn_apply_u") g_bn_apply_u = value;

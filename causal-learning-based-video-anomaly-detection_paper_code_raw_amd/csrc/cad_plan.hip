@@ -364,13 +364,6 @@ struct CadPlanImpl {
   // shared dY buffer (one cross-queue barrier per layer less); ~2x the dY memory (≈210 MB at config 2)
   float* dYL[8] = {};
   int dy_per_layer = 1;
-  // pre-split operand planes of the weight gradients on x3_wgrad_dma_kernel (knob conv_wgrad_dma), per layer: dY and
-  // the layer input relu(bn(x)) as bf16 [3][pixels][channels]; fp32 plans only.  knob cad_dy_planes: layer l's BN
-  // backward writes its dY planes itself; knob cad_x_planes: the training forward splits each layer's input on the
-  // weight-gradient stream (idle in the forward) right after the producer's BN finalize (xpl_ok[l]: this forward did);
-  // otherwise the backward splits them on the weight gradient's queue
-  __bf16 *pl_dy[8] = {}, *pl_x[8] = {};
-  int xpl_ok[8] = {};
   float *sq_parts, *slot_info, *clip;
   int16_t* chunk_slot;
   int64_t parts_floats, dense_scratch_floats, wpart_floats, wpart0_floats, slab_len, act_max;
@@ -397,7 +390,6 @@ struct CadPlanImpl {
   // dYb[b] is done" (st3)
   hipStream_t st3 = nullptr;
   hipEvent_t ev_dy[2] = {nullptr, nullptr}, ev_wg[2] = {nullptr, nullptr}, ev_wgj = nullptr, ev_prep = nullptr;
-  hipEvent_t ev_xp = nullptr, ev_xpd = nullptr;  // forward: a layer input's BN is final / every input plane is split
   // ev_layer[l]: every grad of backbone layer l (conv weight + bias, BN gamma / beta) is final -- recorded after the
   // layer's split-K reduce on the queue that ran it (layer 0: also after the stem backward), for per-layer
   // data-parallel gradient buckets (vad_cad_wait_layer_grads)
@@ -431,8 +423,6 @@ struct CadPlanImpl {
         VAD_HIP(hipEventCreateWithFlags(&ev_wg[b], evf));
       }
       VAD_HIP(hipEventCreateWithFlags(&ev_wgj, evf));
-      VAD_HIP(hipEventCreateWithFlags(&ev_xp, evf));
-      VAD_HIP(hipEventCreateWithFlags(&ev_xpd, evf));
       VAD_HIP(hipEventCreateWithFlags(&ev_prep, evf));
       for (int l = 0; l < 8; ++l) VAD_HIP(hipEventCreateWithFlags(&ev_layer[l], evf));
       VAD_HIP(hipEventCreateWithFlags(&ev_input, evf));
@@ -468,8 +458,6 @@ struct CadPlanImpl {
       if (ev_wg[b]) (void)hipEventDestroy(ev_wg[b]);
     }
     if (ev_wgj) (void)hipEventDestroy(ev_wgj);
-    if (ev_xp) (void)hipEventDestroy(ev_xp);
-    if (ev_xpd) (void)hipEventDestroy(ev_xpd);
     if (ev_prep) (void)hipEventDestroy(ev_prep);
     for (int l = 0; l < 8; ++l)
       if (ev_layer[l]) (void)hipEventDestroy(ev_layer[l]);
@@ -581,10 +569,6 @@ struct CadPlanImpl {
     wpart = w.take<float>(wpart_floats);
     wpart0_floats = std::max<int64_t>(8ll << 20, (int64_t)L[0].Co * 9 * L[0].Ci);
     wpart0 = w.take<float>(wpart0_floats);
-    for (int l = 0; l < 8; ++l) {
-      pl_dy[l] = conv_bf16 ? nullptr : w.take<__bf16>(3 * nf * L[l].OH * L[l].OW * L[l].Co);
-      pl_x[l] = conv_bf16 ? nullptr : w.take<__bf16>(3 * nf * L[l].IH * L[l].IW * L[l].Ci);
-    }
     sq_parts = w.take<float>(1024);
     bnsync = w.take<double>(2 * 256);
     slot_info = w.take<float>(4 * 160);
@@ -817,28 +801,13 @@ struct CadPlanImpl {
     VAD_HIP(hipStreamWaitEvent(st, ev_prep, 0));  // layer1.0 reads the prepared weight images
     const float* src = pool;
     const float* sst = pool_stats;
-    // the weight gradients' input planes (knob cad_x_planes): split on the weight-gradient stream beside the forward
-    const bool xpl = training && grads != nullptr && g_cad_x_planes && pl_x[0] != nullptr && g_cad_wgrad_stream;
-    auto xplanes = [&](int l, const float* s, const float* ss) -> int {
-      xpl_ok[l] = 0;
-      if (!xpl || !x3_wgrad_dma_supported(L[l])) return 0;
-      VAD_HIP(hipEventRecord(ev_xp, st));
-      VAD_HIP(hipStreamWaitEvent(st3, ev_xp, 0));
-      hipStream_t st = st3;
-      TIMED(L_("x_planes", l), planes_split(s, ss, (int64_t)NF * L[l].IH * L[l].IW, L[l].Ci, pl_x[l], st));
-      xpl_ok[l] = 1;
-      return 0;
-    };
-    if (xpl) VAD_TRY(streams());
     for (int l = 0; l < 8; ++l) {
       int cm = 1;  // the split kernels write the partials column-major (coalesced finalize reads)
-      VAD_TRY(xplanes(l, src, sst));
       TIMED(L_("conv_fwd", l), conv3_fwd(L[l], src, sst, wf[l], P(LY.conv_b[l]), y[l], parts, &np, st, &cm));
       VAD_TRY(bn_fwd_stats(l + 1, np, L[l].Co, (double)NF * L[l].OH * L[l].OW, P(LY.bn_w[l]), P(LY.bn_b[l]), st, cm));
       src = y[l];
       sst = stats[l + 1];
     }
-    if (xpl) VAD_HIP(hipEventRecord(ev_xpd, st3));  // (layer 0's weight gradient on the caller's stream waits for it)
     TIMED("avgpool", avgpool_fwd(y[7], stats[8], B, T, HF, WF, 256, feats, pooled, st));
     const int64_t f0 = clip0 * T;
     const int dd[6] = {6144, 512, 256, 128, 64, 20};
@@ -1060,12 +1029,7 @@ struct CadPlanImpl {
       if (wgs && l + 2 <= 7 && !perl) VAD_HIP(hipStreamWaitEvent(st, ev_wg[l & 1], 0));
       // layer 0 with the frozen stem: its dY feeds only its weight gradient, which applies the BN backward itself
       const bool bnf = l == 0 && !stem_grad && conv3_wgrad_bn_fusable(L[0]);
-      const bool dma = !bnf && pl_dy[0] != nullptr && x3_wgrad_dma_supported(L[l]);
-      const bool dypl = dma && g_cad_dy_planes;  // the BN backward writes dY's planes too
-      if (dypl)
-        TIMED(L_("bn_bwd_apply", l), bn_bwd_apply_planes(dA, y[l], stats[l + 1], (int)M, C, dYl, pl_dy[l], st));
-      else if (!bnf)
-        TIMED(L_("bn_bwd_apply", l), bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dYl, nullptr, &nb, st));
+      if (!bnf) TIMED(L_("bn_bwd_apply", l), bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dYl, nullptr, &nb, st));
       const float* src = l == 0 ? pool : y[l - 1];
       const float* sst = l == 0 ? pool_stats : stats[l];
       {
@@ -1092,19 +1056,8 @@ struct CadPlanImpl {
         hipStream_t st = wst;
         int ns = 0;
         // (layer 0 with the frozen stem: little runs beside its weight gradient)
-        if (dma) {
-          // the LDS-DMA weight gradient on pre-split planes (split here those the BN backward / forward did not)
-          if (!dypl) TIMED(L_("wgrad_planes", l), planes_split(dYl, nullptr, M, C, pl_dy[l], st));
-          if (!xpl_ok[l])
-            TIMED(L_("wgrad_planes", l),
-                  planes_split(src, sst, (int64_t)NF * L[l].IH * L[l].IW, L[l].Ci, pl_x[l], st));
-          else if (on_main)
-            VAD_HIP(hipStreamWaitEvent(st, ev_xpd, 0));  // (split on the weight-gradient stream in the forward)
-          TIMED(L_("conv_wgrad", l), x3_wgrad_dma(L[l], pl_dy[l], pl_x[l], slab, &ns, slab_cap, 0, st));
-        } else {
-          TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], bnf ? dA : dYl, src, sst, slab, &ns, slab_cap, st,
-                                                 l == 0 && !stem_grad, bnf ? y[0] : nullptr, bnf ? stats[1] : nullptr));
-        }
+        TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], bnf ? dA : dYl, src, sst, slab, &ns, slab_cap, st,
+                                               l == 0 && !stem_grad, bnf ? y[0] : nullptr, bnf ? stats[1] : nullptr));
         TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], slab, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
         if (wgs && !on_main) VAD_HIP(hipEventRecord(ev_wg[l & 1], st));
         // (layer 0: recorded after the join below -- its data-parallel bucket also holds layers 1-3, whose weight
@@ -1116,13 +1069,7 @@ struct CadPlanImpl {
       if (l > 0) {
         // its epilogue also reduces layer l-1's BN backward (dZ = dA masked by layer l-1's ReLU, dZ * xhat)
         const BnBwdFuse fu{y[l - 1], stats[l], parts, parts_floats, &fused_np};
-        // dY's planes by LDS-DMA (knobs conv_dgrad_s2_dma, conv_dgrad_s1_dma)
-        if (dypl && w3[l] && dgrad_s2_dma_supported(L[l]))
-          TIMED(L_("conv_dgrad", l), dgrad_s2_dma(L[l], pl_dy[l], w3[l], dA, st, &fu));
-        else if (dypl && w3[l] && dgrad_s1_dma_supported(L[l]))
-          TIMED(L_("conv_dgrad", l), dgrad_s1_dma(L[l], pl_dy[l], w3[l], dA, st, &fu));
-        else
-          TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st, &fu, w3[l]));
+        TIMED(L_("conv_dgrad", l), conv3_dgrad(L[l], dYl, wd[l], dA, st, &fu, w3[l]));
       }
       if (l == debug_stop_layer) break;
     }

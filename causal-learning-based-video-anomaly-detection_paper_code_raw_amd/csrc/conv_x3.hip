@@ -1203,7 +1203,7 @@ int g_dgrad_s2_w3 = 1;
 int g_dgrad_s2_nt = 1;  // knob "conv_dgrad_s2_nt": 1 = 32 input channels per block (default: config-2 layer 4 92 -> 75 us, profiles/r04_s2_nt_ab.json), 0 = 64 where the grid allows
 
 bool conv3_dgrad_w3_wanted(const Conv3Layer& L) {
-  return (g_dgrad_s2_w3 && !g_conv_bf16 && conv3_x3_dgrad_s2_supported(L)) || dgrad_s1_dma_supported(L);
+  return g_dgrad_s2_w3 && !g_conv_bf16 && conv3_x3_dgrad_s2_supported(L);
 }
 
 int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,

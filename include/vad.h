@@ -144,11 +144,6 @@ int vad_set_tuning(const char* key, int value);
 /* weight gradient of the same conv: dW[Co][Ci][3][3] = sum over pixels dY x patches(x); split-K slabs in partial */
 int vad_conv3x3_wgrad(const float* x_nhwc, const float* dy_nhwc, int NF, int Ci, int IH, int IW, int Co, int stride,
                       float* dW, float* partial, int64_t partial_floats, void* stream);
-/* input gradient on pre-split operands (the fused step's path with knobs "conv_dgrad_s1_dma" / "conv_dgrad_s2_dma"):
- * dY split into bf16 planes and the Wd image pre-split in scratch (>= 4*9*Ci*Co + 3*NF*OH*OW*Co/2 + 1024 floats),
- * then the LDS-DMA kernel of that stride.  Bit-identical to vad_conv3x3_dgrad's split-bf16 kernel. */
-int vad_conv3x3_dgrad_planes(const float* dy_nhwc, int NF, int Ci, int IH, int IW, const float* w, int Co, int stride,
-                             float* dx_nhwc, float* scratch, int64_t scratch_floats, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * minicausal_vad_complete3.py — SimpleVideoAnomalyDetector (mc:25-102) + StableTrainer step (mc:249-330)

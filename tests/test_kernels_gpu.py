@@ -194,13 +194,9 @@ WGRAD_CASES = [(2, 32, 32, 19, 17, 1), (32, 256, 256, 8, 8, 1), (32, 128, 256, 1
 
 
 def _wgrad_path(nat, patch):
-    """3: split-bf16 transposed-read kernel for both strides (default, conv_x3w.hip), 5: split-bf16 on pre-split
-    operand planes staged by LDS-DMA (conv_x3d.hip; its supported layers), 4: the older split-bf16 kernels
-    (conv_x3.hip), 1: f32 LDS-patch kernel for stride-1 layers, 2: f32 LDS-patch kernel for all strides, 0:
+    """3: split-bf16 transposed-read kernel for both strides (default, conv_x3w.hip), 4: the
+    older split-bf16 kernels (conv_x3.hip), 1: f32 LDS-patch kernel for stride-1 layers, 2: f32 LDS-patch kernel for all strides, 0:
     implicit-GEMM path."""
-    nat.lib().vad_set_tuning(b"conv_wgrad_dma", 1 if patch == 5 else 0)
-    if patch == 5:
-        patch = 3
     split = patch in (3, 4)
     nat.lib().vad_set_tuning(b"conv_wgrad_patch", 1 if split else patch)
     nat.lib().vad_set_tuning(b"conv_wgrad_split", 1 if split else 0)
@@ -208,7 +204,7 @@ def _wgrad_path(nat, patch):
     nat.lib().vad_set_tuning(b"conv_wgrad_tr", 1 if patch == 3 else 0)
 
 
-@pytest.mark.parametrize("patch", [3, 5, 4, 1, 0, 2])
+@pytest.mark.parametrize("patch", [3, 4, 1, 0, 2])
 @pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", WGRAD_CASES)
 def test_conv3x3_wgrad(NF, Ci, Co, IH, IW, s, patch):
     nat = _lib()
@@ -239,8 +235,7 @@ def test_conv3x3_wgrad(NF, Ci, Co, IH, IW, s, patch):
                                               (8, 32, 64, 57, 57, 2), (6, 64, 128, 29, 29, 2),
                                               (8, 128, 256, 15, 15, 2)])
 def test_conv3x3_wgrad_split_accuracy_matches_f32(NF, Ci, Co, IH, IW, s):
-    """Split-bf16 weight gradients (transposed-read kernel 3, LDS-DMA planes kernel 5, older kernels 4) against an fp64
-    reference: worst error
+    """Split-bf16 weight gradients (transposed-read kernel 3, older kernels 4) against an fp64 reference: worst error
     relative to sum_p |dy||x| of each weight within 2x that of the exact-f32 MFMA kernel (a plain bf16 product would
     sit near 4e-3)."""
     nat = _lib()
@@ -255,7 +250,7 @@ def test_conv3x3_wgrad_split_accuracy_matches_f32(NF, Ci, Co, IH, IW, s):
     dyh = dy.permute(0, 2, 3, 1).contiguous().to(d)
     part = torch.empty(1 << 24, device=d)
     errs = {}
-    for patch in ((1, 3, 4, 5) if s == 1 else (2, 3, 4, 5)):
+    for patch in ((1, 3, 4) if s == 1 else (2, 3, 4)):
         _wgrad_path(nat, patch)
         dW = torch.empty(Co, Ci, 3, 3, device=d)
         nat.check(nat.lib().vad_conv3x3_wgrad(xh.data_ptr(), dyh.data_ptr(), NF, Ci, IH, IW, Co, s, dW.data_ptr(),
@@ -263,7 +258,7 @@ def test_conv3x3_wgrad_split_accuracy_matches_f32(NF, Ci, Co, IH, IW, s):
         torch.cuda.synchronize()
         errs[patch] = float(((dW.cpu().double() - ref).abs() / mag).max())
     _wgrad_path(nat, 3)
-    for k in (3, 4, 5):
+    for k in (3, 4):
         assert errs[k] < 1e-6, errs
         assert errs[k] <= 2.0 * errs[1 if s == 1 else 2] + 1e-8, errs
 
@@ -391,73 +386,3 @@ def test_conv3x3_bf16_native_matches_rounded_fp64(NF, Ci, Co, IH, IW, s):
     finally:
         lib.vad_set_tuning(b"act_bf16", 0)
         lib.vad_set_tuning(b"conv_bf16", 0)
-
-
-@pytest.mark.parametrize("NF,Ci,Co,IH,IW", [(2, 32, 64, 57, 57), (3, 64, 128, 29, 29), (4, 128, 256, 15, 15),
-                                            (2, 64, 128, 31, 18), (3, 32, 64, 20, 9)])
-def test_conv3x3_dgrad_s2_dma_bit_identical(NF, Ci, Co, IH, IW):
-    """Stride-2 input gradient on pre-split dY planes + the pre-split Wd image staged by LDS-DMA (knob
-    conv_dgrad_s2_dma, two class tiles per block, ragged tile pairs included) equals the split-bf16 parity-class kernel
-    bit for bit (same products in the same order), and both match the fp64 reference."""
-    nat = _lib()
-    g = torch.Generator().manual_seed(29 + Ci + IH)
-    w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
-    OH, OW = (IH - 1) // 2 + 1, (IW - 1) // 2 + 1
-    dy = torch.randn(NF, Co, OH, OW, generator=g)
-    ref = torch.nn.grad.conv2d_input((NF, Ci, IH, IW), w.double(), dy.double(), stride=2, padding=1)
-    d = torch.device("cuda")
-    dyh = dy.permute(0, 2, 3, 1).contiguous().to(d)
-    wdev = w.contiguous().to(d)
-    wf = torch.empty(9 * Ci * Co, device=d)
-    wd = torch.empty(9 * Ci * Co, device=d)
-    st = nat.stream_of(d)
-    nat.lib().vad_set_tuning(b"conv_dgrad_s2_x3", 1)
-    dx0 = torch.empty(NF, IH, IW, Ci, device=d)
-    nat.check(nat.lib().vad_conv3x3_dgrad(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, 2, dx0.data_ptr(),
-                                          wf.data_ptr(), wd.data_ptr(), st))
-    scratch = torch.empty(4 * 9 * Ci * Co + 3 * NF * OH * OW * Co // 2 + 4096, device=d)
-    dx1 = torch.full((NF, IH, IW, Ci), float("nan"), device=d)
-    nat.lib().vad_set_tuning(b"conv_dgrad_s2_dma", 1)
-    try:
-        nat.check(nat.lib().vad_conv3x3_dgrad_planes(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, 2,
-                                                     dx1.data_ptr(), scratch.data_ptr(), scratch.numel(), st))
-        torch.cuda.synchronize()
-    finally:
-        nat.lib().vad_set_tuning(b"conv_dgrad_s2_dma", 0)
-    np.testing.assert_array_equal(dx1.cpu().numpy(), dx0.cpu().numpy())
-    np.testing.assert_allclose(dx1.cpu().permute(0, 3, 1, 2).double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
-
-
-@pytest.mark.parametrize("NF,Ci,Co,IH,IW", [(2, 32, 32, 57, 57), (3, 64, 64, 29, 29), (4, 128, 128, 15, 15),
-                                            (5, 256, 256, 8, 8), (2, 32, 64, 13, 40)])
-def test_conv3x3_dgrad_s1_dma_bit_identical(NF, Ci, Co, IH, IW):
-    """Stride-1 input gradient on pre-split dY planes + the pre-split (tap-flipped) Wd image staged by LDS-DMA (knob
-    conv_dgrad_s1_dma; 8x32, 16x16 and 4-frame 8x8 tiles, ragged edges) equals the split-bf16 patch kernel bit for
-    bit and matches the fp64 reference."""
-    nat = _lib()
-    g = torch.Generator().manual_seed(31 + Ci + IH)
-    w = torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5
-    dy = torch.randn(NF, Co, IH, IW, generator=g)
-    ref = torch.nn.grad.conv2d_input((NF, Ci, IH, IW), w.double(), dy.double(), stride=1, padding=1)
-    d = torch.device("cuda")
-    dyh = dy.permute(0, 2, 3, 1).contiguous().to(d)
-    wdev = w.contiguous().to(d)
-    wf = torch.empty(9 * Ci * Co, device=d)
-    wd = torch.empty(9 * Ci * Co, device=d)
-    st = nat.stream_of(d)
-    _conv_path(nat, 3)
-    dx0 = torch.empty(NF, IH, IW, Ci, device=d)
-    nat.check(nat.lib().vad_conv3x3_dgrad(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, 1, dx0.data_ptr(),
-                                          wf.data_ptr(), wd.data_ptr(), st))
-    scratch = torch.empty(4 * 9 * Ci * Co + 3 * NF * IH * IW * Co // 2 + 4096, device=d)
-    dx1 = torch.full((NF, IH, IW, Ci), float("nan"), device=d)
-    nat.lib().vad_set_tuning(b"conv_dgrad_s1_dma", 1)
-    try:
-        nat.check(nat.lib().vad_conv3x3_dgrad_planes(dyh.data_ptr(), NF, Ci, IH, IW, wdev.data_ptr(), Co, 1,
-                                                     dx1.data_ptr(), scratch.data_ptr(), scratch.numel(), st))
-        torch.cuda.synchronize()
-    finally:
-        nat.lib().vad_set_tuning(b"conv_dgrad_s1_dma", 0)
-        _conv_default(nat)
-    np.testing.assert_allclose(dx1.cpu().permute(0, 3, 1, 2).double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
-    np.testing.assert_array_equal(dx1.cpu().numpy(), dx0.cpu().numpy())
