@@ -715,6 +715,94 @@ def ae_cpu(args, r):
                        f"{threads} threads), after 1 warm-up step"}, parity)
 
 
+def a2_flops_per_clip(T, H, W):
+    """Algorithmic FLOPs of one a2 train clip (SURVEY §8d counting: 2 per MAC; backward = 2x forward minus the first
+    conv's input gradient): the three k3 p1 Conv3d (strides (1,2,2), 2, 2; 3 -> 16 -> 32 -> 64 channels, a2:19-21) over
+    their output voxels, fc 4096 -> 16 and the causal-discovery / graph-encoder / predictor Linears (a2:27-101)."""
+    def out(n, s):
+        return (n - 1) // s + 1
+    d1, h1, w1 = T, out(H, 2), out(W, 2)
+    d2, h2, w2 = out(d1, 2), out(h1, 2), out(w1, 2)
+    d3, h3, w3 = out(d2, 2), out(h2, 2), out(w2, 2)
+    c1 = d1 * h1 * w1 * 16 * 3 * 27
+    c2 = d2 * h2 * w2 * 32 * 16 * 27
+    c3 = d3 * h3 * w3 * 64 * 32 * 27
+    lin = 4096 * 16 + 16 * 32 + 32 * 256 + 256 * 128 + 128 * 64 + 80 * 64 + 64 * 1
+    fwd = c1 + c2 + c3 + lin
+    return 2 * (3 * fwd - c1)
+
+
+def run_a2(args, rank, world, local_rank):
+    """a2 (avenue_training_script2.py) ImprovedMiniCausalVAD, SURVEY §8 row a15/a16: one step = the fused
+    train_epoch_improved iteration (a2:218-245: forward, compute_improved_loss, the NaN check's host read of the loss,
+    backward, clip_grad_norm_(0.5), AdamW) on args.batch RGB clips of T x 3x64x64 per rank, already resident in HBM."""
+    import torch
+    from vad_amd import _native as nat
+    from vad_amd.a2 import ImprovedMiniCausalVAD
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    vad = ImprovedMiniCausalVAD(device=dev)
+    B, T = args.batch, args.T
+    # (B, 3, T, H, W): plane (clip, c, t) = keyed-hash u8 / 255 of global plane (clip * 3 + c) * T + t
+    x = torch.empty(B, 3, T, args.H, args.W, device=dev)
+    nat.check(nat.lib().vad_synth_frames(17, 0, rank * B * 3 * T, B * 3 * T, args.H * args.W, 1, x.data_ptr(),
+                                         nat.stream_of(dev)))
+    y = torch.zeros(B, device=dev)
+    for _ in range(args.warmup):
+        vad.train_step(x, y)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss, comps, stepped = vad.train_step(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    xp = x[:4]
+    preds, graphs, _ = vad.evaluate_improved([(xp, y[:4])])
+    probe = {"x": xp.cpu(), "preds": preds, "graphs": graphs,
+             "state": {k: v.detach().cpu().clone() for k, v in vad.model.state_dict().items()}}
+    return dict(elapsed=elapsed, step_ms=1e3 * elapsed / args.steps, loss=loss, stepped=stepped, probe=probe)
+
+
+def a2_cpu(args, r):
+    """CPU leg of the a2 line: the GPU eval predictions / graphs after the timed steps against the oracle's forward on
+    the same weights, and the oracle train step (oracle/a2_oracle.py) timed on a bounded sample."""
+    import numpy as np
+    import torch
+    from oracle import a2_oracle as ao
+    threads = cpu_quota()
+    torch.set_num_threads(threads)
+    params = {k: v.double() for k, v in r["probe"]["state"].items()}
+    s, adj, _ = ao.a2_forward(params, r["probe"]["x"].double(), None, False)
+    parity = {"max_abs_score_diff": float(np.abs(s.numpy().reshape(-1) - r["probe"]["preds"]).max()),
+              "max_abs_adjacency_diff": float(np.abs(adj.numpy() - r["probe"]["graphs"]).max()),
+              "tolerance": 1e-4, "sample": "eval forward of 4 clips after the timed steps (float64 oracle)"}
+    B, T = args.batch, args.T
+    params = {k: v.clone() for k, v in r["probe"]["state"].items()}
+    x = ao.synth_clips(17, 0, 0, B, T, args.H, args.W)
+    state = {}
+    ao.a2_train_step(params, state, x, ao.A2Draws.make(17, 0, 0, B))
+    n, t0 = 0, time.perf_counter()
+    while True:
+        ao.a2_train_step(params, state, x, ao.A2Draws.make(17, n + 1, 0, B))
+        n += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds or n >= 200:
+            break
+    el = time.perf_counter() - t0
+    return ({"value": round(B * n / el, 3), "unit": "clips/s", **host_cpu_info(threads), "kind": "port",
+             "sample": f"{n} train steps of B={B} clips x 3x{T}x{args.H}x{args.W} (oracle/a2_oracle.py a2_train_step, "
+                       f"torch CPU fp32, {threads} threads), after 1 warm-up step"}, parity)
+
+
 def finish(world):
     """N > 1: every rank waits until rank 0 has run the CPU legs (after the timed region), then leaves the group."""
     if world > 1:
@@ -748,11 +836,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="2", choices=("1", "2", "4", "5", "cad1"),
+    ap.add_argument("--config", default="2", choices=("1", "2", "4", "5", "cad1", "a2"),
                     help="BASELINE config: 1 = minicausal StableTrainer epoch over 32 clips T=16 64x64, "
                          "2 = T=16 227x227 fp32 (default), 4 = T=32 256x256 bf16 convs, "
                          "5 = bbox clip scorer, mixed T (inference); cad1 = the causal_anomaly_detection1.py "
-                         "memory autoencoder train step (SURVEY §8f, not a BASELINE config)")
+                         "memory autoencoder train step (SURVEY §8f, not a BASELINE config); a2 = the "
+                         "avenue_training_script2.py ImprovedMiniCausalVAD train step (SURVEY §8 a15/a16)")
     ap.add_argument("--batch", type=int, default=8, help="clips per GPU")
     ap.add_argument("--T", type=int, default=None)
     ap.add_argument("--H", type=int, default=None)
@@ -787,14 +876,14 @@ def main():
         for kv in args.tune:
             k, v = kv.split("=")
             nat.check(nat.lib().vad_set_tuning(k.encode(), int(v)))
-    args.config = args.config if args.config == "cad1" else int(args.config)
+    args.config = args.config if args.config in ("cad1", "a2") else int(args.config)
     preset = {1: (16, 64, 64, "fp32"), 2: (16, 227, 227, "fp32"), 4: (32, 256, 256, "bf16"), 5: (0, 64, 64, "fp32"),
-              "cad1": (16, 64, 64, "fp32")}[args.config]
+              "cad1": (16, 64, 64, "fp32"), "a2": (8, 64, 64, "fp32")}[args.config]
     if args.config == 1 and args.batch == 8:
         args.batch = 32  # clips per epoch per rank (BASELINE config 1)
     if args.config == 5 and args.batch == 8:
         args.batch = 64  # clips per rank
-    if args.config == "cad1" and args.batch == 8:
+    if args.config in ("cad1", "a2") and args.batch == 8:
         args.batch = 32
     args.T = args.T or preset[0]
     args.H = args.H or preset[1]
@@ -858,6 +947,29 @@ def main():
                              "traffic": None,
                              "basis": f"{ae_flops_per_clip(args.T)} algorithmic FLOP per clip x clips / step time"},
                 "cpu_baseline": cpu, "parity": parity, "final_loss": r["loss"], "final_status": r["status"]}),
+                flush=True)
+        finish(world)
+        return
+    if args.config == "a2":
+        r = run_a2(args, rank, world, local_rank)
+        if rank == 0:
+            cpu, parity = (None, None) if args.no_cpu_baseline else a2_cpu(args, r)
+            clips = world * args.batch * args.steps
+            fpc = a2_flops_per_clip(args.T, args.H, args.W)
+            tflops = fpc * args.batch / (r["step_ms"] * 1e-3) / 1e12
+            print(json.dumps({
+                "metric": BASELINE_METRIC, "value": round(clips / r["elapsed"], 3), "unit": "clips/s",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["step_ms"], 4),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+                "data": "synthetic RGB clips (keyed-hash u8 / 255); random-init weights (torch.manual_seed(0))",
+                "config": {"workload": "avenue_training_script2.py ImprovedMiniCausalVAD train step (a2:218-245), "
+                                       "SURVEY §8 a15/a16 (the reference loader's batch is 4: --batch 4)",
+                           "clips_per_gpu": args.batch, "global_batch": world * args.batch, "clip_len": args.T,
+                           "frame": f"3x{args.H}x{args.W}", "parallelism": f"dp{world}"},
+                "roofline": {"bound": "mfma", "kernel": "whole step", "achieved": round(tflops, 3),
+                             "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_FP32_TFLOPS, 4),
+                             "traffic": None, "basis": f"{fpc} algorithmic FLOP per clip x clips / step time"},
+                "cpu_baseline": cpu, "parity": parity, "final_loss": r["loss"], "stepped": r["stepped"]}),
                 flush=True)
         finish(world)
         return

@@ -214,8 +214,9 @@ int dense_fwd_splitk(const float* X, int M, int K, const float* W, int N, float*
 int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX, const float* gate, float gscale,
                 const int* skip, hipStream_t st, int gate_rows = 0);
 // dW = dY^T X, db = colsum(dY) (written, not accumulated)
+// target_blocks: split-K blocks to aim for (256: one per CU; tall-M weight gradients want several per CU to hide latency)
 int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW, float* db, float* scratch,
-                int64_t scratch_floats, const int* skip, hipStream_t st);
+                int64_t scratch_floats, const int* skip, hipStream_t st, int target_blocks = 256);
 
 // conv GEMM tuning knobs: conv_fwd_tile / conv_dgrad_tile / conv_wgrad_tile (tile id, -1 = heuristic),
 // conv_wgrad_blocks, conv_wgrad_min_ktiles

@@ -1789,7 +1789,7 @@ int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX,
 }
 
 int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW, float* db, float* scratch,
-                int64_t scratch_floats, const int* skip, hipStream_t st) {
+                int64_t scratch_floats, const int* skip, hipStream_t st, int target_blocks) {
   // GEMM rows = out feature n, cols = in feature k (+ ones column for the bias), reduction over m
   using C = T64x64;
   if (skinny_ok(M, K)) {
@@ -1802,7 +1802,7 @@ int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW,
   DenseKM<C::BM>::Params pa{dY, N, N, M, -1};
   DenseKM<C::BN>::Params pb{X, K, K, M, K};
   const int tiles = (int)(cdiv(N, C::BM) * cdiv(GN, C::BN));
-  int splits = (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(256, tiles)), cdiv(M, 4 * BK));
+  int splits = (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(target_blocks, tiles)), cdiv(M, 4 * BK));
   while (splits > 1 && (int64_t)splits * N * GN > scratch_floats) splits /= 2;
   VAD_CHECK((int64_t)N * GN <= scratch_floats, "dense_wgrad: scratch too small");
   EpiPartial::Params pp{scratch, GN};

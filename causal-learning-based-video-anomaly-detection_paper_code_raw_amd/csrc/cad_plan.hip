@@ -1420,6 +1420,11 @@ int vad_cad_debug_buffer(vad_cad_plan* plan, const char* name, int idx, void** p
   else if (n == "d_pooled") { *ptr = c.d_pooled; *nfloats = (int64_t)c.B * 6144; }
   else if (n == "d_feat_det") { *ptr = c.d_feat_det; *nfloats = NF * 6144; }
   else if (n == "det_logits") { *ptr = c.dlog; *nfloats = NF * 20; }
+  else if (n == "dir_h" && idx >= 0 && idx < 4) {  // direct classifier hidden layer idx (post ReLU / dropout)
+    const int w[4] = {512, 256, 128, 64};
+    *ptr = c.gh[idx];
+    *nfloats = (int64_t)c.B * w[idx];
+  }
   else if (n == "bn_sync") { *ptr = c.bnsync; *nfloats = 2 * 2 * 256; }  // double [2*256]: 1024 float words
   else { vad::set_error("vad_cad_debug_buffer: unknown buffer " + n); return 1; }
   VAD_CHECK(*ptr != nullptr || n == "act_bf16", "vad_cad_debug_buffer: " + n + " is not carved under this plan's options");

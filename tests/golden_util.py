@@ -153,14 +153,16 @@ def reshape_masks(masks, x):
     return [m.reshape(NF, m.shape[1], hh, ww) for m, (hh, ww) in zip(masks, shapes)]
 
 
-def pinned_oracle_grads(state_dict, x, labels, draws, masks, sync_group=None, bf16=False, dtype=torch.float64):
+def pinned_oracle_grads(state_dict, x, labels, draws, masks, sync_group=None, bf16=False, dtype=torch.float64,
+                        head_masks=None):
     """float64 oracle forward/backward of one train step with the ReLU decisions of another forward (masks from
     hip_relu_masks): the exact gradient of that forward's piecewise-linear branch, free of kink flips.  Returns
     (grads {name: float64 tensor or None}, losses {name: float64}, the oracle's result dict incl. "bufs" and
     "record" -- the float64 BatchNorm outputs "z{l}" in front of each pinned ReLU, for check_mask_flips).
     bf16: the backbone as the device computes it in bf16 mode (cad_oracle.backbone_forward_bf16; "reversed": its convs
     sum the input channels in reverse order).  dtype: the oracle's arithmetic (float64; float32 gives further,
-    independent restatements at fp32 accumulation)."""
+    independent restatements at fp32 accumulation).  head_masks: the direct classifier's ReLU decisions too
+    (cad_oracle.direct_forward's masks; its pre-activations land in record["dir_z{i}"])."""
     from oracle import cad_oracle as co
     params = {k: v.detach().to(dtype).clone() for k, v in state_dict.items()
               if "running" not in k and "num_batches" not in k}
@@ -169,6 +171,8 @@ def pinned_oracle_grads(state_dict, x, labels, draws, masks, sync_group=None, bf
     rm = reshape_masks(masks, xd)
     record = {}
     kw = dict(bf16=bf16) if bf16 else {}
+    if head_masks is not None:
+        kw["head_masks"] = head_masks
     res = co.cad_train_step(params, bufs, {}, xd, labels, draws, relu_masks=rm, sync_group=sync_group,
                             record=record, **kw)
     res["bufs"] = bufs  # running stats after the step's forward

@@ -53,3 +53,31 @@ def test_restatement_with_rounding_stays_near_the_exact_step(monkeypatch):
     d = float((emu["out"]["anomaly_scores"] - exact["out"]["anomaly_scores"]).detach().abs().max())
     assert 0 < d < 1e-2
     assert abs(float(emu["losses"]["total"]) / float(exact["losses"]["total"]) - 1) < 1e-2
+
+
+def test_head_masks_of_its_own_decisions_change_nothing():
+    """direct_forward(masks=...) pinned to the oracle's own direct-classifier ReLU decisions is the unpinned step."""
+    sd = make_cad_model(CASE).state_dict()
+    B, T, H, W = CASE["B"], CASE["T"], CASE["H"], CASE["W"]
+    x = co.synth_clips(4, 1, 0, B, T, H, W).double()
+    y = co.synth_labels(0, B)
+
+    def run(**kw):
+        params = {k: v.detach().double().clone() for k, v in sd.items()
+                  if "running" not in k and "num_batches" not in k}
+        for k in list(params):
+            if k.startswith(co.FROZEN_PREFIXES):
+                params[k].requires_grad_(False)
+        bufs = {k: v.detach().double().clone() for k, v in sd.items() if "running" in k}
+        rec = {}
+        res = co.cad_train_step(params, bufs, {}, x, y, co.CadDraws.make(4, 1, 0, B, T), record=rec, **kw)
+        return res, rec
+
+    free, rec = run()
+    pinned, _ = run(head_masks=[rec[f"dir_z{i}"] > 0 for i in range(4)])
+    for n, g in free["grads"].items():
+        if g is None:
+            assert pinned["grads"][n] is None, n
+            continue
+        np.testing.assert_allclose(pinned["grads"][n].detach().numpy(), g.detach().numpy(), rtol=1e-12, atol=1e-15,
+                                   err_msg=n)
