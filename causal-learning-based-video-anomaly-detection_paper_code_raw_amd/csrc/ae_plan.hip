@@ -6,19 +6,23 @@
 // per group t, a contiguous row range in this order.  The decoder is called T times on the same sequence feature
 // (decode_sequence, cad1:254-258); the calls are identical, so it runs once per clip and only its BN running
 // statistics take the T updates.
-//   encoder   4 x [im2col (4x4, s2, p1) -> f32 MFMA GEMM (torch weight [Co][Ci*16] as is) -> per-t BN partial sums
+//   encoder   4 x [Conv2d(4, s2, p1) as an implicit f32 MFMA GEMM over the NHWC frames (backbone.hip conv4_fwd; the
+//             first, 1-channel layer as im2col + GEMM, K = 16) -> per-t BN partial sums
 //             -> grouped finalize (running stats updated once per t, in t order) -> BN + LeakyReLU(0.1); layer 4
 //             straight into the NCHW flatten order] -> Linear(2048, 64) GEMM -> tanh, NaN -> 0
 //   LSTM      input projection of all B*T frames as one GEMM; the recurrence one block per clip with the W_hh rows
 //             in registers and h broadcast from LDS; gates, cell states and h_{t-1} kept for BPTT
-//   decoder   Linear(64, 2048) GEMM -> LeakyReLU into NHWC -> 3 x [ConvTranspose2d as the GEMM X Wt (torch weight
-//             [Ci][Co*16] as is) + col2im with bias -> BN + LeakyReLU] -> ConvTranspose2d(32, 1) -> sigmoid
+//   decoder   Linear(64, 2048) GEMM -> LeakyReLU into NHWC -> 3 x [ConvTranspose2d as four parity-class implicit
+//             GEMMs with the bias in the epilogue (conv4_cls) -> BN + LeakyReLU] -> ConvTranspose2d(32, 1) -> sigmoid
 //   loss      MSE of the T identical reconstructions against the T frames (cad1:340-344) and d MSE / d logits in
 //             one pass; per-clip errors (cad1:545-546)
 //   memory    cosine min-distance to the ring (cad1:262-301), then the ring update (cad1:201-219), both on the
 //             device-resident memory_ptr
-//   backward  mirror image: transposed-conv input grads as convs (im2col of dY x Wt^T), weight grads as GEMMs over
-//             kept columns, grouped BN backward through the LeakyReLU, BPTT one block per clip
+//   backward  mirror image: Conv2d input grads as parity-class GEMMs over dY, ConvTranspose2d input grads as the
+//             16-tap gather over dY, weight grads as split-K correlations of the two operands (conv4_wgrad; the
+//             1-channel ends -- encoder layer 0's weight grad, the last ConvTranspose2d's grads -- over im2col
+//             columns), grouped BN backward through the LeakyReLU, BPTT one block per clip
+// (knob "ae_direct" = 0 at plan creation: every conv on im2col / col2im columns + dense GEMMs, the round-4 path)
 //   update    non-finite-grad skip + clip_grad_norm_(0.1) + Adam with coupled L2 (optim.h)
 // Status word (losses[3]): 0 = skipped before backward (train-loop mode: a non-finite input, cad1:385-387 -- the BN
 // running stats, counters and the memory ring stay untouched, as the reference's `continue` before the forward -- or
@@ -36,6 +40,8 @@
 
 namespace vad {
 
+int g_ae_direct = 1;  // knob "ae_direct" (latched per plan)
+
 constexpr int AE_HW = 64;  // frame side: the encoder's Linear(128 * 4 * 4) fixes 64x64 frames (cad1:151)
 constexpr int AE_PIX = AE_HW * AE_HW;
 constexpr int AE_CHUNKS = AE_PIX / 256;
@@ -46,6 +52,8 @@ constexpr int AE_MEM = 500;  // memory_size (cad1:191-193)
 constexpr float AE_SLOPE = 0.1f;
 constexpr int AE_ST = 8;  // floats per channel of one BN group's stats block
 constexpr int AE_NBN = 7;
+int g_ae_wgrad_blocks = 1024;  // knob "ae_wgrad_blocks": split-K target grid of the implicit-GEMM weight gradients
+                               // (sweep: 1024 3.149, 2048 3.206, 4096 3.202 ms, profiles/r05_cad1_direct.json)
 constexpr int ENC_CI[4] = {1, 32, 64, 128}, ENC_CO[4] = {32, 64, 128, 128}, ENC_IN[4] = {64, 32, 16, 8};
 constexpr int DEC_CI[4] = {128, 128, 64, 32}, DEC_CO[4] = {128, 64, 32, 1}, DEC_IN[4] = {4, 8, 16, 32};
 
@@ -206,52 +214,61 @@ __global__ __launch_bounds__(256) void gbn_partials_kernel(const float* __restri
 
 // batch statistics per group (double combine); running stats updated `repeat` times per group, in group order
 // (momentum 0.1, unbiased variance), not at all when *skip; eval mode normalises with the running stats
+// BN group sums of one channel: 16 lanes per group (groups g0 .. g0 + 15 per pass), each lane adding the partial rows
+// p = lane, lane + 16, ... in order, then a fixed xor butterfly over the 16 lanes (double)
+__device__ inline double gbn_sum16(double v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
+  return v;
+}
+
 __global__ __launch_bounds__(256) void gbn_finalize_kernel(const float* __restrict__ parts, Gbn q,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, float* running_mean,
                                                            float* running_var, int training, int repeat,
                                                            const int* skip, float* __restrict__ stats) {
-  const int c = blockIdx.x, C = q.C;
-  __shared__ double red[2][256];
+  const int c = blockIdx.x, C = q.C, lane = threadIdx.x & 15, gl = threadIdx.x >> 4;
+  __shared__ double red[2][16];
   const double count = (double)q.Mg, mom = 0.1;
   const bool upd = training && !(skip && *skip);
   float rm = running_mean[c], rv = running_var[c];
-  for (int g = 0; g < q.G; ++g) {
+  for (int g0 = 0; g0 < q.G; g0 += 16) {
+    const int g = g0 + gl;
     double a = 0.0, b = 0.0;
-    if (training)
-      for (int p = threadIdx.x; p < q.P; p += 256) {
+    if (training && g < q.G)
+      for (int p = lane; p < q.P; p += 16) {
         const float* pp = parts + ((int64_t)g * q.P + p) * 2 * C;
         a += (double)pp[c];
         b += (double)pp[C + c];
       }
-    red[0][threadIdx.x] = a;
-    red[1][threadIdx.x] = b;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if (threadIdx.x < s) {
-        red[0][threadIdx.x] += red[0][threadIdx.x + s];
-        red[1][threadIdx.x] += red[1][threadIdx.x + s];
-      }
-      __syncthreads();
+    a = gbn_sum16(a);
+    b = gbn_sum16(b);
+    if (lane == 0) {
+      red[0][gl] = a;
+      red[1][gl] = b;
     }
+    __syncthreads();
     if (threadIdx.x == 0) {
-      double mean = rm, var = rv;
-      if (training) {
-        mean = red[0][0] / count;
-        var = red[1][0] / count - mean * mean;
-        if (var < 0) var = 0;
-        if (upd)
-          for (int k = 0; k < repeat; ++k) {
-            rm = (float)((1.0 - mom) * rm + mom * mean);
-            rv = (float)((1.0 - mom) * rv + mom * var * count / (count - 1.0));
-          }
+      // (running stats updated once per group, in group order)
+      for (int k = 0; k < 16 && g0 + k < q.G; ++k) {
+        double mean = rm, var = rv;
+        if (training) {
+          mean = red[0][k] / count;
+          var = red[1][k] / count - mean * mean;
+          if (var < 0) var = 0;
+          if (upd)
+            for (int r = 0; r < repeat; ++r) {
+              rm = (float)((1.0 - mom) * rm + mom * mean);
+              rv = (float)((1.0 - mom) * rv + mom * var * count / (count - 1.0));
+            }
+        }
+        const double invstd = 1.0 / sqrt(var + 1e-5), scale = (double)gamma[c] * invstd;
+        float* s = stats + (int64_t)(g0 + k) * AE_ST * C;
+        s[c] = (float)mean;
+        s[C + c] = (float)invstd;
+        s[2 * C + c] = (float)scale;
+        s[3 * C + c] = (float)((double)beta[c] - mean * scale);
       }
-      const double invstd = 1.0 / sqrt(var + 1e-5), scale = (double)gamma[c] * invstd;
-      float* s = stats + (int64_t)g * AE_ST * C;
-      s[c] = (float)mean;
-      s[C + c] = (float)invstd;
-      s[2 * C + c] = (float)scale;
-      s[3 * C + c] = (float)((double)beta[c] - mean * scale);
     }
     __syncthreads();
   }
@@ -319,36 +336,36 @@ __global__ __launch_bounds__(256) void gbn_bwd_finalize_kernel(const float* __re
                                                                const float* __restrict__ gamma, int training,
                                                                float* __restrict__ stats, float* dgamma,
                                                                float* dbeta) {
-  const int c = blockIdx.x, C = q.C;
-  __shared__ double red[2][256];
+  const int c = blockIdx.x, C = q.C, lane = threadIdx.x & 15, gl = threadIdx.x >> 4;
+  __shared__ double red[2][16];
   const double count = (double)q.Mg;
   double tz = 0.0, tzx = 0.0;
-  for (int g = 0; g < q.G; ++g) {
+  for (int g0 = 0; g0 < q.G; g0 += 16) {
+    const int g = g0 + gl;
     double a = 0.0, b = 0.0;
-    for (int p = threadIdx.x; p < q.P; p += 256) {
-      const float* pp = parts + ((int64_t)g * q.P + p) * 2 * C;
-      a += (double)pp[c];
-      b += (double)pp[C + c];
-    }
-    red[0][threadIdx.x] = a;
-    red[1][threadIdx.x] = b;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if (threadIdx.x < s) {
-        red[0][threadIdx.x] += red[0][threadIdx.x + s];
-        red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    if (g < q.G)
+      for (int p = lane; p < q.P; p += 16) {
+        const float* pp = parts + ((int64_t)g * q.P + p) * 2 * C;
+        a += (double)pp[c];
+        b += (double)pp[C + c];
       }
-      __syncthreads();
+    a = gbn_sum16(a);
+    b = gbn_sum16(b);
+    if (lane == 0) {
+      red[0][gl] = a;
+      red[1][gl] = b;
     }
-    if (threadIdx.x == 0) {
-      float* s = stats + (int64_t)g * AE_ST * C;
-      s[4 * C + c] = gamma[c] * s[C + c];
-      // eval mode: BN is the affine map of the running stats, no batch-mean terms in its backward
-      s[5 * C + c] = training ? (float)(red[0][0] / count) : 0.f;
-      s[6 * C + c] = training ? (float)(red[1][0] / count) : 0.f;
-      tz += red[0][0];
-      tzx += red[1][0];
-    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int k = 0; k < 16 && g0 + k < q.G; ++k) {
+        float* s = stats + (int64_t)(g0 + k) * AE_ST * C;
+        s[4 * C + c] = gamma[c] * s[C + c];
+        // eval mode: BN is the affine map of the running stats, no batch-mean terms in its backward
+        s[5 * C + c] = training ? (float)(red[0][k] / count) : 0.f;
+        s[6 * C + c] = training ? (float)(red[1][k] / count) : 0.f;
+        tz += red[0][k];
+        tzx += red[1][k];
+      }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
@@ -388,13 +405,21 @@ __global__ __launch_bounds__(256) void gbn_bwd_apply_kernel(const float* __restr
   if (bparts) ae_block_store(v, C, bparts + ((int64_t)blockIdx.y * q.P + blockIdx.x) * 2 * C);
 }
 
-// db[c] = sum over blocks of parts[blk][c] (the first half of each block's [2][C] record), fixed order
-__global__ void ae_bias_reduce_kernel(const float* __restrict__ parts, int nblk, int C, float* __restrict__ db) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// db[c] = sum over blocks of parts[blk][c] (the first half of each block's [2][C] record): one block per channel,
+// thread t adding blocks t, t + 256, ... in order, then a fixed tree (double)
+__global__ __launch_bounds__(256) void ae_bias_reduce_kernel(const float* __restrict__ parts, int nblk, int C,
+                                                             float* __restrict__ db) {
+  const int c = blockIdx.x;
+  __shared__ double red[256];
   double s = 0.0;
-  for (int i = 0; i < nblk; ++i) s += (double)parts[(int64_t)i * 2 * C + c];
-  db[c] = (float)s;
+  for (int i = threadIdx.x; i < nblk; i += 256) s += (double)parts[(int64_t)i * 2 * C + c];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) db[c] = (float)red[0];
 }
 
 // out[0] = sum of x[0, n) (one block, fixed order): the bias grad of the single-channel last ConvTranspose2d
@@ -749,6 +774,10 @@ struct AePlanImpl {
   float *xf, *ecols[4], *ey[4], *ea[4], *est[4], *z, *lat, *gx, *gates, *cs, *hprev, *seq;
   float *u, *dx[4], *dy[4], *dst[3], *dylast, *parts, *bparts, *lpart, *losses, *bufA, *bufB, *bcols;
   float *dG, *dlat, *dz, *da3, *dseq, *dU, *scratch;
+  // implicit-GEMM weight images (conv4_prep): encoder layers 1-3 [Co][16 Ci] (forward) / [4][Ci][4 Co] (input grad),
+  // decoder layers [4][Co][4 Ci] (forward) / [Ci][16 Co] (input grad, layers 0-2)
+  float *ewk[4] = {}, *ewc[4] = {}, *dwk[4] = {}, *dwc[4] = {};
+  const int direct = g_ae_direct;
   int* bad;
   double* sum_parts;
   AdamWs aws{};
@@ -773,12 +802,16 @@ struct AePlanImpl {
     xf = w.take<float>((int64_t)NF * AE_PIX);
     for (int l = 0; l < 4; ++l) {
       const int64_t M = ge[l].rows(), Co = ENC_CO[l];
-      ecols[l] = w.take<float>(M * ge[l].K());
+      ecols[l] = (direct && l > 0) ? nullptr : w.take<float>(M * ge[l].K());
       ey[l] = w.take<float>(M * Co);
       ea[l] = w.take<float>(M * Co);
       est[l] = w.take<float>((int64_t)T * AE_ST * Co);
       max_act = std::max(max_act, M * Co);
-      if (l > 0) max_cols = std::max(max_cols, M * ge[l].K());
+      if (l > 0 && !direct) max_cols = std::max(max_cols, M * ge[l].K());
+      if (direct && l > 0) {
+        ewk[l] = w.take<float>(16 * Co * ENC_CI[l]);
+        ewc[l] = w.take<float>(16 * Co * ENC_CI[l]);
+      }
       max_parts = std::max(max_parts, parts_of(enc_bn(l)));
     }
     z = w.take<float>((int64_t)NF * AE_LAT);
@@ -794,7 +827,11 @@ struct AePlanImpl {
       dx[j] = w.take<float>(rows * DEC_CI[j]);
       dy[j] = w.take<float>(gd[j].in.numel());
       max_act = std::max(max_act, std::max(gd[j].in.numel(), rows * DEC_CI[j]));
-      max_cols = std::max(max_cols, rows * gd[j].K());
+      if (!direct || j == 3) max_cols = std::max(max_cols, rows * gd[j].K());
+      if (direct) {
+        dwc[j] = w.take<float>(16 * DEC_CI[j] * DEC_CO[j]);
+        dwk[j] = j < 3 ? w.take<float>(16 * DEC_CI[j] * DEC_CO[j]) : nullptr;
+      }
       if (j < 3) {
         dst[j] = w.take<float>((int64_t)AE_ST * DEC_CO[j]);
         max_parts = std::max(max_parts, parts_of(dec_bn(j)));
@@ -814,7 +851,7 @@ struct AePlanImpl {
     da3 = w.take<float>((int64_t)NF * AE_FLAT);
     dseq = w.take<float>((int64_t)B * AE_LAT);
     dU = w.take<float>((int64_t)B * AE_FLAT);
-    scratch_floats = 8ll << 20;
+    scratch_floats = 32ll << 20;  // (split-K slabs of the weight gradients: 128 MB)
     scratch = w.take<float>(scratch_floats);
     bad = w.take<int>(4);
     aws.sq = w.take<double>(ADAM_MAX_SLOTS * ADAM_SQ_CHUNKS);
@@ -852,7 +889,7 @@ struct AePlanImpl {
                        dbias ? bparts : nullptr);
     VAD_LAUNCH_CHECK();
     if (dbias) {
-      hipLaunchKernelGGL(ae_bias_reduce_kernel, dim3((unsigned)cdiv(q.C, 256)), dim3(256), 0, st, bparts, q.G * q.P,
+      hipLaunchKernelGGL(ae_bias_reduce_kernel, dim3((unsigned)q.C), dim3(256), 0, st, bparts, q.G * q.P,
                          q.C, dbias);
       VAD_LAUNCH_CHECK();
     }
@@ -869,11 +906,19 @@ struct AePlanImpl {
     if (enc) {
       hipLaunchKernelGGL(ae_frames_kernel, grid_for((int64_t)NF * AE_PIX / 4), dim3(256), 0, st, x, B, T, xf, bad);
       VAD_LAUNCH_CHECK();
+      if (direct)
+        for (int l = 1; l < 4; ++l) VAD_TRY(conv4_prep(P(L.enc_w[l]), ENC_CO[l], ENC_CI[l], ewk[l], ewc[l], st));
       for (int l = 0; l < 4; ++l) {
         const int64_t M = ge[l].rows();
-        VAD_TRY(im2col3d(l == 0 ? xf : ea[l - 1], ndhwc_strides(ge[l].in), ge[l], nullptr, nullptr, 0, ecols[l], st));
-        VAD_TRY(dense_fwd(ecols[l], (int)M, ge[l].K(), P(L.enc_w[l]), P(L.enc_b[l]), ENC_CO[l], ey[l], none, scratch,
-                          scratch_floats, st));
+        if (direct && l > 0) {
+          VAD_TRY(conv4_fwd(ea[l - 1], NF, ENC_IN[l], ENC_IN[l], ENC_CI[l], ewk[l], P(L.enc_b[l]), ENC_CO[l], ey[l],
+                            st));
+        } else {
+          VAD_TRY(im2col3d(l == 0 ? xf : ea[l - 1], ndhwc_strides(ge[l].in), ge[l], nullptr, nullptr, 0, ecols[l],
+                           st));
+          VAD_TRY(dense_fwd(ecols[l], (int)M, ge[l].K(), P(L.enc_w[l]), P(L.enc_b[l]), ENC_CO[l], ey[l], none,
+                            scratch, scratch_floats, st));
+        }
         VAD_TRY(bn_fwd(ey[l], enc_bn(l), L.ebn_w[l], L.ebn_b[l], L.erm[l], L.erv[l], 1, skip, est[l], ea[l],
                        l == 3 ? 16 : 0, st));
       }
@@ -897,11 +942,17 @@ struct AePlanImpl {
       VAD_TRY(dense_fwd(seq, B, AE_LAT, P(L.dfc_w), P(L.dfc_b), AE_FLAT, u, none, scratch, scratch_floats, st));
       hipLaunchKernelGGL(ae_dec_in_kernel, grid_for((int64_t)B * AE_FLAT), dim3(256), 0, st, u, B, dx[0]);
       VAD_LAUNCH_CHECK();
+      if (direct)
+        for (int j = 0; j < 4; ++j) VAD_TRY(conv4_prep(P(L.dec_w[j]), DEC_CI[j], DEC_CO[j], dwk[j], dwc[j], st));
       for (int j = 0; j < 4; ++j) {
-        // ConvTranspose2d j: columns = X_j Wt (the transposed conv's GEMM), col2im + bias
-        VAD_TRY(dense_dgrad(dx[j], (int)gd[j].rows(), DEC_CI[j], P(L.dec_w[j]), gd[j].K(), bcols, nullptr, 1.f,
-                            nullptr, st));
-        VAD_TRY(col2im3d(bcols, gd[j], dy[j], st, P(L.dec_b[j])));
+        if (direct) {  // ConvTranspose2d j: four parity-class GEMMs, bias in the epilogue
+          VAD_TRY(conv4_cls(dx[j], B, DEC_IN[j], DEC_IN[j], DEC_CI[j], dwc[j], P(L.dec_b[j]), DEC_CO[j], dy[j], st));
+        } else {
+          // columns = X_j Wt (the transposed conv's GEMM), col2im + bias
+          VAD_TRY(dense_dgrad(dx[j], (int)gd[j].rows(), DEC_CI[j], P(L.dec_w[j]), gd[j].K(), bcols, nullptr, 1.f,
+                              nullptr, st));
+          VAD_TRY(col2im3d(bcols, gd[j], dy[j], st, P(L.dec_b[j])));
+        }
         if (j < 3)
           VAD_TRY(bn_fwd(dy[j], dec_bn(j), L.dbn_w[j], L.dbn_b[j], L.drm[j], L.drv[j], T, skip, dst[j], dx[j + 1], 0,
                          st));
@@ -947,9 +998,17 @@ struct AePlanImpl {
     const float* dcur = dylast;
     for (int j = 3; j >= 0; --j) {
       const int M = (int)gd[j].rows(), K = gd[j].K(), Ci = DEC_CI[j];
-      VAD_TRY(im2col3d(dcur, ndhwc_strides(gd[j].in), gd[j], nullptr, nullptr, 0, bcols, st));
-      VAD_TRY(dense_wgrad(dx[j], M, Ci, bcols, K, G(L.dec_w[j]), nullptr, scratch, scratch_floats, nullptr, st));
-      VAD_TRY(dense_fwd(bcols, M, K, P(L.dec_w[j]), nullptr, Ci, bufA, none, scratch, scratch_floats, st));
+      if (direct && j < 3) {
+        int ns = 0;
+        VAD_TRY(conv4_wgrad(dx[j], Ci, dcur, DEC_CO[j], B, DEC_IN[j], DEC_IN[j], scratch, &ns, scratch_floats,
+                            g_ae_wgrad_blocks, st));
+        VAD_TRY(conv4_wgrad_reduce(scratch, ns, Ci, DEC_CO[j], G(L.dec_w[j]), st));
+        VAD_TRY(conv4_fwd(dcur, B, 2 * DEC_IN[j], 2 * DEC_IN[j], DEC_CO[j], dwk[j], nullptr, Ci, bufA, st));
+      } else {
+        VAD_TRY(im2col3d(dcur, ndhwc_strides(gd[j].in), gd[j], nullptr, nullptr, 0, bcols, st));
+        VAD_TRY(dense_wgrad(dx[j], M, Ci, bcols, K, G(L.dec_w[j]), nullptr, scratch, scratch_floats, nullptr, st));
+        VAD_TRY(dense_fwd(bcols, M, K, P(L.dec_w[j]), nullptr, Ci, bufA, none, scratch, scratch_floats, st));
+      }
       if (j > 0) {
         // X_j = LeakyReLU(BN_{j-1}(y_{j-1})); sum(dY_{j-1}) is the bias grad of ConvTranspose2d j-1
         VAD_TRY(bn_bwd(bufA, dy[j - 1], dec_bn(j - 1), L.dbn_w[j - 1], L.dbn_b[j - 1], dst[j - 1], bufB,
@@ -983,6 +1042,16 @@ struct AePlanImpl {
     // encoder, last layer first
     for (int l = 3; l >= 0; --l) {
       const int M = (int)ge[l].rows(), K = ge[l].K(), Co = ENC_CO[l];
+      if (direct && l > 0) {  // (the conv bias grad = sum of dY, from the BN backward's apply pass)
+        const int OH = ENC_IN[l] / 2;
+        int ns = 0;
+        VAD_TRY(bn_bwd(bufA, ey[l], enc_bn(l), L.ebn_w[l], L.ebn_b[l], est[l], bufB, G(L.enc_b[l]), st));
+        VAD_TRY(conv4_wgrad(bufB, Co, ea[l - 1], ENC_CI[l], NF, OH, OH, scratch, &ns, scratch_floats,
+                            g_ae_wgrad_blocks, st));
+        VAD_TRY(conv4_wgrad_reduce(scratch, ns, Co, ENC_CI[l], G(L.enc_w[l]), st));
+        VAD_TRY(conv4_cls(bufB, NF, OH, OH, Co, ewc[l], nullptr, ENC_CI[l], bufA, st));
+        continue;
+      }
       VAD_TRY(bn_bwd(bufA, ey[l], enc_bn(l), L.ebn_w[l], L.ebn_b[l], est[l], bufB, nullptr, st));
       VAD_TRY(dense_wgrad(bufB, M, Co, ecols[l], K, G(L.enc_w[l]), G(L.enc_b[l]), scratch, scratch_floats, nullptr,
                           st));

@@ -218,6 +218,17 @@ int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX,
 int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW, float* db, float* scratch,
                 int64_t scratch_floats, const int* skip, hipStream_t st, int target_blocks = 256);
 
+// ---------------------------------------------------------------- 4x4 / stride-2 / pad-1 convs (cad1's autoencoder)
+// implicit GEMMs over NHWC frames, no im2col (backbone.hip: the layouts and the parity classes)
+int conv4_prep(const float* w, int D0, int D1, float* wk, float* wc, hipStream_t st);  // wk / wc nullable
+int conv4_fwd(const float* src, int NF, int H, int W, int C, const float* wk, const float* bias, int N, float* out,
+              hipStream_t st);
+int conv4_cls(const float* src, int NF, int SH, int SW, int C, const float* wc, const float* bias, int N, float* out,
+              hipStream_t st);
+int conv4_wgrad(const float* A, int R, const float* src, int C, int NF, int AH, int AW, float* part, int* nsplit,
+                int64_t part_cap, int target_blocks, hipStream_t st);
+int conv4_wgrad_reduce(const float* part, int S, int R, int C, float* dW, hipStream_t st);
+
 // conv GEMM tuning knobs: conv_fwd_tile / conv_dgrad_tile / conv_wgrad_tile (tile id, -1 = heuristic),
 // conv_wgrad_blocks, conv_wgrad_min_ktiles
 int set_tuning(const char* key, int value);

@@ -919,9 +919,9 @@ struct EpiConvFwd {  // y = acc + bias (NHWC rows), plus per-block BN partial su
   }
 };
 
-struct EpiConvDgrad {  // scatter rows of a (parity-class) grid back to the full NHWC input gradient
+struct EpiConvDgrad {  // scatter rows of a (parity-class) grid back to the full NHWC input gradient (+ bias)
   static constexpr int SCRATCH = 0;
-  struct Params { float* dst; int GA, GB, ra, pa, rb, pb, DH, DW, C; };
+  struct Params { float* dst; int GA, GB, ra, pa, rb, pb, DH, DW, C; const float* bias; };
   template <class Cfg>
   static __device__ void apply(const Params& P, f32x16 (&acc)[Cfg::TM][Cfg::TN], int m0, int n0, int wm, int wn,
                                int lane, int M, int N, float*) {
@@ -938,7 +938,7 @@ struct EpiConvDgrad {  // scatter rows of a (parity-class) grid back to the full
 #pragma unroll
         for (int j = 0; j < Cfg::TN; ++j) {
           const int col = n0 + acc_col<Cfg>(wn, j, lane);
-          if (col < N) P.dst[base + col] = acc[i][j][r];
+          if (col < N) P.dst[base + col] = acc[i][j][r] + (P.bias ? P.bias[col] : 0.f);
         }
       }
   }
@@ -1091,6 +1091,7 @@ struct ConvTuning {
 static ConvTuning g_tune;
 
 extern int g_bbox_im2col;  // bbox_plan.hip
+extern int g_ae_direct, g_ae_wgrad_blocks;  // ae_plan.hip
 int set_tuning(const char* key, int value) {
   const std::string k(key);
   if (k == "conv_fwd_tile") g_tune.fwd = value;
@@ -1116,6 +1117,8 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_split_big") g_x3_big = value;
   else if (k == "conv_split_s2big") g_x3_s2big = value;
   else if (k == "bbox_im2col") g_bbox_im2col = value;
+  else if (k == "ae_direct") g_ae_direct = value;
+  else if (k == "ae_wgrad_blocks") g_ae_wgrad_blocks = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "cad_dir_affine") g_cad_dir_affine = value;
@@ -1811,6 +1814,121 @@ int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW,
   const int64_t total = (int64_t)N * GN;
   hipLaunchKernelGGL(dense_wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 2048)), dim3(256),
                      0, st, scratch, used, N, K, dW, db, skip);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+// =====================================================================================================
+// Conv2d(kernel 4, stride 2, padding 1) and ConvTranspose2d(4, 2, 1) as implicit GEMMs over NHWC frames (cad1's
+// VideoAutoEncoder, causal_anomaly_detection1.py:129-188): the im2col / col2im columns are never written.
+//   conv4_fwd   out[p][n] = sum_{tap, c} src[2a - 1 + ky][2b - 1 + kx][c] wk[n][tap C + c] (+ bias): the 16-tap
+//               gather (Conv2d forward; ConvTranspose2d input gradient with src = dY)
+//   conv4_cls   the transposed direction, one GEMM per output parity class (py, px): rows 2a + py take ky in {1, 3}
+//               (py = 0: source rows a, a - 1) or {0, 2} (py = 1: source rows a + 1, a), 2 x 2 taps scattered to
+//               (2a + py, 2b + px) (+ bias) (Conv2d input gradient with src = dY; ConvTranspose2d forward)
+//   conv4_wgrad the correlation sum over A's pixels p of A[p][r] src[2a - 1 + ky][2b - 1 + kx][c] into split-K slabs
+//               [S][R][16 C] (Conv2d: A = dY, src = X; ConvTranspose2d: A = X, src = dY), summed by
+//               conv4_wgrad_reduce into torch's [R][C][4][4] (Conv2d [Co][Ci], ConvTranspose2d [Ci][Co])
+// =====================================================================================================
+__global__ __launch_bounds__(256) void conv4_prep_kernel(const float* __restrict__ w, int D0, int D1,
+                                                         float* __restrict__ wk, float* __restrict__ wc) {
+  const int64_t total = (int64_t)D0 * D1 * 16;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int tap = (int)(i % 16), d1 = (int)((i / 16) % D1);
+    const int64_t d0 = i / (16 * D1);
+    const float v = w[i];
+    if (wk) wk[d0 * 16 * D1 + tap * D1 + d1] = v;
+    if (wc) {
+      const int ky = tap / 4, kx = tap % 4;
+      const int py = (ky & 1) ? 0 : 1, px = (kx & 1) ? 0 : 1;  // (odd ky: class row 0)
+      const int r = ky >> 1, q = kx >> 1;                      // index among the class's 2 x 2 taps
+      wc[((int64_t)(2 * py + px) * D1 + d1) * 4 * D0 + (2 * r + q) * D0 + d0] = v;
+    }
+  }
+}
+
+int conv4_prep(const float* w, int D0, int D1, float* wk, float* wc, hipStream_t st) {
+  const int64_t total = (int64_t)D0 * D1 * 16;
+  hipLaunchKernelGGL(conv4_prep_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 1024)), dim3(256), 0, st, w,
+                     D0, D1, wk, wc);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int conv4_fwd(const float* src, int NF, int H, int W, int C, const float* wk, const float* bias, int N, float* out,
+              hipStream_t st) {
+  VAD_CHECK(C % 32 == 0 && H % 2 == 0 && W % 2 == 0 && N >= 1, "conv4_fwd: C % 32 == 0, even frames");
+  const int OH = H / 2, OW = W / 2;
+  const ConvGeom g{NF, OH, OW, 2, 2, H, W, C};
+  TapTable taps;
+  taps.ntaps = 16;
+  for (int k = 0; k < 16; ++k) {
+    taps.dh[k] = (int8_t)(k / 4 - 1);
+    taps.dw[k] = (int8_t)(k % 4 - 1);
+  }
+  const int M = NF * OH * OW, K = 16 * C;
+  const DenseEpiArgs pe{out, N, bias, 0, 0, 0, 0, 1.f, 0, nullptr, 1.f};
+  return with_tile(pick_fwd_tile(M, N), [&](auto cfg) -> int {
+    using Cf = decltype(cfg);
+    typename ConvGatherKC<Cf::BM>::Params pa{src, g, taps, nullptr, nullptr};
+    typename DenseKC<Cf::BN>::Params pb{wk, K, N, K};
+    return launch_gemm<Cf, ConvGatherKC, DenseKC, EpiDense>(pa, pb, pe, M, N, K, 1, nullptr, st);
+  });
+}
+
+int conv4_cls(const float* src, int NF, int SH, int SW, int C, const float* wc, const float* bias, int N, float* out,
+              hipStream_t st) {
+  VAD_CHECK(C % 32 == 0 && N >= 1, "conv4_cls: C % 32 == 0");
+  for (int cls = 0; cls < 4; ++cls) {
+    const int py = cls >> 1, px = cls & 1;
+    const ConvGeom g{NF, SH, SW, 1, 1, SH, SW, C};
+    TapTable taps;
+    taps.ntaps = 4;
+    for (int r = 0; r < 2; ++r)
+      for (int q = 0; q < 2; ++q) {
+        taps.dh[2 * r + q] = (int8_t)(py == 0 ? -r : 1 - r);
+        taps.dw[2 * r + q] = (int8_t)(px == 0 ? -q : 1 - q);
+      }
+    const EpiConvDgrad::Params pe{out, SH, SW, 2, py, 2, px, 2 * SH, 2 * SW, N, bias};
+    VAD_TRY(dgrad_launch(g, taps, src, wc + (int64_t)cls * N * 4 * C, N, pe, st));
+  }
+  return 0;
+}
+
+int conv4_wgrad(const float* A, int R, const float* src, int C, int NF, int AH, int AW, float* part, int* nsplit,
+                int64_t part_cap, int target_blocks, hipStream_t st) {
+  VAD_CHECK(C % 4 == 0 && R % 4 == 0, "conv4_wgrad: channel counts % 4 == 0");
+  const int M = R, N = 16 * C, K = NF * AH * AW;
+  VAD_CHECK((int64_t)M * N <= part_cap, "conv4_wgrad: slab too small");
+  return with_tile(pick_wgrad_tile(M, N), [&](auto cfg) -> int {
+    using Cf = decltype(cfg);
+    const int tiles = (int)(cdiv(M, Cf::BM) * cdiv(N, Cf::BN));
+    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, tiles), cdiv(K, 16 * BK)));
+    while ((int64_t)splits * M * N > part_cap && splits > 1) splits /= 2;
+    typename DenseKM<Cf::BM>::Params pa{A, R, R, K, -1};
+    typename ConvPatchKM<Cf::BN>::Params pb{src, NF, AH, AW, 2, 1, 2 * AH, 2 * AW, C, 4, N, nullptr, nullptr};
+    const EpiPartial::Params pe{part, N};
+    return launch_gemm<Cf, DenseKM, ConvPatchKM, EpiPartial>(pa, pb, pe, M, N, K, splits, nullptr, st, nsplit);
+  });
+}
+
+// dW[r][c][tap] = sum over the S slabs, in order, of part[s][r][tap C + c]
+__global__ __launch_bounds__(256) void conv4_wgrad_reduce_kernel(const float* __restrict__ part, int S, int R, int C,
+                                                                 float* __restrict__ dW) {
+  const int64_t total = (int64_t)R * 16 * C;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += part[(int64_t)z * total + i];
+    const int c = (int)(i % C), tap = (int)((i / C) % 16);
+    const int64_t r = i / (16 * C);
+    dW[(r * C + c) * 16 + tap] = s;
+  }
+}
+
+int conv4_wgrad_reduce(const float* part, int S, int R, int C, float* dW, hipStream_t st) {
+  const int64_t total = (int64_t)R * 16 * C;
+  hipLaunchKernelGGL(conv4_wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 2048)), dim3(256), 0,
+                     st, part, S, R, C, dW);
   VAD_LAUNCH_CHECK();
   return 0;
 }

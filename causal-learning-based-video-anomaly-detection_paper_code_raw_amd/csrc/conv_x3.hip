@@ -971,33 +971,29 @@ int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float*
 template <int NT, int PC, int NP, int CPH, int CPW>
 __device__ __forceinline__ void dgrad_s2x3_class(f32x16 (&acc)[NT], const __bf16* abase, const __bf16* bbase,
                                                  int WP) {
-  // the class's taps (kh, kw) with their dY offsets (dh, dw), as K steps s = (tap, 16-channel slice); the fragments of
-  // step s + 1 are read before step s's MFMAs (one step of register double-buffering, as conv3x3_x3_kernel)
-  constexpr int NTAP = (CPH ? 2 : 1) * (CPW ? 2 : 1), KK = PC / 16, NSTEP = NTAP * KK;
-  auto frag = [&](int sidx, bf16x8 (&av)[NP], bf16x8 (&bv)[NT][NP]) {
-    const int tp = sidx / KK, kk = sidx % KK, ai = CPW ? tp / 2 : tp, bi = CPW ? tp % 2 : 0;
-    const int kh = CPH ? (ai == 0 ? 0 : 2) : 1, dh = (CPH && ai == 0) ? 1 : 0;
-    const int kw = CPW ? (bi == 0 ? 0 : 2) : 1, dw = (CPW && bi == 0) ? 1 : 0;
-    const __bf16* ap = abase + (dh * 9 + dw) * (NP * PC + 8);
-    const __bf16* bp = bbase + (kh * 3 + kw) * NP * PC;
 #pragma unroll
-    for (int q = 0; q < NP; ++q) av[q] = *reinterpret_cast<const bf16x8*>(ap + q * PC + kk * 16);
+  for (int a = 0; a < (CPH ? 2 : 1); ++a) {
+    const int kh = CPH ? (a == 0 ? 0 : 2) : 1, dh = (CPH && a == 0) ? 1 : 0;
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+    for (int b = 0; b < (CPW ? 2 : 1); ++b) {
+      const int kw = CPW ? (b == 0 ? 0 : 2) : 1, dw = (CPW && b == 0) ? 1 : 0;
+      const __bf16* ap = abase + (dh * 9 + dw) * (NP * PC + 8);
+      const __bf16* bp = bbase + (kh * 3 + kw) * NP * PC;
 #pragma unroll
-      for (int q = 0; q < NP; ++q) bv[nt][q] = *reinterpret_cast<const bf16x8*>(bp + nt * 32 * WP + q * PC + kk * 16);
-  };
-  bf16x8 fa[2][NP], fb[2][NT][NP];
-  frag(0, fa[0], fb[0]);
+      for (int kk = 0; kk < PC / 16; ++kk) {
+        bf16x8 av[NP];
 #pragma unroll
-  for (int sidx = 0; sidx < NSTEP; ++sidx) {
-    const int cur = sidx & 1;
-    if (sidx + 1 < NSTEP) frag(sidx + 1, fa[cur ^ 1], fb[cur ^ 1]);
-    __builtin_amdgcn_sched_barrier(0);  // (keeps those reads ahead of this step's MFMAs)
+        for (int q = 0; q < NP; ++q) av[q] = *reinterpret_cast<const bf16x8*>(ap + q * PC + kk * 16);
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      if constexpr (NP == 3) acc[nt] = mfma_x3(fa[cur], fb[cur][nt], acc[nt]);
-      else acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][0], fb[cur][nt][0], acc[nt], 0, 0, 0);
+        for (int nt = 0; nt < NT; ++nt) {
+          bf16x8 bv[NP];
+#pragma unroll
+          for (int q = 0; q < NP; ++q)
+            bv[q] = *reinterpret_cast<const bf16x8*>(bp + nt * 32 * WP + q * PC + kk * 16);
+          if constexpr (NP == 3) acc[nt] = mfma_x3(av, bv, acc[nt]);
+          else acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[0], acc[nt], 0, 0, 0);
+        }
+      }
     }
   }
 }

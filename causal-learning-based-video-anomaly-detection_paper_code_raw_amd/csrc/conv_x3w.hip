@@ -336,7 +336,8 @@ bool x3_wgrad_tr_supported(const Conv3Layer& L) {
          L.OH < 256 && L.OW < 256;
 }
 
-int g_wgrad_tr_pft = 1;  // knob "conv_wgrad_tr_pft": the next tap's input fragments read before this tap's MFMAs
+int g_wgrad_tr_pft = 0;  // knob "conv_wgrad_tr_pft": the next tap's input fragments read before this tap's MFMAs (off:
+                         // config-2 step 1.696 ms off vs 1.72-1.74 on, profiles/r05_prefetch_ab.json)
 
 template <int S, int NI, int TH, int TW, int NCO, bool BNA = false>
 static int trw_launch(TrwArgs a, int target_blocks, int64_t partial_cap, hipStream_t st, int* nsplit) {

@@ -131,7 +131,7 @@ struct DenseKM {
 // each stride-2 parity class of the transposed conv.
 struct TapTable {
   int ntaps;
-  int8_t dh[9], dw[9];
+  int8_t dh[16], dw[16];  // (16: the 4x4 convs of cad1's autoencoder)
 };
 
 struct ConvGeom {
