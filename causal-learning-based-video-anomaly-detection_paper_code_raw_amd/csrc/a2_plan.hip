@@ -22,6 +22,8 @@
 
 namespace vad {
 
+int g_a2_direct = 1;  // knob "a2_direct": conv3d_1 direct on the VALU (latched per plan; 0: im2col + GEMM)
+
 constexpr int A2_NSLOT = 20;
 constexpr int A2_CO[3] = {16, 32, 64};
 constexpr int A2_MAXB = 256;
@@ -63,19 +65,15 @@ static const A2Offsets& a2_offsets() {
   return o;
 }
 
-// ------------------------------------------------------------------ head: block-wide dense helper
-// out[b][n] = act(sum_k in[b][k] W[n][k] + bias[n]); act 0 none, 1 relu, 2 sigmoid
-__device__ void blk_dense(const float* in, int K, const float* W, const float* bias, int N, float* out, int B,
-                          int act) {
-  for (int idx = threadIdx.x; idx < B * N; idx += blockDim.x) {
-    const int b = idx / N, n = idx % N;
-    const float* x = in + (int64_t)b * K;
-    const float* w = W + (int64_t)n * K;
-    float z = bias[n];
-    for (int k = 0; k < K; ++k) z = fmaf(w[k], x[k], z);
-    out[idx] = act == 1 ? relu_nan(z) : (act == 2 ? 1.f / (1.f + expf(-z)) : z);
-  }
+// ------------------------------------------------------------------ head
+// The head is a chain of small Linear layers over B rows (a2:27-101); each layer is one launch with one thread per
+// output (out[b][n] = sum_k in[b][k] W[n][k] + bias[n], k in order), so the chain spreads over the CUs instead of one
+// block walking it.
+__device__ __forceinline__ float a2_dot(const float* __restrict__ x, const float* __restrict__ w, int K, float z) {
+  for (int k = 0; k < K; ++k) z = fmaf(w[k], x[k], z);
+  return z;
 }
+__device__ __forceinline__ float a2_sigmoid(float z) { return 1.f / (1.f + expf(-z)); }
 
 struct A2HeadArgs {
   int B, training, with_loss;
@@ -91,51 +89,73 @@ struct A2HeadArgs {
   float* d_s;     // [B]  upstream grads written by the loss
   float* d_adj;   // [B][256]
   float* red;     // [256] scratch
+  float* pairs;   // [B][B] mean |A_i - A_j| of the pseudo-normal pairs i < j
+  float* lsc;     // [8] loss scalars between the loss launches: focal sum, acyclicity, edges, avg, csign, np
 };
 
-__global__ __launch_bounds__(512) void a2_head_fwd_kernel(A2HeadArgs a) {
-  const int B = a.B;
+// forward stage st: 0 causal_net.0 (+ReLU), 1 causal_net.2 (+sigmoid) -> sig, adj (zero diagonal), 2 graph_encoder.0
+// (+ReLU, Dropout) -> g1, g1d, 3 graph_encoder.3 -> g2 and the predictor input cat = [f, g2], 4 anomaly_predictor.0
+// (+ReLU), 5 anomaly_predictor.2 (+sigmoid) -> s
+constexpr int A2_FWD_N[6] = {32, 256, 128, 64, 32, 1};
+
+__global__ __launch_bounds__(256) void a2_head_fwd_kernel(A2HeadArgs a, int st) {
+  const int B = a.B, idx = blockIdx.x * 256 + threadIdx.x;
   const float* P = a.P;
   const int64_t* o = a.off;
-  blk_dense(a.f, 16, P + o[S_CN0W], P + o[S_CN0B], 32, a.hc0, B, 1);
-  __syncthreads();
-  blk_dense(a.hc0, 32, P + o[S_CN2W], P + o[S_CN2B], 256, a.sig, B, 2);
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < B * 256; idx += blockDim.x) {
-    const int e = idx % 256;
-    a.adj[idx] = (e / 16 == e % 16) ? a.sig[idx] * 0.f : a.sig[idx];  // * (1 - eye)
+  switch (st) {
+    case 0:
+      if (idx < B * 32) {
+        const int b = idx / 32, n = idx % 32;
+        a.hc0[idx] = relu_nan(a2_dot(a.f + b * 16, P + o[S_CN0W] + n * 16, 16, P[o[S_CN0B] + n]));
+      }
+      break;
+    case 1:
+      if (idx < B * 256) {
+        const int b = idx / 256, e = idx % 256;
+        const float sg = a2_sigmoid(a2_dot(a.hc0 + b * 32, P + o[S_CN2W] + e * 32, 32, P[o[S_CN2B] + e]));
+        a.sig[idx] = sg;
+        a.adj[idx] = (e / 16 == e % 16) ? sg * 0.f : sg;  // * (1 - eye)
+      }
+      break;
+    case 2:
+      if (idx < B * 128) {
+        const int b = idx / 128, n = idx % 128;
+        float v = relu_nan(a2_dot(a.adj + b * 256, P + o[S_GE0W] + n * 256, 256, P[o[S_GE0B] + n]));
+        a.g1[idx] = v;
+        if (a.training)
+          v = rng_u24(a.h_graph, (uint64_t)(a.clip0 + b), (uint64_t)n) >= a.thr_graph ? v * a.s_graph : 0.f;
+        a.g1d[idx] = v;
+      }
+      break;
+    case 3:
+      if (idx < B * 64) {
+        const int b = idx / 64, n = idx % 64;
+        const float v = a2_dot(a.g1d + b * 128, P + o[S_GE3W] + n * 128, 128, P[o[S_GE3B] + n]);
+        a.g2[idx] = v;
+        a.cat[b * 80 + 16 + n] = v;
+      }
+      if (idx < B * 16) a.cat[(idx / 16) * 80 + idx % 16] = a.f[idx];
+      break;
+    case 4:
+      if (idx < B * 32) {
+        const int b = idx / 32, n = idx % 32;
+        a.hp0[idx] = relu_nan(a2_dot(a.cat + b * 80, P + o[S_AP0W] + n * 80, 80, P[o[S_AP0B] + n]));
+      }
+      break;
+    default:
+      if (idx < B) a.s[idx] = a2_sigmoid(a2_dot(a.hp0 + idx * 32, P + o[S_AP2W], 32, P[o[S_AP2B]]));
   }
-  __syncthreads();
-  blk_dense(a.adj, 256, P + o[S_GE0W], P + o[S_GE0B], 128, a.g1, B, 1);
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < B * 128; idx += blockDim.x) {
-    float v = a.g1[idx];
-    if (a.training) {
-      const int b = idx / 128, n = idx % 128;
-      v = rng_u24(a.h_graph, (uint64_t)(a.clip0 + b), (uint64_t)n) >= a.thr_graph ? v * a.s_graph : 0.f;
-    }
-    a.g1d[idx] = v;
-  }
-  __syncthreads();
-  blk_dense(a.g1d, 128, P + o[S_GE3W], P + o[S_GE3B], 64, a.g2, B, 0);
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < B * 80; idx += blockDim.x) {
-    const int b = idx / 80, c = idx % 80;
-    a.cat[idx] = c < 16 ? a.f[b * 16 + c] : a.g2[b * 64 + c - 16];
-  }
-  __syncthreads();
-  blk_dense(a.cat, 80, P + o[S_AP0W], P + o[S_AP0B], 32, a.hp0, B, 1);
-  __syncthreads();
-  blk_dense(a.hp0, 32, P + o[S_AP2W], P + o[S_AP2B], 1, a.s, B, 2);
 }
 
-// compute_improved_loss (a2:135-205) on the saved scores / adjacency, plus d total / d scores and d total / d adj
+// compute_improved_loss (a2:135-205) on the saved scores / adjacency, plus d total / d scores and d total / d adj, as
+// four launches: a2_loss_kernel (pseudo labels, focal BCE and d scores, mean adjacency, edge count: one block),
+// a2_pairs_kernel (one wave per clip pair i < j: mean |A_i - A_j| over the 256 entries, fixed order),
+// a2_loss_fin_kernel (the pair mean in fixed order, the loss terms) and a2_dadj_kernel (d total / d adj, one thread per
+// entry)
 __global__ __launch_bounds__(512) void a2_loss_kernel(A2HeadArgs a) {
   const int B = a.B;
   __shared__ float sh[512];
   __shared__ float sh2[512];
-  __shared__ int nnormal_s, npairs_s;
-  __shared__ float avg_s;
   const int t = threadIdx.x;
   if (t < B) {
     const float u = (float)rng_u24(a.h_pseudo, (uint64_t)(a.clip0 + t), 0) * (1.0f / 16777216.0f);
@@ -186,55 +206,50 @@ __global__ __launch_bounds__(512) void a2_loss_kernel(A2HeadArgs a) {
     if (t < k) sh[t] += sh[t + k];
     __syncthreads();
   }
-  const float edges = sh[0];
-  __syncthreads();
-  // consistency over the pseudo-normal clips: mean over pairs i<j of mean|A_i - A_j|
+  if (t == 0) {
+    a.lsc[0] = focal_sum;
+    a.lsc[1] = acyc;
+    a.lsc[2] = sh[0];
+  }
+}
+
+__global__ __launch_bounds__(64) void a2_pairs_kernel(A2HeadArgs a) {
+  const int B = a.B, i = blockIdx.x / B, j = blockIdx.x % B, lane = threadIdx.x;
+  if (!(i < j && a.pseudo[i] == 0.f && a.pseudo[j] == 0.f)) {
+    if (lane == 0) a.pairs[blockIdx.x] = 0.f;
+    return;
+  }
+  float d = 0.f;
+  for (int e = lane; e < 256; e += 64) d += fabsf(a.adj[i * 256 + e] - a.adj[j * 256 + e]);
+  d = wave_sum(d);
+  if (lane == 0) a.pairs[blockIdx.x] = d / 256.f;
+}
+
+__global__ __launch_bounds__(512) void a2_loss_fin_kernel(A2HeadArgs a) {
+  const int B = a.B, t = threadIdx.x;
+  __shared__ float sh[512];
+  __shared__ int nn_s;
   if (t == 0) {
     int nn = 0;
     for (int b = 0; b < B; ++b) nn += a.pseudo[b] == 0.f;
-    nnormal_s = nn;
-    npairs_s = nn * (nn - 1) / 2;
+    nn_s = nn;
   }
-  __syncthreads();
-  const int np = npairs_s;
   float pd = 0.f;
-  if (nnormal_s > 1) {
-    for (int q = t; q < B * B; q += blockDim.x) {
-      const int i = q / B, j = q % B;
-      if (i < j && a.pseudo[i] == 0.f && a.pseudo[j] == 0.f) {
-        float d = 0.f;
-        for (int e = 0; e < 256; ++e) d += fabsf(a.adj[i * 256 + e] - a.adj[j * 256 + e]);
-        pd += d / 256.f;
-      }
-    }
-  }
+  for (int q = t; q < B * B; q += blockDim.x) pd += a.pairs[q];
   sh[t] = pd;
   __syncthreads();
   for (int k = blockDim.x / 2; k > 0; k >>= 1) {
     if (t < k) sh[t] += sh[t + k];
     __syncthreads();
   }
-  if (t == 0) avg_s = np > 0 ? sh[0] / (float)np : 0.f;
-  __syncthreads();
-  const float avg = avg_s;
-  const float consistency = np > 0 ? fabsf(avg - 0.1f) : 0.f;
-  const float csign = np > 0 ? (avg > 0.1f ? 1.f : (avg < 0.1f ? -1.f : 0.f)) : 0.f;
-  // d total / d adj: 0.01 * d acyc + 0.01 * d consistency  (sparsity / structure carry no gradient)
-  for (int idx = t; idx < B * 256; idx += blockDim.x) {
-    const int b = idx / 256, e = idx % 256;
-    float g = 0.01f * 2.f * a.red[e] / (float)B;
-    if (np > 0 && a.pseudo[b] == 0.f) {
-      float sg = 0.f;
-      for (int j = 0; j < B; ++j) {
-        if (j == b || a.pseudo[j] != 0.f) continue;
-        const float d = a.adj[idx] - a.adj[j * 256 + e];
-        sg += d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-      }
-      g += 0.01f * csign * sg / ((float)np * 256.f);
-    }
-    a.d_adj[idx] = g;
-  }
   if (t == 0) {
+    const int nn = nn_s, np = nn > 1 ? nn * (nn - 1) / 2 : 0;
+    const float avg = np > 0 ? sh[0] / (float)np : 0.f;
+    const float consistency = np > 0 ? fabsf(avg - 0.1f) : 0.f;
+    const float csign = np > 0 ? (avg > 0.1f ? 1.f : (avg < 0.1f ? -1.f : 0.f)) : 0.f;
+    const float focal_sum = a.lsc[0], acyc = a.lsc[1], edges = a.lsc[2];
+    a.lsc[3] = csign;
+    a.lsc[4] = (float)np;
     const float anomaly = focal_sum / (float)B;
     const float ratio = edges / (float)(B * 256);
     const float sparsity = fabsf(ratio - 0.3f);
@@ -249,6 +264,25 @@ __global__ __launch_bounds__(512) void a2_loss_kernel(A2HeadArgs a) {
   }
 }
 
+// d total / d adj: 0.01 * d acyc + 0.01 * d consistency  (sparsity / structure carry no gradient)
+__global__ __launch_bounds__(256) void a2_dadj_kernel(A2HeadArgs a) {
+  const int B = a.B, idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * 256) return;
+  const int b = idx / 256, e = idx % 256;
+  const float csign = a.lsc[3], np = a.lsc[4];
+  float g = 0.01f * 2.f * a.red[e] / (float)B;
+  if (np > 0.f && a.pseudo[b] == 0.f) {
+    float sg = 0.f;
+    for (int j = 0; j < B; ++j) {
+      if (j == b || a.pseudo[j] != 0.f) continue;
+      const float d = a.adj[idx] - a.adj[j * 256 + e];
+      sg += d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+    }
+    g += 0.01f * csign * sg / (np * 256.f);
+  }
+  a.d_adj[idx] = g;
+}
+
 struct A2HeadBwdArgs {
   A2HeadArgs f;
   const float* d_s;    // [B]
@@ -261,82 +295,219 @@ struct A2HeadBwdArgs {
   float s_fc;
 };
 
-__global__ __launch_bounds__(512) void a2_head_bwd_kernel(A2HeadBwdArgs a) {
+// backward stage st (the forward's mirror): 0 predictor output + anomaly_predictor.0 pre-activation grads, 1 d cat ->
+// d g2 and the predictor's share of d features, 2 graph_encoder.0 pre-activation grads (dropout, ReLU), 3 d adj (graph
+// encoder + loss) -> causal_net.2 pre-activation grads, 4 causal_net.0 pre-activation grads, 5 d features (fc output)
+// incl. the fc dropout, 6 every head weight / bias grad (fixed-order sums over the batch, one thread per entry)
+constexpr int A2_BWD_OUT[6] = {32, 80, 128, 256, 32, 16};
+struct A2WSeg {
+  int w, bias, N, K;
+};
+constexpr A2WSeg A2_WSEGS[6] = {{S_AP2W, S_AP2B, 1, 32}, {S_AP0W, S_AP0B, 32, 80},   {S_GE3W, S_GE3B, 64, 128},
+                                {S_GE0W, S_GE0B, 128, 256}, {S_CN2W, S_CN2B, 256, 32}, {S_CN0W, S_CN0B, 32, 16}};
+constexpr int A2_WG_TOTAL = 1 * 33 + 32 * 81 + 64 * 129 + 128 * 257 + 256 * 33 + 32 * 17;
+
+__global__ __launch_bounds__(256) void a2_head_bwd_kernel(A2HeadBwdArgs a, int st) {
   const A2HeadArgs& f = a.f;
-  const int B = f.B, t = threadIdx.x, T = blockDim.x;
+  const int B = f.B, idx = blockIdx.x * 256 + threadIdx.x;
   const float* P = f.P;
   const int64_t* o = f.off;
-  // predictor: s = sigmoid(W2 hp0 + b), hp0 = relu(W0 cat + b)
-  for (int b = t; b < B; b += T) a.dz_ap2[b] = a.d_s[b] * f.s[b] * (1.f - f.s[b]);
-  __syncthreads();
-  for (int idx = t; idx < B * 32; idx += T) {
-    const int b = idx / 32, k = idx % 32;
-    a.dz_ap0[idx] = f.hp0[idx] > 0.f ? a.dz_ap2[b] * P[o[S_AP2W] + k] : 0.f;
-  }
-  __syncthreads();
-  // d cat -> d g2 (64) and the predictor's share of d features (16, kept in dfeat)
-  for (int idx = t; idx < B * 80; idx += T) {
-    const int b = idx / 80, c = idx % 80;
-    float d = 0.f;
-    for (int k = 0; k < 32; ++k) d = fmaf(a.dz_ap0[b * 32 + k], P[o[S_AP0W] + k * 80 + c], d);
-    if (c < 16) a.dfeat[b * 16 + c] = d + (a.d_f ? a.d_f[b * 16 + c] : 0.f);
-    else a.dg2[b * 64 + c - 16] = d;
-  }
-  __syncthreads();
-  // graph encoder: g2 = W3 g1d + b; g1d = drop(relu(W0 adj + b))
-  for (int idx = t; idx < B * 128; idx += T) {
-    const int b = idx / 128, n = idx % 128;
-    float d = 0.f;
-    for (int k = 0; k < 64; ++k) d = fmaf(a.dg2[b * 64 + k], P[o[S_GE3W] + k * 128 + n], d);
-    if (f.training) d = rng_u24(f.h_graph, (uint64_t)(f.clip0 + b), (uint64_t)n) >= f.thr_graph ? d * f.s_graph : 0.f;
-    a.dz_ge0[idx] = f.g1[idx] > 0.f ? d : 0.f;
-  }
-  __syncthreads();
-  // d adj (graph encoder + loss) -> d sig (zero diagonal) -> dz_cn2
-  for (int idx = t; idx < B * 256; idx += T) {
-    const int b = idx / 256, e = idx % 256;
-    float d = a.d_adj ? a.d_adj[idx] : 0.f;
-    for (int k = 0; k < 128; ++k) d = fmaf(a.dz_ge0[b * 128 + k], P[o[S_GE0W] + k * 256 + e], d);
-    const float sg = f.sig[idx];
-    a.dz_cn2[idx] = (e / 16 == e % 16) ? 0.f : d * sg * (1.f - sg);
-  }
-  __syncthreads();
-  for (int idx = t; idx < B * 32; idx += T) {
-    const int b = idx / 32, k = idx % 32;
-    float d = 0.f;
-    for (int e = 0; e < 256; ++e) d = fmaf(a.dz_cn2[b * 256 + e], P[o[S_CN2W] + e * 32 + k], d);
-    a.dz_cn0[idx] = f.hc0[idx] > 0.f ? d : 0.f;
-  }
-  __syncthreads();
-  // d features (fc output after dropout) += W_cn0^T dz_cn0, then the fc dropout backward (in place)
-  for (int idx = t; idx < B * 16; idx += T) {
-    const int b = idx / 16, c = idx % 16;
-    float d = a.dfeat[idx];
-    for (int k = 0; k < 32; ++k) d = fmaf(a.dz_cn0[b * 32 + k], P[o[S_CN0W] + k * 16 + c], d);
-    if (f.training) d = rng_u24(a.h_fc, (uint64_t)(f.clip0 + b), (uint64_t)c) >= a.thr_fc ? d * a.s_fc : 0.f;
-    a.dfeat[idx] = d;
-  }
-  // head weight grads: fixed-order sums over the batch
-  struct Seg { int w, bias, N, K; const float* dz; const float* x; };
-  const Seg segs[6] = {
-      {S_AP2W, S_AP2B, 1, 32, a.dz_ap2, f.hp0},  {S_AP0W, S_AP0B, 32, 80, a.dz_ap0, f.cat},
-      {S_GE3W, S_GE3B, 64, 128, a.dg2, f.g1d},   {S_GE0W, S_GE0B, 128, 256, a.dz_ge0, f.adj},
-      {S_CN2W, S_CN2B, 256, 32, a.dz_cn2, f.hc0}, {S_CN0W, S_CN0B, 32, 16, a.dz_cn0, f.f},
-  };
-  for (int s = 0; s < 6; ++s) {
-    const Seg& g = segs[s];
-    const int tot = g.N * (g.K + 1);
-    for (int idx = t; idx < tot; idx += T) {
-      const int n = idx / (g.K + 1), k = idx % (g.K + 1);
+  switch (st) {
+    case 0:  // predictor: s = sigmoid(W2 hp0 + b), hp0 = relu(W0 cat + b)
+      if (idx < B * 32) {
+        const int b = idx / 32, k = idx % 32;
+        const float dz2 = a.d_s[b] * f.s[b] * (1.f - f.s[b]);
+        if (k == 0) a.dz_ap2[b] = dz2;
+        a.dz_ap0[idx] = f.hp0[idx] > 0.f ? dz2 * P[o[S_AP2W] + k] : 0.f;
+      }
+      break;
+    case 1:
+      if (idx < B * 80) {
+        const int b = idx / 80, c = idx % 80;
+        float d = 0.f;
+        for (int k = 0; k < 32; ++k) d = fmaf(a.dz_ap0[b * 32 + k], P[o[S_AP0W] + k * 80 + c], d);
+        if (c < 16) a.dfeat[b * 16 + c] = d + (a.d_f ? a.d_f[b * 16 + c] : 0.f);
+        else a.dg2[b * 64 + c - 16] = d;
+      }
+      break;
+    case 2:  // graph encoder: g2 = W3 g1d + b; g1d = drop(relu(W0 adj + b))
+      if (idx < B * 128) {
+        const int b = idx / 128, n = idx % 128;
+        float d = 0.f;
+        for (int k = 0; k < 64; ++k) d = fmaf(a.dg2[b * 64 + k], P[o[S_GE3W] + k * 128 + n], d);
+        if (f.training) d = rng_u24(f.h_graph, (uint64_t)(f.clip0 + b), (uint64_t)n) >= f.thr_graph ? d * f.s_graph : 0.f;
+        a.dz_ge0[idx] = f.g1[idx] > 0.f ? d : 0.f;
+      }
+      break;
+    case 3:  // d adj -> d sig (zero diagonal) -> dz_cn2
+      if (idx < B * 256) {
+        const int b = idx / 256, e = idx % 256;
+        float d = a.d_adj ? a.d_adj[idx] : 0.f;
+        for (int k = 0; k < 128; ++k) d = fmaf(a.dz_ge0[b * 128 + k], P[o[S_GE0W] + k * 256 + e], d);
+        const float sg = f.sig[idx];
+        a.dz_cn2[idx] = (e / 16 == e % 16) ? 0.f : d * sg * (1.f - sg);
+      }
+      break;
+    case 4:
+      if (idx < B * 32) {
+        const int b = idx / 32, k = idx % 32;
+        float d = 0.f;
+        for (int e = 0; e < 256; ++e) d = fmaf(a.dz_cn2[b * 256 + e], P[o[S_CN2W] + e * 32 + k], d);
+        a.dz_cn0[idx] = f.hc0[idx] > 0.f ? d : 0.f;
+      }
+      break;
+    case 5:  // d features (fc output after dropout) += W_cn0^T dz_cn0, then the fc dropout backward
+      if (idx < B * 16) {
+        const int b = idx / 16, c = idx % 16;
+        float d = a.dfeat[idx];
+        for (int k = 0; k < 32; ++k) d = fmaf(a.dz_cn0[b * 32 + k], P[o[S_CN0W] + k * 16 + c], d);
+        if (f.training) d = rng_u24(a.h_fc, (uint64_t)(f.clip0 + b), (uint64_t)c) >= a.thr_fc ? d * a.s_fc : 0.f;
+        a.dfeat[idx] = d;
+      }
+      break;
+    default: {
+      int r = idx, s = 0;
+      for (; s < 6; ++s) {
+        const int len = A2_WSEGS[s].N * (A2_WSEGS[s].K + 1);
+        if (r < len) break;
+        r -= len;
+      }
+      if (s >= 6) break;
+      const A2WSeg g = A2_WSEGS[s];
+      const float* dz = s == 0 ? a.dz_ap2 : s == 1 ? a.dz_ap0 : s == 2 ? a.dg2 : s == 3 ? a.dz_ge0 : s == 4 ? a.dz_cn2
+                                                                                                             : a.dz_cn0;
+      const float* x = s == 0 ? f.hp0 : s == 1 ? f.cat : s == 2 ? f.g1d : s == 3 ? f.adj : s == 4 ? f.hc0 : f.f;
+      const int n = r / (g.K + 1), k = r % (g.K + 1);
       float acc = 0.f;
       if (k < g.K) {
-        for (int b = 0; b < B; ++b) acc = fmaf(g.dz[b * g.N + n], g.x[b * g.K + k], acc);
+        for (int b = 0; b < B; ++b) acc = fmaf(dz[b * g.N + n], x[b * g.K + k], acc);
         a.G[o[g.w] + n * g.K + k] = acc;
       } else {
-        for (int b = 0; b < B; ++b) acc += g.dz[b * g.N + n];
+        for (int b = 0; b < B; ++b) acc += dz[b * g.N + n];
         a.G[o[g.bias] + n] = acc;
       }
     }
+  }
+}
+
+// ------------------------------------------------------------------ conv3d_1 (3 -> 16, k3, stride (1, 2, 2), p1) direct
+// (knob "a2_direct", latched per plan; 0: im2col + GEMM).  With 3 input channels the im2col matrix (K = 81) is 6.75x
+// the clip and the GEMM runs 16-wide tiles, so the first conv and its weight gradient run on the VALU from the clip
+// itself (NCDHW):
+//   a2_conv1_fwd   one thread per output voxel: its 3 x 27 inputs x the [81][16] weights (LDS broadcast rows), + bias,
+//                  ReLU, 16 channels out (NDHWC)
+//   a2_conv1_wgrad per block, 64-voxel chunks of the gated dY rows and of the 81-entry input patches in LDS; thread
+//                  (co, tap group) owns up to 6 of the 82 (tap, + the bias "ones" tap) sums; per-block slabs summed
+//                  in fixed order by a2_conv1_wgrad_reduce (64 lanes per entry)
+constexpr int A2C1_TAPS = 81, A2C1_CHUNK = 64;
+
+__global__ __launch_bounds__(256) void a2_conv1_fwd_kernel(const float* __restrict__ x, int B, int T, int H, int W,
+                                                           const float* __restrict__ w, const float* __restrict__ bias,
+                                                           float* __restrict__ y) {
+  __shared__ __attribute__((aligned(16))) float ws[A2C1_TAPS][16];  // [ci*27 + tap][co]
+  for (int i = threadIdx.x; i < 16 * A2C1_TAPS; i += 256) ws[i % A2C1_TAPS][i / A2C1_TAPS] = w[i];
+  __syncthreads();
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const int64_t total = (int64_t)B * T * OH * OW;
+  for (int64_t p = blockIdx.x * 256ll + threadIdx.x; p < total; p += (int64_t)gridDim.x * 256) {
+    const int ow = (int)(p % OW);
+    int64_t r = p / OW;
+    const int oh = (int)(r % OH);
+    r /= OH;
+    const int d = (int)(r % T);
+    const int64_t b = r / T;
+    f32x4 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ci = 0; ci < 3; ++ci) {
+      const float* xc = x + (b * 3 + ci) * T * H * W;
+#pragma unroll
+      for (int t = 0; t < 27; ++t) {
+        const int id = d - 1 + t / 9, ih = 2 * oh - 1 + (t / 3) % 3, iw = 2 * ow - 1 + t % 3;
+        const bool in = id >= 0 && id < T && ih >= 0 && ih < H && iw >= 0 && iw < W;
+        const float v = in ? xc[((int64_t)id * H + ih) * W + iw] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 wv = *reinterpret_cast<const f32x4*>(&ws[ci * 27 + t][4 * q]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[q][e] = fmaf(v, wv[e], acc[q][e]);
+        }
+      }
+    }
+    float* o = y + p * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = relu_nan(acc[q][e] + bias[4 * q + e]);
+      *reinterpret_cast<f32x4*>(o + 4 * q) = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void a2_conv1_wgrad_kernel(const float* __restrict__ dA, const float* __restrict__ x,
+                                                             int B, int T, int H, int W, float* __restrict__ slab) {
+  __shared__ float as[A2C1_CHUNK][17];
+  __shared__ float xs[A2C1_CHUNK][A2C1_TAPS + 1];
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const int64_t total = (int64_t)B * T * OH * OW;
+  const int tid = threadIdx.x, co = tid & 15, g = tid >> 4;
+  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t p0 = (int64_t)blockIdx.x * A2C1_CHUNK; p0 < total; p0 += (int64_t)gridDim.x * A2C1_CHUNK) {
+    __syncthreads();
+    for (int i = tid; i < A2C1_CHUNK * 16; i += 256) {
+      const int pp = i >> 4;
+      as[pp][i & 15] = p0 + pp < total ? dA[(p0 + pp) * 16 + (i & 15)] : 0.f;
+    }
+    for (int i = tid; i < A2C1_CHUNK * (A2C1_TAPS + 1); i += 256) {
+      const int pp = i / (A2C1_TAPS + 1), j = i % (A2C1_TAPS + 1);
+      const int64_t p = p0 + pp;
+      float v = 0.f;
+      if (p < total) {
+        if (j == A2C1_TAPS) {
+          v = 1.f;  // (the conv bias)
+        } else {
+          const int ci = j / 27, t = j % 27;
+          const int ow = (int)(p % OW);
+          int64_t r = p / OW;
+          const int oh = (int)(r % OH);
+          r /= OH;
+          const int d = (int)(r % T);
+          const int64_t b = r / T;
+          const int id = d - 1 + t / 9, ih = 2 * oh - 1 + (t / 3) % 3, iw = 2 * ow - 1 + t % 3;
+          if (id >= 0 && id < T && ih >= 0 && ih < H && iw >= 0 && iw < W)
+            v = x[(((b * 3 + ci) * T + id) * H + ih) * W + iw];
+        }
+      }
+      xs[pp][j] = v;
+    }
+    __syncthreads();
+    for (int pp = 0; pp < A2C1_CHUNK; ++pp) {
+      const float a = as[pp][co];
+#pragma unroll
+      for (int m = 0; m < 6; ++m)
+        if (g + 16 * m <= A2C1_TAPS) acc[m] = fmaf(a, xs[pp][g + 16 * m], acc[m]);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 6; ++m)
+    if (g + 16 * m <= A2C1_TAPS)
+      slab[((int64_t)blockIdx.x * 16 + co) * (A2C1_TAPS + 1) + g + 16 * m] = acc[m];
+}
+
+// dW[co][ci*27 + tap] / db[co] = sum over the S slabs in order: 4 entries per block, 64 lanes each, fixed butterfly
+__global__ __launch_bounds__(256) void a2_conv1_wgrad_reduce_kernel(const float* __restrict__ slab, int S,
+                                                                    float* __restrict__ dW, float* __restrict__ db) {
+  constexpr int NE = 16 * (A2C1_TAPS + 1);
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  float v = 0.f;
+  if (i < NE)
+    for (int z = lane; z < S; z += 64) v += slab[(int64_t)z * NE + i];
+  v = wave_sum(v);
+  if (lane == 0 && i < NE) {
+    const int co = i / (A2C1_TAPS + 1), j = i % (A2C1_TAPS + 1);
+    if (j < A2C1_TAPS) dW[co * A2C1_TAPS + j] = v;
+    else db[co] = v;
   }
 }
 
@@ -414,9 +585,11 @@ struct A2PlanImpl {
   float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr;
   int32_t* steps = nullptr;
   float *cols[3], *y[3], *pooled, *f, *hc0, *sig, *adj, *g1, *g1d, *g2, *cat, *hp0, *s, *losses, *pseudo, *d_s,
-      *d_adj, *red, *dz_ap2, *dz_ap0, *dg2, *dz_ge0, *dz_cn2, *dz_cn0, *dfeat, *dpooled, *dA, *dcols, *scratch,
-      *norms, *ctrl;
+      *d_adj, *red, *pairs, *lsc, *dz_ap2, *dz_ap0, *dg2, *dz_ge0, *dz_cn2, *dz_cn0, *dfeat, *dpooled, *dA, *dcols,
+      *scratch, *norms, *ctrl;
   int64_t* off_dev;
+  float* xin = nullptr;  // (a2_direct) the forward's clip, kept for conv3d_1's weight gradient
+  const int direct = g_a2_direct;
   int64_t scratch_floats = 0;
   int training = 1, with_loss = 0;
   uint64_t seed = 0, step = 0;
@@ -435,8 +608,9 @@ struct A2PlanImpl {
 
   void carve(Ws& w) {
     int64_t max_y = 0, max_dcols = 1;
+    xin = direct ? w.take<float>(g[0].in.numel()) : nullptr;
     for (int s = 0; s < 3; ++s) {
-      cols[s] = w.take<float>(g[s].rows() * g[s].K());
+      cols[s] = (direct && s == 0) ? nullptr : w.take<float>(g[s].rows() * g[s].K());
       y[s] = w.take<float>(g[s].out().numel());
       max_y = std::max(max_y, g[s].out().numel());
       if (s > 0) max_dcols = std::max(max_dcols, g[s].rows() * g[s].K());
@@ -458,6 +632,8 @@ struct A2PlanImpl {
     d_s = w.take<float>(b);
     d_adj = w.take<float>(b * 256);
     red = w.take<float>(256);
+    pairs = w.take<float>((int64_t)b * b);
+    lsc = w.take<float>(8);
     dz_ap2 = w.take<float>(b);
     dz_ap0 = w.take<float>(b * 32);
     dg2 = w.take<float>(b * 64);
@@ -494,11 +670,22 @@ struct A2PlanImpl {
     a.d_s = d_s;
     a.d_adj = d_adj;
     a.red = red;
+    a.pairs = pairs;
+    a.lsc = lsc;
     return a;
   }
 
   int forward(const float* x, hipStream_t st) {
     for (int s3 = 0; s3 < 3; ++s3) {
+      if (direct && s3 == 0) {
+        const int64_t n = g[0].in.numel();
+        VAD_HIP(hipMemcpyAsync(xin, x, sizeof(float) * n, hipMemcpyDeviceToDevice, st));
+        const int64_t vox = g[0].rows();
+        hipLaunchKernelGGL(a2_conv1_fwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(vox, 256), 4096)), dim3(256), 0,
+                           st, xin, B, T, H, W, P(S_C1W), P(S_C1B), y[0]);
+        VAD_LAUNCH_CHECK();
+        continue;
+      }
       const float* src = s3 == 0 ? x : y[s3 - 1];
       const Strides5 str = s3 == 0 ? ncdhw_strides(g[0].in) : ndhwc_strides(g[s3].in);
       VAD_TRY(im2col3d(src, str, g[s3], nullptr, nullptr, 0, cols[s3], st));
@@ -517,15 +704,25 @@ struct A2PlanImpl {
       fc.row0 = clip0;
     }
     VAD_TRY(dense_fwd(pooled, B, 4096, P(S_FCW), P(S_FCB), 16, f, fc, scratch, scratch_floats, st));
-    hipLaunchKernelGGL(a2_head_fwd_kernel, dim3(1), dim3(512), 0, st, head_args());
-    VAD_LAUNCH_CHECK();
+    const A2HeadArgs ha = head_args();
+    for (int s = 0; s < 6; ++s) {
+      hipLaunchKernelGGL(a2_head_fwd_kernel, dim3((unsigned)cdiv(B * A2_FWD_N[s], 256)), dim3(256), 0, st, ha, s);
+      VAD_LAUNCH_CHECK();
+    }
     if (with_loss) VAD_TRY(loss(st));
     return 0;
   }
 
   int loss(hipStream_t st) {
     with_loss = 1;
-    hipLaunchKernelGGL(a2_loss_kernel, dim3(1), dim3(512), 0, st, head_args());
+    const A2HeadArgs ha = head_args();
+    hipLaunchKernelGGL(a2_loss_kernel, dim3(1), dim3(512), 0, st, ha);
+    VAD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(a2_pairs_kernel, dim3((unsigned)(B * B)), dim3(64), 0, st, ha);
+    VAD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(a2_loss_fin_kernel, dim3(1), dim3(512), 0, st, ha);
+    VAD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(a2_dadj_kernel, dim3((unsigned)cdiv(B * 256, 256)), dim3(256), 0, st, ha);
     VAD_LAUNCH_CHECK();
     return 0;
   }
@@ -551,16 +748,29 @@ struct A2PlanImpl {
     hb.h_fc = rng_h1(seed, S_A2_DROP_FC, step);
     hb.thr_fc = drop_threshold(0.3);
     hb.s_fc = 1.0f / (float)(1.0 - 0.3);
-    hipLaunchKernelGGL(a2_head_bwd_kernel, dim3(1), dim3(512), 0, st, hb);
-    VAD_LAUNCH_CHECK();
+    for (int s = 0; s < 7; ++s) {
+      const int n = s < 6 ? B * A2_BWD_OUT[s] : A2_WG_TOTAL;
+      hipLaunchKernelGGL(a2_head_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, hb, s);
+      VAD_LAUNCH_CHECK();
+    }
     VAD_TRY(dense_wgrad(dfeat, B, 16, pooled, 4096, G(S_FCW), G(S_FCB), scratch, scratch_floats, nullptr, st));
     VAD_TRY(dense_dgrad(dfeat, B, 16, P(S_FCW), 4096, dpooled, nullptr, 1.f, nullptr, st));
     VAD_TRY(adaptive_avgpool3d_bwd(dpooled, g[2].out(), 4, 4, 4, dA, st));
     for (int s3 = 2; s3 >= 0; --s3) {
       const int64_t rows = g[s3].rows();
       VAD_TRY(relu_gate(dA, y[s3], rows * A2_CO[s3], st));
+      if (direct && s3 == 0) {
+        const int nb = (int)std::max<int64_t>(1, std::min<int64_t>({cdiv(rows, 4 * A2C1_CHUNK), 512,
+                                                                     scratch_floats / (16 * (A2C1_TAPS + 1))}));
+        hipLaunchKernelGGL(a2_conv1_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, st, dA, xin, B, T, H, W, scratch);
+        VAD_LAUNCH_CHECK();
+        hipLaunchKernelGGL(a2_conv1_wgrad_reduce_kernel, dim3((unsigned)cdiv(16 * (A2C1_TAPS + 1), 4)), dim3(256), 0,
+                           st, scratch, nb, G(S_C1W), G(S_C1B));
+        VAD_LAUNCH_CHECK();
+        continue;
+      }
       VAD_TRY(dense_wgrad(dA, (int)rows, A2_CO[s3], cols[s3], g[s3].K(), G(2 * s3), G(2 * s3 + 1), scratch,
-                          scratch_floats, nullptr, st));
+                          scratch_floats, nullptr, st, 1024));
       if (s3 > 0) {
         VAD_TRY(dense_dgrad(dA, (int)rows, A2_CO[s3], P(2 * s3), g[s3].K(), dcols, nullptr, 1.f, nullptr, st));
         VAD_TRY(col2im3d(dcols, g[s3], dA, st));

@@ -802,7 +802,7 @@ struct AePlanImpl {
     xf = w.take<float>((int64_t)NF * AE_PIX);
     for (int l = 0; l < 4; ++l) {
       const int64_t M = ge[l].rows(), Co = ENC_CO[l];
-      ecols[l] = (direct && l > 0) ? nullptr : w.take<float>(M * ge[l].K());
+      ecols[l] = direct ? nullptr : w.take<float>(M * ge[l].K());
       ey[l] = w.take<float>(M * Co);
       ea[l] = w.take<float>(M * Co);
       est[l] = w.take<float>((int64_t)T * AE_ST * Co);
@@ -827,10 +827,10 @@ struct AePlanImpl {
       dx[j] = w.take<float>(rows * DEC_CI[j]);
       dy[j] = w.take<float>(gd[j].in.numel());
       max_act = std::max(max_act, std::max(gd[j].in.numel(), rows * DEC_CI[j]));
-      if (!direct || j == 3) max_cols = std::max(max_cols, rows * gd[j].K());
-      if (direct) {
+      if (!direct) max_cols = std::max(max_cols, rows * gd[j].K());
+      if (direct && j < 3) {
         dwc[j] = w.take<float>(16 * DEC_CI[j] * DEC_CO[j]);
-        dwk[j] = j < 3 ? w.take<float>(16 * DEC_CI[j] * DEC_CO[j]) : nullptr;
+        dwk[j] = w.take<float>(16 * DEC_CI[j] * DEC_CO[j]);
       }
       if (j < 3) {
         dst[j] = w.take<float>((int64_t)AE_ST * DEC_CO[j]);
@@ -910,9 +910,11 @@ struct AePlanImpl {
         for (int l = 1; l < 4; ++l) VAD_TRY(conv4_prep(P(L.enc_w[l]), ENC_CO[l], ENC_CI[l], ewk[l], ewc[l], st));
       for (int l = 0; l < 4; ++l) {
         const int64_t M = ge[l].rows();
-        if (direct && l > 0) {
+        if (direct && l == 0) {
+          VAD_TRY(conv4_c1_fwd(xf, NF, AE_HW, AE_HW, P(L.enc_w[0]), P(L.enc_b[0]), ey[0], st));
+        } else if (direct) {
           VAD_TRY(conv4_fwd(ea[l - 1], NF, ENC_IN[l], ENC_IN[l], ENC_CI[l], ewk[l], P(L.enc_b[l]), ENC_CO[l], ey[l],
-                            st));
+                            st, scratch, scratch_floats));
         } else {
           VAD_TRY(im2col3d(l == 0 ? xf : ea[l - 1], ndhwc_strides(ge[l].in), ge[l], nullptr, nullptr, 0, ecols[l],
                            st));
@@ -943,10 +945,13 @@ struct AePlanImpl {
       hipLaunchKernelGGL(ae_dec_in_kernel, grid_for((int64_t)B * AE_FLAT), dim3(256), 0, st, u, B, dx[0]);
       VAD_LAUNCH_CHECK();
       if (direct)
-        for (int j = 0; j < 4; ++j) VAD_TRY(conv4_prep(P(L.dec_w[j]), DEC_CI[j], DEC_CO[j], dwk[j], dwc[j], st));
+        for (int j = 0; j < 3; ++j) VAD_TRY(conv4_prep(P(L.dec_w[j]), DEC_CI[j], DEC_CO[j], dwk[j], dwc[j], st));
       for (int j = 0; j < 4; ++j) {
-        if (direct) {  // ConvTranspose2d j: four parity-class GEMMs, bias in the epilogue
-          VAD_TRY(conv4_cls(dx[j], B, DEC_IN[j], DEC_IN[j], DEC_CI[j], dwc[j], P(L.dec_b[j]), DEC_CO[j], dy[j], st));
+        if (direct && j == 3) {  // ConvTranspose2d(32, 1): 128 MACs per output pixel on the VALU
+          VAD_TRY(conv4_c1_tfwd(dx[3], B, DEC_IN[3], DEC_IN[3], P(L.dec_w[3]), P(L.dec_b[3]), dy[3], st));
+        } else if (direct) {  // ConvTranspose2d j: four parity-class GEMMs, bias in the epilogue
+          VAD_TRY(conv4_cls(dx[j], B, DEC_IN[j], DEC_IN[j], DEC_CI[j], dwc[j], P(L.dec_b[j]), DEC_CO[j], dy[j], st,
+                            scratch, scratch_floats));
         } else {
           // columns = X_j Wt (the transposed conv's GEMM), col2im + bias
           VAD_TRY(dense_dgrad(dx[j], (int)gd[j].rows(), DEC_CI[j], P(L.dec_w[j]), gd[j].K(), bcols, nullptr, 1.f,
@@ -998,12 +1003,16 @@ struct AePlanImpl {
     const float* dcur = dylast;
     for (int j = 3; j >= 0; --j) {
       const int M = (int)gd[j].rows(), K = gd[j].K(), Ci = DEC_CI[j];
-      if (direct && j < 3) {
+      if (direct && j == 3) {
+        VAD_TRY(conv4_c1_wgrad(dx[3], dcur, B, DEC_IN[3], DEC_IN[3], G(L.dec_w[3]), scratch, scratch_floats, st));
+        VAD_TRY(conv4_c1_fwd(dcur, B, 2 * DEC_IN[3], 2 * DEC_IN[3], P(L.dec_w[3]), nullptr, bufA, st));
+      } else if (direct) {
         int ns = 0;
         VAD_TRY(conv4_wgrad(dx[j], Ci, dcur, DEC_CO[j], B, DEC_IN[j], DEC_IN[j], scratch, &ns, scratch_floats,
                             g_ae_wgrad_blocks, st));
         VAD_TRY(conv4_wgrad_reduce(scratch, ns, Ci, DEC_CO[j], G(L.dec_w[j]), st));
-        VAD_TRY(conv4_fwd(dcur, B, 2 * DEC_IN[j], 2 * DEC_IN[j], DEC_CO[j], dwk[j], nullptr, Ci, bufA, st));
+        VAD_TRY(conv4_fwd(dcur, B, 2 * DEC_IN[j], 2 * DEC_IN[j], DEC_CO[j], dwk[j], nullptr, Ci, bufA, st, scratch,
+                          scratch_floats));
       } else {
         VAD_TRY(im2col3d(dcur, ndhwc_strides(gd[j].in), gd[j], nullptr, nullptr, 0, bcols, st));
         VAD_TRY(dense_wgrad(dx[j], M, Ci, bcols, K, G(L.dec_w[j]), nullptr, scratch, scratch_floats, nullptr, st));
@@ -1019,7 +1028,8 @@ struct AePlanImpl {
     hipLaunchKernelGGL(ae_dec_in_bwd_kernel, grid_for((int64_t)B * AE_FLAT), dim3(256), 0, st, bufA, u, B, dU);
     VAD_LAUNCH_CHECK();
     VAD_TRY(dense_wgrad(dU, B, AE_FLAT, seq, AE_LAT, G(L.dfc_w), G(L.dfc_b), scratch, scratch_floats, nullptr, st));
-    VAD_TRY(dense_dgrad(dU, B, AE_FLAT, P(L.dfc_w), AE_LAT, dseq, nullptr, 1.f, nullptr, st));
+    VAD_TRY(dense_dgrad(dU, B, AE_FLAT, P(L.dfc_w), AE_LAT, dseq, nullptr, 1.f, nullptr, st, 0, scratch,
+                        scratch_floats));
     if (d_seq) {
       hipLaunchKernelGGL(ae_add_kernel, grid_for((int64_t)B * AE_LAT), dim3(256), 0, st, dseq, d_seq,
                          (int64_t)B * AE_LAT);
@@ -1042,14 +1052,20 @@ struct AePlanImpl {
     // encoder, last layer first
     for (int l = 3; l >= 0; --l) {
       const int M = (int)ge[l].rows(), K = ge[l].K(), Co = ENC_CO[l];
-      if (direct && l > 0) {  // (the conv bias grad = sum of dY, from the BN backward's apply pass)
+      if (direct && l == 0) {  // Conv2d(1, 32): weight grad on the VALU, the bias grad from the BN backward
+        VAD_TRY(bn_bwd(bufA, ey[0], enc_bn(0), L.ebn_w[0], L.ebn_b[0], est[0], bufB, G(L.enc_b[0]), st));
+        VAD_TRY(conv4_c1_wgrad(bufB, xf, NF, ENC_IN[0] / 2, ENC_IN[0] / 2, G(L.enc_w[0]), scratch, scratch_floats,
+                               st));
+        continue;
+      }
+      if (direct) {  // (the conv bias grad = sum of dY, from the BN backward's apply pass)
         const int OH = ENC_IN[l] / 2;
         int ns = 0;
         VAD_TRY(bn_bwd(bufA, ey[l], enc_bn(l), L.ebn_w[l], L.ebn_b[l], est[l], bufB, G(L.enc_b[l]), st));
         VAD_TRY(conv4_wgrad(bufB, Co, ea[l - 1], ENC_CI[l], NF, OH, OH, scratch, &ns, scratch_floats,
                             g_ae_wgrad_blocks, st));
         VAD_TRY(conv4_wgrad_reduce(scratch, ns, Co, ENC_CI[l], G(L.enc_w[l]), st));
-        VAD_TRY(conv4_cls(bufB, NF, OH, OH, Co, ewc[l], nullptr, ENC_CI[l], bufA, st));
+        VAD_TRY(conv4_cls(bufB, NF, OH, OH, Co, ewc[l], nullptr, ENC_CI[l], bufA, st, scratch, scratch_floats));
         continue;
       }
       VAD_TRY(bn_bwd(bufA, ey[l], enc_bn(l), L.ebn_w[l], L.ebn_b[l], est[l], bufB, nullptr, st));

@@ -211,8 +211,10 @@ int dense_fwd_splitk(const float* X, int M, int K, const float* W, int N, float*
                      int* nsplit, hipStream_t st);
 // dX = (dY W) * gate', where gate' = (gate > 0 ? gscale : 0) when gate != nullptr; gate_rows > 0: row m is gated by
 // gate row m % gate_rows
+// scratch (nullable): split-K slabs when the output has few tiles and the reduction is long
 int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX, const float* gate, float gscale,
-                const int* skip, hipStream_t st, int gate_rows = 0);
+                const int* skip, hipStream_t st, int gate_rows = 0, float* scratch = nullptr,
+                int64_t scratch_floats = 0);
 // dW = dY^T X, db = colsum(dY) (written, not accumulated)
 // target_blocks: split-K blocks to aim for (256: one per CU; tall-M weight gradients want several per CU to hide latency)
 int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW, float* db, float* scratch,
@@ -221,13 +223,21 @@ int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW,
 // ---------------------------------------------------------------- 4x4 / stride-2 / pad-1 convs (cad1's autoencoder)
 // implicit GEMMs over NHWC frames, no im2col (backbone.hip: the layouts and the parity classes)
 int conv4_prep(const float* w, int D0, int D1, float* wk, float* wc, hipStream_t st);  // wk / wc nullable
+// scratch (nullable): split-K slabs for grids that leave most CUs idle
 int conv4_fwd(const float* src, int NF, int H, int W, int C, const float* wk, const float* bias, int N, float* out,
-              hipStream_t st);
+              hipStream_t st, float* scratch = nullptr, int64_t scratch_floats = 0);
 int conv4_cls(const float* src, int NF, int SH, int SW, int C, const float* wc, const float* bias, int N, float* out,
-              hipStream_t st);
+              hipStream_t st, float* scratch = nullptr, int64_t scratch_floats = 0);
 int conv4_wgrad(const float* A, int R, const float* src, int C, int NF, int AH, int AW, float* part, int* nsplit,
                 int64_t part_cap, int target_blocks, hipStream_t st);
 int conv4_wgrad_reduce(const float* part, int S, int R, int C, float* dW, hipStream_t st);
+// the single-channel ends, 32 channels on the other side, on the VALU: w = the [32][1][4][4] / [32][16] weight
+int conv4_c1_fwd(const float* src, int NF, int H, int W, const float* w, const float* bias, float* out,
+                 hipStream_t st);
+int conv4_c1_tfwd(const float* src, int NF, int SH, int SW, const float* w, const float* bias, float* out,
+                  hipStream_t st);
+int conv4_c1_wgrad(const float* A, const float* src, int NF, int AH, int AW, float* dW, float* slab,
+                   int64_t slab_floats, hipStream_t st);
 
 // conv GEMM tuning knobs: conv_fwd_tile / conv_dgrad_tile / conv_wgrad_tile (tile id, -1 = heuristic),
 // conv_wgrad_blocks, conv_wgrad_min_ktiles

@@ -1092,6 +1092,7 @@ static ConvTuning g_tune;
 
 extern int g_bbox_im2col;  // bbox_plan.hip
 extern int g_ae_direct, g_ae_wgrad_blocks;  // ae_plan.hip
+extern int g_a2_direct;                     // a2_plan.hip
 int set_tuning(const char* key, int value) {
   const std::string k(key);
   if (k == "conv_fwd_tile") g_tune.fwd = value;
@@ -1119,6 +1120,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "bbox_im2col") g_bbox_im2col = value;
   else if (k == "ae_direct") g_ae_direct = value;
   else if (k == "ae_wgrad_blocks") g_ae_wgrad_blocks = value;
+  else if (k == "a2_direct") g_a2_direct = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "cad_dir_affine") g_cad_dir_affine = value;
@@ -1771,7 +1773,7 @@ int dense_fwd_splitk(const float* X, int M, int K, const float* W, int N, float*
 }
 
 int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX, const float* gate, float gscale,
-                const int* skip, hipStream_t st, int gate_rows) {
+                const int* skip, hipStream_t st, int gate_rows, float* scratch, int64_t scratch_floats) {
   // dX[m][k] = sum_n dY[m][n] W[n][k]: A = dY (KC over n), B(row k, red n) = W[n][k] (KM, ld K)
   using C = T64x64;
   DenseEpiArgs pe{dX, K, nullptr, 0, 0, 0, 0, 1.f, 0, gate, gscale, gate_rows};
@@ -1788,6 +1790,23 @@ int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX,
   }
   DenseKC<C::BM>::Params pa{dY, N, M, N};
   DenseKM<C::BN>::Params pb{W, K, K, N, -1};
+  // few output tiles and a long reduction (e.g. cad1's Linear(64, 2048) input gradient: one tile, N = 2048): split-K
+  // slabs in scratch when the caller gives one, summed in order with the gate by dense_splitk_reduce
+  const int64_t tiles = cdiv(M, C::BM) * cdiv(K, C::BN);
+  if (scratch && tiles < 64 && N >= 8 * BK) {
+    int splits = (int)std::min<int64_t>(cdiv(256, tiles), N / (4 * BK));
+    while (splits > 1 && (int64_t)splits * M * K > scratch_floats) splits /= 2;
+    if (splits > 1) {
+      int used = 1;
+      EpiPartial::Params pp{scratch, K};
+      VAD_TRY((launch_gemm<C, DenseKC, DenseKM, EpiPartial>(pa, pb, pp, M, K, N, splits, skip, st, &used)));
+      const int64_t total = (int64_t)M * K;
+      hipLaunchKernelGGL(dense_splitk_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 1024)),
+                         dim3(256), 0, st, scratch, used, M, K, pe, skip);
+      VAD_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   return launch_gemm<C, DenseKC, DenseKM, EpiDense>(pa, pb, pe, M, K, N, 1, skip, st);
 }
 
@@ -1855,8 +1874,18 @@ int conv4_prep(const float* w, int D0, int D1, float* wk, float* wc, hipStream_t
   return 0;
 }
 
+// split-K when the tile grid leaves most CUs idle (the decoder's 4x4 / 8x8 frames): slabs [S][M][N] in scratch, summed
+// in order (+ bias) by dense_splitk_reduce / conv4_cls_reduce
+static int conv4_splits(int M, int N, int K, int64_t scratch_floats) {
+  const int64_t tiles = cdiv(M, 64) * cdiv(N, 64);
+  if (tiles >= 512 || scratch_floats <= 0) return 1;
+  int s = (int)std::min<int64_t>(cdiv(1024, tiles), K / (2 * BK));
+  while (s > 1 && (int64_t)s * M * N > scratch_floats) s /= 2;
+  return std::max(1, s);
+}
+
 int conv4_fwd(const float* src, int NF, int H, int W, int C, const float* wk, const float* bias, int N, float* out,
-              hipStream_t st) {
+              hipStream_t st, float* scratch, int64_t scratch_floats) {
   VAD_CHECK(C % 32 == 0 && H % 2 == 0 && W % 2 == 0 && N >= 1, "conv4_fwd: C % 32 == 0, even frames");
   const int OH = H / 2, OW = W / 2;
   const ConvGeom g{NF, OH, OW, 2, 2, H, W, C};
@@ -1868,6 +1897,19 @@ int conv4_fwd(const float* src, int NF, int H, int W, int C, const float* wk, co
   }
   const int M = NF * OH * OW, K = 16 * C;
   const DenseEpiArgs pe{out, N, bias, 0, 0, 0, 0, 1.f, 0, nullptr, 1.f};
+  const int splits = conv4_splits(M, N, K, scratch_floats);
+  if (splits > 1) {
+    int used = 1;
+    typename ConvGatherKC<64>::Params pa{src, g, taps, nullptr, nullptr};
+    typename DenseKC<64>::Params pb{wk, K, N, K};
+    const EpiPartial::Params pp{scratch, N};
+    VAD_TRY((launch_gemm<T64x64, ConvGatherKC, DenseKC, EpiPartial>(pa, pb, pp, M, N, K, splits, nullptr, st, &used)));
+    const int64_t total = (int64_t)M * N;
+    hipLaunchKernelGGL(dense_splitk_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 1024)),
+                       dim3(256), 0, st, scratch, used, M, N, pe, nullptr);
+    VAD_LAUNCH_CHECK();
+    return 0;
+  }
   return with_tile(pick_fwd_tile(M, N), [&](auto cfg) -> int {
     using Cf = decltype(cfg);
     typename ConvGatherKC<Cf::BM>::Params pa{src, g, taps, nullptr, nullptr};
@@ -1876,8 +1918,26 @@ int conv4_fwd(const float* src, int NF, int H, int W, int C, const float* wk, co
   });
 }
 
+// out[img][2a + py][2b + px][n] = bias[n] + sum over the slabs of part[s][(img SH + a) SW + b][n]
+__global__ __launch_bounds__(256) void conv4_cls_reduce_kernel(const float* __restrict__ part, int S, int M, int SH,
+                                                               int SW, int N, int py, int px,
+                                                               const float* __restrict__ bias, float* __restrict__ out) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    float v = 0.f;
+    for (int z = 0; z < S; ++z) v += part[(int64_t)z * total + i];
+    const int n = (int)(i % N);
+    const int64_t m = i / N;
+    const int b = (int)(m % SW);
+    const int64_t ia = m / SW;
+    const int a = (int)(ia % SH);
+    const int64_t img = ia / SH;
+    out[((img * 2 * SH + 2 * a + py) * 2 * SW + 2 * b + px) * N + n] = v + (bias ? bias[n] : 0.f);
+  }
+}
+
 int conv4_cls(const float* src, int NF, int SH, int SW, int C, const float* wc, const float* bias, int N, float* out,
-              hipStream_t st) {
+              hipStream_t st, float* scratch, int64_t scratch_floats) {
   VAD_CHECK(C % 32 == 0 && N >= 1, "conv4_cls: C % 32 == 0");
   for (int cls = 0; cls < 4; ++cls) {
     const int py = cls >> 1, px = cls & 1;
@@ -1889,6 +1949,21 @@ int conv4_cls(const float* src, int NF, int SH, int SW, int C, const float* wc, 
         taps.dh[2 * r + q] = (int8_t)(py == 0 ? -r : 1 - r);
         taps.dw[2 * r + q] = (int8_t)(px == 0 ? -q : 1 - q);
       }
+    const int M = NF * SH * SW, K = 4 * C;
+    const int splits = conv4_splits(M, N, K, scratch_floats);
+    if (splits > 1) {
+      int used = 1;
+      typename ConvGatherKC<64>::Params pa{src, g, taps, nullptr, nullptr};
+      typename DenseKC<64>::Params pb{wc + (int64_t)cls * N * 4 * C, K, N, K};
+      const EpiPartial::Params pp{scratch, N};
+      VAD_TRY((launch_gemm<T64x64, ConvGatherKC, DenseKC, EpiPartial>(pa, pb, pp, M, N, K, splits, nullptr, st,
+                                                                     &used)));
+      const int64_t total = (int64_t)M * N;
+      hipLaunchKernelGGL(conv4_cls_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 1024)),
+                         dim3(256), 0, st, scratch, used, M, SH, SW, N, py, px, bias, out);
+      VAD_LAUNCH_CHECK();
+      continue;
+    }
     const EpiConvDgrad::Params pe{out, SH, SW, 2, py, 2, px, 2 * SH, 2 * SW, N, bias};
     VAD_TRY(dgrad_launch(g, taps, src, wc + (int64_t)cls * N * 4 * C, N, pe, st));
   }
@@ -1925,12 +2000,191 @@ __global__ __launch_bounds__(256) void conv4_wgrad_reduce_kernel(const float* __
   }
 }
 
+// the same for small outputs with many slabs: 4 entries per block, 64 lanes each adding slabs lane, lane + 64, ... in
+// order, then a fixed butterfly
+__global__ __launch_bounds__(256) void conv4_wgrad_reduce_small_kernel(const float* __restrict__ part, int S, int R,
+                                                                       int C, float* __restrict__ dW) {
+  const int64_t total = (int64_t)R * 16 * C;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  float v = 0.f;
+  if (i < total)
+    for (int z = lane; z < S; z += 64) v += part[(int64_t)z * total + i];
+  v = wave_sum(v);
+  if (lane == 0 && i < total) {
+    const int c = (int)(i % C), tap = (int)((i / C) % 16);
+    const int64_t r = i / (16 * C);
+    dW[(r * C + c) * 16 + tap] = v;
+  }
+}
+
 int conv4_wgrad_reduce(const float* part, int S, int R, int C, float* dW, hipStream_t st) {
   const int64_t total = (int64_t)R * 16 * C;
+  if (total <= 65536 && S >= 64) {
+    hipLaunchKernelGGL(conv4_wgrad_reduce_small_kernel, dim3((unsigned)cdiv(total, 4)), dim3(256), 0, st, part, S, R, C,
+                       dW);
+    VAD_LAUNCH_CHECK();
+    return 0;
+  }
   hipLaunchKernelGGL(conv4_wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 2048)), dim3(256), 0,
                      st, part, S, R, C, dW);
   VAD_LAUNCH_CHECK();
   return 0;
+}
+
+// ---------------------------------------------------------------- the single-channel ends (cad1:131, cad1:185)
+// conv4_c1_fwd  out[p][n] = sum_tap src[2a - 1 + ky][2b - 1 + kx] w[n][tap] (+ bias[n]), 1-channel NHWC source, 32
+//               outputs per pixel on the VALU (Conv2d(1, 32) forward; ConvTranspose2d(32, 1) input gradient with
+//               src = dY, w = the [32][1][4][4] weight)
+// conv4_c1_tfwd out[2a + py][2b + px] = bias + sum over the class taps and the 32 source channels (ConvTranspose2d(32,
+//               1) forward)
+// conv4_c1_wgrad slab[block][r][tap] = sum over the block's pixels p of A[p][r] src[2a - 1 + ky][2b - 1 + kx] (r < 32;
+//               Conv2d(1, 32): A = dY; ConvTranspose2d(32, 1): A = X, src = dY)
+__global__ __launch_bounds__(256) void conv4_c1_fwd_kernel(const float* __restrict__ src, int NF, int H, int W,
+                                                           const float* __restrict__ w, const float* __restrict__ bias,
+                                                           float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float ws[16][32];  // [tap][n]
+  for (int i = threadIdx.x; i < 512; i += 256) ws[i % 16][i / 16] = w[i];
+  __syncthreads();
+  const int OH = H / 2, OW = W / 2;
+  const int64_t total = (int64_t)NF * OH * OW;
+  for (int64_t p = blockIdx.x * 256ll + threadIdx.x; p < total; p += (int64_t)gridDim.x * 256) {
+    const int ox = (int)(p % OW);
+    const int64_t r = p / OW;
+    const int oy = (int)(r % OH);
+    const float* img = src + (r / OH) * H * W;
+    float x[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int iy = 2 * oy - 1 + t / 4, ix = 2 * ox - 1 + t % 4;
+      x[t] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? img[iy * W + ix] : 0.f;
+    }
+    float* o = out + p * 32;
+#pragma unroll
+    for (int n4 = 0; n4 < 8; ++n4) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const f32x4 wv = *reinterpret_cast<const f32x4*>(&ws[t][4 * n4]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = fmaf(x[t], wv[e], acc[e]);
+      }
+      if (bias) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += bias[4 * n4 + e];
+      }
+      *reinterpret_cast<f32x4*>(o + 4 * n4) = acc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void conv4_c1_tfwd_kernel(const float* __restrict__ src, int NF, int SH, int SW,
+                                                            const float* __restrict__ w, const float* __restrict__ bias,
+                                                            float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float ws[16][32];  // [tap][source channel]
+  for (int i = threadIdx.x; i < 512; i += 256) ws[i % 16][i / 16] = w[i];
+  __syncthreads();
+  const int OH = 2 * SH, OW = 2 * SW;
+  const int64_t total = (int64_t)NF * OH * OW;
+  const float b0 = bias ? bias[0] : 0.f;
+  for (int64_t p = blockIdx.x * 256ll + threadIdx.x; p < total; p += (int64_t)gridDim.x * 256) {
+    const int ox = (int)(p % OW);
+    const int64_t r = p / OW;
+    const int oy = (int)(r % OH);
+    const int64_t img = r / OH;
+    const int py = oy & 1, px = ox & 1, a = oy >> 1, b = ox >> 1;
+    float acc = 0.f;
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int sy = a + (py == 0 ? -rr : 1 - rr), sx = b + (px == 0 ? -q : 1 - q);
+        if (sy < 0 || sy >= SH || sx < 0 || sx >= SW) continue;
+        const int ky = py == 0 ? 1 + 2 * rr : 2 * rr, kx = px == 0 ? 1 + 2 * q : 2 * q;
+        const float* xs = src + ((img * SH + sy) * SW + sx) * 32;
+        const float* wt = ws[ky * 4 + kx];
+#pragma unroll
+        for (int c4 = 0; c4 < 8; ++c4) {
+          const f32x4 xv = *reinterpret_cast<const f32x4*>(xs + 4 * c4);
+          const f32x4 wv = *reinterpret_cast<const f32x4*>(wt + 4 * c4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc = fmaf(xv[e], wv[e], acc);
+        }
+      }
+    out[p] = acc + b0;
+  }
+}
+
+constexpr int C1_CHUNK = 128;  // pixels per staging round of conv4_c1_wgrad_kernel
+
+__global__ __launch_bounds__(256) void conv4_c1_wgrad_kernel(const float* __restrict__ A, const float* __restrict__ src,
+                                                             int NF, int AH, int AW, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) float as[C1_CHUNK][33];
+  __shared__ float xs[C1_CHUNK][17];
+  const int H = 2 * AH, W = 2 * AW;
+  const int64_t total = (int64_t)NF * AH * AW;
+  const int t = threadIdx.x, r = t & 31, tp = (t >> 5) * 2;
+  float acc0 = 0.f, acc1 = 0.f;
+  for (int64_t p0 = (int64_t)blockIdx.x * C1_CHUNK; p0 < total; p0 += (int64_t)gridDim.x * C1_CHUNK) {
+    __syncthreads();
+    for (int i = t; i < C1_CHUNK * 8; i += 256) {  // A rows: 8 float4 per pixel
+      const int pp = i >> 3, c4 = i & 7;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (p0 + pp < total) v = *reinterpret_cast<const f32x4*>(A + (p0 + pp) * 32 + 4 * c4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) as[pp][4 * c4 + e] = v[e];
+    }
+    for (int i = t; i < C1_CHUNK * 16; i += 256) {  // patches
+      const int pp = i >> 4, tap = i & 15;
+      float v = 0.f;
+      const int64_t p = p0 + pp;
+      if (p < total) {
+        const int ox = (int)(p % AW);
+        const int64_t rr = p / AW;
+        const int oy = (int)(rr % AH);
+        const int iy = 2 * oy - 1 + tap / 4, ix = 2 * ox - 1 + tap % 4;
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = src[((rr / AH) * H + iy) * W + ix];
+      }
+      xs[pp][tap] = v;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int pp = 0; pp < C1_CHUNK; ++pp) {
+      const float a = as[pp][r];
+      acc0 = fmaf(a, xs[pp][tp], acc0);
+      acc1 = fmaf(a, xs[pp][tp + 1], acc1);
+    }
+  }
+  slab[(int64_t)blockIdx.x * 512 + r * 16 + tp] = acc0;
+  slab[(int64_t)blockIdx.x * 512 + r * 16 + tp + 1] = acc1;
+}
+
+int conv4_c1_fwd(const float* src, int NF, int H, int W, const float* w, const float* bias, float* out,
+                 hipStream_t st) {
+  VAD_CHECK(H % 2 == 0 && W % 2 == 0, "conv4_c1_fwd: even frames");
+  const int64_t total = (int64_t)NF * (H / 2) * (W / 2);
+  hipLaunchKernelGGL(conv4_c1_fwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 4096)), dim3(256), 0, st,
+                     src, NF, H, W, w, bias, out);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int conv4_c1_tfwd(const float* src, int NF, int SH, int SW, const float* w, const float* bias, float* out,
+                  hipStream_t st) {
+  const int64_t total = (int64_t)NF * 4 * SH * SW;
+  hipLaunchKernelGGL(conv4_c1_tfwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 4096)), dim3(256), 0, st,
+                     src, NF, SH, SW, w, bias, out);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int conv4_c1_wgrad(const float* A, const float* src, int NF, int AH, int AW, float* dW, float* slab,
+                   int64_t slab_floats, hipStream_t st) {
+  const int64_t total = (int64_t)NF * AH * AW;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>({cdiv(total, 4 * C1_CHUNK), 512, slab_floats / 512}));
+  hipLaunchKernelGGL(conv4_c1_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, A, src, NF, AH, AW, slab);
+  VAD_LAUNCH_CHECK();
+  return conv4_wgrad_reduce(slab, blocks, 32, 1, dW, st);
 }
 
 }  // namespace vad

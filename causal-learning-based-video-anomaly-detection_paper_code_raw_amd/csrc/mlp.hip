@@ -235,12 +235,21 @@ __global__ __launch_bounds__(256) void rows_wgrad_kernel(const RowsWgradArgs a) 
   const int R = a.R;
   const int per = (R + 3) / 4;
   const int r0 = wave * per, r1 = min(R, r0 + per);
-  for (int rb = r0; rb < r1; rb += 2) {  // wave-uniform trip count; row rb + h, zero past the share
-    const int r = rb + h;
-    const bool ok = r < r1;
-    const float av = (ok && o < sg.O) ? sg.A[(int64_t)r * sg.O + o] : 0.f;
-    const float xv = !ok ? 0.f : (i < sg.I ? sg.X[(int64_t)r * sg.I + i] : (i == sg.I ? 1.f : 0.f));
-    acc = mfma32(av, xv, acc);
+  // wave-uniform trip count; row rb + 2u + h, zero past the share.  8 row pairs per batch: every load of the batch is
+  // issued before its MFMAs (one load pair per MFMA left each MFMA waiting on an L2 round trip: the 640-row GRU / ReID
+  // segments took 65 us); the MFMAs run in the same row order as one pair at a time (bit-identical)
+  for (int rb = r0; rb < r1; rb += 16) {
+    float av[8], xv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = rb + 2 * u + h;
+      const bool ok = r < r1;
+      av[u] = (ok && o < sg.O) ? sg.A[(int64_t)r * sg.O + o] : 0.f;
+      xv[u] = !ok ? 0.f : (i < sg.I ? sg.X[(int64_t)r * sg.I + i] : (i == sg.I ? 1.f : 0.f));
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (rb + 2 * u < r1) acc = mfma32(av[u], xv[u], acc);
   }
   __shared__ float red[4][16][64];
 #pragma unroll

@@ -1,0 +1,15 @@
+# round 5: a2 head / loss as multi-block launches; cad1 split-K small GEMMs + single-channel VALU ends; rows_wgrad batched
+# loads; dense_dgrad split-K: the kernel, cad, a2 and cad1 GPU tests, then a2 / cad1 / config-2 benches and kernel stats
+set -o pipefail
+mkdir -p gpurun_out
+ROOT=$(pwd)
+timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_a2_gpu.py tests/test_ae_gpu.py tests/test_cad_gpu.py -m gpu -x -q --timeout 280 --timeout-method thread > gpurun_out/r05k_tests.log 2>&1 || exit 1
+timeout -k 10 200 python bench.py --config a2 --steps 30 --cpu-seconds 8 > gpurun_out/r05k_a2.log 2>&1 || exit 1
+timeout -k 10 200 python bench.py --config cad1 --steps 30 --cpu-seconds 8 > gpurun_out/r05k_cad1.log 2>&1 || exit 1
+timeout -k 10 200 python bench.py --no-cpu-baseline --h2d-steps 0 --steps 40 > gpurun_out/r05k_cfg2.log 2>&1 || exit 1
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+  -d $ROOT/gpurun_out/r05k_a2 -o run -- python3 $ROOT/bench.py --config a2 --no-cpu-baseline --steps 10 \
+  --warmup 3 > $ROOT/gpurun_out/r05k_a2_prof.log 2>&1) || exit 1
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+  -d $ROOT/gpurun_out/r05k_cad1 -o run -- python3 $ROOT/bench.py --config cad1 --no-cpu-baseline --steps 10 \
+  --warmup 3 > $ROOT/gpurun_out/r05k_cad1_prof.log 2>&1) || exit 1
