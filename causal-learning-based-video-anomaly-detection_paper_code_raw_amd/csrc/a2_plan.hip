@@ -393,106 +393,146 @@ __global__ __launch_bounds__(256) void a2_head_bwd_kernel(A2HeadBwdArgs a, int s
 // ------------------------------------------------------------------ conv3d_1 (3 -> 16, k3, stride (1, 2, 2), p1) direct
 // (knob "a2_direct", latched per plan; 0: im2col + GEMM).  With 3 input channels the im2col matrix (K = 81) is 6.75x
 // the clip and the GEMM runs 16-wide tiles, so the first conv and its weight gradient run on the VALU from the clip
-// itself (NCDHW):
-//   a2_conv1_fwd   one thread per output voxel: its 3 x 27 inputs x the [81][16] weights (LDS broadcast rows), + bias,
-//                  ReLU, 16 channels out (NDHWC)
-//   a2_conv1_wgrad per block, 64-voxel chunks of the gated dY rows and of the 81-entry input patches in LDS; thread
-//                  (co, tap group) owns up to 6 of the 82 (tap, + the bias "ones" tap) sums; per-block slabs summed
-//                  in fixed order by a2_conv1_wgrad_reduce (64 lanes per entry)
-constexpr int A2C1_TAPS = 81, A2C1_CHUNK = 64;
+// itself (NCDHW), over 2 x 8 x 16-voxel output tiles whose 3 x 4 x 17 x 33 input halo is staged in LDS (coalesced
+// rows):
+//   a2_conv1_fwd   one thread per output voxel: its 81 halo inputs x the [81][16] weights (LDS broadcast rows),
+//                  + bias, ReLU, 16 channels out (NDHWC)
+//   a2_conv1_wgrad thread (co, tap group) owns up to 6 of the 82 (ci, tap) / bias sums and walks the tile's 256 voxels
+//                  (the gated dY tile in LDS beside the halo); per-block slabs summed in fixed order by
+//                  a2_conv1_wgrad_reduce (64 lanes per entry)
+constexpr int A2C1_TAPS = 81, A2T_D = 2, A2T_H = 8, A2T_W = 16;
+constexpr int A2H_D = A2T_D + 2, A2H_H = 2 * A2T_H + 1, A2H_W = 2 * A2T_W + 1, A2_HALO = A2H_D * A2H_H * A2H_W;
+
+struct A2Tiles {
+  int T, H, W, OH, OW, td, th, tw;
+  int64_t n;
+  __host__ __device__ A2Tiles(int B, int T_, int H_, int W_) : T(T_), H(H_), W(W_) {
+    OH = (H - 1) / 2 + 1;
+    OW = (W - 1) / 2 + 1;
+    td = (T + A2T_D - 1) / A2T_D;
+    th = (OH + A2T_H - 1) / A2T_H;
+    tw = (OW + A2T_W - 1) / A2T_W;
+    n = (int64_t)B * td * th * tw;
+  }
+};
+
+// the tile's input halo xs[ci][hd][hh][hw] = x[b][ci][d0 - 1 + hd][2 h0 - 1 + hh][2 w0 - 1 + hw] (0 outside)
+__device__ __forceinline__ void a2_stage_halo(float* xs, const float* __restrict__ x, const A2Tiles& g, int64_t b,
+                                              int d0, int h0, int w0) {
+  for (int i = threadIdx.x; i < 3 * A2H_D * A2H_H * A2H_W; i += 256) {
+    const int hw = i % A2H_W, r = i / A2H_W, hh = r % A2H_H, r2 = r / A2H_H, hd = r2 % A2H_D, ci = r2 / A2H_D;
+    const int id = d0 - 1 + hd, ih = 2 * h0 - 1 + hh, iw = 2 * w0 - 1 + hw;
+    float v = 0.f;
+    if (id >= 0 && id < g.T && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
+      v = x[(((b * 3 + ci) * g.T + id) * g.H + ih) * (int64_t)g.W + iw];
+    xs[i] = v;
+  }
+}
 
 __global__ __launch_bounds__(256) void a2_conv1_fwd_kernel(const float* __restrict__ x, int B, int T, int H, int W,
                                                            const float* __restrict__ w, const float* __restrict__ bias,
                                                            float* __restrict__ y) {
   __shared__ __attribute__((aligned(16))) float ws[A2C1_TAPS][16];  // [ci*27 + tap][co]
+  __shared__ float xs[3 * A2_HALO];
   for (int i = threadIdx.x; i < 16 * A2C1_TAPS; i += 256) ws[i % A2C1_TAPS][i / A2C1_TAPS] = w[i];
-  __syncthreads();
-  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
-  const int64_t total = (int64_t)B * T * OH * OW;
-  for (int64_t p = blockIdx.x * 256ll + threadIdx.x; p < total; p += (int64_t)gridDim.x * 256) {
-    const int ow = (int)(p % OW);
-    int64_t r = p / OW;
-    const int oh = (int)(r % OH);
-    r /= OH;
-    const int d = (int)(r % T);
-    const int64_t b = r / T;
+  const A2Tiles g(B, T, H, W);
+  const int v = threadIdx.x, vd = v / (A2T_H * A2T_W), vh = (v / A2T_W) % A2T_H, vw = v % A2T_W;
+  for (int64_t tile = blockIdx.x; tile < g.n; tile += gridDim.x) {
+    const int bw = (int)(tile % g.tw);
+    int64_t r = tile / g.tw;
+    const int bh = (int)(r % g.th);
+    r /= g.th;
+    const int bd = (int)(r % g.td);
+    const int64_t b = r / g.td;
+    const int d0 = bd * A2T_D, h0 = bh * A2T_H, w0 = bw * A2T_W;
+    __syncthreads();
+    a2_stage_halo(xs, x, g, b, d0, h0, w0);
+    __syncthreads();
+    const int d = d0 + vd, oh = h0 + vh, ow = w0 + vw;
+    if (d >= T || oh >= g.OH || ow >= g.OW) continue;
     f32x4 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int ci = 0; ci < 3; ++ci) {
-      const float* xc = x + (b * 3 + ci) * T * H * W;
+#pragma unroll
+    for (int ci = 0; ci < 3; ++ci)
 #pragma unroll
       for (int t = 0; t < 27; ++t) {
-        const int id = d - 1 + t / 9, ih = 2 * oh - 1 + (t / 3) % 3, iw = 2 * ow - 1 + t % 3;
-        const bool in = id >= 0 && id < T && ih >= 0 && ih < H && iw >= 0 && iw < W;
-        const float v = in ? xc[((int64_t)id * H + ih) * W + iw] : 0.f;
+        const float xv = xs[((ci * A2H_D + vd + t / 9) * A2H_H + 2 * vh + (t / 3) % 3) * A2H_W + 2 * vw + t % 3];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const f32x4 wv = *reinterpret_cast<const f32x4*>(&ws[ci * 27 + t][4 * q]);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[q][e] = fmaf(v, wv[e], acc[q][e]);
+          for (int e = 0; e < 4; ++e) acc[q][e] = fmaf(xv, wv[e], acc[q][e]);
         }
       }
-    }
-    float* o = y + p * 16;
+    float* o = y + (((b * T + d) * g.OH + oh) * (int64_t)g.OW + ow) * 16;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      f32x4 v;
+      f32x4 ov;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = relu_nan(acc[q][e] + bias[4 * q + e]);
-      *reinterpret_cast<f32x4*>(o + 4 * q) = v;
+      for (int e = 0; e < 4; ++e) ov[e] = relu_nan(acc[q][e] + bias[4 * q + e]);
+      *reinterpret_cast<f32x4*>(o + 4 * q) = ov;
     }
   }
 }
 
 __global__ __launch_bounds__(256) void a2_conv1_wgrad_kernel(const float* __restrict__ dA, const float* __restrict__ x,
                                                              int B, int T, int H, int W, float* __restrict__ slab) {
-  __shared__ float as[A2C1_CHUNK][17];
-  __shared__ float xs[A2C1_CHUNK][A2C1_TAPS + 1];
-  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
-  const int64_t total = (int64_t)B * T * OH * OW;
-  const int tid = threadIdx.x, co = tid & 15, g = tid >> 4;
-  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int64_t p0 = (int64_t)blockIdx.x * A2C1_CHUNK; p0 < total; p0 += (int64_t)gridDim.x * A2C1_CHUNK) {
-    __syncthreads();
-    for (int i = tid; i < A2C1_CHUNK * 16; i += 256) {
-      const int pp = i >> 4;
-      as[pp][i & 15] = p0 + pp < total ? dA[(p0 + pp) * 16 + (i & 15)] : 0.f;
-    }
-    for (int i = tid; i < A2C1_CHUNK * (A2C1_TAPS + 1); i += 256) {
-      const int pp = i / (A2C1_TAPS + 1), j = i % (A2C1_TAPS + 1);
-      const int64_t p = p0 + pp;
-      float v = 0.f;
-      if (p < total) {
-        if (j == A2C1_TAPS) {
-          v = 1.f;  // (the conv bias)
-        } else {
-          const int ci = j / 27, t = j % 27;
-          const int ow = (int)(p % OW);
-          int64_t r = p / OW;
-          const int oh = (int)(r % OH);
-          r /= OH;
-          const int d = (int)(r % T);
-          const int64_t b = r / T;
-          const int id = d - 1 + t / 9, ih = 2 * oh - 1 + (t / 3) % 3, iw = 2 * ow - 1 + t % 3;
-          if (id >= 0 && id < T && ih >= 0 && ih < H && iw >= 0 && iw < W)
-            v = x[(((b * 3 + ci) * T + id) * H + ih) * W + iw];
-        }
-      }
-      xs[pp][j] = v;
-    }
-    __syncthreads();
-    for (int pp = 0; pp < A2C1_CHUNK; ++pp) {
-      const float a = as[pp][co];
+  __shared__ float xs[3 * A2_HALO];
+  __shared__ float as[256][17];
+  const A2Tiles g(B, T, H, W);
+  const int tid = threadIdx.x, co = tid & 15, grp = tid >> 4;
+  int off[6];  // per owned pair: its halo offset at voxel (0, 0, 0), -1 = the bias pair, -2 = none
 #pragma unroll
-      for (int m = 0; m < 6; ++m)
-        if (g + 16 * m <= A2C1_TAPS) acc[m] = fmaf(a, xs[pp][g + 16 * m], acc[m]);
+  for (int m = 0; m < 6; ++m) {
+    const int j = grp + 16 * m;
+    if (j > A2C1_TAPS) off[m] = -2;
+    else if (j == A2C1_TAPS) off[m] = -1;
+    else {
+      const int ci = j / 27, t = j % 27;
+      off[m] = ((ci * A2H_D + t / 9) * A2H_H + (t / 3) % 3) * A2H_W + t % 3;
+    }
+  }
+  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t tile = blockIdx.x; tile < g.n; tile += gridDim.x) {
+    const int bw = (int)(tile % g.tw);
+    int64_t r = tile / g.tw;
+    const int bh = (int)(r % g.th);
+    r /= g.th;
+    const int bd = (int)(r % g.td);
+    const int64_t b = r / g.td;
+    const int d0 = bd * A2T_D, h0 = bh * A2T_H, w0 = bw * A2T_W;
+    __syncthreads();
+    a2_stage_halo(xs, x, g, b, d0, h0, w0);
+    {  // the gated dY rows of the tile's voxels (zero outside the volume)
+      const int vd = tid / (A2T_H * A2T_W), vh = (tid / A2T_W) % A2T_H, vw = tid % A2T_W;
+      const int d = d0 + vd, oh = h0 + vh, ow = w0 + vw;
+      const bool ok = d < T && oh < g.OH && ow < g.OW;
+      const float* row = dA + (((b * T + d) * g.OH + oh) * (int64_t)g.OW + ow) * 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v4 = ok ? *reinterpret_cast<const f32x4*>(row + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) as[tid][4 * q + e] = v4[e];
+      }
+    }
+    __syncthreads();
+    for (int v = 0; v < 256; ++v) {
+      const int vd = v / (A2T_H * A2T_W), vh = (v / A2T_W) % A2T_H, vw = v % A2T_W;
+      const int base = (vd * A2H_H + 2 * vh) * A2H_W + 2 * vw;
+      const float a = as[v][co];
+      // branch-free: every pair's LDS read issues unconditionally (the bias pair and the unused ones read offset 0 and
+      // select / discard), so the six reads of a voxel share one wait
+      float xv[6];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) xv[m] = xs[max(off[m], 0) + base];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) acc[m] = fmaf(a, off[m] == -1 ? 1.f : xv[m], acc[m]);
     }
   }
 #pragma unroll
   for (int m = 0; m < 6; ++m)
-    if (g + 16 * m <= A2C1_TAPS)
-      slab[((int64_t)blockIdx.x * 16 + co) * (A2C1_TAPS + 1) + g + 16 * m] = acc[m];
+    if (off[m] != -2) slab[((int64_t)blockIdx.x * 16 + co) * (A2C1_TAPS + 1) + grp + 16 * m] = acc[m];
 }
 
 // dW[co][ci*27 + tap] / db[co] = sum over the S slabs in order: 4 entries per block, 64 lanes each, fixed butterfly
@@ -526,11 +566,14 @@ static int relu_gate(float* d, const float* y, int64_t n, hipStream_t st) {
 struct A2SlotTab {
   int64_t off[A2_NSLOT], numel[A2_NSLOT];
 };
-__global__ __launch_bounds__(256) void a2_sqsum_kernel(const float* __restrict__ g, A2SlotTab t, float* norms) {
+// per-slot squared sums in A2_SQ_CHUNKS fixed strided parts (block (slot, part)); a2_opt_prepare adds the parts in
+// order and takes each slot's norm (torch's per-tensor norm, then the norm of norms)
+constexpr int A2_SQ_CHUNKS = 16;
+__global__ __launch_bounds__(256) void a2_sqsum_kernel(const float* __restrict__ g, A2SlotTab t, double* sqp) {
   const int s = blockIdx.x;
   __shared__ double red[256];
   double acc = 0.0;
-  for (int64_t i = threadIdx.x; i < t.numel[s]; i += 256) {
+  for (int64_t i = blockIdx.y * 256ll + threadIdx.x; i < t.numel[s]; i += 256ll * A2_SQ_CHUNKS) {
     const float v = g[t.off[s] + i];
     acc += (double)v * (double)v;
   }
@@ -540,16 +583,21 @@ __global__ __launch_bounds__(256) void a2_sqsum_kernel(const float* __restrict__
     if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
     __syncthreads();
   }
-  if (threadIdx.x == 0) norms[s] = (float)sqrt(red[0]);
+  if (threadIdx.x == 0) sqp[s * A2_SQ_CHUNKS + blockIdx.y] = red[0];
 }
 // ctrl: [0] step?, [1] clip coefficient, [2] -lr/bc1, [3] sqrt(bc2), [4] 1 - lr*wd
-__global__ void a2_opt_prepare_kernel(const float* norms, float* losses, int32_t* steps, float lr, float b1, float b2,
+__global__ void a2_opt_prepare_kernel(const double* sqp, float* losses, int32_t* steps, float lr, float b1, float b2,
                                       float wd, float max_norm, float* ctrl) {
   if (threadIdx.x != 0) return;
   ctrl[0] = 0.f;
   if (losses[9] < 1.f) return;
   double tot = 0.0;
-  for (int s = 0; s < A2_NSLOT; ++s) tot += (double)norms[s] * (double)norms[s];
+  for (int s = 0; s < A2_NSLOT; ++s) {
+    double q = 0.0;
+    for (int c = 0; c < A2_SQ_CHUNKS; ++c) q += sqp[s * A2_SQ_CHUNKS + c];
+    const float nrm = (float)sqrt(q);
+    tot += (double)nrm * (double)nrm;
+  }
   const float total = (float)sqrt(tot);
   losses[8] = total;
   ctrl[1] = fminf(1.f, max_norm / (total + 1e-6f));
@@ -586,9 +634,13 @@ struct A2PlanImpl {
   int32_t* steps = nullptr;
   float *cols[3], *y[3], *pooled, *f, *hc0, *sig, *adj, *g1, *g1d, *g2, *cat, *hp0, *s, *losses, *pseudo, *d_s,
       *d_adj, *red, *pairs, *lsc, *dz_ap2, *dz_ap0, *dg2, *dz_ge0, *dz_cn2, *dz_cn0, *dfeat, *dpooled, *dA, *dcols,
-      *scratch, *norms, *ctrl;
+      *scratch, *ctrl;
+  double* sqp;
   int64_t* off_dev;
   float* xin = nullptr;  // (a2_direct) the forward's clip, kept for conv3d_1's weight gradient
+  // (a2_direct) conv3d_2 / conv3d_3 weight images (conv3s2_prep: [Co][27 Ci] + the 8 parity-class images) and the
+  // second input-gradient buffer
+  float *wk3[3] = {}, *wc3[3] = {}, *dA2 = nullptr;
   const int direct = g_a2_direct;
   int64_t scratch_floats = 0;
   int training = 1, with_loss = 0;
@@ -610,10 +662,14 @@ struct A2PlanImpl {
     int64_t max_y = 0, max_dcols = 1;
     xin = direct ? w.take<float>(g[0].in.numel()) : nullptr;
     for (int s = 0; s < 3; ++s) {
-      cols[s] = (direct && s == 0) ? nullptr : w.take<float>(g[s].rows() * g[s].K());
+      cols[s] = direct ? nullptr : w.take<float>(g[s].rows() * g[s].K());
+      if (direct && s > 0) {
+        wk3[s] = w.take<float>((int64_t)27 * g[s].in.C * A2_CO[s]);
+        wc3[s] = w.take<float>((int64_t)27 * g[s].in.C * A2_CO[s]);
+      }
       y[s] = w.take<float>(g[s].out().numel());
       max_y = std::max(max_y, g[s].out().numel());
-      if (s > 0) max_dcols = std::max(max_dcols, g[s].rows() * g[s].K());
+      if (s > 0 && !direct) max_dcols = std::max(max_dcols, g[s].rows() * g[s].K());
     }
     const int64_t b = B;
     pooled = w.take<float>(b * 4096);
@@ -643,10 +699,11 @@ struct A2PlanImpl {
     dfeat = w.take<float>(b * 16);
     dpooled = w.take<float>(b * 4096);
     dA = w.take<float>(max_y);
+    dA2 = direct ? w.take<float>(max_y) : nullptr;
     dcols = w.take<float>(max_dcols);
     scratch_floats = 8ll << 20;
     scratch = w.take<float>(scratch_floats);
-    norms = w.take<float>(A2_NSLOT);
+    sqp = w.take<double>(A2_NSLOT * A2_SQ_CHUNKS);
     ctrl = w.take<float>(8);
     off_dev = w.take<int64_t>(A2_NSLOT);
   }
@@ -680,10 +737,16 @@ struct A2PlanImpl {
       if (direct && s3 == 0) {
         const int64_t n = g[0].in.numel();
         VAD_HIP(hipMemcpyAsync(xin, x, sizeof(float) * n, hipMemcpyDeviceToDevice, st));
-        const int64_t vox = g[0].rows();
-        hipLaunchKernelGGL(a2_conv1_fwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(vox, 256), 4096)), dim3(256), 0,
-                           st, xin, B, T, H, W, P(S_C1W), P(S_C1B), y[0]);
+        const A2Tiles tl(B, T, H, W);
+        hipLaunchKernelGGL(a2_conv1_fwd_kernel, dim3((unsigned)std::min<int64_t>(tl.n, 4096)), dim3(256), 0, st, xin, B,
+                           T, H, W, P(S_C1W), P(S_C1B), y[0]);
         VAD_LAUNCH_CHECK();
+        continue;
+      }
+      if (direct) {  // conv3d_2 / conv3d_3: implicit GEMM, bias + ReLU in the epilogue
+        const Vol5& in = g[s3].in;
+        VAD_TRY(conv3s2_prep(P(2 * s3), A2_CO[s3], in.C, wk3[s3], wc3[s3], st));
+        VAD_TRY(conv3s2_fwd(y[s3 - 1], B, in.D, in.H, in.W, in.C, wk3[s3], P(2 * s3 + 1), A2_CO[s3], 1, y[s3], st));
         continue;
       }
       const float* src = s3 == 0 ? x : y[s3 - 1];
@@ -756,12 +819,25 @@ struct A2PlanImpl {
     VAD_TRY(dense_wgrad(dfeat, B, 16, pooled, 4096, G(S_FCW), G(S_FCB), scratch, scratch_floats, nullptr, st));
     VAD_TRY(dense_dgrad(dfeat, B, 16, P(S_FCW), 4096, dpooled, nullptr, 1.f, nullptr, st));
     VAD_TRY(adaptive_avgpool3d_bwd(dpooled, g[2].out(), 4, 4, 4, dA, st));
+    float* cur = dA;  // (direct: the input gradients ping-pong between dA and dA2)
     for (int s3 = 2; s3 >= 0; --s3) {
       const int64_t rows = g[s3].rows();
+      float* dA = cur;
       VAD_TRY(relu_gate(dA, y[s3], rows * A2_CO[s3], st));
+      if (direct && s3 > 0) {  // conv3d_2 / conv3d_3 on the implicit GEMMs
+        const Vol5& in = g[s3].in;
+        float* nxt = dA == this->dA ? dA2 : this->dA;
+        VAD_TRY(col_sum(dA, rows, A2_CO[s3], G(2 * s3 + 1), st));
+        VAD_TRY(conv3s2_wgrad(dA, A2_CO[s3], y[s3 - 1], in.C, B, in.D, in.H, in.W, G(2 * s3), scratch, scratch_floats,
+                              1024, st));
+        VAD_TRY(conv3s2_dgrad(dA, B, A2_CO[s3], wc3[s3], in.C, nxt, in.D, in.H, in.W, st));
+        cur = nxt;
+        continue;
+      }
       if (direct && s3 == 0) {
-        const int nb = (int)std::max<int64_t>(1, std::min<int64_t>({cdiv(rows, 4 * A2C1_CHUNK), 512,
-                                                                     scratch_floats / (16 * (A2C1_TAPS + 1))}));
+        const A2Tiles tl(B, T, H, W);
+        const int64_t cap = scratch_floats / (16 * (A2C1_TAPS + 1));
+        const int nb = (int)std::max<int64_t>(1, std::min<int64_t>({tl.n, 512, cap}));
         hipLaunchKernelGGL(a2_conv1_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, st, dA, xin, B, T, H, W, scratch);
         VAD_LAUNCH_CHECK();
         hipLaunchKernelGGL(a2_conv1_wgrad_reduce_kernel, dim3((unsigned)cdiv(16 * (A2C1_TAPS + 1), 4)), dim3(256), 0,
@@ -785,9 +861,9 @@ struct A2PlanImpl {
       t.off[i] = a2_offsets().off[i];
       t.numel[i] = A2_SLOTS[i].numel;
     }
-    hipLaunchKernelGGL(a2_sqsum_kernel, dim3(A2_NSLOT), dim3(256), 0, st, grads, t, norms);
+    hipLaunchKernelGGL(a2_sqsum_kernel, dim3(A2_NSLOT, A2_SQ_CHUNKS), dim3(256), 0, st, grads, t, sqp);
     VAD_LAUNCH_CHECK();
-    hipLaunchKernelGGL(a2_opt_prepare_kernel, dim3(1), dim3(64), 0, st, norms, losses, steps, lr, b1, b2, wd,
+    hipLaunchKernelGGL(a2_opt_prepare_kernel, dim3(1), dim3(64), 0, st, sqp, losses, steps, lr, b1, b2, wd,
                        max_norm, ctrl);
     VAD_LAUNCH_CHECK();
     const int64_t n = a2_offsets().total;

@@ -201,6 +201,8 @@ __global__ __launch_bounds__(256) void gbn_partials_kernel(const float* __restri
   const float* yg = y + (int64_t)blockIdx.y * q.Mg * C;
   const int64_t r0 = (int64_t)blockIdx.x * q.R, r1 = min(q.Mg, r0 + q.R);
   float v[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  // (4 rows in flight per thread: the loads of an unrolled group issue before its arithmetic; same summation order)
+#pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += lanes) {
     const f32x4 a = *reinterpret_cast<const f32x4*>(yg + r * C + c);
 #pragma unroll
@@ -316,6 +318,8 @@ __global__ __launch_bounds__(256) void gbn_bwd_reduce_kernel(const float* __rest
   const int64_t base = (int64_t)blockIdx.y * q.Mg * C;
   const int64_t r0 = (int64_t)blockIdx.x * q.R, r1 = min(q.Mg, r0 + q.R);
   float v[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  // (4 rows in flight per thread: the loads of an unrolled group issue before its arithmetic; same summation order)
+#pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += lanes) {
     const f32x4 a = *reinterpret_cast<const f32x4*>(dA + base + r * C + c);
     const f32x4 yy = *reinterpret_cast<const f32x4*>(y + base + r * C + c);
@@ -388,6 +392,8 @@ __global__ __launch_bounds__(256) void gbn_bwd_apply_kernel(const float* __restr
   const int64_t base = (int64_t)blockIdx.y * q.Mg * C;
   const int64_t r0 = (int64_t)blockIdx.x * q.R, r1 = min(q.Mg, r0 + q.R);
   float v[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  // (4 rows in flight per thread: the loads of an unrolled group issue before its arithmetic; same summation order)
+#pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += lanes) {
     const f32x4 a = *reinterpret_cast<const f32x4*>(dA + base + r * C + c);
     const f32x4 yy = *reinterpret_cast<const f32x4*>(y + base + r * C + c);

@@ -231,6 +231,16 @@ int conv4_cls(const float* src, int NF, int SH, int SW, int C, const float* wc, 
 int conv4_wgrad(const float* A, int R, const float* src, int C, int NF, int AH, int AW, float* part, int* nsplit,
                 int64_t part_cap, int target_blocks, hipStream_t st);
 int conv4_wgrad_reduce(const float* part, int S, int R, int C, float* dW, hipStream_t st);
+// ---------------------------------------------------------------- Conv3d(k3, stride 2, p1) implicit GEMMs (a2)
+// wk [Co][27 Ci]; wc: 8 parity-class images back to back (27 Ci Co floats in all); C % 4 == 0
+int conv3s2_prep(const float* w, int Co, int Ci, float* wk, float* wc, hipStream_t st);
+int conv3s2_fwd(const float* src, int NF, int D, int H, int W, int C, const float* wk, const float* bias, int N,
+                int relu, float* out, hipStream_t st);
+int conv3s2_dgrad(const float* dy, int NF, int Co, const float* wc, int Ci, float* dx, int D, int H, int W,
+                  hipStream_t st);
+int conv3s2_wgrad(const float* dy, int Co, const float* src, int Ci, int NF, int D, int H, int W, float* dW,
+                  float* part, int64_t part_cap, int target_blocks, hipStream_t st);
+int col_sum(const float* x, int64_t M, int N, float* db, hipStream_t st);
 // the single-channel ends, 32 channels on the other side, on the VALU: w = the [32][1][4][4] / [32][16] weight
 int conv4_c1_fwd(const float* src, int NF, int H, int W, const float* w, const float* bias, float* out,
                  hipStream_t st);

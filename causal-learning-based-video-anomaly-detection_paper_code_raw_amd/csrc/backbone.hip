@@ -1918,6 +1918,34 @@ int conv4_fwd(const float* src, int NF, int H, int W, int C, const float* wk, co
   });
 }
 
+struct EpiConv3DgradCls {  // EpiConv3Dgrad for the class-batched GEMM: class = blockIdx.z, its own grid
+  static constexpr int SCRATCH = 0;
+  struct Params { float* dst; int imgs; int GD[8], GA[8], GB[8]; int DD, DH, DW, C; const float* bias; };
+  template <class Cfg>
+  static __device__ void apply(const Params& P, f32x16 (&acc)[Cfg::TM][Cfg::TN], int m0, int n0, int wm, int wn,
+                               int lane, int, int N, float*) {
+    const int z = blockIdx.z, pd = (z >> 2) & 1, ph = (z >> 1) & 1, pw = z & 1;
+    const int GA = P.GA[z], GB = P.GB[z], per = P.GD[z] * GA * GB;
+    if (per == 0) return;
+#pragma unroll
+    for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + acc_row<Cfg>(wm, i, r, lane);
+        const int img = row / per, rem = row - img * per;
+        if (img >= P.imgs) continue;
+        const int a = rem / (GA * GB), r2 = rem - a * GA * GB;
+        const int b = r2 / GB, c = r2 - b * GB;
+        const int64_t base = ((((int64_t)img * P.DD + 2 * a + pd) * P.DH + 2 * b + ph) * P.DW + 2 * c + pw) * P.C;
+#pragma unroll
+        for (int j = 0; j < Cfg::TN; ++j) {
+          const int col = n0 + acc_col<Cfg>(wn, j, lane);
+          if (col < N) P.dst[base + col] = acc[i][j][r] + (P.bias ? P.bias[col] : 0.f);
+        }
+      }
+  }
+};
+
 // out[img][2a + py][2b + px][n] = bias[n] + sum over the slabs of part[s][(img SH + a) SW + b][n]
 __global__ __launch_bounds__(256) void conv4_cls_reduce_kernel(const float* __restrict__ part, int S, int M, int SH,
                                                                int SW, int N, int py, int px,
@@ -1939,6 +1967,43 @@ __global__ __launch_bounds__(256) void conv4_cls_reduce_kernel(const float* __re
 int conv4_cls(const float* src, int NF, int SH, int SW, int C, const float* wc, const float* bias, int N, float* out,
               hipStream_t st, float* scratch, int64_t scratch_floats) {
   VAD_CHECK(C % 32 == 0 && N >= 1, "conv4_cls: C % 32 == 0");
+  const int Mc = NF * SH * SW;
+  if (cdiv(Mc, 64) * cdiv(N, 64) * 4 >= 512 || scratch_floats <= 0) {
+    // the four classes in one launch (blockIdx.z = class, the 3-D class-batched GEMM with a depth of 1)
+    Conv3ClsGeom g{};
+    g.imgs = NF; g.SD = 1; g.SH = SH; g.SW = SW; g.C = C;
+    EpiConv3DgradCls::Params pe{};
+    pe.dst = out; pe.imgs = NF; pe.DD = 1; pe.DH = 2 * SH; pe.DW = 2 * SW; pe.C = N; pe.bias = bias;
+    for (int cls = 0; cls < 4; ++cls) {
+      const int py = cls >> 1, px = cls & 1;
+      g.GD[cls] = pe.GD[cls] = 1;
+      g.GA[cls] = pe.GA[cls] = SH;
+      g.GB[cls] = pe.GB[cls] = SW;
+      TapTable3& taps = g.taps[cls];
+      taps.ntaps = 4;
+      for (int r = 0; r < 2; ++r)
+        for (int q = 0; q < 2; ++q) {
+          taps.dd[2 * r + q] = 0;
+          taps.dh[2 * r + q] = (int8_t)(py == 0 ? -r : 1 - r);
+          taps.dw[2 * r + q] = (int8_t)(px == 0 ? -q : 1 - q);
+        }
+    }
+    const int K = 4 * C;
+    return with_tile(pick_dgrad_tile(Mc, N), [&](auto cfg) -> int {
+      using Cf = decltype(cfg);
+      typename ConvGather3ClsKC<Cf::BM>::Params pa{src, g};
+      typename DenseKCz<Cf::BN>::Params pb{wc, {}, {}, N};
+      for (int c = 0; c < 4; ++c) {
+        pb.off[c] = (int64_t)c * N * K;
+        pb.kdim[c] = K;
+      }
+      const dim3 grid((unsigned)cdiv(Mc, Cf::BM), (unsigned)cdiv(N, Cf::BN), 4u);
+      VAD_KLAUNCH((gemm_kernel<Cf, ConvGather3ClsKC<Cf::BM>, DenseKCz<Cf::BN>, EpiConv3DgradCls>), grid, dim3(256), 0,
+                  st, pa, pb, pe, Mc, N, K, -1, nullptr);
+      VAD_LAUNCH_CHECK();
+      return 0;
+    });
+  }
   for (int cls = 0; cls < 4; ++cls) {
     const int py = cls >> 1, px = cls & 1;
     const ConvGeom g{NF, SH, SW, 1, 1, SH, SW, C};
@@ -1987,24 +2052,25 @@ int conv4_wgrad(const float* A, int R, const float* src, int C, int NF, int AH, 
   });
 }
 
-// dW[r][c][tap] = sum over the S slabs, in order, of part[s][r][tap C + c]
+// dW[r][c][tap] = sum over the S slabs, in order, of part[s][r][tap C + c] (NT taps: 16 for the 4x4 convs, 27 for
+// the 3-D ones)
 __global__ __launch_bounds__(256) void conv4_wgrad_reduce_kernel(const float* __restrict__ part, int S, int R, int C,
-                                                                 float* __restrict__ dW) {
-  const int64_t total = (int64_t)R * 16 * C;
+                                                                 int NT, float* __restrict__ dW) {
+  const int64_t total = (int64_t)R * NT * C;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
     float s = 0.f;
     for (int z = 0; z < S; ++z) s += part[(int64_t)z * total + i];
-    const int c = (int)(i % C), tap = (int)((i / C) % 16);
-    const int64_t r = i / (16 * C);
-    dW[(r * C + c) * 16 + tap] = s;
+    const int c = (int)(i % C), tap = (int)((i / C) % NT);
+    const int64_t r = i / ((int64_t)NT * C);
+    dW[(r * C + c) * NT + tap] = s;
   }
 }
 
 // the same for small outputs with many slabs: 4 entries per block, 64 lanes each adding slabs lane, lane + 64, ... in
 // order, then a fixed butterfly
 __global__ __launch_bounds__(256) void conv4_wgrad_reduce_small_kernel(const float* __restrict__ part, int S, int R,
-                                                                       int C, float* __restrict__ dW) {
-  const int64_t total = (int64_t)R * 16 * C;
+                                                                       int C, int NT, float* __restrict__ dW) {
+  const int64_t total = (int64_t)R * NT * C;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   float v = 0.f;
@@ -2012,24 +2078,28 @@ __global__ __launch_bounds__(256) void conv4_wgrad_reduce_small_kernel(const flo
     for (int z = lane; z < S; z += 64) v += part[(int64_t)z * total + i];
   v = wave_sum(v);
   if (lane == 0 && i < total) {
-    const int c = (int)(i % C), tap = (int)((i / C) % 16);
-    const int64_t r = i / (16 * C);
-    dW[(r * C + c) * 16 + tap] = v;
+    const int c = (int)(i % C), tap = (int)((i / C) % NT);
+    const int64_t r = i / ((int64_t)NT * C);
+    dW[(r * C + c) * NT + tap] = v;
   }
 }
 
-int conv4_wgrad_reduce(const float* part, int S, int R, int C, float* dW, hipStream_t st) {
-  const int64_t total = (int64_t)R * 16 * C;
+static int taps_wgrad_reduce(const float* part, int S, int R, int C, int NT, float* dW, hipStream_t st) {
+  const int64_t total = (int64_t)R * NT * C;
   if (total <= 65536 && S >= 64) {
     hipLaunchKernelGGL(conv4_wgrad_reduce_small_kernel, dim3((unsigned)cdiv(total, 4)), dim3(256), 0, st, part, S, R, C,
-                       dW);
+                       NT, dW);
     VAD_LAUNCH_CHECK();
     return 0;
   }
   hipLaunchKernelGGL(conv4_wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 2048)), dim3(256), 0,
-                     st, part, S, R, C, dW);
+                     st, part, S, R, C, NT, dW);
   VAD_LAUNCH_CHECK();
   return 0;
+}
+
+int conv4_wgrad_reduce(const float* part, int S, int R, int C, float* dW, hipStream_t st) {
+  return taps_wgrad_reduce(part, S, R, C, 16, dW, st);
 }
 
 // ---------------------------------------------------------------- the single-channel ends (cad1:131, cad1:185)
@@ -2185,6 +2255,186 @@ int conv4_c1_wgrad(const float* A, const float* src, int NF, int AH, int AW, flo
   hipLaunchKernelGGL(conv4_c1_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, A, src, NF, AH, AW, slab);
   VAD_LAUNCH_CHECK();
   return conv4_wgrad_reduce(slab, blocks, 32, 1, dW, st);
+}
+
+// =====================================================================================================
+// Conv3d(kernel 3, stride 2, padding 1) as implicit GEMMs over NDHWC volumes (a2's conv3d_2 / conv3d_3,
+// avenue_training_script2.py:20-21): no im2col / col2im columns.
+//   conv3s2_fwd    out[p][n] = act(sum_{tap, c} src[2a - 1 + kd][2b - 1 + kh][2c - 1 + kw][c] wk[n][tap C + c] + bias)
+//   conv3s2_dgrad  the input gradient as 8 parity-class GEMMs over dY: along each dim an even input index takes k = 1
+//                  (dY index = its half), an odd one k = 0 (half + 1) and k = 2 (half); scattered to (2a + pd, ...)
+//   conv3s2_wgrad  split-K correlation dY x patch3(src) into slabs, summed into torch's [Co][Ci][27] layout
+// Weight images (conv3s2_prep) of torch [Co][Ci][27]: wk [Co][27 Ci]; wc = the 8 class images [Ci][nt Co] back to back
+// (class cls = 4 pd + 2 ph + pw, nt = its tap count 1 / 2 / 4 / 8, taps d-major over the per-dim lists).
+// =====================================================================================================
+__device__ __host__ inline int c3_nt(int cls) { return (1 + ((cls >> 2) & 1)) * (1 + ((cls >> 1) & 1)) * (1 + (cls & 1)); }
+
+__global__ __launch_bounds__(256) void conv3s2_prep_kernel(const float* __restrict__ w, int Co, int Ci,
+                                                           float* __restrict__ wk, float* __restrict__ wc) {
+  const int64_t total = (int64_t)Co * Ci * 27;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int tap = (int)(i % 27), ci = (int)((i / 27) % Ci);
+    const int64_t co = i / (27 * Ci);
+    const float v = w[i];
+    wk[co * 27 * Ci + tap * Ci + ci] = v;
+    const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+    const int pd = kd == 1 ? 0 : 1, ph = kh == 1 ? 0 : 1, pw = kw == 1 ? 0 : 1;
+    const int id = kd == 2 ? 1 : 0, ih = kh == 2 ? 1 : 0, iw = kw == 2 ? 1 : 0;  // index in the dim's tap list
+    const int cls = 4 * pd + 2 * ph + pw, nh = 1 + ph, nw = 1 + pw, nt = c3_nt(cls);
+    int64_t off = 0;
+    for (int c = 0; c < cls; ++c) off += (int64_t)c3_nt(c) * Ci * Co;
+    const int t = (id * nh + ih) * nw + iw;
+    wc[off + ((int64_t)ci * nt + t) * Co + co] = v;
+  }
+}
+
+int conv3s2_prep(const float* w, int Co, int Ci, float* wk, float* wc, hipStream_t st) {
+  const int64_t total = (int64_t)Co * Ci * 27;
+  hipLaunchKernelGGL(conv3s2_prep_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 1024)), dim3(256), 0, st,
+                     w, Co, Ci, wk, wc);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+
+int conv3s2_fwd(const float* src, int NF, int D, int H, int W, int C, const float* wk, const float* bias, int N,
+                int relu, float* out, hipStream_t st) {
+  VAD_CHECK(C % 4 == 0 && N >= 1, "conv3s2_fwd: C % 4 == 0");
+  const int OD = (D - 1) / 2 + 1, OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  ConvGeom3 g{NF, OD, OH, OW, 2, 2, 2, D, H, W, C};
+  TapTable3 taps;
+  taps.ntaps = 27;
+  for (int t = 0; t < 27; ++t) {
+    taps.dd[t] = (int8_t)(t / 9 - 1);
+    taps.dh[t] = (int8_t)((t / 3) % 3 - 1);
+    taps.dw[t] = (int8_t)(t % 3 - 1);
+  }
+  const int M = NF * OD * OH * OW, K = 27 * C;
+  const DenseEpiArgs pe{out, N, bias, relu, 0, 0, 0, 1.f, 0, nullptr, 1.f};
+  return with_tile(pick_fwd_tile(M, N), [&](auto cfg) -> int {
+    using Cf = decltype(cfg);
+    typename ConvGather3KC<Cf::BM>::Params pa{src, g, taps};
+    typename DenseKC<Cf::BN>::Params pb{wk, K, N, K};
+    return launch_gemm<Cf, ConvGather3KC, DenseKC, EpiDense>(pa, pb, pe, M, N, K, 1, nullptr, st);
+  });
+}
+
+struct EpiConv3Dgrad {  // scatter the rows of a parity-class grid to the NDHWC input gradient
+  static constexpr int SCRATCH = 0;
+  struct Params { float* dst; int GD, GA, GB, pd, ph, pw, DD, DH, DW, C; };
+  template <class Cfg>
+  static __device__ void apply(const Params& P, f32x16 (&acc)[Cfg::TM][Cfg::TN], int m0, int n0, int wm, int wn,
+                               int lane, int M, int N, float*) {
+    const int per = P.GD * P.GA * P.GB;
+#pragma unroll
+    for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + acc_row<Cfg>(wm, i, r, lane);
+        if (row >= M) continue;
+        const int img = row / per, rem = row - img * per;
+        const int a = rem / (P.GA * P.GB), r2 = rem - a * P.GA * P.GB;
+        const int b = r2 / P.GB, c = r2 - b * P.GB;
+        const int64_t base =
+            ((((int64_t)img * P.DD + 2 * a + P.pd) * P.DH + 2 * b + P.ph) * P.DW + 2 * c + P.pw) * P.C;
+#pragma unroll
+        for (int j = 0; j < Cfg::TN; ++j) {
+          const int col = n0 + acc_col<Cfg>(wn, j, lane);
+          if (col < N) P.dst[base + col] = acc[i][j][r];
+        }
+      }
+  }
+};
+
+int conv3s2_dgrad(const float* dy, int NF, int Co, const float* wc, int Ci, float* dx, int D, int H, int W,
+                  hipStream_t st) {
+  VAD_CHECK(Co % 4 == 0, "conv3s2_dgrad: Co % 4 == 0");
+  const int OD = (D - 1) / 2 + 1, OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  // the 8 parity classes in one launch (blockIdx.z = class; K = 8 taps x Co, zero past a class's own taps)
+  Conv3ClsGeom g{};
+  g.imgs = NF; g.SD = OD; g.SH = OH; g.SW = OW; g.C = Co;
+  typename DenseKCz<64>::Params pb0{};
+  EpiConv3DgradCls::Params pe{};
+  pe.dst = dx; pe.imgs = NF; pe.DD = D; pe.DH = H; pe.DW = W; pe.C = Ci;
+  int64_t off = 0;
+  int Mmax = 0;
+  for (int cls = 0; cls < 8; ++cls) {
+    const int pd = (cls >> 2) & 1, ph = (cls >> 1) & 1, pw = cls & 1, nt = c3_nt(cls);
+    g.GD[cls] = pe.GD[cls] = std::max(0, (D - pd + 1) / 2);
+    g.GA[cls] = pe.GA[cls] = std::max(0, (H - ph + 1) / 2);
+    g.GB[cls] = pe.GB[cls] = std::max(0, (W - pw + 1) / 2);
+    Mmax = std::max(Mmax, NF * g.GD[cls] * g.GA[cls] * g.GB[cls]);
+    TapTable3& taps = g.taps[cls];
+    taps.ntaps = nt;
+    const int nh = 1 + ph, nw = 1 + pw;
+    for (int t = 0; t < nt; ++t) {
+      const int id = t / (nh * nw), ih = (t / nw) % nh, iw = t % nw;
+      // even parity: k = 1, offset 0; odd: k = 0 -> offset +1, k = 2 -> offset 0
+      taps.dd[t] = (int8_t)(pd == 0 ? 0 : (id == 0 ? 1 : 0));
+      taps.dh[t] = (int8_t)(ph == 0 ? 0 : (ih == 0 ? 1 : 0));
+      taps.dw[t] = (int8_t)(pw == 0 ? 0 : (iw == 0 ? 1 : 0));
+    }
+    pb0.off[cls] = off;
+    pb0.kdim[cls] = nt * Co;
+    off += (int64_t)nt * Ci * Co;
+  }
+  if (Mmax == 0) return 0;
+  const int K = 8 * Co;
+  return with_tile(pick_dgrad_tile(Mmax, Ci), [&](auto cfg) -> int {
+    using Cf = decltype(cfg);
+    typename ConvGather3ClsKC<Cf::BM>::Params pa{dy, g};
+    typename DenseKCz<Cf::BN>::Params pb{wc, {}, {}, Ci};
+    for (int c = 0; c < 8; ++c) {
+      pb.off[c] = pb0.off[c];
+      pb.kdim[c] = pb0.kdim[c];
+    }
+    const dim3 grid((unsigned)cdiv(Mmax, Cf::BM), (unsigned)cdiv(Ci, Cf::BN), 8u);
+    VAD_KLAUNCH((gemm_kernel<Cf, ConvGather3ClsKC<Cf::BM>, DenseKCz<Cf::BN>, EpiConv3DgradCls>), grid, dim3(256), 0, st,
+                pa, pb, pe, Mmax, Ci, K, -1, nullptr);
+    VAD_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int conv3s2_wgrad(const float* dy, int Co, const float* src, int Ci, int NF, int D, int H, int W, float* dW,
+                  float* part, int64_t part_cap, int target_blocks, hipStream_t st) {
+  VAD_CHECK(Ci % 4 == 0 && Co % 4 == 0, "conv3s2_wgrad: channel counts % 4 == 0");
+  const int OD = (D - 1) / 2 + 1, OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const int M = Co, N = 27 * Ci, K = NF * OD * OH * OW;
+  VAD_CHECK((int64_t)M * N <= part_cap, "conv3s2_wgrad: slab too small");
+  int used = 1;
+  VAD_TRY(with_tile(pick_wgrad_tile(M, N), [&](auto cfg) -> int {
+    using Cf = decltype(cfg);
+    const int tiles = (int)(cdiv(M, Cf::BM) * cdiv(N, Cf::BN));
+    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, tiles), cdiv(K, 8 * BK)));
+    while ((int64_t)splits * M * N > part_cap && splits > 1) splits /= 2;
+    typename DenseKM<Cf::BM>::Params pa{dy, Co, Co, K, -1};
+    typename ConvPatch3KM<Cf::BN>::Params pb{src, NF, OD, OH, OW, 2, 2, 2, 1, D, H, W, Ci, N};
+    const EpiPartial::Params pe{part, N};
+    return launch_gemm<Cf, DenseKM, ConvPatch3KM, EpiPartial>(pa, pb, pe, M, N, K, splits, nullptr, st, &used);
+  }));
+  return taps_wgrad_reduce(part, used, Co, Ci, 27, dW, st);
+}
+
+// db[n] = sum over the M rows of x[m][n], fixed order: one block per column, 256-way strided + tree (double)
+__global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ x, int64_t M, int N,
+                                                      float* __restrict__ db) {
+  __shared__ double red[256];
+  const int n = blockIdx.x;
+  double s = 0.0;
+  for (int64_t m = threadIdx.x; m < M; m += 256) s += (double)x[m * N + n];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) db[n] = (float)red[0];
+}
+
+int col_sum(const float* x, int64_t M, int N, float* db, hipStream_t st) {
+  hipLaunchKernelGGL(col_sum_kernel, dim3((unsigned)N), dim3(256), 0, st, x, M, N, db);
+  VAD_LAUNCH_CHECK();
+  return 0;
 }
 
 }  // namespace vad

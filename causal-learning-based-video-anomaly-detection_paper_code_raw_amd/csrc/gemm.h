@@ -210,6 +210,8 @@ struct ConvGatherKC {
 // B operand of the conv weight gradient (K-major over output pixels):
 //   k = output pixel p = (img, oh, ow) of the forward conv, r = tap*C + c,
 //   value = act(src[img][oh*s - pad + kh][ow*s - pad + kw][c]).
+// A thread's rows r (hence tap, c) are fixed and its pixels advance by BK per K slice: both are decomposed once
+// (init / the first load of a split) and the pixel coordinates then stepped, not divided, per slice.
 template <int R>
 struct ConvPatchKM {
   static constexpr bool KC = false;
@@ -219,29 +221,55 @@ struct ConvPatchKM {
     const float* scale; const float* shift;
   };
   const Params* P;
-  int r0, tid;
+  int r0, tid, nextk;
+  int kh[NL], kw[NL], cc[NL];  // tap rows / columns and channel of the thread's r (kh < 0: r out of range)
+  int img[NL], oh[NL], ow[NL];  // the pixel of the thread's next load
   f32x4 reg[NL];
-  __device__ void init(const Params& Pp, int r0_, int tid_) { P = &Pp; r0 = r0_; tid = tid_; }
-  __device__ void load(int k0) {
-    const int npix = P->imgs * P->OH * P->OW;
+  __device__ void init(const Params& Pp, int r0_, int tid_) {
+    P = &Pp; r0 = r0_; tid = tid_; nextk = -1;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int q = tid + 256 * j;
-      const int kr = q / (R / 4), rq = q % (R / 4);
-      const int p = k0 + kr, r = r0 + rq * 4;
+      const int r = r0 + (q % (R / 4)) * 4;
+      if (r < Pp.rows) {
+        const int tap = r / Pp.C;
+        cc[j] = r - tap * Pp.C;
+        kh[j] = tap / Pp.KW;
+        kw[j] = tap - kh[j] * Pp.KW;
+      } else {
+        cc[j] = 0; kh[j] = -1; kw[j] = 0;
+      }
+    }
+  }
+  __device__ void load(int k0) {
+    const Params& q = *P;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int kr = (tid + 256 * j) / (R / 4);
+      if (k0 != nextk) {  // (first slice of this split: full decomposition)
+        const int p = k0 + kr;
+        img[j] = p / (q.OH * q.OW);
+        const int rem = p - img[j] * q.OH * q.OW;
+        oh[j] = rem / q.OW;
+        ow[j] = rem - oh[j] * q.OW;
+      } else {  // the previous slice's pixel + BK
+        ow[j] += BK;
+        while (ow[j] >= q.OW) {
+          ow[j] -= q.OW;
+          if (++oh[j] == q.OH) {
+            oh[j] = 0;
+            ++img[j];
+          }
+        }
+      }
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (p < npix && r < P->rows) {
-        const int tap = r / P->C, c = r - tap * P->C;
-        const int kh = tap / P->KW, kw = tap - kh * P->KW;
-        const int img = p / (P->OH * P->OW);
-        const int rem = p - img * P->OH * P->OW;
-        const int oh = rem / P->OW, ow = rem - oh * P->OW;
-        const int y = oh * P->stride - P->pad + kh, x = ow * P->stride - P->pad + kw;
-        if (y >= 0 && y < P->SH && x >= 0 && x < P->SW) {
-          v = *reinterpret_cast<const f32x4*>(P->src + (((int64_t)img * P->SH + y) * P->SW + x) * P->C + c);
-          if (P->scale) {
-            const f32x4 sc = *reinterpret_cast<const f32x4*>(P->scale + c);
-            const f32x4 sh = *reinterpret_cast<const f32x4*>(P->shift + c);
+      if (img[j] < q.imgs && kh[j] >= 0) {
+        const int y = oh[j] * q.stride - q.pad + kh[j], x = ow[j] * q.stride - q.pad + kw[j];
+        if (y >= 0 && y < q.SH && x >= 0 && x < q.SW) {
+          v = *reinterpret_cast<const f32x4*>(q.src + (((int64_t)img[j] * q.SH + y) * q.SW + x) * q.C + cc[j]);
+          if (q.scale) {
+            const f32x4 sc = *reinterpret_cast<const f32x4*>(q.scale + cc[j]);
+            const f32x4 sh = *reinterpret_cast<const f32x4*>(q.shift + cc[j]);
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
           }
@@ -249,12 +277,258 @@ struct ConvPatchKM {
       }
       reg[j] = v;
     }
+    nextk = k0 + BK;
   }
   __device__ void store(float* lds) const {
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int q = tid + 256 * j;
       const int kr = q / (R / 4), rq = q % (R / 4);
+      *reinterpret_cast<f32x4*>(lds + kr * R + rq * 4) = reg[j];
+    }
+  }
+};
+
+// 3-D variants (a2's strided Conv3d, avenue_training_script2.py:19-21): row m = (img, a, b, c) of a GD x GA x GB grid,
+// k = tap * C + ch over up to 27 (dd, dh, dw) taps; C % 4 == 0 (each thread's 4 channels lie in one tap), K need not be
+// a multiple of BK (k >= taps * C loads zero).
+struct TapTable3 {
+  int ntaps;
+  int8_t dd[27], dh[27], dw[27];
+};
+struct ConvGeom3 {
+  int imgs;
+  int GD, GA, GB;  // destination grid
+  int sd, sa, sb;  // source step per grid step
+  int SD, SH, SW, C;
+};
+
+template <int R>
+struct ConvGather3KC {
+  static constexpr bool KC = true;
+  static constexpr int NL = R / 32;
+  struct Params {
+    const float* src; ConvGeom3 g; TapTable3 taps;
+  };
+  const Params* P;
+  int tid;
+  int64_t vox_base[NL];  // img * SD * SH * SW
+  int zd[NL], ya[NL], xb[NL];  // a * sd, b * sa, c * sb (zd < 0: an out-of-range row)
+  f32x4 reg[NL];
+  __device__ void init(const Params& Pp, int r0, int tid_) {
+    P = &Pp; tid = tid_;
+    const ConvGeom3& g = Pp.g;
+    const int per = g.GD * g.GA * g.GB;
+    const int M = g.imgs * per;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int m = r0 + tid / 8 + 32 * j;
+      if (m < M) {
+        const int img = m / per, rem = m - img * per;
+        const int a = rem / (g.GA * g.GB), r2 = rem - a * g.GA * g.GB;
+        const int b = r2 / g.GB, c = r2 - b * g.GB;
+        vox_base[j] = (int64_t)img * g.SD * g.SH * g.SW;
+        zd[j] = a * g.sd;
+        ya[j] = b * g.sa;
+        xb[j] = c * g.sb;
+      } else {
+        vox_base[j] = 0; zd[j] = -100000; ya[j] = 0; xb[j] = 0;
+      }
+    }
+  }
+  __device__ void load(int k0) {
+    const ConvGeom3& g = P->g;
+    const int k = k0 + (tid % 8) * 4;
+    const int tap = k / g.C, c = k - tap * g.C;
+    const bool kin = tap < P->taps.ntaps;
+    const int dd = kin ? P->taps.dd[tap] : 0, dh = kin ? P->taps.dh[tap] : 0, dw = kin ? P->taps.dw[tap] : 0;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int z = zd[j] + dd, y = ya[j] + dh, x = xb[j] + dw;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (kin && z >= 0 && z < g.SD && y >= 0 && y < g.SH && x >= 0 && x < g.SW)
+        v = *reinterpret_cast<const f32x4*>(P->src + ((vox_base[j] + ((int64_t)z * g.SH + y) * g.SW + x) * g.C + c));
+      reg[j] = v;
+    }
+  }
+  __device__ void store(float* lds) const {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int row = tid / 8 + 32 * j, kq = tid % 8;
+      *reinterpret_cast<f32x4*>(lds + row * KC_STRIDE + kq * 4) = reg[j];
+    }
+  }
+};
+
+// The parity classes of a stride-2 3-D conv's input gradient as one batched GEMM (blockIdx.z = class; k_per_split < 0):
+// class z gathers its own taps over its own grid (rows beyond the class's grid load zeros; taps beyond its count too).
+struct Conv3ClsGeom {
+  int imgs, SD, SH, SW, C;
+  int GD[8], GA[8], GB[8];
+  TapTable3 taps[8];
+};
+template <int R>
+struct ConvGather3ClsKC {
+  static constexpr bool KC = true;
+  static constexpr int NL = R / 32;
+  struct Params {
+    const float* src; Conv3ClsGeom g;
+  };
+  const Params* P;
+  const TapTable3* taps;
+  int tid;
+  int64_t vox_base[NL];
+  int zd[NL], ya[NL], xb[NL];
+  f32x4 reg[NL];
+  __device__ void init(const Params& Pp, int r0, int tid_) {
+    P = &Pp; tid = tid_;
+    const Conv3ClsGeom& g = Pp.g;
+    const int z = blockIdx.z;
+    taps = &g.taps[z];
+    const int GA = g.GA[z], GB = g.GB[z], per = g.GD[z] * GA * GB, M = g.imgs * per;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int m = r0 + tid / 8 + 32 * j;
+      if (m < M) {
+        const int img = m / per, rem = m - img * per;
+        const int a = rem / (GA * GB), r2 = rem - a * GA * GB;
+        const int b = r2 / GB, c = r2 - b * GB;
+        vox_base[j] = (int64_t)img * g.SD * g.SH * g.SW;
+        zd[j] = a; ya[j] = b; xb[j] = c;
+      } else {
+        vox_base[j] = 0; zd[j] = -100000; ya[j] = 0; xb[j] = 0;
+      }
+    }
+  }
+  __device__ void load(int k0) {
+    const Conv3ClsGeom& g = P->g;
+    const int k = k0 + (tid % 8) * 4;
+    const int tap = k / g.C, c = k - tap * g.C;
+    const bool kin = tap < taps->ntaps;
+    const int dd = kin ? taps->dd[tap] : 0, dh = kin ? taps->dh[tap] : 0, dw = kin ? taps->dw[tap] : 0;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int z = zd[j] + dd, y = ya[j] + dh, x = xb[j] + dw;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (kin && z >= 0 && z < g.SD && y >= 0 && y < g.SH && x >= 0 && x < g.SW)
+        v = *reinterpret_cast<const f32x4*>(P->src + ((vox_base[j] + ((int64_t)z * g.SH + y) * g.SW + x) * g.C + c));
+      reg[j] = v;
+    }
+  }
+  __device__ void store(float* lds) const {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int row = tid / 8 + 32 * j, kq = tid % 8;
+      *reinterpret_cast<f32x4*>(lds + row * KC_STRIDE + kq * 4) = reg[j];
+    }
+  }
+};
+
+// Row-major matrices X_z[rows][kdim_z] at p + off[z] (blockIdx.z = batch), read K-contiguous (as DenseKC)
+template <int R>
+struct DenseKCz {
+  static constexpr bool KC = true;
+  static constexpr int NL = R / 32;
+  struct Params { const float* p; int64_t off[8]; int kdim[8]; int rows; };
+  const float* base; int kdim, rows, r0, tid;
+  f32x4 reg[NL];
+  __device__ void init(const Params& P, int r0_, int tid_) {
+    base = P.p + P.off[blockIdx.z]; kdim = P.kdim[blockIdx.z]; rows = P.rows; r0 = r0_; tid = tid_;
+  }
+  __device__ void load(int k0) {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int row = tid / 8 + 32 * j, kq = tid % 8;
+      const int r = r0 + row, k = k0 + kq * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (r < rows && k < kdim) {  // (kdim % 4 == 0)
+        v = *reinterpret_cast<const f32x4*>(base + (int64_t)r * kdim + k);
+      }
+      reg[j] = v;
+    }
+  }
+  __device__ void store(float* lds) const {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int row = tid / 8 + 32 * j, kq = tid % 8;
+      *reinterpret_cast<f32x4*>(lds + row * KC_STRIDE + kq * 4) = reg[j];
+    }
+  }
+};
+
+// B operand of the 3-D conv weight gradient (K-major over output voxels): k = output voxel p = (img, od, oh, ow),
+// r = tap * C + c (27 taps kd, kh, kw), value = src[od * s - pad + kd][oh * s - pad + kh][ow * s - pad + kw][c]; the
+// voxel coordinates are stepped by BK per slice as in ConvPatchKM
+template <int R>
+struct ConvPatch3KM {
+  static constexpr bool KC = false;
+  static constexpr int NL = R / 32;
+  struct Params {
+    const float* src; int imgs, OD, OH, OW, sd, sh, sw, pad, SD, SH, SW, C, rows;  // rows = 27 * C
+  };
+  const Params* P;
+  int r0, tid, nextk;
+  int kd[NL], kh[NL], kw[NL], cc[NL];  // kd < 0: r out of range
+  int img[NL], od[NL], oh[NL], ow[NL];
+  f32x4 reg[NL];
+  __device__ void init(const Params& Pp, int r0_, int tid_) {
+    P = &Pp; r0 = r0_; tid = tid_; nextk = -1;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int r = r0 + ((tid + 256 * j) % (R / 4)) * 4;
+      if (r < Pp.rows) {
+        const int tap = r / Pp.C;
+        cc[j] = r - tap * Pp.C;
+        kd[j] = tap / 9;
+        kh[j] = (tap / 3) % 3;
+        kw[j] = tap % 3;
+      } else {
+        cc[j] = 0; kd[j] = -1; kh[j] = 0; kw[j] = 0;
+      }
+    }
+  }
+  __device__ void load(int k0) {
+    const Params& q = *P;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int kr = (tid + 256 * j) / (R / 4);
+      if (k0 != nextk) {
+        const int p = k0 + kr, per = q.OD * q.OH * q.OW;
+        img[j] = p / per;
+        const int rem = p - img[j] * per;
+        od[j] = rem / (q.OH * q.OW);
+        const int r2 = rem - od[j] * q.OH * q.OW;
+        oh[j] = r2 / q.OW;
+        ow[j] = r2 - oh[j] * q.OW;
+      } else {
+        ow[j] += BK;
+        while (ow[j] >= q.OW) {
+          ow[j] -= q.OW;
+          if (++oh[j] == q.OH) {
+            oh[j] = 0;
+            if (++od[j] == q.OD) {
+              od[j] = 0;
+              ++img[j];
+            }
+          }
+        }
+      }
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (img[j] < q.imgs && kd[j] >= 0) {
+        const int z = od[j] * q.sd - q.pad + kd[j], y = oh[j] * q.sh - q.pad + kh[j], x = ow[j] * q.sw - q.pad + kw[j];
+        if (z >= 0 && z < q.SD && y >= 0 && y < q.SH && x >= 0 && x < q.SW)
+          v = *reinterpret_cast<const f32x4*>(q.src + ((((int64_t)img[j] * q.SD + z) * q.SH + y) * q.SW + x) * q.C +
+                                              cc[j]);
+      }
+      reg[j] = v;
+    }
+    nextk = k0 + BK;
+  }
+  __device__ void store(float* lds) const {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int qq = tid + 256 * j;
+      const int kr = qq / (R / 4), rq = qq % (R / 4);
       *reinterpret_cast<f32x4*>(lds + kr * R + rq * 4) = reg[j];
     }
   }
@@ -276,8 +550,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const typename LA::Params pa,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int kbeg = blockIdx.z * k_per_split;
-  const int kend = min(K, kbeg + k_per_split);
+  // k_per_split < 0: blockIdx.z is a batch index the loaders / epilogue read themselves (the whole K per block)
+  const int kbeg = k_per_split > 0 ? (int)blockIdx.z * k_per_split : 0;
+  const int kend = k_per_split > 0 ? min(K, kbeg + k_per_split) : K;
 
   LA la; la.init(pa, m0, tid);
   LB lb; lb.init(pb, n0, tid);
