@@ -1169,7 +1169,7 @@ static int pick_fwd_tile(int M, int N) {
 }
 static int pick_dgrad_tile(int M, int N) {
   if (g_tune.dgrad >= 0) return g_tune.dgrad;
-  if (N == 32) return 0;
+  if (N <= 32) return 0;  // (128 x 32: a2's 16-channel input gradient wastes half a tile instead of three quarters)
   return M >= 64 * 1024 ? 3 : 2;
 }
 static int pick_wgrad_tile(int M, int N) {
@@ -2185,48 +2185,49 @@ __global__ __launch_bounds__(256) void conv4_c1_tfwd_kernel(const float* __restr
   }
 }
 
-constexpr int C1_CHUNK = 128;  // pixels per staging round of conv4_c1_wgrad_kernel
+// conv4_c1_wgrad: a block walks tiles of 256 consecutive A pixels (256 / AW whole rows of one image); the tile's A rows
+// (256 x 32) and its 1-channel source halo ((2 TR + 2) x (2 AW + 2)) in LDS, thread (channel r, tap pair) sums over the
+// tile's pixels (three LDS reads, two FMAs per pixel)
+constexpr int C1_TILE = 256;
 
 __global__ __launch_bounds__(256) void conv4_c1_wgrad_kernel(const float* __restrict__ A, const float* __restrict__ src,
                                                              int NF, int AH, int AW, float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) float as[C1_CHUNK][33];
-  __shared__ float xs[C1_CHUNK][17];
-  const int H = 2 * AH, W = 2 * AW;
-  const int64_t total = (int64_t)NF * AH * AW;
+  __shared__ float as[C1_TILE][33];
+  __shared__ float xs[(2 * C1_TILE / 8 + 2) * (2 * 64 + 2)];  // (AW >= 8, AW <= 64)
+  const int H = 2 * AH, W = 2 * AW, TR = C1_TILE / AW, XW = 2 * AW + 2, XR = 2 * TR + 2;
+  const int64_t ntiles = (int64_t)NF * AH / TR;
   const int t = threadIdx.x, r = t & 31, tp = (t >> 5) * 2;
+  const int k0 = tp, k1 = tp + 1;
+  const int o0 = (k0 / 4) * XW + k0 % 4, o1 = (k1 / 4) * XW + k1 % 4;  // tap offsets in the halo
   float acc0 = 0.f, acc1 = 0.f;
-  for (int64_t p0 = (int64_t)blockIdx.x * C1_CHUNK; p0 < total; p0 += (int64_t)gridDim.x * C1_CHUNK) {
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t img = tile / (AH / TR);
+    const int y0 = (int)(tile % (AH / TR)) * TR;  // first A row of the tile
     __syncthreads();
-    for (int i = t; i < C1_CHUNK * 8; i += 256) {  // A rows: 8 float4 per pixel
-      const int pp = i >> 3, c4 = i & 7;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (p0 + pp < total) v = *reinterpret_cast<const f32x4*>(A + (p0 + pp) * 32 + 4 * c4);
+    const float* arow = A + ((img * AH + y0) * (int64_t)AW) * 32;
+    for (int i = t; i < C1_TILE * 8; i += 256) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(arow + (int64_t)i * 4);
+      const int pp = i >> 3, c4 = (i & 7) * 4;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) as[pp][4 * c4 + e] = v[e];
+      for (int e = 0; e < 4; ++e) as[pp][c4 + e] = v[e];
     }
-    for (int i = t; i < C1_CHUNK * 16; i += 256) {  // patches
-      const int pp = i >> 4, tap = i & 15;
-      float v = 0.f;
-      const int64_t p = p0 + pp;
-      if (p < total) {
-        const int ox = (int)(p % AW);
-        const int64_t rr = p / AW;
-        const int oy = (int)(rr % AH);
-        const int iy = 2 * oy - 1 + tap / 4, ix = 2 * ox - 1 + tap % 4;
-        if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = src[((rr / AH) * H + iy) * W + ix];
-      }
-      xs[pp][tap] = v;
+    const float* simg = src + img * (int64_t)H * W;
+    for (int i = t; i < XR * XW; i += 256) {
+      const int hy = i / XW, hx = i - hy * XW;
+      const int iy = 2 * y0 - 1 + hy, ix = hx - 1;
+      xs[i] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? simg[(int64_t)iy * W + ix] : 0.f;
     }
     __syncthreads();
-#pragma unroll 8
-    for (int pp = 0; pp < C1_CHUNK; ++pp) {
-      const float a = as[pp][r];
-      acc0 = fmaf(a, xs[pp][tp], acc0);
-      acc1 = fmaf(a, xs[pp][tp + 1], acc1);
+    for (int v = 0; v < C1_TILE; ++v) {
+      const int vy = v / AW, vx = v - vy * AW;
+      const int base = 2 * vy * XW + 2 * vx;
+      const float a = as[v][r];
+      acc0 = fmaf(a, xs[base + o0], acc0);
+      acc1 = fmaf(a, xs[base + o1], acc1);
     }
   }
-  slab[(int64_t)blockIdx.x * 512 + r * 16 + tp] = acc0;
-  slab[(int64_t)blockIdx.x * 512 + r * 16 + tp + 1] = acc1;
+  slab[(int64_t)blockIdx.x * 512 + r * 16 + k0] = acc0;
+  slab[(int64_t)blockIdx.x * 512 + r * 16 + k1] = acc1;
 }
 
 int conv4_c1_fwd(const float* src, int NF, int H, int W, const float* w, const float* bias, float* out,
@@ -2250,8 +2251,10 @@ int conv4_c1_tfwd(const float* src, int NF, int SH, int SW, const float* w, cons
 
 int conv4_c1_wgrad(const float* A, const float* src, int NF, int AH, int AW, float* dW, float* slab,
                    int64_t slab_floats, hipStream_t st) {
-  const int64_t total = (int64_t)NF * AH * AW;
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>({cdiv(total, 4 * C1_CHUNK), 512, slab_floats / 512}));
+  VAD_CHECK(AW >= 8 && AW <= 64 && C1_TILE % AW == 0 && AH % (C1_TILE / AW) == 0,
+            "conv4_c1_wgrad: 256 / AW whole rows per tile");
+  const int64_t ntiles = (int64_t)NF * AH * AW / C1_TILE;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>({ntiles, 512, slab_floats / 512}));
   hipLaunchKernelGGL(conv4_c1_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, A, src, NF, AH, AW, slab);
   VAD_LAUNCH_CHECK();
   return conv4_wgrad_reduce(slab, blocks, 32, 1, dW, st);

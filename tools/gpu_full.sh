@@ -1,6 +1,6 @@
 # Full validation on one MI355X box: every GPU test, smoke(), then bench.py at configs 2, 4, 5, 1, cad1 and a2
 # (JSON lines under gpurun_out/); stops at the first failure.
-# usage: gpurun --timeout 1200 -- 'bash tools/tools/gpu_full.sh TAG'
+# usage: gpurun --timeout 1200 -- 'bash tools/gpu_full.sh TAG'
 set -o pipefail
 TAG=${1:-r05}
 mkdir -p gpurun_out
