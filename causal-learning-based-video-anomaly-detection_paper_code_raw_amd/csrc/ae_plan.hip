@@ -238,6 +238,7 @@ __global__ __launch_bounds__(256) void gbn_finalize_kernel(const float* __restri
     const int g = g0 + gl;
     double a = 0.0, b = 0.0;
     if (training && g < q.G)
+#pragma unroll 4
       for (int p = lane; p < q.P; p += 16) {
         const float* pp = parts + ((int64_t)g * q.P + p) * 2 * C;
         a += (double)pp[c];
@@ -348,6 +349,7 @@ __global__ __launch_bounds__(256) void gbn_bwd_finalize_kernel(const float* __re
     const int g = g0 + gl;
     double a = 0.0, b = 0.0;
     if (g < q.G)
+#pragma unroll 4
       for (int p = lane; p < q.P; p += 16) {
         const float* pp = parts + ((int64_t)g * q.P + p) * 2 * C;
         a += (double)pp[c];
