@@ -434,6 +434,7 @@ __global__ __launch_bounds__(256) void a2_conv1_fwd_kernel(const float* __restri
                                                            float* __restrict__ y) {
   __shared__ __attribute__((aligned(16))) float ws[A2C1_TAPS][16];  // [ci*27 + tap][co]
   __shared__ float xs[3 * A2_HALO];
+  __shared__ float os[256 * 17];
   for (int i = threadIdx.x; i < 16 * A2C1_TAPS; i += 256) ws[i % A2C1_TAPS][i / A2C1_TAPS] = w[i];
   const A2Tiles g(B, T, H, W);
   const int v = threadIdx.x, vd = v / (A2T_H * A2T_W), vh = (v / A2T_W) % A2T_H, vw = v % A2T_W;
@@ -448,9 +449,7 @@ __global__ __launch_bounds__(256) void a2_conv1_fwd_kernel(const float* __restri
     __syncthreads();
     a2_stage_halo(xs, x, g, b, d0, h0, w0);
     __syncthreads();
-    const int d = d0 + vd, oh = h0 + vh, ow = w0 + vw;
-    if (d >= T || oh >= g.OH || ow >= g.OW) continue;
-    f32x4 acc[4];
+    f32x4 acc[4];  // (voxels past the volume compute on zero halo and are not stored)
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -465,13 +464,21 @@ __global__ __launch_bounds__(256) void a2_conv1_fwd_kernel(const float* __restri
           for (int e = 0; e < 4; ++e) acc[q][e] = fmaf(xv, wv[e], acc[q][e]);
         }
       }
-    float* o = y + (((b * T + d) * g.OH + oh) * (int64_t)g.OW + ow) * 16;
+    // (through LDS: a voxel row of the output is 64 B, so per-voxel stores would leave every store instruction at a
+    // 64-B lane stride; the tile's W-runs of 16 voxels x 16 channels = 1 KB are written back contiguous)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      f32x4 ov;
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) ov[e] = relu_nan(acc[q][e] + bias[4 * q + e]);
-      *reinterpret_cast<f32x4*>(o + 4 * q) = ov;
+      for (int e = 0; e < 4; ++e) os[v * 17 + 4 * q + e] = relu_nan(acc[q][e] + bias[4 * q + e]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < 256 * 4; i += 256) {  // (voxel, float4) in tile order: W-runs contiguous in y
+      const int vv = i >> 2, c4 = (i & 3) * 4;
+      const int ud = vv / (A2T_H * A2T_W), uh = (vv / A2T_W) % A2T_H, uw = vv % A2T_W;
+      const int dd = d0 + ud, hh = h0 + uh, ww = w0 + uw;
+      if (dd < T && hh < g.OH && ww < g.OW) {
+        const f32x4 o4 = {os[vv * 17 + c4], os[vv * 17 + c4 + 1], os[vv * 17 + c4 + 2], os[vv * 17 + c4 + 3]};
+        *reinterpret_cast<f32x4*>(y + (((b * T + dd) * g.OH + hh) * (int64_t)g.OW + ww) * 16 + c4) = o4;
+      }
     }
   }
 }

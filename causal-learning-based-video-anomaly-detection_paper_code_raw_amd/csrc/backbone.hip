@@ -2114,36 +2114,43 @@ __global__ __launch_bounds__(256) void conv4_c1_fwd_kernel(const float* __restri
                                                            const float* __restrict__ w, const float* __restrict__ bias,
                                                            float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) float ws[16][32];  // [tap][n]
+  __shared__ __attribute__((aligned(16))) float os[256 * 33];  // the block's 256 output rows, written back coalesced
   for (int i = threadIdx.x; i < 512; i += 256) ws[i % 16][i / 16] = w[i];
-  __syncthreads();
   const int OH = H / 2, OW = W / 2;
   const int64_t total = (int64_t)NF * OH * OW;
-  for (int64_t p = blockIdx.x * 256ll + threadIdx.x; p < total; p += (int64_t)gridDim.x * 256) {
-    const int ox = (int)(p % OW);
-    const int64_t r = p / OW;
-    const int oy = (int)(r % OH);
-    const float* img = src + (r / OH) * H * W;
-    float x[16];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int iy = 2 * oy - 1 + t / 4, ix = 2 * ox - 1 + t % 4;
-      x[t] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? img[iy * W + ix] : 0.f;
-    }
-    float* o = out + p * 32;
-#pragma unroll
-    for (int n4 = 0; n4 < 8; ++n4) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t p0 = blockIdx.x * 256ll; p0 < total; p0 += (int64_t)gridDim.x * 256) {
+    __syncthreads();
+    const int64_t p = p0 + threadIdx.x;
+    if (p < total) {
+      const int ox = (int)(p % OW);
+      const int64_t r = p / OW;
+      const int oy = (int)(r % OH);
+      const float* img = src + (r / OH) * H * W;
+      float x[16];
 #pragma unroll
       for (int t = 0; t < 16; ++t) {
-        const f32x4 wv = *reinterpret_cast<const f32x4*>(&ws[t][4 * n4]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] = fmaf(x[t], wv[e], acc[e]);
+        const int iy = 2 * oy - 1 + t / 4, ix = 2 * ox - 1 + t % 4;
+        x[t] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? img[iy * W + ix] : 0.f;
       }
-      if (bias) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] += bias[4 * n4 + e];
+      for (int n4 = 0; n4 < 8; ++n4) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          const f32x4 wv = *reinterpret_cast<const f32x4*>(&ws[t][4 * n4]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[e] = fmaf(x[t], wv[e], acc[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) os[threadIdx.x * 33 + 4 * n4 + e] = acc[e] + (bias ? bias[4 * n4 + e] : 0.f);
       }
-      *reinterpret_cast<f32x4*>(o + 4 * n4) = acc;
+    }
+    __syncthreads();
+    const int64_t nrow = min((int64_t)256, total - p0);
+    for (int i = threadIdx.x; i < nrow * 8; i += 256) {  // 8 float4 per output row, consecutive lanes -> consecutive
+      const int row = i >> 3, c4 = (i & 7) * 4;
+      const f32x4 v = {os[row * 33 + c4], os[row * 33 + c4 + 1], os[row * 33 + c4 + 2], os[row * 33 + c4 + 3]};
+      *reinterpret_cast<f32x4*>(out + (p0 + row) * 32 + c4) = v;
     }
   }
 }
