@@ -829,15 +829,15 @@ struct A2PlanImpl {
     float* cur = dA;  // (direct: the input gradients ping-pong between dA and dA2)
     for (int s3 = 2; s3 >= 0; --s3) {
       const int64_t rows = g[s3].rows();
-      float* dA = cur;
-      VAD_TRY(relu_gate(dA, y[s3], rows * A2_CO[s3], st));
+      float* const dg = cur;  // the gradient w.r.t. this stage's output (then its pre-activation)
+      VAD_TRY(relu_gate(dg, y[s3], rows * A2_CO[s3], st));
       if (direct && s3 > 0) {  // conv3d_2 / conv3d_3 on the implicit GEMMs
         const Vol5& in = g[s3].in;
-        float* nxt = dA == this->dA ? dA2 : this->dA;
-        VAD_TRY(col_sum(dA, rows, A2_CO[s3], G(2 * s3 + 1), st));
-        VAD_TRY(conv3s2_wgrad(dA, A2_CO[s3], y[s3 - 1], in.C, B, in.D, in.H, in.W, G(2 * s3), scratch, scratch_floats,
+        float* nxt = dg == dA ? dA2 : dA;
+        VAD_TRY(col_sum(dg, rows, A2_CO[s3], G(2 * s3 + 1), st));
+        VAD_TRY(conv3s2_wgrad(dg, A2_CO[s3], y[s3 - 1], in.C, B, in.D, in.H, in.W, G(2 * s3), scratch, scratch_floats,
                               1024, st));
-        VAD_TRY(conv3s2_dgrad(dA, B, A2_CO[s3], wc3[s3], in.C, nxt, in.D, in.H, in.W, st));
+        VAD_TRY(conv3s2_dgrad(dg, B, A2_CO[s3], wc3[s3], in.C, nxt, in.D, in.H, in.W, st));
         cur = nxt;
         continue;
       }
@@ -845,18 +845,18 @@ struct A2PlanImpl {
         const A2Tiles tl(B, T, H, W);
         const int64_t cap = scratch_floats / (16 * (A2C1_TAPS + 1));
         const int nb = (int)std::max<int64_t>(1, std::min<int64_t>({tl.n, 512, cap}));
-        hipLaunchKernelGGL(a2_conv1_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, st, dA, xin, B, T, H, W, scratch);
+        hipLaunchKernelGGL(a2_conv1_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, st, dg, xin, B, T, H, W, scratch);
         VAD_LAUNCH_CHECK();
         hipLaunchKernelGGL(a2_conv1_wgrad_reduce_kernel, dim3((unsigned)cdiv(16 * (A2C1_TAPS + 1), 4)), dim3(256), 0,
                            st, scratch, nb, G(S_C1W), G(S_C1B));
         VAD_LAUNCH_CHECK();
         continue;
       }
-      VAD_TRY(dense_wgrad(dA, (int)rows, A2_CO[s3], cols[s3], g[s3].K(), G(2 * s3), G(2 * s3 + 1), scratch,
+      VAD_TRY(dense_wgrad(dg, (int)rows, A2_CO[s3], cols[s3], g[s3].K(), G(2 * s3), G(2 * s3 + 1), scratch,
                           scratch_floats, nullptr, st, 1024));
       if (s3 > 0) {
-        VAD_TRY(dense_dgrad(dA, (int)rows, A2_CO[s3], P(2 * s3), g[s3].K(), dcols, nullptr, 1.f, nullptr, st));
-        VAD_TRY(col2im3d(dcols, g[s3], dA, st));
+        VAD_TRY(dense_dgrad(dg, (int)rows, A2_CO[s3], P(2 * s3), g[s3].K(), dcols, nullptr, 1.f, nullptr, st));
+        VAD_TRY(col2im3d(dcols, g[s3], dg, st));
       }
     }
     return 0;
