@@ -542,19 +542,23 @@ __global__ __launch_bounds__(256) void a2_conv1_wgrad_kernel(const float* __rest
     if (off[m] != -2) slab[((int64_t)blockIdx.x * 16 + co) * (A2C1_TAPS + 1) + grp + 16 * m] = acc[m];
 }
 
-// dW[co][ci*27 + tap] / db[co] = sum over the S slabs in order: 4 entries per block, 64 lanes each, fixed butterfly
+// dW[co][ci*27 + tap] / db[co] = sum over the S slabs: 64 consecutive entries x 4 slab lanes per block (lane l adds
+// slabs l, l + 4, ... in order, coalesced across the entries), the lane sums combined in a fixed order
 __global__ __launch_bounds__(256) void a2_conv1_wgrad_reduce_kernel(const float* __restrict__ slab, int S,
                                                                     float* __restrict__ dW, float* __restrict__ db) {
   constexpr int NE = 16 * (A2C1_TAPS + 1);
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  __shared__ float red[4][64];
+  const int e = threadIdx.x & 63, sl = threadIdx.x >> 6, i = blockIdx.x * 64 + e;
   float v = 0.f;
   if (i < NE)
-    for (int z = lane; z < S; z += 64) v += slab[(int64_t)z * NE + i];
-  v = wave_sum(v);
-  if (lane == 0 && i < NE) {
+    for (int z = sl; z < S; z += 4) v += slab[(int64_t)z * NE + i];
+  red[sl][e] = v;
+  __syncthreads();
+  if (sl == 0 && i < NE) {
+    const float t = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
     const int co = i / (A2C1_TAPS + 1), j = i % (A2C1_TAPS + 1);
-    if (j < A2C1_TAPS) dW[co * A2C1_TAPS + j] = v;
-    else db[co] = v;
+    if (j < A2C1_TAPS) dW[co * A2C1_TAPS + j] = t;
+    else db[co] = t;
   }
 }
 
@@ -834,7 +838,7 @@ struct A2PlanImpl {
       if (direct && s3 > 0) {  // conv3d_2 / conv3d_3 on the implicit GEMMs
         const Vol5& in = g[s3].in;
         float* nxt = dg == dA ? dA2 : dA;
-        VAD_TRY(col_sum(dg, rows, A2_CO[s3], G(2 * s3 + 1), st));
+        VAD_TRY(col_sum(dg, rows, A2_CO[s3], G(2 * s3 + 1), reinterpret_cast<double*>(scratch), st));
         VAD_TRY(conv3s2_wgrad(dg, A2_CO[s3], y[s3 - 1], in.C, B, in.D, in.H, in.W, G(2 * s3), scratch, scratch_floats,
                               1024, st));
         VAD_TRY(conv3s2_dgrad(dg, B, A2_CO[s3], wc3[s3], in.C, nxt, in.D, in.H, in.W, st));
@@ -847,7 +851,7 @@ struct A2PlanImpl {
         const int nb = (int)std::max<int64_t>(1, std::min<int64_t>({tl.n, 512, cap}));
         hipLaunchKernelGGL(a2_conv1_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, st, dg, xin, B, T, H, W, scratch);
         VAD_LAUNCH_CHECK();
-        hipLaunchKernelGGL(a2_conv1_wgrad_reduce_kernel, dim3((unsigned)cdiv(16 * (A2C1_TAPS + 1), 4)), dim3(256), 0,
+        hipLaunchKernelGGL(a2_conv1_wgrad_reduce_kernel, dim3((unsigned)cdiv(16 * (A2C1_TAPS + 1), 64)), dim3(256), 0,
                            st, scratch, nb, G(S_C1W), G(S_C1B));
         VAD_LAUNCH_CHECK();
         continue;

@@ -240,7 +240,8 @@ int conv3s2_dgrad(const float* dy, int NF, int Co, const float* wc, int Ci, floa
                   hipStream_t st);
 int conv3s2_wgrad(const float* dy, int Co, const float* src, int Ci, int NF, int D, int H, int W, float* dW,
                   float* part, int64_t part_cap, int target_blocks, hipStream_t st);
-int col_sum(const float* x, int64_t M, int N, float* db, hipStream_t st);
+// scratch: 256 * N doubles
+int col_sum(const float* x, int64_t M, int N, float* db, double* scratch, hipStream_t st);
 // the single-channel ends, 32 channels on the other side, on the VALU: w = the [32][1][4][4] / [32][16] weight
 int conv4_c1_fwd(const float* src, int NF, int H, int W, const float* w, const float* bias, float* out,
                  hipStream_t st);

@@ -2066,28 +2066,40 @@ __global__ __launch_bounds__(256) void conv4_wgrad_reduce_kernel(const float* __
   }
 }
 
-// the same for small outputs with many slabs: 4 entries per block, 64 lanes each adding slabs lane, lane + 64, ... in
-// order, then a fixed butterfly
+// the same for many slabs: 64 consecutive entries x 4 slab lanes per block (lane l adds slabs l, l + 4, ... in order
+// with 8 loads in flight, coalesced across the 64 entries), the 4 lane sums combined in a fixed order
 __global__ __launch_bounds__(256) void conv4_wgrad_reduce_small_kernel(const float* __restrict__ part, int S, int R,
                                                                        int C, int NT, float* __restrict__ dW) {
+  __shared__ float red[4][64];
   const int64_t total = (int64_t)R * NT * C;
-  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+  const int e = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + e;
   float v = 0.f;
-  if (i < total)
-    for (int z = lane; z < S; z += 64) v += part[(int64_t)z * total + i];
-  v = wave_sum(v);
-  if (lane == 0 && i < total) {
+  if (i < total) {
+    const int n = S > sl ? (S - sl + 3) / 4 : 0;
+    for (int k0 = 0; k0 < n; k0 += 8) {
+      float u[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) u[q] = part[(int64_t)(sl + 4 * min(k0 + q, n - 1)) * total + i];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (k0 + q < n) v += u[q];
+    }
+  }
+  red[sl][e] = v;
+  __syncthreads();
+  if (sl == 0 && i < total) {
+    const float t = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
     const int c = (int)(i % C), tap = (int)((i / C) % NT);
     const int64_t r = i / ((int64_t)NT * C);
-    dW[(r * C + c) * NT + tap] = v;
+    dW[(r * C + c) * NT + tap] = t;
   }
 }
 
 static int taps_wgrad_reduce(const float* part, int S, int R, int C, int NT, float* dW, hipStream_t st) {
   const int64_t total = (int64_t)R * NT * C;
-  if (total <= 65536 && S >= 64) {
-    hipLaunchKernelGGL(conv4_wgrad_reduce_small_kernel, dim3((unsigned)cdiv(total, 4)), dim3(256), 0, st, part, S, R, C,
+  if (S >= 16) {
+    hipLaunchKernelGGL(conv4_wgrad_reduce_small_kernel, dim3((unsigned)cdiv(total, 64)), dim3(256), 0, st, part, S, R, C,
                        NT, dW);
     VAD_LAUNCH_CHECK();
     return 0;
@@ -2225,12 +2237,15 @@ __global__ __launch_bounds__(256) void conv4_c1_wgrad_kernel(const float* __rest
       xs[i] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? simg[(int64_t)iy * W + ix] : 0.f;
     }
     __syncthreads();
-    for (int v = 0; v < C1_TILE; ++v) {
-      const int vy = v / AW, vx = v - vy * AW;
-      const int base = 2 * vy * XW + 2 * vx;
-      const float a = as[v][r];
-      acc0 = fmaf(a, xs[base + o0], acc0);
-      acc1 = fmaf(a, xs[base + o1], acc1);
+    for (int vy = 0; vy < TR; ++vy) {  // (pixel v = vy * AW + vx, walked without divisions)
+      const float* arow = &as[vy * AW][r];
+      const float* xrow = xs + 2 * vy * XW;
+#pragma unroll 4
+      for (int vx = 0; vx < AW; ++vx) {
+        const float a = arow[vx * 33];
+        acc0 = fmaf(a, xrow[2 * vx + o0], acc0);
+        acc1 = fmaf(a, xrow[2 * vx + o1], acc1);
+      }
     }
   }
   slab[(int64_t)blockIdx.x * 512 + r * 16 + k0] = acc0;
@@ -2425,24 +2440,41 @@ int conv3s2_wgrad(const float* dy, int Co, const float* src, int Ci, int NF, int
   return taps_wgrad_reduce(part, used, Co, Ci, 27, dW, st);
 }
 
-// db[n] = sum over the M rows of x[m][n], fixed order: one block per column, 256-way strided + tree (double)
-__global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ x, int64_t M, int N,
-                                                      float* __restrict__ db) {
+// db[n] = sum over the M rows of x[m][n], fixed order, two passes: block b sums the rows of its contiguous range with
+// 256 / N row lanes per column (coalesced rows), lanes combined by a fixed tree -> part[b][n]; then one block adds the
+// block sums in order (double).  N divides 256.
+__global__ __launch_bounds__(256) void col_sum_part_kernel(const float* __restrict__ x, int64_t M, int N, int64_t rows,
+                                                           double* __restrict__ part) {
   __shared__ double red[256];
-  const int n = blockIdx.x;
+  const int n = threadIdx.x % N, lane = threadIdx.x / N, lanes = 256 / N;
+  const int64_t r0 = (int64_t)blockIdx.x * rows, r1 = min(M, r0 + rows);
   double s = 0.0;
-  for (int64_t m = threadIdx.x; m < M; m += 256) s += (double)x[m * N + n];
+#pragma unroll 4
+  for (int64_t m = r0 + lane; m < r1; m += lanes) s += (double)x[m * N + n];
   red[threadIdx.x] = s;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+  for (int o = lanes / 2; o > 0; o >>= 1) {
+    if (lane < o) red[threadIdx.x] += red[threadIdx.x + o * N];
     __syncthreads();
   }
-  if (threadIdx.x == 0) db[n] = (float)red[0];
+  if (lane == 0) part[(int64_t)blockIdx.x * N + n] = red[n];
+}
+__global__ __launch_bounds__(256) void col_sum_fin_kernel(const double* __restrict__ part, int P, int N,
+                                                          float* __restrict__ db) {
+  for (int n = threadIdx.x; n < N; n += 256) {
+    double s = 0.0;
+    for (int p = 0; p < P; ++p) s += part[(int64_t)p * N + n];
+    db[n] = (float)s;
+  }
 }
 
-int col_sum(const float* x, int64_t M, int N, float* db, hipStream_t st) {
-  hipLaunchKernelGGL(col_sum_kernel, dim3((unsigned)N), dim3(256), 0, st, x, M, N, db);
+int col_sum(const float* x, int64_t M, int N, float* db, double* scratch, hipStream_t st) {
+  VAD_CHECK(N >= 1 && N <= 256 && 256 % N == 0, "col_sum: N divides 256");
+  const int64_t rows = std::max<int64_t>(256 / N, cdiv(M, 256));
+  const int P = (int)cdiv(M, rows);
+  hipLaunchKernelGGL(col_sum_part_kernel, dim3((unsigned)P), dim3(256), 0, st, x, M, N, rows, scratch);
+  VAD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(col_sum_fin_kernel, dim3(1), dim3(256), 0, st, scratch, P, N, db);
   VAD_LAUNCH_CHECK();
   return 0;
 }
