@@ -542,23 +542,30 @@ __global__ __launch_bounds__(256) void a2_conv1_wgrad_kernel(const float* __rest
     if (off[m] != -2) slab[((int64_t)blockIdx.x * 16 + co) * (A2C1_TAPS + 1) + grp + 16 * m] = acc[m];
 }
 
-// dW[co][ci*27 + tap] / db[co] = sum over the S slabs: 64 consecutive entries x 4 slab lanes per block (lane l adds
-// slabs l, l + 4, ... in order, coalesced across the entries), the lane sums combined in a fixed order
+// dW[co][ci*27 + tap] / db[co] = sum over the S slabs: 16 consecutive entries x 16 slab lanes per block (lane l adds
+// slabs l, l + 16, ... in order, 8 loads in flight), the lane sums combined by a fixed tree
 __global__ __launch_bounds__(256) void a2_conv1_wgrad_reduce_kernel(const float* __restrict__ slab, int S,
                                                                     float* __restrict__ dW, float* __restrict__ db) {
   constexpr int NE = 16 * (A2C1_TAPS + 1);
-  __shared__ float red[4][64];
-  const int e = threadIdx.x & 63, sl = threadIdx.x >> 6, i = blockIdx.x * 64 + e;
+  __shared__ float red[16][17];
+  const int e = threadIdx.x & 15, sl = threadIdx.x >> 4, i = blockIdx.x * 16 + e;
   float v = 0.f;
-  if (i < NE)
-    for (int z = sl; z < S; z += 4) v += slab[(int64_t)z * NE + i];
+  if (i < NE) {
+#pragma unroll 8
+    for (int z = sl; z < S; z += 16) v += slab[(int64_t)z * NE + i];
+  }
   red[sl][e] = v;
   __syncthreads();
   if (sl == 0 && i < NE) {
-    const float t = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+    float t[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[k] = red[2 * k][e] + red[2 * k + 1][e];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] = t[2 * k] + t[2 * k + 1];
+    const float r = (t[0] + t[1]) + (t[2] + t[3]);
     const int co = i / (A2C1_TAPS + 1), j = i % (A2C1_TAPS + 1);
-    if (j < A2C1_TAPS) dW[co * A2C1_TAPS + j] = t;
-    else db[co] = t;
+    if (j < A2C1_TAPS) dW[co * A2C1_TAPS + j] = r;
+    else db[co] = r;
   }
 }
 
@@ -851,7 +858,7 @@ struct A2PlanImpl {
         const int nb = (int)std::max<int64_t>(1, std::min<int64_t>({tl.n, 512, cap}));
         hipLaunchKernelGGL(a2_conv1_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, st, dg, xin, B, T, H, W, scratch);
         VAD_LAUNCH_CHECK();
-        hipLaunchKernelGGL(a2_conv1_wgrad_reduce_kernel, dim3((unsigned)cdiv(16 * (A2C1_TAPS + 1), 64)), dim3(256), 0,
+        hipLaunchKernelGGL(a2_conv1_wgrad_reduce_kernel, dim3((unsigned)cdiv(16 * (A2C1_TAPS + 1), 16)), dim3(256), 0,
                            st, scratch, nb, G(S_C1W), G(S_C1B));
         VAD_LAUNCH_CHECK();
         continue;

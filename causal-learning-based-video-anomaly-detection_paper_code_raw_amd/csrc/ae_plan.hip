@@ -41,6 +41,9 @@
 namespace vad {
 
 int g_ae_direct = 1;  // knob "ae_direct" (latched per plan)
+// knob "ae_wgrad_stream" (latched per plan, direct mode): the backward's weight gradients run on a low-priority stream
+// of the plan beside the input-gradient chain, on their own split-K scratch, with dY alternating between two buffers
+int g_ae_wgrad_stream = 1;
 
 constexpr int AE_HW = 64;  // frame side: the encoder's Linear(128 * 4 * 4) fixes 64x64 frames (cad1:151)
 constexpr int AE_PIX = AE_HW * AE_HW;
@@ -780,12 +783,16 @@ struct AePlanImpl {
   int32_t* steps = nullptr;
   // workspace
   float *xf, *ecols[4], *ey[4], *ea[4], *est[4], *z, *lat, *gx, *gates, *cs, *hprev, *seq;
-  float *u, *dx[4], *dy[4], *dst[3], *dylast, *parts, *bparts, *lpart, *losses, *bufA, *bufB, *bcols;
-  float *dG, *dlat, *dz, *da3, *dseq, *dU, *scratch;
+  float *u, *dx[4], *dy[4], *dst[3], *dylast, *parts, *bparts, *bparts2 = nullptr, *lpart, *losses, *bufA, *bufB, *bcols;
+  float *dG, *dlat, *dz, *da3, *dseq, *dU, *scratch, *bufC = nullptr, *scratch2 = nullptr;
   // implicit-GEMM weight images (conv4_prep): encoder layers 1-3 [Co][16 Ci] (forward) / [4][Ci][4 Co] (input grad),
   // decoder layers [4][Co][4 Ci] (forward) / [Ci][16 Co] (input grad, layers 0-2)
   float *ewk[4] = {}, *ewc[4] = {}, *dwk[4] = {}, *dwc[4] = {};
   const int direct = g_ae_direct;
+  const int side = g_ae_direct && g_ae_wgrad_stream;
+  hipStream_t sw = nullptr;  // weight-gradient stream (side)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_wg[2] = {nullptr, nullptr};
+  int wg_pending[2] = {0, 0};
   int* bad;
   double* sum_parts;
   AdamWs aws{};
@@ -801,6 +808,46 @@ struct AePlanImpl {
   float* P(int s) const { return params + ae_layout().slots[s].offset; }
   float* G(int s) const { return grads + ae_layout().slots[s].offset; }
   float* RB(int b) const { return bufs + ae_layout().bufs[b].offset; }
+  ~AePlanImpl() {
+    for (hipEvent_t e : {ev_fork, ev_join, ev_wg[0], ev_wg[1]})
+      if (e) (void)hipEventDestroy(e);
+    if (sw) (void)hipStreamDestroy(sw);
+  }
+  // the weight-gradient stream, ordered after everything queued so far on st (st itself without the side stream)
+  int fork(hipStream_t st, hipStream_t* out) {
+    *out = st;
+    if (!side) return 0;
+    if (!sw) {
+      int lo = 0, hi = 0;
+      VAD_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      VAD_HIP(hipStreamCreateWithPriority(&sw, hipStreamNonBlocking, lo));
+      const unsigned evf = hipEventDisableTiming | (unsigned)hipEventDisableSystemFence;
+      for (hipEvent_t* e : {&ev_fork, &ev_join, &ev_wg[0], &ev_wg[1]}) VAD_HIP(hipEventCreateWithFlags(e, evf));
+    }
+    VAD_HIP(hipEventRecord(ev_fork, st));
+    VAD_HIP(hipStreamWaitEvent(sw, ev_fork, 0));
+    *out = sw;
+    return 0;
+  }
+  // dY buffer k: the side stream's reads of it are queued (mark), st must not overwrite it before they end (reuse)
+  int wg_mark(int k) {
+    if (!side) return 0;
+    VAD_HIP(hipEventRecord(ev_wg[k], sw));
+    wg_pending[k] = 1;
+    return 0;
+  }
+  int wg_reuse(int k, hipStream_t st) {
+    if (side && wg_pending[k]) VAD_HIP(hipStreamWaitEvent(st, ev_wg[k], 0));
+    wg_pending[k] = 0;
+    return 0;
+  }
+  int join(hipStream_t st) {
+    if (!side || !sw) return 0;
+    VAD_HIP(hipEventRecord(ev_join, sw));
+    VAD_HIP(hipStreamWaitEvent(st, ev_join, 0));
+    wg_pending[0] = wg_pending[1] = 0;
+    return 0;
+  }
   Gbn enc_bn(int l) const { return gbn(T, ge[l].rows() / T, ENC_CO[l]); }
   Gbn dec_bn(int j) const { return gbn(1, gd[j].in.voxels(), DEC_CO[j]); }
 
@@ -848,10 +895,12 @@ struct AePlanImpl {
     dylast = w.take<float>((int64_t)B * AE_PIX);
     parts = w.take<float>(max_parts);
     bparts = w.take<float>(max_parts);
+    if (side) bparts2 = w.take<float>(max_parts);
     lpart = w.take<float>((int64_t)B * AE_CHUNKS);
     losses = w.take<float>(4);
     bufA = w.take<float>(max_act);
     bufB = w.take<float>(max_act);
+    if (side) bufC = w.take<float>(max_act);
     bcols = w.take<float>(max_cols);
     dG = w.take<float>((int64_t)NF * AE_GATES);
     dlat = w.take<float>((int64_t)NF * AE_LAT);
@@ -861,6 +910,7 @@ struct AePlanImpl {
     dU = w.take<float>((int64_t)B * AE_FLAT);
     scratch_floats = 32ll << 20;  // (split-K slabs of the weight gradients: 128 MB)
     scratch = w.take<float>(scratch_floats);
+    if (side) scratch2 = w.take<float>(scratch_floats);
     bad = w.take<int>(4);
     aws.sq = w.take<double>(ADAM_MAX_SLOTS * ADAM_SQ_CHUNKS);
     aws.bad = w.take<int>(ADAM_MAX_SLOTS * ADAM_SQ_CHUNKS);
@@ -886,19 +936,23 @@ struct AePlanImpl {
   }
 
   // dY = grad through LeakyReLU(BN(y)) given dA; gamma / beta grads into slots gw / gb; dbias (nullable) = sum(dY)
+  // kb: the dY buffer's index -- with the side stream the conv-bias sum (dbias) runs there, on bparts / bparts2 by kb
+  // (the same reuse event as the dY buffer: the side stream's weight gradient of dY is queued after it)
   int bn_bwd(const float* dA, const float* y, const Gbn& q, int gw, int gb, float* stats, float* dY, float* dbias,
-             hipStream_t st) {
+             hipStream_t st, int kb = 0) {
+    float* const bp = side && kb ? bparts2 : bparts;
     hipLaunchKernelGGL(gbn_bwd_reduce_kernel, dim3(q.P, q.G), dim3(256), 0, st, dA, y, stats, q, parts);
     VAD_LAUNCH_CHECK();
     hipLaunchKernelGGL(gbn_bwd_finalize_kernel, dim3(q.C), dim3(256), 0, st, parts, q, P(gw), training, stats, G(gw),
                        G(gb));
     VAD_LAUNCH_CHECK();
     hipLaunchKernelGGL(gbn_bwd_apply_kernel, dim3(q.P, q.G), dim3(256), 0, st, dA, y, stats, q, dY,
-                       dbias ? bparts : nullptr);
+                       dbias ? bp : nullptr);
     VAD_LAUNCH_CHECK();
     if (dbias) {
-      hipLaunchKernelGGL(ae_bias_reduce_kernel, dim3((unsigned)q.C), dim3(256), 0, st, bparts, q.G * q.P,
-                         q.C, dbias);
+      hipStream_t bs = st;
+      VAD_TRY(fork(st, &bs));
+      hipLaunchKernelGGL(ae_bias_reduce_kernel, dim3((unsigned)q.C), dim3(256), 0, bs, bp, q.G * q.P, q.C, dbias);
       VAD_LAUNCH_CHECK();
     }
     return 0;
@@ -909,18 +963,31 @@ struct AePlanImpl {
     const AeLayout& L = ae_layout();
     const bool enc = stages & 1, dec = stages & 2;
     const int* skip = loss_mode == 2 ? bad : nullptr;
+    bool dec_prepped = false, prep_wait = false;
     const DenseAct none{};
     VAD_HIP(hipMemsetAsync(bad, 0, sizeof(int), st));
     if (enc) {
       hipLaunchKernelGGL(ae_frames_kernel, grid_for((int64_t)NF * AE_PIX / 4), dim3(256), 0, st, x, B, T, xf, bad);
       VAD_LAUNCH_CHECK();
-      if (direct)
-        for (int l = 1; l < 4; ++l) VAD_TRY(conv4_prep(P(L.enc_w[l]), ENC_CO[l], ENC_CI[l], ewk[l], ewc[l], st));
+      if (direct) {  // the weight images on the side stream, beside the first layer (waited for before layer 1)
+        hipStream_t ps = st;
+        VAD_TRY(fork(st, &ps));
+        for (int l = 1; l < 4; ++l) VAD_TRY(conv4_prep(P(L.enc_w[l]), ENC_CO[l], ENC_CI[l], ewk[l], ewc[l], ps));
+        if (dec)
+          for (int j = 0; j < 3; ++j) VAD_TRY(conv4_prep(P(L.dec_w[j]), DEC_CI[j], DEC_CO[j], dwk[j], dwc[j], ps));
+        dec_prepped = dec;
+        if (ps != st) {
+          VAD_HIP(hipEventRecord(ev_join, ps));
+          prep_wait = true;
+        }
+      }
       for (int l = 0; l < 4; ++l) {
         const int64_t M = ge[l].rows();
         if (direct && l == 0) {
           VAD_TRY(conv4_c1_fwd(xf, NF, AE_HW, AE_HW, P(L.enc_w[0]), P(L.enc_b[0]), ey[0], st));
         } else if (direct) {
+          if (prep_wait) VAD_HIP(hipStreamWaitEvent(st, ev_join, 0));
+          prep_wait = false;
           VAD_TRY(conv4_fwd(ea[l - 1], NF, ENC_IN[l], ENC_IN[l], ENC_CI[l], ewk[l], P(L.enc_b[l]), ENC_CO[l], ey[l],
                             st, scratch, scratch_floats));
         } else {
@@ -952,7 +1019,7 @@ struct AePlanImpl {
       VAD_TRY(dense_fwd(seq, B, AE_LAT, P(L.dfc_w), P(L.dfc_b), AE_FLAT, u, none, scratch, scratch_floats, st));
       hipLaunchKernelGGL(ae_dec_in_kernel, grid_for((int64_t)B * AE_FLAT), dim3(256), 0, st, u, B, dx[0]);
       VAD_LAUNCH_CHECK();
-      if (direct)
+      if (direct && !dec_prepped)
         for (int j = 0; j < 3; ++j) VAD_TRY(conv4_prep(P(L.dec_w[j]), DEC_CI[j], DEC_CO[j], dwk[j], dwc[j], st));
       for (int j = 0; j < 4; ++j) {
         if (direct && j == 3) {  // ConvTranspose2d(32, 1): 128 MACs per output pixel on the VALU
@@ -1002,23 +1069,37 @@ struct AePlanImpl {
                          dylast);
       VAD_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(ae_sum_parts_kernel, dim3(AE_SUM_BLOCKS), dim3(256), 0, st, dylast, (int64_t)B * AE_PIX,
+    // direct mode with the side stream: weight gradients (and their split-K reduces) on sw with scratch2, dY of the
+    // BN backwards alternating between bufB / bufC so the next layer's dY never overwrites one still being read
+    float* const dyb[2] = {bufB, side ? bufC : bufB};
+    int kb = 1;
+    auto next_dy = [&](hipStream_t s) -> float* {
+      kb ^= side;
+      if (wg_reuse(kb, s)) return nullptr;
+      return dyb[kb];
+    };
+    float* const scr2 = side ? scratch2 : scratch;
+    hipStream_t ws = st;
+    VAD_TRY(fork(st, &ws));
+    hipLaunchKernelGGL(ae_sum_parts_kernel, dim3(AE_SUM_BLOCKS), dim3(256), 0, ws, dylast, (int64_t)B * AE_PIX,
                        sum_parts);
     VAD_LAUNCH_CHECK();
-    hipLaunchKernelGGL(ae_sum_kernel, dim3(1), dim3(AE_SUM_BLOCKS), 0, st, sum_parts, G(L.dec_b[3]));
+    hipLaunchKernelGGL(ae_sum_kernel, dim3(1), dim3(AE_SUM_BLOCKS), 0, ws, sum_parts, G(L.dec_b[3]));
     VAD_LAUNCH_CHECK();
     // decoder, last ConvTranspose2d first: dX_j = im2col(dY_j) Wt^T, dWt = X_j^T im2col(dY_j)
     const float* dcur = dylast;
     for (int j = 3; j >= 0; --j) {
       const int M = (int)gd[j].rows(), K = gd[j].K(), Ci = DEC_CI[j];
       if (direct && j == 3) {
-        VAD_TRY(conv4_c1_wgrad(dx[3], dcur, B, DEC_IN[3], DEC_IN[3], G(L.dec_w[3]), scratch, scratch_floats, st));
+        VAD_TRY(conv4_c1_wgrad(dx[3], dcur, B, DEC_IN[3], DEC_IN[3], G(L.dec_w[3]), scr2, scratch_floats, ws));
         VAD_TRY(conv4_c1_fwd(dcur, B, 2 * DEC_IN[3], 2 * DEC_IN[3], P(L.dec_w[3]), nullptr, bufA, st));
       } else if (direct) {
         int ns = 0;
-        VAD_TRY(conv4_wgrad(dx[j], Ci, dcur, DEC_CO[j], B, DEC_IN[j], DEC_IN[j], scratch, &ns, scratch_floats,
-                            g_ae_wgrad_blocks, st));
-        VAD_TRY(conv4_wgrad_reduce(scratch, ns, Ci, DEC_CO[j], G(L.dec_w[j]), st));
+        VAD_TRY(fork(st, &ws));
+        VAD_TRY(conv4_wgrad(dx[j], Ci, dcur, DEC_CO[j], B, DEC_IN[j], DEC_IN[j], scr2, &ns, scratch_floats,
+                            g_ae_wgrad_blocks, ws));
+        VAD_TRY(conv4_wgrad_reduce(scr2, ns, Ci, DEC_CO[j], G(L.dec_w[j]), ws));
+        VAD_TRY(wg_mark(kb));
         VAD_TRY(conv4_fwd(dcur, B, 2 * DEC_IN[j], 2 * DEC_IN[j], DEC_CO[j], dwk[j], nullptr, Ci, bufA, st, scratch,
                           scratch_floats));
       } else {
@@ -1028,14 +1109,17 @@ struct AePlanImpl {
       }
       if (j > 0) {
         // X_j = LeakyReLU(BN_{j-1}(y_{j-1})); sum(dY_{j-1}) is the bias grad of ConvTranspose2d j-1
-        VAD_TRY(bn_bwd(bufA, dy[j - 1], dec_bn(j - 1), L.dbn_w[j - 1], L.dbn_b[j - 1], dst[j - 1], bufB,
-                       G(L.dec_b[j - 1]), st));
-        dcur = bufB;
+        float* dY = next_dy(st);
+        VAD_CHECK(dY != nullptr, "vad_ae_backward: stream wait failed");
+        VAD_TRY(bn_bwd(bufA, dy[j - 1], dec_bn(j - 1), L.dbn_w[j - 1], L.dbn_b[j - 1], dst[j - 1], dY,
+                       G(L.dec_b[j - 1]), st, kb));
+        dcur = dY;
       }
     }
     hipLaunchKernelGGL(ae_dec_in_bwd_kernel, grid_for((int64_t)B * AE_FLAT), dim3(256), 0, st, bufA, u, B, dU);
     VAD_LAUNCH_CHECK();
-    VAD_TRY(dense_wgrad(dU, B, AE_FLAT, seq, AE_LAT, G(L.dfc_w), G(L.dfc_b), scratch, scratch_floats, nullptr, st));
+    VAD_TRY(fork(st, &ws));
+    VAD_TRY(dense_wgrad(dU, B, AE_FLAT, seq, AE_LAT, G(L.dfc_w), G(L.dfc_b), scr2, scratch_floats, nullptr, ws));
     VAD_TRY(dense_dgrad(dU, B, AE_FLAT, P(L.dfc_w), AE_LAT, dseq, nullptr, 1.f, nullptr, st, 0, scratch,
                         scratch_floats));
     if (d_seq) {
@@ -1046,13 +1130,15 @@ struct AePlanImpl {
     // LSTM BPTT, then the W_ih / W_hh / bias grads and d latents as GEMMs over all frames
     hipLaunchKernelGGL(ae_lstm_bwd_kernel, dim3(B), dim3(AE_GATES), 0, st, gates, cs, P(L.whh), dseq, B, T, dG);
     VAD_LAUNCH_CHECK();
-    VAD_TRY(dense_wgrad(dG, NF, AE_GATES, lat, AE_LAT, G(L.wih), G(L.bih), scratch, scratch_floats, nullptr, st));
-    VAD_TRY(dense_wgrad(dG, NF, AE_GATES, hprev, AE_LAT, G(L.whh), G(L.bhh), scratch, scratch_floats, nullptr, st));
+    VAD_TRY(fork(st, &ws));
+    VAD_TRY(dense_wgrad(dG, NF, AE_GATES, lat, AE_LAT, G(L.wih), G(L.bih), scr2, scratch_floats, nullptr, ws));
+    VAD_TRY(dense_wgrad(dG, NF, AE_GATES, hprev, AE_LAT, G(L.whh), G(L.bhh), scr2, scratch_floats, nullptr, ws));
     VAD_TRY(dense_dgrad(dG, NF, AE_GATES, P(L.wih), AE_LAT, dlat, nullptr, 1.f, nullptr, st));
     hipLaunchKernelGGL(ae_latent_bwd_kernel, grid_for((int64_t)NF * AE_LAT), dim3(256), 0, st, dlat, d_ff, lat, z, B,
                        T, dz);
     VAD_LAUNCH_CHECK();
-    VAD_TRY(dense_wgrad(dz, NF, AE_LAT, ea[3], AE_FLAT, G(L.efc_w), G(L.efc_b), scratch, scratch_floats, nullptr, st));
+    VAD_TRY(fork(st, &ws));
+    VAD_TRY(dense_wgrad(dz, NF, AE_LAT, ea[3], AE_FLAT, G(L.efc_w), G(L.efc_b), scr2, scratch_floats, nullptr, ws));
     VAD_TRY(dense_dgrad(dz, NF, AE_LAT, P(L.efc_w), AE_FLAT, da3, nullptr, 1.f, nullptr, st));
     hipLaunchKernelGGL(ae_unflatten_kernel, grid_for((int64_t)NF * AE_FLAT), dim3(256), 0, st, da3, (int64_t)NF, 128,
                        16, bufA);
@@ -1061,19 +1147,25 @@ struct AePlanImpl {
     for (int l = 3; l >= 0; --l) {
       const int M = (int)ge[l].rows(), K = ge[l].K(), Co = ENC_CO[l];
       if (direct && l == 0) {  // Conv2d(1, 32): weight grad on the VALU, the bias grad from the BN backward
-        VAD_TRY(bn_bwd(bufA, ey[0], enc_bn(0), L.ebn_w[0], L.ebn_b[0], est[0], bufB, G(L.enc_b[0]), st));
-        VAD_TRY(conv4_c1_wgrad(bufB, xf, NF, ENC_IN[0] / 2, ENC_IN[0] / 2, G(L.enc_w[0]), scratch, scratch_floats,
-                               st));
+        float* dY = next_dy(st);
+        VAD_CHECK(dY != nullptr, "vad_ae_backward: stream wait failed");
+        VAD_TRY(bn_bwd(bufA, ey[0], enc_bn(0), L.ebn_w[0], L.ebn_b[0], est[0], dY, G(L.enc_b[0]), st, kb));
+        VAD_TRY(fork(st, &ws));
+        VAD_TRY(conv4_c1_wgrad(dY, xf, NF, ENC_IN[0] / 2, ENC_IN[0] / 2, G(L.enc_w[0]), scr2, scratch_floats, ws));
         continue;
       }
       if (direct) {  // (the conv bias grad = sum of dY, from the BN backward's apply pass)
         const int OH = ENC_IN[l] / 2;
         int ns = 0;
-        VAD_TRY(bn_bwd(bufA, ey[l], enc_bn(l), L.ebn_w[l], L.ebn_b[l], est[l], bufB, G(L.enc_b[l]), st));
-        VAD_TRY(conv4_wgrad(bufB, Co, ea[l - 1], ENC_CI[l], NF, OH, OH, scratch, &ns, scratch_floats,
-                            g_ae_wgrad_blocks, st));
-        VAD_TRY(conv4_wgrad_reduce(scratch, ns, Co, ENC_CI[l], G(L.enc_w[l]), st));
-        VAD_TRY(conv4_cls(bufB, NF, OH, OH, Co, ewc[l], nullptr, ENC_CI[l], bufA, st, scratch, scratch_floats));
+        float* dY = next_dy(st);
+        VAD_CHECK(dY != nullptr, "vad_ae_backward: stream wait failed");
+        VAD_TRY(bn_bwd(bufA, ey[l], enc_bn(l), L.ebn_w[l], L.ebn_b[l], est[l], dY, G(L.enc_b[l]), st, kb));
+        VAD_TRY(fork(st, &ws));
+        VAD_TRY(conv4_wgrad(dY, Co, ea[l - 1], ENC_CI[l], NF, OH, OH, scr2, &ns, scratch_floats, g_ae_wgrad_blocks,
+                            ws));
+        VAD_TRY(conv4_wgrad_reduce(scr2, ns, Co, ENC_CI[l], G(L.enc_w[l]), ws));
+        VAD_TRY(wg_mark(kb));
+        VAD_TRY(conv4_cls(dY, NF, OH, OH, Co, ewc[l], nullptr, ENC_CI[l], bufA, st, scratch, scratch_floats));
         continue;
       }
       VAD_TRY(bn_bwd(bufA, ey[l], enc_bn(l), L.ebn_w[l], L.ebn_b[l], est[l], bufB, nullptr, st));
@@ -1084,7 +1176,7 @@ struct AePlanImpl {
         VAD_TRY(col2im3d(bcols, ge[l], bufA, st));
       }
     }
-    return 0;
+    return join(st);
   }
 
   int optimizer(float lr, float b1, float b2, float eps, float wd, float max_norm, float grad_scale, hipStream_t st) {

@@ -1091,7 +1091,7 @@ struct ConvTuning {
 static ConvTuning g_tune;
 
 extern int g_bbox_im2col;  // bbox_plan.hip
-extern int g_ae_direct, g_ae_wgrad_blocks;  // ae_plan.hip
+extern int g_ae_direct, g_ae_wgrad_blocks, g_ae_wgrad_stream;  // ae_plan.hip
 extern int g_a2_direct;                     // a2_plan.hip
 int set_tuning(const char* key, int value) {
   const std::string k(key);
@@ -1120,6 +1120,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "bbox_im2col") g_bbox_im2col = value;
   else if (k == "ae_direct") g_ae_direct = value;
   else if (k == "ae_wgrad_blocks") g_ae_wgrad_blocks = value;
+  else if (k == "ae_wgrad_stream") g_ae_wgrad_stream = value;
   else if (k == "a2_direct") g_a2_direct = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
@@ -2459,13 +2460,22 @@ __global__ __launch_bounds__(256) void col_sum_part_kernel(const float* __restri
   }
   if (lane == 0) part[(int64_t)blockIdx.x * N + n] = red[n];
 }
+// 256 / N lanes per column each add a strided subset of the P block sums (loads independent, in flight together),
+// then the same fixed tree as the first pass
 __global__ __launch_bounds__(256) void col_sum_fin_kernel(const double* __restrict__ part, int P, int N,
                                                           float* __restrict__ db) {
-  for (int n = threadIdx.x; n < N; n += 256) {
-    double s = 0.0;
-    for (int p = 0; p < P; ++p) s += part[(int64_t)p * N + n];
-    db[n] = (float)s;
+  __shared__ double red[256];
+  const int n = threadIdx.x % N, lane = threadIdx.x / N, lanes = 256 / N;
+  double s = 0.0;
+#pragma unroll 8
+  for (int p = lane; p < P; p += lanes) s += part[(int64_t)p * N + n];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = lanes / 2; o > 0; o >>= 1) {
+    if (lane < o) red[threadIdx.x] += red[threadIdx.x + o * N];
+    __syncthreads();
   }
+  if (lane == 0) db[n] = (float)red[n];
 }
 
 int col_sum(const float* x, int64_t M, int N, float* db, double* scratch, hipStream_t st) {

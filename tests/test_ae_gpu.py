@@ -178,3 +178,30 @@ def test_ae_eval_and_standalone_memory_ops_match_oracle():
         s = torch.randn(5, 64)
         np.testing.assert_allclose(model.compute_anomaly_score(s.cuda()).cpu().numpy(),
                                    ae.memory_score(s, mem["memory"], ptr).numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_ae_wgrad_stream_is_bit_identical():
+    """The backward's weight gradients on the plan's side stream (knob ae_wgrad_stream, the default) against the same
+    kernels all on the caller's stream: grads after the first step and params after the second step bit-equal."""
+    from vad_amd import _native as nat
+    from vad_amd.ae import AeTrainer
+    case = dict(B=4, T=8, seed=47, lr=1e-4, labels=[[0] * 4], val_labels=[0], test_labels=[0], mem=(30, 30))
+    x = ae.synth_clips(47, 0, 0, 4, 8).cuda()
+    res = []
+    for side in (0, 1):
+        nat.check(nat.lib().vad_set_tuning(b"ae_wgrad_stream", side))
+        try:
+            model = make_ae_model(case).cuda()
+            tr = AeTrainer(model, lr=case["lr"])
+            l1 = tr.step(x).cpu().numpy()
+            g1 = model.engine().grads.cpu().clone()
+            tr.step(x)
+            torch.cuda.synchronize()
+            res.append((l1, g1, {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}))
+        finally:
+            nat.check(nat.lib().vad_set_tuning(b"ae_wgrad_stream", 1))
+    assert int(res[0][0][3]) == 2 and int(res[1][0][3]) == 2
+    assert np.array_equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+    for k in res[0][2]:
+        assert torch.equal(res[0][2][k], res[1][2][k]), k
