@@ -1351,6 +1351,7 @@ int conv3_fwd(const Conv3Layer& L, const float* src, const float* src_stats, con
   const int id = pick_fwd_tile(M, N);
   return with_tile(id, [&](auto cfg) -> int {
     using C = decltype(cfg);
+    VAD_CHECK(gather_fits((int64_t)g.imgs * g.SH * g.SW * g.C), "conv gather: source over 2 GB");
     typename ConvGatherKC<C::BM>::Params pa{src, g, taps, src_stats ? src_stats + 2 * L.Ci : nullptr,
                                             src_stats ? src_stats + 3 * L.Ci : nullptr};
     typename DenseKC<C::BN>::Params pb{wf, K, N, K};
@@ -1365,6 +1366,7 @@ static int dgrad_launch(const ConvGeom& g, const TapTable& taps, const float* dY
   const int M = g.imgs * g.GA * g.GB, K = taps.ntaps * g.C;
   return with_tile(pick_dgrad_tile(M, N), [&](auto cfg) -> int {
     using C = decltype(cfg);
+    VAD_CHECK(gather_fits((int64_t)g.imgs * g.SH * g.SW * g.C), "conv gather: source over 2 GB");
     typename ConvGatherKC<C::BM>::Params pa{dY, g, taps, nullptr, nullptr};
     typename DenseKC<C::BN>::Params pb{wd, K, N, K};
     return launch_gemm<C, ConvGatherKC, DenseKC, EpiConvDgrad>(pa, pb, pe, M, N, K, 1, nullptr, st);
@@ -1477,7 +1479,9 @@ int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const fl
     int splits = (int)std::max<int64_t>(
         1, std::min<int64_t>(cdiv(g_tune.wgrad_blocks, tiles), cdiv(K, (int64_t)g_tune.wgrad_min_ktiles * BK)));
     while ((int64_t)splits * M * N > partial_cap && splits > 1) splits /= 2;
+    VAD_CHECK(gather_fits((int64_t)K * L.Co), "dense gather: operand over 2 GB");
     typename DenseKM<C::BM>::Params pa{dY, L.Co, L.Co, K, -1};
+    VAD_CHECK(gather_fits((int64_t)L.NF * L.IH * L.IW * L.Ci), "conv patch: source over 2 GB");
     typename ConvPatchKM<C::BN>::Params pb{src, L.NF, L.OH, L.OW, L.stride, 1, L.IH, L.IW, L.Ci, 3, N,
                                            src_stats ? src_stats + 2 * L.Ci : nullptr,
                                            src_stats ? src_stats + 3 * L.Ci : nullptr};
@@ -1790,6 +1794,7 @@ int dense_dgrad(const float* dY, int M, int N, const float* W, int K, float* dX,
     return 0;
   }
   DenseKC<C::BM>::Params pa{dY, N, M, N};
+  VAD_CHECK(gather_fits((int64_t)N * K), "dense gather: operand over 2 GB");
   DenseKM<C::BN>::Params pb{W, K, K, N, -1};
   // few output tiles and a long reduction (e.g. cad1's Linear(64, 2048) input gradient: one tile, N = 2048): split-K
   // slabs in scratch when the caller gives one, summed in order with the gate by dense_splitk_reduce
@@ -1822,6 +1827,7 @@ int dense_wgrad(const float* dY, int M, int N, const float* X, int K, float* dW,
     return 0;
   }
   const int GN = K + 1;
+  VAD_CHECK(gather_fits((int64_t)M * N) && gather_fits((int64_t)M * K), "dense gather: operand over 2 GB");
   DenseKM<C::BM>::Params pa{dY, N, N, M, -1};
   DenseKM<C::BN>::Params pb{X, K, K, M, K};
   const int tiles = (int)(cdiv(N, C::BM) * cdiv(GN, C::BN));
@@ -1901,6 +1907,7 @@ int conv4_fwd(const float* src, int NF, int H, int W, int C, const float* wk, co
   const int splits = conv4_splits(M, N, K, scratch_floats);
   if (splits > 1) {
     int used = 1;
+    VAD_CHECK(gather_fits((int64_t)g.imgs * g.SH * g.SW * g.C), "conv gather: source over 2 GB");
     typename ConvGatherKC<64>::Params pa{src, g, taps, nullptr, nullptr};
     typename DenseKC<64>::Params pb{wk, K, N, K};
     const EpiPartial::Params pp{scratch, N};
@@ -1913,6 +1920,7 @@ int conv4_fwd(const float* src, int NF, int H, int W, int C, const float* wk, co
   }
   return with_tile(pick_fwd_tile(M, N), [&](auto cfg) -> int {
     using Cf = decltype(cfg);
+    VAD_CHECK(gather_fits((int64_t)g.imgs * g.SH * g.SW * g.C), "conv gather: source over 2 GB");
     typename ConvGatherKC<Cf::BM>::Params pa{src, g, taps, nullptr, nullptr};
     typename DenseKC<Cf::BN>::Params pb{wk, K, N, K};
     return launch_gemm<Cf, ConvGatherKC, DenseKC, EpiDense>(pa, pb, pe, M, N, K, 1, nullptr, st);
@@ -1992,6 +2000,7 @@ int conv4_cls(const float* src, int NF, int SH, int SW, int C, const float* wc, 
     const int K = 4 * C;
     return with_tile(pick_dgrad_tile(Mc, N), [&](auto cfg) -> int {
       using Cf = decltype(cfg);
+      VAD_CHECK(gather_fits((int64_t)g.imgs * g.SD * g.SH * g.SW * g.C), "conv gather: source over 2 GB");
       typename ConvGather3ClsKC<Cf::BM>::Params pa{src, g};
       typename DenseKCz<Cf::BN>::Params pb{wc, {}, {}, N};
       for (int c = 0; c < 4; ++c) {
@@ -2019,6 +2028,7 @@ int conv4_cls(const float* src, int NF, int SH, int SW, int C, const float* wc, 
     const int splits = conv4_splits(M, N, K, scratch_floats);
     if (splits > 1) {
       int used = 1;
+      VAD_CHECK(gather_fits((int64_t)g.imgs * g.SH * g.SW * g.C), "conv gather: source over 2 GB");
       typename ConvGatherKC<64>::Params pa{src, g, taps, nullptr, nullptr};
       typename DenseKC<64>::Params pb{wc + (int64_t)cls * N * 4 * C, K, N, K};
       const EpiPartial::Params pp{scratch, N};
@@ -2046,7 +2056,9 @@ int conv4_wgrad(const float* A, int R, const float* src, int C, int NF, int AH, 
     const int tiles = (int)(cdiv(M, Cf::BM) * cdiv(N, Cf::BN));
     int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, tiles), cdiv(K, 16 * BK)));
     while ((int64_t)splits * M * N > part_cap && splits > 1) splits /= 2;
+    VAD_CHECK(gather_fits((int64_t)K * R), "dense gather: operand over 2 GB");
     typename DenseKM<Cf::BM>::Params pa{A, R, R, K, -1};
+    VAD_CHECK(gather_fits((int64_t)NF * 2 * AH * 2 * AW * C), "conv patch: source over 2 GB");
     typename ConvPatchKM<Cf::BN>::Params pb{src, NF, AH, AW, 2, 1, 2 * AH, 2 * AW, C, 4, N, nullptr, nullptr};
     const EpiPartial::Params pe{part, N};
     return launch_gemm<Cf, DenseKM, ConvPatchKM, EpiPartial>(pa, pb, pe, M, N, K, splits, nullptr, st, nsplit);
@@ -2338,6 +2350,7 @@ int conv3s2_fwd(const float* src, int NF, int D, int H, int W, int C, const floa
   const DenseEpiArgs pe{out, N, bias, relu, 0, 0, 0, 1.f, 0, nullptr, 1.f};
   return with_tile(pick_fwd_tile(M, N), [&](auto cfg) -> int {
     using Cf = decltype(cfg);
+    VAD_CHECK(gather_fits((int64_t)g.imgs * g.SD * g.SH * g.SW * g.C), "conv gather: source over 2 GB");
     typename ConvGather3KC<Cf::BM>::Params pa{src, g, taps};
     typename DenseKC<Cf::BN>::Params pb{wk, K, N, K};
     return launch_gemm<Cf, ConvGather3KC, DenseKC, EpiDense>(pa, pb, pe, M, N, K, 1, nullptr, st);
@@ -2407,6 +2420,7 @@ int conv3s2_dgrad(const float* dy, int NF, int Co, const float* wc, int Ci, floa
   const int K = 8 * Co;
   return with_tile(pick_dgrad_tile(Mmax, Ci), [&](auto cfg) -> int {
     using Cf = decltype(cfg);
+    VAD_CHECK(gather_fits((int64_t)g.imgs * g.SD * g.SH * g.SW * g.C), "conv gather: source over 2 GB");
     typename ConvGather3ClsKC<Cf::BM>::Params pa{dy, g};
     typename DenseKCz<Cf::BN>::Params pb{wc, {}, {}, Ci};
     for (int c = 0; c < 8; ++c) {
@@ -2433,7 +2447,9 @@ int conv3s2_wgrad(const float* dy, int Co, const float* src, int Ci, int NF, int
     const int tiles = (int)(cdiv(M, Cf::BM) * cdiv(N, Cf::BN));
     int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(target_blocks, tiles), cdiv(K, 8 * BK)));
     while ((int64_t)splits * M * N > part_cap && splits > 1) splits /= 2;
+    VAD_CHECK(gather_fits((int64_t)K * Co), "dense gather: operand over 2 GB");
     typename DenseKM<Cf::BM>::Params pa{dy, Co, Co, K, -1};
+    VAD_CHECK(gather_fits((int64_t)NF * D * H * W * Ci), "conv patch: source over 2 GB");
     typename ConvPatch3KM<Cf::BN>::Params pb{src, NF, OD, OH, OW, 2, 2, 2, 1, D, H, W, Ci, N};
     const EpiPartial::Params pe{part, N};
     return launch_gemm<Cf, DenseKM, ConvPatch3KM, EpiPartial>(pa, pb, pe, M, N, K, splits, nullptr, st, &used);

@@ -12,6 +12,8 @@
 // Loaders: dense row-major KC/KM matrices, the NHWC conv patch gather (implicit GEMM with a tap table and
 // optional BN+ReLU applied on load), and the K-major patch gather used by the conv weight gradient.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace vad {
@@ -43,6 +45,30 @@ __device__ inline void frag_km(const float* __restrict__ lds, int row, int kbase
 #pragma unroll
   for (int s = 0; s < 4; ++s) v[s] = lds[(kbase + s) * R + row];
 }
+
+// ------------------------------------------------------------------ gather helpers
+// The conv gathers load through buffer resources with 32-bit offsets (the host checks every gathered tensor is below
+// 2^31 bytes, gather_fits): an element outside the source image takes an offset past the buffer's end and loads
+// zeros, so a K slice issues the same loads on every lane with no branches (the counted waits never drain the
+// prefetch) and no 64-bit address arithmetic.
+constexpr int GATHER_OOB = 0x7ffffff0;
+inline bool gather_fits(int64_t numel) { return numel >= 0 && numel * 4 < 0x7ffffff0ll; }
+__device__ inline __amdgpu_buffer_rsrc_t gather_rsrc(const float* p, int64_t numel) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(numel * 4 < 0x7ffffff0ll ? numel * 4 : 0x7ffffff0ll),
+                                           0x00020000);
+}
+__device__ inline f32x4 gather_load(__amdgpu_buffer_rsrc_t r, bool ok, int elem) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, ok ? elem * 4 : GATHER_OOB, 0, 0));
+}
+// loaders that keep a per-block table in LDS declare TAB (ints); gemm_kernel allocates it and passes it to init
+template <class L, class = void>
+struct LoaderTab {
+  static constexpr int n = 0;
+};
+template <class L>
+struct LoaderTab<L, std::void_t<decltype(L::TAB)>> {
+  static constexpr int n = L::TAB;
+};
 
 // ------------------------------------------------------------------ dense loaders
 // Row-major matrix X[rows][ld] read as operand rows=r, k=c (K-contiguous).
@@ -82,37 +108,41 @@ struct DenseKC {
   }
 };
 
-// Row-major matrix X[kdim][ld] read as operand k=row of X, r=column of X (K-major).
-// Optional virtual "ones" column at r == ones_col (used to fold bias grads into weight-grad GEMMs).
+// Row-major matrix X[kdim][ld] read as operand k=row of X, r=column of X (K-major), below 2^31 bytes (host:
+// gather_fits).  Loads go through a buffer resource with out-of-range elements at an offset past its end (zeros, no
+// branches): one 16-B load per float4 when ld and rows are multiples of 4, else four 4-B loads.  Optional virtual
+// "ones" column at r == ones_col (used to fold bias grads into weight-grad GEMMs), set at store time so the prefetch
+// is never waited for at load time.
 template <int R>
 struct DenseKM {
   static constexpr bool KC = false;
   static constexpr int NL = R / 32;
   struct Params { const float* p; int64_t ld; int rows; int kdim; int ones_col; };
-  const float* base; int64_t ld; int rows, kdim, ones_col; int r0, tid;
+  int ld, rows, kdim, ones_col, r0, tid, k0s;
+  bool vec;
+  __amdgpu_buffer_rsrc_t rs;
   f32x4 reg[NL];
   __device__ void init(const Params& P, int r0_, int tid_) {
-    base = P.p; ld = P.ld; rows = P.rows; kdim = P.kdim; ones_col = P.ones_col; r0 = r0_; tid = tid_;
+    ld = (int)P.ld; rows = P.rows; kdim = P.kdim; ones_col = P.ones_col; r0 = r0_; tid = tid_;
+    vec = ((ld | rows) & 3) == 0;
+    rs = gather_rsrc(P.p, (int64_t)kdim * P.ld);
   }
   __device__ void load(int k0) {
+    k0s = k0;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int q = tid + 256 * j;
       const int kr = q / (R / 4), rq = q % (R / 4);
       const int k = k0 + kr, r = r0 + rq * 4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (k < kdim) {
-        const float* src = base + (int64_t)k * ld + r;
-        if (r + 3 < rows && ((ld & 3) == 0)) v = *reinterpret_cast<const f32x4*>(src);
-        else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (r + e < rows) ? src[e] : 0.f;
-        }
+      if (vec) {
+        reg[j] = gather_load(rs, k < kdim && r < rows, k * ld + r);
+      } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (r + e == ones_col) v[e] = 1.f;
+          reg[j][e] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(rs, (k < kdim && r + e < rows) ? (k * ld + r + e) * 4
+                                                                                          : GATHER_OOB, 0, 0));
       }
-      reg[j] = v;
     }
   }
   __device__ void store(float* lds) const {
@@ -120,7 +150,12 @@ struct DenseKM {
     for (int j = 0; j < NL; ++j) {
       const int q = tid + 256 * j;
       const int kr = q / (R / 4), rq = q % (R / 4);
-      *reinterpret_cast<f32x4*>(lds + kr * R + rq * 4) = reg[j];
+      const int k = k0s + kr, r = r0 + rq * 4;
+      f32x4 v = reg[j];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (k < kdim && r + e == ones_col) v[e] = 1.f;
+      *reinterpret_cast<f32x4*>(lds + kr * R + rq * 4) = v;
     }
   }
 };
@@ -142,6 +177,7 @@ struct ConvGeom {
 };
 
 // A operand of forward / data-grad conv: row m = (img, a, b), k = tap*C + c; value = act(src[img][sh][sw][c]).
+// C % 32 == 0, so a K slice lies in one tap (uniform: its offsets are scalar).
 template <int R>
 struct ConvGatherKC {
   static constexpr bool KC = true;
@@ -151,33 +187,39 @@ struct ConvGatherKC {
     const float* scale; const float* shift;  // BN+ReLU applied on load when scale != nullptr
   };
   const Params* P;
-  int tid;
-  int64_t pix_base[NL];  // img*SH*SW
+  __amdgpu_buffer_rsrc_t rs;
+  int cq;
+  int rowoff[NL];        // element offset of the row's pixel (a*sa, b*sb) in its image
   int ya[NL], xb[NL];    // a*sa, b*sb  (ya < 0 marks an out-of-range row)
   f32x4 reg[NL];
-  __device__ void init(const Params& Pp, int r0, int tid_) {
-    P = &Pp; tid = tid_;
-    const int M = Pp.g.imgs * Pp.g.GA * Pp.g.GB;
+  __device__ void init(const Params& Pp, int r0, int tid) {
+    P = &Pp;
+    cq = (tid % 8) * 4;
+    const ConvGeom& g = Pp.g;
+    rs = gather_rsrc(Pp.src, (int64_t)g.imgs * g.SH * g.SW * g.C);
+    const int M = g.imgs * g.GA * g.GB;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int m = r0 + tid / 8 + 32 * j;
       if (m < M) {
-        const int img = m / (Pp.g.GA * Pp.g.GB);
-        const int rem = m - img * Pp.g.GA * Pp.g.GB;
-        const int a = rem / Pp.g.GB, b = rem - a * Pp.g.GB;
-        pix_base[j] = (int64_t)img * Pp.g.SH * Pp.g.SW;
-        ya[j] = a * Pp.g.sa;
-        xb[j] = b * Pp.g.sb;
+        const int img = m / (g.GA * g.GB);
+        const int rem = m - img * g.GA * g.GB;
+        const int a = rem / g.GB, b = rem - a * g.GB;
+        ya[j] = a * g.sa;
+        xb[j] = b * g.sb;
+        rowoff[j] = ((img * g.SH + ya[j]) * g.SW + xb[j]) * g.C;
       } else {
-        pix_base[j] = 0; ya[j] = -100000; xb[j] = 0;
+        rowoff[j] = 0; ya[j] = -100000; xb[j] = 0;
       }
     }
   }
   __device__ void load(int k0) {
-    const int C = P->g.C;
+    const ConvGeom& g = P->g;
+    const int C = g.C;
     const int tap = k0 / C;
-    const int c = k0 - tap * C + (tid % 8) * 4;
+    const int c = k0 - tap * C + cq;
     const int dh = P->taps.dh[tap], dw = P->taps.dw[tap];
+    const int toff = (dh * g.SW + dw) * C + c;
     f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
     const bool bn = P->scale != nullptr;
     if (bn) {
@@ -186,19 +228,17 @@ struct ConvGatherKC {
     }
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      const int y = ya[j] + dh, x = xb[j] + dw;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (y >= 0 && y < P->g.SH && x >= 0 && x < P->g.SW) {
-        v = *reinterpret_cast<const f32x4*>(P->src + ((pix_base[j] + (int64_t)y * P->g.SW + x) * C + c));
-        if (bn) {
+      const bool ok = (unsigned)(ya[j] + dh) < (unsigned)g.SH && (unsigned)(xb[j] + dw) < (unsigned)g.SW;
+      f32x4 v = gather_load(rs, ok, rowoff[j] + toff);
+      if (bn) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
-        }
+        for (int e = 0; e < 4; ++e) v[e] = ok ? fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f) : 0.f;
       }
       reg[j] = v;
     }
   }
   __device__ void store(float* lds) const {
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int row = tid / 8 + 32 * j, kq = tid % 8;
@@ -221,12 +261,14 @@ struct ConvPatchKM {
     const float* scale; const float* shift;
   };
   const Params* P;
-  int r0, tid, nextk;
-  int kh[NL], kw[NL], cc[NL];  // tap rows / columns and channel of the thread's r (kh < 0: r out of range)
+  __amdgpu_buffer_rsrc_t rs;
+  int nextk;
+  int kh[NL], kw[NL], cc[NL];  // tap rows / columns (minus pad) and channel of the thread's r (kh < -64: r out of range)
   int img[NL], oh[NL], ow[NL];  // the pixel of the thread's next load
   f32x4 reg[NL];
-  __device__ void init(const Params& Pp, int r0_, int tid_) {
-    P = &Pp; r0 = r0_; tid = tid_; nextk = -1;
+  __device__ void init(const Params& Pp, int r0, int tid) {
+    P = &Pp; nextk = -1;
+    rs = gather_rsrc(Pp.src, (int64_t)Pp.imgs * Pp.SH * Pp.SW * Pp.C);
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int q = tid + 256 * j;
@@ -234,15 +276,16 @@ struct ConvPatchKM {
       if (r < Pp.rows) {
         const int tap = r / Pp.C;
         cc[j] = r - tap * Pp.C;
-        kh[j] = tap / Pp.KW;
-        kw[j] = tap - kh[j] * Pp.KW;
+        kh[j] = tap / Pp.KW - Pp.pad;
+        kw[j] = tap - (tap / Pp.KW) * Pp.KW - Pp.pad;
       } else {
-        cc[j] = 0; kh[j] = -1; kw[j] = 0;
+        cc[j] = 0; kh[j] = -100000; kw[j] = 0;
       }
     }
   }
   __device__ void load(int k0) {
     const Params& q = *P;
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int kr = (tid + 256 * j) / (R / 4);
@@ -252,34 +295,31 @@ struct ConvPatchKM {
         const int rem = p - img[j] * q.OH * q.OW;
         oh[j] = rem / q.OW;
         ow[j] = rem - oh[j] * q.OW;
-      } else {  // the previous slice's pixel + BK
-        ow[j] += BK;
-        while (ow[j] >= q.OW) {
-          ow[j] -= q.OW;
-          if (++oh[j] == q.OH) {
-            oh[j] = 0;
-            ++img[j];
-          }
-        }
+      } else {  // the previous slice's pixel + BK, as a mixed-radix add of (BK / (OH OW), BK / OW % OH, BK % OW)
+        const int sw = BK % q.OW, sh = (BK / q.OW) % q.OH, si = BK / (q.OH * q.OW);
+        ow[j] += sw;
+        const bool cw = ow[j] >= q.OW;
+        ow[j] -= cw ? q.OW : 0;
+        oh[j] += sh + cw;
+        const bool ch = oh[j] >= q.OH;
+        oh[j] -= ch ? q.OH : 0;
+        img[j] += si + ch;
       }
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (img[j] < q.imgs && kh[j] >= 0) {
-        const int y = oh[j] * q.stride - q.pad + kh[j], x = ow[j] * q.stride - q.pad + kw[j];
-        if (y >= 0 && y < q.SH && x >= 0 && x < q.SW) {
-          v = *reinterpret_cast<const f32x4*>(q.src + (((int64_t)img[j] * q.SH + y) * q.SW + x) * q.C + cc[j]);
-          if (q.scale) {
-            const f32x4 sc = *reinterpret_cast<const f32x4*>(q.scale + cc[j]);
-            const f32x4 sh = *reinterpret_cast<const f32x4*>(q.shift + cc[j]);
+      const int y = oh[j] * q.stride + kh[j], x = ow[j] * q.stride + kw[j];
+      const bool ok = img[j] < q.imgs && (unsigned)y < (unsigned)q.SH && (unsigned)x < (unsigned)q.SW;
+      f32x4 v = gather_load(rs, ok, ((img[j] * q.SH + y) * q.SW + x) * q.C + cc[j]);
+      if (q.scale) {
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(q.scale + cc[j]);
+        const f32x4 sh = *reinterpret_cast<const f32x4*>(q.shift + cc[j]);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
-          }
-        }
+        for (int e = 0; e < 4; ++e) v[e] = ok ? fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f) : 0.f;
       }
       reg[j] = v;
     }
     nextk = k0 + BK;
   }
   __device__ void store(float* lds) const {
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int q = tid + 256 * j;
@@ -303,21 +343,56 @@ struct ConvGeom3 {
   int SD, SH, SW, C;
 };
 
+// Per-thread tap walk of the 3-D gathers: a thread's k = k0 + cq advances by BK per slice, its (tap, channel) is
+// decomposed at the first slice of a split and then stepped; the taps' (dd, dh, dw, element offset) sit in an LDS
+// table (one ds_read_b128 per slice instead of three dependent table loads), entries past the tap count out of range.
+constexpr int G3_TAB = 40;  // taps (27 + the tail of a K padded to BK with C >= 4)
+__device__ inline void gather3_fill(int* tab, const TapTable3& t, int SH, int SW, int C, int tid) {
+  if (tid < G3_TAB) {
+    int4 e = {-100000, 0, 0, 0};
+    if (tid < t.ntaps) e = {t.dd[tid], t.dh[tid], t.dw[tid], ((t.dd[tid] * SH + t.dh[tid]) * SW + t.dw[tid]) * C};
+    reinterpret_cast<int4*>(tab)[tid] = e;
+  }
+}
+struct Gather3Walk {
+  int tap, c, nextk;
+  __device__ void step(int k0, int cq, int C) {
+    if (k0 != nextk) {
+      const int k = k0 + cq;
+      tap = k / C;
+      c = k - tap * C;
+    } else {
+      c += BK;
+      while (c >= C) {
+        c -= C;
+        ++tap;
+      }
+    }
+    nextk = k0 + BK;
+  }
+};
+
 template <int R>
 struct ConvGather3KC {
   static constexpr bool KC = true;
   static constexpr int NL = R / 32;
+  static constexpr int TAB = 4 * G3_TAB;
   struct Params {
     const float* src; ConvGeom3 g; TapTable3 taps;
   };
   const Params* P;
-  int tid;
-  int64_t vox_base[NL];  // img * SD * SH * SW
+  const int* tab;
+  __amdgpu_buffer_rsrc_t rs;
+  int cq;
+  Gather3Walk w;
+  int rowoff[NL];             // element offset of the row's voxel (a * sd, b * sa, c * sb)
   int zd[NL], ya[NL], xb[NL];  // a * sd, b * sa, c * sb (zd < 0: an out-of-range row)
   f32x4 reg[NL];
-  __device__ void init(const Params& Pp, int r0, int tid_) {
-    P = &Pp; tid = tid_;
+  __device__ void init(const Params& Pp, int r0, int tid, int* tab_) {
+    P = &Pp; tab = tab_; cq = (tid % 8) * 4; w.nextk = -1;
     const ConvGeom3& g = Pp.g;
+    rs = gather_rsrc(Pp.src, (int64_t)g.imgs * g.SD * g.SH * g.SW * g.C);
+    gather3_fill(tab_, Pp.taps, g.SH, g.SW, g.C, tid);
     const int per = g.GD * g.GA * g.GB;
     const int M = g.imgs * per;
 #pragma unroll
@@ -327,31 +402,29 @@ struct ConvGather3KC {
         const int img = m / per, rem = m - img * per;
         const int a = rem / (g.GA * g.GB), r2 = rem - a * g.GA * g.GB;
         const int b = r2 / g.GB, c = r2 - b * g.GB;
-        vox_base[j] = (int64_t)img * g.SD * g.SH * g.SW;
         zd[j] = a * g.sd;
         ya[j] = b * g.sa;
         xb[j] = c * g.sb;
+        rowoff[j] = (((img * g.SD + zd[j]) * g.SH + ya[j]) * g.SW + xb[j]) * g.C;
       } else {
-        vox_base[j] = 0; zd[j] = -100000; ya[j] = 0; xb[j] = 0;
+        rowoff[j] = 0; zd[j] = -100000; ya[j] = 0; xb[j] = 0;
       }
     }
   }
   __device__ void load(int k0) {
     const ConvGeom3& g = P->g;
-    const int k = k0 + (tid % 8) * 4;
-    const int tap = k / g.C, c = k - tap * g.C;
-    const bool kin = tap < P->taps.ntaps;
-    const int dd = kin ? P->taps.dd[tap] : 0, dh = kin ? P->taps.dh[tap] : 0, dw = kin ? P->taps.dw[tap] : 0;
+    w.step(k0, cq, g.C);
+    const int4 t = reinterpret_cast<const int4*>(tab)[min(w.tap, G3_TAB - 1)];
+    const int toff = t.w + w.c;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      const int z = zd[j] + dd, y = ya[j] + dh, x = xb[j] + dw;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (kin && z >= 0 && z < g.SD && y >= 0 && y < g.SH && x >= 0 && x < g.SW)
-        v = *reinterpret_cast<const f32x4*>(P->src + ((vox_base[j] + ((int64_t)z * g.SH + y) * g.SW + x) * g.C + c));
-      reg[j] = v;
+      const bool ok = (unsigned)(zd[j] + t.x) < (unsigned)g.SD && (unsigned)(ya[j] + t.y) < (unsigned)g.SH &&
+                      (unsigned)(xb[j] + t.z) < (unsigned)g.SW;
+      reg[j] = gather_load(rs, ok, rowoff[j] + toff);
     }
   }
   __device__ void store(float* lds) const {
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int row = tid / 8 + 32 * j, kq = tid % 8;
@@ -371,20 +444,24 @@ template <int R>
 struct ConvGather3ClsKC {
   static constexpr bool KC = true;
   static constexpr int NL = R / 32;
+  static constexpr int TAB = 4 * G3_TAB;
   struct Params {
     const float* src; Conv3ClsGeom g;
   };
   const Params* P;
-  const TapTable3* taps;
-  int tid;
-  int64_t vox_base[NL];
+  const int* tab;
+  __amdgpu_buffer_rsrc_t rs;
+  int cq;
+  Gather3Walk w;
+  int rowoff[NL];
   int zd[NL], ya[NL], xb[NL];
   f32x4 reg[NL];
-  __device__ void init(const Params& Pp, int r0, int tid_) {
-    P = &Pp; tid = tid_;
+  __device__ void init(const Params& Pp, int r0, int tid, int* tab_) {
+    P = &Pp; tab = tab_; cq = (tid % 8) * 4; w.nextk = -1;
     const Conv3ClsGeom& g = Pp.g;
     const int z = blockIdx.z;
-    taps = &g.taps[z];
+    rs = gather_rsrc(Pp.src, (int64_t)g.imgs * g.SD * g.SH * g.SW * g.C);
+    gather3_fill(tab_, g.taps[z], g.SH, g.SW, g.C, tid);
     const int GA = g.GA[z], GB = g.GB[z], per = g.GD[z] * GA * GB, M = g.imgs * per;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
@@ -393,29 +470,27 @@ struct ConvGather3ClsKC {
         const int img = m / per, rem = m - img * per;
         const int a = rem / (GA * GB), r2 = rem - a * GA * GB;
         const int b = r2 / GB, c = r2 - b * GB;
-        vox_base[j] = (int64_t)img * g.SD * g.SH * g.SW;
         zd[j] = a; ya[j] = b; xb[j] = c;
+        rowoff[j] = (((img * g.SD + a) * g.SH + b) * g.SW + c) * g.C;
       } else {
-        vox_base[j] = 0; zd[j] = -100000; ya[j] = 0; xb[j] = 0;
+        rowoff[j] = 0; zd[j] = -100000; ya[j] = 0; xb[j] = 0;
       }
     }
   }
   __device__ void load(int k0) {
     const Conv3ClsGeom& g = P->g;
-    const int k = k0 + (tid % 8) * 4;
-    const int tap = k / g.C, c = k - tap * g.C;
-    const bool kin = tap < taps->ntaps;
-    const int dd = kin ? taps->dd[tap] : 0, dh = kin ? taps->dh[tap] : 0, dw = kin ? taps->dw[tap] : 0;
+    w.step(k0, cq, g.C);
+    const int4 t = reinterpret_cast<const int4*>(tab)[min(w.tap, G3_TAB - 1)];
+    const int toff = t.w + w.c;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      const int z = zd[j] + dd, y = ya[j] + dh, x = xb[j] + dw;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (kin && z >= 0 && z < g.SD && y >= 0 && y < g.SH && x >= 0 && x < g.SW)
-        v = *reinterpret_cast<const f32x4*>(P->src + ((vox_base[j] + ((int64_t)z * g.SH + y) * g.SW + x) * g.C + c));
-      reg[j] = v;
+      const bool ok = (unsigned)(zd[j] + t.x) < (unsigned)g.SD && (unsigned)(ya[j] + t.y) < (unsigned)g.SH &&
+                      (unsigned)(xb[j] + t.z) < (unsigned)g.SW;
+      reg[j] = gather_load(rs, ok, rowoff[j] + toff);
     }
   }
   __device__ void store(float* lds) const {
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int row = tid / 8 + 32 * j, kq = tid % 8;
@@ -467,12 +542,14 @@ struct ConvPatch3KM {
     const float* src; int imgs, OD, OH, OW, sd, sh, sw, pad, SD, SH, SW, C, rows;  // rows = 27 * C
   };
   const Params* P;
+  __amdgpu_buffer_rsrc_t rs;
   int r0, tid, nextk;
   int kd[NL], kh[NL], kw[NL], cc[NL];  // kd < 0: r out of range
   int img[NL], od[NL], oh[NL], ow[NL];
   f32x4 reg[NL];
   __device__ void init(const Params& Pp, int r0_, int tid_) {
     P = &Pp; r0 = r0_; tid = tid_; nextk = -1;
+    rs = gather_rsrc(Pp.src, (int64_t)Pp.imgs * Pp.SD * Pp.SH * Pp.SW * Pp.C);
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int r = r0 + ((tid + 256 * j) % (R / 4)) * 4;
@@ -500,27 +577,24 @@ struct ConvPatch3KM {
         const int r2 = rem - od[j] * q.OH * q.OW;
         oh[j] = r2 / q.OW;
         ow[j] = r2 - oh[j] * q.OW;
-      } else {
-        ow[j] += BK;
-        while (ow[j] >= q.OW) {
-          ow[j] -= q.OW;
-          if (++oh[j] == q.OH) {
-            oh[j] = 0;
-            if (++od[j] == q.OD) {
-              od[j] = 0;
-              ++img[j];
-            }
-          }
-        }
+      } else {  // + BK as a mixed-radix add over (img, od, oh, ow)
+        const int sw = BK % q.OW, sh = (BK / q.OW) % q.OH, sd = (BK / (q.OW * q.OH)) % q.OD,
+                  si = BK / (q.OD * q.OH * q.OW);
+        ow[j] += sw;
+        const bool cw = ow[j] >= q.OW;
+        ow[j] -= cw ? q.OW : 0;
+        oh[j] += sh + cw;
+        const bool ch = oh[j] >= q.OH;
+        oh[j] -= ch ? q.OH : 0;
+        od[j] += sd + ch;
+        const bool cd = od[j] >= q.OD;
+        od[j] -= cd ? q.OD : 0;
+        img[j] += si + cd;
       }
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (img[j] < q.imgs && kd[j] >= 0) {
-        const int z = od[j] * q.sd - q.pad + kd[j], y = oh[j] * q.sh - q.pad + kh[j], x = ow[j] * q.sw - q.pad + kw[j];
-        if (z >= 0 && z < q.SD && y >= 0 && y < q.SH && x >= 0 && x < q.SW)
-          v = *reinterpret_cast<const f32x4*>(q.src + ((((int64_t)img[j] * q.SD + z) * q.SH + y) * q.SW + x) * q.C +
-                                              cc[j]);
-      }
-      reg[j] = v;
+      const int z = od[j] * q.sd - q.pad + kd[j], y = oh[j] * q.sh - q.pad + kh[j], x = ow[j] * q.sw - q.pad + kw[j];
+      const bool ok = img[j] < q.imgs && kd[j] >= 0 && (unsigned)z < (unsigned)q.SD && (unsigned)y < (unsigned)q.SH &&
+                      (unsigned)x < (unsigned)q.SW;
+      reg[j] = gather_load(rs, ok, (((img[j] * q.SD + z) * q.SH + y) * q.SW + x) * q.C + cc[j]);
     }
     nextk = k0 + BK;
   }
@@ -545,6 +619,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const typename LA::Params pa,
   constexpr int STAGE = A_FL + B_FL;
   constexpr int TOTAL = 2 * STAGE > Epi::SCRATCH ? 2 * STAGE : Epi::SCRATCH;
   __shared__ __attribute__((aligned(16))) float lds[TOTAL];
+  constexpr int TA = LoaderTab<LA>::n, TB = LoaderTab<LB>::n;
+  __shared__ __attribute__((aligned(16))) int tabs[TA + TB + 4];
   if (skip_if_zero != nullptr && *skip_if_zero == 0) return;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -554,8 +630,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(const typename LA::Params pa,
   const int kbeg = k_per_split > 0 ? (int)blockIdx.z * k_per_split : 0;
   const int kend = k_per_split > 0 ? min(K, kbeg + k_per_split) : K;
 
-  LA la; la.init(pa, m0, tid);
-  LB lb; lb.init(pb, n0, tid);
+  LA la;
+  LB lb;
+  if constexpr (TA > 0) la.init(pa, m0, tid, tabs);
+  else la.init(pa, m0, tid);
+  if constexpr (TB > 0) lb.init(pb, n0, tid, tabs + TA);
+  else lb.init(pb, n0, tid);
+  if constexpr (TA + TB > 0) __syncthreads();
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
