@@ -1092,6 +1092,7 @@ static ConvTuning g_tune;
 
 extern int g_bbox_im2col;  // bbox_plan.hip
 extern int g_ae_direct, g_ae_wgrad_blocks, g_ae_wgrad_stream;  // ae_plan.hip
+extern int g_conv4_cls_batch_min, g_conv4_split_tiles;
 extern int g_a2_direct;                     // a2_plan.hip
 int set_tuning(const char* key, int value) {
   const std::string k(key);
@@ -1121,6 +1122,8 @@ int set_tuning(const char* key, int value) {
   else if (k == "ae_direct") g_ae_direct = value;
   else if (k == "ae_wgrad_blocks") g_ae_wgrad_blocks = value;
   else if (k == "ae_wgrad_stream") g_ae_wgrad_stream = value;
+  else if (k == "conv4_cls_batch_min") g_conv4_cls_batch_min = value;
+  else if (k == "conv4_split_tiles") g_conv4_split_tiles = value;
   else if (k == "a2_direct") g_a2_direct = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
@@ -1883,9 +1886,11 @@ int conv4_prep(const float* w, int D0, int D1, float* wk, float* wc, hipStream_t
 
 // split-K when the tile grid leaves most CUs idle (the decoder's 4x4 / 8x8 frames): slabs [S][M][N] in scratch, summed
 // in order (+ bias) by dense_splitk_reduce / conv4_cls_reduce
+// knob "conv4_split_tiles": implicit-GEMM convs with fewer 64 x 64 output tiles than this split K (slabs + a reduce)
+int g_conv4_split_tiles = 512;
 static int conv4_splits(int M, int N, int K, int64_t scratch_floats) {
   const int64_t tiles = cdiv(M, 64) * cdiv(N, 64);
-  if (tiles >= 512 || scratch_floats <= 0) return 1;
+  if (tiles >= g_conv4_split_tiles || scratch_floats <= 0) return 1;
   int s = (int)std::min<int64_t>(cdiv(1024, tiles), K / (2 * BK));
   while (s > 1 && (int64_t)s * M * N > scratch_floats) s /= 2;
   return std::max(1, s);
@@ -1973,11 +1978,14 @@ __global__ __launch_bounds__(256) void conv4_cls_reduce_kernel(const float* __re
   }
 }
 
+// knob "conv4_cls_batch_min": the four parity classes go to one batched launch (whole K per block, bias in the
+// epilogue) from this many 64 x 64 class tiles up; below it, per-class split-K launches with a reduce each
+int g_conv4_cls_batch_min = 0;  // (sweep at cad1: 512 1.845-1.850, 128 1.813-1.817, 0 1.785-1.795 ms)
 int conv4_cls(const float* src, int NF, int SH, int SW, int C, const float* wc, const float* bias, int N, float* out,
               hipStream_t st, float* scratch, int64_t scratch_floats) {
   VAD_CHECK(C % 32 == 0 && N >= 1, "conv4_cls: C % 32 == 0");
   const int Mc = NF * SH * SW;
-  if (cdiv(Mc, 64) * cdiv(N, 64) * 4 >= 512 || scratch_floats <= 0) {
+  if (cdiv(Mc, 64) * cdiv(N, 64) * 4 >= g_conv4_cls_batch_min || scratch_floats <= 0) {
     // the four classes in one launch (blockIdx.z = class, the 3-D class-batched GEMM with a depth of 1)
     Conv3ClsGeom g{};
     g.imgs = NF; g.SD = 1; g.SH = SH; g.SW = SW; g.C = C;
