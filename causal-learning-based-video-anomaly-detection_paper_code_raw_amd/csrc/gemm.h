@@ -71,35 +71,55 @@ struct LoaderTab<L, std::void_t<decltype(L::TAB)>> {
 };
 
 // ------------------------------------------------------------------ dense loaders
-// Row-major matrix X[rows][ld] read as operand rows=r, k=c (K-contiguous).
+// Row-major matrix X[rows][ld] read as operand rows=r, k=c (K-contiguous).  Below 2^31 bytes the loads go through a
+// buffer resource (out-of-range elements at an offset past its end: zeros, no branches), one 16-B load per float4 when
+// ld and kdim are multiples of 4, else four 4-B loads; larger matrices take plain guarded loads.
 template <int R>
 struct DenseKC {
   static constexpr bool KC = true;
   static constexpr int NL = R / 32;  // float4 per thread per tile
   struct Params { const float* p; int64_t ld; int rows; int kdim; };
-  const float* base; int64_t ld; int rows, kdim; int r0, tid;
+  const float* base; int64_t ld; int rows, kdim; int r0;
+  bool buf, vec;
+  __amdgpu_buffer_rsrc_t rs;
   f32x4 reg[NL];
   __device__ void init(const Params& P, int r0_, int tid_) {
-    base = P.p; ld = P.ld; rows = P.rows; kdim = P.kdim; r0 = r0_; tid = tid_;
+    base = P.p; ld = P.ld; rows = P.rows; kdim = P.kdim; r0 = r0_;
+    const int64_t numel = (int64_t)rows * ld;
+    buf = numel * 4 < 0x7ffffff0ll;
+    vec = ((ld | kdim) & 3) == 0;
+    rs = gather_rsrc(base, numel);
   }
   __device__ void load(int k0) {
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int row = tid / 8 + 32 * j, kq = tid % 8;
       const int r = r0 + row, k = k0 + kq * 4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (r < rows && k < kdim) {
-        const float* src = base + (int64_t)r * ld + k;
-        if (k + 3 < kdim && ((ld & 3) == 0)) v = *reinterpret_cast<const f32x4*>(src);
-        else {
+      if (buf && vec) {
+        reg[j] = gather_load(rs, r < rows && k < kdim, r * (int)ld + k);
+      } else if (buf) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (k + e < kdim) ? src[e] : 0.f;
+        for (int e = 0; e < 4; ++e)
+          reg[j][e] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(rs, (r < rows && k + e < kdim) ? (r * (int)ld + k + e) * 4
+                                                                                        : GATHER_OOB, 0, 0));
+      } else {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (r < rows && k < kdim) {
+          const float* src = base + (int64_t)r * ld + k;
+          if (k + 3 < kdim && ((ld & 3) == 0)) v = *reinterpret_cast<const f32x4*>(src);
+          else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = (k + e < kdim) ? src[e] : 0.f;
+          }
         }
+        reg[j] = v;
       }
-      reg[j] = v;
     }
   }
   __device__ void store(float* lds) const {
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int row = tid / 8 + 32 * j, kq = tid % 8;
@@ -499,30 +519,31 @@ struct ConvGather3ClsKC {
   }
 };
 
-// Row-major matrices X_z[rows][kdim_z] at p + off[z] (blockIdx.z = batch), read K-contiguous (as DenseKC)
+// Row-major matrices X_z[rows][kdim_z] at p + off[z] (blockIdx.z = batch), read K-contiguous (as DenseKC; kdim_z % 4
+// == 0, each below 2^31 bytes: buffer loads)
 template <int R>
 struct DenseKCz {
   static constexpr bool KC = true;
   static constexpr int NL = R / 32;
   struct Params { const float* p; int64_t off[8]; int kdim[8]; int rows; };
-  const float* base; int kdim, rows, r0, tid;
+  int kdim, rows, r0;
+  __amdgpu_buffer_rsrc_t rs;
   f32x4 reg[NL];
   __device__ void init(const Params& P, int r0_, int tid_) {
-    base = P.p + P.off[blockIdx.z]; kdim = P.kdim[blockIdx.z]; rows = P.rows; r0 = r0_; tid = tid_;
+    kdim = P.kdim[blockIdx.z]; rows = P.rows; r0 = r0_;
+    rs = gather_rsrc(P.p + P.off[blockIdx.z], (int64_t)rows * kdim);
   }
   __device__ void load(int k0) {
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int row = tid / 8 + 32 * j, kq = tid % 8;
       const int r = r0 + row, k = k0 + kq * 4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (r < rows && k < kdim) {  // (kdim % 4 == 0)
-        v = *reinterpret_cast<const f32x4*>(base + (int64_t)r * kdim + k);
-      }
-      reg[j] = v;
+      reg[j] = gather_load(rs, r < rows && k < kdim, r * kdim + k);
     }
   }
   __device__ void store(float* lds) const {
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int row = tid / 8 + 32 * j, kq = tid % 8;
