@@ -363,9 +363,10 @@ class ImprovedMiniCausalVAD:
     def train_epoch_improved(self, dataloader):
         total_loss = 0.0
         comps_sum = {k: 0.0 for k in LOSS_KEYS}
-        for videos, labels in dataloader:
+        for batch_idx, (videos, labels) in enumerate(dataloader):
             loss, comps, stepped = self.train_step(videos, labels)
             if not stepped:
+                print(f"NaN loss detected at batch {batch_idx}, skipping...")
                 continue
             total_loss += loss
             for k, v in comps.items():

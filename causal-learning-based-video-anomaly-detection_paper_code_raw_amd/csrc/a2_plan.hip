@@ -939,6 +939,29 @@ int vad_a2_bind(vad_a2_plan* plan, void* workspace, float* params, float* grads,
   return 0;
 }
 
+}  // extern "C"
+
+namespace vad {
+// the plan's small outputs handed to the caller's buffers in one launch (instead of one copy-engine blit each)
+struct A2Copies {
+  const float* src[4];
+  float* dst[4];
+  int n[4];
+};
+__global__ __launch_bounds__(256) void a2_copies_kernel(A2Copies c) {
+  const int k = blockIdx.x;
+  for (int i = threadIdx.x; i < c.n[k]; i += 256) c.dst[k][i] = c.src[k][i];
+}
+static int a2_copies(const A2Copies& c, int nseg, hipStream_t st) {
+  if (nseg == 0) return 0;
+  hipLaunchKernelGGL(a2_copies_kernel, dim3((unsigned)nseg), dim3(256), 0, st, c);
+  VAD_LAUNCH_CHECK();
+  return 0;
+}
+}  // namespace vad
+
+extern "C" {
+
 int vad_a2_forward(vad_a2_plan* plan, const float* x, int training, uint64_t seed, uint64_t step, int64_t clip0,
                    int with_loss, float* scores, float* adj, float* features, float* losses, void* stream) {
   VAD_CHECK(plan && x, "vad_a2_forward: null argument");
@@ -952,12 +975,21 @@ int vad_a2_forward(vad_a2_plan* plan, const float* x, int training, uint64_t see
   c.with_loss = with_loss;
   VAD_TRY(c.forward(x, st));
   const int B = c.B;
-  if (scores) VAD_HIP(hipMemcpyAsync(scores, c.s, sizeof(float) * B, hipMemcpyDeviceToDevice, st));
-  if (adj) VAD_HIP(hipMemcpyAsync(adj, c.adj, sizeof(float) * B * 256, hipMemcpyDeviceToDevice, st));
-  if (features) VAD_HIP(hipMemcpyAsync(features, c.f, sizeof(float) * B * 16, hipMemcpyDeviceToDevice, st));
+  A2Copies cp{};
+  int k = 0;
+  auto add = [&](float* d, const float* s, int n) {
+    if (d) {
+      cp.dst[k] = d;
+      cp.src[k] = s;
+      cp.n[k++] = n;
+    }
+  };
+  add(scores, c.s, B);
+  add(adj, c.adj, B * 256);
+  add(features, c.f, B * 16);
   plan->user_losses = losses;
-  if (losses && with_loss) VAD_HIP(hipMemcpyAsync(losses, c.losses, sizeof(float) * 10, hipMemcpyDeviceToDevice, st));
-  return 0;
+  add(with_loss ? losses : nullptr, c.losses, 10);
+  return a2_copies(cp, k, st);
 }
 
 int vad_a2_loss(vad_a2_plan* plan, uint64_t seed, uint64_t step, int64_t clip0, float* losses, void* stream) {
@@ -977,9 +1009,15 @@ int vad_a2_loss_grads(vad_a2_plan* plan, float* d_scores, float* d_adj, void* st
   VAD_CHECK(plan != nullptr, "vad_a2_loss_grads: null plan");
   A2PlanImpl& c = plan->impl;
   hipStream_t st = (hipStream_t)stream;
-  if (d_scores) VAD_HIP(hipMemcpyAsync(d_scores, c.d_s, sizeof(float) * c.B, hipMemcpyDeviceToDevice, st));
-  if (d_adj) VAD_HIP(hipMemcpyAsync(d_adj, c.d_adj, sizeof(float) * c.B * 256, hipMemcpyDeviceToDevice, st));
-  return 0;
+  A2Copies cp{};
+  int k = 0;
+  if (d_scores) {
+    cp.dst[k] = d_scores; cp.src[k] = c.d_s; cp.n[k++] = c.B;
+  }
+  if (d_adj) {
+    cp.dst[k] = d_adj; cp.src[k] = c.d_adj; cp.n[k++] = c.B * 256;
+  }
+  return a2_copies(cp, k, st);
 }
 
 int vad_a2_backward(vad_a2_plan* plan, const float* d_scores, const float* d_adj, const float* d_features,
