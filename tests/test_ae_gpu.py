@@ -205,3 +205,27 @@ def test_ae_wgrad_stream_is_bit_identical():
     assert torch.equal(res[0][1], res[1][1])
     for k in res[0][2]:
         assert torch.equal(res[0][2][k], res[1][2][k]), k
+
+
+def test_ae_class_launch_paths_agree():
+    """The transposed convs' parity classes in one batched launch (default, knob conv4_cls_batch_min = 0) against the
+    per-class split-K launches (conv4_cls_batch_min = 512 restores them for the small layers): the train step's
+    losses and grads agree to float rounding (different summation order of the split-K slabs)."""
+    from vad_amd import _native as nat
+    from vad_amd.ae import AeTrainer
+    case = dict(B=4, T=8, seed=48, lr=1e-4, labels=[[0] * 4], val_labels=[0], test_labels=[0], mem=(30, 30))
+    x = ae.synth_clips(48, 0, 0, 4, 8).cuda()
+    res = []
+    for v in (0, 512):
+        nat.check(nat.lib().vad_set_tuning(b"conv4_cls_batch_min", v))
+        try:
+            model = make_ae_model(case).cuda()
+            tr = AeTrainer(model, lr=case["lr"])
+            l1 = tr.step(x).cpu().numpy()
+            res.append((l1, model.engine().grads.cpu().clone()))
+        finally:
+            nat.check(nat.lib().vad_set_tuning(b"conv4_cls_batch_min", 0))
+    assert int(res[0][0][3]) == 2 and int(res[1][0][3]) == 2
+    np.testing.assert_allclose(res[0][0][:2], res[1][0][:2], rtol=1e-5)
+    g0, g1 = res[0][1].double(), res[1][1].double()
+    assert float((g0 - g1).norm()) <= 1e-5 * float(g1.norm()) + 1e-12
