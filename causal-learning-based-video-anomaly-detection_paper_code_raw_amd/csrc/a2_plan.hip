@@ -483,16 +483,19 @@ __global__ __launch_bounds__(256) void a2_conv1_fwd_kernel(const float* __restri
   }
 }
 
+// thread = 4 output channels (co quad q = tid & 3) x 2 (ci, tap) pairs (pair lane pl = tid >> 2: pairs pl and pl + 64,
+// pair 81 = the bias); per voxel one 16-B read of its dY quad and two halo reads feed 8 FMAs, branch-free (the bias
+// pair and the unused pair slot read offset 0 and select / discard)
 __global__ __launch_bounds__(256) void a2_conv1_wgrad_kernel(const float* __restrict__ dA, const float* __restrict__ x,
                                                              int B, int T, int H, int W, float* __restrict__ slab) {
   __shared__ float xs[3 * A2_HALO];
-  __shared__ float as[256][17];
+  __shared__ __attribute__((aligned(16))) float as[256][16];
   const A2Tiles g(B, T, H, W);
-  const int tid = threadIdx.x, co = tid & 15, grp = tid >> 4;
-  int off[6];  // per owned pair: its halo offset at voxel (0, 0, 0), -1 = the bias pair, -2 = none
+  const int tid = threadIdx.x, q = tid & 3, pl = tid >> 2;
+  int off[2];  // per owned pair: its halo offset at voxel (0, 0, 0), -1 = the bias pair, -2 = none
 #pragma unroll
-  for (int m = 0; m < 6; ++m) {
-    const int j = grp + 16 * m;
+  for (int m = 0; m < 2; ++m) {
+    const int j = pl + 64 * m;
     if (j > A2C1_TAPS) off[m] = -2;
     else if (j == A2C1_TAPS) off[m] = -1;
     else {
@@ -500,7 +503,7 @@ __global__ __launch_bounds__(256) void a2_conv1_wgrad_kernel(const float* __rest
       off[m] = ((ci * A2H_D + t / 9) * A2H_H + (t / 3) % 3) * A2H_W + t % 3;
     }
   }
-  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   for (int64_t tile = blockIdx.x; tile < g.n; tile += gridDim.x) {
     const int bw = (int)(tile % g.tw);
     int64_t r = tile / g.tw;
@@ -517,29 +520,32 @@ __global__ __launch_bounds__(256) void a2_conv1_wgrad_kernel(const float* __rest
       const bool ok = d < T && oh < g.OH && ow < g.OW;
       const float* row = dA + (((b * T + d) * g.OH + oh) * (int64_t)g.OW + ow) * 16;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 v4 = ok ? *reinterpret_cast<const f32x4*>(row + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) as[tid][4 * q + e] = v4[e];
-      }
+      for (int k = 0; k < 4; ++k)
+        *reinterpret_cast<f32x4*>(&as[tid][4 * k]) =
+            ok ? *reinterpret_cast<const f32x4*>(row + 4 * k) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     __syncthreads();
     for (int v = 0; v < 256; ++v) {
       const int vd = v / (A2T_H * A2T_W), vh = (v / A2T_W) % A2T_H, vw = v % A2T_W;
       const int base = (vd * A2H_H + 2 * vh) * A2H_W + 2 * vw;
-      const float a = as[v][co];
-      // branch-free: every pair's LDS read issues unconditionally (the bias pair and the unused ones read offset 0 and
-      // select / discard), so the six reads of a voxel share one wait
-      float xv[6];
+      const f32x4 a = *reinterpret_cast<const f32x4*>(&as[v][4 * q]);
+      float xv[2];
 #pragma unroll
-      for (int m = 0; m < 6; ++m) xv[m] = xs[max(off[m], 0) + base];
+      for (int m = 0; m < 2; ++m) xv[m] = xs[max(off[m], 0) + base];
 #pragma unroll
-      for (int m = 0; m < 6; ++m) acc[m] = fmaf(a, off[m] == -1 ? 1.f : xv[m], acc[m]);
+      for (int m = 0; m < 2; ++m) {
+        const float xm = off[m] == -1 ? 1.f : xv[m];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[m][e] = fmaf(a[e], xm, acc[m][e]);
+      }
     }
   }
 #pragma unroll
-  for (int m = 0; m < 6; ++m)
-    if (off[m] != -2) slab[((int64_t)blockIdx.x * 16 + co) * (A2C1_TAPS + 1) + grp + 16 * m] = acc[m];
+  for (int m = 0; m < 2; ++m)
+    if (off[m] != -2)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        slab[((int64_t)blockIdx.x * 16 + 4 * q + e) * (A2C1_TAPS + 1) + pl + 64 * m] = acc[m][e];
 }
 
 // dW[co][ci*27 + tap] / db[co] = sum over the S slabs: 16 consecutive entries x 16 slab lanes per block (lane l adds
