@@ -2230,27 +2230,27 @@ __global__ __launch_bounds__(256) void conv4_c1_tfwd_kernel(const float* __restr
 // tile's pixels (three LDS reads, two FMAs per pixel)
 constexpr int C1_TILE = 256;
 
+// thread = 4 output channels (quad q) x 2 taps (pair p) over one wave's share of the tile's pixel rows (wave w takes
+// rows w, w + 4, ...): per pixel one 16-B read of the dY quad and two halo reads feed 8 FMAs; the four waves' sums are
+// combined in a fixed order at the end
 __global__ __launch_bounds__(256) void conv4_c1_wgrad_kernel(const float* __restrict__ A, const float* __restrict__ src,
                                                              int NF, int AH, int AW, float* __restrict__ slab) {
-  __shared__ float as[C1_TILE][33];
+  __shared__ __attribute__((aligned(16))) float as[C1_TILE][32];
   __shared__ float xs[(2 * C1_TILE / 8 + 2) * (2 * 64 + 2)];  // (AW >= 8, AW <= 64)
+  __shared__ float red[4][512];
   const int H = 2 * AH, W = 2 * AW, TR = C1_TILE / AW, XW = 2 * AW + 2, XR = 2 * TR + 2;
   const int64_t ntiles = (int64_t)NF * AH / TR;
-  const int t = threadIdx.x, r = t & 31, tp = (t >> 5) * 2;
-  const int k0 = tp, k1 = tp + 1;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, q = lane & 7, p = lane >> 3;
+  const int k0 = 2 * p, k1 = 2 * p + 1;
   const int o0 = (k0 / 4) * XW + k0 % 4, o1 = (k1 / 4) * XW + k1 % 4;  // tap offsets in the halo
-  float acc0 = 0.f, acc1 = 0.f;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t img = tile / (AH / TR);
     const int y0 = (int)(tile % (AH / TR)) * TR;  // first A row of the tile
     __syncthreads();
     const float* arow = A + ((img * AH + y0) * (int64_t)AW) * 32;
-    for (int i = t; i < C1_TILE * 8; i += 256) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(arow + (int64_t)i * 4);
-      const int pp = i >> 3, c4 = (i & 7) * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) as[pp][c4 + e] = v[e];
-    }
+    for (int i = t; i < C1_TILE * 8; i += 256)
+      *reinterpret_cast<f32x4*>(&as[i >> 3][(i & 7) * 4]) = *reinterpret_cast<const f32x4*>(arow + (int64_t)i * 4);
     const float* simg = src + img * (int64_t)H * W;
     for (int i = t; i < XR * XW; i += 256) {
       const int hy = i / XW, hx = i - hy * XW;
@@ -2258,19 +2258,29 @@ __global__ __launch_bounds__(256) void conv4_c1_wgrad_kernel(const float* __rest
       xs[i] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? simg[(int64_t)iy * W + ix] : 0.f;
     }
     __syncthreads();
-    for (int vy = 0; vy < TR; ++vy) {  // (pixel v = vy * AW + vx, walked without divisions)
-      const float* arow = &as[vy * AW][r];
+    for (int vy = wv; vy < TR; vy += 4) {  // (pixel v = vy * AW + vx, walked without divisions)
       const float* xrow = xs + 2 * vy * XW;
 #pragma unroll 4
       for (int vx = 0; vx < AW; ++vx) {
-        const float a = arow[vx * 33];
-        acc0 = fmaf(a, xrow[2 * vx + o0], acc0);
-        acc1 = fmaf(a, xrow[2 * vx + o1], acc1);
+        const f32x4 a = *reinterpret_cast<const f32x4*>(&as[vy * AW + vx][4 * q]);
+        const float x0 = xrow[2 * vx + o0], x1 = xrow[2 * vx + o1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc0[e] = fmaf(a[e], x0, acc0[e]);
+          acc1[e] = fmaf(a[e], x1, acc1[e]);
+        }
       }
     }
   }
-  slab[(int64_t)blockIdx.x * 512 + r * 16 + k0] = acc0;
-  slab[(int64_t)blockIdx.x * 512 + r * 16 + k1] = acc1;
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[wv][(4 * q + e) * 16 + k0] = acc0[e];
+    red[wv][(4 * q + e) * 16 + k1] = acc1[e];
+  }
+  __syncthreads();
+  for (int i = t; i < 512; i += 256)
+    slab[(int64_t)blockIdx.x * 512 + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
 }
 
 int conv4_c1_fwd(const float* src, int NF, int H, int W, const float* w, const float* bias, float* out,
