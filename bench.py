@@ -340,6 +340,33 @@ def run_gpu(args, rank, world, local_rank):
                "path": "pinned u8 host clips -> ClipStager.issue (H2D copy + u8->fp32 conversion on the stager stream, "
                     "batch k+1 during step k) -> step(inputs_ready=event): the early stem waits for it, the critical "
                     "stream does not"}
+    # drop-in loop leg (rank 0, N=1): the package's own train_model inner loop (vad_amd.train.train_epoch) over a
+    # loader of pinned host u8 clips -- prefetch + ClipStager, one fused step per batch, and the per-step host read of
+    # the loss vector the reference does (loss.item(), cad:692) -- i.e. what a drop-in caller of train_model gets
+    dropin = None
+    if rank == 0 and world == 1 and args.h2d_steps > 0:
+        from vad_amd.data import ClipStager
+        from vad_amd.train import train_epoch
+        stager = ClipStager(dev, mode=0)
+        u8 = [torch.randint(0, 256, (B, T, 1, H, W), dtype=torch.uint8).pin_memory() for _ in range(2)]
+        lab_cpu = labels.cpu()
+
+        def loader(n):
+            for i in range(n):
+                yield u8[i % 2], lab_cpu
+
+        train_epoch(trainer, loader(3), stager, log=None)  # warm-up
+        torch.cuda.synchronize()
+        n_loop = max(2 * args.h2d_steps, 10)
+        t0 = time.perf_counter()
+        tot, nb = train_epoch(trainer, loader(n_loop), stager, log=None)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        dropin = {"value": round(B * n_loop / el, 3), "unit": "clips/s", "steps": n_loop,
+                  "ms_per_step": round(1e3 * el / n_loop, 4), "mean_total_loss": round(tot / max(nb, 1), 6),
+                  "path": "vad_amd.train.train_epoch (train_model's inner loop): pinned u8 loader -> prefetch / "
+                          "ClipStager (batch k+1 staged during step k) -> CadTrainer.step(inputs_ready=event, "
+                          "host_losses=True) -> losses.tolist() every step (cad:692's loss.item())"}
     # whole-step algorithmic FLOP rate (all 3x3 convs fwd/dgrad/wgrad + conv1 fwd), for context
     conv_flops = sum(2.0 * NF * oh * ow * co * ci * 9 for NF, ci, co, oh, ow in conv_shapes(B, T, H, W))
     dgrad_flops = conv_flops - 2.0 * B * T * conv_shapes(B, T, H, W)[0][3] * conv_shapes(B, T, H, W)[0][4] * 32 * 32 * 9
@@ -349,7 +376,7 @@ def run_gpu(args, rank, world, local_rank):
     roof["instrumented_ms_per_step"] = round(prof_ms_per_step, 4)
     return dict(elapsed=elapsed, step_ms=step_ms, host_enqueue_ms=1e3 * (t_enq - t_loop0) / args.steps, roof=roof,
                 breakdown=breakdown, dominant=dominant,
-                final_loss=final_loss, step_tflops=step_flops / (step_ms * 1e-3) / 1e12, probe=probe, h2d=h2d,
+                final_loss=final_loss, step_tflops=step_flops / (step_ms * 1e-3) / 1e12, probe=probe, h2d=h2d, dropin=dropin,
                 allreduce_bytes=allreduce_bytes, post_backbone_us=post_backbone_us)
 
 
@@ -1017,6 +1044,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "h2d_inclusive": r.get("h2d"),
+            "dropin_loop": r.get("dropin"),
             "bn_stats": "group (SyncBatchNorm)" if (args.sync_bn and world > 1) else "per rank",
             "step_roofline": step_roofline(args, clips / r["elapsed"] / world, r["step_tflops"]),
             "allreduce_bytes_per_step": r["allreduce_bytes"],

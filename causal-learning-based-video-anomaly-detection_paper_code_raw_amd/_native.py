@@ -171,3 +171,12 @@ def require_hip(t) -> None:
     if not (isinstance(t, torch.Tensor) and t.is_cuda):
         raise RuntimeError("this build runs on MI355X (HIP) devices only; got a tensor on "
                            f"{getattr(t, 'device', type(t))}")
+
+
+def host_device_ptr(t) -> int:
+    """Device address of a pinned host tensor (kernels write it over PCIe; vad_host_device_ptr)."""
+    if not t.is_pinned():
+        raise ValueError("host_device_ptr: the tensor must be pinned")
+    out = ctypes.c_void_p()
+    check(lib().vad_host_device_ptr(t.data_ptr(), ctypes.addressof(out)))
+    return out.value

@@ -253,17 +253,24 @@ class ClipStager:
         return self.finish(self.issue(batch_u8))
 
 
-def prefetch(loader, stager: ClipStager):
+def prefetch(loader, stager: ClipStager, with_ready: bool = False):
     """Iterate (device clips, device labels) one batch ahead: the H2D copy of batch k+1 is issued before batch k is
     yielded (it runs on the copy stream while step k computes) and converted when batch k+1 is yielded.  uint8
-    batches go through the stager; float batches (the reference's own datasets) are copied as they are."""
+    batches go through the stager; float batches (the reference's own datasets) are copied as they are.
+    with_ready=True: yields (clips, labels, ready) -- for a staged batch the current stream does not wait for it and
+    ``ready`` is the event that completes it (hand it to CadTrainer.step(inputs_ready=...)); None otherwise."""
     def issue(x, y):
         h = stager.issue(x) if x.dtype == torch.uint8 else x
         return h, y
 
     def finish(h, y):
-        xd = stager.finish(h) if not isinstance(h, torch.Tensor) else h.to(stager.device, non_blocking=True)
-        return xd, y.to(stager.device, non_blocking=True)
+        yd = y.to(stager.device, non_blocking=True)
+        if isinstance(h, torch.Tensor):
+            xd = h.to(stager.device, non_blocking=True)
+            return (xd, yd, None) if with_ready else (xd, yd)
+        if with_ready:
+            return stager.finish(h, wait=False), yd, h.ready
+        return stager.finish(h), yd
 
     it = iter(loader)
     try:

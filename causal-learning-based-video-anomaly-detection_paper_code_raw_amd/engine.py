@@ -196,8 +196,10 @@ class CadEngine:
 
     # ------------------------------------------------------------------ compute
     def forward(self, x: torch.Tensor, training: bool, seed: int, step: int, clip0: int, labels=None,
-                want_outputs: bool = True):
-        """Runs the fused forward.  want_outputs=False returns only the loss vector (no output copies)."""
+                want_outputs: bool = True, loss_host=None):
+        """Runs the fused forward.  want_outputs=False returns only the loss vector (no output copies); with
+        loss_host (a pinned 5-float CPU tensor) the loss-tail kernel writes the vector straight into it over PCIe,
+        so a host read needs only an event recorded after this call, not the queued backward and optimizer."""
         nat.require_hip(x)
         if x.dim() != 5:
             raise ValueError(f"Expected 5D tensor (B,T,C,H,W), got {tuple(x.shape)}")
@@ -217,16 +219,21 @@ class CadEngine:
                 torch.cuda.current_stream(self.device).cuda_stream)))
         dev = self.device
         if not want_outputs:
-            if self._loss_buf is None:
-                self._loss_buf = torch.empty(5, device=dev)
+            if loss_host is not None:
+                if loss_host.numel() != 5 or loss_host.dtype != torch.float32 or not loss_host.is_contiguous():
+                    raise ValueError("loss_host: a contiguous 5-float pinned CPU tensor")
+                loss_ptr, loss_t = nat.host_device_ptr(loss_host), loss_host
+            else:
+                if self._loss_buf is None:
+                    self._loss_buf = torch.empty(5, device=dev)
+                loss_ptr, loss_t = self._loss_buf.data_ptr(), self._loss_buf
             lab = None if labels is None else labels.to(device=dev, dtype=torch.int64).contiguous()
             nat.check(nat.lib().vad_cad_forward(
                 pl.h, x.data_ptr(), 1 if training else 0, seed & ((1 << 64) - 1), step, clip0, nat.ptr(lab),
-                None, None, None, None, None, None, None, None, None, self._loss_buf.data_ptr(), None,
-                nat.stream_of(dev)))
+                None, None, None, None, None, None, None, None, None, loss_ptr, None, nat.stream_of(dev)))
             self.generation += 1
             self._last = (pl, lab, x)
-            return {"losses": self._loss_buf}
+            return {"losses": loss_t}
         o = dict(
             final=torch.empty(B, device=dev), probs=torch.empty(B, 2, device=dev),
             causal=torch.empty(B, device=dev), kl=torch.empty(B, device=dev),

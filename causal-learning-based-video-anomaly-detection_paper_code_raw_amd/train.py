@@ -97,9 +97,12 @@ class CadTrainer:
             self._bn_pg = dist.new_group(ranks=ranks)
             self.eng.set_bn_sync(self._bn_pg)
 
-    def step(self, videos, labels, lr=None, want_outputs=False, inputs_ready=None):
+    def step(self, videos, labels, lr=None, want_outputs=False, inputs_ready=None, host_losses=False):
         """One training step; returns the (device) loss vector [cls, anomaly, causal, kl, total] (want_outputs: the
-        forward's output dict, see CadEngine.forward).  inputs_ready: None -- the clips are produced on the current
+        forward's output dict, see CadEngine.forward).  host_losses=True: returns that vector as a CPU tensor instead
+        -- the reference reads loss.item() every step (cad:692); here the forward's loss-tail kernel writes it into
+        pinned host memory and the host waits only for the forward (an event), so the backward and optimizer it has
+        already queued keep the device busy while the caller prepares the next step.  inputs_ready: None -- the clips are produced on the current
         stream, the step is ordered after it; True -- they are complete on the device already (staged and
         synchronised before); a torch.cuda.Stream -- its queued work completes them; a torch.cuda.Event -- its
         completion does (ClipStager.finish(h, wait=False) with h.ready).  Given, the frozen stem may start
@@ -110,12 +113,12 @@ class CadTrainer:
             caller = torch.cuda.current_stream(self.eng.device)
             self.prio_stream.wait_stream(caller)
             with torch.cuda.stream(self.prio_stream):
-                o = self._step(videos, labels, lr, want_outputs, inputs_ready)
+                o = self._step(videos, labels, lr, want_outputs, inputs_ready, host_losses)
             caller.wait_stream(self.prio_stream)
             return o
-        return self._step(videos, labels, lr, want_outputs, inputs_ready)
+        return self._step(videos, labels, lr, want_outputs, inputs_ready, host_losses)
 
-    def _step(self, videos, labels, lr, want_outputs, inputs_ready=None):
+    def _step(self, videos, labels, lr, want_outputs, inputs_ready=None, host_losses=False):
         eng = self.eng
         B = videos.shape[0]
         cur = torch.cuda.current_stream(eng.device) if eng.grads.is_cuda else None
@@ -148,7 +151,17 @@ class CadTrainer:
                 self._arm_stream.wait_event(self._bufs_ev)
             T, H, W = videos.shape[1], videos.shape[3], videos.shape[4]
             eng.input_ready(B, T, H, W, stream=self._arm_stream)
-        o = eng.forward(videos, True, self.seed, self.step_idx, self.rank * B, labels, want_outputs=want_outputs)
+        lh = None
+        if host_losses and not want_outputs and cur is not None:
+            if getattr(self, "_loss_host", None) is None:
+                # (one buffer: the host has read step k's losses before step k+1's forward is queued)
+                self._loss_host = torch.zeros(5, dtype=torch.float32).pin_memory()
+                self._loss_ev = torch.cuda.Event()
+            lh = self._loss_host
+        kw = {"loss_host": lh} if lh is not None else {}
+        o = eng.forward(videos, True, self.seed, self.step_idx, self.rank * B, labels, want_outputs=want_outputs, **kw)
+        if lh is not None:
+            self._loss_ev.record(cur)
         if bcast:
             # the running statistics are final once the forward has run (the backward does not touch them): every
             # rank takes rank 0's here -- the values the reference's replicas start the next step from
@@ -167,6 +180,11 @@ class CadTrainer:
         eng.optimizer_step(self.lr if lr is None else lr, self.betas, self.eps, self.wd, self.max_norm,
                            1.0 / self.world)
         self.step_idx += 1
+        if lh is not None:
+            self._loss_ev.synchronize()  # the forward (loss tail) is done; backward + optimizer may still run
+            return lh.clone()
+        if host_losses and not want_outputs:
+            return o["losses"].cpu()
         return o if want_outputs else o["losses"]
 
     def _reduce(self, t):
@@ -216,6 +234,30 @@ def _eval_losses(model, videos, labels):
     return o
 
 
+def train_epoch(trainer, train_loader, stager, epoch=0, num_epochs=1, lr=None, log=print):
+    """One epoch of train_model's inner loop (cad:637-700): per batch one fused step and the per-step loss read the
+    reference does (loss.item(), cad:692), the running total and the batch print every 5 batches.  Returns
+    (summed total loss, batches).  u8 clips (vad_amd.data datasets) are staged through pinned memory and normalised on
+    the device one batch ahead, the step's early stem waiting for them (inputs_ready); the losses come back through
+    pinned memory right after the forward (CadTrainer.step(host_losses=True)), so reading them does not drain the
+    queued backward.  Float clips (the reference's own datasets) are copied as they are."""
+    tot, nb = 0.0, 0
+    for batch_idx, (videos, labels, ready) in enumerate(prefetch(train_loader, stager, with_ready=True)):
+        try:
+            l = trainer.step(videos, labels, lr=lr, inputs_ready=ready, host_losses=True).tolist()
+            tot += l[4]
+            nb += 1
+            if batch_idx % 5 == 0 and log is not None:
+                log(f"Epoch {epoch+1}/{num_epochs}, Batch {batch_idx+1}, Total: {l[4]:.6f}, Class: {l[0]:.6f}")
+        except RuntimeError as e:
+            if "out of memory" in str(e):
+                print(f"CUDA out of memory at batch {batch_idx}. Skipping batch...")
+                torch.cuda.empty_cache()
+                continue
+            raise
+    return tot, nb
+
+
 def train_model(model, train_loader, val_loader, num_epochs=20, lr=3e-4):
     """Training loop with the multi-objective loss (cad:609-790).  Returns (model, train_losses, val_losses)."""
     model = apply_memory_efficient_training(model)
@@ -228,23 +270,7 @@ def train_model(model, train_loader, val_loader, num_epochs=20, lr=3e-4):
     for epoch in range(num_epochs):
         model.train()
         cur_lr = _cosine_lr(lr, epoch, num_epochs)
-        tot, nb = 0.0, 0
-        # u8 clips (vad_amd.data datasets) are staged through pinned memory and normalised on the device, one batch
-        # ahead of the step; float clips (the reference's datasets) are copied as they are
-        for batch_idx, (videos, labels) in enumerate(prefetch(train_loader, stager)):
-            try:
-                losses = trainer.step(videos, labels, lr=cur_lr)
-                l = losses.tolist()
-                tot += l[4]
-                nb += 1
-                if batch_idx % 5 == 0:
-                    print(f"Epoch {epoch+1}/{num_epochs}, Batch {batch_idx+1}, Total: {l[4]:.6f}, Class: {l[0]:.6f}")
-            except RuntimeError as e:
-                if "out of memory" in str(e):
-                    print(f"CUDA out of memory at batch {batch_idx}. Skipping batch...")
-                    torch.cuda.empty_cache()
-                    continue
-                raise
+        tot, nb = train_epoch(trainer, train_loader, stager, epoch, num_epochs, cur_lr)
         model.eval()
         vtot, vb, correct, total = 0.0, 0, 0, 0
         with torch.no_grad():

@@ -207,3 +207,52 @@ def test_train_model_on_u8_frame_folders_equals_float_clips(tree):
     assert res[0][1] == res[1][1] and res[0][2] == res[1][2]
     np.testing.assert_array_equal(res[0][3], res[1][3])
     assert np.isfinite(res[0][1][0])
+
+
+@pytest.mark.gpu
+def test_train_epoch_host_losses_equal_device_losses():
+    """train_model's inner loop (train_epoch: prefetch with ready events, the early stem waiting for them, the losses
+    read through pinned memory right after each forward) gives the same per-step losses and weights as serial steps
+    on synchronously staged clips whose losses are read from the device after each whole step."""
+    import contextlib
+    import io
+    from vad_amd.cad import CausalAnomalyDetector
+    from vad_amd.data import ClipStager
+    from vad_amd.train import CadTrainer, apply_memory_efficient_training, train_epoch
+    g = torch.Generator().manual_seed(9)
+    batches = [(torch.randint(0, 256, (2, 4, 1, 64, 64), generator=g, dtype=torch.uint8), torch.tensor([i % 2, 1]))
+               for i in range(5)]
+    res = []
+    for loop in (False, True):
+        torch.manual_seed(0)
+        m = CausalAnomalyDetector()
+        with contextlib.redirect_stdout(io.StringIO()):
+            apply_memory_efficient_training(m)
+        tr = CadTrainer(m.cuda(), lr=3e-4, seed=3)
+        st = ClipStager("cuda", mode=0)
+        per_step = []
+        if loop:
+            logs = []
+            tot, nb = train_epoch(tr, batches, st, lr=2e-4, log=logs.append)
+            assert nb == 5 and len(logs) == 1
+        else:
+            tot, nb = 0.0, 0
+            for x, y in batches:
+                l = tr.step(st.stage(x), y.cuda(), lr=2e-4).tolist()  # (device losses after the whole step)
+                per_step.append(l)
+                tot += l[4]
+                nb += 1
+        torch.cuda.synchronize()
+        res.append((tot, torch.cat([p.detach().reshape(-1).cpu() for p in m.parameters()])))
+        if not loop:
+            # host_losses on its own: the same vector as the device's, read after the forward only
+            torch.manual_seed(0)
+            m2 = CausalAnomalyDetector()
+            with contextlib.redirect_stdout(io.StringIO()):
+                apply_memory_efficient_training(m2)
+            tr2 = CadTrainer(m2.cuda(), lr=3e-4, seed=3)
+            for (x, y), want in zip(batches, per_step):
+                got = tr2.step(st.stage(x), y.cuda(), lr=2e-4, host_losses=True)
+                assert got.device.type == "cpu" and got.tolist() == want
+    assert res[0][0] == res[1][0]
+    np.testing.assert_array_equal(res[0][1].numpy(), res[1][1].numpy())
