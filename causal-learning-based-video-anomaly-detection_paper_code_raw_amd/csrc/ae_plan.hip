@@ -1298,6 +1298,19 @@ int vad_ae_optimizer_step(vad_ae_plan* plan, float lr, float beta1, float beta2,
   return 0;
 }
 
+int vad_ae_debug_buffer(vad_ae_plan* plan, const char* name, int idx, void** ptr, int64_t* nfloats) {
+  VAD_CHECK(plan && name && ptr && nfloats, "vad_ae_debug_buffer: null argument");
+  AePlanImpl& c = plan->impl;
+  const std::string n(name);
+  if (n == "ey" && idx >= 0 && idx < 4) { *ptr = c.ey[idx]; *nfloats = c.ge[idx].rows() * ENC_CO[idx]; }
+  else if (n == "est" && idx >= 0 && idx < 4) { *ptr = c.est[idx]; *nfloats = (int64_t)c.T * AE_ST * ENC_CO[idx]; }
+  else if (n == "dy" && idx >= 0 && idx < 3) { *ptr = c.dy[idx]; *nfloats = c.gd[idx].in.numel(); }
+  else if (n == "dst" && idx >= 0 && idx < 3) { *ptr = c.dst[idx]; *nfloats = (int64_t)AE_ST * DEC_CO[idx]; }
+  else if (n == "u") { *ptr = c.u; *nfloats = (int64_t)c.B * AE_FLAT; }
+  else { vad::set_error("vad_ae_debug_buffer: unknown buffer " + n); return 1; }
+  return 0;
+}
+
 int vad_ae_update_memory(float* memory, int64_t* memory_ptr, const float* features, int n, void* stream) {
   VAD_CHECK(memory && memory_ptr && features && n >= 0 && n <= AE_MEM,
             "vad_ae_update_memory: bad arguments (at most 500 features of 64)");

@@ -279,6 +279,11 @@ int vad_ae_optimizer_step(vad_ae_plan* plan, float lr, float beta1, float beta2,
                           float max_norm, float grad_scale, void* stream);
 /* the memory ring of any VideoAutoEncoder: update_memory (cad1:201-219; n <= 500 features (n, 64)) and
  * compute_anomaly_score (cad1:262-301; n sequence features -> scores (n,)) */
+/* test access to the last forward's pre-activations (the gradient tests pin their LeakyReLU decisions): "ey" idx l:
+ * encoder conv l's raw output [T*B frames, t-major][H][W][Co]; "est" idx l: its per-frame-index BN state [T][8][Co]
+ * (mean | invstd | scale | shift | ...); "dy" idx j < 3: decoder ConvTranspose2d j's raw output [B][H][W][Co]; "dst"
+ * idx j: its BN state [8][Co]; "u": the decoder Linear's output [B][2048].  Device pointers (vad_debug_d2h). */
+int vad_ae_debug_buffer(vad_ae_plan* plan, const char* name, int idx, void** ptr, int64_t* nfloats);
 int vad_ae_update_memory(float* memory, int64_t* memory_ptr, const float* features, int n, void* stream);
 int vad_ae_memory_score(const float* memory, const int64_t* memory_ptr, const float* seq, int n, float* scores,
                         void* stream);

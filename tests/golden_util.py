@@ -56,6 +56,40 @@ def golden_names():
 
 
 # ---------------------------------------------------------------- mask-pinned oracle gradients (GPU tests)
+def read_ae_debug(plan, name, idx=0):
+    """Copy a cad1 plan's debug buffer (vad_ae_debug_buffer) to the host (float32)."""
+    import ctypes
+    from vad_amd import _native as nat
+    p, k = ctypes.c_void_p(), ctypes.c_int64()
+    nat.check(nat.lib().vad_ae_debug_buffer(plan.h, name.encode(), idx, ctypes.byref(p), ctypes.byref(k)))
+    out = np.empty(k.value, np.float32)
+    nat.check(nat.lib().vad_debug_d2h(out.ctypes.data, p.value, out.nbytes))
+    return out
+
+
+def ae_leaky_pins(plan, B, T):
+    """The LeakyReLU decisions of the device's last cad1 forward, in the oracle's layout (ae_oracle.ae_forward pins):
+    the sign of y * scale + shift computed exactly in float64 from the device's raw conv outputs and BN state (the
+    device's fp32 fma decision), and of the decoder Linear's output."""
+    from oracle import ae_oracle as ae
+    enc_hw = (32, 16, 8, 4)
+    enc = [[None] * 4 for _ in range(T)]
+    for l in range(4):
+        C, hw = (32, 64, 128, 128)[l], enc_hw[l]
+        y = read_ae_debug(plan, "ey", l).astype(np.float64).reshape(T, B, hw, hw, C)
+        st = read_ae_debug(plan, "est", l).astype(np.float64).reshape(T, 8, C)
+        z = y * st[:, None, None, None, 2, :] + st[:, None, None, None, 3, :]
+        m = torch.from_numpy(np.ascontiguousarray((z > 0).transpose(0, 1, 4, 2, 3)))
+        for t in range(T):
+            enc[t][l] = m[t]
+    dec = [torch.from_numpy(read_ae_debug(plan, "u").reshape(B, 2048) > 0)]
+    for j in range(3):
+        C, hw = (128, 64, 32)[j], (8, 16, 32)[j]
+        y = read_ae_debug(plan, "dy", j).astype(np.float64).reshape(B, hw, hw, C)
+        st = read_ae_debug(plan, "dst", j).astype(np.float64).reshape(8, C)
+        dec.append(torch.from_numpy(np.ascontiguousarray((y * st[2] + st[3] > 0).transpose(0, 3, 1, 2))))
+    assert len(ae.ENC_CONVS) == 4
+    return {"enc": enc, "dec": dec}
 def read_debug(plan, name, idx=0, n=None, dtype=np.float32):
     """Copy a plan's debug buffer (vad_cad_debug_buffer) to the host."""
     import ctypes
