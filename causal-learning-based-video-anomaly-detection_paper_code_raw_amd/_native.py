@@ -130,6 +130,7 @@ _SIGS = {
     "vad_ae_optimizer_step": (_I, [_P, _F, _F, _F, _F, _F, _F, _F, _P]),
     "vad_ae_update_memory": (_I, [_P, _P, _P, _I, _P]),
     "vad_ae_memory_score": (_I, [_P, _P, _P, _I, _P, _P]),
+    "vad_a2_set_option": (_I, [_P, ctypes.c_char_p, _I64]),
     "vad_ae_debug_buffer": (_I, [_P, ctypes.c_char_p, _I, ctypes.POINTER(_P), ctypes.POINTER(_I64)]),
 }
 

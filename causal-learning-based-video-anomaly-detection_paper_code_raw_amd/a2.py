@@ -130,6 +130,7 @@ class _A2Plan:
         f = dict(dtype=torch.float32, device=e.device)
         self.scores, self.adj, self.feats = torch.zeros(B, **f), torch.zeros(B, 16, 16, **f), torch.zeros(B, 16, **f)
         self.d_s, self.d_adj = torch.zeros(B, **f), torch.zeros(B, 16, 16, **f)
+        self.borrow = False
 
     def __del__(self):
         try:
@@ -182,8 +183,12 @@ class A2Engine:
     def stream(self):
         return nat.stream_of(self.device)
 
-    def forward(self, x, training, seed, step, clip0, with_loss):
+    def forward(self, x, training, seed, step, clip0, with_loss, borrow_input=False):
+        """borrow_input: x stays unchanged until the backward (the fused train step): conv3d_1 reads it in place."""
         p = self.cur
+        if p.borrow != bool(borrow_input):
+            nat.check(nat.lib().vad_a2_set_option(p.plan, b"borrow_input", int(bool(borrow_input))))
+            p.borrow = bool(borrow_input)
         nat.check(nat.lib().vad_a2_forward(p.plan, nat.ptr(x), int(training), ctypes.c_uint64(seed),
                                            ctypes.c_uint64(step), ctypes.c_int64(clip0), int(with_loss),
                                            nat.ptr(p.scores), nat.ptr(p.adj), nat.ptr(p.feats),
@@ -349,7 +354,7 @@ class ImprovedMiniCausalVAD:
         e = self.model.engine(videos)
         self.optimizer.push_state(e)
         g = self.optimizer.param_groups[0]
-        e.forward(videos, True, self.seed, self.global_step, self.clip0, with_loss=True)
+        e.forward(videos, True, self.seed, self.global_step, self.clip0, with_loss=True, borrow_input=True)
         vals = e.losses.cpu().tolist()
         comps = dict(zip(LOSS_KEYS, vals[1:8]))
         stepped = not np.isnan(vals[0])

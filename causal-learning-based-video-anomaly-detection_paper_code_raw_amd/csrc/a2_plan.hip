@@ -22,6 +22,7 @@
 
 namespace vad {
 
+int g_a2_head_clip = 1;  // knob "a2_head_clip": the head forward / backward one block per clip (0: one launch per layer)
 int g_a2_direct = 1;  // knob "a2_direct": conv3d_1 direct on the VALU (latched per plan; 0: im2col + GEMM)
 
 constexpr int A2_NSLOT = 20;
@@ -145,6 +146,43 @@ __global__ __launch_bounds__(256) void a2_head_fwd_kernel(A2HeadArgs a, int st) 
     default:
       if (idx < B) a.s[idx] = a2_sigmoid(a2_dot(a.hp0 + idx * 32, P + o[S_AP2W], 32, P[o[S_AP2B]]));
   }
+}
+
+// The whole head of one clip per block (B blocks): the six stages above in order, each output computed by one thread
+// with a2_dot's arithmetic (k in order) -- bit-identical to the per-stage launches -- with the stage inputs read from
+// LDS; the saved activations still go to global memory for the backward.  One launch instead of six dependent ones.
+__global__ __launch_bounds__(256) void a2_head_fwd_clip_kernel(A2HeadArgs a) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  const float* P = a.P;
+  const int64_t* o = a.off;
+  __shared__ float sf[16], shc0[32], sadj[256], sg1d[128], scat[80], shp0[32];
+  if (t < 16) sf[t] = scat[t] = a.f[b * 16 + t];
+  __syncthreads();
+  if (t < 32) shc0[t] = a.hc0[b * 32 + t] = relu_nan(a2_dot(sf, P + o[S_CN0W] + t * 16, 16, P[o[S_CN0B] + t]));
+  __syncthreads();
+  {
+    const float sg = a2_sigmoid(a2_dot(shc0, P + o[S_CN2W] + t * 32, 32, P[o[S_CN2B] + t]));
+    a.sig[b * 256 + t] = sg;
+    sadj[t] = a.adj[b * 256 + t] = (t / 16 == t % 16) ? sg * 0.f : sg;  // * (1 - eye)
+  }
+  __syncthreads();
+  if (t < 128) {
+    float v = relu_nan(a2_dot(sadj, P + o[S_GE0W] + t * 256, 256, P[o[S_GE0B] + t]));
+    a.g1[b * 128 + t] = v;
+    if (a.training) v = rng_u24(a.h_graph, (uint64_t)(a.clip0 + b), (uint64_t)t) >= a.thr_graph ? v * a.s_graph : 0.f;
+    sg1d[t] = a.g1d[b * 128 + t] = v;
+  }
+  __syncthreads();
+  if (t < 64) {
+    const float v = a2_dot(sg1d, P + o[S_GE3W] + t * 128, 128, P[o[S_GE3B] + t]);
+    a.g2[b * 64 + t] = v;
+    scat[16 + t] = a.cat[b * 80 + 16 + t] = v;
+  }
+  if (t < 16) a.cat[b * 80 + t] = sf[t];
+  __syncthreads();
+  if (t < 32) shp0[t] = a.hp0[b * 32 + t] = relu_nan(a2_dot(scat, P + o[S_AP0W] + t * 80, 80, P[o[S_AP0B] + t]));
+  __syncthreads();
+  if (t == 0) a.s[b] = a2_sigmoid(a2_dot(shp0, P + o[S_AP2W], 32, P[o[S_AP2B]]));
 }
 
 // compute_improved_loss (a2:135-205) on the saved scores / adjacency, plus d total / d scores and d total / d adj, as
@@ -294,6 +332,55 @@ struct A2HeadBwdArgs {
   uint32_t thr_fc;
   float s_fc;
 };
+
+// Backward stages 0-5 of one clip per block (B blocks), the per-stage launches' arithmetic in the same order
+// (bit-identical), stage inputs from LDS, every stage's output also written out for the weight-gradient launch (stage 6)
+__global__ __launch_bounds__(256) void a2_head_bwd_clip_kernel(A2HeadBwdArgs a) {
+  const A2HeadArgs& f = a.f;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const float* P = f.P;
+  const int64_t* o = f.off;
+  __shared__ float sap0[32], sdg2[64], sdfeat[16], sge0[128], scn2[256], scn0[32];
+  if (t < 32) {  // predictor: s = sigmoid(W2 hp0 + b), hp0 = relu(W0 cat + b)
+    const float dz2 = a.d_s[b] * f.s[b] * (1.f - f.s[b]);
+    if (t == 0) a.dz_ap2[b] = dz2;
+    sap0[t] = a.dz_ap0[b * 32 + t] = f.hp0[b * 32 + t] > 0.f ? dz2 * P[o[S_AP2W] + t] : 0.f;
+  }
+  __syncthreads();
+  if (t < 80) {
+    float d = 0.f;
+    for (int k = 0; k < 32; ++k) d = fmaf(sap0[k], P[o[S_AP0W] + k * 80 + t], d);
+    if (t < 16) sdfeat[t] = d + (a.d_f ? a.d_f[b * 16 + t] : 0.f);
+    else sdg2[t - 16] = a.dg2[b * 64 + t - 16] = d;
+  }
+  __syncthreads();
+  if (t < 128) {  // graph encoder: g2 = W3 g1d + b; g1d = drop(relu(W0 adj + b))
+    float d = 0.f;
+    for (int k = 0; k < 64; ++k) d = fmaf(sdg2[k], P[o[S_GE3W] + k * 128 + t], d);
+    if (f.training) d = rng_u24(f.h_graph, (uint64_t)(f.clip0 + b), (uint64_t)t) >= f.thr_graph ? d * f.s_graph : 0.f;
+    sge0[t] = a.dz_ge0[b * 128 + t] = f.g1[b * 128 + t] > 0.f ? d : 0.f;
+  }
+  __syncthreads();
+  {  // d adj -> d sig (zero diagonal) -> dz_cn2
+    float d = a.d_adj ? a.d_adj[b * 256 + t] : 0.f;
+    for (int k = 0; k < 128; ++k) d = fmaf(sge0[k], P[o[S_GE0W] + k * 256 + t], d);
+    const float sg = f.sig[b * 256 + t];
+    scn2[t] = a.dz_cn2[b * 256 + t] = (t / 16 == t % 16) ? 0.f : d * sg * (1.f - sg);
+  }
+  __syncthreads();
+  if (t < 32) {
+    float d = 0.f;
+    for (int e = 0; e < 256; ++e) d = fmaf(scn2[e], P[o[S_CN2W] + e * 32 + t], d);
+    scn0[t] = a.dz_cn0[b * 32 + t] = f.hc0[b * 32 + t] > 0.f ? d : 0.f;
+  }
+  __syncthreads();
+  if (t < 16) {  // d features (fc output after dropout) += W_cn0^T dz_cn0, then the fc dropout backward
+    float d = sdfeat[t];
+    for (int k = 0; k < 32; ++k) d = fmaf(scn0[k], P[o[S_CN0W] + k * 16 + t], d);
+    if (f.training) d = rng_u24(a.h_fc, (uint64_t)(f.clip0 + b), (uint64_t)t) >= a.thr_fc ? d * a.s_fc : 0.f;
+    a.dfeat[b * 16 + t] = d;
+  }
+}
 
 // backward stage st (the forward's mirror): 0 predictor output + anomaly_predictor.0 pre-activation grads, 1 d cat ->
 // d g2 and the predictor's share of d features, 2 graph_encoder.0 pre-activation grads (dropout, ReLU), 3 d adj (graph
@@ -662,6 +749,8 @@ struct A2PlanImpl {
   double* sqp;
   int64_t* off_dev;
   float* xin = nullptr;  // (a2_direct) the forward's clip, kept for conv3d_1's weight gradient
+  const float* xsrc = nullptr;  // the clip conv3d_1 reads: xin, or the caller's x itself with option borrow_input
+  int borrow_input = 0;  // option: the caller keeps x unchanged until the backward (the fused step): no copy
   // (a2_direct) conv3d_2 / conv3d_3 weight images (conv3s2_prep: [Co][27 Ci] + the 8 parity-class images) and the
   // second input-gradient buffer
   float *wk3[3] = {}, *wc3[3] = {}, *dA2 = nullptr;
@@ -760,9 +849,14 @@ struct A2PlanImpl {
     for (int s3 = 0; s3 < 3; ++s3) {
       if (direct && s3 == 0) {
         const int64_t n = g[0].in.numel();
-        VAD_HIP(hipMemcpyAsync(xin, x, sizeof(float) * n, hipMemcpyDeviceToDevice, st));
+        if (borrow_input) {
+          xsrc = x;
+        } else {
+          VAD_HIP(hipMemcpyAsync(xin, x, sizeof(float) * n, hipMemcpyDeviceToDevice, st));
+          xsrc = xin;
+        }
         const A2Tiles tl(B, T, H, W);
-        hipLaunchKernelGGL(a2_conv1_fwd_kernel, dim3((unsigned)std::min<int64_t>(tl.n, 4096)), dim3(256), 0, st, xin, B,
+        hipLaunchKernelGGL(a2_conv1_fwd_kernel, dim3((unsigned)std::min<int64_t>(tl.n, 4096)), dim3(256), 0, st, xsrc, B,
                            T, H, W, P(S_C1W), P(S_C1B), y[0]);
         VAD_LAUNCH_CHECK();
         continue;
@@ -792,9 +886,14 @@ struct A2PlanImpl {
     }
     VAD_TRY(dense_fwd(pooled, B, 4096, P(S_FCW), P(S_FCB), 16, f, fc, scratch, scratch_floats, st));
     const A2HeadArgs ha = head_args();
-    for (int s = 0; s < 6; ++s) {
-      hipLaunchKernelGGL(a2_head_fwd_kernel, dim3((unsigned)cdiv(B * A2_FWD_N[s], 256)), dim3(256), 0, st, ha, s);
+    if (g_a2_head_clip) {
+      hipLaunchKernelGGL(a2_head_fwd_clip_kernel, dim3((unsigned)B), dim3(256), 0, st, ha);
       VAD_LAUNCH_CHECK();
+    } else {
+      for (int s = 0; s < 6; ++s) {
+        hipLaunchKernelGGL(a2_head_fwd_kernel, dim3((unsigned)cdiv(B * A2_FWD_N[s], 256)), dim3(256), 0, st, ha, s);
+        VAD_LAUNCH_CHECK();
+      }
     }
     if (with_loss) VAD_TRY(loss(st));
     return 0;
@@ -835,7 +934,11 @@ struct A2PlanImpl {
     hb.h_fc = rng_h1(seed, S_A2_DROP_FC, step);
     hb.thr_fc = drop_threshold(0.3);
     hb.s_fc = 1.0f / (float)(1.0 - 0.3);
-    for (int s = 0; s < 7; ++s) {
+    if (g_a2_head_clip) {
+      hipLaunchKernelGGL(a2_head_bwd_clip_kernel, dim3((unsigned)B), dim3(256), 0, st, hb);
+      VAD_LAUNCH_CHECK();
+    }
+    for (int s = g_a2_head_clip ? 6 : 0; s < 7; ++s) {
       const int n = s < 6 ? B * A2_BWD_OUT[s] : A2_WG_TOTAL;
       hipLaunchKernelGGL(a2_head_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, hb, s);
       VAD_LAUNCH_CHECK();
@@ -862,7 +965,7 @@ struct A2PlanImpl {
         const A2Tiles tl(B, T, H, W);
         const int64_t cap = scratch_floats / (16 * (A2C1_TAPS + 1));
         const int nb = (int)std::max<int64_t>(1, std::min<int64_t>({tl.n, 512, cap}));
-        hipLaunchKernelGGL(a2_conv1_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, st, dg, xin, B, T, H, W, scratch);
+        hipLaunchKernelGGL(a2_conv1_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, st, dg, xsrc, B, T, H, W, scratch);
         VAD_LAUNCH_CHECK();
         hipLaunchKernelGGL(a2_conv1_wgrad_reduce_kernel, dim3((unsigned)cdiv(16 * (A2C1_TAPS + 1), 16)), dim3(256), 0,
                            st, scratch, nb, G(S_C1W), G(S_C1B));
@@ -967,6 +1070,17 @@ static int a2_copies(const A2Copies& c, int nseg, hipStream_t st) {
 }  // namespace vad
 
 extern "C" {
+
+int vad_a2_set_option(vad_a2_plan* plan, const char* key, int64_t value) {
+  VAD_CHECK(plan && key, "vad_a2_set_option: null argument");
+  const std::string k(key);
+  if (k == "borrow_input") plan->impl.borrow_input = value != 0;
+  else {
+    vad::set_error("vad_a2_set_option: unknown option " + k);
+    return 1;
+  }
+  return 0;
+}
 
 int vad_a2_forward(vad_a2_plan* plan, const float* x, int training, uint64_t seed, uint64_t step, int64_t clip0,
                    int with_loss, float* scores, float* adj, float* features, float* losses, void* stream) {

@@ -7,7 +7,8 @@
 // (decode_sequence, cad1:254-258); the calls are identical, so it runs once per clip and only its BN running
 // statistics take the T updates.
 //   encoder   4 x [Conv2d(4, s2, p1) as an implicit f32 MFMA GEMM over the NHWC frames (backbone.hip conv4_fwd; the
-//             first, 1-channel layer as im2col + GEMM, K = 16) -> per-t BN partial sums
+//             first, 1-channel layer on the VALU, conv4_c1_fwd: 32 outputs per pixel from its 4x4 window) -> per-t BN
+//             partial sums
 //             -> grouped finalize (running stats updated once per t, in t order) -> BN + LeakyReLU(0.1); layer 4
 //             straight into the NCHW flatten order] -> Linear(2048, 64) GEMM -> tanh, NaN -> 0
 //   LSTM      input projection of all B*T frames as one GEMM; the recurrence one block per clip with the W_hh rows
@@ -20,9 +21,11 @@
 //             device-resident memory_ptr
 //   backward  mirror image: Conv2d input grads as parity-class GEMMs over dY, ConvTranspose2d input grads as the
 //             16-tap gather over dY, weight grads as split-K correlations of the two operands (conv4_wgrad; the
-//             1-channel ends -- encoder layer 0's weight grad, the last ConvTranspose2d's grads -- over im2col
-//             columns), grouped BN backward through the LeakyReLU, BPTT one block per clip
-// (knob "ae_direct" = 0 at plan creation: every conv on im2col / col2im columns + dense GEMMs, the round-4 path)
+//             1-channel ends -- encoder layer 0's weight grad, the last ConvTranspose2d's grads -- on the VALU,
+//             conv4_c1_wgrad / conv4_c1_fwd), grouped BN backward through the LeakyReLU, BPTT one block per clip
+// (knob "ae_direct" = 0 at plan creation: every conv, the 1-channel ends included, on im2col / col2im columns + dense
+// GEMMs with K = 16 for the 1-channel layer -- the round-4 path, kept as the cross-check of the direct kernels:
+// tests/test_ae_gpu.py::test_ae_direct_and_im2col_paths_agree)
 //   update    non-finite-grad skip + clip_grad_norm_(0.1) + Adam with coupled L2 (optim.h)
 // Status word (losses[3]): 0 = skipped before backward (train-loop mode: a non-finite input, cad1:385-387 -- the BN
 // running stats, counters and the memory ring stay untouched, as the reference's `continue` before the forward -- or

@@ -150,12 +150,8 @@ int conv3_wgrad_x3(const Conv3Layer& L, const float* dY, const float* src, const
 // fp32 weight gradients (both strides) on the split-bf16 MFMA with transposed LDS fragment reads (conv_x3w.hip)
 extern int g_wgrad_tr, g_wgrad_tr_blocks, g_wgrad_tr_pft;  // knobs "conv_wgrad_tr", "conv_wgrad_tr_blocks", "conv_wgrad_tr_pft"
 bool x3_wgrad_tr_supported(const Conv3Layer& L);
-// bny != nullptr: dY holds dA and the layer's BN backward apply (y = bny, BN state bnst) runs in the staging
 int x3_wgrad_tr(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
-                int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st, const float* bny = nullptr,
-                const float* bnst = nullptr);
-extern int g_wgrad_bn_fused;  // knob "conv_wgrad_bn_fused"
-bool x3_wgrad_tr_bn_supported(const Conv3Layer& L);
+                int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);
 bool conv3_wgrad_patch_supported(const Conv3Layer& L);
 int conv3_wgrad_patch(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
                       int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st);
@@ -184,13 +180,9 @@ int conv3_path(const Conv3Layer& L, int kind);
 // every pass of this layer (forward, input gradient when dgrad, weight gradient) runs on a split kernel under the
 // current knobs, i.e. can take bf16 activations
 bool conv3_act_bf16_ok(const Conv3Layer& L, bool dgrad);
-// alone: nothing else runs beside this weight gradient (the last layer's): the grid fills every CU.  bny != nullptr:
-// dY holds dA and the layer's BN backward apply (y = bny, BN state bnst) is folded into the staging
-// (x3_wgrad_tr_bn_supported layers, fp32 activations)
+// alone: nothing else runs beside this weight gradient (the last layer's): the grid fills every CU
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
-                int* nsplit, int64_t partial_cap, hipStream_t st, bool alone = false, const float* bny = nullptr,
-                const float* bnst = nullptr);
-bool conv3_wgrad_bn_fusable(const Conv3Layer& L);
+                int* nsplit, int64_t partial_cap, hipStream_t st, bool alone = false);
 int conv3_wgrad_reduce(const Conv3Layer& L, const float* partial, int nsplit, const float* bias_partials,
                        int nbias_parts, float* dW, float* db, hipStream_t st);
 

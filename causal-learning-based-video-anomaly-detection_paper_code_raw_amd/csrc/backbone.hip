@@ -1093,7 +1093,7 @@ static ConvTuning g_tune;
 extern int g_bbox_im2col;  // bbox_plan.hip
 extern int g_ae_direct, g_ae_wgrad_blocks, g_ae_wgrad_stream;  // ae_plan.hip
 extern int g_conv4_cls_batch_min, g_conv4_split_tiles;
-extern int g_a2_direct;                     // a2_plan.hip
+extern int g_a2_direct, g_a2_head_clip;     // a2_plan.hip
 int set_tuning(const char* key, int value) {
   const std::string k(key);
   if (k == "conv_fwd_tile") g_tune.fwd = value;
@@ -1125,6 +1125,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv4_cls_batch_min") g_conv4_cls_batch_min = value;
   else if (k == "conv4_split_tiles") g_conv4_split_tiles = value;
   else if (k == "a2_direct") g_a2_direct = value;
+  else if (k == "a2_head_clip") g_a2_head_clip = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "cad_dir_affine") g_cad_dir_affine = value;
@@ -1150,7 +1151,6 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_bfc_s2_ni2") g_bfc_s2_ni2 = value;
   else if (k == "conv3d_direct") g_conv3d_direct = value;
   else if (k == "conv3d_wgrad_blocks") g_conv3d_wg_blocks = value;
-  else if (k == "conv_wgrad_bn_fused") g_wgrad_bn_fused = value;
   else if (k == "conv_dgrad_s2_w3") g_dgrad_s2_w3 = value;
   else if (k == "conv_dgrad_s2_nt") g_dgrad_s2_nt = value;
   else if (k == "bn_apply_u") g_bn_apply_u = value;
@@ -1453,17 +1453,8 @@ int conv3_path(const Conv3Layer& L, int kind) {
   return x3 ? (g_conv_bf16 ? 1 : 6) : 0;
 }
 
-bool conv3_wgrad_bn_fusable(const Conv3Layer& L) {
-  return !g_act_bf16 && g_tune.wgrad_patch && !bfc_wgrad_supported(L) && x3_wgrad_tr_bn_supported(L);
-}
-
 int conv3_wgrad(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* partial,
-                int* nsplit, int64_t partial_cap, hipStream_t st, bool alone, const float* bny, const float* bnst) {
-  if (bny) {  // dY = dA: the BN backward apply happens in the weight gradient's staging
-    VAD_CHECK(conv3_wgrad_bn_fusable(L), "conv3_wgrad: fused BN apply unsupported");
-    return x3_wgrad_tr(L, dY, src, src_stats, partial, nsplit, partial_cap, alone ? g_tune.wgrad_alone_blocks : 0, st,
-                       bny, bnst);
-  }
+                int* nsplit, int64_t partial_cap, hipStream_t st, bool alone) {
   if (bfc_wgrad_supported(L))
     return bfc_wgrad(L, reinterpret_cast<const __bf16*>(dY), reinterpret_cast<const __bf16*>(src), src_stats, partial,
                      nsplit, partial_cap, st);

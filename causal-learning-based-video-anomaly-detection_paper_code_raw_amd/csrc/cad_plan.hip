@@ -1027,9 +1027,7 @@ struct CadPlanImpl {
       VAD_TRY(bn_bwd_stats(l + 1, np, C, (double)M, P(LY.bn_w[l]), G(LY.bn_w[l]), G(LY.bn_b[l]), G(LY.conv_b[l]), st));
       // dYl was last read by layer l+2's weight gradient
       if (wgs && l + 2 <= 7 && !perl) VAD_HIP(hipStreamWaitEvent(st, ev_wg[l & 1], 0));
-      // layer 0 with the frozen stem: its dY feeds only its weight gradient, which applies the BN backward itself
-      const bool bnf = l == 0 && !stem_grad && conv3_wgrad_bn_fusable(L[0]);
-      if (!bnf) TIMED(L_("bn_bwd_apply", l), bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dYl, nullptr, &nb, st));
+      TIMED(L_("bn_bwd_apply", l), bn_bwd_apply(dA, y[l], stats[l + 1], (int)M, C, dYl, nullptr, &nb, st));
       const float* src = l == 0 ? pool : y[l - 1];
       const float* sst = l == 0 ? pool_stats : stats[l];
       {
@@ -1056,8 +1054,7 @@ struct CadPlanImpl {
         hipStream_t st = wst;
         int ns = 0;
         // (layer 0 with the frozen stem: little runs beside its weight gradient)
-        TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], bnf ? dA : dYl, src, sst, slab, &ns, slab_cap, st,
-                                               l == 0 && !stem_grad, bnf ? y[0] : nullptr, bnf ? stats[1] : nullptr));
+        TIMED(L_("conv_wgrad", l), conv3_wgrad(L[l], dYl, src, sst, slab, &ns, slab_cap, st, l == 0 && !stem_grad));
         TIMED(L_("wgrad_reduce", l), conv3_wgrad_reduce(L[l], slab, ns, nullptr, 0, G(LY.conv_w[l]), nullptr, st));
         if (wgs && !on_main) VAD_HIP(hipEventRecord(ev_wg[l & 1], st));
         // (layer 0: recorded after the join below -- its data-parallel bucket also holds layers 1-3, whose weight

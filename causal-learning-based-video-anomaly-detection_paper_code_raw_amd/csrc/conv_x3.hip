@@ -23,6 +23,7 @@
 namespace vad {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 struct X3Args {
   const float* src;    // NHWC [NF][IH][IW][C]
@@ -60,9 +61,9 @@ struct BnBwdLane {
   }
   // (the y values are loaded for the whole epilogue first: one wait instead of a round trip per pixel)
   template <bool AB>
-  __device__ __forceinline__ void add(float yy, float v, float& s1, float& s2) const {
+  __device__ __forceinline__ void add(float yy, float v, float& s1, float& s2, bool in = true) const {
     const float a = AB ? (float)(__bf16)v : v;
-    const float dz = fmaf(yy, sc, sh) > 0.f ? a : 0.f;
+    const float dz = (in && fmaf(yy, sc, sh) > 0.f) ? a : 0.f;  // (in = false: adds exact zeros)
     s1 += dz;
     s2 = fmaf(dz, (yy - mean) * inv, s2);
   }
@@ -964,10 +965,33 @@ int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float*
 // Stride-2 input gradient on the split-bf16 MFMA (the parity-class scheme of conv_patch.hip's f32 kernel): the four
 // parity classes (ph, pw) of a 16x16 dX tile read one 9x9 dY patch -- class (ph, pw) uses the kernel rows kh with
 // ph + 1 - kh even at dY row offset (ph + 1 - kh) / 2, likewise columns -- so one staged patch and one staged
-// 9-tap weight slice serve 1 + 2 + 2 + 4 taps.  Wave w takes the class-tile half w & 1 (32 class pixels) of two
+// 9-tap weight slice serve 1 + 2 + 2 + 4 taps.  Wave w takes the class-tile half w & 1 (4 x 8 class pixels) of two
 // classes, (1,1)+(0,0) for waves 0-1 and (0,1)+(1,0) for waves 2-3 (5 / 4 taps), for 32*NT input channels.
 // p.src = dY [NF][IH][IW][C = Co], p.w = Wd [N = Ci][9][C], p.out = dX [NF][OH][OW][N].
+//
+// LDS geometry (SQ_LDS_BANK_CONFLICT was 0.27 of the LDS cycles with 9-pixel patch rows): patch row py is stored at
+// LDS row 12 py (12 pixel slots per patch row, 3 unused) and MFMA row m of a wave takes class pixel S2_PERM[m], which
+// puts rows 0 and 2 of its 4 x 8 half on the lanes of one ds_read_b128 group ({0-3, 12-15, 20-27}) and rows 1 and 3
+// on the other: the 16 lanes of a group then address 16 distinct 16-B slots of the 64 banks (LDS row index mod 16 is
+// a bijection for both groups and the 7-slot row pitch is odd), for every tap's uniform (dh, dw) shift.  Staging:
+// every global load goes through a buffer resource at a 32-bit offset computed once per thread (per chunk only + c0),
+// out-of-range pieces at an offset past the buffer's end (zeros, no selects); the patch pieces are assigned so the 8
+// lanes of a ds_write_b128 group store 8 consecutive patch pixels of one channel half.
 // =====================================================================================================
+#ifndef S2_EXP
+#define S2_EXP 1
+#endif
+#if S2_EXP
+__constant__ constexpr int S2_PERM[32] = {0,  1,  2,  3,  8,  9,  10, 11, 12, 13, 14, 15, 4,  5,  6,  7,
+                                          24, 25, 26, 27, 16, 17, 18, 19, 20, 21, 22, 23, 28, 29, 30, 31};
+constexpr int S2_PR = 12;    // LDS pixel slots per patch row
+#else
+__constant__ constexpr int S2_PERM[32] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
+                                          16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31};
+constexpr int S2_PR = 10;
+#endif
+constexpr int S2_DUMMY = 9;  // patch row 0's pixel slot 9: never read, the target of the staging's empty slots
+
 template <int NT, int PC, int NP, int CPH, int CPW>
 __device__ __forceinline__ void dgrad_s2x3_class(f32x16 (&acc)[NT], const __bf16* abase, const __bf16* bbase,
                                                  int WP) {
@@ -977,7 +1001,7 @@ __device__ __forceinline__ void dgrad_s2x3_class(f32x16 (&acc)[NT], const __bf16
 #pragma unroll
     for (int b = 0; b < (CPW ? 2 : 1); ++b) {
       const int kw = CPW ? (b == 0 ? 0 : 2) : 1, dw = (CPW && b == 0) ? 1 : 0;
-      const __bf16* ap = abase + (dh * 9 + dw) * (NP * PC + 8);
+      const __bf16* ap = abase + (dh * S2_PR + dw) * (NP * PC + 8);
       const __bf16* bp = bbase + (kh * 3 + kw) * NP * PC;
 #pragma unroll
       for (int kk = 0; kk < PC / 16; ++kk) {
@@ -998,16 +1022,22 @@ __device__ __forceinline__ void dgrad_s2x3_class(f32x16 (&acc)[NT], const __bf16
   }
 }
 
+constexpr int S2_OOB = 0x7ffffff0;  // a byte offset past every buffer's end: the load returns zeros
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t s2_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
+                                           (int)(bytes < (int64_t)S2_OOB ? bytes : (int64_t)S2_OOB), 0x00020000);
+}
+__device__ __forceinline__ int s2_add(int off, int add) { return off == S2_OOB ? S2_OOB : off + add; }
+
 // W3: the weight slices come pre-split (p.w3, PC == 16, NP == 3): plain 16-B copies instead of the fp32 load + split
 template <int NT, int PC, int NP, bool AB = false, bool W3 = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args p) {
   static_assert(!W3 || (NP == 3 && PC == 16), "pre-split weights: 3 planes of 16-channel slices");
-  static_assert(PC % 16 == 0, "16-deep K steps");
+  static_assert(PC == 16, "16-channel chunks (two 8-channel halves per patch pixel)");
   static_assert(!AB || NP == 1, "bf16 storage with bf16 operands only");
   using TA = act_t<AB>;
-  const TA* src = reinterpret_cast<const TA*>(p.src);
   TA* out = reinterpret_cast<TA*>(p.out);
-  constexpr int NC = 32 * NT, G8 = PC / 8, PROWS = 81;
+  constexpr int NC = 32 * NT, PROWS = 9 * S2_PR;
   constexpr int RP = NP * PC + 8, WP = 9 * NP * PC + 8;
   static_assert(((RP * 2 / 16) & 1) && ((WP * 2 / 16) & 1), "odd 16-B row pitch");
   __shared__ __attribute__((aligned(16))) __bf16 sm[PROWS * RP + NC * WP];
@@ -1020,88 +1050,97 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args
   const int i0 = (trem / p.tiles_w) * 8, j0 = (trem % p.tiles_w) * 8;  // class-grid origin = dY patch origin
   const int n0 = blockIdx.y * NC;
   const int g = wave & 1;  // class-tile rows 4g .. 4g+3
-  const __bf16* abase = patch + ((4 * g + j / 8) * 9 + j % 8) * RP + 8 * h;
+  const int pj = S2_PERM[j];
+  const __bf16* abase = patch + ((4 * g + pj / 8) * S2_PR + pj % 8) * RP + 8 * h;
   const __bf16* bbase = wl + j * WP + 8 * h;
   const int nch = p.C / PC;
 
-  constexpr int PQ = PROWS * G8, PIT = (PQ + 255) / 256;
-  constexpr int WQ = NC * 9 * G8, WIT = (WQ + 255) / 256;
-  constexpr int W3Q = NC * 9 * 6, W3IT = (W3Q + 255) / 256;  // W3: 16-B pieces, 6 per (n, tap) row
-  const int g8 = tid % G8;
-  act_raw4<AB> pv[PIT][2];
-  f32x4 wv[W3 ? 1 : WIT][2];
-  bf16x8 w3v[W3 ? W3IT : 1];
-  bool pok[PIT], wok[W3 ? W3IT : WIT];
-  // unconditional loads from clamped addresses; out-of-range rows are zeroed at stash time (see conv3x3_x3_kernel)
+  // ---- per-thread staging geometry, computed once (a chunk adds its channel offset to the global offsets)
+  // patch pieces: q -> pixel (q / 16) * 8 + q % 8 of the 81, channel half (q / 8) & 1 (176 slots for 162 pieces)
+  constexpr int PIT = 1;
+  constexpr int WQ = NC * 9 * 2, W3Q = NC * 9 * 6;  // fp32 weights: 8-channel halves; W3: 16-B pieces, 6 per row
+  constexpr int WN = ((W3 ? W3Q : WQ) + 255) / 256;
+  const __amdgpu_buffer_rsrc_t src_rs = s2_rsrc(p.src, (int64_t)p.NF * p.IH * p.IW * p.C * (int64_t)sizeof(TA));
+  const __amdgpu_buffer_rsrc_t w_rs =
+      W3 ? s2_rsrc(p.w3, (int64_t)p.N * 9 * p.C * 3 * 2) : s2_rsrc(p.w, (int64_t)p.N * 9 * p.C * 4);
+  // global byte offset (S2_OOB: a zero piece) / LDS element offset (slots past the pieces store into S2_DUMMY, an
+  // unused pixel slot of patch row 0: no branches in the staging)
+  int poff[PIT], plds[PIT];
+#pragma unroll
+  for (int it = 0; it < PIT; ++it) {
+    const int q = tid + it * 256;
+    const int row = (q >> 4) * 8 + (q & 7), half = (q >> 3) & 1;
+    const int y = i0 + row / 9, x = j0 + row % 9;
+    const bool ok = row < 81 && y < p.IH && x < p.IW;
+    poff[it] = ok ? (((img * p.IH + y) * p.IW + x) * p.C + half * 8) * (int)sizeof(TA) : S2_OOB;
+    plds[it] = row < 81 ? ((row / 9) * S2_PR + row % 9) * RP + half * 8 : S2_DUMMY * RP;
+  }
+  int woff[WN], wlds[WN];
+#pragma unroll
+  for (int it = 0; it < WN; ++it) {
+    const int q = tid + it * 256;
+    if constexpr (W3) {
+      const int n = q / 54, t = (q / 6) % 9, jj = q % 6;
+      woff[it] = (q < W3Q && n0 + n < p.N) ? (((n0 + n) * 9 + t) * (p.C / 16) * 48 + jj * 8) * 2 : S2_OOB;
+      wlds[it] = q < W3Q ? PROWS * RP + n * WP + t * NP * PC + jj * 8 : S2_DUMMY * RP;
+    } else {
+      const int n = q / 18, t = (q / 2) % 9, half = q % 2;
+      woff[it] = (q < WQ && n0 + n < p.N) ? (((n0 + n) * 9 + t) * p.C + half * 8) * 4 : S2_OOB;
+      wlds[it] = q < WQ ? PROWS * RP + n * WP + t * NP * PC + half * 8 : S2_DUMMY * RP;
+    }
+  }
+
+  u32x4 pv[PIT][AB ? 1 : 2];
+  u32x4 wv[WN][W3 ? 1 : 2];
   auto fetch = [&](int c0) {
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
-      const int q = tid + it * 256, row = q / G8;
-      const int y = i0 + row / 9, x = j0 + row % 9;
-      pok[it] = q < PQ && y < p.IH && x < p.IW;
-      const TA* s = src + c0 + g8 * 8 + (pok[it] ? (((int64_t)img * p.IH + y) * p.IW + x) * p.C : (int64_t)0);
-      pv[it][0] = act_ld4(s);
-      pv[it][1] = act_ld4(s + 4);
+      const int o = s2_add(poff[it], c0 * (int)sizeof(TA));
+      pv[it][0] = __builtin_amdgcn_raw_buffer_load_b128(src_rs, o, 0, 0);
+      if constexpr (!AB) pv[it][1] = __builtin_amdgcn_raw_buffer_load_b128(src_rs, s2_add(o, 16), 0, 0);
     }
-    if constexpr (W3) {
 #pragma unroll
-      for (int it = 0; it < W3IT; ++it) {
-        const int q = tid + it * 256, n = q / 54, t = (q / 6) % 9, j = q % 6;
-        wok[it] = q < W3Q && n0 + n < p.N;
-        const __bf16* s = p.w3 + (wok[it] ? (((int64_t)(n0 + n) * 9 + t) * (p.C / 16) + c0 / 16) * 48 + j * 8 : 0);
-        w3v[it] = *reinterpret_cast<const bf16x8*>(s);
-      }
-    } else {
-#pragma unroll
-      for (int it = 0; it < WIT; ++it) {
-        const int q = tid + it * 256, n = q / (9 * G8), t = (q / G8) % 9;
-        wok[it] = q < WQ && n0 + n < p.N;
-        const float* s = p.w + c0 + g8 * 8 + (wok[it] ? ((int64_t)(n0 + n) * 9 + t) * p.C : (int64_t)0);
-        wv[it][0] = *reinterpret_cast<const f32x4*>(s);
-        wv[it][1] = *reinterpret_cast<const f32x4*>(s + 4);
+    for (int it = 0; it < WN; ++it) {
+      if constexpr (W3) {
+        wv[it][0] = __builtin_amdgcn_raw_buffer_load_b128(w_rs, s2_add(woff[it], c0 * 6), 0, 0);  // (c0 / 16 x 96 B)
+      } else {
+        const int o = s2_add(woff[it], c0 * 4);
+        wv[it][0] = __builtin_amdgcn_raw_buffer_load_b128(w_rs, o, 0, 0);
+        wv[it][1] = __builtin_amdgcn_raw_buffer_load_b128(w_rs, s2_add(o, 16), 0, 0);
       }
     }
   };
   auto stash = [&]() {
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
-      const int q = tid + it * 256;
-      if (q < PQ) {
-        float v[8];
-        const f32x4 v0 = act_f4(pv[it][0]), v1 = act_f4(pv[it][1]);
+      float v[8];
+      if constexpr (AB) {
+        const bf16x8 b = __builtin_bit_cast(bf16x8, pv[it][0]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (float)b[e];
+      } else {
+        const f32x4 v0 = __builtin_bit_cast(f32x4, pv[it][0]), v1 = __builtin_bit_cast(f32x4, pv[it][1]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = pok[it] ? v0[e] : 0.f;
-          v[4 + e] = pok[it] ? v1[e] : 0.f;
+          v[e] = v0[e];
+          v[4 + e] = v1[e];
         }
-        put_planes<NP>(patch + (q / G8) * RP + g8 * 8, PC, v, false);
       }
+      put_planes<NP>(sm + plds[it], PC, v, false);
     }
-    if constexpr (W3) {
 #pragma unroll
-      for (int it = 0; it < W3IT; ++it) {
-        const int q = tid + it * 256;
-        if (q < W3Q) {
-          const int n = q / 54, t = (q / 6) % 9, j = q % 6;
-          bf16x8 v = w3v[it];
-          if (!wok[it]) v = bf16x8{};
-          *reinterpret_cast<bf16x8*>(wl + n * WP + t * NP * PC + j * 8) = v;
+    for (int it = 0; it < WN; ++it) {
+      if constexpr (W3) {
+        *reinterpret_cast<u32x4*>(sm + wlds[it]) = wv[it][0];
+      } else {
+        float v[8];
+        const f32x4 v0 = __builtin_bit_cast(f32x4, wv[it][0]), v1 = __builtin_bit_cast(f32x4, wv[it][1]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = v0[e];
+          v[4 + e] = v1[e];
         }
-      }
-    } else {
-#pragma unroll
-      for (int it = 0; it < WIT; ++it) {
-        const int q = tid + it * 256;
-        if (q < WQ) {
-          const int n = q / (9 * G8), t = (q / G8) % 9;
-          float v[8];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] = wok[it] ? wv[it][0][e] : 0.f;
-            v[4 + e] = wok[it] ? wv[it][1][e] : 0.f;
-          }
-          put_planes<NP>(wl + n * WP + t * NP * PC + g8 * 8, PC, v, false);
-        }
+        put_planes<NP>(sm + wlds[it], PC, v, false);
       }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // (see conv3x3_x3_kernel's stash)
@@ -1136,33 +1175,52 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dgrad_s2x3_kernel(const X3Args
     s1[nt] = s2[nt] = 0.f;
     if (bnb) bl[nt].load(p.bnst, p.N, min(n0 + nt * 32 + j, p.N - 1));
   }
-  // (two passes, one per parity class: the y values of a pass are loaded first, one wait instead of one per pixel)
+  // Two passes, one per parity class.  Branch-free: every store / y load goes through a buffer resource, a pixel
+  // outside dX at an offset past the buffer's end (the store is dropped, the load reads 0 and the BN sums mask it).
+  // MFMA row m of lane half h is class pixel (cy, cx) = S2_PERM[m] (compile-time per r and h: one select each), at
+  // element offset base + cy * 2 OW N + cx * 2 N (32-bit: the host checks dX is below 2 GB).
+  const __amdgpu_buffer_rsrc_t out_rs = s2_rsrc(p.out, (int64_t)p.NF * p.OH * p.OW * p.N * (int64_t)sizeof(TA));
+  const __amdgpu_buffer_rsrc_t y_rs = s2_rsrc(p.bny, bnb ? (int64_t)p.NF * p.OH * p.OW * p.N * (int64_t)sizeof(TA) : 0);
+  const int N2 = 2 * p.N, OWN2 = 2 * p.OW * p.N;
 #pragma unroll
   for (int cls = 0; cls < 2; ++cls) {
     const int ph = cls ? ph1 : ph0, pw = cls ? pw1 : pw0;
+    const int y0 = 2 * (i0 + 4 * g) + ph, x0 = 2 * j0 + pw;
+    const int ylim = p.OH - y0, xlim = p.OW - x0;  // class pixel (cy, cx) lies in dX iff 2 cy < ylim, 2 cx < xlim
+    const int base = ((img * p.OH + y0) * p.OW + x0) * p.N + n0 + j;
+    int off[16][NT];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m0 = (r & 3) + 8 * (r >> 2);  // C row of lane half 0 (half 1: m0 + 4)
+      const int cy = h ? S2_PERM[m0 + 4] / 8 : S2_PERM[m0] / 8, cx = h ? S2_PERM[m0 + 4] % 8 : S2_PERM[m0] % 8;
+      const bool ok = 2 * cy < ylim && 2 * cx < xlim;
+      const int o = base + cy * OWN2 + cx * N2;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        off[r][nt] = (ok && n0 + nt * 32 + j < p.N) ? (o + nt * 32) * (int)sizeof(TA) : S2_OOB;
+    }
     float yb[16][NT];
     if (bnb) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int pm = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int yy = 2 * (i0 + 4 * g + pm / 8) + ph, xx = 2 * (j0 + pm % 8) + pw;
-        const bool ok = yy < p.OH && xx < p.OW;
-        const int64_t base = ok ? (((int64_t)img * p.OH + yy) * p.OW + xx) * p.N : 0;
+      for (int r = 0; r < 16; ++r)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) yb[r][nt] = BnBwdLane::ld<AB>(p.bny, base + min(n0 + nt * 32 + j, p.N - 1));
-      }
+        for (int nt = 0; nt < NT; ++nt) {
+          if constexpr (AB)
+            yb[r][nt] = (float)__builtin_bit_cast(__bf16, __builtin_amdgcn_raw_buffer_load_b16(y_rs, off[r][nt], 0, 0));
+          else
+            yb[r][nt] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(y_rs, off[r][nt], 0, 0));
+        }
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int pm = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int yy = 2 * (i0 + 4 * g + pm / 8) + ph, xx = 2 * (j0 + pm % 8) + pw;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        const int col = n0 + nt * 32 + j;
-        if (col >= p.N || yy >= p.OH || xx >= p.OW) continue;
         const float v = cls ? acc1[nt][r] : acc0[nt][r];
-        act_st(out + (((int64_t)img * p.OH + yy) * p.OW + xx) * p.N + col, v);
-        if (bnb) bl[nt].template add<AB>(yb[r][nt], v, s1[nt], s2[nt]);
+        if constexpr (AB)
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)v), out_rs, off[r][nt], 0, 0);
+        else
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), out_rs, off[r][nt], 0, 0);
+        if (bnb) bl[nt].template add<AB>(yb[r][nt], v, s1[nt], s2[nt], off[r][nt] != S2_OOB);
       }
     }
   }
@@ -1205,6 +1263,9 @@ bool conv3_dgrad_w3_wanted(const Conv3Layer& L) {
 int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, float* dX, hipStream_t st,
                       const BnBwdFuse* f, const __bf16* w3) {
   VAD_CHECK(conv3_x3_dgrad_s2_supported(L), "conv3_x3_dgrad_s2: unsupported layer");
+  VAD_CHECK((int64_t)L.NF * L.IH * L.IW * L.Ci * 4 < 0x7ffffff0ll && (int64_t)L.NF * L.OH * L.OW * L.Co * 4 < 0x7ffffff0ll &&
+                (int64_t)L.Ci * 9 * L.Co * 6 < 0x7ffffff0ll,
+            "conv3_x3_dgrad_s2: 32-bit offsets (dX, dY and the weight image below 2 GB)");
   X3Args a{};
   a.src = dY;
   a.w = wd;
@@ -1255,7 +1316,6 @@ int conv3_x3_dgrad_s2(const Conv3Layer& L, const float* dY, const float* wd, flo
 // accumulators; the 4 waves are combined in a fixed order at the end ((0+2) + (1+3)), and the block's sum lands
 // in slab blockIdx.z of the [S][co][t*Ci + ci] split-K layout that conv3_wgrad_reduce consumes.
 // =====================================================================================================
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 struct WgX3Args {
   const float* dY;     // [NF][OH][OW][Co]

@@ -63,15 +63,12 @@ struct TrwArgs {
   const float* scale;  // BN + ReLU on load (nullable)
   const float* shift;
   float* slab;         // [S][Co][9 Ci]
-  const float* bny;    // BNA: dY is the BN backward of dA (= the dY pointer) over y = bny with BN state bnst
-  const float* bnst;   //      [mean | invstd | scale | shift | k | mean dz | mean dz xhat] x Co (bn_bwd_apply's)
   int NF, IH, IW, Ci, OH, OW, Co;
   int tiles_h, tiles_w, ntiles;
   int dy_bytes, x_bytes;  // buffer extents (< 2^31)
 };
 
-// BNA: the BatchNorm backward apply of the layer (bn_bwd_apply's expression, bit-identical) folded into the dY staging
-template <int S, int NI, int TH, int TW, int NCO, bool BNA = false, bool PFT = false>
+template <int S, int NI, int TH, int TW, int NCO, bool PFT = false>
 __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
   constexpr int TPX = NI * TH * TW, KS = TPX / 32, KSW = NCO == 2 ? KS : KS / 2;
   static_assert(TW % 8 == 0 && TPX % 32 == 0 && KS % (3 - NCO) == 0 && (NCO == 1 || NCO == 2), "whole K steps");
@@ -84,7 +81,6 @@ __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
   __shared__ __attribute__((aligned(16))) __bf16 sm[6 * (NCO * YH + XH)];
   __bf16* const ys = sm;                  // [co tile][half][plane][TPX][16]
   __bf16* const xs = sm + 6 * NCO * YH;   // [half][plane][PROWS + 1][16]
-  __shared__ __attribute__((aligned(16))) float bnc[BNA ? 7 * 32 * NCO : 4];  // the block's BN state columns
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;  // transposed-read roles
   const int co0 = blockIdx.x * 32 * NCO, ci0 = blockIdx.y * 32;
@@ -132,14 +128,8 @@ __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
   constexpr int OOB = 0x7ffffff0;
   const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void*)p.dY, (short)0, p.dy_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.src, (short)0, p.x_bytes, 0x00020000);
-  if constexpr (BNA) {
-    for (int q = tid; q < 7 * 32 * NCO; q += 256) bnc[q] = p.bnst[(q / (32 * NCO)) * p.Co + co0 + q % (32 * NCO)];
-    __syncthreads();
-  }
-  const __amdgpu_buffer_rsrc_t rb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(BNA ? p.bny : p.dY), (short)0, p.dy_bytes, 0x00020000);
-  f32x4 yv[YIT], xv[XIT], bv[BNA ? YIT : 1];
-  int xmask = 0, ymask = 0;  // (ymask, BNA: the dY pieces inside the frames -- the BN apply of a padding zero is not 0)
+  f32x4 yv[YIT], xv[XIT];
+  int xmask = 0;
   auto fetch = [&](int tile) {
     const int img0 = (tile / tiles_per_img) * NI, tr = tile % tiles_per_img;
     const int y0 = (tr / p.tiles_w) * TH, x0 = (tr % p.tiles_w) * TW;
@@ -152,10 +142,6 @@ __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
       const int ok = (img0 + mi < p.NF) & (y0 + py < p.OH) & (x0 + px < p.OW);
       const int off = ybase + ((((mi * p.OH + py) * p.OW + px) * p.Co + cg * 32) << 2);
       yv[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, ok ? off : OOB, 0, 0));
-      if constexpr (BNA) {
-        bv[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? off : OOB, 0, 0));
-        ymask = it == 0 ? ok : (ymask | (ok << it));
-      }
     }
     xmask = 0;
 #pragma unroll
@@ -178,25 +164,6 @@ __global__ __launch_bounds__(256, 2) void x3_wgrad_tr_kernel(const TrwArgs p) {
       const int q = ltid + it * 256, cg = q / (TPX * 8), m = (q % (TPX * 8)) >> 3;
       bfv4w a, b, c;
       f32x4 dy = yv[it];
-      if constexpr (BNA) {  // dY = k (dz - mean dz - xhat mean(dz xhat)), dz = dA where the forward ReLU passed
-        const int cc = cg * 32 + c4 * 4;
-        const f32x4 mean = *reinterpret_cast<const f32x4*>(bnc + 0 * 32 * NCO + cc);
-        const f32x4 inv = *reinterpret_cast<const f32x4*>(bnc + 1 * 32 * NCO + cc);
-        const f32x4 bsc = *reinterpret_cast<const f32x4*>(bnc + 2 * 32 * NCO + cc);
-        const f32x4 bsh = *reinterpret_cast<const f32x4*>(bnc + 3 * 32 * NCO + cc);
-        const f32x4 kk = *reinterpret_cast<const f32x4*>(bnc + 4 * 32 * NCO + cc);
-        const f32x4 mdz = *reinterpret_cast<const f32x4*>(bnc + 5 * 32 * NCO + cc);
-        const f32x4 mdzx = *reinterpret_cast<const f32x4*>(bnc + 6 * 32 * NCO + cc);
-        const bool ok = (ymask >> it) & 1;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float yy = bv[it][e];
-          const float dz = fmaf(yy, bsc[e], bsh[e]) > 0.f ? dy[e] : 0.f;
-          const float xh = (yy - mean[e]) * inv[e];
-          const float o = kk[e] * (dz - mdz[e] - xh * mdzx[e]);
-          dy[e] = ok ? o : 0.f;
-        }
-      }
       split4(dy, a, b, c);
       __bf16* d = ys + (cg * 2 + chal) * 3 * YH + m * 16 + ccol;
       *reinterpret_cast<bfv4w*>(d) = a;
@@ -339,7 +306,7 @@ bool x3_wgrad_tr_supported(const Conv3Layer& L) {
 int g_wgrad_tr_pft = 0;  // knob "conv_wgrad_tr_pft": the next tap's input fragments read before this tap's MFMAs (off:
                          // config-2 step 1.696 ms off vs 1.72-1.74 on, profiles/r05_prefetch_ab.json)
 
-template <int S, int NI, int TH, int TW, int NCO, bool BNA = false>
+template <int S, int NI, int TH, int TW, int NCO>
 static int trw_launch(TrwArgs a, int target_blocks, int64_t partial_cap, hipStream_t st, int* nsplit) {
   a.tiles_h = (int)cdiv(a.OH, TH);
   a.tiles_w = (int)cdiv(a.OW, TW);
@@ -351,33 +318,22 @@ static int trw_launch(TrwArgs a, int target_blocks, int64_t partial_cap, hipStre
   bool launched = false;
   if constexpr (S == 1) {
     if (g_wgrad_tr_pft) {
-      VAD_KLAUNCH((x3_wgrad_tr_kernel<S, NI, TH, TW, NCO, BNA, true>), dim3(a.Co / (32 * NCO), a.Ci / 32, (unsigned)z),
+      VAD_KLAUNCH((x3_wgrad_tr_kernel<S, NI, TH, TW, NCO, true>), dim3(a.Co / (32 * NCO), a.Ci / 32, (unsigned)z),
                   dim3(256), 0, st, a);
       launched = true;
     }
   }
   if (!launched)
-    VAD_KLAUNCH((x3_wgrad_tr_kernel<S, NI, TH, TW, NCO, BNA, false>), dim3(a.Co / (32 * NCO), a.Ci / 32, (unsigned)z),
+    VAD_KLAUNCH((x3_wgrad_tr_kernel<S, NI, TH, TW, NCO, false>), dim3(a.Co / (32 * NCO), a.Ci / 32, (unsigned)z),
                 dim3(256), 0, st, a);
   VAD_LAUNCH_CHECK();
   *nsplit = (int)z;
   return 0;
 }
 
-// knob "conv_wgrad_bn_fused": layer 0's BN backward apply inside its weight gradient.  Off: measured neutral to
-// slightly slower at config 2 (the fused weight gradient 125 us against 61 + 54 for the two passes,
-// profiles/r04_wgrad_bn_fused_ab.json) -- the extra loads and VALU land in a kernel that is issue-bound already
-int g_wgrad_bn_fused = 0;
-
-bool x3_wgrad_tr_bn_supported(const Conv3Layer& L) {
-  return g_wgrad_bn_fused && x3_wgrad_tr_supported(L) && L.stride == 1 && L.Co % 64 != 0;
-}
-
 int x3_wgrad_tr(const Conv3Layer& L, const float* dY, const float* src, const float* src_stats, float* slab,
-                int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st, const float* bny,
-                const float* bnst) {
+                int* nsplit, int64_t partial_cap, int target_blocks, hipStream_t st) {
   VAD_CHECK(x3_wgrad_tr_supported(L), "x3_wgrad_tr: unsupported layer");
-  VAD_CHECK(!bny || x3_wgrad_tr_bn_supported(L), "x3_wgrad_tr: fused BN backward on an unsupported layer");
   VAD_CHECK(partial_cap >= (int64_t)L.Co * 9 * L.Ci, "x3_wgrad_tr: slab capacity below one split");
   TrwArgs a{};
   a.dY = dY;
@@ -385,8 +341,6 @@ int x3_wgrad_tr(const Conv3Layer& L, const float* dY, const float* src, const fl
   a.scale = src_stats ? src_stats + 2 * L.Ci : nullptr;
   a.shift = src_stats ? src_stats + 3 * L.Ci : nullptr;
   a.slab = slab;
-  a.bny = bny;
-  a.bnst = bnst;
   a.NF = L.NF; a.IH = L.IH; a.IW = L.IW; a.Ci = L.Ci; a.OH = L.OH; a.OW = L.OW; a.Co = L.Co;
   a.dy_bytes = (int)((int64_t)L.NF * L.OH * L.OW * L.Co * 4);
   a.x_bytes = (int)((int64_t)L.NF * L.IH * L.IW * L.Ci * 4);
@@ -400,8 +354,7 @@ int x3_wgrad_tr(const Conv3Layer& L, const float* dY, const float* src, const fl
     return c64 ? trw_launch<2, 1, 4, 16, 2>(a, tb, partial_cap, st, nsplit)
                : trw_launch<2, 1, 4, 16, 1>(a, tb, partial_cap, st, nsplit);
   }
-  if (!c64) return bny ? trw_launch<1, 1, 8, 16, 1, true>(a, tb, partial_cap, st, nsplit)
-                       : trw_launch<1, 1, 8, 16, 1>(a, tb, partial_cap, st, nsplit);
+  if (!c64) return trw_launch<1, 1, 8, 16, 1>(a, tb, partial_cap, st, nsplit);
   if (L.OW <= 8 && L.OH <= 8) return trw_launch<1, 1, 8, 8, 2>(a, tb, partial_cap, st, nsplit);
   return trw_launch<1, 1, 4, 16, 2>(a, tb, partial_cap, st, nsplit);
 }

@@ -204,6 +204,9 @@ int vad_a2_bind(vad_a2_plan* plan, void* workspace, float* params, float* grads,
  * consistency, structure, edge_count, sparsity_ratio, grad norm (optimizer), status (0 NaN skip, 2 stepped) */
 int vad_a2_forward(vad_a2_plan* plan, const float* x, int training, uint64_t seed, uint64_t step, int64_t clip0,
                    int with_loss, float* scores, float* adj, float* features, float* losses, void* stream);
+/* "borrow_input" 1: the next forwards read x in place and the backward reads it again (the caller keeps it unchanged
+ * until then, as the fused train step does); 0 (default): the forward copies x for conv3d_1's weight gradient */
+int vad_a2_set_option(vad_a2_plan* plan, const char* key, int64_t value);
 /* compute_improved_loss alone, on the last forward's scores / adjacency (pseudo-labels keyed by seed/step/clip0);
  * vad_a2_loss_grads copies d total / d scores (B,) and d total / d adj (B,16,16) of that loss */
 int vad_a2_loss(vad_a2_plan* plan, uint64_t seed, uint64_t step, int64_t clip0, float* losses, void* stream);

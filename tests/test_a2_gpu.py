@@ -82,3 +82,47 @@ def test_a2_autograd_loss_path_matches_oracle():
         gr, gref = p.grad.cpu().numpy(), leaves[n].grad.numpy()
         scale = float(np.abs(gref).max()) + 1e-12
         np.testing.assert_allclose(gr, gref, rtol=2e-3, atol=2e-4 * scale, err_msg=n)
+
+
+def test_a2_direct_and_im2col_paths_agree():
+    """conv3d_1 direct on LDS halo tiles + conv3d_2 / _3 as implicit GEMMs (knob a2_direct = 1, the default) against
+    the im2col + GEMM path (a2_direct = 0, latched at plan creation): the train step's loss and every gradient tensor
+    agree to float rounding."""
+    from vad_amd import _native as nat
+    case = dict(B=6, T=8, H=48, W=40, seed=26, step=1, ckpt=False)
+    x = ao.synth_clips(26, 1, 0, 6, 8, 48, 40)
+    res = []
+    for d in (1, 0):
+        nat.check(nat.lib().vad_set_tuning(b"a2_direct", d))
+        try:
+            vad = _vad(case)
+            avg, _ = vad.train_epoch_improved([(x, ao.synth_labels(0, 6))])
+            e = vad.model._engine
+            res.append((avg, {n: e.grads[off:off + k].cpu().double() for n, off, k in e.slots}))
+        finally:
+            nat.check(nat.lib().vad_set_tuning(b"a2_direct", 1))
+    assert res[0][0] == pytest.approx(res[1][0], rel=1e-6)
+    for n, g0 in res[0][1].items():
+        g1 = res[1][1][n]
+        assert float((g0 - g1).norm()) <= 1e-5 * float(g1.norm()) + 1e-12, n
+
+
+def test_a2_head_per_clip_launch_is_bit_identical():
+    """The head forward / backward as one block per clip (knob a2_head_clip = 1, the default) against one launch per
+    Linear layer (0): the same per-output arithmetic in the same order, so the step's losses, outputs and every
+    gradient are bit-identical."""
+    from vad_amd import _native as nat
+    case = dict(B=6, T=8, H=48, W=40, seed=27, step=2, ckpt=True)
+    x = ao.synth_clips(27, 2, 0, 6, 8, 48, 40)
+    res = []
+    for v in (1, 0):
+        nat.check(nat.lib().vad_set_tuning(b"a2_head_clip", v))
+        try:
+            vad = _vad(case)
+            avg, comps = vad.train_epoch_improved([(x, ao.synth_labels(0, 6))])
+            e = vad.model._engine
+            res.append((avg, comps, e.cur.scores.cpu().clone(), e.grads.cpu().clone()))
+        finally:
+            nat.check(nat.lib().vad_set_tuning(b"a2_head_clip", 1))
+    assert res[0][0] == res[1][0] and res[0][1] == res[1][1]
+    assert torch.equal(res[0][2], res[1][2]) and torch.equal(res[0][3], res[1][3])

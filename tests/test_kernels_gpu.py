@@ -386,3 +386,30 @@ def test_conv3x3_bf16_native_matches_rounded_fp64(NF, Ci, Co, IH, IW, s):
     finally:
         lib.vad_set_tuning(b"act_bf16", 0)
         lib.vad_set_tuning(b"conv_bf16", 0)
+
+
+@pytest.mark.parametrize("NF,Ci,Co,IH,IW,s", [(8, 32, 32, 57, 57, 1), (6, 128, 128, 15, 15, 1), (8, 32, 64, 57, 57, 2),
+                                              (8, 128, 256, 15, 15, 2)])
+def test_conv3x3_wgrad_tr_prefetch_is_bit_identical(NF, Ci, Co, IH, IW, s):
+    """The transposed-read weight gradient with the next tap's input fragments read before this tap's MFMAs (knob
+    conv_wgrad_tr_pft = 1, off by default) computes the same products in the same order: bit-identical dW."""
+    nat = _lib()
+    _wgrad_path(nat, 3)
+    g = torch.Generator().manual_seed(NF + Ci + Co + IH + s)
+    d = torch.device("cuda")
+    xh = torch.randn(NF, IH, IW, Ci, generator=g).to(d)
+    OH, OW = (IH - 1) // s + 1, (IW - 1) // s + 1
+    dyh = torch.randn(NF, OH, OW, Co, generator=g).to(d)
+    part = torch.empty(1 << 24, device=d)
+    out = []
+    for pft in (0, 1):
+        nat.check(nat.lib().vad_set_tuning(b"conv_wgrad_tr_pft", pft))
+        try:
+            dW = torch.empty(Co, Ci, 3, 3, device=d)
+            nat.check(nat.lib().vad_conv3x3_wgrad(xh.data_ptr(), dyh.data_ptr(), NF, Ci, IH, IW, Co, s, dW.data_ptr(),
+                                                  part.data_ptr(), part.numel(), nat.stream_of(d)))
+            torch.cuda.synchronize()
+            out.append(dW.cpu())
+        finally:
+            nat.check(nat.lib().vad_set_tuning(b"conv_wgrad_tr_pft", 0))
+    assert torch.equal(out[0], out[1])

@@ -5,7 +5,7 @@ TAG=$1; shift
 PKG=causal-learning-based-video-anomaly-detection_paper_code_raw_amd
 mkdir -p gpurun_out
 for rep in 1 2; do
-  for v in A B; do
+  for v in ${VARIANTS:-A B}; do
     cp ab/libvadhip_$v.so $PKG/libvadhip.so || exit 1
     timeout -k 10 120 python tools/r6/conv_standalone.py --tag $v "$@" >> gpurun_out/${TAG}_standalone.jsonl 2>> gpurun_out/${TAG}_standalone.err || exit 1
   done
