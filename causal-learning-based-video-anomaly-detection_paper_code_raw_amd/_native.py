@@ -145,7 +145,10 @@ def lib():
         raise RuntimeError(f"libvadhip.so is not built ({LIB_PATH}); run __graft_entry__.build()")
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
-        fn = getattr(L, name)
+        try:
+            fn = getattr(L, name)
+        except AttributeError:  # (an older build, e.g. an A/B baseline: calling the entry point raises then)
+            continue
         fn.restype = res
         fn.argtypes = args
     if L.vad_abi_version() != 1:

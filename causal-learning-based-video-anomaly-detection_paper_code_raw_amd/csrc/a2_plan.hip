@@ -945,19 +945,21 @@ struct A2PlanImpl {
     }
     VAD_TRY(dense_wgrad(dfeat, B, 16, pooled, 4096, G(S_FCW), G(S_FCB), scratch, scratch_floats, nullptr, st));
     VAD_TRY(dense_dgrad(dfeat, B, 16, P(S_FCW), 4096, dpooled, nullptr, 1.f, nullptr, st));
-    VAD_TRY(adaptive_avgpool3d_bwd(dpooled, g[2].out(), 4, 4, 4, dA, st));
+    // (direct: each ReLU backward is fused into the producer of its gradient -- the average-pool backward for
+    // conv3d_3, the parity-class input gradients for conv3d_2 / conv3d_1 -- instead of a relu_gate pass)
+    VAD_TRY(adaptive_avgpool3d_bwd(dpooled, g[2].out(), 4, 4, 4, dA, st, direct ? y[2] : nullptr));
     float* cur = dA;  // (direct: the input gradients ping-pong between dA and dA2)
     for (int s3 = 2; s3 >= 0; --s3) {
       const int64_t rows = g[s3].rows();
       float* const dg = cur;  // the gradient w.r.t. this stage's output (then its pre-activation)
-      VAD_TRY(relu_gate(dg, y[s3], rows * A2_CO[s3], st));
+      if (!direct) VAD_TRY(relu_gate(dg, y[s3], rows * A2_CO[s3], st));
       if (direct && s3 > 0) {  // conv3d_2 / conv3d_3 on the implicit GEMMs
         const Vol5& in = g[s3].in;
         float* nxt = dg == dA ? dA2 : dA;
         VAD_TRY(col_sum(dg, rows, A2_CO[s3], G(2 * s3 + 1), reinterpret_cast<double*>(scratch), st));
         VAD_TRY(conv3s2_wgrad(dg, A2_CO[s3], y[s3 - 1], in.C, B, in.D, in.H, in.W, G(2 * s3), scratch, scratch_floats,
                               1024, st));
-        VAD_TRY(conv3s2_dgrad(dg, B, A2_CO[s3], wc3[s3], in.C, nxt, in.D, in.H, in.W, st));
+        VAD_TRY(conv3s2_dgrad(dg, B, A2_CO[s3], wc3[s3], in.C, nxt, in.D, in.H, in.W, st, y[s3 - 1]));
         cur = nxt;
         continue;
       }

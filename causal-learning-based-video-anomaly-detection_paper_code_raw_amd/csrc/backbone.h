@@ -229,7 +229,7 @@ int conv3s2_prep(const float* w, int Co, int Ci, float* wk, float* wc, hipStream
 int conv3s2_fwd(const float* src, int NF, int D, int H, int W, int C, const float* wk, const float* bias, int N,
                 int relu, float* out, hipStream_t st);
 int conv3s2_dgrad(const float* dy, int NF, int Co, const float* wc, int Ci, float* dx, int D, int H, int W,
-                  hipStream_t st);
+                  hipStream_t st, const float* gate = nullptr);
 int conv3s2_wgrad(const float* dy, int Co, const float* src, int Ci, int NF, int D, int H, int W, float* dW,
                   float* part, int64_t part_cap, int target_blocks, hipStream_t st);
 // scratch: 256 * N doubles

@@ -1925,7 +1925,10 @@ int conv4_fwd(const float* src, int NF, int H, int W, int C, const float* wk, co
 
 struct EpiConv3DgradCls {  // EpiConv3Dgrad for the class-batched GEMM: class = blockIdx.z, its own grid
   static constexpr int SCRATCH = 0;
-  struct Params { float* dst; int imgs; int GD[8], GA[8], GB[8]; int DD, DH, DW, C; const float* bias; };
+  struct Params {
+    float* dst; int imgs; int GD[8], GA[8], GB[8]; int DD, DH, DW, C; const float* bias;
+    const float* gate;  // nullable, dst's layout: dst = 0 where !(gate > 0) (the producing ReLU's backward, fused)
+  };
   template <class Cfg>
   static __device__ void apply(const Params& P, f32x16 (&acc)[Cfg::TM][Cfg::TN], int m0, int n0, int wm, int wn,
                                int lane, int, int N, float*) {
@@ -1945,7 +1948,10 @@ struct EpiConv3DgradCls {  // EpiConv3Dgrad for the class-batched GEMM: class = 
 #pragma unroll
         for (int j = 0; j < Cfg::TN; ++j) {
           const int col = n0 + acc_col<Cfg>(wn, j, lane);
-          if (col < N) P.dst[base + col] = acc[i][j][r] + (P.bias ? P.bias[col] : 0.f);
+          if (col < N) {
+            const float v = acc[i][j][r] + (P.bias ? P.bias[col] : 0.f);
+            P.dst[base + col] = (P.gate && !(P.gate[base + col] > 0.f)) ? 0.f : v;
+          }
         }
       }
   }
@@ -2394,7 +2400,7 @@ struct EpiConv3Dgrad {  // scatter the rows of a parity-class grid to the NDHWC 
 };
 
 int conv3s2_dgrad(const float* dy, int NF, int Co, const float* wc, int Ci, float* dx, int D, int H, int W,
-                  hipStream_t st) {
+                  hipStream_t st, const float* gate) {
   VAD_CHECK(Co % 4 == 0, "conv3s2_dgrad: Co % 4 == 0");
   const int OD = (D - 1) / 2 + 1, OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
   // the 8 parity classes in one launch (blockIdx.z = class; K = 8 taps x Co, zero past a class's own taps)
@@ -2402,7 +2408,7 @@ int conv3s2_dgrad(const float* dy, int NF, int Co, const float* wc, int Ci, floa
   g.imgs = NF; g.SD = OD; g.SH = OH; g.SW = OW; g.C = Co;
   typename DenseKCz<64>::Params pb0{};
   EpiConv3DgradCls::Params pe{};
-  pe.dst = dx; pe.imgs = NF; pe.DD = D; pe.DH = H; pe.DW = W; pe.C = Ci;
+  pe.dst = dx; pe.imgs = NF; pe.DD = D; pe.DH = H; pe.DW = W; pe.C = Ci; pe.gate = gate;
   int64_t off = 0;
   int Mmax = 0;
   for (int cls = 0; cls < 8; ++cls) {

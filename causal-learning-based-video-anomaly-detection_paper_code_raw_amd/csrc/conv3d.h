@@ -57,7 +57,9 @@ int maxpool3d_bwd(const float* y, const float* stats, int relu, const Vol5& v, i
 int adaptive_avgpool3d_fwd(const float* x, const float* stats, int relu, const Vol5& v, int OD, int OH, int OW,
                            float* out, hipStream_t st);
 // dx (NDHWC) = backward of the average (act' is NOT applied: callers route through their ReLU/BN backward)
-int adaptive_avgpool3d_bwd(const float* dout, const Vol5& v, int OD, int OH, int OW, float* dx, hipStream_t st);
+// gate (nullable, dx's layout): dx = 0 where !(gate > 0) -- the backward of a ReLU whose output is gate, fused
+int adaptive_avgpool3d_bwd(const float* dout, const Vol5& v, int OD, int OH, int OW, float* dx, hipStream_t st,
+                           const float* gate = nullptr);
 
 // Conv3d k3 p1 s1 on NDHWC volumes (B clips x D slices x H x W x C) with split-bf16 MFMA (fp32-class numerics,
 // conv_x3.hip): w3 = weights as [kd][N][kh*3+kw][C] (conv3d_prep_w3), out = conv + bias (no activation), NDHWC

@@ -315,7 +315,8 @@ int adaptive_avgpool3d_fwd(const float* x, const float* stats, int relu, const V
 }
 
 __global__ __launch_bounds__(256) void adaptive_avgpool3d_bwd_kernel(const float* __restrict__ dout, Vol5 v, int OD,
-                                                                     int OH, int OW, float* __restrict__ dx) {
+                                                                     int OH, int OW, float* __restrict__ dx,
+                                                                     const float* __restrict__ gate) {
   const int C = v.C, per = OD * OH * OW;
   const int64_t total = v.numel();
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
@@ -342,15 +343,16 @@ __global__ __launch_bounds__(256) void adaptive_avgpool3d_bwd_kernel(const float
         }
       }
     }
-    dx[i] = g;
+    dx[i] = (gate && !(gate[i] > 0.f)) ? 0.f : g;  // (gate: the ReLU backward of gate = y fused)
   }
 }
 
-int adaptive_avgpool3d_bwd(const float* dout, const Vol5& v, int OD, int OH, int OW, float* dx, hipStream_t st) {
+int adaptive_avgpool3d_bwd(const float* dout, const Vol5& v, int OD, int OH, int OW, float* dx, hipStream_t st,
+                           const float* gate) {
   const int64_t total = v.numel();
   if (total == 0) return 0;
   hipLaunchKernelGGL(adaptive_avgpool3d_bwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 16384)),
-                     dim3(256), 0, st, dout, v, OD, OH, OW, dx);
+                     dim3(256), 0, st, dout, v, OD, OH, OW, dx, gate);
   VAD_LAUNCH_CHECK();
   return 0;
 }

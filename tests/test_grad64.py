@@ -80,6 +80,11 @@ AE_BENCH = dict(name="bench_b32t16", B=32, T=16, seed=50, lr=1e-5, labels=[[0] *
 
 @pytest.mark.parametrize("case", AE_CASES + [AE_BENCH], ids=[c["name"] for c in AE_CASES] + ["bench_b32t16"])
 def test_ae_first_step_grads_match_float64(case):
+    ae_step_vs_float64(case)
+
+
+def ae_step_vs_float64(case):
+    """cad1's first train step on the device vs the float64 step pinned to the device's LeakyReLU decisions."""
     from vad_amd.ae import AeTrainer
     model = make_ae_model(case)
     params, bufs, _ = ae.split_state(model.state_dict())
