@@ -321,6 +321,7 @@ __global__ __launch_bounds__(256) void a2_dadj_kernel(A2HeadArgs a) {
   a.d_adj[idx] = g;
 }
 
+
 struct A2HeadBwdArgs {
   A2HeadArgs f;
   const float* d_s;    // [B]

@@ -978,18 +978,9 @@ int conv3_x3_dgrad(const Conv3Layer& L, const float* dY, const float* wd, float*
 // out-of-range pieces at an offset past the buffer's end (zeros, no selects); the patch pieces are assigned so the 8
 // lanes of a ds_write_b128 group store 8 consecutive patch pixels of one channel half.
 // =====================================================================================================
-#ifndef S2_EXP
-#define S2_EXP 1
-#endif
-#if S2_EXP
 __constant__ constexpr int S2_PERM[32] = {0,  1,  2,  3,  8,  9,  10, 11, 12, 13, 14, 15, 4,  5,  6,  7,
                                           24, 25, 26, 27, 16, 17, 18, 19, 20, 21, 22, 23, 28, 29, 30, 31};
 constexpr int S2_PR = 12;    // LDS pixel slots per patch row
-#else
-__constant__ constexpr int S2_PERM[32] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
-                                          16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31};
-constexpr int S2_PR = 10;
-#endif
 constexpr int S2_DUMMY = 9;  // patch row 0's pixel slot 9: never read, the target of the staging's empty slots
 
 template <int NT, int PC, int NP, int CPH, int CPW>

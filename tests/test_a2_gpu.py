@@ -110,7 +110,8 @@ def test_a2_direct_and_im2col_paths_agree():
 def test_a2_head_per_clip_launch_is_bit_identical():
     """The head forward / backward as one block per clip (knob a2_head_clip = 1, the default) against one launch per
     Linear layer (0): the same per-output arithmetic in the same order, so the step's losses, outputs and every
-    gradient are bit-identical."""
+    gradient are bit-identical.  (compute_improved_loss stays four launches: as phases of one block its B x B clip
+    pairs ran as serial rounds of global loads, a2 0.53 -> 0.70 ms/step, profiles/r06_bench_a2_loss_block.json.)"""
     from vad_amd import _native as nat
     case = dict(B=6, T=8, H=48, W=40, seed=27, step=2, ckpt=True)
     x = ao.synth_clips(27, 2, 0, 6, 8, 48, 40)
