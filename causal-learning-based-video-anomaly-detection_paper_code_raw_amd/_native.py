@@ -66,6 +66,7 @@ _SIGS = {
     "vad_cad_profile_marks": (_I, [_P, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _I]),
     "vad_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "vad_conv3x3_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I64, _P]),
+    "vad_bn_bwd_apply": (_I, [_P, _P, _P, _I, _I, _P, _I, _P]),
     # minicausal (config 1)
     "vad_mc_create": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(_P)]),
     "vad_mc_destroy": (None, [_P]),

@@ -40,3 +40,13 @@ extern "C" int vad_conv3x3_wgrad(const float* x_nhwc, const float* dy_nhwc, int 
 }
 
 extern "C" int vad_set_tuning(const char* key, int value) { return vad::set_tuning(key, value); }
+
+// The BN backward apply pass alone (measurement / tests): dY = k (dZ - mean dZ - xhat mean(dZ xhat)), dZ = dA masked by
+// the ReLU of s y + t; stats = the layer's [7 C] BN state; bf16: dA / y / dY stored as bf16 (config 4).
+extern "C" int vad_bn_bwd_apply(const void* dA, const void* y, const float* stats, int M, int C, void* dY, int bf16,
+                                void* stream) {
+  ActStorage abf(bf16);
+  int nb = 0;
+  return bn_bwd_apply(reinterpret_cast<const float*>(dA), reinterpret_cast<const float*>(y), stats, M, C,
+                      reinterpret_cast<float*>(dY), nullptr, &nb, (hipStream_t)stream);
+}

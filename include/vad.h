@@ -144,6 +144,12 @@ int vad_set_tuning(const char* key, int value);
 /* weight gradient of the same conv: dW[Co][Ci][3][3] = sum over pixels dY x patches(x); split-K slabs in partial */
 int vad_conv3x3_wgrad(const float* x_nhwc, const float* dy_nhwc, int NF, int Ci, int IH, int IW, int Co, int stride,
                       float* dW, float* partial, int64_t partial_floats, void* stream);
+/* the backbone's BatchNorm backward apply pass (cad:116,131,136 -- the per-element half of BatchNorm2d + ReLU
+ * backward): dY = k (dZ - mean dZ - xhat mean(dZ xhat)), dZ = dA [s y + t > 0]; rows M = NF*H*W, channels C;
+ * stats = the layer's [7 C] state [mean | invstd | scale | shift | k | mean dZ | mean dZ xhat]; bf16 != 0: dA, y, dY
+ * are bf16 (config 4), else fp32 */
+int vad_bn_bwd_apply(const void* dA, const void* y, const float* stats, int M, int C, void* dY, int bf16,
+                     void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * minicausal_vad_complete3.py — SimpleVideoAnomalyDetector (mc:25-102) + StableTrainer step (mc:249-330)

@@ -413,3 +413,40 @@ def test_conv3x3_wgrad_tr_prefetch_is_bit_identical(NF, Ci, Co, IH, IW, s):
         finally:
             nat.check(nat.lib().vad_set_tuning(b"conv_wgrad_tr_pft", 0))
     assert torch.equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("bf", [False, True])
+@pytest.mark.parametrize("M,C", [(128 * 57 * 57, 32), (7 * 29 * 29 + 3, 64), (128 * 8 * 8, 256), (5, 128)])
+def test_bn_bwd_apply_matches_formula(M, C, bf):
+    """The BN-backward apply pass alone (vad_bn_bwd_apply; fp32 = config 2, bf16 storage = config 4) against the
+    BatchNorm2d + ReLU backward formula in float64 (cad:116,131,136): dY = k (dZ - mean dZ - xhat mean(dZ xhat)),
+    dZ = dA [s y + t > 0]; fp32 within a few ulps, bf16 within one bf16 rounding of the output."""
+    nat = _lib()
+    g = torch.Generator().manual_seed(M + C + bf)
+    dt = torch.bfloat16 if bf else torch.float32
+    dA = torch.randn(M, C, generator=g).to(dt)
+    y = torch.randn(M, C, generator=g).to(dt)
+    mean, inv = torch.randn(C, generator=g) * 0.1, torch.rand(C, generator=g) + 0.5
+    sc, sh, k = torch.randn(C, generator=g), torch.randn(C, generator=g) * 0.1, torch.rand(C, generator=g)
+    mdz, mdzx = torch.randn(C, generator=g) * 1e-2, torch.randn(C, generator=g) * 1e-2
+    stats = torch.cat([mean, inv, sc, sh, k, mdz, mdzx])
+    d = torch.device("cuda")
+    dY = torch.full((M, C), float("nan"), device=d, dtype=dt)
+    dAd, yd = dA.to(d), y.to(d)
+    nat.check(nat.lib().vad_bn_bwd_apply(dAd.data_ptr(), yd.data_ptr(), stats.to(d).data_ptr(), M, C, dY.data_ptr(),
+                                         1 if bf else 0, nat.stream_of(d)))
+    torch.cuda.synchronize()
+    a, yy = dA.double(), y.double()
+    z = yy * sc.double() + sh.double()
+    dz = torch.where(z > 0, a, torch.zeros_like(a))
+    xh = (yy - mean.double()) * inv.double()
+    ref = k.double() * (dz - mdz.double() - xh * mdzx.double())
+    out = dY.cpu().double()
+    # error bound: fp32 rounding of each term (mag = the terms' magnitudes; the sum may cancel) + for bf16 storage the
+    # output's own rounding; a ReLU decision within rounding of 0 may go either way: those elements are excluded
+    mag = k.double().abs() * (dz.abs() + mdz.double().abs() + xh.abs() * mdzx.double().abs())
+    keep = (z.abs() > 1e-5)
+    bound = 1e-6 * mag + (2.0 ** -8 * ref.abs() if bf else 0.0)
+    assert torch.isfinite(out).all()
+    bad = ((out - ref).abs() > bound) & keep
+    assert not bool(bad.any()), float(((out - ref).abs() - bound)[keep].max())
