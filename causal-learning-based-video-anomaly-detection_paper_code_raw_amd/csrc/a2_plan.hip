@@ -865,7 +865,8 @@ struct A2PlanImpl {
       if (direct) {  // conv3d_2 / conv3d_3: implicit GEMM, bias + ReLU in the epilogue
         const Vol5& in = g[s3].in;
         VAD_TRY(conv3s2_prep(P(2 * s3), A2_CO[s3], in.C, wk3[s3], wc3[s3], st));
-        VAD_TRY(conv3s2_fwd(y[s3 - 1], B, in.D, in.H, in.W, in.C, wk3[s3], P(2 * s3 + 1), A2_CO[s3], 1, y[s3], st));
+        VAD_TRY(conv3s2_fwd(y[s3 - 1], B, in.D, in.H, in.W, in.C, wk3[s3], P(2 * s3 + 1), A2_CO[s3], 1, y[s3], st,
+                            scratch, scratch_floats));
         continue;
       }
       const float* src = s3 == 0 ? x : y[s3 - 1];

@@ -226,8 +226,9 @@ int conv4_wgrad_reduce(const float* part, int S, int R, int C, float* dW, hipStr
 // ---------------------------------------------------------------- Conv3d(k3, stride 2, p1) implicit GEMMs (a2)
 // wk [Co][27 Ci]; wc: 8 parity-class images back to back (27 Ci Co floats in all); C % 4 == 0
 int conv3s2_prep(const float* w, int Co, int Ci, float* wk, float* wc, hipStream_t st);
+// scratch (nullable): split-K slabs when the output grid leaves most CUs idle (summed in order, bias + ReLU after)
 int conv3s2_fwd(const float* src, int NF, int D, int H, int W, int C, const float* wk, const float* bias, int N,
-                int relu, float* out, hipStream_t st);
+                int relu, float* out, hipStream_t st, float* scratch = nullptr, int64_t scratch_floats = 0);
 int conv3s2_dgrad(const float* dy, int NF, int Co, const float* wc, int Ci, float* dx, int D, int H, int W,
                   hipStream_t st, const float* gate = nullptr);
 int conv3s2_wgrad(const float* dy, int Co, const float* src, int Ci, int NF, int D, int H, int W, float* dW,

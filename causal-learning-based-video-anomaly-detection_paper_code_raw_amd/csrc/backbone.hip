@@ -1928,11 +1928,12 @@ struct EpiConv3DgradCls {  // EpiConv3Dgrad for the class-batched GEMM: class = 
   struct Params {
     float* dst; int imgs; int GD[8], GA[8], GB[8]; int DD, DH, DW, C; const float* bias;
     const float* gate;  // nullable, dst's layout: dst = 0 where !(gate > 0) (the producing ReLU's backward, fused)
+    int rev;            // blockIdx.z = 7 - class (the heaviest classes dispatched first); the tables are in z order
   };
   template <class Cfg>
   static __device__ void apply(const Params& P, f32x16 (&acc)[Cfg::TM][Cfg::TN], int m0, int n0, int wm, int wn,
                                int lane, int, int N, float*) {
-    const int z = blockIdx.z, pd = (z >> 2) & 1, ph = (z >> 1) & 1, pw = z & 1;
+    const int z = blockIdx.z, cls = P.rev ? 7 - z : z, pd = (cls >> 2) & 1, ph = (cls >> 1) & 1, pw = cls & 1;
     const int GA = P.GA[z], GB = P.GB[z], per = P.GD[z] * GA * GB;
     if (per == 0) return;
 #pragma unroll
@@ -2350,7 +2351,7 @@ int conv3s2_prep(const float* w, int Co, int Ci, float* wk, float* wc, hipStream
 }
 
 int conv3s2_fwd(const float* src, int NF, int D, int H, int W, int C, const float* wk, const float* bias, int N,
-                int relu, float* out, hipStream_t st) {
+                int relu, float* out, hipStream_t st, float* scratch, int64_t scratch_floats) {
   VAD_CHECK(C % 4 == 0 && N >= 1, "conv3s2_fwd: C % 4 == 0");
   const int OD = (D - 1) / 2 + 1, OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
   ConvGeom3 g{NF, OD, OH, OW, 2, 2, 2, D, H, W, C};
@@ -2368,7 +2369,20 @@ int conv3s2_fwd(const float* src, int NF, int D, int H, int W, int C, const floa
     VAD_CHECK(gather_fits((int64_t)g.imgs * g.SD * g.SH * g.SW * g.C), "conv gather: source over 2 GB");
     typename ConvGather3KC<Cf::BM>::Params pa{src, g, taps};
     typename DenseKC<Cf::BN>::Params pb{wk, K, N, K};
-    return launch_gemm<Cf, ConvGather3KC, DenseKC, EpiDense>(pa, pb, pe, M, N, K, 1, nullptr, st);
+    // (conv3d_3 at B = 32: 64 output tiles of 27 K slices each -- split K four ways, slabs summed in order by
+    // dense_splitk_reduce, which applies the bias and the ReLU)
+    const int tiles = (int)(cdiv(M, Cf::BM) * cdiv(N, Cf::BN));
+    int splits = (int)std::min<int64_t>(cdiv(256, tiles), cdiv(K, 4 * BK));
+    while (splits > 1 && (int64_t)splits * M * N > scratch_floats) splits /= 2;
+    if (!scratch || splits <= 1) return launch_gemm<Cf, ConvGather3KC, DenseKC, EpiDense>(pa, pb, pe, M, N, K, 1, nullptr, st);
+    EpiPartial::Params pp{scratch, N};
+    int used = 1;
+    VAD_TRY((launch_gemm<Cf, ConvGather3KC, DenseKC, EpiPartial>(pa, pb, pp, M, N, K, splits, nullptr, st, &used)));
+    const int64_t total = (int64_t)M * N;
+    hipLaunchKernelGGL(dense_splitk_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 1024)), dim3(256),
+                       0, st, scratch, used, M, N, pe, nullptr);
+    VAD_LAUNCH_CHECK();
+    return 0;
   });
 }
 
@@ -2403,21 +2417,22 @@ int conv3s2_dgrad(const float* dy, int NF, int Co, const float* wc, int Ci, floa
                   hipStream_t st, const float* gate) {
   VAD_CHECK(Co % 4 == 0, "conv3s2_dgrad: Co % 4 == 0");
   const int OD = (D - 1) / 2 + 1, OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
-  // the 8 parity classes in one launch (blockIdx.z = class; K = 8 taps x Co, zero past a class's own taps)
+  // the 8 parity classes in one launch (blockIdx.z = 7 - class: the 8-tap class first, the 1-tap class last, so the
+  // longest blocks are dispatched first; each block's K loop stops at its class's own taps x Co)
   Conv3ClsGeom g{};
   g.imgs = NF; g.SD = OD; g.SH = OH; g.SW = OW; g.C = Co;
   typename DenseKCz<64>::Params pb0{};
   EpiConv3DgradCls::Params pe{};
-  pe.dst = dx; pe.imgs = NF; pe.DD = D; pe.DH = H; pe.DW = W; pe.C = Ci; pe.gate = gate;
+  pe.dst = dx; pe.imgs = NF; pe.DD = D; pe.DH = H; pe.DW = W; pe.C = Ci; pe.gate = gate; pe.rev = 1;
   int64_t off = 0;
   int Mmax = 0;
   for (int cls = 0; cls < 8; ++cls) {
-    const int pd = (cls >> 2) & 1, ph = (cls >> 1) & 1, pw = cls & 1, nt = c3_nt(cls);
-    g.GD[cls] = pe.GD[cls] = std::max(0, (D - pd + 1) / 2);
-    g.GA[cls] = pe.GA[cls] = std::max(0, (H - ph + 1) / 2);
-    g.GB[cls] = pe.GB[cls] = std::max(0, (W - pw + 1) / 2);
-    Mmax = std::max(Mmax, NF * g.GD[cls] * g.GA[cls] * g.GB[cls]);
-    TapTable3& taps = g.taps[cls];
+    const int pd = (cls >> 2) & 1, ph = (cls >> 1) & 1, pw = cls & 1, nt = c3_nt(cls), z = 7 - cls;
+    g.GD[z] = pe.GD[z] = std::max(0, (D - pd + 1) / 2);
+    g.GA[z] = pe.GA[z] = std::max(0, (H - ph + 1) / 2);
+    g.GB[z] = pe.GB[z] = std::max(0, (W - pw + 1) / 2);
+    Mmax = std::max(Mmax, NF * g.GD[z] * g.GA[z] * g.GB[z]);
+    TapTable3& taps = g.taps[z];
     taps.ntaps = nt;
     const int nh = 1 + ph, nw = 1 + pw;
     for (int t = 0; t < nt; ++t) {
@@ -2427,8 +2442,8 @@ int conv3s2_dgrad(const float* dy, int NF, int Co, const float* wc, int Ci, floa
       taps.dh[t] = (int8_t)(ph == 0 ? 0 : (ih == 0 ? 1 : 0));
       taps.dw[t] = (int8_t)(pw == 0 ? 0 : (iw == 0 ? 1 : 0));
     }
-    pb0.off[cls] = off;
-    pb0.kdim[cls] = nt * Co;
+    pb0.off[z] = off;
+    pb0.kdim[z] = nt * Co;
     off += (int64_t)nt * Ci * Co;
   }
   if (Mmax == 0) return 0;

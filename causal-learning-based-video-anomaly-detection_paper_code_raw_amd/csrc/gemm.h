@@ -497,6 +497,9 @@ struct ConvGather3ClsKC {
       }
     }
   }
+  // the class's real K extent (its own taps x C; the batched launch's K is the largest class's): the K loop of a
+  // block stops there instead of multiplying the zero-padded taps
+  static __device__ int batch_kend(const Params& Pp) { return Pp.g.taps[blockIdx.z].ntaps * Pp.g.C; }
   __device__ void load(int k0) {
     const Conv3ClsGeom& g = P->g;
     w.step(k0, cq, g.C);
@@ -629,6 +632,12 @@ struct ConvPatch3KM {
   }
 };
 
+// loaders of a batched launch (k_per_split < 0) may bound each batch's K: static batch_kend(params) (detection idiom)
+template <class L, class = void>
+struct HasBatchK : std::false_type {};
+template <class L>
+struct HasBatchK<L, std::void_t<decltype(L::batch_kend(std::declval<const typename L::Params&>()))>> : std::true_type {};
+
 // ------------------------------------------------------------------ the kernel body
 // Epi::apply(params, acc, m0, n0, wm, wn, lane, lds_scratch) writes the block's results.
 template <class Cfg, class LA, class LB, class Epi>
@@ -649,7 +658,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const typename LA::Params pa,
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   // k_per_split < 0: blockIdx.z is a batch index the loaders / epilogue read themselves (the whole K per block)
   const int kbeg = k_per_split > 0 ? (int)blockIdx.z * k_per_split : 0;
-  const int kend = k_per_split > 0 ? min(K, kbeg + k_per_split) : K;
+  int kend = k_per_split > 0 ? min(K, kbeg + k_per_split) : K;
+  if constexpr (HasBatchK<LA>::value)
+    if (k_per_split < 0) kend = min(kend, (LA::batch_kend(pa) + BK - 1) / BK * BK);
 
   LA la;
   LB lb;
