@@ -958,9 +958,9 @@ struct A2PlanImpl {
       if (direct && s3 > 0) {  // conv3d_2 / conv3d_3 on the implicit GEMMs
         const Vol5& in = g[s3].in;
         float* nxt = dg == dA ? dA2 : dA;
-        VAD_TRY(col_sum(dg, rows, A2_CO[s3], G(2 * s3 + 1), reinterpret_cast<double*>(scratch), st));
+        // (weight and bias gradients from one split-K GEMM: the bias is a column of ones beside the patch columns)
         VAD_TRY(conv3s2_wgrad(dg, A2_CO[s3], y[s3 - 1], in.C, B, in.D, in.H, in.W, G(2 * s3), scratch, scratch_floats,
-                              1024, st));
+                              1024, st, G(2 * s3 + 1)));
         VAD_TRY(conv3s2_dgrad(dg, B, A2_CO[s3], wc3[s3], in.C, nxt, in.D, in.H, in.W, st, y[s3 - 1]));
         cur = nxt;
         continue;

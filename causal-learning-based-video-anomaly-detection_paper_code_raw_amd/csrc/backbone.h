@@ -231,8 +231,9 @@ int conv3s2_fwd(const float* src, int NF, int D, int H, int W, int C, const floa
                 int relu, float* out, hipStream_t st, float* scratch = nullptr, int64_t scratch_floats = 0);
 int conv3s2_dgrad(const float* dy, int NF, int Co, const float* wc, int Ci, float* dx, int D, int H, int W,
                   hipStream_t st, const float* gate = nullptr);
+// db (nullable): the conv bias gradient (dY's column sums) from the same GEMM (a ones column)
 int conv3s2_wgrad(const float* dy, int Co, const float* src, int Ci, int NF, int D, int H, int W, float* dW,
-                  float* part, int64_t part_cap, int target_blocks, hipStream_t st);
+                  float* part, int64_t part_cap, int target_blocks, hipStream_t st, float* db = nullptr);
 // scratch: 256 * N doubles
 int col_sum(const float* x, int64_t M, int N, float* db, double* scratch, hipStream_t st);
 // the single-channel ends, 32 channels on the other side, on the VALU: w = the [32][1][4][4] / [32][16] weight

@@ -2073,33 +2073,44 @@ int conv4_wgrad(const float* A, int R, const float* src, int C, int NF, int AH, 
 
 // dW[r][c][tap] = sum over the S slabs, in order, of part[s][r][tap C + c] (NT taps: 16 for the 4x4 convs, 27 for
 // the 3-D ones)
+// (slab rows of ld floats: the NT C weight columns, then with db the bias column NT C)
 __global__ __launch_bounds__(256) void conv4_wgrad_reduce_kernel(const float* __restrict__ part, int S, int R, int C,
-                                                                 int NT, float* __restrict__ dW) {
-  const int64_t total = (int64_t)R * NT * C;
+                                                                 int NT, int ld, float* __restrict__ dW,
+                                                                 float* __restrict__ db) {
+  const int W1 = NT * C + (db ? 1 : 0);
+  const int64_t total = (int64_t)R * W1, slab = (int64_t)R * ld;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / W1;
+    const int col = (int)(i - r * W1);
     float s = 0.f;
-    for (int z = 0; z < S; ++z) s += part[(int64_t)z * total + i];
-    const int c = (int)(i % C), tap = (int)((i / C) % NT);
-    const int64_t r = i / ((int64_t)NT * C);
-    dW[(r * C + c) * NT + tap] = s;
+    for (int z = 0; z < S; ++z) s += part[(int64_t)z * slab + r * ld + col];
+    if (col == NT * C) {
+      db[r] = s;
+    } else {
+      const int c = col % C, tap = col / C;
+      dW[(r * C + c) * NT + tap] = s;
+    }
   }
 }
 
 // the same for many slabs: 64 consecutive entries x 4 slab lanes per block (lane l adds slabs l, l + 4, ... in order
 // with 8 loads in flight, coalesced across the 64 entries), the 4 lane sums combined in a fixed order
 __global__ __launch_bounds__(256) void conv4_wgrad_reduce_small_kernel(const float* __restrict__ part, int S, int R,
-                                                                       int C, int NT, float* __restrict__ dW) {
+                                                                       int C, int NT, int ld, float* __restrict__ dW,
+                                                                       float* __restrict__ db) {
   __shared__ float red[4][64];
-  const int64_t total = (int64_t)R * NT * C;
+  const int W1 = NT * C + (db ? 1 : 0);
+  const int64_t total = (int64_t)R * W1, slab = (int64_t)R * ld;
   const int e = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + e;
+  const int64_t row = i / W1, col = i - row * W1, pi = row * ld + col;
   float v = 0.f;
   if (i < total) {
     const int n = S > sl ? (S - sl + 3) / 4 : 0;
     for (int k0 = 0; k0 < n; k0 += 8) {
       float u[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) u[q] = part[(int64_t)(sl + 4 * min(k0 + q, n - 1)) * total + i];
+      for (int q = 0; q < 8; ++q) u[q] = part[(int64_t)(sl + 4 * min(k0 + q, n - 1)) * slab + pi];
 #pragma unroll
       for (int q = 0; q < 8; ++q)
         if (k0 + q < n) v += u[q];
@@ -2109,22 +2120,28 @@ __global__ __launch_bounds__(256) void conv4_wgrad_reduce_small_kernel(const flo
   __syncthreads();
   if (sl == 0 && i < total) {
     const float t = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
-    const int c = (int)(i % C), tap = (int)((i / C) % NT);
-    const int64_t r = i / ((int64_t)NT * C);
-    dW[(r * C + c) * NT + tap] = t;
+    if (col == NT * C) {
+      db[row] = t;
+    } else {
+      const int c = (int)(col % C), tap = (int)(col / C);
+      dW[(row * C + c) * NT + tap] = t;
+    }
   }
 }
 
-static int taps_wgrad_reduce(const float* part, int S, int R, int C, int NT, float* dW, hipStream_t st) {
-  const int64_t total = (int64_t)R * NT * C;
+// slabs [S][R][ld] -> dW (torch [R][C][taps]) and, with db, the bias column NT C of each row
+static int taps_wgrad_reduce(const float* part, int S, int R, int C, int NT, float* dW, hipStream_t st, int ld = 0,
+                             float* db = nullptr) {
+  if (ld <= 0) ld = NT * C;
+  const int64_t total = (int64_t)R * (NT * C + (db ? 1 : 0));
   if (S >= 16) {
     hipLaunchKernelGGL(conv4_wgrad_reduce_small_kernel, dim3((unsigned)cdiv(total, 64)), dim3(256), 0, st, part, S, R, C,
-                       NT, dW);
+                       NT, ld, dW, db);
     VAD_LAUNCH_CHECK();
     return 0;
   }
   hipLaunchKernelGGL(conv4_wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 2048)), dim3(256), 0,
-                     st, part, S, R, C, NT, dW);
+                     st, part, S, R, C, NT, ld, dW, db);
   VAD_LAUNCH_CHECK();
   return 0;
 }
@@ -2466,10 +2483,11 @@ int conv3s2_dgrad(const float* dy, int NF, int Co, const float* wc, int Ci, floa
 }
 
 int conv3s2_wgrad(const float* dy, int Co, const float* src, int Ci, int NF, int D, int H, int W, float* dW,
-                  float* part, int64_t part_cap, int target_blocks, hipStream_t st) {
+                  float* part, int64_t part_cap, int target_blocks, hipStream_t st, float* db) {
   VAD_CHECK(Ci % 4 == 0 && Co % 4 == 0, "conv3s2_wgrad: channel counts % 4 == 0");
   const int OD = (D - 1) / 2 + 1, OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
-  const int M = Co, N = 27 * Ci, K = NF * OD * OH * OW;
+  // (db: the bias gradient = dY's column sums, as one more GEMM column of ones beside the 27 Ci patch columns)
+  const int M = Co, N = 27 * Ci + (db ? 1 : 0), K = NF * OD * OH * OW;
   VAD_CHECK((int64_t)M * N <= part_cap, "conv3s2_wgrad: slab too small");
   int used = 1;
   VAD_TRY(with_tile(pick_wgrad_tile(M, N), [&](auto cfg) -> int {
@@ -2480,11 +2498,11 @@ int conv3s2_wgrad(const float* dy, int Co, const float* src, int Ci, int NF, int
     VAD_CHECK(gather_fits((int64_t)K * Co), "dense gather: operand over 2 GB");
     typename DenseKM<Cf::BM>::Params pa{dy, Co, Co, K, -1};
     VAD_CHECK(gather_fits((int64_t)NF * D * H * W * Ci), "conv patch: source over 2 GB");
-    typename ConvPatch3KM<Cf::BN>::Params pb{src, NF, OD, OH, OW, 2, 2, 2, 1, D, H, W, Ci, N};
+    typename ConvPatch3KM<Cf::BN>::Params pb{src, NF, OD, OH, OW, 2, 2, 2, 1, D, H, W, Ci, 27 * Ci, db ? 1 : 0};
     const EpiPartial::Params pe{part, N};
     return launch_gemm<Cf, DenseKM, ConvPatch3KM, EpiPartial>(pa, pb, pe, M, N, K, splits, nullptr, st, &used);
   }));
-  return taps_wgrad_reduce(part, used, Co, Ci, 27, dW, st);
+  return taps_wgrad_reduce(part, used, Co, Ci, 27, dW, st, N, db);
 }
 
 // db[n] = sum over the M rows of x[m][n], fixed order, two passes: block b sums the rows of its contiguous range with

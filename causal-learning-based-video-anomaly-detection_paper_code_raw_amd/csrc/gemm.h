@@ -564,6 +564,7 @@ struct ConvPatch3KM {
   static constexpr int NL = R / 32;
   struct Params {
     const float* src; int imgs, OD, OH, OW, sd, sh, sw, pad, SD, SH, SW, C, rows;  // rows = 27 * C
+    int ones;  // 1: column `rows` is 1 for every pixel (the conv bias gradient as one more GEMM column)
   };
   const Params* P;
   __amdgpu_buffer_rsrc_t rs;
@@ -583,8 +584,8 @@ struct ConvPatch3KM {
         kd[j] = tap / 9;
         kh[j] = (tap / 3) % 3;
         kw[j] = tap % 3;
-      } else {
-        cc[j] = 0; kd[j] = -1; kh[j] = 0; kw[j] = 0;
+      } else {  // (kd = -2: the ones column, r == rows)
+        cc[j] = 0; kd[j] = (Pp.ones && r == Pp.rows) ? -2 : -1; kh[j] = 0; kw[j] = 0;
       }
     }
   }
@@ -618,7 +619,9 @@ struct ConvPatch3KM {
       const int z = od[j] * q.sd - q.pad + kd[j], y = oh[j] * q.sh - q.pad + kh[j], x = ow[j] * q.sw - q.pad + kw[j];
       const bool ok = img[j] < q.imgs && kd[j] >= 0 && (unsigned)z < (unsigned)q.SD && (unsigned)y < (unsigned)q.SH &&
                       (unsigned)x < (unsigned)q.SW;
-      reg[j] = gather_load(rs, ok, (((img[j] * q.SD + z) * q.SH + y) * q.SW + x) * q.C + cc[j]);
+      const f32x4 v = gather_load(rs, ok, (((img[j] * q.SD + z) * q.SH + y) * q.SW + x) * q.C + cc[j]);
+      const float one = (kd[j] == -2 && img[j] < q.imgs) ? 1.f : 0.f;
+      reg[j] = kd[j] == -2 ? f32x4{one, 0.f, 0.f, 0.f} : v;
     }
     nextk = k0 + BK;
   }
