@@ -517,13 +517,39 @@ __device__ __forceinline__ void a2_stage_halo(float* xs, const float* __restrict
   }
 }
 
+// The per-step weight images of the direct path in one launch: conv3d_2 / conv3d_3's GEMM and parity-class images
+// (conv3s2_prep_elem) and conv3d_1's [ci*27 + tap][co] rows + its bias (w1t: a2_conv1_fwd_kernel copies them into LDS
+// without transposing).
+struct A2Prep {
+  const float* w[3];
+  float *wk[3], *wc[3];
+  int Co[3], Ci[3];
+  int64_t end[3];  // prefix sums of the element counts: conv3d_1 (16 * 81 + 16), conv3d_2, conv3d_3
+  const float* b1;
+  float* w1t;
+};
+__global__ __launch_bounds__(256) void a2_prep_kernel(const A2Prep p) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < p.end[2]; i += (int64_t)gridDim.x * 256) {
+    if (i < p.end[0]) {
+      if (i < 16 * A2C1_TAPS) {
+        const int co = (int)(i / A2C1_TAPS), j = (int)(i % A2C1_TAPS);
+        p.w1t[j * 16 + co] = p.w[0][i];
+      } else {
+        p.w1t[i] = p.b1[i - 16 * A2C1_TAPS];
+      }
+    } else {
+      const int s = i < p.end[1] ? 1 : 2;
+      conv3s2_prep_elem(p.w[s], p.Co[s], p.Ci[s], p.wk[s], p.wc[s], i - p.end[s - 1]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void a2_conv1_fwd_kernel(const float* __restrict__ x, int B, int T, int H, int W,
-                                                           const float* __restrict__ w, const float* __restrict__ bias,
-                                                           float* __restrict__ y) {
-  __shared__ __attribute__((aligned(16))) float ws[A2C1_TAPS][16];  // [ci*27 + tap][co]
+                                                           const float* __restrict__ w1t, float* __restrict__ y) {
+  __shared__ __attribute__((aligned(16))) float ws[A2C1_TAPS + 1][16];  // [ci*27 + tap][co], then the bias row
   __shared__ float xs[3 * A2_HALO];
   __shared__ float os[256 * 17];
-  for (int i = threadIdx.x; i < 16 * A2C1_TAPS; i += 256) ws[i % A2C1_TAPS][i / A2C1_TAPS] = w[i];
+  for (int i = threadIdx.x; i < 16 * (A2C1_TAPS + 1); i += 256) ws[i / 16][i % 16] = w1t[i];
   const A2Tiles g(B, T, H, W);
   const int v = threadIdx.x, vd = v / (A2T_H * A2T_W), vh = (v / A2T_W) % A2T_H, vw = v % A2T_W;
   for (int64_t tile = blockIdx.x; tile < g.n; tile += gridDim.x) {
@@ -546,7 +572,8 @@ __global__ __launch_bounds__(256) void a2_conv1_fwd_kernel(const float* __restri
       for (int t = 0; t < 27; ++t) {
         const float xv = xs[((ci * A2H_D + vd + t / 9) * A2H_H + 2 * vh + (t / 3) % 3) * A2H_W + 2 * vw + t % 3];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < 4; ++q) {  // (LDS broadcast reads; weights through the scalar path measured 3.6x slower:
+                                       // the waits on the scalar loads are exposed)
           const f32x4 wv = *reinterpret_cast<const f32x4*>(&ws[ci * 27 + t][4 * q]);
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc[q][e] = fmaf(xv, wv[e], acc[q][e]);
@@ -557,7 +584,7 @@ __global__ __launch_bounds__(256) void a2_conv1_fwd_kernel(const float* __restri
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) os[v * 17 + 4 * q + e] = relu_nan(acc[q][e] + bias[4 * q + e]);
+      for (int e = 0; e < 4; ++e) os[v * 17 + 4 * q + e] = relu_nan(acc[q][e] + ws[A2C1_TAPS][4 * q + e]);
     __syncthreads();
     for (int i = threadIdx.x; i < 256 * 4; i += 256) {  // (voxel, float4) in tile order: W-runs contiguous in y
       const int vv = i >> 2, c4 = (i & 3) * 4;
@@ -755,6 +782,7 @@ struct A2PlanImpl {
   // (a2_direct) conv3d_2 / conv3d_3 weight images (conv3s2_prep: [Co][27 Ci] + the 8 parity-class images) and the
   // second input-gradient buffer
   float *wk3[3] = {}, *wc3[3] = {}, *dA2 = nullptr;
+  float* w1t = nullptr;  // conv3d_1's [81][16] weight rows + bias (a2_prep_kernel)
   const int direct = g_a2_direct;
   int64_t scratch_floats = 0;
   int training = 1, with_loss = 0;
@@ -781,6 +809,7 @@ struct A2PlanImpl {
         wk3[s] = w.take<float>((int64_t)27 * g[s].in.C * A2_CO[s]);
         wc3[s] = w.take<float>((int64_t)27 * g[s].in.C * A2_CO[s]);
       }
+      if (direct && s == 0) w1t = w.take<float>(16 * (A2C1_TAPS + 1));
       y[s] = w.take<float>(g[s].out().numel());
       max_y = std::max(max_y, g[s].out().numel());
       if (s > 0 && !direct) max_dcols = std::max(max_dcols, g[s].rows() * g[s].K());
@@ -856,15 +885,31 @@ struct A2PlanImpl {
           VAD_HIP(hipMemcpyAsync(xin, x, sizeof(float) * n, hipMemcpyDeviceToDevice, st));
           xsrc = xin;
         }
+        A2Prep pp{};
+        int64_t acc = 16 * (A2C1_TAPS + 1);
+        pp.end[0] = acc;
+        pp.w[0] = P(S_C1W);
+        pp.b1 = P(S_C1B);
+        pp.w1t = w1t;
+        for (int s = 1; s < 3; ++s) {
+          pp.w[s] = P(2 * s);
+          pp.wk[s] = wk3[s];
+          pp.wc[s] = wc3[s];
+          pp.Co[s] = A2_CO[s];
+          pp.Ci[s] = g[s].in.C;
+          acc += (int64_t)27 * g[s].in.C * A2_CO[s];
+          pp.end[s] = acc;
+        }
+        hipLaunchKernelGGL(a2_prep_kernel, dim3((unsigned)std::min<int64_t>(cdiv(acc, 256), 1024)), dim3(256), 0, st, pp);
+        VAD_LAUNCH_CHECK();
         const A2Tiles tl(B, T, H, W);
         hipLaunchKernelGGL(a2_conv1_fwd_kernel, dim3((unsigned)std::min<int64_t>(tl.n, 4096)), dim3(256), 0, st, xsrc, B,
-                           T, H, W, P(S_C1W), P(S_C1B), y[0]);
+                           T, H, W, w1t, y[0]);
         VAD_LAUNCH_CHECK();
         continue;
       }
-      if (direct) {  // conv3d_2 / conv3d_3: implicit GEMM, bias + ReLU in the epilogue
+      if (direct) {  // conv3d_2 / conv3d_3: implicit GEMM, bias + ReLU in the epilogue (images from a2_prep_kernel)
         const Vol5& in = g[s3].in;
-        VAD_TRY(conv3s2_prep(P(2 * s3), A2_CO[s3], in.C, wk3[s3], wc3[s3], st));
         VAD_TRY(conv3s2_fwd(y[s3 - 1], B, in.D, in.H, in.W, in.C, wk3[s3], P(2 * s3 + 1), A2_CO[s3], 1, y[s3], st,
                             scratch, scratch_floats));
         continue;

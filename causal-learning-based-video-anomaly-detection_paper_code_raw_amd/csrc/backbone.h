@@ -226,6 +226,25 @@ int conv4_wgrad_reduce(const float* part, int S, int R, int C, float* dW, hipStr
 // ---------------------------------------------------------------- Conv3d(k3, stride 2, p1) implicit GEMMs (a2)
 // wk [Co][27 Ci]; wc: 8 parity-class images back to back (27 Ci Co floats in all); C % 4 == 0
 int conv3s2_prep(const float* w, int Co, int Ci, float* wk, float* wc, hipStream_t st);
+// taps of parity class cls (4 pd + 2 ph + pw) of a stride-2 3-D conv's input gradient
+__device__ __host__ inline int c3_nt(int cls) { return (1 + ((cls >> 2) & 1)) * (1 + ((cls >> 1) & 1)) * (1 + (cls & 1)); }
+// element i (torch layout [Co][Ci][27]) of conv3s2_prep, for fused preps (a2_plan.hip)
+__device__ inline void conv3s2_prep_elem(const float* __restrict__ w, int Co, int Ci, float* __restrict__ wk,
+                                  float* __restrict__ wc, int64_t i) {
+  const int tap = (int)(i % 27), ci = (int)((i / 27) % Ci);
+  const int64_t co = i / (27 * Ci);
+  const float v = w[i];
+  wk[co * 27 * Ci + tap * Ci + ci] = v;
+  const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+  const int pd = kd == 1 ? 0 : 1, ph = kh == 1 ? 0 : 1, pw = kw == 1 ? 0 : 1;
+  const int id = kd == 2 ? 1 : 0, ih = kh == 2 ? 1 : 0, iw = kw == 2 ? 1 : 0;  // index in the dim's tap list
+  const int cls = 4 * pd + 2 * ph + pw, nh = 1 + ph, nw = 1 + pw, nt = c3_nt(cls);
+  int64_t off = 0;
+  for (int c = 0; c < cls; ++c) off += (int64_t)c3_nt(c) * Ci * Co;
+  const int t = (id * nh + ih) * nw + iw;
+  wc[off + ((int64_t)ci * nt + t) * Co + co] = v;
+}
+
 // scratch (nullable): split-K slabs when the output grid leaves most CUs idle (summed in order, bias + ReLU after)
 int conv3s2_fwd(const float* src, int NF, int D, int H, int W, int C, const float* wk, const float* bias, int N,
                 int relu, float* out, hipStream_t st, float* scratch = nullptr, int64_t scratch_floats = 0);

@@ -2338,25 +2338,12 @@ int conv4_c1_wgrad(const float* A, const float* src, int NF, int AH, int AW, flo
 // Weight images (conv3s2_prep) of torch [Co][Ci][27]: wk [Co][27 Ci]; wc = the 8 class images [Ci][nt Co] back to back
 // (class cls = 4 pd + 2 ph + pw, nt = its tap count 1 / 2 / 4 / 8, taps d-major over the per-dim lists).
 // =====================================================================================================
-__device__ __host__ inline int c3_nt(int cls) { return (1 + ((cls >> 2) & 1)) * (1 + ((cls >> 1) & 1)) * (1 + (cls & 1)); }
 
 __global__ __launch_bounds__(256) void conv3s2_prep_kernel(const float* __restrict__ w, int Co, int Ci,
                                                            float* __restrict__ wk, float* __restrict__ wc) {
   const int64_t total = (int64_t)Co * Ci * 27;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int tap = (int)(i % 27), ci = (int)((i / 27) % Ci);
-    const int64_t co = i / (27 * Ci);
-    const float v = w[i];
-    wk[co * 27 * Ci + tap * Ci + ci] = v;
-    const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
-    const int pd = kd == 1 ? 0 : 1, ph = kh == 1 ? 0 : 1, pw = kw == 1 ? 0 : 1;
-    const int id = kd == 2 ? 1 : 0, ih = kh == 2 ? 1 : 0, iw = kw == 2 ? 1 : 0;  // index in the dim's tap list
-    const int cls = 4 * pd + 2 * ph + pw, nh = 1 + ph, nw = 1 + pw, nt = c3_nt(cls);
-    int64_t off = 0;
-    for (int c = 0; c < cls; ++c) off += (int64_t)c3_nt(c) * Ci * Co;
-    const int t = (id * nh + ih) * nw + iw;
-    wc[off + ((int64_t)ci * nt + t) * Co + co] = v;
-  }
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256)
+    conv3s2_prep_elem(w, Co, Ci, wk, wc, i);
 }
 
 int conv3s2_prep(const float* w, int Co, int Ci, float* wk, float* wc, hipStream_t st) {
