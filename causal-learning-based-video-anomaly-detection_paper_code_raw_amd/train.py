@@ -44,9 +44,13 @@ class CadTrainer:
 
     def __init__(self, model, lr=3e-4, weight_decay=1e-5, eps=1e-8, betas=(0.9, 0.999), max_norm=1.0, seed=0,
                  process_group=None, engine=None, compute_dtype=None, sync_bn=False, force_dist=False,
-                 prio_stream=False):
+                 prio_stream=False, skip_zero_detector=False):
         """force_dist: run the data-parallel protocol (broadcasts, bucketed all-reduces, SyncBN callback) even at
         world size 1 of an initialised process group -- exercises the collective path on one device (tests).
+        skip_zero_detector (world > 1): all-reduce the ranks' detector has-grad flags after the forward and read the
+        sum on the host; when it is zero (no box in range on any rank, cad:221-226) the detector's 13.3 MB of grads --
+        zero on every rank -- are left out of the head bucket.  One small collective and a host wait per step instead
+        of 13.3 MB on the wire: for interconnect-bound setups (the default sums it and never waits).
         prio_stream: run each step on a stream of the device's greatest priority (ordered after and before the
         caller's stream), so with the plan's low-priority weight-gradient stream (knob cad_stream_prio) the dispatcher
         prefers the critical path's workgroups."""
@@ -64,6 +68,8 @@ class CadTrainer:
         self.dist = initialised and (self.world > 1 or force_dist)
         self.eng.init_optimizer_state()
         self.sync_bn = bool(sync_bn) and self.dist
+        self.skip_zero_detector = bool(skip_zero_detector) and self.dist
+        self._det_flag = None
         # gradient buckets of the flat grad buffer (slot order: backbone | detector | causal head | direct classifier
         # | has-grad flags): everything from the detector on is one bucket, summed beside the backbone backward
         names = self.eng.slot_names
@@ -160,6 +166,9 @@ class CadTrainer:
             lh = self._loss_host
         kw = {"loss_host": lh} if lh is not None else {}
         o = eng.forward(videos, True, self.seed, self.step_idx, self.rank * B, labels, want_outputs=want_outputs, **kw)
+        # (the forward's per-rank "detector has a grad" flag; an engine without it: the grad buffer's flag after the
+        # backward, see _head_bucket_start)
+        self._det_flag = o["flags"][:1] if self.skip_zero_detector and "flags" in o else None
         if lh is not None:
             self._loss_ev.record(cur)
         if bcast:
@@ -174,9 +183,8 @@ class CadTrainer:
         else:
             eng.backward(True)
             if self.dist:
-                d0 = self.det_range[0]
-                self._reduce(eng.grads[d0:])  # detector + causal head + direct classifier + has-grad flags
-                self._reduce(eng.grads[:d0])
+                self._reduce(eng.grads[self._head_bucket_start():])  # detector + causal head + direct classifier + flags
+                self._reduce(eng.grads[:self.det_range[0]])
         eng.optimizer_step(self.lr if lr is None else lr, self.betas, self.eps, self.wd, self.max_norm,
                            1.0 / self.world)
         self.step_idx += 1
@@ -208,7 +216,7 @@ class CadTrainer:
         if getattr(self, "_comm", None) is None:
             self._comm = torch.cuda.Stream(eng.device)
         side = self._comm
-        d0 = self.det_range[0]
+        d0 = self._head_bucket_start()
         # stage 2: the causal-head / detector backward keeps running on the plan's side stream while the backbone
         # (stage 1) starts; the all-reduce stream waits for both that side stream and the compute stream
         eng.backward(True, stage=2)
@@ -222,6 +230,21 @@ class CadTrainer:
             with torch.cuda.stream(side):
                 self._reduce(eng.grads[lo:hi])
         main.wait_stream(side)
+
+
+    def _head_bucket_start(self):
+        """Start of the head bucket in the flat grad buffer: the detector's first grad, or with skip_zero_detector
+        and no rank's detector having a grad this step (the summed flag read on the host: the same decision on every
+        rank), the slot after the detector's."""
+        if not self.skip_zero_detector:
+            return self.det_range[0]
+        src = self._det_flag
+        if src is None:  # (engines whose forward reports no flags: the grad buffer's, final after the backward)
+            src = self.eng.grads[self.eng.param_floats:self.eng.param_floats + 1]
+        f = src.detach().clone().float()
+        self._reduce(f)
+        self.det_flag_sum = float(f.item())
+        return self.det_range[1] if self.det_flag_sum == 0.0 else self.det_range[0]
 
 
 def _cosine_lr(base, epoch, t_max):
