@@ -598,27 +598,24 @@ __global__ __launch_bounds__(256) void a2_conv1_fwd_kernel(const float* __restri
   }
 }
 
-// thread = 4 output channels (co quad q = tid & 3) x 2 (ci, tap) pairs (pair lane pl = tid >> 2: pairs pl and pl + 64,
-// pair 81 = the bias); per voxel one 16-B read of its dY quad and two halo reads feed 8 FMAs, branch-free (the bias
-// pair and the unused pair slot read offset 0 and select / discard)
+// thread = one (ci, tap) pair j = tid % 82 (pair 81 = the bias) x all 16 output channels, over one of three voxel
+// groups vg = tid / 82 (voxels vg, vg + 3, ...; threads 246..255 idle): per voxel four 16-B reads of its dY row (the
+// same row for every lane of a group: broadcast) and one halo read feed 16 FMAs (was 8 FMAs per 3 reads with 4 channels
+// x 2 pairs per thread, a third of the pair slots empty); the three group sums are added in a fixed order
 __global__ __launch_bounds__(256) void a2_conv1_wgrad_kernel(const float* __restrict__ dA, const float* __restrict__ x,
                                                              int B, int T, int H, int W, float* __restrict__ slab) {
   __shared__ float xs[3 * A2_HALO];
   __shared__ __attribute__((aligned(16))) float as[256][16];
   const A2Tiles g(B, T, H, W);
-  const int tid = threadIdx.x, q = tid & 3, pl = tid >> 2;
-  int off[2];  // per owned pair: its halo offset at voxel (0, 0, 0), -1 = the bias pair, -2 = none
-#pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    const int j = pl + 64 * m;
-    if (j > A2C1_TAPS) off[m] = -2;
-    else if (j == A2C1_TAPS) off[m] = -1;
-    else {
-      const int ci = j / 27, t = j % 27;
-      off[m] = ((ci * A2H_D + t / 9) * A2H_H + (t / 3) % 3) * A2H_W + t % 3;
-    }
+  const int tid = threadIdx.x, j = tid % (A2C1_TAPS + 1), vg = tid / (A2C1_TAPS + 1);
+  int off = -1;  // the pair's halo offset at voxel (0, 0, 0); -1: the bias pair
+  if (j < A2C1_TAPS) {
+    const int ci = j / 27, t = j % 27;
+    off = ((ci * A2H_D + t / 9) * A2H_H + (t / 3) % 3) * A2H_W + t % 3;
   }
-  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  f32x4 acc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int64_t tile = blockIdx.x; tile < g.n; tile += gridDim.x) {
     const int bw = (int)(tile % g.tw);
     int64_t r = tile / g.tw;
@@ -640,27 +637,34 @@ __global__ __launch_bounds__(256) void a2_conv1_wgrad_kernel(const float* __rest
             ok ? *reinterpret_cast<const f32x4*>(row + 4 * k) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     __syncthreads();
-    for (int v = 0; v < 256; ++v) {
-      const int vd = v / (A2T_H * A2T_W), vh = (v / A2T_W) % A2T_H, vw = v % A2T_W;
-      const int base = (vd * A2H_H + 2 * vh) * A2H_W + 2 * vw;
-      const f32x4 a = *reinterpret_cast<const f32x4*>(&as[v][4 * q]);
-      float xv[2];
+    if (vg < 3) {
+      for (int v = vg; v < 256; v += 3) {
+        const int vd = v / (A2T_H * A2T_W), vh = (v / A2T_W) % A2T_H, vw = v % A2T_W;
+        const int base = (vd * A2H_H + 2 * vh) * A2H_W + 2 * vw;
+        const float xv = xs[max(off, 0) + base];
+        const float xm = off < 0 ? 1.f : xv;
 #pragma unroll
-      for (int m = 0; m < 2; ++m) xv[m] = xs[max(off[m], 0) + base];
+        for (int k = 0; k < 4; ++k) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(&as[v][4 * k]);
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        const float xm = off[m] == -1 ? 1.f : xv[m];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[m][e] = fmaf(a[e], xm, acc[m][e]);
+          for (int e = 0; e < 4; ++e) acc[k][e] = fmaf(a[e], xm, acc[k][e]);
+        }
       }
     }
   }
+  // the three voxel groups' sums, fixed order (rows vg * 82 + j of the dY staging array)
+  __syncthreads();
+  if (vg < 3)
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
-    if (off[m] != -2)
+    for (int k = 0; k < 4; ++k) *reinterpret_cast<f32x4*>(&as[tid][4 * k]) = acc[k];
+  __syncthreads();
+  if (vg == 0) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        slab[((int64_t)blockIdx.x * 16 + 4 * q + e) * (A2C1_TAPS + 1) + pl + 64 * m] = acc[m][e];
+    for (int c = 0; c < 16; ++c) {
+      const float t = (as[j][c] + as[A2C1_TAPS + 1 + j][c]) + as[2 * (A2C1_TAPS + 1) + j][c];
+      slab[((int64_t)blockIdx.x * 16 + c) * (A2C1_TAPS + 1) + j] = t;
+    }
+  }
 }
 
 // dW[co][ci*27 + tap] / db[co] = sum over the S slabs: 16 consecutive entries x 16 slab lanes per block (lane l adds
