@@ -1094,6 +1094,7 @@ extern int g_bbox_im2col;  // bbox_plan.hip
 extern int g_ae_direct, g_ae_wgrad_blocks, g_ae_wgrad_stream;  // ae_plan.hip
 extern int g_conv4_cls_batch_min, g_conv4_split_tiles;
 extern int g_a2_direct, g_a2_head_clip;     // a2_plan.hip
+extern int g_conv3s2_fwd_blocks;
 int set_tuning(const char* key, int value) {
   const std::string k(key);
   if (k == "conv_fwd_tile") g_tune.fwd = value;
@@ -1127,6 +1128,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "a2_direct") g_a2_direct = value;
   else if (k == "a2_head_clip") g_a2_head_clip = value;
   else if (k == "cad_prep_stream") g_cad_prep_stream = value;
+  else if (k == "conv3s2_fwd_blocks") g_conv3s2_fwd_blocks = value;
   else if (k == "cad_wgrad_stream") g_cad_wgrad_stream = value;
   else if (k == "cad_dir_affine") g_cad_dir_affine = value;
   else if (k == "cad_det_gate") g_cad_det_gate = value;
@@ -2354,6 +2356,7 @@ int conv3s2_prep(const float* w, int Co, int Ci, float* wk, float* wc, hipStream
   return 0;
 }
 
+int g_conv3s2_fwd_blocks = 512;  // knob "conv3s2_fwd_blocks": split K until the grid reaches this many blocks
 int conv3s2_fwd(const float* src, int NF, int D, int H, int W, int C, const float* wk, const float* bias, int N,
                 int relu, float* out, hipStream_t st, float* scratch, int64_t scratch_floats) {
   VAD_CHECK(C % 4 == 0 && N >= 1, "conv3s2_fwd: C % 4 == 0");
@@ -2376,7 +2379,7 @@ int conv3s2_fwd(const float* src, int NF, int D, int H, int W, int C, const floa
     // (conv3d_3 at B = 32: 64 output tiles of 27 K slices each -- split K four ways, slabs summed in order by
     // dense_splitk_reduce, which applies the bias and the ReLU)
     const int tiles = (int)(cdiv(M, Cf::BM) * cdiv(N, Cf::BN));
-    int splits = (int)std::min<int64_t>(cdiv(256, tiles), cdiv(K, 4 * BK));
+    int splits = (int)std::min<int64_t>(cdiv(g_conv3s2_fwd_blocks, tiles), cdiv(K, 4 * BK));
     while (splits > 1 && (int64_t)splits * M * N > scratch_floats) splits /= 2;
     if (!scratch || splits <= 1) return launch_gemm<Cf, ConvGather3KC, DenseKC, EpiDense>(pa, pb, pe, M, N, K, 1, nullptr, st);
     EpiPartial::Params pp{scratch, N};
