@@ -355,12 +355,22 @@ class ImprovedMiniCausalVAD:
         self.optimizer.push_state(e)
         g = self.optimizer.param_groups[0]
         e.forward(videos, True, self.seed, self.global_step, self.clip0, with_loss=True, borrow_input=True)
-        vals = e.losses.cpu().tolist()
+        # The reference reads the loss after the forward and skips the backward and the step on NaN (a2:230-232).
+        # Here the losses go to pinned host memory behind the forward, the backward and the optimizer step are queued
+        # at once -- the optimizer kernels skip the update on device when the loss is NaN (status word losses[9]) and
+        # the backward's grads are overwritten by the next one -- and the host waits for the forward only, so the
+        # device never idles on the host round trip.
+        if getattr(self, "_loss_host", None) is None:
+            self._loss_host = torch.zeros(10, dtype=torch.float32).pin_memory()
+            self._loss_ev = torch.cuda.Event()
+        self._loss_host.copy_(e.losses, non_blocking=True)
+        self._loss_ev.record()
+        e.backward()
+        e.optimizer_step(g["lr"], g["weight_decay"], max_norm=0.5)
+        self._loss_ev.synchronize()
+        vals = self._loss_host.tolist()
         comps = dict(zip(LOSS_KEYS, vals[1:8]))
         stepped = not np.isnan(vals[0])
-        if stepped:
-            e.backward()
-            e.optimizer_step(g["lr"], g["weight_decay"], max_norm=0.5)
         self.global_step += 1
         self.clip0 += videos.shape[0]
         return vals[0], comps, stepped

@@ -127,3 +127,31 @@ def test_a2_head_per_clip_launch_is_bit_identical():
             nat.check(nat.lib().vad_set_tuning(b"a2_head_clip", 1))
     assert res[0][0] == res[1][0] and res[0][1] == res[1][1]
     assert torch.equal(res[0][2], res[1][2]) and torch.equal(res[0][3], res[1][3])
+
+
+def test_a2_nan_loss_skips_the_step():
+    """train_step queues the backward and the optimizer step before reading the loss; on a NaN loss the device gate
+    (status word losses[9]) leaves parameters, AdamW moments and step counts untouched like the reference's skip
+    (a2:230-232), and the next step is bit-identical to the same step of a run that never saw the NaN batch."""
+    case = A2_CASES[0]
+    B, T, H, W = case["B"], case["T"], case["H"], case["W"]
+    x = ao.synth_clips(case["seed"], case["step"], 0, B, T, H, W)
+    y = ao.synth_labels(0, B)
+    xn = x.clone()
+    xn[0, 0, 0, 0, 0] = float("nan")
+    a, b = _vad(case), _vad(case)
+    p0 = torch.cat([p.detach().reshape(-1).clone() for p in a.model.parameters()])
+    loss, _, stepped = a.train_step(xn, y)
+    torch.cuda.synchronize()
+    assert not stepped and np.isnan(loss)
+    e = a.model._engine
+    assert torch.equal(torch.cat([p.detach().reshape(-1) for p in a.model.parameters()]), p0)
+    assert float(e.exp_avg.abs().max()) == 0.0 and int(e.steps.max()) == 0
+    # the same clean step on both (b never saw the NaN batch; a's skipped step kept its keys' step counter)
+    b.global_step, b.clip0 = a.global_step, a.clip0
+    la, _, sa = a.train_step(x, y)
+    lb, _, sb = b.train_step(x, y)
+    torch.cuda.synchronize()
+    assert sa and sb and la == lb
+    assert torch.equal(torch.cat([p.detach().reshape(-1) for p in a.model.parameters()]),
+                       torch.cat([p.detach().reshape(-1) for p in b.model.parameters()]))
