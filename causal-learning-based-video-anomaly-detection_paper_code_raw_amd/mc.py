@@ -276,8 +276,9 @@ class StableTrainer:
     def _lr(self):
         return self.optimizer.param_groups[0]["lr"]
 
-    def train_step(self, data, targets):
-        """One mc:259-318 iteration on device; returns (loss, correct, n, counted) as host numbers."""
+    def _queue_step(self, data, targets):
+        """Queue one mc:259-318 iteration on device and an asynchronous copy of its host-visible results (loss,
+        status, correct count) into a pinned slot; returns the handle _finish reads."""
         data = data.to(device=self.device, dtype=torch.float32).contiguous()
         targets = targets.to(device=self.device, dtype=torch.float32).contiguous()
         self.model.train()
@@ -288,22 +289,52 @@ class StableTrainer:
         e.optimizer_step(self._lr(), wd=g["weight_decay"], b1=g["betas"][0], b2=g["betas"][1], eps=g["eps"])
         self.global_step += 1
         self.clip0 += data.shape[0]
-        out = e.scores
-        losses = e.losses.cpu()
+        if getattr(self, "_res_host", None) is None:
+            self._res_host = torch.zeros(2, 3, dtype=torch.float32).pin_memory()
+            self._res_ev = [torch.cuda.Event(), torch.cuda.Event()]
+            self._slot = 0
+        k = self._slot
+        self._slot ^= 1
+        corr = ((e.scores > 0.5).float() == targets).sum().reshape(1)
+        dev = torch.cat([e.losses[0:1], e.losses[3:4], corr.float()])
+        self._res_host[k].copy_(dev, non_blocking=True)
+        self._res_ev[k].record()
+        return k, targets.numel()
+
+    def _finish(self, h):
+        k, n = h
+        self._res_ev[k].synchronize()
+        loss, status, corr = self._res_host[k].tolist()
         # status 0: skipped before backward (not counted); 1: counted, no update (non-finite grads); 2: stepped
-        counted = bool(losses[3] > 0.5)
-        correct = int(((out > 0.5).float() == targets).sum()) if counted else 0
-        return float(losses[0]), correct, targets.numel(), counted
+        counted = status > 0.5
+        return loss, (int(corr) if counted else 0), n, counted
+
+    def train_step(self, data, targets):
+        """One mc:259-318 iteration on device; returns (loss, correct, n, counted) as host numbers."""
+        return self._finish(self._queue_step(data, targets))
 
     def train_epoch(self):
+        """mc:259-330 over the loader.  The host reads iteration k's loss / status / accuracy (the reference's
+        per-iteration .item() reads) after it has queued iteration k+1, so the device never idles on the host round
+        trip; the sums are the same numbers in the same order."""
         total_loss, correct, total = 0.0, 0, 0
+        pending = None
+
+        def take(h):
+            nonlocal total_loss, correct, total
+            loss, c, n, counted = self._finish(h)
+            if counted:
+                total_loss += loss
+                correct += c
+                total += n
+
         for data, targets in self.train_loader:
-            loss, c, n, counted = self.train_step(data, targets)
-            if not counted:
-                continue
-            total_loss += loss
-            correct += c
-            total += n
+            h = self._queue_step(data, targets)
+            if pending is not None:
+                take(pending)
+            pending = h
+        if pending is not None:
+            take(pending)
         n = len(self.train_loader)
         return (total_loss / n if n > 0 else 0), (correct / total if total > 0 else 0)
 
