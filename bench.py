@@ -984,6 +984,8 @@ def main():
             clips = world * args.batch * args.steps
             fpc = a2_flops_per_clip(args.T, args.H, args.W)
             tflops = fpc * args.batch / (r["step_ms"] * 1e-3) / 1e12
+            a2_step_bytes, a2_src = pmc_step("cfga2") if (args.batch, args.T, args.H, args.W) == (32, 8, 64, 64) \
+                else (None, None)
             print(json.dumps({
                 "metric": BASELINE_METRIC, "value": round(clips / r["elapsed"], 3), "unit": "clips/s",
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["step_ms"], 4),
@@ -995,7 +997,9 @@ def main():
                            "frame": f"3x{args.H}x{args.W}", "parallelism": f"dp{world}"},
                 "roofline": {"bound": "mfma", "kernel": "whole step", "achieved": round(tflops, 3),
                              "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_FP32_TFLOPS, 4),
-                             "traffic": None, "basis": f"{fpc} algorithmic FLOP per clip x clips / step time"},
+                             "traffic": a2_step_bytes, "traffic_unit": "HBM bytes per step (every kernel; PMC "
+                             "FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": a2_src,
+                             "basis": f"{fpc} algorithmic FLOP per clip x clips / step time"},
                 "cpu_baseline": cpu, "parity": parity, "final_loss": r["loss"], "stepped": r["stepped"]}),
                 flush=True)
         finish(world)
