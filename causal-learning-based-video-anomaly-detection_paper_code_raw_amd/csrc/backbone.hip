@@ -1936,24 +1936,45 @@ struct EpiConv3DgradCls {  // EpiConv3Dgrad for the class-batched GEMM: class = 
   static __device__ void apply(const Params& P, f32x16 (&acc)[Cfg::TM][Cfg::TN], int m0, int n0, int wm, int wn,
                                int lane, int, int N, float*) {
     const int z = blockIdx.z, cls = P.rev ? 7 - z : z, pd = (cls >> 2) & 1, ph = (cls >> 1) & 1, pw = cls & 1;
-    const int GA = P.GA[z], GB = P.GB[z], per = P.GD[z] * GA * GB;
+    const int GD = P.GD[z], GA = P.GA[z], GB = P.GB[z], per = GD * GA * GB;
     if (per == 0) return;
+    // a lane's 16 rows come in 4 runs of 4 consecutive rows (acc_row): the first row of a run is decomposed into
+    // (img, a, b, c) by division, the next three by a carrying +1 (the divisions by the class grid were most of the
+    // kernel's VALU work: 38 VALU per MFMA)
 #pragma unroll
     for (int i = 0; i < Cfg::TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + acc_row<Cfg>(wm, i, r, lane);
-        const int img = row / per, rem = row - img * per;
-        if (img >= P.imgs) continue;
-        const int a = rem / (GA * GB), r2 = rem - a * GA * GB;
-        const int b = r2 / GB, c = r2 - b * GB;
-        const int64_t base = ((((int64_t)img * P.DD + 2 * a + pd) * P.DH + 2 * b + ph) * P.DW + 2 * c + pw) * P.C;
+      for (int q = 0; q < 4; ++q) {
+        const int row0 = m0 + acc_row<Cfg>(wm, i, 4 * q, lane);
+        int img = row0 / per;
+        const int rem = row0 - img * per;
+        int a = rem / (GA * GB);
+        const int r2 = rem - a * GA * GB;
+        int b = r2 / GB, c = r2 - b * GB;
 #pragma unroll
-        for (int j = 0; j < Cfg::TN; ++j) {
-          const int col = n0 + acc_col<Cfg>(wn, j, lane);
-          if (col < N) {
-            const float v = acc[i][j][r] + (P.bias ? P.bias[col] : 0.f);
-            P.dst[base + col] = (P.gate && !(P.gate[base + col] > 0.f)) ? 0.f : v;
+        for (int u = 0; u < 4; ++u) {
+          if (u > 0) {  // row0 + u: c + 1 with carries into b, a, img
+            ++c;
+            const bool cb = c == GB;
+            c = cb ? 0 : c;
+            b += cb;
+            const bool ca = b == GA;
+            b = ca ? 0 : b;
+            a += ca;
+            const bool ci = a == GD;
+            a = ci ? 0 : a;
+            img += ci;
+          }
+          if (img >= P.imgs) continue;
+          const int64_t base = ((((int64_t)img * P.DD + 2 * a + pd) * P.DH + 2 * b + ph) * P.DW + 2 * c + pw) * P.C;
+          const int r = 4 * q + u;
+#pragma unroll
+          for (int j = 0; j < Cfg::TN; ++j) {
+            const int col = n0 + acc_col<Cfg>(wn, j, lane);
+            if (col < N) {
+              const float v = acc[i][j][r] + (P.bias ? P.bias[col] : 0.f);
+              P.dst[base + col] = (P.gate && !(P.gate[base + col] > 0.f)) ? 0.f : v;
+            }
           }
         }
       }
