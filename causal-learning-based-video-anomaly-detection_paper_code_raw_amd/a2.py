@@ -195,6 +195,14 @@ class A2Engine:
                                            nat.ptr(self.losses) if with_loss else None, self.stream()))
         return p.scores, p.adj, p.feats
 
+    def set_host_losses(self, buf):
+        """Let the current plan's forward also write its 10 loss words into `buf` (a pinned CPU tensor; None: stop)."""
+        p = self.cur
+        ptr = buf.data_ptr() if buf is not None else 0
+        if getattr(p, "host_ptr", 0) != ptr:
+            nat.check(nat.lib().vad_a2_set_option(p.plan, b"host_losses", ctypes.c_int64(ptr)))
+            p.host_ptr = ptr
+
     def loss(self, seed, step, clip0):
         nat.check(nat.lib().vad_a2_loss(self.cur.plan, ctypes.c_uint64(seed), ctypes.c_uint64(step),
                                         ctypes.c_int64(clip0), nat.ptr(self.losses), self.stream()))
@@ -354,16 +362,16 @@ class ImprovedMiniCausalVAD:
         e = self.model.engine(videos)
         self.optimizer.push_state(e)
         g = self.optimizer.param_groups[0]
-        e.forward(videos, True, self.seed, self.global_step, self.clip0, with_loss=True, borrow_input=True)
         # The reference reads the loss after the forward and skips the backward and the step on NaN (a2:230-232).
-        # Here the losses go to pinned host memory behind the forward, the backward and the optimizer step are queued
-        # at once -- the optimizer kernels skip the update on device when the loss is NaN (status word losses[9]) and
-        # the backward's grads are overwritten by the next one -- and the host waits for the forward only, so the
-        # device never idles on the host round trip.
+        # Here the forward's copy kernel also writes the losses into pinned host memory (plan option host_losses),
+        # the backward and the optimizer step are queued at once -- the optimizer kernels skip the update on device
+        # when the loss is NaN (status word losses[9]) and the backward's grads are overwritten by the next one --
+        # and the host waits for the forward only, so the device never idles on the host round trip.
         if getattr(self, "_loss_host", None) is None:
             self._loss_host = torch.zeros(10, dtype=torch.float32).pin_memory()
             self._loss_ev = torch.cuda.Event()
-        self._loss_host.copy_(e.losses, non_blocking=True)
+        e.set_host_losses(self._loss_host)
+        e.forward(videos, True, self.seed, self.global_step, self.clip0, with_loss=True, borrow_input=True)
         self._loss_ev.record()
         e.backward()
         e.optimizer_step(g["lr"], g["weight_decay"], max_norm=0.5)

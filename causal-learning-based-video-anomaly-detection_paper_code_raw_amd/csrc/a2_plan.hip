@@ -730,7 +730,7 @@ __global__ __launch_bounds__(256) void a2_sqsum_kernel(const float* __restrict__
 }
 // ctrl: [0] step?, [1] clip coefficient, [2] -lr/bc1, [3] sqrt(bc2), [4] 1 - lr*wd
 __global__ void a2_opt_prepare_kernel(const double* sqp, float* losses, int32_t* steps, float lr, float b1, float b2,
-                                      float wd, float max_norm, float* ctrl) {
+                                      float wd, float max_norm, float* ctrl, float* user_losses) {
   if (threadIdx.x != 0) return;
   ctrl[0] = 0.f;
   if (losses[9] < 1.f) return;
@@ -743,6 +743,7 @@ __global__ void a2_opt_prepare_kernel(const double* sqp, float* losses, int32_t*
   }
   const float total = (float)sqrt(tot);
   losses[8] = total;
+  if (user_losses) user_losses[8] = total;
   ctrl[1] = fminf(1.f, max_norm / (total + 1e-6f));
   const int step = steps[0] + 1;
   for (int s = 0; s < A2_NSLOT; ++s) steps[s] = step;
@@ -1035,7 +1036,8 @@ struct A2PlanImpl {
     return 0;
   }
 
-  int optimizer(float lr, float b1, float b2, float eps, float wd, float max_norm, hipStream_t st) {
+  int optimizer(float lr, float b1, float b2, float eps, float wd, float max_norm, hipStream_t st,
+                float* user_losses = nullptr) {
     A2SlotTab t{};
     for (int i = 0; i < A2_NSLOT; ++i) {
       t.off[i] = a2_offsets().off[i];
@@ -1044,7 +1046,7 @@ struct A2PlanImpl {
     hipLaunchKernelGGL(a2_sqsum_kernel, dim3(A2_NSLOT, A2_SQ_CHUNKS), dim3(256), 0, st, grads, t, sqp);
     VAD_LAUNCH_CHECK();
     hipLaunchKernelGGL(a2_opt_prepare_kernel, dim3(1), dim3(64), 0, st, sqp, losses, steps, lr, b1, b2, wd,
-                       max_norm, ctrl);
+                       max_norm, ctrl, user_losses);
     VAD_LAUNCH_CHECK();
     const int64_t n = a2_offsets().total;
     hipLaunchKernelGGL(a2_adamw_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 1024)), dim3(256), 0, st,
@@ -1062,6 +1064,9 @@ struct vad_a2_plan {
   vad_a2_plan(int B, int T, int H, int W) : impl(B, T, H, W) {}
   A2PlanImpl impl;
   float* user_losses = nullptr;
+  // option "host_losses": a pinned (device-visible) 10-float host buffer the forward's copy kernel also writes, so a
+  // caller waiting for the forward's event reads the losses without a copy-engine transfer on the stream
+  float* host_losses = nullptr;
 };
 
 extern "C" {
@@ -1106,9 +1111,9 @@ int vad_a2_bind(vad_a2_plan* plan, void* workspace, float* params, float* grads,
 namespace vad {
 // the plan's small outputs handed to the caller's buffers in one launch (instead of one copy-engine blit each)
 struct A2Copies {
-  const float* src[4];
-  float* dst[4];
-  int n[4];
+  const float* src[5];
+  float* dst[5];
+  int n[5];
 };
 __global__ __launch_bounds__(256) void a2_copies_kernel(A2Copies c) {
   const int k = blockIdx.x;
@@ -1128,6 +1133,7 @@ int vad_a2_set_option(vad_a2_plan* plan, const char* key, int64_t value) {
   VAD_CHECK(plan && key, "vad_a2_set_option: null argument");
   const std::string k(key);
   if (k == "borrow_input") plan->impl.borrow_input = value != 0;
+  else if (k == "host_losses") plan->host_losses = reinterpret_cast<float*>(value);  // pinned 10 floats, 0 = none
   else {
     vad::set_error("vad_a2_set_option: unknown option " + k);
     return 1;
@@ -1162,6 +1168,7 @@ int vad_a2_forward(vad_a2_plan* plan, const float* x, int training, uint64_t see
   add(features, c.f, B * 16);
   plan->user_losses = losses;
   add(with_loss ? losses : nullptr, c.losses, 10);
+  add(with_loss ? plan->host_losses : nullptr, c.losses, 10);
   return a2_copies(cp, k, st);
 }
 
@@ -1204,9 +1211,9 @@ int vad_a2_optimizer_step(vad_a2_plan* plan, float lr, float beta1, float beta2,
   VAD_CHECK(plan != nullptr, "vad_a2_optimizer_step: null plan");
   A2PlanImpl& c = plan->impl;
   hipStream_t st = (hipStream_t)stream;
-  VAD_TRY(c.optimizer(lr, beta1, beta2, eps, weight_decay, max_norm, st));
-  if (plan->user_losses)
-    VAD_HIP(hipMemcpyAsync(plan->user_losses, c.losses, sizeof(float) * 10, hipMemcpyDeviceToDevice, st));
+  // (the optimizer changes only the total grad norm, losses[8]: its prepare kernel writes it into the caller's buffer
+  // too -- no copy launch)
+  VAD_TRY(c.optimizer(lr, beta1, beta2, eps, weight_decay, max_norm, st, plan->user_losses));
   return 0;
 }
 
