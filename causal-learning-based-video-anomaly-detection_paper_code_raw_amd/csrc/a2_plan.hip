@@ -92,6 +92,11 @@ struct A2HeadArgs {
   float* red;     // [256] scratch
   float* pairs;   // [B][B] mean |A_i - A_j| of the pseudo-normal pairs i < j
   float* lsc;     // [8] loss scalars between the loss launches: focal sum, acyclicity, edges, avg, csign, np
+  // fc (a2:?: Linear(4096, 16) + Dropout(0.3) on the pooled features) inside the per-clip forward: pooled [B][4096]
+  const float* pooled;  // null: f was written by dense_fwd (the per-layer launch path)
+  uint64_t h_fc;
+  uint32_t thr_fc;
+  float s_fc;
 };
 
 // forward stage st: 0 causal_net.0 (+ReLU), 1 causal_net.2 (+sigmoid) -> sig, adj (zero diagonal), 2 graph_encoder.0
@@ -156,7 +161,32 @@ __global__ __launch_bounds__(256) void a2_head_fwd_clip_kernel(A2HeadArgs a) {
   const float* P = a.P;
   const int64_t* o = a.off;
   __shared__ float sf[16], shc0[32], sadj[256], sg1d[128], scat[80], shp0[32];
-  if (t < 16) sf[t] = scat[t] = a.f[b * 16 + t];
+  if (a.pooled) {
+    // f = Dropout(fc(pooled)): output n by the 16 lanes of a row group (each 256 of the 4096 inputs, 16-B loads),
+    // summed by butterflies within the group; the keyed dropout as dense_fwd's epilogue (row = clip0 + b, col = n)
+    const int n = t >> 4, l = t & 15;
+    const float* w = P + o[S_FCW] + (int64_t)n * 4096;
+    const float* x = a.pooled + (int64_t)b * 4096;
+    float acc = 0.f;
+#pragma unroll 4
+    for (int k = 4 * l; k < 4096; k += 64) {
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(w + k), xv = *reinterpret_cast<const f32x4*>(x + k);
+      acc = fmaf(wv[0], xv[0], acc);
+      acc = fmaf(wv[1], xv[1], acc);
+      acc = fmaf(wv[2], xv[2], acc);
+      acc = fmaf(wv[3], xv[3], acc);
+    }
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 16);
+    if (l == 0) {
+      float v = acc + P[o[S_FCB] + n];
+      if (a.training) v = rng_u24(a.h_fc, (uint64_t)(a.clip0 + b), (uint64_t)n) >= a.thr_fc ? v * a.s_fc : 0.f;
+      a.f[b * 16 + n] = v;
+      sf[n] = scat[n] = v;
+    }
+  } else if (t < 16) {
+    sf[t] = scat[t] = a.f[b * 16 + t];
+  }
   __syncthreads();
   if (t < 32) shc0[t] = a.hc0[b * 32 + t] = relu_nan(a2_dot(sf, P + o[S_CN0W] + t * 16, 16, P[o[S_CN0B] + t]));
   __syncthreads();
@@ -877,6 +907,9 @@ struct A2PlanImpl {
     a.red = red;
     a.pairs = pairs;
     a.lsc = lsc;
+    a.h_fc = rng_h1(seed, S_A2_DROP_FC, step);
+    a.thr_fc = drop_threshold(0.3);
+    a.s_fc = 1.0f / (float)(1.0 - 0.3);
     return a;
   }
 
@@ -936,12 +969,13 @@ struct A2PlanImpl {
       fc.dscale = 1.0f / (float)(1.0 - 0.3);
       fc.row0 = clip0;
     }
-    VAD_TRY(dense_fwd(pooled, B, 4096, P(S_FCW), P(S_FCB), 16, f, fc, scratch, scratch_floats, st));
-    const A2HeadArgs ha = head_args();
-    if (g_a2_head_clip) {
+    A2HeadArgs ha = head_args();
+    if (g_a2_head_clip) {  // (fc inside the per-clip kernel: no split-K GEMM + reduce launches)
+      ha.pooled = pooled;
       hipLaunchKernelGGL(a2_head_fwd_clip_kernel, dim3((unsigned)B), dim3(256), 0, st, ha);
       VAD_LAUNCH_CHECK();
     } else {
+      VAD_TRY(dense_fwd(pooled, B, 4096, P(S_FCW), P(S_FCB), 16, f, fc, scratch, scratch_floats, st));
       for (int s = 0; s < 6; ++s) {
         hipLaunchKernelGGL(a2_head_fwd_kernel, dim3((unsigned)cdiv(B * A2_FWD_N[s], 256)), dim3(256), 0, st, ha, s);
         VAD_LAUNCH_CHECK();

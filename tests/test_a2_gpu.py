@@ -107,11 +107,13 @@ def test_a2_direct_and_im2col_paths_agree():
         assert float((g0 - g1).norm()) <= 1e-5 * float(g1.norm()) + 1e-12, n
 
 
-def test_a2_head_per_clip_launch_is_bit_identical():
+def test_a2_head_per_clip_launch_agrees():
     """The head forward / backward as one block per clip (knob a2_head_clip = 1, the default) against one launch per
-    Linear layer (0): the same per-output arithmetic in the same order, so the step's losses, outputs and every
-    gradient are bit-identical.  (compute_improved_loss stays four launches: as phases of one block its B x B clip
-    pairs ran as serial rounds of global loads, a2 0.53 -> 0.70 ms/step, profiles/r06_bench_a2_loss_block.json.)"""
+    Linear layer (0): the same per-output arithmetic in the same order for every head layer; only fc (Linear(4096,
+    16), inside the per-clip kernel on the default path, a split-K GEMM on the other) sums its 4096 products in
+    another order -- so the step agrees to fp32 rounding (rel 1e-5), not bit for bit.  (compute_improved_loss stays
+    four launches: as phases of one block its B x B clip pairs ran as serial rounds of global loads, a2 0.53 -> 0.70
+    ms/step, profiles/r06_bench_a2_loss_block.json.)"""
     from vad_amd import _native as nat
     case = dict(B=6, T=8, H=48, W=40, seed=27, step=2, ckpt=True)
     x = ao.synth_clips(27, 2, 0, 6, 8, 48, 40)
@@ -125,8 +127,12 @@ def test_a2_head_per_clip_launch_is_bit_identical():
             res.append((avg, comps, e.cur.scores.cpu().clone(), e.grads.cpu().clone()))
         finally:
             nat.check(nat.lib().vad_set_tuning(b"a2_head_clip", 1))
-    assert res[0][0] == res[1][0] and res[0][1] == res[1][1]
-    assert torch.equal(res[0][2], res[1][2]) and torch.equal(res[0][3], res[1][3])
+    assert res[0][0] == pytest.approx(res[1][0], rel=1e-5)
+    for k, v in res[0][1].items():
+        assert v == pytest.approx(res[1][1][k], rel=1e-5, abs=1e-7), k
+    torch.testing.assert_close(res[0][2], res[1][2], rtol=1e-5, atol=1e-7)
+    g0, g1 = res[0][3].double(), res[1][3].double()
+    assert float((g0 - g1).norm() / g1.norm()) < 1e-5
 
 
 def test_a2_nan_loss_skips_the_step():
