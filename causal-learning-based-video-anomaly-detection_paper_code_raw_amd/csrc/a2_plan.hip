@@ -362,6 +362,11 @@ struct A2HeadBwdArgs {
   uint64_t h_fc;
   uint32_t thr_fc;
   float s_fc;
+  // per-clip path: fc's backward inside the head launches (pooled: the fc input; dpooled: its gradient, written by
+  // a2_head_bwd_clip_kernel; nseg 7: fc's weight / bias grads as the 7th segment of stage 6); null / 6: dense GEMMs
+  const float* pooled;
+  float* dpooled;
+  int nseg;
 };
 
 // Backward stages 0-5 of one clip per block (B blocks), the per-stage launches' arithmetic in the same order
@@ -410,6 +415,18 @@ __global__ __launch_bounds__(256) void a2_head_bwd_clip_kernel(A2HeadBwdArgs a) 
     for (int k = 0; k < 32; ++k) d = fmaf(scn0[k], P[o[S_CN0W] + k * 16 + t], d);
     if (f.training) d = rng_u24(a.h_fc, (uint64_t)(f.clip0 + b), (uint64_t)t) >= a.thr_fc ? d * a.s_fc : 0.f;
     a.dfeat[b * 16 + t] = d;
+    sdfeat[t] = d;
+  }
+  if (a.dpooled) {  // d pooled = W_fc^T d features (16-term dots, 16 of the 4096 inputs per thread)
+    __syncthreads();
+    const float* W = P + o[S_FCW];
+#pragma unroll 4
+    for (int k = t; k < 4096; k += 256) {
+      float acc = 0.f;
+#pragma unroll
+      for (int n = 0; n < 16; ++n) acc = fmaf(sdfeat[n], W[n * 4096 + k], acc);
+      a.dpooled[b * 4096 + k] = acc;
+    }
   }
 }
 
@@ -421,9 +438,11 @@ constexpr int A2_BWD_OUT[6] = {32, 80, 128, 256, 32, 16};
 struct A2WSeg {
   int w, bias, N, K;
 };
-constexpr A2WSeg A2_WSEGS[6] = {{S_AP2W, S_AP2B, 1, 32}, {S_AP0W, S_AP0B, 32, 80},   {S_GE3W, S_GE3B, 64, 128},
-                                {S_GE0W, S_GE0B, 128, 256}, {S_CN2W, S_CN2B, 256, 32}, {S_CN0W, S_CN0B, 32, 16}};
+constexpr A2WSeg A2_WSEGS[7] = {{S_AP2W, S_AP2B, 1, 32},     {S_AP0W, S_AP0B, 32, 80},   {S_GE3W, S_GE3B, 64, 128},
+                                {S_GE0W, S_GE0B, 128, 256}, {S_CN2W, S_CN2B, 256, 32}, {S_CN0W, S_CN0B, 32, 16},
+                                {S_FCW, S_FCB, 16, 4096}};
 constexpr int A2_WG_TOTAL = 1 * 33 + 32 * 81 + 64 * 129 + 128 * 257 + 256 * 33 + 32 * 17;
+constexpr int A2_WG_TOTAL_FC = A2_WG_TOTAL + 16 * 4097;
 
 __global__ __launch_bounds__(256) void a2_head_bwd_kernel(A2HeadBwdArgs a, int st) {
   const A2HeadArgs& f = a.f;
@@ -485,16 +504,17 @@ __global__ __launch_bounds__(256) void a2_head_bwd_kernel(A2HeadBwdArgs a, int s
       break;
     default: {
       int r = idx, s = 0;
-      for (; s < 6; ++s) {
+      for (; s < a.nseg; ++s) {
         const int len = A2_WSEGS[s].N * (A2_WSEGS[s].K + 1);
         if (r < len) break;
         r -= len;
       }
-      if (s >= 6) break;
+      if (s >= a.nseg) break;
       const A2WSeg g = A2_WSEGS[s];
       const float* dz = s == 0 ? a.dz_ap2 : s == 1 ? a.dz_ap0 : s == 2 ? a.dg2 : s == 3 ? a.dz_ge0 : s == 4 ? a.dz_cn2
-                                                                                                             : a.dz_cn0;
-      const float* x = s == 0 ? f.hp0 : s == 1 ? f.cat : s == 2 ? f.g1d : s == 3 ? f.adj : s == 4 ? f.hc0 : f.f;
+                        : s == 5 ? a.dz_cn0 : a.dfeat;
+      const float* x = s == 0 ? f.hp0 : s == 1 ? f.cat : s == 2 ? f.g1d : s == 3 ? f.adj : s == 4 ? f.hc0
+                       : s == 5 ? f.f : a.pooled;
       const int n = r / (g.K + 1), k = r % (g.K + 1);
       float acc = 0.f;
       if (k < g.K) {
@@ -1020,17 +1040,23 @@ struct A2PlanImpl {
     hb.h_fc = rng_h1(seed, S_A2_DROP_FC, step);
     hb.thr_fc = drop_threshold(0.3);
     hb.s_fc = 1.0f / (float)(1.0 - 0.3);
-    if (g_a2_head_clip) {
+    hb.nseg = 6;
+    if (g_a2_head_clip) {  // (fc's backward inside these two launches: no dense weight / input gradient GEMMs)
+      hb.pooled = pooled;
+      hb.dpooled = dpooled;
+      hb.nseg = 7;
       hipLaunchKernelGGL(a2_head_bwd_clip_kernel, dim3((unsigned)B), dim3(256), 0, st, hb);
       VAD_LAUNCH_CHECK();
     }
     for (int s = g_a2_head_clip ? 6 : 0; s < 7; ++s) {
-      const int n = s < 6 ? B * A2_BWD_OUT[s] : A2_WG_TOTAL;
+      const int n = s < 6 ? B * A2_BWD_OUT[s] : (hb.nseg == 7 ? A2_WG_TOTAL_FC : A2_WG_TOTAL);
       hipLaunchKernelGGL(a2_head_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, hb, s);
       VAD_LAUNCH_CHECK();
     }
-    VAD_TRY(dense_wgrad(dfeat, B, 16, pooled, 4096, G(S_FCW), G(S_FCB), scratch, scratch_floats, nullptr, st));
-    VAD_TRY(dense_dgrad(dfeat, B, 16, P(S_FCW), 4096, dpooled, nullptr, 1.f, nullptr, st));
+    if (!g_a2_head_clip) {
+      VAD_TRY(dense_wgrad(dfeat, B, 16, pooled, 4096, G(S_FCW), G(S_FCB), scratch, scratch_floats, nullptr, st));
+      VAD_TRY(dense_dgrad(dfeat, B, 16, P(S_FCW), 4096, dpooled, nullptr, 1.f, nullptr, st));
+    }
     // (direct: each ReLU backward is fused into the producer of its gradient -- the average-pool backward for
     // conv3d_3, the parity-class input gradients for conv3d_2 / conv3d_1 -- instead of a relu_gate pass)
     VAD_TRY(adaptive_avgpool3d_bwd(dpooled, g[2].out(), 4, 4, 4, dA, st, direct ? y[2] : nullptr));
