@@ -1091,6 +1091,7 @@ struct ConvTuning {
 static ConvTuning g_tune;
 
 extern int g_bbox_im2col;  // bbox_plan.hip
+extern int g_maxpool_bwd_win;  // conv3d.hip
 extern int g_ae_direct, g_ae_wgrad_blocks, g_ae_wgrad_stream;  // ae_plan.hip
 extern int g_conv4_cls_batch_min, g_conv4_split_tiles;
 extern int g_a2_direct, g_a2_head_clip;     // a2_plan.hip
@@ -1152,6 +1153,7 @@ int set_tuning(const char* key, int value) {
   else if (k == "conv_bfc_blocks") g_bfc_blocks = value;
   else if (k == "conv_bfc_s2_ni2") g_bfc_s2_ni2 = value;
   else if (k == "conv3d_direct") g_conv3d_direct = value;
+  else if (k == "maxpool3d_bwd_win") g_maxpool_bwd_win = value;
   else if (k == "conv3d_wgrad_blocks") g_conv3d_wg_blocks = value;
   else if (k == "conv_dgrad_s2_w3") g_dgrad_s2_w3 = value;
   else if (k == "conv_dgrad_s2_nt") g_dgrad_s2_nt = value;

@@ -224,10 +224,71 @@ __global__ __launch_bounds__(256) void maxpool3d_bwd_kernel(const float* __restr
   }
 }
 
+// The same backward with one thread per pooling window (output): the window's first max found once, its kd kh kw
+// input gradients written together (dout at the max, 0 elsewhere) -- every y value read once instead of once per
+// element of its window (the per-element kernel above re-scans the window kd kh kw times).  Input elements outside
+// every window (extents not divisible by the window) are cleared first.
+template <typename I>
+__global__ __launch_bounds__(256) void maxpool3d_bwd_win_kernel(const float* __restrict__ y,
+                                                                const float* __restrict__ stats, int relu, Vol5 v,
+                                                                int kd, int kh, int kw,
+                                                                const float* __restrict__ dout,
+                                                                float* __restrict__ dA) {
+  const int OD = v.D / kd, OH = v.H / kh, OW = v.W / kw, C = v.C;
+  const I total = (I)v.N * OD * OH * OW * C;
+  for (I i = blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    I r = i / C;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    r /= OH;
+    const int od = (int)(r % OD);
+    const int n = (int)(r / OD);
+    // first max of the window in (d, h, w) scan order (torch max_pool3d CPU: val > max || isnan(val))
+    float m = -INFINITY;
+    int arg = -1;
+    for (int a = 0; a < kd; ++a)
+      for (int b = 0; b < kh; ++b)
+        for (int e = 0; e < kw; ++e) {
+          const I idx = ((((I)n * v.D + od * kd + a) * v.H + oh * kh + b) * v.W + ow * kw + e) * C + c;
+          const float val = pool_act(y, stats, relu, C, c, idx);
+          if (arg < 0 || val > m || isnan(val)) {
+            m = val;
+            arg = (a * kh + b) * kw + e;
+          }
+        }
+    const float g = dout[i];
+    for (int a = 0; a < kd; ++a)
+      for (int b = 0; b < kh; ++b)
+        for (int e = 0; e < kw; ++e) {
+          const I idx = ((((I)n * v.D + od * kd + a) * v.H + oh * kh + b) * v.W + ow * kw + e) * C + c;
+          dA[idx] = (a * kh + b) * kw + e == arg ? g : 0.f;
+        }
+  }
+}
+
+int g_maxpool_bwd_win = 1;  // knob "maxpool3d_bwd_win": one thread per window (0: one per input element)
+
 int maxpool3d_bwd(const float* y, const float* stats, int relu, const Vol5& v, int kd, int kh, int kw,
                   const float* dout, float* dA, hipStream_t st) {
   const int64_t total = v.numel();
   if (total == 0) return 0;
+  if (g_maxpool_bwd_win) {
+    const int OD = v.D / kd, OH = v.H / kh, OW = v.W / kw;
+    if (OD * kd != v.D || OH * kh != v.H || OW * kw != v.W)
+      VAD_HIP(hipMemsetAsync(dA, 0, sizeof(float) * (size_t)total, st));
+    const int64_t nw = (int64_t)v.N * OD * OH * OW * v.C;
+    if (nw == 0) return 0;
+    const dim3 g2((unsigned)std::min<int64_t>(cdiv(nw, 256), 16384));
+    if (total + (int64_t)g2.x * 256 < (1ll << 31))
+      hipLaunchKernelGGL(maxpool3d_bwd_win_kernel<int>, g2, dim3(256), 0, st, y, stats, relu, v, kd, kh, kw, dout, dA);
+    else
+      hipLaunchKernelGGL(maxpool3d_bwd_win_kernel<int64_t>, g2, dim3(256), 0, st, y, stats, relu, v, kd, kh, kw, dout,
+                         dA);
+    VAD_LAUNCH_CHECK();
+    return 0;
+  }
   const dim3 grid((unsigned)std::min<int64_t>(cdiv(total, 256), 16384));
   if (total + (int64_t)grid.x * 256 < (1ll << 31))
     hipLaunchKernelGGL(maxpool3d_bwd_kernel<int>, grid, dim3(256), 0, st, y, stats, relu, v, kd, kh, kw, dout, dA);

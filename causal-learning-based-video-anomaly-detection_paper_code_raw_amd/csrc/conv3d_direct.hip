@@ -228,8 +228,17 @@ __global__ __launch_bounds__(256) void conv3d_direct_wgrad_reduce_kernel(const f
   const int P = Ci * 27 + 1, total = P * CO;
   const int q = blockIdx.x * 64 + threadIdx.x % 64, grp = threadIdx.x / 64;
   float v = 0.f;
-  if (q < total)
-    for (int b = grp; b < nblk; b += 4) v += slab[(int64_t)b * total + q];
+  if (q < total) {  // blocks grp, grp + 4, ... in order, 8 loads in flight (clamped indices, unconditional loads)
+    const int n = nblk > grp ? (nblk - grp + 3) / 4 : 0;
+    for (int k0 = 0; k0 < n; k0 += 8) {
+      float u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = slab[(int64_t)(grp + 4 * min(k0 + k, n - 1)) * total + q];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k0 + k < n) v += u[k];
+    }
+  }
   red[grp][threadIdx.x % 64] = v;
   __syncthreads();
   if (grp == 0 && q < total) {

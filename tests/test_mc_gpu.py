@@ -132,3 +132,23 @@ def test_mc_nonfinite_input_skips_step():
     assert int(model._engine.losses[3]) == 0
     for n, p in model.named_parameters():
         assert torch.equal(p.detach(), before[n].to(p.device)), n
+
+
+@pytest.mark.parametrize("case", MC_CASES, ids=[c["name"] for c in MC_CASES])
+def test_mc_maxpool_window_backward_is_bit_identical(case):
+    """MaxPool3d backward with one thread per window (knob maxpool3d_bwd_win = 1, the default: the first max found once,
+    the window's gradients written together) against one thread per input element (0): the same torch first-max rule,
+    so the post-step params are bit-identical.  (Extents the windows do not divide are cleared first on the window
+    path; the reference's shapes divide evenly.)"""
+    from vad_amd import _native as nat
+    out = []
+    for v in (1, 0):
+        nat.check(nat.lib().vad_set_tuning(b"maxpool3d_bwd_win", v))
+        try:
+            model = make_mc_model(case)
+            tr = _trainer(case, model)
+            tr.train_epoch()
+            out.append(torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()]))
+        finally:
+            nat.check(nat.lib().vad_set_tuning(b"maxpool3d_bwd_win", 1))
+    assert torch.equal(out[0], out[1])
