@@ -1001,13 +1001,27 @@ struct EpiDense {
   }
 };
 
+// sum_{z < S} p[z * stride] in z order, 8 loads in flight (clamped, unconditional): the slab sums of the split-K
+// reduces (a plain loop leaves one dependent load round trip per slab)
+__device__ __forceinline__ float slab_sum(const float* __restrict__ p, int S, int64_t stride) {
+  float s = 0.f;
+  for (int z0 = 0; z0 < S; z0 += 8) {
+    float u[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) u[k] = p[(int64_t)min(z0 + k, S - 1) * stride];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (z0 + k < S) s += u[k];
+  }
+  return s;
+}
+
 __global__ __launch_bounds__(256) void dense_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
                                                                   DenseEpiArgs P, const int* skip) {
   if (skip && *skip == 0) return;
   const int64_t total = (int64_t)M * N;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    float s = 0.f;
-    for (int z = 0; z < S; ++z) s += part[z * total + i];
+    const float s = slab_sum(part + i, S, total);
     const int row = (int)(i / N), col = (int)(i % N);
     P.out[(int64_t)row * P.ldc + col] = dense_finish(P, row, col, s);
   }
@@ -1021,8 +1035,7 @@ __global__ __launch_bounds__(256) void dense_wgrad_reduce_kernel(const float* __
   const int64_t ld = K + 1;
   const int64_t total = (int64_t)N * ld;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    float s = 0.f;
-    for (int z = 0; z < S; ++z) s += part[z * total + i];
+    const float s = slab_sum(part + i, S, total);
     const int row = (int)(i / ld), col = (int)(i % ld);
     if (col < K) dW[(int64_t)row * K + col] = s;
     else if (db) db[row] = s;
@@ -1989,8 +2002,7 @@ __global__ __launch_bounds__(256) void conv4_cls_reduce_kernel(const float* __re
                                                                const float* __restrict__ bias, float* __restrict__ out) {
   const int64_t total = (int64_t)M * N;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    float v = 0.f;
-    for (int z = 0; z < S; ++z) v += part[(int64_t)z * total + i];
+    const float v = slab_sum(part + i, S, total);
     const int n = (int)(i % N);
     const int64_t m = i / N;
     const int b = (int)(m % SW);
@@ -2107,8 +2119,7 @@ __global__ __launch_bounds__(256) void conv4_wgrad_reduce_kernel(const float* __
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
     const int64_t r = i / W1;
     const int col = (int)(i - r * W1);
-    float s = 0.f;
-    for (int z = 0; z < S; ++z) s += part[(int64_t)z * slab + r * ld + col];
+    const float s = slab_sum(part + r * ld + col, S, slab);
     if (col == NT * C) {
       db[r] = s;
     } else {
